@@ -1,0 +1,165 @@
+/*
+ * rcmdyn.h -- C-ABI of the MI355X-native RegCM4 dynamical-core step engine.
+ *
+ * Drop-in boundary for the reference hot path:
+ *
+ *   reference seam                                  replaced by
+ *   ---------------------------------------------   -------------------------------
+ *   call tend        Main/mod_regcm_interface.F90:189 rcmdyn_tend()
+ *   call bdyval      Main/mod_regcm_interface.F90:208 rcmdyn_bdyval()
+ *   tend+bdyval loop Main/mod_regcm_interface.F90:172-228   rcmdyn_step()
+ *   module state     Main/mod_atm_interface.F90:39-70 rcmdyn_put()/rcmdyn_get()
+ *   bdyin (b0,bt)    Main/mod_bdycod.F90:654-889      rcmdyn_set_bdy_time() + put XxB_*
+ *   rcmtimer/dt/xbctime Main/mpplib/mod_runparams.F90 rcmdyn_set_time()/get_time()
+ *   exchange*        Main/mpplib/mod_mppparam.F90:6065-13190  internal (local copies / RCCL)
+ *   fatal('CFL VIOLATION') Main/mod_tendency.F90:702  return code + rcmdyn_last_error()
+ *
+ * Conventions
+ *  - Every entry point returns 0 on success, non-zero on failure; the message of the
+ *    last failure is available from rcmdyn_last_error().
+ *  - Host arrays cross the boundary in the reference's Fortran layout: column-major
+ *    (j fastest, then i, then k), with explicit GLOBAL index bounds j1:j2, i1:i2, k1:k2
+ *    (Fortran 1-based, as allocated by getmem*: Share/mod_memutil.F90).  In C/numpy
+ *    terms that is a C-order [k][i][j] array.  The engine copies the intersection of
+ *    the host box with the tiles it owns; it never keeps a host pointer.
+ *  - All arithmetic is fp64 (rkx = rk8, Share/mod_realkinds.F90:44-55).
+ *  - No torch / HIP types appear in any signature.
+ */
+#ifndef RCMDYN_H
+#define RCMDYN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RCMDYN_ABI_VERSION 1
+#define RCMDYN_MAXKZ 64
+#define RCMDYN_MAXSPLIT 4
+
+/* Run/grid configuration.  Scalars mirror the namelist / mod_runparams globals that
+ * the reference dyn core reads (Share/mod_dynparam.F90:453-476, Main/mod_params.F90:85-170,
+ * Main/mpplib/mod_runparams.F90:97-232).  Vertical-mode constants are the outputs of the
+ * host-side init (spinit/vmodes, Main/mod_split.F90:75-239, Main/mod_vmodes.F90:86-594). */
+typedef struct rcmdyn_config {
+  int32_t abi_version;          /* = RCMDYN_ABI_VERSION */
+  /* global grid: jx (west-east dot points), iy (south-north), kz (levels) */
+  int32_t jx, iy, kz;
+  /* 2-D decomposition in tiles (set_nproc rule, Main/mpplib/mod_mppparam.F90:1133-1186);
+   * tile t has cartesian location (t / nproc_i, t % nproc_i) = (j-coord, i-coord). */
+  int32_t nproc_j, nproc_i;
+  /* tiles owned by this engine instance: [tile_first, tile_first + tile_count) */
+  int32_t tile_first, tile_count;
+  /* dynamics options (defaults in brackets) */
+  int32_t idynamic;             /* [1] hydrostatic (2 = non-hydrostatic: not yet built) */
+  int32_t iboudy;               /* [5] exponential relaxation (1 = linear) */
+  int32_t idiffu;               /* [1] 4th-order diffusion */
+  int32_t ipgf;                 /* [0] */
+  int32_t nsplit;               /* [2] */
+  int32_t nspgx, nspgd;         /* [12,12] boundary relaxation band width */
+  int32_t diffu_hgtf;           /* [1] topographic diffusion reduction */
+  int32_t upstream_mode;        /* [1] */
+  int32_t stability_enhance;    /* [1] */
+  int32_t present_qc;           /* [0] ICBC carries qc (Main/mod_bdycod.F90:306-310) */
+  /* scalars */
+  double ds;                    /* grid spacing, km */
+  double dtsec;                 /* namelist dt, s */
+  double ptop;                  /* model top, cb */
+  double gnu1, gnu2;            /* Robert-Asselin [0.0625] */
+  double uoffc;                 /* [0.25] */
+  double t_extrema;             /* [5] */
+  double q_rel_extrema;         /* [0.2] */
+  double ckh, adyndif;          /* [1,1] */
+  double high_nudge, medium_nudge, low_nudge; /* [3,2,1] */
+  double bdy_nm, bdy_dm;        /* [-1,-1] -> derived from dt */
+  double dtbdys;                /* boundary interval, s [6*3600] */
+  /* vertical structure */
+  double sigma[RCMDYN_MAXKZ + 1];          /* full sigma levels, k = 1..kz+1 */
+  /* split-explicit constants (after spinit scaling), Fortran index order noted */
+  double zmatx[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ];   /* zmatx(k,l) -> zmatx[l-1][k-1] */
+  double zmatxr[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ];  /* zmatxr(l,k) -> zmatxr[l-1][k-1] */
+  double am[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ];      /* am(k,l) -> am[l-1][k-1] */
+  double tau[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ];     /* tau(l,k) -> tau[l-1][k-1] */
+  double varpa1[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ + 1]; /* varpa1(l,k) -> varpa1[l-1][k-1] */
+  double an[RCMDYN_MAXSPLIT];
+  double hbar[RCMDYN_MAXSPLIT];
+  double aam[RCMDYN_MAXSPLIT];
+  double dtau[RCMDYN_MAXSPLIT];
+  double sigmah[RCMDYN_MAXKZ + 1];
+  double pd;                    /* vmodes reference p* (cb) */
+  /* multi-process (RCCL) -- used only when tile_count < nproc_j*nproc_i */
+  int32_t comm_rank, comm_size; /* process rank / size in the RCCL communicator */
+  int32_t device;               /* HIP device ordinal, -1 = current */
+  uint8_t comm_unique_id[128];  /* ncclUniqueId from rcmdyn_comm_unique_id() on rank 0 */
+} rcmdyn_config;
+
+/* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */
+enum rcmdyn_field {
+  /* prognostic state, coupled with p* exactly as the reference stores it */
+  RCMDYN_ATM1_U = 0, RCMDYN_ATM1_V, RCMDYN_ATM1_T, RCMDYN_ATM1_QV, RCMDYN_ATM1_QC,
+  RCMDYN_ATM2_U, RCMDYN_ATM2_V, RCMDYN_ATM2_T, RCMDYN_ATM2_QV, RCMDYN_ATM2_QC,
+  RCMDYN_PSA, RCMDYN_PSB,                 /* 2-D (k1=k2=1) */
+  RCMDYN_DSTOR, RCMDYN_HSTOR,             /* 2-D x nsplit (k = 1..nsplit) */
+  /* static fields, as left by param (Main/mod_params.F90:1982-2002): map factors
+   * already inverted, ht already converted to geopotential */
+  RCMDYN_MSFX, RCMDYN_MSFD, RCMDYN_CORIOL, RCMDYN_HT,
+  /* lateral boundary data (v3dbound / v2dbound b0, bt) */
+  RCMDYN_XUB_B0, RCMDYN_XUB_BT, RCMDYN_XVB_B0, RCMDYN_XVB_BT,
+  RCMDYN_XTB_B0, RCMDYN_XTB_BT, RCMDYN_XQB_B0, RCMDYN_XQB_BT,
+  RCMDYN_XPSB_B0, RCMDYN_XPSB_BT,
+  /* read-only diagnostics of the last tend */
+  RCMDYN_PSC, RCMDYN_PTEN, RCMDYN_PSDOTA,
+  RCMDYN_TTEN, RCMDYN_UTEN, RCMDYN_VTEN, RCMDYN_QVTEN, RCMDYN_QCTEN,
+  RCMDYN_OMEGA, RCMDYN_QDOT /* k = 1..kz+1 */, RCMDYN_XKC, RCMDYN_PHI,
+  RCMDYN_NFIELDS
+};
+
+typedef struct rcmdyn_engine rcmdyn_t;
+
+/* Lifetime */
+int rcmdyn_create(const rcmdyn_config* cfg, rcmdyn_t** out);
+int rcmdyn_destroy(rcmdyn_t* h);
+const char* rcmdyn_last_error(rcmdyn_t* h);    /* h may be NULL: last global error */
+
+/* Decomposition (set_nproc, Main/mpplib/mod_mppparam.F90:1053-1371), host-only, no GPU:
+ * fills cpus[2] = {cpus_j, cpus_i} for nproc ranks on a jx x iy grid. */
+int rcmdyn_set_nproc(int32_t nproc, int32_t jx, int32_t iy, int32_t cpus[2]);
+/* Tile extents in global indices: ext[8] = {jde1,jde2,ide1,ide2,jce1,jce2,ice1,ice2},
+ * bdy[4] = {has_bdyleft, has_bdyright, has_bdybottom, has_bdytop}.  Host-only. */
+int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
+                       int32_t tile, int32_t ext[8], int32_t bdy[4]);
+
+/* State transfer (host <-> device), Fortran layout, global index bounds. */
+int rcmdyn_put(rcmdyn_t* h, int32_t field, const double* src,
+               int32_t j1, int32_t j2, int32_t i1, int32_t i2, int32_t k1, int32_t k2);
+int rcmdyn_get(rcmdyn_t* h, int32_t field, double* dst,
+               int32_t j1, int32_t j2, int32_t i1, int32_t i2, int32_t k1, int32_t k2);
+
+/* rcm_timer state: lcount (steps done), dt (current leapfrog dt, s), xbctime (s since
+ * the current boundary interval started). */
+int rcmdyn_set_time(rcmdyn_t* h, int64_t lcount, double dt, double xbctime);
+int rcmdyn_get_time(rcmdyn_t* h, int64_t* lcount, double* dt, double* xbctime);
+
+/* The hot path. */
+int rcmdyn_tend(rcmdyn_t* h);                  /* one mod_tendency::tend */
+int rcmdyn_bdyval(rcmdyn_t* h);                /* one mod_bdycod::bdyval */
+int rcmdyn_step(rcmdyn_t* h, int32_t nsteps);  /* nsteps x (tend + bdyval), graph-replayed */
+int rcmdyn_synchronize(rcmdyn_t* h);
+
+/* Diagnostics of the last tend: out[0]=ptntot, out[1]=pt2tot (Bleck noise sums of the
+ * owned tiles, Main/mod_tendency.F90:1449-1459), out[2]=1 if ptntot is NaN. */
+int rcmdyn_diagnostics(rcmdyn_t* h, double out[4]);
+
+/* Multi-process: rank 0 creates the id, the host broadcasts it (MPI / torch.distributed),
+ * every rank passes it in rcmdyn_config.comm_unique_id. */
+int rcmdyn_comm_unique_id(uint8_t out[128]);
+
+/* Wall-clock of device work: average ms per step of the last rcmdyn_step call measured
+ * with HIP events on the engine's compute stream. */
+int rcmdyn_last_step_ms(rcmdyn_t* h, double* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RCMDYN_H */

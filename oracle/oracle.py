@@ -1,0 +1,132 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the CPU restatement (librcm_oracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+It exposes the same host API as ``regcm_amd.dycore.DynCore`` (tend / bdyval / step / put /
+get) so parity tests read like the reference's own driver (Main/mod_regcm_interface.F90:172-228).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from regcm_amd.config import (FIELD, RcmdynConfig, build_config, field_levels)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "librcm_oracle.so")
+_lib = None
+
+EXCH_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                           ctypes.c_int, ctypes.c_int, ctypes.c_int)
+EXCHB_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                            ctypes.c_int, ctypes.c_int)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = ctypes.CDLL(_LIB)
+        P = ctypes.c_void_p
+        dp = ctypes.POINTER(ctypes.c_double)
+        i = ctypes.c_int
+        L.orc_create.restype = P
+        L.orc_create.argtypes = [ctypes.POINTER(RcmdynConfig)]
+        L.orc_destroy.argtypes = [P]
+        L.orc_set_exchange.argtypes = [P, EXCH_FN, EXCHB_FN, P]
+        L.orc_frame_info.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+        L.orc_put.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_get.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_set_time.argtypes = [P, ctypes.c_longlong, ctypes.c_double, ctypes.c_double]
+        L.orc_get_time.argtypes = [P, ctypes.POINTER(ctypes.c_longlong),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.orc_tend.restype = i
+        L.orc_tend.argtypes = [P]
+        L.orc_bdyval.argtypes = [P]
+        L.orc_step.restype = i
+        L.orc_step.argtypes = [P, i]
+        L.orc_diagnostics.argtypes = [P, dp]
+        _lib = L
+    return _lib
+
+
+class OracleCore:
+    """One tile of the CPU restatement.  ``tile`` indexes the set_nproc decomposition."""
+
+    def __init__(self, rc, split, nproc_j=1, nproc_i=1, tile=0):
+        self.rc = rc
+        self.cfg = build_config(rc, split, nproc_j, nproc_i, tile_first=tile, tile_count=1)
+        self.h = lib().orc_create(ctypes.byref(self.cfg))
+        if not self.h:
+            raise RuntimeError("orc_create failed")
+        info = (ctypes.c_int * 16)()
+        lib().orc_frame_info(self.h, info)
+        self.info = list(info)
+        self._cb = None
+
+    def close(self):
+        if self.h:
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_exchange(self, fn, bfn):
+        self._cb = (EXCH_FN(fn), EXCHB_FN(bfn))
+        lib().orc_set_exchange(self.h, self._cb[0], self._cb[1], None)
+
+    def put(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        nk, ni, nj = a.shape
+        rc = lib().orc_put(self.h, FIELD[name], a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                           1, nj, 1, ni, 1, nk)
+        if rc:
+            raise KeyError(name)
+
+    def get(self, name):
+        nk = field_levels(name, self.rc.kz, self.rc.nsplit)
+        out = np.zeros((nk, self.rc.iy, self.rc.jx))
+        rc = lib().orc_get(self.h, FIELD[name], out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                           1, self.rc.jx, 1, self.rc.iy, 1, nk)
+        if rc:
+            raise KeyError(name)
+        return out
+
+    def put_state(self, st):
+        for name, arr in st.items():
+            self.put(name, arr)
+
+    def set_time(self, lcount, dt, xbctime):
+        lib().orc_set_time(self.h, lcount, dt, xbctime)
+
+    def get_time(self):
+        a, b, c = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+        lib().orc_get_time(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def tend(self):
+        if lib().orc_tend(self.h):
+            raise FloatingPointError("CFL VIOLATION")
+
+    def bdyval(self):
+        lib().orc_bdyval(self.h)
+
+    def step(self, n=1):
+        if lib().orc_step(self.h, n):
+            raise FloatingPointError("CFL VIOLATION")
+
+    def diagnostics(self):
+        out = (ctypes.c_double * 4)()
+        lib().orc_diagnostics(self.h, out)
+        return list(out)

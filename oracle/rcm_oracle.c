@@ -1,0 +1,1574 @@
+/*
+ * rcm_oracle.c -- TEST INFRASTRUCTURE ONLY (see rcm_oracle.h).
+ *
+ * Plain-C restatement of the RegCM 4.7 hydrostatic dynamical-core step, written loop
+ * nest by loop nest after the reference so that every floating-point expression is
+ * evaluated in the reference's order (Fortran left-to-right, no reassociation, no FMA:
+ * compile with -ffp-contract=off).  Each routine cites the reference file:line it
+ * restates.  Physics is stubbed exactly as BASELINE configuration C2/C3 ("physics
+ * stubbed"): every *phy tendency is zero (Main/mod_tendency.F90:1682-1820 with no-op
+ * cumulus/microscheme/radiation/pbl and heatrt = 0).
+ *
+ * Scope (defaults assumed): idynamic=1, upstream_mode and
+ * stability_enhance on, idiffu=1, iboudy=5 (or 1), ipgf=0, nsplit from config,
+ * nqx=2 (qv,qc), isladvec=0, ibltyp!=2, ichem=0, idiag=0, iboudy time-dependent.
+ *
+ * Parity unpinned: no execution of the reference is available (netCDF-Fortran absent),
+ * no golden vectors exist in the reference tree.
+ */
+#include "rcm_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+/* ---- constants: Share/mod_constants.F90 (evaluated exactly as written) ---- */
+static const double d_zero = 0.0, d_one = 1.0, d_two = 2.0, d_four = 4.0;
+static const double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
+#define EGRAV   9.80665                      /* :85  */
+#define BOLTZK  1.3806504e-23                /* :92  */
+#define NAVGDR  6.02214129e23                /* :94  */
+#define AMD     28.96454                     /* :107 */
+#define AMW     18.01528                     /* :109 */
+#define MINQQ   1.0e-8                       /* :57  */
+#define DLOWVAL 1.0e-20                      /* :68  */
+#define VONKAR  0.4                          /* :296 */
+static double c_rgas, c_cpd, c_c287, c_ep1, c_regrav;
+static const double alpha_hyd = 0.0;         /* :319 */
+static const double beta_hyd = 1.0 - 2.0 * 0.0; /* :320 */
+/* mod_diffusion.F90:69-71 */
+static const double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
+
+static void init_constants(void) {
+  double rgasmol = NAVGDR * BOLTZK;          /* :130 */
+  c_c287 = rgasmol / AMD;                    /* :132 */
+  c_rgas = c_c287 * 1000.0;                  /* :134 */
+  c_cpd = 3.5 * c_rgas;                      /* :144 */
+  c_ep1 = AMD / AMW - d_one;                 /* :303 */
+  c_regrav = d_one / EGRAV;                  /* :182 */
+}
+
+#define GO 3   /* frame ghost width (covers ga/gb/gc halos) */
+
+struct orc {
+  rcmdyn_config cfg;
+  int jx, iy, kz, kzp1, nsplit, nqx;
+  /* tile index ranges (global, Fortran), Main/mod_atm_interface.F90:181-381 */
+  int jde1, jde2, jdi1, jdi2, jdii1, jdii2, ide1, ide2, idi1, idi2, idii1, idii2;
+  int jce1, jce2, jci1, jci2, jcii1, jcii2, ice1, ice2, ici1, ici2, icii1, icii2;
+  int jde1ga, jde2ga, ide1ga, ide2ga, jce1ga, jce2ga, ice1ga, ice2ga;
+  int jci1ga, jci2ga, ici1ga, ici2ga;
+  int jde1gb, jde2gb, ide1gb, ide2gb, jce1gb, jce2gb, ice1gb, ice2gb;
+  int bl, br, bb, bt;                       /* has_bdyleft/right/bottom/top */
+  /* frame */
+  int j0, i0, nj, ni;
+  size_t plane;
+  /* time */
+  long long lcount;
+  double dt, dtsec, xbctime;
+  /* derived constants */
+  double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop;
+  double ul, xkhmax, dydc, xkhz, fnudge, gnudge;
+  double sigma[RCMDYN_MAXKZ + 2], hsigma[RCMDYN_MAXKZ + 1], dsigma[RCMDYN_MAXKZ + 1];
+  double twt1[RCMDYN_MAXKZ + 1], twt2[RCMDYN_MAXKZ + 1], qcon[RCMDYN_MAXKZ + 1];
+  double xds[RCMDYN_MAXKZ + 1], dds[RCMDYN_MAXKZ + 2];
+  double hefc[256][RCMDYN_MAXKZ + 1], hegc[256][RCMDYN_MAXKZ + 1]; /* (n,k), n=2..nspgx-1 */
+  double fcx[256], gcx[256];
+  double pdlog[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ + 2], eps1[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ + 2];
+  /* boundary masks: 0 none, 1 S, 2 N, 3 W, 4 E; ibnd */
+  signed char *rg_cr, *rg_dt;
+  int *ib_cr, *ib_dt;
+  /* state */
+  double *a1u, *a1v, *a1t, *a1q[2], *a2u, *a2v, *a2t, *a2q[2];
+  double *psa, *psb, *psc, *psdota, *psdotb, *dstor, *hstor;
+  double *msfx, *msfd, *xmsf, *dmsf, *coriol, *ht, *hgfact, *map;
+  double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
+  /* work */
+  double *rpsa, *rpsb, *rpsc, *rpsda, *srpsb, *rpsdotb;
+  double *uc, *vc, *umc, *vmc, *ud, *vd, *xt, *xq[2], *xtv;
+  double *cr, *pten, *qdot, *omega, *dummy;
+  double *ubd, *vbd, *tb3d, *qb3d[2], *pb3d, *pf3d;
+  double *xkc, *xkd;
+  double *tten, *tdyn, *uten, *udyn, *vten, *vdyn, *qten[2], *qdyn[2];
+  double *fg, *uavg1, *uavg2, *vavg1, *vavg2, *dotqdot;
+  double *fg1, *fg2;
+  double *ct, *cq[2], *cu, *cv;
+  double *td, *tvfac, *phi;
+  double *deld, *delh, *ddsum, *dhsum, *xdelh, *work, *uu, *vv, *uuu, *vvv;
+  /* boundary slices (Main/mod_bdycod.F90:58-61): indexed by frame j or i, then k */
+  double *wue, *wui, *eue, *eui, *wve, *wvi, *eve, *evi;
+  double *sue, *sui, *nue, *nui, *sve, *svi, *nve, *nvi;
+  /* diagnostics */
+  double ptntot, pt2tot;
+  /* exchange */
+  orc_exchange_fn xfn;
+  orc_exchange_bdy_fn bfn;
+  void* xctx;
+};
+
+/* ---- indexing: frame [k][i][j], global Fortran indices ---- */
+#define IX(j, i) ((size_t)((i) - o->i0) * (size_t)o->nj + (size_t)((j) - o->j0))
+#define A2(a, j, i) (a)[IX(j, i)]
+#define A3(a, j, i, k) (a)[((size_t)(k) - 1) * o->plane + IX(j, i)]
+#define SJ(s, j, k) (s)[((size_t)(k) - 1) * (size_t)o->nj + (size_t)((j) - o->j0)]
+#define SI(s, i, k) (s)[((size_t)(k) - 1) * (size_t)o->ni + (size_t)((i) - o->i0)]
+#define DELD(j, i, n, s) o->deld[(((size_t)(s) - 1) * o->nsplit + ((n) - 1)) * o->plane + IX(j, i)]
+#define DELH(j, i, n, s) o->delh[(((size_t)(s) - 1) * o->nsplit + ((n) - 1)) * o->plane + IX(j, i)]
+
+static double* alloc3(orc_t* o, int nk) {
+  return (double*)calloc((size_t)nk * o->plane, sizeof(double));
+}
+static double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }
+static double dmin(double a, double b) { return (a < b) ? a : (b < a ? b : a); }
+
+static void xch(orc_t* o, double* a, int nk, int nex, int sides) {
+  if (o->xfn) o->xfn(o->xctx, a, nk, nex, sides);
+}
+static void xchb(orc_t* o, double* s, int along) {
+  if (o->bfn) o->bfn(o->xctx, s, o->kz, along);
+}
+
+/* ---- set_nproc tile extents, Main/mpplib/mod_mppparam.F90:1295-1360 ---- */
+static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4]) {
+  int lj = tile / ci, li = tile % ci;
+  int jxp = jx / cj, iyp = iy / ci;
+  int js = lj * jxp + 1, is = li * iyp + 1;
+  if (jxp * cj < jx) {
+    int imiss = jx - jxp * cj;
+    if (lj < imiss) { js += lj; jxp += 1; } else { js += imiss; }
+  }
+  if (iyp * ci < iy) {
+    int imiss = iy - iyp * ci;
+    if (li < imiss) { is += li; iyp += 1; } else { is += imiss; }
+  }
+  int je = js + jxp - 1, ie = is + iyp - 1;
+  ext[0] = js; ext[1] = je; ext[2] = is; ext[3] = ie;
+  ext[4] = js; ext[5] = (je == jx) ? je - 1 : je;
+  ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
+  bdy[0] = (lj == 0); bdy[1] = (lj == cj - 1); bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+}
+
+/* ---- setup_boundaries, Main/mod_atm_interface.F90:383-542 (non-band, non-CRM) ---- */
+static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
+  int jx = o->jx, iy = o->iy;
+  int icx = ldot ? 0 : 1, icy = ldot ? 0 : 1;
+  int nsp = ldot ? o->cfg.nspgd : o->cfg.nspgx;
+  int igbb1 = 2, igbb2 = nsp - 1, jgbl1 = 2, jgbl2 = nsp - 1;
+  int igbt1 = iy - icy - nsp + 2, igbt2 = iy - icy - 1;
+  int jgbr1 = jx - icx - nsp + 2, jgbr2 = jx - icx - 1;
+  for (int i = o->i0; i < o->i0 + o->ni; i++)
+    for (int j = o->j0; j < o->j0 + o->nj; j++) { A2(rg, j, i) = 0; A2(ib, j, i) = -1; }
+  for (int i = o->ide1; i <= o->ide2; i++) {   /* South */
+    if (i >= igbb1 && i <= igbb2)
+      for (int j = o->jde1; j <= o->jde2; j++)
+        if (j >= jgbl1 && j <= jgbr2) {
+          if (j <= jgbl2 && i >= j) continue;
+          if (j >= jgbr1 && i >= (jgbr2 - j + 2)) continue;
+          A2(ib, j, i) = i - igbb1 + 2; A2(rg, j, i) = 1;
+        }
+  }
+  for (int i = o->ide1; i <= o->ide2; i++) {   /* North */
+    if (i >= igbt1 && i <= igbt2)
+      for (int j = o->jde1; j <= o->jde2; j++)
+        if (j >= jgbl1 && j <= jgbr2) {
+          if (j <= jgbl2 && (igbt2 - i + 2) >= j) continue;
+          if (j >= jgbr1 && (igbt2 - i) >= (jgbr2 - j)) continue;
+          A2(ib, j, i) = igbt2 - i + 2; A2(rg, j, i) = 2;
+        }
+  }
+  for (int i = o->ide1; i <= o->ide2; i++) {   /* West */
+    if (i < igbb1 || i > igbt2) continue;
+    for (int j = o->jde1; j <= o->jde2; j++)
+      if (j >= jgbl1 && j <= jgbl2) {
+        if (i < igbb2 && j > i) continue;
+        if (i > igbt1 && j > (igbt2 - i + 2)) continue;
+        A2(ib, j, i) = j - jgbl1 + 2; A2(rg, j, i) = 3;
+      }
+  }
+  for (int i = o->ide1; i <= o->ide2; i++) {   /* East */
+    if (i < igbb1 || i > igbt2) continue;
+    for (int j = o->jde1; j <= o->jde2; j++)
+      if (j >= jgbr1 && j <= jgbr2) {
+        if (i < igbb2 && (jgbr2 - j + 2) > i) continue;
+        if (i > igbt1 && (jgbr2 - j) > (igbt2 - i)) continue;
+        A2(ib, j, i) = jgbr2 - j + 2; A2(rg, j, i) = 4;
+      }
+  }
+}
+
+orc_t* orc_create(const rcmdyn_config* cfg) {
+  init_constants();
+  if (cfg->tile_count != 1 || cfg->kz > RCMDYN_MAXKZ || cfg->nsplit > RCMDYN_MAXSPLIT)
+    return NULL;
+  orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
+  o->cfg = *cfg;
+  o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
+  o->nsplit = cfg->nsplit; o->nqx = 2;
+  int ext[8], bdy[4];
+  tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy);
+  o->bl = bdy[0]; o->br = bdy[1]; o->bb = bdy[2]; o->bt = bdy[3];
+  /* Main/mod_atm_interface.F90:231-302 */
+  o->jde1 = o->jdi1 = o->jdii1 = ext[0]; o->jde2 = o->jdi2 = o->jdii2 = ext[1];
+  o->ide1 = o->idi1 = o->idii1 = ext[2]; o->ide2 = o->idi2 = o->idii2 = ext[3];
+  if (o->bl) { o->jdi1 = o->jde1 + 1; o->jdii1 = o->jde1 + 2; }
+  if (o->br) { o->jdi2 = o->jde2 - 1; o->jdii2 = o->jde2 - 2; }
+  if (o->bb) { o->idi1 = o->ide1 + 1; o->idii1 = o->ide1 + 2; }
+  if (o->bt) { o->idi2 = o->ide2 - 1; o->idii2 = o->ide2 - 2; }
+  o->jce1 = o->jci1 = o->jcii1 = ext[4]; o->jce2 = o->jci2 = o->jcii2 = ext[5];
+  o->ice1 = o->ici1 = o->icii1 = ext[6]; o->ice2 = o->ici2 = o->icii2 = ext[7];
+  if (o->bl) { o->jci1 = o->jce1 + 1; o->jcii1 = o->jce1 + 2; }
+  if (o->br) { o->jci2 = o->jce2 - 1; o->jcii2 = o->jce2 - 2; }
+  if (o->bb) { o->ici1 = o->ice1 + 1; o->icii1 = o->ice1 + 2; }
+  if (o->bt) { o->ici2 = o->ice2 - 1; o->icii2 = o->ice2 - 2; }
+  int gl = o->bl ? 0 : 1, gr = o->br ? 0 : 1, gbm = o->bb ? 0 : 1, gt = o->bt ? 0 : 1;
+  o->jde1ga = o->jde1 - gl; o->jde2ga = o->jde2 + gr; o->ide1ga = o->ide1 - gbm; o->ide2ga = o->ide2 + gt;
+  o->jce1ga = o->jce1 - gl; o->jce2ga = o->jce2 + gr; o->ice1ga = o->ice1 - gbm; o->ice2ga = o->ice2 + gt;
+  o->jci1ga = o->jci1 - gl; o->jci2ga = o->jci2 + gr; o->ici1ga = o->ici1 - gbm; o->ici2ga = o->ici2 + gt;
+  o->jde1gb = o->jde1 - 2 * gl; o->jde2gb = o->jde2 + 2 * gr; o->ide1gb = o->ide1 - 2 * gbm; o->ide2gb = o->ide2 + 2 * gt;
+  o->jce1gb = o->jce1 - 2 * gl; o->jce2gb = o->jce2 + 2 * gr; o->ice1gb = o->ice1 - 2 * gbm; o->ice2gb = o->ice2 + 2 * gt;
+  o->j0 = o->jde1 - GO; o->i0 = o->ide1 - GO;
+  o->nj = (o->jde2 - o->jde1 + 1) + 2 * GO; o->ni = (o->ide2 - o->ide1 + 1) + 2 * GO;
+  o->plane = (size_t)o->nj * (size_t)o->ni;
+
+  /* derived run constants, Main/mod_params.F90:1628-1770, 2006-2011, 2208-2215 */
+  o->dtsec = cfg->dtsec; o->dt = cfg->dtsec; o->lcount = 0; o->xbctime = 0.0;
+  o->ptop = cfg->ptop;
+  o->dx = cfg->ds * d_1000; o->dx2 = d_two * o->dx; o->dx4 = d_four * o->dx;
+  o->dx8 = 8.0 * o->dx; o->dx16 = 16.0 * o->dx; o->dxsq = o->dx * o->dx;
+  o->rdxsq = 1.0 / o->dxsq;
+  int kz = o->kz;
+  for (int k = 1; k <= kz + 1; k++) o->sigma[k] = cfg->sigma[k - 1];
+  for (int k = 1; k <= kz; k++) {
+    o->hsigma[k] = (o->sigma[k + 1] + o->sigma[k]) * d_half;
+    o->dsigma[k] = (o->sigma[k + 1] - o->sigma[k]);
+  }
+  o->twt1[1] = 0; o->twt2[1] = 0; o->qcon[1] = 0;
+  for (int k = 2; k <= kz; k++) {
+    o->twt1[k] = (o->sigma[k] - o->hsigma[k - 1]) / (o->hsigma[k] - o->hsigma[k - 1]);
+    o->twt2[k] = d_one - o->twt1[k];
+    o->qcon[k] = (o->sigma[k] - o->hsigma[k]) / (o->hsigma[k - 1] - o->hsigma[k]);
+  }
+  /* init_advection, Main/mod_advection.F90:100-106 (dt == dtsec at init: quirk kept) */
+  for (int k = 1; k <= kz; k++) o->xds[k] = d_one / o->dsigma[k];
+  o->dds[1] = 0; o->dds[kz + 1] = 0;
+  for (int k = 2; k <= kz; k++) o->dds[k] = d_one / (o->dsigma[k] + o->dsigma[k - 1]);
+  o->ul = cfg->uoffc * d_half * o->dt / o->dx;
+  /* initialize_diffusion, Main/mod_diffusion.F90:104-107 (idynamic = 1) */
+  o->xkhmax = o->dxsq / (64.0 * o->dtsec);
+  o->dydc = cfg->adyndif * VONKAR * VONKAR * o->dx * d_rfour;
+  o->xkhz = cfg->ckh * 1.5e-3 * o->dxsq / o->dtsec;
+  /* setup_bdycon, Main/mod_bdycod.F90:203-274 */
+  o->fnudge = (cfg->bdy_nm > 0) ? cfg->bdy_nm : 0.1 / o->dt;
+  o->gnudge = (cfg->bdy_dm > 0) ? cfg->bdy_dm : d_one / (o->dt * 50.0);
+  for (int n = 2; n <= cfg->nspgx - 1 && n < 256; n++) {
+    double xfun = (double)(cfg->nspgx - n) / (double)(cfg->nspgx - 2);
+    o->fcx[n] = o->fnudge * xfun; o->gcx[n] = o->gnudge * xfun;
+  }
+  for (int k = 1; k <= kz; k++) {
+    double an = (o->hsigma[k] < 0.4) ? cfg->high_nudge
+              : (o->hsigma[k] < 0.8) ? cfg->medium_nudge : cfg->low_nudge;
+    for (int n = 2; n <= cfg->nspgx - 1 && n < 256; n++) {
+      double xfun = exp(-((double)(n - 2) / an));
+      o->hefc[n][k] = o->fnudge * xfun; o->hegc[n][k] = o->gnudge * xfun;
+    }
+  }
+  /* splitf scalar geopotential terms, Main/mod_split.F90:343-353 */
+  for (int l = 1; l <= o->nsplit; l++)
+    for (int k = 1; k <= kz + 1; k++) {
+      double sh = cfg->sigmah[k - 1], va = cfg->varpa1[l - 1][k - 1];
+      o->pdlog[l - 1][k] = va * log(sh * cfg->pd + o->ptop);
+      o->eps1[l - 1][k] = va * sh / (sh * cfg->pd + o->ptop);
+    }
+
+  int kp = kz + 1;
+  o->rg_cr = (signed char*)calloc(o->plane, 1); o->rg_dt = (signed char*)calloc(o->plane, 1);
+  o->ib_cr = (int*)calloc(o->plane, sizeof(int)); o->ib_dt = (int*)calloc(o->plane, sizeof(int));
+  setup_boundaries(o, 0, o->rg_cr, o->ib_cr);
+  setup_boundaries(o, 1, o->rg_dt, o->ib_dt);
+  o->a1u = alloc3(o, kz); o->a1v = alloc3(o, kz); o->a1t = alloc3(o, kz);
+  o->a2u = alloc3(o, kz); o->a2v = alloc3(o, kz); o->a2t = alloc3(o, kz);
+  for (int n = 0; n < 2; n++) {
+    o->a1q[n] = alloc3(o, kz); o->a2q[n] = alloc3(o, kz); o->xq[n] = alloc3(o, kz);
+    o->qb3d[n] = alloc3(o, kz); o->qten[n] = alloc3(o, kz); o->qdyn[n] = alloc3(o, kz);
+    o->cq[n] = alloc3(o, kz);
+  }
+  o->psa = alloc3(o, 1); o->psb = alloc3(o, 1); o->psc = alloc3(o, 1);
+  o->psdota = alloc3(o, 1); o->psdotb = alloc3(o, 1);
+  o->dstor = alloc3(o, o->nsplit); o->hstor = alloc3(o, o->nsplit);
+  o->msfx = alloc3(o, 1); o->msfd = alloc3(o, 1); o->xmsf = alloc3(o, 1); o->dmsf = alloc3(o, 1);
+  o->coriol = alloc3(o, 1); o->ht = alloc3(o, 1); o->hgfact = alloc3(o, 1); o->map = alloc3(o, 1);
+  o->ub0 = alloc3(o, kz); o->ubt = alloc3(o, kz); o->vb0 = alloc3(o, kz); o->vbt = alloc3(o, kz);
+  o->tb0 = alloc3(o, kz); o->tbt = alloc3(o, kz); o->qb0 = alloc3(o, kz); o->qbt = alloc3(o, kz);
+  o->pb0 = alloc3(o, 1); o->pbt = alloc3(o, 1);
+  o->rpsa = alloc3(o, 1); o->rpsb = alloc3(o, 1); o->rpsc = alloc3(o, 1); o->rpsda = alloc3(o, 1);
+  o->srpsb = alloc3(o, 1); o->rpsdotb = alloc3(o, 1);
+  o->uc = alloc3(o, kz); o->vc = alloc3(o, kz); o->umc = alloc3(o, kz); o->vmc = alloc3(o, kz);
+  o->ud = alloc3(o, kz); o->vd = alloc3(o, kz); o->xt = alloc3(o, kz); o->xtv = alloc3(o, kz);
+  o->cr = alloc3(o, kz); o->pten = alloc3(o, 1); o->qdot = alloc3(o, kp); o->omega = alloc3(o, kz);
+  o->dummy = alloc3(o, 1);
+  o->ubd = alloc3(o, kz); o->vbd = alloc3(o, kz); o->tb3d = alloc3(o, kz);
+  o->pb3d = alloc3(o, kz); o->pf3d = alloc3(o, kp);
+  o->xkc = alloc3(o, kz); o->xkd = alloc3(o, kz);
+  o->tten = alloc3(o, kz); o->tdyn = alloc3(o, kz); o->uten = alloc3(o, kz); o->udyn = alloc3(o, kz);
+  o->vten = alloc3(o, kz); o->vdyn = alloc3(o, kz);
+  o->fg = alloc3(o, kz); o->uavg1 = alloc3(o, kz); o->uavg2 = alloc3(o, kz);
+  o->vavg1 = alloc3(o, kz); o->vavg2 = alloc3(o, kz); o->dotqdot = alloc3(o, kz);
+  o->fg1 = alloc3(o, kp); o->fg2 = alloc3(o, kz);
+  o->ct = alloc3(o, kz); o->cu = alloc3(o, kz); o->cv = alloc3(o, kz);
+  o->td = alloc3(o, kz); o->tvfac = alloc3(o, kz); o->phi = alloc3(o, kz);
+  o->deld = alloc3(o, 3 * o->nsplit); o->delh = alloc3(o, 3 * o->nsplit);
+  o->ddsum = alloc3(o, o->nsplit); o->dhsum = alloc3(o, o->nsplit);
+  o->xdelh = alloc3(o, 1); o->work = alloc3(o, 3); o->uu = alloc3(o, 1); o->vv = alloc3(o, 1);
+  o->uuu = alloc3(o, kz); o->vvv = alloc3(o, kz);
+  size_t sjn = (size_t)o->nj * kz, sin_ = (size_t)o->ni * kz;
+  o->sue = calloc(sjn, 8); o->sui = calloc(sjn, 8); o->nue = calloc(sjn, 8); o->nui = calloc(sjn, 8);
+  o->sve = calloc(sjn, 8); o->svi = calloc(sjn, 8); o->nve = calloc(sjn, 8); o->nvi = calloc(sjn, 8);
+  o->wue = calloc(sin_, 8); o->wui = calloc(sin_, 8); o->eue = calloc(sin_, 8); o->eui = calloc(sin_, 8);
+  o->wve = calloc(sin_, 8); o->wvi = calloc(sin_, 8); o->eve = calloc(sin_, 8); o->evi = calloc(sin_, 8);
+  return o;
+}
+
+void orc_destroy(orc_t* o) {
+  if (!o) return;
+  double** ptrs[] = {
+    &o->a1u, &o->a1v, &o->a1t, &o->a2u, &o->a2v, &o->a2t, &o->psa, &o->psb, &o->psc,
+    &o->psdota, &o->psdotb, &o->dstor, &o->hstor, &o->msfx, &o->msfd, &o->xmsf, &o->dmsf,
+    &o->coriol, &o->ht, &o->hgfact, &o->map, &o->ub0, &o->ubt, &o->vb0, &o->vbt, &o->tb0,
+    &o->tbt, &o->qb0, &o->qbt, &o->pb0, &o->pbt, &o->rpsa, &o->rpsb, &o->rpsc, &o->rpsda,
+    &o->srpsb, &o->rpsdotb, &o->uc, &o->vc, &o->umc, &o->vmc, &o->ud, &o->vd, &o->xt, &o->xtv,
+    &o->cr, &o->pten, &o->qdot, &o->omega, &o->dummy, &o->ubd, &o->vbd, &o->tb3d, &o->pb3d,
+    &o->pf3d, &o->xkc, &o->xkd, &o->tten, &o->tdyn, &o->uten, &o->udyn, &o->vten, &o->vdyn,
+    &o->fg, &o->uavg1, &o->uavg2, &o->vavg1, &o->vavg2, &o->dotqdot, &o->fg1, &o->fg2, &o->ct,
+    &o->cu, &o->cv, &o->td, &o->tvfac, &o->phi, &o->deld, &o->delh, &o->ddsum, &o->dhsum,
+    &o->xdelh, &o->work, &o->uu, &o->vv, &o->uuu, &o->vvv, &o->sue, &o->sui, &o->nue, &o->nui,
+    &o->sve, &o->svi, &o->nve, &o->nvi, &o->wue, &o->wui, &o->eue, &o->eui, &o->wve, &o->wvi,
+    &o->eve, &o->evi};
+  for (size_t p = 0; p < sizeof(ptrs) / sizeof(ptrs[0]); p++) free(*ptrs[p]);
+  for (int n = 0; n < 2; n++) {
+    free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
+    free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
+  }
+  free(o->rg_cr); free(o->rg_dt); free(o->ib_cr); free(o->ib_dt);
+  free(o);
+}
+
+void orc_set_exchange(orc_t* o, orc_exchange_fn fn, orc_exchange_bdy_fn bfn, void* ctx) {
+  o->xfn = fn; o->bfn = bfn; o->xctx = ctx;
+}
+
+void orc_frame_info(const orc_t* o, int info[16]) {
+  info[0] = o->j0; info[1] = o->i0; info[2] = o->nj; info[3] = o->ni;
+  info[4] = o->jde1; info[5] = o->jde2; info[6] = o->ide1; info[7] = o->ide2;
+  info[8] = o->jce1; info[9] = o->jce2; info[10] = o->ice1; info[11] = o->ice2;
+  info[12] = o->bl; info[13] = o->br; info[14] = o->bb; info[15] = o->bt;
+}
+
+void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime) {
+  o->lcount = lcount; o->dt = dt; o->xbctime = xbctime;
+}
+void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime) {
+  *lcount = o->lcount; *dt = o->dt; *xbctime = o->xbctime;
+}
+void orc_diagnostics(const orc_t* o, double out[4]) {
+  out[0] = o->ptntot; out[1] = o->pt2tot; out[2] = isnan(o->ptntot) ? 1.0 : 0.0; out[3] = 0;
+}
+
+static double* field_ptr(orc_t* o, int f, int* nk) {
+  *nk = o->kz;
+  switch (f) {
+    case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
+    case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
+    case RCMDYN_ATM1_QC: return o->a1q[1];
+    case RCMDYN_ATM2_U: return o->a2u;   case RCMDYN_ATM2_V: return o->a2v;
+    case RCMDYN_ATM2_T: return o->a2t;   case RCMDYN_ATM2_QV: return o->a2q[0];
+    case RCMDYN_ATM2_QC: return o->a2q[1];
+    case RCMDYN_XUB_B0: return o->ub0;   case RCMDYN_XUB_BT: return o->ubt;
+    case RCMDYN_XVB_B0: return o->vb0;   case RCMDYN_XVB_BT: return o->vbt;
+    case RCMDYN_XTB_B0: return o->tb0;   case RCMDYN_XTB_BT: return o->tbt;
+    case RCMDYN_XQB_B0: return o->qb0;   case RCMDYN_XQB_BT: return o->qbt;
+    case RCMDYN_TTEN: return o->tten;    case RCMDYN_UTEN: return o->uten;
+    case RCMDYN_VTEN: return o->vten;    case RCMDYN_QVTEN: return o->qten[0];
+    case RCMDYN_QCTEN: return o->qten[1];
+    case RCMDYN_OMEGA: return o->omega;  case RCMDYN_XKC: return o->xkc;
+    case RCMDYN_PHI: return o->phi;
+    case RCMDYN_QDOT: *nk = o->kz + 1; return o->qdot;
+    case RCMDYN_DSTOR: *nk = o->nsplit; return o->dstor;
+    case RCMDYN_HSTOR: *nk = o->nsplit; return o->hstor;
+    default: break;
+  }
+  *nk = 1;
+  switch (f) {
+    case RCMDYN_PSA: return o->psa;      case RCMDYN_PSB: return o->psb;
+    case RCMDYN_MSFX: return o->msfx;    case RCMDYN_MSFD: return o->msfd;
+    case RCMDYN_CORIOL: return o->coriol; case RCMDYN_HT: return o->ht;
+    case RCMDYN_XPSB_B0: return o->pb0;  case RCMDYN_XPSB_BT: return o->pbt;
+    case RCMDYN_PSC: return o->psc;      case RCMDYN_PTEN: return o->pten;
+    case RCMDYN_PSDOTA: return o->psdota;
+    default: return NULL;
+  }
+}
+
+static void prepare_static(orc_t* o);
+
+int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
+  int nk; double* a = field_ptr(o, field, &nk);
+  if (!a) return 1;
+  int nj = j2 - j1 + 1, ni = i2 - i1 + 1;
+  for (int k = k1; k <= k2; k++) {
+    if (k < 1 || k > nk) continue;
+    for (int i = i1; i <= i2; i++) {
+      if (i < o->i0 || i >= o->i0 + o->ni) continue;
+      for (int j = j1; j <= j2; j++) {
+        if (j < o->j0 || j >= o->j0 + o->nj) continue;
+        A3(a, j, i, k) = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)];
+      }
+    }
+  }
+  if (field == RCMDYN_MSFX || field == RCMDYN_MSFD || field == RCMDYN_HT) prepare_static(o);
+  return 0;
+}
+
+int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
+  int nk; double* a = field_ptr(o, field, &nk);
+  if (!a) return 1;
+  int nj = j2 - j1 + 1, ni = i2 - i1 + 1;
+  for (int k = k1; k <= k2; k++) {
+    if (k < 1 || k > nk) continue;
+    for (int i = i1; i <= i2; i++) {
+      if (i < o->ide1 || i > o->ide2) continue;
+      for (int j = j1; j <= j2; j++) {
+        if (j < o->jde1 || j > o->jde2) continue;
+        dst[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)] = A3(a, j, i, k);
+      }
+    }
+  }
+  return 0;
+}
+
+/* Static derived fields: Main/mod_params.F90:1993-2001 (xmsf, dmsf),
+ * Main/mod_diffusion.F90:124-140 (hgfact), Main/mod_split.F90:99-101 (map). */
+static void prepare_static(orc_t* o) {
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++) {
+      A2(o->dmsf, j, i) = d_one / (A2(o->msfd, j, i) * A2(o->msfd, j, i) * o->dx16);
+      A2(o->xmsf, j, i) = d_one / (A2(o->msfx, j, i) * A2(o->msfx, j, i) * o->dx4);
+    }
+  for (int i = o->ice1ga; i <= o->ice2ga; i++)
+    for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->hgfact, j, i) = o->xkhz;
+  if (o->cfg.diffu_hgtf == 1) {
+    for (int i = o->ici1ga; i <= o->ici2ga; i++)
+      for (int j = o->jci1ga; j <= o->jci2ga; j++) {
+        double h = A2(o->ht, j, i);
+        double hg1 = fabs((h - A2(o->ht, j, i - 1)) / o->dx);
+        double hg2 = fabs((h - A2(o->ht, j, i + 1)) / o->dx);
+        double hg3 = fabs((h - A2(o->ht, j - 1, i)) / o->dx);
+        double hg4 = fabs((h - A2(o->ht, j + 1, i)) / o->dx);
+        double hgmax = dmax(dmax(dmax(hg1, hg2), hg3), hg4) * c_regrav * 1.0e3;
+        A2(o->hgfact, j, i) = o->xkhz / (d_one + hgmax * hgmax);
+      }
+  }
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++)
+      A2(o->map, j, i) = d_one / (A2(o->msfx, j, i) * A2(o->msfx, j, i));
+}
+
+/* psc2psd, Main/mpplib/mod_mppparam.F90:13811-13862 */
+static void psc2psd(orc_t* o, const double* pc, double* pd) {
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++)
+      A2(pd, j, i) = (A2(pc, j, i) + A2(pc, j, i - 1) + A2(pc, j - 1, i) + A2(pc, j - 1, i - 1)) * d_rfour;
+  if (o->bt) for (int j = o->jdi1; j <= o->jdi2; j++)
+    A2(pd, j, o->ide2) = (A2(pc, j, o->ice2) + A2(pc, j - 1, o->ice2)) * d_half;
+  if (o->bb) for (int j = o->jdi1; j <= o->jdi2; j++)
+    A2(pd, j, o->ide1) = (A2(pc, j, o->ice1) + A2(pc, j - 1, o->ice1)) * d_half;
+  if (o->bl) for (int i = o->idi1; i <= o->idi2; i++)
+    A2(pd, o->jde1, i) = (A2(pc, o->jce1, i) + A2(pc, o->jce1, i - 1)) * d_half;
+  if (o->br) for (int i = o->idi1; i <= o->idi2; i++)
+    A2(pd, o->jde2, i) = (A2(pc, o->jce2, i) + A2(pc, o->jce2, i - 1)) * d_half;
+  if (o->bb && o->bl) A2(pd, o->jde1, o->ide1) = A2(pc, o->jce1, o->ice1);
+  if (o->bt && o->bl) A2(pd, o->jde1, o->ide2) = A2(pc, o->jce1, o->ice2);
+  if (o->bb && o->br) A2(pd, o->jde2, o->ide1) = A2(pc, o->jce2, o->ice1);
+  if (o->bt && o->br) A2(pd, o->jde2, o->ide2) = A2(pc, o->jce2, o->ice2);
+}
+
+/* surface_pressures, Main/mod_tendency.F90:815-834 */
+static void surface_pressures(orc_t* o) {
+  xch(o, o->psa, 1, 1, 0);
+  for (int i = o->ice1ga; i <= o->ice2ga; i++)
+    for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->rpsa, j, i) = d_one / A2(o->psa, j, i);
+  psc2psd(o, o->psa, o->psdota);
+  xch(o, o->psdota, 1, 1, 0);
+  xch(o, o->psb, 1, 2, 0);
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) A2(o->rpsb, j, i) = d_one / A2(o->psb, j, i);
+  psc2psd(o, o->psb, o->psdotb);
+  xch(o, o->psdotb, 1, 2, 0);
+}
+
+/* decouple, Main/mod_tendency.F90:852-1116 (hydrostatic branches) */
+static void decouple(orc_t* o) {
+  int kz = o->kz;
+  for (int i = o->ide1ga; i <= o->ide2ga; i++)
+    for (int j = o->jde1ga; j <= o->jde2ga; j++) A2(o->rpsda, j, i) = d_one / A2(o->psdota, j, i);
+  xch(o, o->a1u, kz, 1, 0); xch(o, o->a1v, kz, 1, 0); xch(o, o->a1t, kz, 1, 0);
+  xch(o, o->a1q[0], kz, 1, 0); xch(o, o->a1q[1], kz, 1, 0);
+  for (int k = 1; k <= kz; k++)                                   /* :879-884 */
+    for (int i = o->ide1ga; i <= o->ide2ga; i++)
+      for (int j = o->jde1ga; j <= o->jde2ga; j++) {
+        A3(o->uc, j, i, k) = A3(o->a1u, j, i, k);
+        A3(o->vc, j, i, k) = A3(o->a1v, j, i, k);
+        A3(o->umc, j, i, k) = A3(o->a1u, j, i, k) * A2(o->msfd, j, i);
+        A3(o->vmc, j, i, k) = A3(o->a1v, j, i, k) * A2(o->msfd, j, i);
+      }
+  for (int k = 1; k <= kz; k++)                                   /* :888-891 */
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->ud, j, i, k) = A3(o->a1u, j, i, k) * A2(o->rpsda, j, i);
+        A3(o->vd, j, i, k) = A3(o->a1v, j, i, k) * A2(o->rpsda, j, i);
+      }
+  if (o->bl) {                                                    /* :895-907 */
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->ud, o->jdi1, i, k) = SI(o->wui, i, k) * A2(o->rpsda, o->jdi1, i);
+        A3(o->vd, o->jdi1, i, k) = SI(o->wvi, i, k) * A2(o->rpsda, o->jdi1, i);
+      }
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->ud, o->jde1, i, k) = SI(o->wue, i, k) * A2(o->rpsda, o->jde1, i);
+        A3(o->vd, o->jde1, i, k) = SI(o->wve, i, k) * A2(o->rpsda, o->jde1, i);
+      }
+  }
+  if (o->br) {                                                    /* :920-932 */
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->ud, o->jdi2, i, k) = SI(o->eui, i, k) * A2(o->rpsda, o->jdi2, i);
+        A3(o->vd, o->jdi2, i, k) = SI(o->evi, i, k) * A2(o->rpsda, o->jdi2, i);
+      }
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->ud, o->jde2, i, k) = SI(o->eue, i, k) * A2(o->rpsda, o->jde2, i);
+        A3(o->vd, o->jde2, i, k) = SI(o->eve, i, k) * A2(o->rpsda, o->jde2, i);
+      }
+  }
+  if (o->bb) {                                                    /* :945-957 */
+    for (int k = 1; k <= kz; k++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->ud, j, o->idi1, k) = SJ(o->sui, j, k) * A2(o->rpsda, j, o->idi1);
+        A3(o->vd, j, o->idi1, k) = SJ(o->svi, j, k) * A2(o->rpsda, j, o->idi1);
+      }
+    for (int k = 1; k <= kz; k++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->ud, j, o->ide1, k) = SJ(o->sue, j, k) * A2(o->rpsda, j, o->ide1);
+        A3(o->vd, j, o->ide1, k) = SJ(o->sve, j, k) * A2(o->rpsda, j, o->ide1);
+      }
+  }
+  if (o->bt) {                                                    /* :970-982 */
+    for (int k = 1; k <= kz; k++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->ud, j, o->idi2, k) = SJ(o->nui, j, k) * A2(o->rpsda, j, o->idi2);
+        A3(o->vd, j, o->idi2, k) = SJ(o->nvi, j, k) * A2(o->rpsda, j, o->idi2);
+      }
+    for (int k = 1; k <= kz; k++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->ud, j, o->ide2, k) = SJ(o->nue, j, k) * A2(o->rpsda, j, o->ide2);
+        A3(o->vd, j, o->ide2, k) = SJ(o->nve, j, k) * A2(o->rpsda, j, o->ide2);
+      }
+  }
+  xch(o, o->ud, kz, 1, 0); xch(o, o->vd, kz, 1, 0);            /* :1003-1004 */
+  /* umd/vmd (:1005-1008) feed only non-hydrostatic terms: not needed for idynamic=1 */
+  for (int k = 1; k <= kz; k++)                                   /* :1013-1025 */
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++) {
+        double rp = A2(o->rpsa, j, i);
+        A3(o->xt, j, i, k) = A3(o->a1t, j, i, k) * rp;
+        A3(o->xq[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) * rp, MINQQ);
+        A3(o->xq[1], j, i, k) = dmax(A3(o->a1q[1], j, i, k) * rp, d_zero);
+        A3(o->xtv, j, i, k) = A3(o->xt, j, i, k) * (d_one + c_ep1 * A3(o->xq[0], j, i, k));
+      }
+  /* atm1%pr/rho (:1037-1040) and atm2%pr (:1094-1096) feed only physics: skipped */
+  xch(o, o->a2u, kz, 2, 0); xch(o, o->a2v, kz, 2, 0); xch(o, o->a2t, kz, 2, 0);
+  xch(o, o->a2q[0], kz, 2, 0); xch(o, o->a2q[1], kz, 2, 0);
+}
+
+/* compute_omega, Main/mod_tendency.F90:1118-1215 (hydrostatic) */
+static void compute_omega(orc_t* o) {
+  int kz = o->kz;
+  memset(o->qdot, 0, sizeof(double) * o->plane * (kz + 1));
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++)
+      A2(o->dummy, j, i) = d_one / (o->dx2 * A2(o->msfx, j, i) * A2(o->msfx, j, i));
+  memset(o->pten, 0, sizeof(double) * o->plane);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double a = A3(o->umc, j + 1, i + 1, k) + A3(o->umc, j + 1, i, k) - A3(o->umc, j, i + 1, k) - A3(o->umc, j, i, k);
+        double b = A3(o->vmc, j + 1, i + 1, k) + A3(o->vmc, j, i + 1, k) - A3(o->vmc, j + 1, i, k) - A3(o->vmc, j, i, k);
+        A3(o->cr, j, i, k) = (a + b) * A2(o->dummy, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A2(o->pten, j, i) = A2(o->pten, j, i) - A3(o->cr, j, i, k) * o->dsigma[k];
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++)
+      for (int k = 2; k <= kz; k++)
+        A3(o->qdot, j, i, k) = A3(o->qdot, j, i, k - 1) -
+            (A2(o->pten, j, i) + A3(o->cr, j, i, k - 1)) * o->dsigma[k - 1] * A2(o->rpsa, j, i);
+  xch(o, o->cr, kz, 1, 0);
+  xch(o, o->qdot, kz + 1, 1, 0);
+  memset(o->omega, 0, sizeof(double) * o->plane * kz);
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      A2(o->dummy, j, i) = d_one / (o->dx8 * A2(o->msfx, j, i));
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double su = A3(o->ud, j, i, k) + A3(o->ud, j, i + 1, k) + A3(o->ud, j + 1, i + 1, k) + A3(o->ud, j + 1, i, k);
+        double sv = A3(o->vd, j, i, k) + A3(o->vd, j, i + 1, k) + A3(o->vd, j + 1, i + 1, k) + A3(o->vd, j + 1, i, k);
+        double x = su * (A2(o->psa, j + 1, i) - A2(o->psa, j - 1, i)) +
+                   sv * (A2(o->psa, j, i + 1) - A2(o->psa, j, i - 1));
+        A3(o->omega, j, i, k) = d_half * (A3(o->qdot, j, i, k + 1) + A3(o->qdot, j, i, k)) * A2(o->psa, j, i) +
+                                o->hsigma[k] * (A2(o->pten, j, i) + x * A2(o->dummy, j, i));
+      }
+}
+
+/* mkslice, Main/mod_slice.F90:102-300 -- the subset the hydrostatic dyn core reads
+ * (ubd3d, vbd3d, tb3d, qxb3d, pb3d, pf3d); the physics-only slices are not built. */
+static void mkslice(orc_t* o) {
+  int kz = o->kz;
+  for (int i = o->ice1gb; i <= o->ice2gb; i++)
+    for (int j = o->jce1gb; j <= o->jce2gb; j++) A2(o->srpsb, j, i) = d_one / A2(o->psb, j, i);
+  for (int i = o->ide1gb; i <= o->ide2gb; i++)
+    for (int j = o->jde1gb; j <= o->jde2gb; j++) A2(o->rpsdotb, j, i) = d_one / A2(o->psdotb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1gb; i <= o->ide2gb; i++)
+      for (int j = o->jde1gb; j <= o->jde2gb; j++) {
+        A3(o->ubd, j, i, k) = A3(o->a2u, j, i, k) * A2(o->rpsdotb, j, i);
+        A3(o->vbd, j, i, k) = A3(o->a2v, j, i, k) * A2(o->rpsdotb, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1gb; i <= o->ice2gb; i++)
+      for (int j = o->jce1gb; j <= o->jce2gb; j++) {
+        double rp = A2(o->srpsb, j, i);
+        A3(o->tb3d, j, i, k) = A3(o->a2t, j, i, k) * rp;
+        A3(o->qb3d[0], j, i, k) = dmax(A3(o->a2q[0], j, i, k) * rp, MINQQ);
+        A3(o->qb3d[1], j, i, k) = dmax(A3(o->a2q[1], j, i, k) * rp, d_zero);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->pb3d, j, i, k) = (o->hsigma[k] * A2(o->psb, j, i) + o->ptop) * d_1000;
+  for (int k = 1; k <= kz + 1; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->pf3d, j, i, k) = (o->sigma[k] * A2(o->psb, j, i) + o->ptop) * d_1000;
+}
+
+/* generic relaxation step shared by nudge2d/3d/4d3d/uv, Main/mod_bdycod.F90:4218-4766 */
+static inline double relax(double ften, double xf, double xg, double f0, double f1, double f2,
+                           double f3, double f4) {
+  return ften + xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0);
+}
+static void nudge_coef(orc_t* o, int ib, int k, double* xf, double* xg) {
+  if (o->cfg.iboudy == 1) { *xf = o->fcx[ib]; *xg = o->gcx[ib]; }
+  else { *xf = o->hefc[ib][k]; *xg = o->hegc[ib][k]; }
+}
+
+/* new_pressure, Main/mod_tendency.F90:1428-1460 (+ nudge2d :4597-4766) */
+static void new_pressure(orc_t* o) {
+  double xt = o->xbctime + o->dt;
+  for (int i = o->ice1ga; i <= o->ice2ga; i++)
+    for (int j = o->jce1ga; j <= o->jce2ga; j++)
+      A3(o->fg1, j, i, 1) = (A2(o->pb0, j, i) + xt * A2(o->pbt, j, i)) - A2(o->psb, j, i);
+  for (int r = 1; r <= 4; r++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        if (A2(o->rg_cr, j, i) != r) continue;
+        double xf, xg;
+        nudge_coef(o, A2(o->ib_cr, j, i), o->kz, &xf, &xg);
+        A2(o->pten, j, i) = relax(A2(o->pten, j, i), xf, xg, A3(o->fg1, j, i, 1), A3(o->fg1, j - 1, i, 1),
+                                  A3(o->fg1, j + 1, i, 1), A3(o->fg1, j, i - 1, 1), A3(o->fg1, j, i + 1, 1));
+      }
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) {
+      A2(o->psc, j, i) = A2(o->psb, j, i) + A2(o->pten, j, i) * o->dt;
+      A2(o->rpsc, j, i) = d_one / A2(o->psc, j, i);
+    }
+  o->ptntot = 0; o->pt2tot = 0;
+  if (o->lcount > 0)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        o->ptntot = o->ptntot + fabs(A2(o->pten, j, i));
+        o->pt2tot = o->pt2tot + fabs((A2(o->psc, j, i) + A2(o->psb, j, i) - d_two * A2(o->psa, j, i)) /
+                                     (o->dt * o->dt * d_rfour));
+      }
+}
+
+/* calc_coeff, Main/mod_diffusion.F90:169-251 (idiffu = 1, idynamic = 1) */
+static void calc_coeff(orc_t* o) {
+  int kz = o->kz;
+  memset(o->xkc, 0, sizeof(double) * o->plane * kz);
+  memset(o->xkd, 0, sizeof(double) * o->plane * kz);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double dudx = A3(o->ubd, j + 1, i, k) + A3(o->ubd, j + 1, i + 1, k) - A3(o->ubd, j, i, k) - A3(o->ubd, j, i + 1, k);
+        double dvdx = A3(o->vbd, j + 1, i, k) + A3(o->vbd, j + 1, i + 1, k) - A3(o->vbd, j, i, k) - A3(o->vbd, j, i + 1, k);
+        double dudy = A3(o->ubd, j, i + 1, k) + A3(o->ubd, j + 1, i + 1, k) - A3(o->ubd, j, i, k) - A3(o->ubd, j + 1, i, k);
+        double dvdy = A3(o->vbd, j, i + 1, k) + A3(o->vbd, j + 1, i + 1, k) - A3(o->vbd, j, i, k) - A3(o->vbd, j + 1, i, k);
+        double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
+        A3(o->xkc, j, i, k) = dmin(A2(o->hgfact, j, i) + o->dydc * duv, o->xkhmax);
+      }
+  xch(o, o->xkc, kz, 1, 0);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++)
+        A3(o->xkd, j, i, k) = d_rfour * (A3(o->xkc, j, i, k) + A3(o->xkc, j - 1, i - 1, k) +
+                                         A3(o->xkc, j - 1, i, k) + A3(o->xkc, j, i - 1, k));
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->xkc, j, i, k) = A3(o->xkc, j, i, k) * o->rdxsq * A2(o->psb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++)
+        A3(o->xkd, j, i, k) = A3(o->xkd, j, i, k) * o->rdxsq * A2(o->psdotb, j, i);
+}
+
+/* ---- advection, Main/mod_advection.F90 ---- */
+static void start_advect(orc_t* o) {                               /* :111-120 */
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(o->uavg1, j, i, k) = A3(o->umc, j, i + 1, k) + A3(o->umc, j, i, k);
+        A3(o->uavg2, j, i, k) = A3(o->umc, j + 1, i + 1, k) + A3(o->umc, j + 1, i, k);
+        A3(o->vavg1, j, i, k) = A3(o->vmc, j + 1, i, k) + A3(o->vmc, j, i, k);
+        A3(o->vavg2, j, i, k) = A3(o->vmc, j + 1, i + 1, k) + A3(o->vmc, j, i + 1, k);
+      }
+}
+
+static void hadvuv(orc_t* o) {                                     /* :203-233 */
+  const double* ua = o->umc; const double* va = o->vmc;
+  const double* u = o->ud; const double* v = o->vd;
+  double ul = o->ul;
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double ucmona = A3(ua, j, i + 1, k) + d_two * A3(ua, j, i, k) + A3(ua, j, i - 1, k);
+        double ucmonb = A3(ua, j + 1, i + 1, k) + d_two * A3(ua, j + 1, i, k) + A3(ua, j + 1, i - 1, k);
+        double ucmonc = A3(ua, j - 1, i + 1, k) + d_two * A3(ua, j - 1, i, k) + A3(ua, j - 1, i - 1, k);
+        double vcmona = A3(va, j + 1, i, k) + d_two * A3(va, j, i, k) + A3(va, j - 1, i, k);
+        double vcmonb = A3(va, j + 1, i + 1, k) + d_two * A3(va, j, i + 1, k) + A3(va, j - 1, i + 1, k);
+        double vcmonc = A3(va, j + 1, i - 1, k) + d_two * A3(va, j, i - 1, k) + A3(va, j - 1, i - 1, k);
+        double ff1 = ul * (A3(u, j + 1, i, k) + A3(u, j, i, k));
+        double ff2 = ul * (A3(u, j - 1, i, k) + A3(u, j, i, k));
+        double ff3 = ul * (A3(v, j, i + 1, k) + A3(v, j, i, k));
+        double ff4 = ul * (A3(v, j, i - 1, k) + A3(v, j, i, k));
+        ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+        ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+        vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+        vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        double dm = A2(o->dmsf, j, i);
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) - dm *
+            ((A3(u, j + 1, i, k) + A3(u, j, i, k)) * ucmonb - (A3(u, j, i, k) + A3(u, j - 1, i, k)) * ucmonc +
+             (A3(u, j, i + 1, k) + A3(u, j, i, k)) * vcmonb - (A3(u, j, i, k) + A3(u, j, i - 1, k)) * vcmonc);
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - dm *
+            ((A3(v, j + 1, i, k) + A3(v, j, i, k)) * ucmonb - (A3(v, j, i, k) + A3(v, j - 1, i, k)) * ucmonc +
+             (A3(v, j, i + 1, k) + A3(v, j, i, k)) * vcmonb - (A3(v, j, i, k) + A3(v, j, i - 1, k)) * vcmonc);
+      }
+}
+
+static void vadvuv(orc_t* o) {                                     /* :286-299 */
+  for (int k = 2; k <= o->kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double qq = d_rfour * (A3(o->qdot, j, i, k) + A3(o->qdot, j, i - 1, k) +
+                               A3(o->qdot, j - 1, i, k) + A3(o->qdot, j - 1, i - 1, k));
+        double uu = qq * (o->twt1[k] * A3(o->uc, j, i, k) + o->twt2[k] * A3(o->uc, j, i, k - 1));
+        double vv = qq * (o->twt1[k] * A3(o->vc, j, i, k) + o->twt2[k] * A3(o->vc, j, i, k - 1));
+        A3(o->udyn, j, i, k - 1) = A3(o->udyn, j, i, k - 1) - uu * o->xds[k - 1];
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + uu * o->xds[k];
+        A3(o->vdyn, j, i, k - 1) = A3(o->vdyn, j, i, k - 1) - vv * o->xds[k - 1];
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) + vv * o->xds[k];
+      }
+}
+
+/* upstream flux form shared by hadvt/hadvqv/hadvqx (:337-351, :547-561, :639-653) */
+static void hadv_scalar(orc_t* o, const double* f, double* ften, int limiter /*0 none,1 t,2 q*/) {
+  double ul = o->ul;
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double ps = A2(o->psa, j, i);
+        double f1 = d_half * ul * (A3(o->uavg2, j, i, k) + A3(o->uavg1, j, i, k)) / ps;
+        double f2 = d_half * ul * (A3(o->vavg2, j, i, k) + A3(o->vavg1, j, i, k)) / ps;
+        double fx1 = (d_one + f1) * A3(f, j - 1, i, k) + (d_one - f1) * A3(f, j, i, k);
+        double fx2 = (d_one + f1) * A3(f, j, i, k) + (d_one - f1) * A3(f, j + 1, i, k);
+        double fy1 = (d_one + f2) * A3(f, j, i - 1, k) + (d_one - f2) * A3(f, j, i, k);
+        double fy2 = (d_one + f2) * A3(f, j, i, k) + (d_one - f2) * A3(f, j, i + 1, k);
+        A3(o->fg, j, i, k) = -A2(o->xmsf, j, i) *
+            (A3(o->uavg2, j, i, k) * fx2 - A3(o->uavg1, j, i, k) * fx1 +
+             A3(o->vavg2, j, i, k) * fy2 - A3(o->vavg1, j, i, k) * fy1);
+      }
+  if (limiter && o->cfg.stability_enhance) {                       /* :359-386, :569-596 */
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double fc = A3(f, j, i, k);
+          double fn = A3(f, j, i + 1, k), fs = A3(f, j, i - 1, k);
+          double fe = A3(f, j + 1, i, k), fw = A3(f, j - 1, i, k);
+          double den, thr;
+          if (limiter == 1) { den = A2(o->psa, j, i); thr = o->cfg.t_extrema; }
+          else { den = dmax(fc, DLOWVAL); thr = o->cfg.q_rel_extrema; }
+          double* g = &A3(o->fg, j, i, k);
+          if (fabs(fn + fs - d_two * fc) / den > thr) {
+            if (fc > fn && fc > fs) *g = dmin(*g, d_zero);
+            else if (fc < fn && fc < fs) *g = dmax(*g, d_zero);
+          }
+          if (fabs(fe + fw - d_two * fc) / den > thr) {
+            if (fc > fe && fc > fw) *g = dmin(*g, d_zero);
+            else if (fc < fe && fc < fw) *g = dmax(*g, d_zero);
+          }
+        }
+  }
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(ften, j, i, k) = A3(ften, j, i, k) + A3(o->fg, j, i, k);
+}
+
+static void vadv3d_t(orc_t* o) {                                   /* :771-783, ind = 1 */
+  const double* f = o->a1t;
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) A3(o->dotqdot, j, i, 1) = d_zero;
+  for (int k = 2; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double pf = A3(o->pf3d, j, i, k);
+        A3(o->dotqdot, j, i, k) = A3(o->qdot, j, i, k) *
+            (o->twt1[k] * A3(f, j, i, k) * pow(pf / A3(o->pb3d, j, i, k), c_c287) +
+             o->twt2[k] * A3(f, j, i, k - 1) * pow(pf / A3(o->pb3d, j, i, k - 1), c_c287));
+      }
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      for (int k = 2; k <= o->kz; k++) {
+        A3(o->tdyn, j, i, k - 1) = A3(o->tdyn, j, i, k - 1) - A3(o->dotqdot, j, i, k) * o->xds[k - 1];
+        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + A3(o->dotqdot, j, i, k) * o->xds[k];
+      }
+}
+
+static void vadvqv(orc_t* o) {                                     /* :811-836 */
+  const double* f = o->a1q[0];
+  memset(o->fg, 0, sizeof(double) * o->plane * o->kz);
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      for (int k = 2; k <= o->kz; k++) {
+        double thr = MINQQ * A2(o->psa, j, i);
+        if (A3(f, j, i, k) > thr && A3(f, j, i, k - 1) > thr)
+          A3(o->fg, j, i, k) = A3(f, j, i, k) * pow(A3(f, j, i, k - 1) / A3(f, j, i, k), o->qcon[k]);
+      }
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      for (int k = 2; k <= o->kz; k++) {
+        double* t = o->qdyn[0];
+        A3(t, j, i, k - 1) = A3(t, j, i, k - 1) - A3(o->qdot, j, i, k) * A3(o->fg, j, i, k) * o->xds[k - 1];
+        A3(t, j, i, k) = A3(t, j, i, k) + A3(o->qdot, j, i, k) * A3(o->fg, j, i, k) * o->xds[k];
+      }
+}
+
+static void vadv4d_qc(orc_t* o) {                                  /* :859-961, ind = 1 */
+  const double* f = o->a1q[1];
+  memset(o->fg, 0, sizeof(double) * o->plane * o->kz);
+  for (int k = 2; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double svv = A3(o->qdot, j, i, k);
+        double thr = MINQQ * MINQQ * A2(o->psa, j, i);
+        double fk = A3(f, j, i, k), fkm = A3(f, j, i, k - 1);
+        if (svv > d_zero) {
+          A3(o->fg, j, i, k) = (fkm > thr) ? svv * (o->twt1[k] * fk + o->twt2[k] * fkm) : d_zero;
+        } else {
+          A3(o->fg, j, i, k) = (fk > thr) ? svv * (o->twt1[k] * fk + o->twt2[k] * fkm) : d_zero;
+        }
+      }
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      for (int k = 2; k <= o->kz; k++) {
+        double* t = o->qdyn[1];
+        A3(t, j, i, k - 1) = A3(t, j, i, k - 1) - A3(o->fg, j, i, k) * o->xds[k - 1];
+        A3(t, j, i, k) = A3(t, j, i, k) + A3(o->fg, j, i, k) * o->xds[k];
+      }
+}
+
+/* advection driver, Main/mod_tendency.F90:1270-1392 (hydrostatic, isladvec = 0) */
+static void advection(orc_t* o) {
+  start_advect(o);
+  hadvuv(o);
+  vadvuv(o);
+  hadv_scalar(o, o->xt, o->tdyn, 1);      /* hadvt */
+  vadv3d_t(o);
+  hadv_scalar(o, o->xq[0], o->qdyn[0], 2); /* hadvqv */
+  vadvqv(o);                               /* all(icup /= 1) */
+  hadv_scalar(o, o->xq[1], o->qdyn[1], 0); /* hadvqx */
+  vadv4d_qc(o);
+}
+
+/* curvature, Main/mod_tendency.F90:1829-1838 */
+static void curvature(orc_t* o) {
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A2(o->coriol, j, i) * A3(o->vc, j, i, k);
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - A2(o->coriol, j, i) * A3(o->uc, j, i, k);
+      }
+}
+
+/* adiabatic, Main/mod_tendency.F90:1561-1575; cpmf Share/cpmf.inc */
+static void adiabatic(orc_t* o) {
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double rovcpm = c_rgas / (c_cpd * (d_one + 0.80 * A3(o->xq[0], j, i, k)));
+        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) +
+            (A3(o->omega, j, i, k) * rovcpm * A3(o->xtv, j, i, k)) /
+            (o->ptop * A2(o->rpsa, j, i) + o->hsigma[k]);
+      }
+}
+
+/* boundary, Main/mod_tendency.F90:1462-1471 -> nudge3d/nudge4d3d/nudgeuv */
+static void boundary(orc_t* o) {
+  int kz = o->kz;
+  double xt = o->xbctime + o->dt;
+  /* nudge3d(atm2%t, xtb, tdyn), Main/mod_bdycod.F90:4218-4406 */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A3(o->fg1, j, i, k) = (A3(o->tb0, j, i, k) + xt * A3(o->tbt, j, i, k)) - A3(o->a2t, j, i, k);
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          double xf, xg; nudge_coef(o, A2(o->ib_cr, j, i), k, &xf, &xg);
+          A3(o->tdyn, j, i, k) = relax(A3(o->tdyn, j, i, k), xf, xg, A3(o->fg1, j, i, k),
+              A3(o->fg1, j - 1, i, k), A3(o->fg1, j + 1, i, k), A3(o->fg1, j, i - 1, k), A3(o->fg1, j, i + 1, k));
+        }
+  /* nudge4d3d(atm2%qx, xqb, qxdyn, iqv), :3206-3392 */
+  const double nfac = 1.0e3, rfac = d_one / nfac;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A3(o->fg1, j, i, k) = nfac * (A3(o->qb0, j, i, k) + xt * A3(o->qbt, j, i, k)) - nfac * A3(o->a2q[0], j, i, k);
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          double xf, xg; nudge_coef(o, A2(o->ib_cr, j, i), k, &xf, &xg);
+          double f0 = A3(o->fg1, j, i, k), f1 = A3(o->fg1, j - 1, i, k), f2 = A3(o->fg1, j + 1, i, k);
+          double f3 = A3(o->fg1, j, i - 1, k), f4 = A3(o->fg1, j, i + 1, k);
+          A3(o->qdyn[0], j, i, k) = A3(o->qdyn[0], j, i, k) + rfac * (xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0));
+        }
+  /* nudgeuv(atm2%u, atm2%v, xub, xvb, udyn, vdyn), :3581-3823 (iboudy=5 uses hefc/hegc) */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1ga; i <= o->ide2ga; i++)
+      for (int j = o->jde1ga; j <= o->jde2ga; j++) {
+        A3(o->fg1, j, i, k) = ((A3(o->ub0, j, i, k) + xt * A3(o->ubt, j, i, k)) - A3(o->a2u, j, i, k));
+        A3(o->fg2, j, i, k) = ((A3(o->vb0, j, i, k) + xt * A3(o->vbt, j, i, k)) - A3(o->a2v, j, i, k));
+      }
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          if (A2(o->rg_dt, j, i) != r) continue;
+          int ib = A2(o->ib_dt, j, i);
+          double xf, xg;
+          if (o->cfg.iboudy == 1) { xf = o->fcx[ib]; xg = o->gcx[ib]; }  /* fcd==fcx when nspgd==nspgx */
+          else { xf = o->hefc[ib][k]; xg = o->hegc[ib][k]; }
+          A3(o->udyn, j, i, k) = relax(A3(o->udyn, j, i, k), xf, xg, A3(o->fg1, j, i, k),
+              A3(o->fg1, j - 1, i, k), A3(o->fg1, j + 1, i, k), A3(o->fg1, j, i - 1, k), A3(o->fg1, j, i + 1, k));
+          A3(o->vdyn, j, i, k) = relax(A3(o->vdyn, j, i, k), xf, xg, A3(o->fg2, j, i, k),
+              A3(o->fg2, j - 1, i, k), A3(o->fg2, j + 1, i, k), A3(o->fg2, j, i - 1, k), A3(o->fg2, j, i + 1, k));
+        }
+}
+
+/* diffusion, Main/mod_tendency.F90:1515-1526 -> diffu_d, diffu_x3d, diffu_x4d */
+static void diffu_x(orc_t* o, double* ften, const double* f, double fac) {
+  /* diffu_x3d / diffu_x4d3d idiffu = 1, Main/mod_diffusion.F90:673-713, 808-... */
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->icii1; i <= o->icii2; i++)
+      for (int j = o->jcii1; j <= o->jcii2; j++)
+        A3(ften, j, i, k) = A3(ften, j, i, k) - fac * A3(o->xkc, j, i, k) *
+            (z4_c1 * (A3(f, j + 2, i, k) + A3(f, j - 2, i, k) + A3(f, j, i + 2, k) + A3(f, j, i - 2, k)) +
+             z4_c2 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
+             z4_c3 * A3(f, j, i, k));
+#define LAP2(J, I) \
+  A3(ften, J, I, k) = A3(ften, J, I, k) + fac * A3(o->xkc, J, I, k) * \
+      (z4_c1 * (A3(f, (J) + 1, I, k) + A3(f, (J) - 1, I, k) + A3(f, J, (I) + 1, k) + A3(f, J, (I) - 1, k)) + \
+       z4_c2 * A3(f, J, I, k))
+  if (o->bl) for (int k = 1; k <= o->kz; k++) for (int i = o->ici1; i <= o->ici2; i++) LAP2(o->jci1, i);
+  if (o->br) for (int k = 1; k <= o->kz; k++) for (int i = o->ici1; i <= o->ici2; i++) LAP2(o->jci2, i);
+  if (o->bb) for (int k = 1; k <= o->kz; k++) for (int j = o->jci1; j <= o->jci2; j++) LAP2(j, o->ici1);
+  if (o->bt) for (int k = 1; k <= o->kz; k++) for (int j = o->jci1; j <= o->jci2; j++) LAP2(j, o->ici2);
+#undef LAP2
+}
+
+static void diffu_d(orc_t* o) {                                    /* :281-385 */
+  const double* m = o->msfd;
+#define UM(a, J, I) (A3(a, J, I, k) / A2(m, J, I))
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->idii1; i <= o->idii2; i++)
+      for (int j = o->jdii1; j <= o->jdii2; j++) {
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) - A3(o->xkd, j, i, k) *
+            (z4_c1 * (UM(o->ubd, j + 2, i) + UM(o->ubd, j - 2, i) + UM(o->ubd, j, i + 2) + UM(o->ubd, j, i - 2)) +
+             z4_c2 * (UM(o->ubd, j + 1, i) + UM(o->ubd, j - 1, i) + UM(o->ubd, j, i + 1) + UM(o->ubd, j, i - 1)) +
+             z4_c3 * (UM(o->ubd, j, i)));
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - A3(o->xkd, j, i, k) *
+            (z4_c1 * (UM(o->vbd, j + 2, i) + UM(o->vbd, j - 2, i) + UM(o->vbd, j, i + 2) + UM(o->vbd, j, i - 2)) +
+             z4_c2 * (UM(o->vbd, j + 1, i) + UM(o->vbd, j - 1, i) + UM(o->vbd, j, i + 1) + UM(o->vbd, j, i - 1)) +
+             z4_c3 * (UM(o->vbd, j, i)));
+      }
+#define LAPD(J, I) do { \
+  A3(o->udyn, J, I, k) = A3(o->udyn, J, I, k) + A3(o->xkd, J, I, k) * \
+      (z4_c1 * (UM(o->ubd, (J) + 1, I) + UM(o->ubd, (J) - 1, I) + UM(o->ubd, J, (I) + 1) + UM(o->ubd, J, (I) - 1)) + \
+       z4_c2 * (UM(o->ubd, J, I))); \
+  A3(o->vdyn, J, I, k) = A3(o->vdyn, J, I, k) + A3(o->xkd, J, I, k) * \
+      (z4_c1 * (UM(o->vbd, (J) + 1, I) + UM(o->vbd, (J) - 1, I) + UM(o->vbd, J, (I) + 1) + UM(o->vbd, J, (I) - 1)) + \
+       z4_c2 * (UM(o->vbd, J, I))); } while (0)
+  if (o->bl) for (int k = 1; k <= o->kz; k++) for (int i = o->idi1; i <= o->idi2; i++) LAPD(o->jdi1, i);
+  if (o->br) for (int k = 1; k <= o->kz; k++) for (int i = o->idi1; i <= o->idi2; i++) LAPD(o->jdi2, i);
+  if (o->bb) for (int k = 1; k <= o->kz; k++) for (int j = o->jdi1; j <= o->jdi2; j++) LAPD(j, o->idi1);
+  if (o->bt) for (int k = 1; k <= o->kz; k++) for (int j = o->jdi1; j <= o->jdi2; j++) LAPD(j, o->idi2);
+#undef LAPD
+#undef UM
+}
+
+/* pressure_gradient_force, Main/mod_tendency.F90:1965-2115 (ipgf = 0) */
+static void pressure_gradient_force(orc_t* o) {
+  int kz = o->kz;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double tva = A3(o->a1t, j, i, k) * (d_one + c_ep1 * A3(o->xq[0], j, i, k));
+        double tvb = A3(o->a2t, j, i, k) * (d_one + c_ep1 * A3(o->a2q[0], j, i, k) * A2(o->rpsb, j, i));
+        double tvc = A3(o->ct, j, i, k) * (d_one + c_ep1 * A3(o->cq[0], j, i, k) * A2(o->rpsc, j, i));
+        A3(o->td, j, i, k) = alpha_hyd * (tvc + tvb) + beta_hyd * tva;
+      }
+#define TDB(J, I) A3(o->td, J, I, k) = A3(o->a1t, J, I, k) * (d_one + c_ep1 * A3(o->xq[0], J, I, k))
+  if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) TDB(o->jce1, i);
+  if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) TDB(o->jce2, i);
+  if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TDB(j, o->ice1);
+  if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TDB(j, o->ice2);
+#undef TDB
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double rtbar = d_rfour * (A3(o->xtv, j - 1, i - 1, k) + A3(o->xtv, j - 1, i, k) +
+                                  A3(o->xtv, j, i - 1, k) + A3(o->xtv, j, i, k));
+        rtbar = c_rgas * rtbar * A2(o->psdota, j, i);
+        double hs = o->hsigma[k], pt = o->ptop;
+        double den = o->dx * A2(o->msfd, j, i);
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) - rtbar *
+            (log(d_half * (A2(o->psa, j, i) + A2(o->psa, j, i - 1)) * hs + pt) -
+             log(d_half * (A2(o->psa, j - 1, i) + A2(o->psa, j - 1, i - 1)) * hs + pt)) / den;
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - rtbar *
+            (log(d_half * (A2(o->psa, j, i) + A2(o->psa, j - 1, i)) * hs + pt) -
+             log(d_half * (A2(o->psa, j - 1, i - 1) + A2(o->psa, j, i - 1)) * hs + pt)) / den;
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->tvfac, j, i, k) = d_one / (d_one + A3(o->xq[1], j, i, k) / (d_one + A3(o->xq[0], j, i, k)));
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) {
+      double rp = A2(o->rpsa, j, i);
+      double tv = A3(o->td, j, i, kz) * rp * A3(o->tvfac, j, i, kz);
+      A3(o->phi, j, i, kz) = A2(o->ht, j, i) - c_rgas * tv *
+          log((o->hsigma[kz] + o->ptop * rp) / (d_one + o->ptop * rp));
+    }
+  for (int k = 1; k <= kz - 1; k++) {
+    int lev = kz - k;
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double rp = A2(o->rpsa, j, i);
+        double tvavg = ((A3(o->td, j, i, lev) * o->dsigma[lev] + A3(o->td, j, i, lev + 1) * o->dsigma[lev + 1]) /
+                        (A2(o->psa, j, i) * (o->dsigma[lev] + o->dsigma[lev + 1]))) * A3(o->tvfac, j, i, lev);
+        A3(o->phi, j, i, lev) = A3(o->phi, j, i, lev + 1) - c_rgas * tvavg *
+            log((o->hsigma[lev] + o->ptop * rp) / (o->hsigma[lev + 1] + o->ptop * rp));
+      }
+  }
+  xch(o, o->phi, kz, 1, 1);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double den = o->dx2 * A2(o->msfd, j, i);
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) - A2(o->psdota, j, i) *
+            (A3(o->phi, j, i, k) + A3(o->phi, j, i - 1, k) - A3(o->phi, j - 1, i, k) - A3(o->phi, j - 1, i - 1, k)) / den;
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - A2(o->psdota, j, i) *
+            (A3(o->phi, j, i, k) + A3(o->phi, j - 1, i, k) - A3(o->phi, j, i - 1, k) - A3(o->phi, j - 1, i - 1, k)) / den;
+      }
+}
+
+/* spstep, Main/mod_split.F90:463-669 */
+static void sp_gradient_divergence(orc_t* o, int ns, int nsrc) {
+  double rdx2 = d_one / o->dx2;
+  for (int i = o->ide1; i <= o->ide2; i++)
+    for (int j = o->jde1; j <= o->jde2; j++) A2(o->xdelh, j, i) = DELH(j, i, ns, nsrc);
+  xch(o, o->xdelh, 1, 1, 1);
+  double *w1 = o->work, *w2 = o->work + o->plane, *w3 = o->work + 2 * o->plane;
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++) {
+      double fac = o->dx2 * A2(o->msfx, j, i);
+      A2(w1, j, i) = (A2(o->xdelh, j, i) + A2(o->xdelh, j, i - 1) - A2(o->xdelh, j - 1, i) - A2(o->xdelh, j - 1, i - 1)) / fac;
+      A2(w2, j, i) = (A2(o->xdelh, j, i) + A2(o->xdelh, j - 1, i) - A2(o->xdelh, j, i - 1) - A2(o->xdelh, j - 1, i - 1)) / fac;
+    }
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++) A2(w1, j, i) = A2(w1, j, i) * A2(o->psdota, j, i);
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++) A2(w2, j, i) = A2(w2, j, i) * A2(o->psdota, j, i);
+  for (int i = o->idi1; i <= o->idi2; i++)
+    for (int j = o->jdi1; j <= o->jdi2; j++) {
+      A2(o->uu, j, i) = A2(w1, j, i) * A2(o->msfd, j, i);
+      A2(o->vv, j, i) = A2(w2, j, i) * A2(o->msfd, j, i);
+    }
+  xch(o, o->uu, 1, 1, 2); xch(o, o->vv, 1, 1, 2);
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++)
+      A2(w3, j, i) = rdx2 * A2(o->map, j, i) *
+          (-A2(o->uu, j, i + 1) + A2(o->uu, j + 1, i + 1) - A2(o->uu, j, i) + A2(o->uu, j + 1, i) +
+           A2(o->vv, j, i + 1) + A2(o->vv, j + 1, i + 1) - A2(o->vv, j, i) - A2(o->vv, j + 1, i));
+}
+
+static void spstep(orc_t* o) {
+  const rcmdyn_config* c = &o->cfg;
+  double* w3 = o->work + 2 * o->plane;
+  memset(o->ddsum, 0, sizeof(double) * o->plane * o->nsplit);
+  memset(o->dhsum, 0, sizeof(double) * o->plane * o->nsplit);
+  for (int ns = 1; ns <= o->nsplit; ns++) {
+    double* dd = o->ddsum + (size_t)(ns - 1) * o->plane;
+    double* dh = o->dhsum + (size_t)(ns - 1) * o->plane;
+    int n0 = 1, n1 = 2, n2 = n0;
+    double aam = c->aam[ns - 1], dtau = c->dtau[ns - 1], hbar = c->hbar[ns - 1];
+    int m2 = (int)aam * 2;
+    double dtau2 = dtau * d_two;
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) { A2(dd, j, i) = DELD(j, i, ns, n0); A2(dh, j, i) = DELH(j, i, ns, n0); }
+    sp_gradient_divergence(o, ns, n0);
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        DELD(j, i, ns, n1) = DELD(j, i, ns, n0) - dtau * A2(w3, j, i) + DELD(j, i, ns, 3) / (double)m2;
+        DELH(j, i, ns, n1) = DELH(j, i, ns, n0) - dtau * hbar * DELD(j, i, ns, n0) / A2(o->psa, j, i) +
+                             DELH(j, i, ns, 3) / (double)m2;
+      }
+    double fac = (aam - d_one) / aam;
+    if (o->bl) for (int i = o->ici1; i <= o->ici2; i++) DELH(o->jce1, i, ns, n1) = DELH(o->jce1, i, ns, n0) * fac;
+    if (o->br) for (int i = o->ici1; i <= o->ici2; i++) DELH(o->jce2, i, ns, n1) = DELH(o->jce2, i, ns, n0) * fac;
+    if (o->bb) for (int j = o->jce1; j <= o->jce2; j++) DELH(j, o->ice1, ns, n1) = DELH(j, o->ice1, ns, n0) * fac;
+    if (o->bt) for (int j = o->jce1; j <= o->jce2; j++) DELH(j, o->ice2, ns, n1) = DELH(j, o->ice2, ns, n0) * fac;
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A2(dd, j, i) = A2(dd, j, i) + DELD(j, i, ns, n1);
+        A2(dh, j, i) = A2(dh, j, i) + DELH(j, i, ns, n1);
+      }
+    for (int n = 2; n <= m2; n++) {
+      sp_gradient_divergence(o, ns, n1);
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          DELD(j, i, ns, n2) = DELD(j, i, ns, n0) - dtau2 * A2(w3, j, i) + DELD(j, i, ns, 3) / aam;
+          DELH(j, i, ns, n2) = DELH(j, i, ns, n0) - dtau2 * hbar * DELD(j, i, ns, n1) / A2(o->psa, j, i) +
+                               DELH(j, i, ns, 3) / aam;
+        }
+      if (o->bl) for (int i = o->ici1; i <= o->ici2; i++)
+        DELH(o->jce1, i, ns, n2) = d_two * DELH(o->jce1, i, ns, n1) - DELH(o->jce1, i, ns, n0);
+      if (o->br) for (int i = o->ici1; i <= o->ici2; i++)
+        DELH(o->jce2, i, ns, n2) = d_two * DELH(o->jce2, i, ns, n1) - DELH(o->jce2, i, ns, n0);
+      if (o->bb) for (int j = o->jce1; j <= o->jce2; j++)
+        DELH(j, o->ice1, ns, n2) = d_two * DELH(j, o->ice1, ns, n1) - DELH(j, o->ice1, ns, n0);
+      if (o->bt) for (int j = o->jce1; j <= o->jce2; j++)
+        DELH(j, o->ice2, ns, n2) = d_two * DELH(j, o->ice2, ns, n1) - DELH(j, o->ice2, ns, n0);
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) {
+          A2(dd, j, i) = A2(dd, j, i) + DELD(j, i, ns, n2);
+          A2(dh, j, i) = A2(dh, j, i) + DELH(j, i, ns, n2);
+        }
+      n0 = n1; n1 = n2; n2 = n0;
+    }
+  }
+}
+
+/* divergence projection used three times in splitf, Main/mod_split.F90:286-294 */
+static void project_div(orc_t* o, const double* u, const double* v, int slot) {
+  int kz = o->kz;
+  double rdx2 = d_one / o->dx2;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->uuu, j, i, k) = A3(u, j, i, k) * A2(o->msfd, j, i);
+        A3(o->vvv, j, i, k) = A3(v, j, i, k) * A2(o->msfd, j, i);
+      }
+  xch(o, o->uuu, kz, 1, 2); xch(o, o->vvv, kz, 1, 2);
+  for (int l = 1; l <= o->nsplit; l++) {
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) DELD(j, i, l, slot) = d_zero;
+    for (int k = 1; k <= kz; k++) {
+      double zr = o->cfg.zmatxr[l - 1][k - 1];
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++)
+          DELD(j, i, l, slot) = DELD(j, i, l, slot) + zr * rdx2 * A2(o->map, j, i) *
+              (-A3(o->uuu, j, i + 1, k) + A3(o->uuu, j + 1, i + 1, k) - A3(o->uuu, j, i, k) + A3(o->uuu, j + 1, i, k) +
+               A3(o->vvv, j, i + 1, k) + A3(o->vvv, j + 1, i + 1, k) - A3(o->vvv, j, i, k) - A3(o->vvv, j + 1, i, k));
+    }
+  }
+}
+
+static void project_geo(orc_t* o, const double* ps, const double* t, int slot) {
+  int kz = o->kz;
+  for (int l = 1; l <= o->nsplit; l++) {
+    double pdl = o->pdlog[l - 1][kz + 1], e1 = o->eps1[l - 1][kz + 1];
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double eps = e1 * (A2(ps, j, i) - o->cfg.pd);
+        DELH(j, i, l, slot) = pdl + eps;
+      }
+    for (int k = 1; k <= kz; k++) {
+      double pdk = o->pdlog[l - 1][k], ek = o->eps1[l - 1][k], ta = o->cfg.tau[l - 1][k - 1];
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) {
+          double eps = ek * (A2(ps, j, i) - o->cfg.pd);
+          DELH(j, i, l, slot) = DELH(j, i, l, slot) + pdk + ta * A3(t, j, i, k) / A2(ps, j, i) + eps;
+        }
+    }
+  }
+}
+
+/* splitf, Main/mod_split.F90:243-461 */
+static void splitf(orc_t* o) {
+  int kz = o->kz, nsp = o->nsplit;
+  memset(o->deld, 0, sizeof(double) * o->plane * 3 * nsp);
+  memset(o->delh, 0, sizeof(double) * o->plane * 3 * nsp);
+  xch(o, o->psa, 1, 1, 0);
+  psc2psd(o, o->psa, o->psdota);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        DELD(j, i, n, 1) = A3(o->dstor, j, i, n);
+        DELH(j, i, n, 1) = A3(o->hstor, j, i, n);
+      }
+  project_div(o, o->a1u, o->a1v, 3);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) DELD(j, i, n, 3) = DELD(j, i, n, 3) - DELD(j, i, n, 1);
+  project_div(o, o->a2u, o->a2v, 2);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) DELD(j, i, n, 1) = DELD(j, i, n, 1) - DELD(j, i, n, 2);
+  project_geo(o, o->psa, o->a1t, 3);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) DELH(j, i, n, 3) = DELH(j, i, n, 3) - DELH(j, i, n, 1);
+  project_geo(o, o->psb, o->a2t, 2);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) DELH(j, i, n, 1) = DELH(j, i, n, 1) - DELH(j, i, n, 2);
+  for (int n = 1; n <= nsp; n++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->dstor, j, i, n) = DELD(j, i, n, 2);
+        A3(o->hstor, j, i, n) = DELH(j, i, n, 2);
+      }
+  spstep(o);
+  double gnu1 = o->cfg.gnu1;
+  for (int l = 1; l <= nsp; l++) {
+    double an = o->cfg.an[l - 1], gnuan = gnu1 * an;
+    double* dd = o->ddsum + (size_t)(l - 1) * o->plane;
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A2(o->psa, j, i) = A2(o->psa, j, i) - an * A2(dd, j, i);
+        A2(o->psb, j, i) = A2(o->psb, j, i) - gnuan * A2(dd, j, i);
+      }
+  }
+  for (int l = 1; l <= nsp; l++) {
+    double* dd = o->ddsum + (size_t)(l - 1) * o->plane;
+    for (int k = 1; k <= kz; k++) {
+      double am = o->cfg.am[l - 1][k - 1], gnuam = gnu1 * am;
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          A3(o->a1t, j, i, k) = A3(o->a1t, j, i, k) + am * A2(dd, j, i);
+          A3(o->a2t, j, i, k) = A3(o->a2t, j, i, k) + gnuam * A2(dd, j, i);
+        }
+    }
+  }
+  xch(o, o->dhsum, nsp, 1, 1);
+  for (int l = 1; l <= nsp; l++) {
+    double* dh = o->dhsum + (size_t)(l - 1) * o->plane;
+    for (int k = 1; k <= kz; k++) {
+      double zm = o->cfg.zmatx[l - 1][k - 1], gnuzm = gnu1 * zm;
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          double fac = A2(o->psdota, j, i) / (o->dx2 * A2(o->msfd, j, i));
+          double x = fac * (A2(dh, j, i) + A2(dh, j, i - 1) - A2(dh, j - 1, i) - A2(dh, j - 1, i - 1));
+          double y = fac * (A2(dh, j, i) - A2(dh, j, i - 1) + A2(dh, j - 1, i) - A2(dh, j - 1, i - 1));
+          A3(o->a1u, j, i, k) = A3(o->a1u, j, i, k) - zm * x;
+          A3(o->a1v, j, i, k) = A3(o->a1v, j, i, k) - zm * y;
+          A3(o->a2u, j, i, k) = A3(o->a2u, j, i, k) - gnuzm * x;
+          A3(o->a2v, j, i, k) = A3(o->a2v, j, i, k) - gnuzm * y;
+        }
+    }
+  }
+}
+
+/* tend, Main/mod_tendency.F90:212-726 (hydrostatic, physics stubbed) */
+int orc_tend(orc_t* o) {
+  int kz = o->kz;
+  size_t n3 = o->plane * (size_t)kz;
+  surface_pressures(o);
+  decouple(o);
+  compute_omega(o);
+  mkslice(o);
+  new_pressure(o);
+  calc_coeff(o);
+  /* init_tendencies, :1227-1268 (total/dynamic/physic components all zero) */
+  memset(o->tten, 0, n3 * 8); memset(o->tdyn, 0, n3 * 8);
+  memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
+  memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
+  for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
+  advection(o);
+  curvature(o);
+  adiabatic(o);
+  boundary(o);
+  /* physical_parametrizations: stubbed -> tphy = qxphy = uphy = vphy = 0 */
+  diffu_d(o);
+  diffu_x(o, o->tdyn, o->tb3d, d_one);
+  diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
+  diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
+  /* sums, :285-294 and :332-349 (tphy = qxphy = 0) */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + 0.0;
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + 0.0;
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + 0.0;
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + 0.0;
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
+      }
+  /* forecast t, qx, :368-393 */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->ct, j, i, k) = A3(o->a2t, j, i, k) + o->dt * A3(o->tten, j, i, k);
+  for (int n = 0; n < 2; n++) {
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(o->cq[n], j, i, k) = A3(o->a2q[n], j, i, k);
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->cq[n], j, i, k) = A3(o->cq[n], j, i, k) + o->dt * A3(o->qten[n], j, i, k);
+  }
+  xch(o, o->cq[0], kz, 1, 0); xch(o, o->cq[1], kz, 1, 0);
+  for (int n = 0; n < 2; n++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          if (A3(o->cq[n], j, i, k) < d_zero) {
+            double s = 0.0;
+            for (int ii = i - 1; ii <= i + 1; ii++)
+              for (int jj = j - 1; jj <= j + 1; jj++) s = s + fabs(A3(o->cq[n], jj, ii, k));
+            A3(o->cq[n], j, i, k) = 0.01 * s / 9.0;
+          }
+  pressure_gradient_force(o);
+  for (int k = 1; k <= kz; k++)                                     /* :404-411 */
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + 0.0;
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + 0.0;
+      }
+  /* time filters, :419-427, Main/mod_timefilter.F90 */
+  double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;
+  for (int i = o->ici1; i <= o->ici2; i++)                          /* filter_ra_2d */
+    for (int j = o->jci1; j <= o->jci2; j++) {
+      double d = g1 * (A2(o->psc, j, i) + A2(o->psb, j, i) - d_two * A2(o->psa, j, i));
+      A2(o->psb, j, i) = A2(o->psa, j, i) + d;
+      A2(o->psa, j, i) = A2(o->psc, j, i);
+    }
+  for (int k = 1; k <= kz; k++)                                     /* filter_ra_3d */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g1 * (A3(o->ct, j, i, k) + A3(o->a2t, j, i, k) - d_two * A3(o->a1t, j, i, k));
+        A3(o->a2t, j, i, k) = A3(o->a1t, j, i, k) + d;
+        A3(o->a1t, j, i, k) = A3(o->ct, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)                                     /* filter_raw_qv */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g1 * (A3(o->cq[0], j, i, k) + A3(o->a2q[0], j, i, k) - d_two * A3(o->a1q[0], j, i, k));
+        A3(o->a2q[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) + beta * d, MINQQ * A2(o->psa, j, i));
+        A3(o->a1q[0], j, i, k) = dmax(A3(o->cq[0], j, i, k) + (beta - d_one) * d, MINQQ * A2(o->psb, j, i));
+      }
+  for (int k = 1; k <= kz; k++)                                     /* filter_raw_4d */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g2 * (A3(o->cq[1], j, i, k) + A3(o->a2q[1], j, i, k) - d_two * A3(o->a1q[1], j, i, k));
+        A3(o->a2q[1], j, i, k) = A3(o->a1q[1], j, i, k) + beta * d;
+        A3(o->a1q[1], j, i, k) = A3(o->cq[1], j, i, k) + (beta - d_one) * d;
+        if (A3(o->a2q[1], j, i, k) < d_zero) A3(o->a2q[1], j, i, k) = d_zero;
+        if (A3(o->a1q[1], j, i, k) < d_zero) A3(o->a1q[1], j, i, k) = d_zero;
+      }
+  for (int k = 1; k <= kz; k++)                                     /* :433-440 */
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->cu, j, i, k) = A3(o->a2u, j, i, k) + o->dt * A3(o->uten, j, i, k);
+        A3(o->cv, j, i, k) = A3(o->a2v, j, i, k) + o->dt * A3(o->vten, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)                                     /* filter_ra_uv */
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double d = g1 * (A3(o->cu, j, i, k) + A3(o->a2u, j, i, k) - d_two * A3(o->a1u, j, i, k));
+        A3(o->a2u, j, i, k) = A3(o->a1u, j, i, k) + d;
+        A3(o->a1u, j, i, k) = A3(o->cu, j, i, k);
+        d = g1 * (A3(o->cv, j, i, k) + A3(o->a2v, j, i, k) - d_two * A3(o->a1v, j, i, k));
+        A3(o->a2v, j, i, k) = A3(o->a1v, j, i, k) + d;
+        A3(o->a1v, j, i, k) = A3(o->cv, j, i, k);
+      }
+  splitf(o);
+  /* rcmtimer%advance and dt switch, :608-616 */
+  o->lcount += 1;
+  if (o->lcount == 2) o->dt = d_two * o->dtsec;
+  /* NaN / CFL check, :624-703 */
+  if (isnan(o->ptntot)) return 1;
+  return 0;
+}
+
+/* bdyuv, Main/mod_bdycod.F90:896-1094 (time-dependent branch) */
+static void bdyuv(orc_t* o, double xt) {
+  int kz = o->kz;
+  if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+    SI(o->wui, i, k) = A3(o->a1u, o->jdi1, i, k); SI(o->wvi, i, k) = A3(o->a1v, o->jdi1, i, k); }
+  if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+    SI(o->eui, i, k) = A3(o->a1u, o->jdi2, i, k); SI(o->evi, i, k) = A3(o->a1v, o->jdi2, i, k); }
+  if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jdi1; j <= o->jdi2; j++) {
+    SJ(o->sui, j, k) = A3(o->a1u, j, o->idi1, k); SJ(o->svi, j, k) = A3(o->a1v, j, o->idi1, k); }
+  if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jdi1; j <= o->jdi2; j++) {
+    SJ(o->nui, j, k) = A3(o->a1u, j, o->idi2, k); SJ(o->nvi, j, k) = A3(o->a1v, j, o->idi2, k); }
+  if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+    SI(o->wue, i, k) = (A3(o->ub0, o->jde1, i, k) + xt * A3(o->ubt, o->jde1, i, k));
+    SI(o->wve, i, k) = (A3(o->vb0, o->jde1, i, k) + xt * A3(o->vbt, o->jde1, i, k)); }
+  if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+    SI(o->eue, i, k) = (A3(o->ub0, o->jde2, i, k) + xt * A3(o->ubt, o->jde2, i, k));
+    SI(o->eve, i, k) = (A3(o->vb0, o->jde2, i, k) + xt * A3(o->vbt, o->jde2, i, k)); }
+  if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
+    SJ(o->sue, j, k) = (A3(o->ub0, j, o->ide1, k) + xt * A3(o->ubt, j, o->ide1, k));
+    SJ(o->sve, j, k) = (A3(o->vb0, j, o->ide1, k) + xt * A3(o->vbt, j, o->ide1, k)); }
+  if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
+    SJ(o->nue, j, k) = (A3(o->ub0, j, o->ide2, k) + xt * A3(o->ubt, j, o->ide2, k));
+    SJ(o->nve, j, k) = (A3(o->vb0, j, o->ide2, k) + xt * A3(o->vbt, j, o->ide2, k)); }
+  if (o->bt && o->bl) for (int k = 1; k <= kz; k++) {
+    SI(o->wui, o->ide2, k) = SJ(o->nue, o->jdi1, k); SI(o->wvi, o->ide2, k) = SJ(o->nve, o->jdi1, k);
+    SJ(o->nui, o->jde1, k) = SI(o->wue, o->idi2, k); SJ(o->nvi, o->jde1, k) = SI(o->wve, o->idi2, k); }
+  if (o->bb && o->bl) for (int k = 1; k <= kz; k++) {
+    SI(o->wui, o->ide1, k) = SJ(o->sue, o->jdi1, k); SI(o->wvi, o->ide1, k) = SJ(o->sve, o->jdi1, k);
+    SJ(o->sui, o->jde1, k) = SI(o->wue, o->idi1, k); SJ(o->svi, o->jde1, k) = SI(o->wve, o->idi1, k); }
+  if (o->bt && o->br) for (int k = 1; k <= kz; k++) {
+    SI(o->eui, o->ide2, k) = SJ(o->nue, o->jdi2, k); SI(o->evi, o->ide2, k) = SJ(o->nve, o->jdi2, k);
+    SJ(o->nui, o->jde2, k) = SI(o->eue, o->idi2, k); SJ(o->nvi, o->jde2, k) = SI(o->eve, o->idi2, k); }
+  if (o->bb && o->br) for (int k = 1; k <= kz; k++) {
+    SI(o->eui, o->ide1, k) = SJ(o->sue, o->jdi2, k); SI(o->evi, o->ide1, k) = SJ(o->sve, o->jdi2, k);
+    SJ(o->sui, o->jde2, k) = SI(o->eue, o->idi1, k); SJ(o->svi, o->jde2, k) = SI(o->eve, o->idi1, k); }
+  if (o->bt) { xchb(o, o->nue, 0); xchb(o, o->nui, 0); xchb(o, o->nve, 0); xchb(o, o->nvi, 0); }
+  if (o->bb) { xchb(o, o->sue, 0); xchb(o, o->sui, 0); xchb(o, o->sve, 0); xchb(o, o->svi, 0); }
+  if (o->bl) { xchb(o, o->wue, 1); xchb(o, o->wui, 1); xchb(o, o->wve, 1); xchb(o, o->wvi, 1); }
+  if (o->br) { xchb(o, o->eue, 1); xchb(o, o->eui, 1); xchb(o, o->eve, 1); xchb(o, o->evi, 1); }
+}
+
+/* bdyval, Main/mod_bdycod.F90:1109-2571 (idynamic = 1, iboudy /= 0, bdyflow) */
+void orc_bdyval(orc_t* o) {
+  int kz = o->kz;
+  double xt = o->xbctime + o->dt;
+  if (o->lcount > 0) {                                              /* :1126-1310 */
+    if (o->bl) {
+      for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->a2u, o->jde1, i, k) = A3(o->a1u, o->jde1, i, k); A3(o->a2v, o->jde1, i, k) = A3(o->a1v, o->jde1, i, k); }
+      for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce1, i, k) = A3(o->a1t, o->jce1, i, k);
+      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
+        A3(o->a2q[n], o->jce1, i, k) = A3(o->a1q[n], o->jce1, i, k);
+      for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce1, i) = A2(o->psa, o->jce1, i);
+    }
+    if (o->br) {
+      for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->a2u, o->jde2, i, k) = A3(o->a1u, o->jde2, i, k); A3(o->a2v, o->jde2, i, k) = A3(o->a1v, o->jde2, i, k); }
+      for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce2, i, k) = A3(o->a1t, o->jce2, i, k);
+      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
+        A3(o->a2q[n], o->jce2, i, k) = A3(o->a1q[n], o->jce2, i, k);
+      for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce2, i) = A2(o->psa, o->jce2, i);
+    }
+    if (o->bb) {
+      for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->a2u, j, o->ide1, k) = A3(o->a1u, j, o->ide1, k); A3(o->a2v, j, o->ide1, k) = A3(o->a1v, j, o->ide1, k); }
+      for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice1, k) = A3(o->a1t, j, o->ice1, k);
+      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->a2q[n], j, o->ice1, k) = A3(o->a1q[n], j, o->ice1, k);
+      for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice1) = A2(o->psa, j, o->ice1);
+    }
+    if (o->bt) {
+      for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->a2u, j, o->ide2, k) = A3(o->a1u, j, o->ide2, k); A3(o->a2v, j, o->ide2, k) = A3(o->a1v, j, o->ide2, k); }
+      for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice2, k) = A3(o->a1t, j, o->ice2, k);
+      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->a2q[n], j, o->ice2, k) = A3(o->a1q[n], j, o->ice2, k);
+      for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice2) = A2(o->psa, j, o->ice2);
+    }
+  }
+  /* p* and p*u, p*v boundary values, :1430-1526 */
+  if (o->bl) for (int i = o->ici1; i <= o->ici2; i++) A2(o->psa, o->jce1, i) = A2(o->pb0, o->jce1, i) + xt * A2(o->pbt, o->jce1, i);
+  if (o->br) for (int i = o->ici1; i <= o->ici2; i++) A2(o->psa, o->jce2, i) = A2(o->pb0, o->jce2, i) + xt * A2(o->pbt, o->jce2, i);
+  if (o->bb) for (int j = o->jce1; j <= o->jce2; j++) A2(o->psa, j, o->ice1) = A2(o->pb0, j, o->ice1) + xt * A2(o->pbt, j, o->ice1);
+  if (o->bt) for (int j = o->jce1; j <= o->jce2; j++) A2(o->psa, j, o->ice2) = A2(o->pb0, j, o->ice2) + xt * A2(o->pbt, j, o->ice2);
+#define UVB(J, I) do { \
+  A3(o->a1u, J, I, k) = A3(o->ub0, J, I, k) + xt * A3(o->ubt, J, I, k); \
+  A3(o->a1v, J, I, k) = A3(o->vb0, J, I, k) + xt * A3(o->vbt, J, I, k); } while (0)
+  if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) UVB(o->jde1, i);
+  if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) UVB(o->jde2, i);
+  if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) UVB(j, o->ide1);
+  if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) UVB(j, o->ide2);
+#undef UVB
+  bdyuv(o, xt);
+  /* p*t and p*qv boundary values, :1700-1805 */
+#define TQB(J, I) do { \
+  A3(o->a1t, J, I, k) = A3(o->tb0, J, I, k) + xt * A3(o->tbt, J, I, k); \
+  A3(o->a1q[0], J, I, k) = A3(o->qb0, J, I, k) + xt * A3(o->qbt, J, I, k); } while (0)
+  if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) TQB(o->jce1, i);
+  if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) TQB(o->jce2, i);
+  if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice1);
+  if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice2);
+#undef TQB
+  /* qc inflow/outflow (not present_qc, bdyflow), :2153-2220 */
+  if (!o->cfg.present_qc) {
+    double* q = o->a1q[1];
+    if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->ice1; i <= o->ice2; i++) {
+      double qxint = A3(q, o->jci1, i, k) / A2(o->psa, o->jci1, i);
+      double w = SI(o->wue, i, k) + SI(o->wue, i + 1, k) + SI(o->wui, i, k) + SI(o->wui, i + 1, k);
+      A3(q, o->jce1, i, k) = (w > d_zero) ? d_zero : qxint * A2(o->psa, o->jce1, i); }
+    if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->ice1; i <= o->ice2; i++) {
+      double qxint = A3(q, o->jci2, i, k) / A2(o->psa, o->jci2, i);
+      double w = SI(o->eue, i, k) + SI(o->eue, i + 1, k) + SI(o->eui, i, k) + SI(o->eui, i + 1, k);
+      A3(q, o->jce2, i, k) = (w < d_zero) ? d_zero : qxint * A2(o->psa, o->jce2, i); }
+    if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jci1; j <= o->jci2; j++) {
+      double qxint = A3(q, j, o->ici1, k) / A2(o->psa, j, o->ici1);
+      double w = SJ(o->sve, j, k) + SJ(o->sve, j + 1, k) + SJ(o->svi, j, k) + SJ(o->svi, j + 1, k);
+      A3(q, j, o->ice1, k) = (w > d_zero) ? d_zero : qxint * A2(o->psa, j, o->ice1); }
+    if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jci1; j <= o->jci2; j++) {
+      double qxint = A3(q, j, o->ici2, k) / A2(o->psa, j, o->ici2);
+      double w = SJ(o->nve, j, k) + SJ(o->nve, j + 1, k) + SJ(o->nvi, j, k) + SJ(o->nvi, j + 1, k);
+      A3(q, j, o->ice2, k) = (w < d_zero) ? d_zero : qxint * A2(o->psa, j, o->ice2); }
+  }
+  o->xbctime = o->xbctime + o->dtsec;                               /* :2566 */
+}
+
+int orc_step(orc_t* o, int nsteps) {
+  for (int s = 0; s < nsteps; s++) {
+    if (orc_tend(o)) return 1;
+    orc_bdyval(o);
+  }
+  return 0;
+}

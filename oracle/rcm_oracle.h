@@ -1,0 +1,59 @@
+/*
+ * rcm_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, fp64, no FMA contraction) of the RegCM 4.7 hydrostatic
+ * dynamical-core step `tend` + `bdyval` (Main/mod_tendency.F90:212-2121,
+ * Main/mod_bdycod.F90:896-2571 and the modules they call).  It is the checker the parity
+ * tests compare the HIP engine against, and the `cpu_baseline` leg of bench.py.  Nothing
+ * in the product path (regcm_amd/, include/) may link or call it.
+ *
+ * Parity status: "parity unpinned" against executions of the reference -- the reference
+ * is Fortran that cannot be built in this image without stand-ins for netCDF-Fortran
+ * (Share/mod_dynparam.F90:28 `use netcdf`), and it ships no golden vectors (SURVEY.md
+ * section 4).  See DESIGN.md "Oracle".
+ *
+ * The oracle is tile-aware: it owns ONE tile of the set_nproc decomposition and calls a
+ * user-supplied exchange callback wherever the reference calls mpplib `exchange*`, so a
+ * multi-rank test can run it under torch.distributed (gloo).
+ */
+#ifndef RCM_ORACLE_H
+#define RCM_ORACLE_H
+#include "../include/rcmdyn.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc orc_t;
+
+/* sides: 0 = all 8 neighbours (exchange), 1 = left/bottom (+bottom-left corner)
+ * (exchange_lb), 2 = right/top (+top-right corner) (exchange_rt).
+ * field points at a frame array of nk levels, layout [k][i][j] over the tile frame
+ * (see orc_frame_info). */
+typedef void (*orc_exchange_fn)(void* ctx, double* field, int nk, int nex, int sides);
+/* boundary-slice exchange along the boundary (exchange_bdy_lr / _bt):
+ * along = 0: slice indexed by j (south/north slices), exchanged with left/right tiles;
+ * along = 1: slice indexed by i (west/east slices), exchanged with bottom/top tiles. */
+typedef void (*orc_exchange_bdy_fn)(void* ctx, double* slice, int nk, int along);
+
+/* config->tile_first selects the tile; tile_count must be 1. */
+orc_t* orc_create(const rcmdyn_config* cfg);
+void orc_destroy(orc_t* o);
+void orc_set_exchange(orc_t* o, orc_exchange_fn fn, orc_exchange_bdy_fn bfn, void* ctx);
+/* info[0..3] = j0, i0 (frame origin, global index), nj, ni (frame size);
+ * info[4..11] = jde1,jde2,ide1,ide2,jce1,jce2,ice1,ice2; info[12..15] = bdy flags L,R,B,T */
+void orc_frame_info(const orc_t* o, int info[16]);
+int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int i2, int k1, int k2);
+int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2);
+void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
+void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);
+int orc_tend(orc_t* o);     /* returns 1 on CFL violation (NaN ptntot) */
+void orc_bdyval(orc_t* o);
+void orc_diagnostics(const orc_t* o, double out[4]);
+/* OpenMP-free, single thread.  Runs nsteps x (tend + bdyval); returns first error. */
+int orc_step(orc_t* o, int nsteps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

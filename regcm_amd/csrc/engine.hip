@@ -1,0 +1,936 @@
+// engine.hip -- host side of the MI355X dynamical-core engine and the extern "C" ABI
+// (include/rcmdyn.h).
+//
+// One engine instance owns one or more tiles of the set_nproc decomposition
+// (Main/mpplib/mod_mppparam.F90:1053-1371) on one GPU.  A step is the reference sequence
+// tend + bdyval (Main/mod_regcm_interface.F90:189,208) issued as ~30 kernels on one HIP
+// stream; rcmdyn_step captures one step per ping-pong parity into a hipGraph and replays it.
+// Halo exchanges mirror every mpplib exchange the reference performs; tiles on the same
+// device exchange through a ghost-fill kernel, tiles on other ranks through RCCL
+// (comm.hip).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "comm.hpp"
+#include "engine.hpp"
+#include "kernels.hpp"
+
+using namespace rcm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess)                                                                \
+      throw HipError(std::string(#x) + ": " + hipGetErrorString(e_) + " @" + std::to_string(__LINE__)); \
+  } while (0)
+
+// constants, Share/mod_constants.F90 (same expressions as oracle/rcm_oracle.c)
+constexpr double EGRAV = 9.80665, BOLTZK = 1.3806504e-23, NAVGDR = 6.02214129e23;
+constexpr double AMD = 28.96454, AMW = 18.01528, VONKAR = 0.4;
+
+void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4]) {
+  int lj = tile / ci, li = tile % ci;
+  int jxp = jx / cj, iyp = iy / ci;
+  int js = lj * jxp + 1, is = li * iyp + 1;
+  if (jxp * cj < jx) {
+    int imiss = jx - jxp * cj;
+    if (lj < imiss) { js += lj; jxp += 1; } else { js += imiss; }
+  }
+  if (iyp * ci < iy) {
+    int imiss = iy - iyp * ci;
+    if (li < imiss) { is += li; iyp += 1; } else { is += imiss; }
+  }
+  int je = js + jxp - 1, ie = is + iyp - 1;
+  ext[0] = js; ext[1] = je; ext[2] = is; ext[3] = ie;
+  ext[4] = js; ext[5] = (je == jx) ? je - 1 : je;
+  ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
+  bdy[0] = (lj == 0); bdy[1] = (lj == cj - 1); bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+}
+
+Geom make_geom(int jx, int iy, int cj, int ci, int tile) {
+  int ext[8], bdy[4];
+  tile_extent(jx, iy, cj, ci, tile, ext, bdy);
+  Geom g{};
+  g.bl = bdy[0]; g.br = bdy[1]; g.bb = bdy[2]; g.bt = bdy[3];
+  g.jde1 = g.jdi1 = g.jdii1 = ext[0]; g.jde2 = g.jdi2 = g.jdii2 = ext[1];
+  g.ide1 = g.idi1 = g.idii1 = ext[2]; g.ide2 = g.idi2 = g.idii2 = ext[3];
+  if (g.bl) { g.jdi1 = g.jde1 + 1; g.jdii1 = g.jde1 + 2; }
+  if (g.br) { g.jdi2 = g.jde2 - 1; g.jdii2 = g.jde2 - 2; }
+  if (g.bb) { g.idi1 = g.ide1 + 1; g.idii1 = g.ide1 + 2; }
+  if (g.bt) { g.idi2 = g.ide2 - 1; g.idii2 = g.ide2 - 2; }
+  g.jce1 = g.jci1 = g.jcii1 = ext[4]; g.jce2 = g.jci2 = g.jcii2 = ext[5];
+  g.ice1 = g.ici1 = g.icii1 = ext[6]; g.ice2 = g.ici2 = g.icii2 = ext[7];
+  if (g.bl) { g.jci1 = g.jce1 + 1; g.jcii1 = g.jce1 + 2; }
+  if (g.br) { g.jci2 = g.jce2 - 1; g.jcii2 = g.jce2 - 2; }
+  if (g.bb) { g.ici1 = g.ice1 + 1; g.icii1 = g.ice1 + 2; }
+  if (g.bt) { g.ici2 = g.ice2 - 1; g.icii2 = g.ice2 - 2; }
+  int gl = g.bl ? 0 : 1, gr = g.br ? 0 : 1, gb = g.bb ? 0 : 1, gt = g.bt ? 0 : 1;
+  g.jde1ga = g.jde1 - gl; g.jde2ga = g.jde2 + gr; g.ide1ga = g.ide1 - gb; g.ide2ga = g.ide2 + gt;
+  g.jce1ga = g.jce1 - gl; g.jce2ga = g.jce2 + gr; g.ice1ga = g.ice1 - gb; g.ice2ga = g.ice2 + gt;
+  g.jci1ga = g.jci1 - gl; g.jci2ga = g.jci2 + gr; g.ici1ga = g.ici1 - gb; g.ici2ga = g.ici2 + gt;
+  g.jde1gb = g.jde1 - 2 * gl; g.jde2gb = g.jde2 + 2 * gr; g.ide1gb = g.ide1 - 2 * gb; g.ide2gb = g.ide2 + 2 * gt;
+  g.jce1gb = g.jce1 - 2 * gl; g.jce2gb = g.jce2 + 2 * gr; g.ice1gb = g.ice1 - 2 * gb; g.ice2gb = g.ice2 + 2 * gt;
+  g.j0 = g.jde1 - G; g.i0 = g.ide1 - G;
+  g.nj = (g.jde2 - g.jde1 + 1) + 2 * G;
+  g.ni = (g.ide2 - g.ide1 + 1) + 2 * G;
+  g.pitch = (g.nj + 15) / 16 * 16;
+  g.plane = (long)g.pitch * g.ni;
+  return g;
+}
+
+// setup_boundaries, Main/mod_atm_interface.F90:383-542 (global indices, non-band)
+void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::vector<int8_t>& rg,
+                      std::vector<int16_t>& ib) {
+  int icx = ldot ? 0 : 1, icy = ldot ? 0 : 1;
+  int igbb1 = 2, igbb2 = nsp - 1, jgbl1 = 2, jgbl2 = nsp - 1;
+  int igbt1 = iy - icy - nsp + 2, igbt2 = iy - icy - 1;
+  int jgbr1 = jx - icx - nsp + 2, jgbr2 = jx - icx - 1;
+  rg.assign(g.plane, 0);
+  ib.assign(g.plane, -1);
+  auto set = [&](int j, int i, int r, int b) { rg[g.ix(j, i)] = (int8_t)r; ib[g.ix(j, i)] = (int16_t)b; };
+  for (int i = g.ide1; i <= g.ide2; i++)
+    if (i >= igbb1 && i <= igbb2)
+      for (int j = g.jde1; j <= g.jde2; j++)
+        if (j >= jgbl1 && j <= jgbr2) {
+          if (j <= jgbl2 && i >= j) continue;
+          if (j >= jgbr1 && i >= (jgbr2 - j + 2)) continue;
+          set(j, i, 1, i - igbb1 + 2);
+        }
+  for (int i = g.ide1; i <= g.ide2; i++)
+    if (i >= igbt1 && i <= igbt2)
+      for (int j = g.jde1; j <= g.jde2; j++)
+        if (j >= jgbl1 && j <= jgbr2) {
+          if (j <= jgbl2 && (igbt2 - i + 2) >= j) continue;
+          if (j >= jgbr1 && (igbt2 - i) >= (jgbr2 - j)) continue;
+          set(j, i, 2, igbt2 - i + 2);
+        }
+  for (int i = g.ide1; i <= g.ide2; i++) {
+    if (i < igbb1 || i > igbt2) continue;
+    for (int j = g.jde1; j <= g.jde2; j++)
+      if (j >= jgbl1 && j <= jgbl2) {
+        if (i < igbb2 && j > i) continue;
+        if (i > igbt1 && j > (igbt2 - i + 2)) continue;
+        set(j, i, 3, j - jgbl1 + 2);
+      }
+  }
+  for (int i = g.ide1; i <= g.ide2; i++) {
+    if (i < igbb1 || i > igbt2) continue;
+    for (int j = g.jde1; j <= g.jde2; j++)
+      if (j >= jgbr1 && j <= jgbr2) {
+        if (i < igbb2 && (jgbr2 - j + 2) > i) continue;
+        if (i > igbt1 && (jgbr2 - j) > (igbt2 - i)) continue;
+        set(j, i, 4, jgbr2 - j + 2);
+      }
+  }
+}
+
+inline dim3 grid3(int nj, int ni, int nk) { return dim3((nj + 63) / 64, (ni + 3) / 4, nk); }
+const dim3 BLK(64, 4, 1);
+
+}  // namespace
+
+// Buffers that exchanges refer to, resolved per tile.
+enum class FK {
+  A1U, A1V, A1T, A1QV, A1QC, A2U, A2V, A2T, A2QV, A2QC, PSA, PSB, PSDOTA, PSDOTB,
+  UD, VD, QDOT, XKC, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
+  UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR
+};
+
+struct rcmdyn_engine {
+  rcmdyn_config cfg{};
+  Consts hc{};
+  Consts* dc = nullptr;
+  StepState* ds = nullptr;
+  StepState hs{};            // host mirror of the time state
+  int ntiles = 0;
+  std::vector<Geom> all;     // every tile of the decomposition
+  std::vector<Tile> tiles;   // tiles owned here
+  hipStream_t stream = nullptr;
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};
+  bool statics_dirty = true;
+  bool bdy_dirty = true;
+  bool capturing = false;
+  long slen = 0;
+  double last_ms = 0.0;
+  std::string err;
+  std::unique_ptr<Comm> comm;
+  int device = 0;
+
+  int nsplit() const { return cfg.nsplit; }
+
+  // ------------------------------------------------------------------ setup
+  void compute_constants() {
+    Consts& c = hc;
+    std::memset(&c, 0, sizeof(c));
+    c.kz = cfg.kz; c.nsplit = cfg.nsplit; c.iboudy = cfg.iboudy; c.nspgx = cfg.nspgx;
+    c.stability_enhance = cfg.stability_enhance; c.present_qc = cfg.present_qc;
+    const double rgasmol = NAVGDR * BOLTZK;
+    c.c287 = rgasmol / AMD; c.rgas = c.c287 * 1000.0; c.cpd = 3.5 * c.rgas;
+    c.ep1 = AMD / AMW - 1.0; c.regrav = 1.0 / EGRAV;
+    c.dx = cfg.ds * 1000.0; c.dx2 = 2.0 * c.dx; c.dx4 = 4.0 * c.dx; c.dx8 = 8.0 * c.dx;
+    c.dx16 = 16.0 * c.dx; c.dxsq = c.dx * c.dx; c.rdxsq = 1.0 / c.dxsq;
+    c.ptop = cfg.ptop; c.dtsec = cfg.dtsec; c.gnu1 = cfg.gnu1; c.gnu2 = cfg.gnu2;
+    c.t_extrema = cfg.t_extrema; c.q_rel_extrema = cfg.q_rel_extrema;
+    const int kz = cfg.kz;
+    for (int k = 1; k <= kz + 1; k++) c.sigma[k] = cfg.sigma[k - 1];
+    for (int k = 1; k <= kz; k++) {
+      c.hsigma[k] = (c.sigma[k + 1] + c.sigma[k]) * 0.5;
+      c.dsigma[k] = (c.sigma[k + 1] - c.sigma[k]);
+    }
+    for (int k = 2; k <= kz; k++) {                         // Main/mod_params.F90:2208-2215
+      c.twt1[k] = (c.sigma[k] - c.hsigma[k - 1]) / (c.hsigma[k] - c.hsigma[k - 1]);
+      c.twt2[k] = 1.0 - c.twt1[k];
+      c.qcon[k] = (c.sigma[k] - c.hsigma[k]) / (c.hsigma[k - 1] - c.hsigma[k]);
+    }
+    for (int k = 1; k <= kz; k++) c.xds[k] = 1.0 / c.dsigma[k];  // Main/mod_advection.F90:100
+    c.ul = cfg.uoffc * 0.5 * cfg.dtsec / c.dx;                       // :106 (init dt)
+    c.xkhmax = c.dxsq / (64.0 * cfg.dtsec);                          // Main/mod_diffusion.F90:104
+    c.dydc = cfg.adyndif * VONKAR * VONKAR * c.dx * 0.25;
+    c.xkhz = cfg.ckh * 1.5e-3 * c.dxsq / cfg.dtsec;
+    const double fnudge = (cfg.bdy_nm > 0) ? cfg.bdy_nm : 0.1 / cfg.dtsec;   // Main/mod_bdycod.F90:204-215
+    const double gnudge = (cfg.bdy_dm > 0) ? cfg.bdy_dm : 1.0 / (cfg.dtsec * 50.0);
+    for (int n = 2; n <= cfg.nspgx - 1 && n < MAXNSP; n++) {
+      double xfun = (double)(cfg.nspgx - n) / (double)(cfg.nspgx - 2);
+      c.fcx[n] = fnudge * xfun; c.gcx[n] = gnudge * xfun;
+    }
+    for (int k = 1; k <= kz; k++) {
+      double an = (c.hsigma[k] < 0.4) ? cfg.high_nudge : (c.hsigma[k] < 0.8) ? cfg.medium_nudge : cfg.low_nudge;
+      for (int n = 2; n <= cfg.nspgx - 1 && n < MAXNSP; n++) {
+        double xfun = std::exp(-((double)(n - 2) / an));
+        c.hefc[n][k] = fnudge * xfun; c.hegc[n][k] = gnudge * xfun;
+      }
+    }
+    for (int l = 0; l < cfg.nsplit; l++) {
+      for (int k = 0; k < kz; k++) {
+        c.zmatx[l][k] = cfg.zmatx[l][k]; c.zmatxr[l][k] = cfg.zmatxr[l][k];
+        c.am[l][k] = cfg.am[l][k]; c.tau[l][k] = cfg.tau[l][k];
+      }
+      c.an[l] = cfg.an[l]; c.hbar[l] = cfg.hbar[l]; c.aam[l] = cfg.aam[l]; c.dtau[l] = cfg.dtau[l];
+      for (int k = 1; k <= kz + 1; k++) {                  // Main/mod_split.F90:343-353
+        double sh = cfg.sigmah[k - 1], va = cfg.varpa1[l][k - 1];
+        c.pdlog[l][k] = va * std::log(sh * cfg.pd + cfg.ptop);
+        c.eps1[l][k] = va * sh / (sh * cfg.pd + cfg.ptop);
+      }
+    }
+    c.pd = cfg.pd;
+  }
+
+  double* dalloc(Tile& t, size_t n) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, n * sizeof(double)));
+    HIPCHK(hipMemset(p, 0, n * sizeof(double)));
+    t.allocs.push_back(p);
+    return (double*)p;
+  }
+  template <class T>
+  T* talloc(Tile& t, size_t n) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, n * sizeof(T)));
+    HIPCHK(hipMemset(p, 0, n * sizeof(T)));
+    t.allocs.push_back(p);
+    return (T*)p;
+  }
+
+  void setup_tile(Tile& t, int index) {
+    t.index = index;
+    t.lj = index / cfg.nproc_i; t.li = index % cfg.nproc_i;
+    t.g = all[index];
+    const Geom& g = t.g;
+    const int kz = cfg.kz, ns = cfg.nsplit;
+    const size_t P = g.plane, P3 = P * kz;
+    // neighbours L, R, B, T, BL, BR, TL, TR
+    const int dj[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, di[8] = {0, 0, -1, 1, -1, -1, 1, 1};
+    for (int d = 0; d < 8; d++) {
+      int lj = t.lj + dj[d], li = t.li + di[d];
+      t.nbr[d] = (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
+    }
+    for (int b = 0; b < 2; b++) {
+      t.a1u[b] = dalloc(t, P3); t.a1v[b] = dalloc(t, P3); t.a1t[b] = dalloc(t, P3);
+      t.a1qv[b] = dalloc(t, P3); t.a1qc[b] = dalloc(t, P3);
+      t.a2u[b] = dalloc(t, P3); t.a2v[b] = dalloc(t, P3); t.a2t[b] = dalloc(t, P3);
+      t.a2qv[b] = dalloc(t, P3); t.a2qc[b] = dalloc(t, P3);
+    }
+    t.psa = dalloc(t, P); t.psb = dalloc(t, P);
+    t.dstor = dalloc(t, P * ns); t.hstor = dalloc(t, P * ns);
+    t.msfx = dalloc(t, P); t.msfd = dalloc(t, P); t.coriol = dalloc(t, P); t.ht = dalloc(t, P);
+    t.xmsf = dalloc(t, P); t.dmsf = dalloc(t, P); t.hgfact = dalloc(t, P); t.mapf = dalloc(t, P);
+    t.rgcr = talloc<int8_t>(t, P); t.rgdt = talloc<int8_t>(t, P);
+    t.ibcr = talloc<int16_t>(t, P); t.ibdt = talloc<int16_t>(t, P);
+    t.ub0 = dalloc(t, P3); t.ubt = dalloc(t, P3); t.vb0 = dalloc(t, P3); t.vbt = dalloc(t, P3);
+    t.tb0 = dalloc(t, P3); t.tbt = dalloc(t, P3); t.qb0 = dalloc(t, P3); t.qbt = dalloc(t, P3);
+    t.pb0 = dalloc(t, P); t.pbt = dalloc(t, P);
+    t.rpsa = dalloc(t, P); t.rpsb = dalloc(t, P); t.rpsc = dalloc(t, P); t.rpsda = dalloc(t, P);
+    t.psc = dalloc(t, P); t.psdota = dalloc(t, P); t.psdotb = dalloc(t, P); t.pten = dalloc(t, 2 * P);
+    t.umc = dalloc(t, P3); t.vmc = dalloc(t, P3); t.ud = dalloc(t, P3); t.vd = dalloc(t, P3);
+    t.xt = dalloc(t, P3); t.xqv = dalloc(t, P3); t.xqc = dalloc(t, P3); t.xtv = dalloc(t, P3);
+    t.qdot = dalloc(t, P * (kz + 1));
+    t.ubd = dalloc(t, P3); t.vbd = dalloc(t, P3); t.tb3d = dalloc(t, P3); t.qvb = dalloc(t, P3);
+    t.qcb = dalloc(t, P3); t.xkc = dalloc(t, P3); t.phi = dalloc(t, P3);
+    t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
+    t.dep = talloc<uint8_t>(t, 2 * P3); t.depplane = talloc<int>(t, 2 * kz);
+    t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
+    t.ddsum = dalloc(t, P * ns); t.dhsum = dalloc(t, P * ns);
+    t.uu = dalloc(t, P); t.vv = dalloc(t, P);
+    t.tten = dalloc(t, P3); t.uten = dalloc(t, P3); t.vten = dalloc(t, P3);
+    t.qvten = dalloc(t, P3); t.qcten = dalloc(t, P3); t.omega = dalloc(t, P3); t.xkcs = dalloc(t, P3);
+    slen = std::max<long>(g.pitch, g.ni);
+    for (int s = 0; s < 16; s++) t.sl[s] = dalloc(t, (size_t)slen * kz);
+    dim3 gr = grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1);
+    t.nred = gr.x * gr.y;
+    t.red = dalloc(t, 2 * (size_t)t.nred + 2);
+    // boundary masks
+    std::vector<int8_t> rg;
+    std::vector<int16_t> ib;
+    setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgx, false, rg, ib);
+    HIPCHK(hipMemcpy(t.rgcr, rg.data(), P, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.ibcr, ib.data(), P * 2, hipMemcpyHostToDevice));
+    setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgd, true, rg, ib);
+    HIPCHK(hipMemcpy(t.rgdt, rg.data(), P, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t.ibdt, ib.data(), P * 2, hipMemcpyHostToDevice));
+  }
+
+  void create(const rcmdyn_config* c) {
+    cfg = *c;
+    if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
+    if (cfg.idynamic != 1) throw std::runtime_error("rcmdyn: only idynamic=1 (hydrostatic) is built");
+    if (cfg.idiffu != 1) throw std::runtime_error("rcmdyn: only idiffu=1 is built");
+    if (cfg.ipgf != 0) throw std::runtime_error("rcmdyn: only ipgf=0 is built");
+    if (cfg.iboudy != 5 && cfg.iboudy != 1) throw std::runtime_error("rcmdyn: iboudy must be 1 or 5");
+    if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
+    if (cfg.nsplit < 1 || cfg.nsplit > MAXSPLIT) throw std::runtime_error("rcmdyn: nsplit out of range");
+    if (cfg.nspgx >= MAXNSP || cfg.nspgd != cfg.nspgx) throw std::runtime_error("rcmdyn: nspgx/nspgd unsupported");
+    ntiles = cfg.nproc_j * cfg.nproc_i;
+    if (ntiles < 1 || cfg.tile_first < 0 || cfg.tile_count < 1 || cfg.tile_first + cfg.tile_count > ntiles)
+      throw std::runtime_error("rcmdyn: bad tile range");
+    if (cfg.device >= 0) HIPCHK(hipSetDevice(cfg.device));
+    HIPCHK(hipGetDevice(&device));
+    for (int t = 0; t < ntiles; t++) {
+      all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t));
+      const Geom& g = all.back();
+      if (g.jde2 - g.jde1 + 1 < 3 || g.ide2 - g.ide1 + 1 < 3)
+        throw std::runtime_error("rcmdyn: Too much processors (tile < 3x3), mod_mppparam.F90:1365");
+    }
+    compute_constants();
+    HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&dc, sizeof(Consts)));
+    HIPCHK(hipMemcpy(dc, &hc, sizeof(Consts), hipMemcpyHostToDevice));
+    hs = StepState{};
+    hs.dt = cfg.dtsec; hs.xbctime = 0.0; hs.lcount = 0;
+    HIPCHK(hipMalloc(&ds, sizeof(StepState)));
+    HIPCHK(hipMemcpy(ds, &hs, sizeof(StepState), hipMemcpyHostToDevice));
+    tiles.resize(cfg.tile_count);
+    for (int t = 0; t < cfg.tile_count; t++) setup_tile(tiles[t], cfg.tile_first + t);
+    if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg, stream));
+  }
+
+  void destroy() {
+    for (int p = 0; p < 2; p++)
+      if (gexec[p]) hipGraphExecDestroy(gexec[p]);
+    for (auto& t : tiles)
+      for (void* p : t.allocs) hipFree(p);
+    tiles.clear();
+    comm.reset();
+    if (dc) hipFree(dc);
+    if (ds) hipFree(ds);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  void invalidate_graphs() {
+    for (int p = 0; p < 2; p++)
+      if (gexec[p]) { hipGraphExecDestroy(gexec[p]); gexec[p] = nullptr; }
+  }
+
+  // ------------------------------------------------------------------ field access
+  double* fptr(Tile& t, FK f) {
+    const int c = t.cur;
+    switch (f) {
+      case FK::A1U: return t.a1u[c]; case FK::A1V: return t.a1v[c]; case FK::A1T: return t.a1t[c];
+      case FK::A1QV: return t.a1qv[c]; case FK::A1QC: return t.a1qc[c];
+      case FK::A2U: return t.a2u[c]; case FK::A2V: return t.a2v[c]; case FK::A2T: return t.a2t[c];
+      case FK::A2QV: return t.a2qv[c]; case FK::A2QC: return t.a2qc[c];
+      case FK::PSA: return t.psa; case FK::PSB: return t.psb;
+      case FK::PSDOTA: return t.psdota; case FK::PSDOTB: return t.psdotb;
+      case FK::UD: return t.ud; case FK::VD: return t.vd; case FK::QDOT: return t.qdot;
+      case FK::XKC: return t.xkc; case FK::CQV: return t.cqv; case FK::CQC: return t.cqc;
+      case FK::PHI: return t.phi; case FK::UU: return t.uu; case FK::VV: return t.vv;
+      case FK::DHSUM: return t.dhsum; case FK::DELH: return t.delh;
+      case FK::MSFX: return t.msfx; case FK::MSFD: return t.msfd; case FK::HT: return t.ht;
+      case FK::CORIOL: return t.coriol;
+      case FK::UB0: return t.ub0; case FK::UBT: return t.ubt; case FK::VB0: return t.vb0;
+      case FK::VBT: return t.vbt; case FK::TB0: return t.tb0; case FK::TBT: return t.tbt;
+      case FK::QB0: return t.qb0; case FK::QBT: return t.qbt; case FK::PB0: return t.pb0;
+      case FK::PBT: return t.pbt; case FK::DSTOR: return t.dstor; case FK::HSTOR: return t.hstor;
+    }
+    return nullptr;
+  }
+
+  // public field id -> (pointer, levels)
+  double* field_ptr(Tile& t, int f, int& nk) {
+    nk = cfg.kz;
+    const int c = t.cur;
+    switch (f) {
+      case RCMDYN_ATM1_U: return t.a1u[c]; case RCMDYN_ATM1_V: return t.a1v[c];
+      case RCMDYN_ATM1_T: return t.a1t[c]; case RCMDYN_ATM1_QV: return t.a1qv[c];
+      case RCMDYN_ATM1_QC: return t.a1qc[c];
+      case RCMDYN_ATM2_U: return t.a2u[c]; case RCMDYN_ATM2_V: return t.a2v[c];
+      case RCMDYN_ATM2_T: return t.a2t[c]; case RCMDYN_ATM2_QV: return t.a2qv[c];
+      case RCMDYN_ATM2_QC: return t.a2qc[c];
+      case RCMDYN_XUB_B0: return t.ub0; case RCMDYN_XUB_BT: return t.ubt;
+      case RCMDYN_XVB_B0: return t.vb0; case RCMDYN_XVB_BT: return t.vbt;
+      case RCMDYN_XTB_B0: return t.tb0; case RCMDYN_XTB_BT: return t.tbt;
+      case RCMDYN_XQB_B0: return t.qb0; case RCMDYN_XQB_BT: return t.qbt;
+      case RCMDYN_TTEN: return t.tten; case RCMDYN_UTEN: return t.uten; case RCMDYN_VTEN: return t.vten;
+      case RCMDYN_QVTEN: return t.qvten; case RCMDYN_QCTEN: return t.qcten;
+      case RCMDYN_OMEGA: return t.omega; case RCMDYN_XKC: return t.xkcs; case RCMDYN_PHI: return t.phi;
+      case RCMDYN_QDOT: nk = cfg.kz + 1; return t.qdot;
+      case RCMDYN_DSTOR: nk = cfg.nsplit; return t.dstor;
+      case RCMDYN_HSTOR: nk = cfg.nsplit; return t.hstor;
+      default: break;
+    }
+    nk = 1;
+    switch (f) {
+      case RCMDYN_PSA: return t.psa; case RCMDYN_PSB: return t.psb;
+      case RCMDYN_MSFX: return t.msfx; case RCMDYN_MSFD: return t.msfd;
+      case RCMDYN_CORIOL: return t.coriol; case RCMDYN_HT: return t.ht;
+      case RCMDYN_XPSB_B0: return t.pb0; case RCMDYN_XPSB_BT: return t.pbt;
+      case RCMDYN_PSC: return t.psc; case RCMDYN_PTEN: return t.pten + t.g.plane;
+      case RCMDYN_PSDOTA: return t.psdota;
+      default: return nullptr;
+    }
+  }
+
+  void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
+    if (f < 0 || f > RCMDYN_XPSB_BT) throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
+    HIPCHK(hipStreamSynchronize(stream));
+    const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
+    for (auto& t : tiles) {
+      int nk;
+      double* d = field_ptr(t, f, nk);
+      const Geom& g = t.g;
+      std::vector<double> h((size_t)nk * g.plane);
+      HIPCHK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+      for (int k = std::max(k1, 1); k <= std::min(k2, nk); k++)
+        for (int i = std::max(i1, g.i0); i <= std::min(i2, g.i0 + g.ni - 1); i++)
+          for (int j = std::max(j1, g.j0); j <= std::min(j2, g.j0 + g.nj - 1); j++)
+            h[(size_t)(k - 1) * g.plane + g.ix(j, i)] = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)];
+      HIPCHK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    }
+    if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
+    if (f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) bdy_dirty = true;
+  }
+
+  void get(int f, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
+    HIPCHK(hipStreamSynchronize(stream));
+    const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
+    for (auto& t : tiles) {
+      int nk;
+      double* d = field_ptr(t, f, nk);
+      if (!d) throw std::runtime_error("rcmdyn_get: unknown field");
+      const Geom& g = t.g;
+      std::vector<double> h((size_t)nk * g.plane);
+      HIPCHK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+      for (int k = std::max(k1, 1); k <= std::min(k2, nk); k++)
+        for (int i = std::max(i1, g.ide1); i <= std::min(i2, g.ide2); i++)
+          for (int j = std::max(j1, g.jde1); j <= std::min(j2, g.jde2); j++)
+            dst[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)] = h[(size_t)(k - 1) * g.plane + g.ix(j, i)];
+    }
+  }
+
+  // ------------------------------------------------------------------ halo exchange
+  // exchange / exchange_lb / exchange_rt (sides 0 / 1 / 2), Main/mpplib/mod_mppparam.F90
+  void xch(FK f, int nk, int width, int sides) {
+    if (ntiles == 1) return;
+    for (auto& t : tiles) {
+      NbrTable nt{};
+      for (int d = 0; d < 9; d++) nt.base[d] = nullptr;
+      const int dj9[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, di9[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+      for (int d = 0; d < 9; d++) {
+        if (d == 4) continue;
+        int lj = t.lj + dj9[d], li = t.li + di9[d];
+        if (lj < 0 || lj >= cfg.nproc_j || li < 0 || li >= cfg.nproc_i) continue;
+        int idx = lj * cfg.nproc_i + li;
+        Tile* nb = local_tile(idx);
+        if (!nb) continue;                       // remote: handled by the RCCL transport
+        nt.base[d] = fptr(*nb, f);
+        nt.j0[d] = nb->g.j0; nt.i0[d] = nb->g.i0; nt.pitch[d] = nb->g.pitch; nt.plane[d] = nb->g.plane;
+      }
+      hipLaunchKernelGGL(k_ghost_fill, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fptr(t, f), nk, width,
+                         sides, nt);
+    }
+    if (comm) comm->exchange(*this->tiles.data(), fptr(tiles[0], f), nk, width, sides);
+  }
+
+  Tile* local_tile(int idx) {
+    int o = idx - cfg.tile_first;
+    return (o >= 0 && o < (int)tiles.size()) ? &tiles[o] : nullptr;
+  }
+
+  // exchange_bdy_lr / exchange_bdy_bt of the bdyuv slices (Main/mod_bdycod.F90:1063-1089)
+  void xch_slices() {
+    if (ntiles == 1) return;
+    const int kz = cfg.kz;
+    for (auto& t : tiles) {
+      const Geom& g = t.g;
+      auto fill = [&](int s, int along) {
+        // along 0: j-indexed slices (south/north) exchanged with left/right tiles
+        // along 1: i-indexed slices (west/east) exchanged with bottom/top tiles
+        for (int side = 0; side < 2; side++) {
+          int nbidx = along == 0 ? t.nbr[side == 0 ? 0 : 1] : t.nbr[side == 0 ? 2 : 3];
+          if (nbidx < 0) continue;
+          Tile* nb = local_tile(nbidx);
+          if (!nb) continue;
+          const Geom& h = nb->g;
+          int dst_idx, src_idx;
+          if (along == 0) {
+            int jdst = side == 0 ? g.jde1 - 1 : g.jde2 + 1;
+            dst_idx = jdst - g.j0; src_idx = jdst - h.j0;
+          } else {
+            int idst = side == 0 ? g.ide1 - 1 : g.ide2 + 1;
+            dst_idx = idst - g.i0; src_idx = idst - h.i0;
+          }
+          hipLaunchKernelGGL(k_slice_fill, dim3(1), dim3(64), 0, stream, t.sl[s], nb->sl[s], dst_idx, src_idx,
+                             slen, slen, kz);
+        }
+      };
+      if (g.bt) for (int s : {10, 11, 14, 15}) fill(s, 0);
+      if (g.bb) for (int s : {8, 9, 12, 13}) fill(s, 0);
+      if (g.bl) for (int s : {0, 1, 4, 5}) fill(s, 1);
+      if (g.br) for (int s : {2, 3, 6, 7}) fill(s, 1);
+    }
+    if (comm) comm->exchange_slices(tiles[0], tiles[0].sl, slen, kz);
+  }
+
+  // ------------------------------------------------------------------ the step
+  template <class F>
+  void each(F fn) { for (auto& t : tiles) fn(t); }
+
+  void prepare() {
+    if (statics_dirty) {
+      xch(FK::MSFX, 1, 2, 0); xch(FK::MSFD, 1, 2, 0); xch(FK::HT, 1, 2, 0); xch(FK::CORIOL, 1, 2, 0);
+      each([&](Tile& t) {
+        hipLaunchKernelGGL(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
+                           t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
+      });
+      statics_dirty = false;
+      invalidate_graphs();
+    }
+    if (bdy_dirty) {
+      const int kz = cfg.kz;
+      for (FK f : {FK::UB0, FK::UBT, FK::VB0, FK::VBT, FK::TB0, FK::TBT, FK::QB0, FK::QBT}) xch(f, kz, 1, 0);
+      xch(FK::PB0, 1, 1, 0); xch(FK::PBT, 1, 1, 0);
+      bdy_dirty = false;
+      invalidate_graphs();
+    }
+  }
+
+  void tend() {
+    const int kz = cfg.kz, ns = cfg.nsplit;
+    // surface_pressures, Main/mod_tendency.F90:815-834
+    xch(FK::PSA, 1, 1, 0); xch(FK::PSB, 1, 2, 0);
+    each([&](Tile& t) {
+      hipLaunchKernelGGL(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, t.psa, t.psb, t.rpsa,
+                         t.rpsb, t.psdota, t.psdotb);
+    });
+    xch(FK::PSDOTA, 1, 1, 0); xch(FK::PSDOTB, 1, 2, 0);
+    // decouple, :852-1116
+    for (FK f : {FK::A1U, FK::A1V, FK::A1T, FK::A1QV, FK::A1QC}) xch(f, kz, 1, 0);
+    each([&](Tile& t) {
+      const int c = t.cur;
+      hipLaunchKernelGGL(k_decouple, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, t.a1u[c], t.a1v[c], t.a1t[c],
+                         t.a1qv[c], t.a1qc[c], t.msfd, t.psdota, t.rpsa, t.rpsda, t.umc, t.vmc, t.ud, t.vd, t.xt,
+                         t.xqv, t.xqc, t.xtv, hc.ep1);
+    });
+    xch(FK::UD, kz, 1, 0); xch(FK::VD, kz, 1, 0);
+    for (FK f : {FK::A2U, FK::A2V, FK::A2T, FK::A2QV, FK::A2QC}) xch(f, kz, 2, 0);
+    // compute_omega column part, :1118-1156
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_omega_col, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc,
+                         t.umc, t.vmc, t.msfx, t.rpsa, t.pten, t.qdot);
+    });
+    xch(FK::QDOT, kz + 1, 1, 0);
+    // mkslice, Main/mod_slice.F90:102-300 (dyn subset)
+    each([&](Tile& t) {
+      const int c = t.cur;
+      hipLaunchKernelGGL(k_mkslice, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, t.a2u[c], t.a2v[c], t.a2t[c],
+                         t.a2qv[c], t.a2qc[c], t.psb, t.psdotb, t.ubd, t.vbd, t.tb3d, t.qvb, t.qcb);
+    });
+    // new_pressure, :1428-1460
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      dim3 gr = grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1);
+      hipLaunchKernelGGL(k_new_pressure, gr, BLK, 0, stream, g, dc, ds, t.psa, t.psb, t.pb0, t.pbt, t.rgcr, t.ibcr,
+                         t.pten, t.pten + g.plane, t.psc, t.rpsc, t.red);
+    });
+    each([&](Tile& t) { hipLaunchKernelGGL(k_reduce_noise, dim3(1), dim3(256), 0, stream, t.red, t.nred, ds); });
+    // calc_coeff, Main/mod_diffusion.F90:169-251
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_calc_coeff, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc,
+                         t.ubd, t.vbd, t.hgfact, t.xkc);
+    });
+    xch(FK::XKC, kz, 1, 0);
+    // geopotential for the PGF, :2033-2099
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_phi_col, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
+                         t.a1t[t.cur], t.xqv, t.xqc, t.psa, t.rpsa, t.ht, t.phi);
+    });
+    xch(FK::PHI, kz, 1, 1);
+    // fused tendencies + forecast + time filter
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur, n = 1 - c;
+      hipLaunchKernelGGL(k_momentum, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, t.a1u[c], t.a1v[c],
+                         t.a2u[c], t.a2v[c], t.a1u[n], t.a1v[n], t.a2u[n], t.a2v[n], t.umc, t.vmc, t.ud, t.vd,
+                         t.qdot, t.coriol, t.dmsf, t.msfd, t.ub0, t.ubt, t.vb0, t.vbt, t.rgdt, t.ibdt, t.xkc,
+                         t.psdotb, t.ubd, t.vbd, t.xtv, t.psdota, t.psa, t.phi, t.uten, t.vten);
+      hipLaunchKernelGGL(k_temperature, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, t.a1t[c], t.a2t[c],
+                         t.a1t[n], t.a2t[n], t.xt, t.umc, t.vmc, t.psa, t.psb, t.xmsf, t.qdot, t.pten, t.ud, t.vd,
+                         t.msfx, t.xqv, t.xtv, t.rpsa, t.tb0, t.tbt, t.rgcr, t.ibcr, t.xkc, t.tb3d, t.tten,
+                         t.omega, t.xkcs);
+      hipLaunchKernelGGL(k_moisture, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc, ds,
+                         t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.xqv, t.xqc, t.umc, t.vmc, t.psa, t.psb,
+                         t.xmsf, t.qdot, t.qb0, t.qbt, t.rgcr, t.ibcr, t.xkc, t.qvb, t.qcb, t.cqv, t.cqc, t.qvten,
+                         t.qcten);
+    });
+    xch(FK::CQV, kz, 1, 0); xch(FK::CQC, kz, 1, 0);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_ps_filter, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, 1), BLK, 0, stream, g, dc,
+                         t.psa, t.psb, t.psc);
+      hipLaunchKernelGGL(k_negfix, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, kz,
+                         t.cqv, t.cqc, t.fqv, t.fqc, t.dep, t.depplane);
+      hipLaunchKernelGGL(k_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, kz, t.cqv, t.cqc, t.fqv, t.fqc,
+                         t.dep, t.depplane);
+      const int c = t.cur, n = 1 - c;
+      hipLaunchKernelGGL(k_moisture_filter, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, t.a1qv[c], t.a1qc[c],
+                         t.a2qv[c], t.a2qc[c], t.a1qv[n], t.a1qc[n], t.a2qv[n], t.a2qc[n], t.fqv, t.fqc, t.psa,
+                         t.psb);
+      t.cur = n;
+    });
+    // splitf, Main/mod_split.F90:243-461
+    xch(FK::PSA, 1, 1, 0);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_psc2psd, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, t.psa,
+                         t.psdota);
+    });
+    for (FK f : {FK::A1U, FK::A1V, FK::A2U, FK::A2V}) xch(f, kz, 1, 2);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur;
+      hipLaunchKernelGGL(k_split_project, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
+                         dc, t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa, t.psb, t.msfd,
+                         t.mapf, t.dstor, t.hstor, t.deld, t.delh);
+      hipLaunchKernelGGL(k_spstep_init, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc,
+                         t.deld, t.delh, t.ddsum, t.dhsum);
+    });
+    // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
+    for (int l = 1; l <= ns; l++) {
+      int n0 = 1, n1 = 2, n2 = n0;
+      const int m2 = (int)hc.aam[l - 1] * 2;
+      sp_substep(l, n0, n0, n0, n1, 0);
+      for (int n = 2; n <= m2; n++) {
+        sp_substep(l, n1, n0, n1, n2, 1);
+        n0 = n1; n1 = n2; n2 = n0;
+      }
+    }
+    xch(FK::DHSUM, ns, 1, 1);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur;
+      hipLaunchKernelGGL(k_split_correct, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
+                         dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa, t.psb, t.a1t[c], t.a2t[c], t.a1u[c],
+                         t.a1v[c], t.a2u[c], t.a2v[c]);
+    });
+    hipLaunchKernelGGL(k_advance_time, dim3(1), dim3(1), 0, stream, ds, cfg.dtsec);
+    hs.lcount += 1;
+    if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+
+  // one spstep substep: gradient of delh(src) -> (uu,vv) -> divergence -> mode update
+  void sp_substep(int l, int src, int n0, int n1, int nn, int leap) {
+    xch_delh_slot(l, src);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_spstep_grad, grid3(g.jdi2 - g.jdi1 + 1, g.idi2 - g.idi1 + 1, 1), BLK, 0, stream, g, dc, l,
+                         src, t.delh, t.msfx, t.msfd, t.psdota, t.uu, t.vv);
+    });
+    xch(FK::UU, 1, 1, 2); xch(FK::VV, 1, 1, 2);
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      hipLaunchKernelGGL(k_spstep_update, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
+                         l, n0, n1, nn, leap, t.uu, t.vv, t.mapf, t.psa, t.deld, t.delh, t.ddsum, t.dhsum);
+    });
+  }
+
+  // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
+  void xch_delh_slot(int l, int src) {
+    if (ntiles == 1) return;
+    const long off = ((long)(src - 1) * cfg.nsplit + (l - 1));
+    for (auto& t : tiles) {
+      NbrTable nt{};
+      const int dj9[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, di9[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
+      for (int d = 0; d < 9; d++) {
+        nt.base[d] = nullptr;
+        if (d == 4) continue;
+        int lj = t.lj + dj9[d], li = t.li + di9[d];
+        if (lj < 0 || lj >= cfg.nproc_j || li < 0 || li >= cfg.nproc_i) continue;
+        Tile* nb = local_tile(lj * cfg.nproc_i + li);
+        if (!nb) continue;
+        nt.base[d] = nb->delh + off * nb->g.plane;
+        nt.j0[d] = nb->g.j0; nt.i0[d] = nb->g.i0; nt.pitch[d] = nb->g.pitch; nt.plane[d] = nb->g.plane;
+      }
+      hipLaunchKernelGGL(k_ghost_fill, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, t.delh + off * t.g.plane, 1,
+                         1, 1, nt);
+    }
+    if (comm) comm->exchange(tiles[0], tiles[0].delh + off * tiles[0].g.plane, 1, 1, 1);
+  }
+
+  void bdyval() {
+    const int kz = cfg.kz;
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur;
+      Slices sl;
+      for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
+      hipLaunchKernelGGL(k_bdyval_set, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, ds,
+                         t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
+                         t.a2qv[c], t.a2qc[c], t.psa, t.psb, t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt,
+                         t.pb0, t.pbt, sl, slen);
+      hipLaunchKernelGGL(k_bdyval_corners, dim3(1), dim3(64), 0, stream, g, kz, sl, slen);
+    });
+    xch_slices();
+    if (!cfg.present_qc) {
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        Slices sl;
+        for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
+        if (g.bl || g.br)
+          hipLaunchKernelGGL(k_bdyval_qc_we, dim3((g.ice2 - g.ice1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
+                             t.a1qc[t.cur], t.psa, sl, slen);
+      });
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        Slices sl;
+        for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
+        if (g.bb || g.bt)
+          hipLaunchKernelGGL(k_bdyval_qc_sn, dim3((g.jci2 - g.jci1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
+                             t.a1qc[t.cur], t.psa, sl, slen);
+      });
+    }
+    hipLaunchKernelGGL(k_bdyval_time, dim3(1), dim3(1), 0, stream, ds, cfg.dtsec);
+    hs.xbctime = hs.xbctime + cfg.dtsec;
+  }
+
+  // ------------------------------------------------------------------ graph replay
+  void step(int n) {
+    prepare();
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    const bool use_graph = !(comm && !comm->graph_safe());
+    HIPCHK(hipEventRecord(e0, stream));
+    for (int s = 0; s < n; s++) {
+      const int par = tiles[0].cur;
+      if (use_graph) {
+        if (!gexec[par]) capture(par);
+        HIPCHK(hipGraphLaunch(gexec[par], stream));
+        // replay the host-side bookkeeping of one tend + bdyval
+        for (auto& t : tiles) t.cur = 1 - t.cur;
+        hs.lcount += 1;
+        if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+        hs.xbctime = hs.xbctime + cfg.dtsec;
+      } else {
+        tend();
+        bdyval();
+      }
+    }
+    HIPCHK(hipEventRecord(e1, stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    last_ms = n > 0 ? (double)ms / n : 0.0;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+  }
+
+  void capture(int par) {
+    // capture one tend + bdyval for the current ping-pong parity; host bookkeeping done in
+    // tend()/bdyval() is rolled back because step() replays it per launch.
+    const StepState save = hs;
+    std::vector<int> curs;
+    for (auto& t : tiles) curs.push_back(t.cur);
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    tend();
+    bdyval();
+    HIPCHK(hipStreamEndCapture(stream, &graph));
+    HIPCHK(hipGraphInstantiate(&gexec[par], graph, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(graph));
+    hs = save;
+    for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
+  }
+
+  void set_time(long long lcount, double dt, double xbctime) {
+    HIPCHK(hipStreamSynchronize(stream));
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    st.lcount = lcount; st.dt = dt; st.xbctime = xbctime; st.nanflag = 0;
+    HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
+    hs.lcount = lcount; hs.dt = dt; hs.xbctime = xbctime;
+  }
+
+  void diagnostics(double out[4]) {
+    HIPCHK(hipStreamSynchronize(stream));
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    out[0] = st.ptntot; out[1] = st.pt2tot; out[2] = std::isnan(st.ptntot) ? 1.0 : 0.0; out[3] = st.nanflag;
+  }
+};
+
+// ======================================================================== C-ABI
+namespace {
+template <class F>
+int guard(rcmdyn_t* h, F fn) {
+  try {
+    fn();
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    if (h) h->err = e.what();
+    return 1;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int rcmdyn_create(const rcmdyn_config* cfg, rcmdyn_t** out) {
+  if (!cfg || !out) { g_last_error = "rcmdyn_create: null argument"; return 1; }
+  auto* h = new rcmdyn_engine();
+  int rc = guard(h, [&] { h->create(cfg); });
+  if (rc) {
+    g_last_error = h->err;
+    h->destroy();
+    delete h;
+    *out = nullptr;
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+
+int rcmdyn_destroy(rcmdyn_t* h) {
+  if (!h) return 0;
+  int rc = guard(h, [&] { h->destroy(); });
+  delete h;
+  return rc;
+}
+
+const char* rcmdyn_last_error(rcmdyn_t* h) { return h ? h->err.c_str() : g_last_error.c_str(); }
+
+int rcmdyn_set_nproc(int32_t nproc, int32_t jx, int32_t iy, int32_t cpus[2]) {
+  // Main/mpplib/mod_mppparam.F90:1152-1186
+  if (nproc < 1 || !cpus) return 1;
+  if (nproc == 1) { cpus[0] = 1; cpus[1] = 1; return 0; }
+  if (nproc < 4) { cpus[0] = nproc; cpus[1] = 1; return 0; }
+  int cj = ((int)std::lround(std::sqrt((double)nproc)) / 2) * 2;
+  if (iy > (int)(1.5 * (double)jx)) {
+    cj -= 1;
+    while (nproc % cj != 0) cj -= 1;
+  } else if (jx > (int)(1.5 * (double)iy)) {
+    cj += 1;
+    while (nproc % cj != 0) cj += 1;
+  } else {
+    while (nproc % cj != 0) cj += 1;
+  }
+  cpus[0] = cj; cpus[1] = nproc / cj;
+  return 0;
+}
+
+int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i, int32_t tile, int32_t ext[8],
+                       int32_t bdy[4]) {
+  if (tile < 0 || tile >= nproc_j * nproc_i) return 1;
+  tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy);
+  return 0;
+}
+
+int rcmdyn_put(rcmdyn_t* h, int32_t field, const double* src, int32_t j1, int32_t j2, int32_t i1, int32_t i2,
+               int32_t k1, int32_t k2) {
+  return guard(h, [&] { h->put(field, src, j1, j2, i1, i2, k1, k2); });
+}
+
+int rcmdyn_get(rcmdyn_t* h, int32_t field, double* dst, int32_t j1, int32_t j2, int32_t i1, int32_t i2, int32_t k1,
+               int32_t k2) {
+  return guard(h, [&] { h->get(field, dst, j1, j2, i1, i2, k1, k2); });
+}
+
+int rcmdyn_set_time(rcmdyn_t* h, int64_t lcount, double dt, double xbctime) {
+  return guard(h, [&] { h->set_time(lcount, dt, xbctime); });
+}
+
+int rcmdyn_get_time(rcmdyn_t* h, int64_t* lcount, double* dt, double* xbctime) {
+  return guard(h, [&] {
+    *lcount = h->hs.lcount; *dt = h->hs.dt; *xbctime = h->hs.xbctime;
+  });
+}
+
+int rcmdyn_tend(rcmdyn_t* h) {
+  return guard(h, [&] {
+    h->prepare();
+    h->tend();
+    HIPCHK(hipStreamSynchronize(h->stream));
+    StepState st;
+    HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
+    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+  });
+}
+
+int rcmdyn_bdyval(rcmdyn_t* h) {
+  return guard(h, [&] {
+    h->prepare();
+    h->bdyval();
+    HIPCHK(hipStreamSynchronize(h->stream));
+  });
+}
+
+int rcmdyn_step(rcmdyn_t* h, int32_t nsteps) { return guard(h, [&] { h->step(nsteps); }); }
+
+int rcmdyn_synchronize(rcmdyn_t* h) { return guard(h, [&] { HIPCHK(hipStreamSynchronize(h->stream)); }); }
+
+int rcmdyn_diagnostics(rcmdyn_t* h, double out[4]) { return guard(h, [&] { h->diagnostics(out); }); }
+
+int rcmdyn_comm_unique_id(uint8_t out[128]) {
+  try {
+    comm_unique_id(out);
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return 1;
+  }
+}
+
+int rcmdyn_last_step_ms(rcmdyn_t* h, double* ms) { return guard(h, [&] { *ms = h->last_ms; }); }
+
+}  // extern "C"

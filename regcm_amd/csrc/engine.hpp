@@ -1,0 +1,102 @@
+// engine.hpp -- internal types of the MI355X dynamical-core engine (not part of the C-ABI).
+//
+// Data layout in HBM (DESIGN.md "Data layout"): every field of a tile lives on one 2-D frame
+// covering the tile's dot-point extents plus a G-point ghost ring, rows j-fastest with a
+// padded pitch (multiple of 16 doubles = 128 B), planes stacked by level k:
+//   addr(j,i,k) = base + (k-1)*plane + (i-i0)*pitch + (j-j0),   j,i global Fortran indices.
+// Cross-point fields use the same frame (their last row/column on the east/north tiles is
+// unused), so every kernel indexes every field with the same affine map.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rcmdyn.h"
+
+namespace rcm {
+
+constexpr int G = 2;               // ghost width (idif = 2 for idiffu = 1)
+constexpr int MAXKZ = RCMDYN_MAXKZ;
+constexpr int MAXSPLIT = RCMDYN_MAXSPLIT;
+constexpr int MAXNSP = 256;        // max boundary-band width (nspgx)
+
+// Index ranges of one tile, Main/mod_atm_interface.F90:181-381 (global indices).
+struct Geom {
+  int jde1, jde2, jdi1, jdi2, jdii1, jdii2, ide1, ide2, idi1, idi2, idii1, idii2;
+  int jce1, jce2, jci1, jci2, jcii1, jcii2, ice1, ice2, ici1, ici2, icii1, icii2;
+  int jde1ga, jde2ga, ide1ga, ide2ga, jce1ga, jce2ga, ice1ga, ice2ga;
+  int jci1ga, jci2ga, ici1ga, ici2ga;
+  int jde1gb, jde2gb, ide1gb, ide2gb, jce1gb, jce2gb, ice1gb, ice2gb;
+  int bl, br, bb, bt;              // has_bdyleft/right/bottom/top
+  int j0, i0;                      // global index of frame origin
+  int nj, ni;                      // frame size (nj <= pitch)
+  int pitch;
+  long plane;
+  __host__ __device__ __forceinline__ long ix(int j, int i) const {
+    return (long)(i - i0) * pitch + (j - j0);
+  }
+};
+
+// Run constants (read-only on device, one copy per engine).
+struct Consts {
+  int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc;
+  double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
+  double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;
+  double rgas, cpd, c287, ep1, regrav;
+  double sigma[MAXKZ + 2], hsigma[MAXKZ + 1], dsigma[MAXKZ + 1];
+  double twt1[MAXKZ + 1], twt2[MAXKZ + 1], qcon[MAXKZ + 1], xds[MAXKZ + 1];
+  double hefc[MAXNSP][MAXKZ + 1], hegc[MAXNSP][MAXKZ + 1];
+  double fcx[MAXNSP], gcx[MAXNSP];
+  double zmatx[MAXSPLIT][MAXKZ], zmatxr[MAXSPLIT][MAXKZ], am[MAXSPLIT][MAXKZ];
+  double tau[MAXSPLIT][MAXKZ];
+  double an[MAXSPLIT], hbar[MAXSPLIT], aam[MAXSPLIT], dtau[MAXSPLIT];
+  double pdlog[MAXSPLIT][MAXKZ + 2], eps1[MAXSPLIT][MAXKZ + 2], pd;
+};
+
+// rcm_timer state on the device, advanced by kernels so one captured step is replayable.
+struct StepState {
+  double dt;          // current leapfrog dt
+  double xbctime;     // s since boundary interval start
+  long long lcount;   // completed steps
+  double ptntot, pt2tot;
+  int nanflag;        // sticky: set when a step produced NaN ptntot
+  int pad;
+};
+
+// Per-tile device buffers.
+struct Tile {
+  int index = 0;                   // tile number in the decomposition
+  int lj = 0, li = 0;              // cartesian location
+  Geom g{};
+  int nbr[8];                      // neighbour tiles: L, R, B, T, BL, BR, TL, TR (-1 none)
+  // prognostic state, ping-pong for the 3-D fields written by the fused update kernels
+  double *a1u[2], *a1v[2], *a1t[2], *a1qv[2], *a1qc[2];
+  double *a2u[2], *a2v[2], *a2t[2], *a2qv[2], *a2qc[2];
+  int cur = 0;
+  double *psa, *psb, *dstor, *hstor;
+  // statics
+  double *msfx, *msfd, *coriol, *ht, *xmsf, *dmsf, *hgfact, *mapf;
+  int8_t *rgcr, *rgdt;
+  int16_t *ibcr, *ibdt;
+  // boundary data
+  double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
+  // work
+  double *rpsa, *rpsb, *rpsc, *rpsda, *psc, *psdota, *psdotb, *pten;
+  double *umc, *vmc, *ud, *vd, *xt, *xqv, *xqc, *xtv, *qdot;
+  double *ubd, *vbd, *tb3d, *qvb, *qcb, *xkc, *phi;
+  double *cqv, *cqc, *fqv, *fqc;
+  uint8_t *dep;                    // negative-moisture dependency flags (2 x kz planes)
+  int *depplane;                   // per (n,k) plane flag
+  double *deld, *delh, *ddsum, *dhsum, *uu, *vv;
+  // diagnostics of the last tend
+  double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
+  // boundary slices (Main/mod_bdycod.F90:58-61): [k][frame index]
+  double *sl[16];
+  // reduction partials
+  double *red;
+  int nred;
+  std::vector<void*> allocs;
+};
+
+}  // namespace rcm
