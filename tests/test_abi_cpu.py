@@ -1,0 +1,105 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads and exports every entry point
+that include/rcmdyn.h declares, the ctypes image of rcmdyn_config matches the C layout, and
+the host-only decomposition entry points agree with mpplib's rule.  No compute call is made."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from regcm_amd import dycore
+from regcm_amd.config import RcmdynConfig, set_nproc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rcmdyn.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rcmdyn_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declarations_exported():
+    names = declared_functions()
+    assert len(names) >= 15
+    L = dycore.lib()
+    for n in names:
+        assert hasattr(L, n), n
+    assert sorted(dycore.EXPORTED) == names
+
+
+def test_exported_symbols_in_elf():
+    out = subprocess.run(["nm", "-D", "--defined-only", dycore.LIB_PATH], capture_output=True, text=True).stdout
+    for n in declared_functions():
+        assert re.search(rf"\bT {n}$", out, re.M), n
+
+
+def test_config_layout_matches_c():
+    probe = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rcmdyn.h"
+#define O(f) printf("%s %zu\n", #f, offsetof(rcmdyn_config, f))
+int main(void) {
+  printf("size %zu\n", sizeof(rcmdyn_config));
+  O(jx); O(present_qc); O(ds); O(dtbdys); O(sigma); O(zmatx); O(zmatxr); O(am); O(tau);
+  O(varpa1); O(an); O(hbar); O(aam); O(dtau); O(sigmah); O(pd); O(comm_rank); O(device);
+  O(comm_unique_id);
+  return 0;
+}
+"""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(d, "p")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", exe, c], check=True)
+        lines = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = dict(l.split() for l in lines if l)
+    assert int(got.pop("size")) == ctypes.sizeof(RcmdynConfig)
+    for name, off in got.items():
+        assert getattr(RcmdynConfig, name).offset == int(off), name
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 6, 8, 12, 16])
+@pytest.mark.parametrize("shape", [(192, 192), (384, 192), (96, 200), (48, 48)])
+def test_set_nproc_c_matches_python(n, shape):
+    assert dycore.set_nproc(n, *shape) == set_nproc(n, *shape)
+
+
+def test_tile_extents_partition_domain():
+    """Tiles cover the dot grid exactly once; remainder points go to the low tiles and the
+    last tile in each direction has one fewer cross point (mod_mppparam.F90:1295-1360)."""
+    jx, iy = 97, 50
+    cj, ci = 3, 2
+    cover = [[0] * (jx + 1) for _ in range(iy + 1)]
+    for t in range(cj * ci):
+        ext, bdy = dycore.tile_extent(jx, iy, cj, ci, t)
+        jde1, jde2, ide1, ide2, jce1, jce2, ice1, ice2 = ext
+        for i in range(ide1, ide2 + 1):
+            for j in range(jde1, jde2 + 1):
+                cover[i][j] += 1
+        assert jce2 == (jde2 - 1 if jde2 == jx else jde2)
+        assert ice2 == (ide2 - 1 if ide2 == iy else ide2)
+        assert bdy == [t // ci == 0, t // ci == cj - 1, t % ci == 0, t % ci == ci - 1]
+    assert all(cover[i][j] == 1 for i in range(1, iy + 1) for j in range(1, jx + 1))
+    widths = [dycore.tile_extent(jx, iy, cj, ci, t * ci)[0][1] - dycore.tile_extent(jx, iy, cj, ci, t * ci)[0][0] + 1
+              for t in range(cj)]
+    assert widths == [33, 32, 32]
+
+
+def test_create_without_gpu_fails_loudly():
+    """On a host without a GPU the engine refuses to start (no silent CPU fallback)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    from regcm_amd.config import CONFIGS
+    from regcm_amd import icbc
+    rc = CONFIGS["C1"]
+    data = icbc.generate(rc)
+    with pytest.raises(dycore.EngineError):
+        dycore.DynCore(rc, data["split"])

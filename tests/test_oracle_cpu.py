@@ -1,0 +1,152 @@
+"""CPU tests: synthetic inputs, host-side init, the oracle restatement against the committed
+fixtures, and oracle invariants.  No GPU needed."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from regcm_amd.config import CONFIGS, STATE_FIELDS, set_nproc
+from regcm_amd import icbc
+from regcm_amd.vmodes import vmodes, spinit_constants
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "c1_oracle.json")
+
+
+def _fp_match(arr, fp):
+    flat = np.ascontiguousarray(arr).ravel()
+    assert list(arr.shape) == fp["shape"]
+    got = [float(flat[i]).hex() for i in fp["samples_idx"]]
+    assert got == fp["samples"]
+    assert float(np.sum(flat)) == fp["sum"]
+    assert float(np.sum(np.abs(flat))) == fp["abssum"]
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def test_syn_icbc_fingerprint(golden, c1_data):
+    rc, data = c1_data
+    for name, fp in golden["inputs"].items():
+        _fp_match(data["state"][name], fp)
+    for key, vals in golden["split"].items():
+        assert [float(x).hex() for x in np.ravel(data["split"][key])] == vals
+
+
+def test_vmodes_structure():
+    """vmodes/spinit invariants (Main/mod_vmodes.F90:358-426, Main/mod_split.F90:86-175)."""
+    for kz in (18, 23, 41):
+        rc = dict(C1=CONFIGS["C1"], C2=CONFIGS["C2"])["C1" if kz == 18 else "C2"]
+        sig = np.array(__import__("regcm_amd.config", fromlist=["SIGMA_TABLES"]).SIGMA_TABLES[kz])
+        vm = vmodes(sig, 5.0, kz)
+        hb = vm["hbar"]
+        assert np.all(hb > 0) and np.all(np.diff(hb) <= 0)
+        z = vm["zmatx"]
+        ds = np.diff(sig)
+        # vnorml: mass-weighted unit columns, largest component positive
+        assert np.allclose(np.sum(ds[:, None] * z * z, axis=0), 1.0, atol=1e-12)
+        assert np.all(z[np.argmax(np.abs(z), axis=0), np.arange(kz)] > 0)
+        assert np.allclose(vm["zmatxr"] @ z, np.eye(kz), atol=1e-9)
+        # tau z = z diag(hbar)
+        assert np.allclose(vm["tau"] @ z, z * hb[None, :], rtol=1e-8, atol=1e-6 * hb[0])
+    sp = spinit_constants(CONFIGS["C3"].sigma, 5.0, 23, 150.0, 2)
+    assert list(sp["aam"]) == [4.0, 2.0]                     # m2 = 8 and 4 sub-steps
+    assert list(sp["dtau"]) == [37.5, 75.0]
+
+
+def test_set_nproc_rule():
+    """set_nproc, Main/mpplib/mod_mppparam.F90:1152-1186."""
+    assert set_nproc(1, 192, 192) == (1, 1)
+    assert set_nproc(2, 192, 192) == (2, 1)
+    assert set_nproc(4, 192, 192) == (2, 2)
+    assert set_nproc(8, 192, 192) == (2, 4)
+    assert set_nproc(8, 400, 100) == (4, 2)
+    assert set_nproc(6, 60, 200) == (1, 6)
+
+
+def test_oracle_matches_golden(golden, c1_data):
+    from oracle.oracle import OracleCore
+    rc, data = c1_data
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    done = 0
+    for n in (1, 10, 40):
+        o.step(n - done)
+        done = n
+        ref = golden["steps"][str(n)]
+        for name in STATE_FIELDS:
+            _fp_match(o.get(name), ref[name])
+        assert list(o.get_time()) == ref["_time"]
+        assert [float(x).hex() for x in o.diagnostics()[:2]] == ref["_diag"]
+
+
+def test_oracle_leapfrog_schedule(c1_data):
+    """First two steps use dt = dtsec, then 2*dtsec (Main/mod_tendency.F90:608-616);
+    xbctime advances by dtsec per bdyval (Main/mod_bdycod.F90:2566)."""
+    from oracle.oracle import OracleCore
+    rc, data = c1_data
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    assert o.get_time() == (0, rc.dt, rc.dt)
+    o.step(1)
+    assert o.get_time() == (1, rc.dt, 2 * rc.dt)
+    o.step(1)
+    assert o.get_time() == (2, 2 * rc.dt, 3 * rc.dt)
+
+
+def test_oracle_stability_and_mass(c1_data):
+    """100 steps of the restatement stay finite and bounded; boundary-forced p* stays in range."""
+    from oracle.oracle import OracleCore
+    rc, data = c1_data
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    o.step(100)
+    psa = o.get("PSA")[0, : rc.iy - 1, : rc.jx - 1]
+    assert np.all(np.isfinite(psa)) and psa.min() > 50.0 and psa.max() < 110.0
+    t = o.get("ATM1_T")[:, : rc.iy - 1, : rc.jx - 1] / psa[None]
+    assert t.min() > 150.0 and t.max() < 340.0
+    qv = o.get("ATM1_QV")[:, 1: rc.iy - 2, 1: rc.jx - 2]
+    assert qv.min() >= 0.0
+
+
+def test_oracle_zero_state_fixed_point():
+    """A resting, horizontally uniform isothermal atmosphere with matching boundaries and no
+    terrain is a fixed point of advection/diffusion: winds stay zero after a step."""
+    from oracle.oracle import OracleCore
+    rc = CONFIGS["C1"]
+    data = icbc.generate(rc)
+    st = data["state"]
+    kz, iy, jx = rc.kz, rc.iy, rc.jx
+    ps = np.full((1, iy, jx), 95.0)
+    for lvl in ("ATM1", "ATM2"):
+        st[f"{lvl}_U"][:] = 0.0
+        st[f"{lvl}_V"][:] = 0.0
+        st[f"{lvl}_T"][:] = 260.0 * 95.0
+        st[f"{lvl}_QV"][:] = 0.0
+        st[f"{lvl}_QC"][:] = 0.0
+    for n in ("XUB", "XVB", "XQB"):
+        st[n + "_B0"][:] = 0.0
+        st[n + "_BT"][:] = 0.0
+    st["XTB_B0"][:] = 260.0 * 95.0
+    st["XTB_BT"][:] = 0.0
+    st["XPSB_B0"][:] = 95.0
+    st["XPSB_BT"][:] = 0.0
+    st["PSA"][:] = ps
+    st["PSB"][:] = ps
+    st["HT"][:] = 0.0
+    st["CORIOL"][:] = 0.0
+    st["MSFX"][:] = 1.0
+    st["MSFD"][:] = 1.0
+    st["DSTOR"], st["HSTOR"] = icbc.spinit_storage(rc, data["split"], st)
+    o = OracleCore(rc, data["split"])
+    o.put_state(st)
+    o.bdyval()
+    o.step(2)
+    u = o.get("ATM1_U")
+    assert np.max(np.abs(u)) < 1e-9
