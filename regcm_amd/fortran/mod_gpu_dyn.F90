@@ -1,0 +1,169 @@
+!
+! mod_gpu_dyn -- Fortran 2003 ISO_C_BINDING shim over the rcmdyn C-ABI (include/rcmdyn.h).
+!
+! This is the module a RegCM 4.7 host links to run the dynamical-core step on MI355X
+! instead of `call tend` / `call bdyval` (Main/mod_regcm_interface.F90:189,208).  Arrays are
+! passed with their Fortran bounds exactly as getmem* allocated them (j fastest), so the
+! host keeps its own layout and never sees device memory.  See INTEGRATION.md.
+!
+module mod_gpu_dyn
+  use iso_c_binding
+  implicit none
+  private
+
+  integer, parameter, public :: rcmdyn_abi_version = 1
+  integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
+
+  ! field ids (enum rcmdyn_field)
+  integer(c_int32_t), parameter, public :: &
+    f_atm1_u = 0, f_atm1_v = 1, f_atm1_t = 2, f_atm1_qv = 3, f_atm1_qc = 4, &
+    f_atm2_u = 5, f_atm2_v = 6, f_atm2_t = 7, f_atm2_qv = 8, f_atm2_qc = 9, &
+    f_psa = 10, f_psb = 11, f_dstor = 12, f_hstor = 13, &
+    f_msfx = 14, f_msfd = 15, f_coriol = 16, f_ht = 17, &
+    f_xub_b0 = 18, f_xub_bt = 19, f_xvb_b0 = 20, f_xvb_bt = 21, f_xtb_b0 = 22, &
+    f_xtb_bt = 23, f_xqb_b0 = 24, f_xqb_bt = 25, f_xpsb_b0 = 26, f_xpsb_bt = 27, &
+    f_psc = 28, f_pten = 29, f_psdota = 30, f_tten = 31, f_uten = 32, f_vten = 33, &
+    f_qvten = 34, f_qcten = 35, f_omega = 36, f_qdot = 37, f_xkc = 38, f_phi = 39
+
+  type, bind(c), public :: rcmdyn_config
+    integer(c_int32_t) :: abi_version
+    integer(c_int32_t) :: jx, iy, kz
+    integer(c_int32_t) :: nproc_j, nproc_i
+    integer(c_int32_t) :: tile_first, tile_count
+    integer(c_int32_t) :: idynamic, iboudy, idiffu, ipgf, nsplit, nspgx, nspgd
+    integer(c_int32_t) :: diffu_hgtf, upstream_mode, stability_enhance, present_qc
+    real(c_double) :: ds, dtsec, ptop, gnu1, gnu2, uoffc, t_extrema, q_rel_extrema
+    real(c_double) :: ckh, adyndif, high_nudge, medium_nudge, low_nudge
+    real(c_double) :: bdy_nm, bdy_dm, dtbdys
+    real(c_double) :: sigma(rcmdyn_maxkz+1)
+    real(c_double) :: zmatx(rcmdyn_maxkz,rcmdyn_maxsplit)   ! zmatx(k,l)
+    real(c_double) :: zmatxr(rcmdyn_maxkz,rcmdyn_maxsplit)  ! zmatxr(l,k) stored (k,l)
+    real(c_double) :: am(rcmdyn_maxkz,rcmdyn_maxsplit)      ! am(k,l)
+    real(c_double) :: tau(rcmdyn_maxkz,rcmdyn_maxsplit)     ! tau(l,k) stored (k,l)
+    real(c_double) :: varpa1(rcmdyn_maxkz+1,rcmdyn_maxsplit)! varpa1(l,k) stored (k,l)
+    real(c_double) :: an(rcmdyn_maxsplit), hbar(rcmdyn_maxsplit)
+    real(c_double) :: aam(rcmdyn_maxsplit), dtau(rcmdyn_maxsplit)
+    real(c_double) :: sigmah(rcmdyn_maxkz+1)
+    real(c_double) :: pd
+    integer(c_int32_t) :: comm_rank, comm_size, device
+    integer(c_int8_t) :: comm_unique_id(128)
+  end type rcmdyn_config
+
+  interface
+    integer(c_int) function rcmdyn_create(cfg, h) bind(c, name='rcmdyn_create')
+      import :: c_int, c_ptr, rcmdyn_config
+      type(rcmdyn_config), intent(in) :: cfg
+      type(c_ptr), intent(out) :: h
+    end function
+    integer(c_int) function rcmdyn_destroy(h) bind(c, name='rcmdyn_destroy')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
+    type(c_ptr) function rcmdyn_last_error(h) bind(c, name='rcmdyn_last_error')
+      import :: c_ptr
+      type(c_ptr), value :: h
+    end function
+    integer(c_int) function rcmdyn_put(h, f, src, j1, j2, i1, i2, k1, k2) bind(c, name='rcmdyn_put')
+      import :: c_int, c_ptr, c_int32_t, c_double
+      type(c_ptr), value :: h
+      integer(c_int32_t), value :: f, j1, j2, i1, i2, k1, k2
+      real(c_double), intent(in) :: src(*)
+    end function
+    integer(c_int) function rcmdyn_get(h, f, dst, j1, j2, i1, i2, k1, k2) bind(c, name='rcmdyn_get')
+      import :: c_int, c_ptr, c_int32_t, c_double
+      type(c_ptr), value :: h
+      integer(c_int32_t), value :: f, j1, j2, i1, i2, k1, k2
+      real(c_double), intent(out) :: dst(*)
+    end function
+    integer(c_int) function rcmdyn_set_time(h, lcount, dt, xbctime) bind(c, name='rcmdyn_set_time')
+      import :: c_int, c_ptr, c_int64_t, c_double
+      type(c_ptr), value :: h
+      integer(c_int64_t), value :: lcount
+      real(c_double), value :: dt, xbctime
+    end function
+    integer(c_int) function rcmdyn_get_time(h, lcount, dt, xbctime) bind(c, name='rcmdyn_get_time')
+      import :: c_int, c_ptr, c_int64_t, c_double
+      type(c_ptr), value :: h
+      integer(c_int64_t), intent(out) :: lcount
+      real(c_double), intent(out) :: dt, xbctime
+    end function
+    integer(c_int) function rcmdyn_tend(h) bind(c, name='rcmdyn_tend')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
+    integer(c_int) function rcmdyn_bdyval(h) bind(c, name='rcmdyn_bdyval')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
+    integer(c_int) function rcmdyn_step(h, n) bind(c, name='rcmdyn_step')
+      import :: c_int, c_ptr, c_int32_t
+      type(c_ptr), value :: h
+      integer(c_int32_t), value :: n
+    end function
+    integer(c_int) function rcmdyn_diagnostics(h, out) bind(c, name='rcmdyn_diagnostics')
+      import :: c_int, c_ptr, c_double
+      type(c_ptr), value :: h
+      real(c_double), intent(out) :: out(4)
+    end function
+    integer(c_int) function rcmdyn_comm_unique_id(out) bind(c, name='rcmdyn_comm_unique_id')
+      import :: c_int, c_int8_t
+      integer(c_int8_t), intent(out) :: out(128)
+    end function
+  end interface
+
+  public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
+  public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics
+  public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d
+
+  contains
+
+  ! Abort like the reference's fatal() (Share/mod_message.F90:90-103) on any engine error.
+  subroutine gpu_dyn_check(h, ierr, where)
+    type(c_ptr), intent(in) :: h
+    integer(c_int), intent(in) :: ierr
+    character(len=*), intent(in) :: where
+    character(kind=c_char), pointer :: msg(:)
+    integer :: n
+    if ( ierr == 0 ) return
+    call c_f_pointer(rcmdyn_last_error(h), msg, [1024])
+    n = 0
+    do while ( n < 1024 )
+      if ( msg(n+1) == c_null_char ) exit
+      n = n + 1
+    end do
+    write(0,*) 'mod_gpu_dyn: ', where, ': ', msg(1:n)
+    error stop 1
+  end subroutine gpu_dyn_check
+
+  ! Put/get a pointer array allocated as a(j1:j2,i1:i2,k1:k2) by getmem3d: pointer
+  ! dummies keep the host's lower bounds, which the C-ABI takes as global indices.
+  subroutine gpu_put3d(h, f, a)
+    type(c_ptr), intent(in) :: h
+    integer(c_int32_t), intent(in) :: f
+    real(c_double), pointer, contiguous, intent(in) :: a(:,:,:)
+    call gpu_dyn_check(h, rcmdyn_put(h, f, a, lbound(a,1), ubound(a,1), lbound(a,2), &
+         ubound(a,2), lbound(a,3), ubound(a,3)), 'put3d')
+  end subroutine gpu_put3d
+  subroutine gpu_get3d(h, f, a)
+    type(c_ptr), intent(in) :: h
+    integer(c_int32_t), intent(in) :: f
+    real(c_double), pointer, contiguous, intent(in) :: a(:,:,:)
+    call gpu_dyn_check(h, rcmdyn_get(h, f, a, lbound(a,1), ubound(a,1), lbound(a,2), &
+         ubound(a,2), lbound(a,3), ubound(a,3)), 'get3d')
+  end subroutine gpu_get3d
+  subroutine gpu_put2d(h, f, a)
+    type(c_ptr), intent(in) :: h
+    integer(c_int32_t), intent(in) :: f
+    real(c_double), pointer, contiguous, intent(in) :: a(:,:)
+    call gpu_dyn_check(h, rcmdyn_put(h, f, a, lbound(a,1), ubound(a,1), lbound(a,2), &
+         ubound(a,2), 1, 1), 'put2d')
+  end subroutine gpu_put2d
+  subroutine gpu_get2d(h, f, a)
+    type(c_ptr), intent(in) :: h
+    integer(c_int32_t), intent(in) :: f
+    real(c_double), pointer, contiguous, intent(in) :: a(:,:)
+    call gpu_dyn_check(h, rcmdyn_get(h, f, a, lbound(a,1), ubound(a,1), lbound(a,2), &
+         ubound(a,2), 1, 1), 'get2d')
+  end subroutine gpu_get2d
+
+end module mod_gpu_dyn
