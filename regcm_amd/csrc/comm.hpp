@@ -1,25 +1,32 @@
 // comm.hpp -- inter-process halo transport over RCCL (xGMI) for the engine.
 //
 // Replaces the MPI point-to-point halo of mpplib (`exchange`, `exchange_lb`, `exchange_rt`,
-// `exchange_bdy_lr/_bt`, Main/mpplib/mod_mppparam.F90:6065-13190): every exchange packs the
-// owned edge boxes of a field with one kernel, moves them with one grouped ncclSend/ncclRecv
-// per neighbour (each neighbour sits on its own xGMI link) and unpacks into the ghost ring.
+// `exchange_bdy_lr/_bt`, Main/mpplib/mod_mppparam.F90:6065-13190).  The engine packs the
+// owned edge boxes of all fields of one exchange point into one staging buffer per
+// neighbour (k_pack_segs) and calls sendrecv(): one grouped ncclSend/ncclRecv per neighbour,
+// each neighbour on its own xGMI link; tiles on the same device use device copies instead
+// of this class with the identical staging layout.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/rcmdyn.h"
-#include "engine.hpp"
 
 namespace rcm {
+
+struct Xfer {
+  int peer;          // rank (= tile index)
+  double* ptr;       // device staging pointer
+  size_t count;      // doubles
+};
 
 class Comm {
  public:
   virtual ~Comm() = default;
-  // sides: 0 all 8 neighbours, 1 receive left/bottom(+corner), 2 receive right/top(+corner)
-  virtual void exchange(const Tile& t, double* field, int nk, int width, int sides) = 0;
-  virtual void exchange_slices(const Tile& t, double* const* sl, long slen, int kz) = 0;
+  virtual void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) = 0;
   virtual bool graph_safe() const = 0;
 };
 

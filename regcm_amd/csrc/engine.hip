@@ -167,6 +167,7 @@ struct rcmdyn_engine {
   bool bdy_dirty = true;
   bool capturing = false;
   long slen = 0;
+  long staging_cap = 0;
   double last_ms = 0.0;
   std::string err;
   std::unique_ptr<Comm> comm;
@@ -291,6 +292,10 @@ struct rcmdyn_engine {
     t.qvten = dalloc(t, P3); t.qcten = dalloc(t, P3); t.omega = dalloc(t, P3); t.xkcs = dalloc(t, P3);
     slen = std::max<long>(g.pitch, g.ni);
     for (int s = 0; s < 16; s++) t.sl[s] = dalloc(t, (size_t)slen * kz);
+    // halo staging: 8 directions x widest exchange (6 fields x width 2 x (kz+1) levels)
+    staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 2 * (kz + 1) * 8);
+    t.sbuf = dalloc(t, staging_cap);
+    t.rbuf = dalloc(t, staging_cap);
     dim3 gr = grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1);
     t.nred = gr.x * gr.y;
     t.red = dalloc(t, 2 * (size_t)t.nred + 2);
@@ -453,67 +458,170 @@ struct rcmdyn_engine {
   }
 
   // ------------------------------------------------------------------ halo exchange
-  // exchange / exchange_lb / exchange_rt (sides 0 / 1 / 2), Main/mpplib/mod_mppparam.F90
-  void xch(FK f, int nk, int width, int sides) {
-    if (ntiles == 1) return;
-    for (auto& t : tiles) {
-      NbrTable nt{};
-      for (int d = 0; d < 9; d++) nt.base[d] = nullptr;
-      const int dj9[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, di9[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
-      for (int d = 0; d < 9; d++) {
-        if (d == 4) continue;
-        int lj = t.lj + dj9[d], li = t.li + di9[d];
-        if (lj < 0 || lj >= cfg.nproc_j || li < 0 || li >= cfg.nproc_i) continue;
-        int idx = lj * cfg.nproc_i + li;
-        Tile* nb = local_tile(idx);
-        if (!nb) continue;                       // remote: handled by the RCCL transport
-        nt.base[d] = fptr(*nb, f);
-        nt.j0[d] = nb->g.j0; nt.i0[d] = nb->g.i0; nt.pitch[d] = nb->g.pitch; nt.plane[d] = nb->g.plane;
-      }
-      hipLaunchKernelGGL(k_ghost_fill, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fptr(t, f), nk, width,
-                         sides, nt);
-    }
-    if (comm) comm->exchange(*this->tiles.data(), fptr(tiles[0], f), nk, width, sides);
+  // Every exchange stages the owned edge boxes of its fields per neighbour direction
+  // (0 L, 1 R, 2 B, 3 T, 4 BL, 5 BR, 6 TL, 7 TR) with k_pack_segs, moves each direction's
+  // contiguous span to the peer (device copy for a tile on this GPU, RCCL for a remote one)
+  // and unpacks the ghost boxes.  sides: 0 exchange, 1 exchange_lb, 2 exchange_rt.
+  static constexpr int DJ[8] = {-1, 1, 0, 0, -1, 1, -1, 1};
+  static constexpr int DI[8] = {0, 0, -1, 1, -1, -1, 1, 1};
+  static constexpr int OPP[8] = {1, 0, 3, 2, 7, 6, 5, 4};
+  static bool recv_dir(int sides, int d) {
+    if (sides == 0) return true;
+    if (sides == 1) return d == 0 || d == 2 || d == 4;
+    return d == 1 || d == 3 || d == 7;
   }
-
+  int peer_of(const Tile& t, int d) const {
+    const int lj = t.lj + DJ[d], li = t.li + DI[d];
+    return (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
+  }
   Tile* local_tile(int idx) {
     int o = idx - cfg.tile_first;
     return (o >= 0 && o < (int)tiles.size()) ? &tiles[o] : nullptr;
   }
+  struct XField { FK f; int nk; };
+  // (j1,j2,i1,i2) of the box sent toward d (send) or received from d (recv)
+  static void box(const Geom& g, int d, int w, bool send, int b[4]) {
+    b[0] = g.jde1; b[1] = g.jde2; b[2] = g.ide1; b[3] = g.ide2;
+    if (send) {
+      if (DJ[d] < 0) b[1] = g.jde1 + w - 1;
+      if (DJ[d] > 0) b[0] = g.jde2 - w + 1;
+      if (DI[d] < 0) b[3] = g.ide1 + w - 1;
+      if (DI[d] > 0) b[2] = g.ide2 - w + 1;
+    } else {
+      if (DJ[d] < 0) { b[0] = g.jde1 - w; b[1] = g.jde1 - 1; }
+      if (DJ[d] > 0) { b[0] = g.jde2 + 1; b[1] = g.jde2 + w; }
+      if (DI[d] < 0) { b[2] = g.ide1 - w; b[3] = g.ide1 - 1; }
+      if (DI[d] > 0) { b[2] = g.ide2 + 1; b[3] = g.ide2 + w; }
+    }
+  }
+  // segment builder: appends the segments of direction d (send or recv) for tile t
+  using SegFn = std::function<void(Tile&, int, bool, std::vector<Seg>&)>;
+  struct Layout {
+    std::vector<Seg> segs;
+    long start[8], count[8];
+  };
+  Layout layout(Tile& t, const SegFn& fn, bool send, const std::function<bool(int)>& dir_on) {
+    Layout L;
+    long off = 0;
+    for (int d = 0; d < 8; d++) {
+      L.start[d] = off; L.count[d] = 0;
+      if (peer_of(t, d) < 0 || !dir_on(d)) continue;
+      std::vector<Seg> v;
+      fn(t, d, send, v);
+      for (Seg& s : v) {
+        s.off = off;
+        off += (long)(s.j2 - s.j1 + 1) * (s.i2 - s.i1 + 1) * s.nk;
+        L.segs.push_back(s);
+      }
+      L.count[d] = off - L.start[d];
+    }
+    if (off > staging_cap) throw std::runtime_error("rcmdyn: halo staging buffer too small");
+    return L;
+  }
+  void launch_segs(const std::vector<Seg>& segs, double* buf, int unpack) {
+    for (size_t a = 0; a < segs.size(); a += MAXSEG) {
+      SegList L{};
+      L.n = (int)std::min<size_t>(MAXSEG, segs.size() - a);
+      for (int q = 0; q < L.n; q++) L.s[q] = segs[a + q];
+      hipLaunchKernelGGL(k_pack_segs, dim3(32, L.n), dim3(256), 0, stream, L, buf, unpack);
+    }
+  }
+  void exchange_generic(const SegFn& fn, const std::function<bool(int)>& send_on,
+                        const std::function<bool(int)>& recv_on) {
+    if (ntiles == 1) return;
+    std::vector<Layout> S, R;
+    for (auto& t : tiles) {
+      S.push_back(layout(t, fn, true, send_on));
+      R.push_back(layout(t, fn, false, recv_on));
+    }
+    for (size_t q = 0; q < tiles.size(); q++) launch_segs(S[q].segs, tiles[q].sbuf, 0);
+    std::vector<Xfer> sends, recvs;
+    for (size_t q = 0; q < tiles.size(); q++) {
+      Tile& t = tiles[q];
+      for (int d = 0; d < 8; d++) {
+        const int p = peer_of(t, d);
+        if (p < 0) continue;
+        Tile* pt = local_tile(p);
+        if (S[q].count[d]) {
+          if (pt) {
+            const size_t pq = pt - tiles.data();
+            if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
+            HIPCHK(hipMemcpyAsync(pt->rbuf + R[pq].start[OPP[d]], t.sbuf + S[q].start[d],
+                                  S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
+          } else {
+            sends.push_back({p, t.sbuf + S[q].start[d], (size_t)S[q].count[d]});
+          }
+        }
+        if (R[q].count[d] && !pt) recvs.push_back({p, t.rbuf + R[q].start[d], (size_t)R[q].count[d]});
+      }
+    }
+    if (!sends.empty() || !recvs.empty()) {
+      if (!comm) throw std::runtime_error("rcmdyn: remote neighbour without a communicator");
+      comm->sendrecv(sends, recvs);
+    }
+    for (size_t q = 0; q < tiles.size(); q++) launch_segs(R[q].segs, tiles[q].rbuf, 1);
+  }
 
-  // exchange_bdy_lr / exchange_bdy_bt of the bdyuv slices (Main/mod_bdycod.F90:1063-1089)
+  Seg field_seg(Tile& t, double* p, int nk, int d, int w, bool send) {
+    int b[4];
+    box(t.g, d, w, send, b);
+    Seg s{};
+    s.p = p; s.kstride = t.g.plane; s.pitch = t.g.pitch; s.j0 = t.g.j0; s.i0 = t.g.i0;
+    s.j1 = b[0]; s.j2 = b[1]; s.i1 = b[2]; s.i2 = b[3]; s.nk = nk;
+    return s;
+  }
+
+  // exchange / exchange_lb / exchange_rt of several fields at once
+  void xch(std::initializer_list<XField> fields, int width, int sides) {
+    if (ntiles == 1) return;
+    std::vector<XField> fs(fields);
+    auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
+      for (const XField& x : fs) v.push_back(field_seg(t, fptr(t, x.f), x.nk, d, width, send));
+    };
+    exchange_generic(fn, [&](int d) { return recv_dir(sides, OPP[d]); }, [&](int d) { return recv_dir(sides, d); });
+  }
+  void xch(FK f, int nk, int width, int sides) { xch({XField{f, nk}}, width, sides); }
+
+  // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
+  void xch_delh_slot(int l, int src) {
+    if (ntiles == 1) return;
+    const long off = ((long)(src - 1) * cfg.nsplit + (l - 1));
+    auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
+      v.push_back(field_seg(t, t.delh + off * t.g.plane, 1, d, 1, send));
+    };
+    exchange_generic(fn, [&](int d) { return recv_dir(1, OPP[d]); }, [&](int d) { return recv_dir(1, d); });
+  }
+
+  // exchange_bdy_lr / exchange_bdy_bt of the bdyuv slices (Main/mod_bdycod.F90:1063-1089):
+  // south/north slices (by j) with the left/right tiles, west/east slices (by i) with the
+  // bottom/top tiles; width 1, every level.
   void xch_slices() {
     if (ntiles == 1) return;
     const int kz = cfg.kz;
-    for (auto& t : tiles) {
+    auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
       const Geom& g = t.g;
-      auto fill = [&](int s, int along) {
-        // along 0: j-indexed slices (south/north) exchanged with left/right tiles
-        // along 1: i-indexed slices (west/east) exchanged with bottom/top tiles
-        for (int side = 0; side < 2; side++) {
-          int nbidx = along == 0 ? t.nbr[side == 0 ? 0 : 1] : t.nbr[side == 0 ? 2 : 3];
-          if (nbidx < 0) continue;
-          Tile* nb = local_tile(nbidx);
-          if (!nb) continue;
-          const Geom& h = nb->g;
-          int dst_idx, src_idx;
-          if (along == 0) {
-            int jdst = side == 0 ? g.jde1 - 1 : g.jde2 + 1;
-            dst_idx = jdst - g.j0; src_idx = jdst - h.j0;
-          } else {
-            int idst = side == 0 ? g.ide1 - 1 : g.ide2 + 1;
-            dst_idx = idst - g.i0; src_idx = idst - h.i0;
-          }
-          hipLaunchKernelGGL(k_slice_fill, dim3(1), dim3(64), 0, stream, t.sl[s], nb->sl[s], dst_idx, src_idx,
-                             slen, slen, kz);
-        }
-      };
-      if (g.bt) for (int s : {10, 11, 14, 15}) fill(s, 0);
-      if (g.bb) for (int s : {8, 9, 12, 13}) fill(s, 0);
-      if (g.bl) for (int s : {0, 1, 4, 5}) fill(s, 1);
-      if (g.br) for (int s : {2, 3, 6, 7}) fill(s, 1);
-    }
-    if (comm) comm->exchange_slices(tiles[0], tiles[0].sl, slen, kz);
+      std::vector<int> ids;
+      int lo, hi, origin;
+      if (d == 0 || d == 1) {
+        if (g.bt) ids.insert(ids.end(), {10, 11, 14, 15});
+        if (g.bb) ids.insert(ids.end(), {8, 9, 12, 13});
+        lo = g.jde1; hi = g.jde2; origin = g.j0;
+      } else {
+        if (g.bl) ids.insert(ids.end(), {0, 1, 4, 5});
+        if (g.br) ids.insert(ids.end(), {2, 3, 6, 7});
+        lo = g.ide1; hi = g.ide2; origin = g.i0;
+      }
+      const bool low = (d == 0 || d == 2);
+      const int x = send ? (low ? lo : hi) : (low ? lo - 1 : hi + 1);
+      for (int s : ids) {
+        Seg sg{};
+        sg.p = t.sl[s]; sg.kstride = slen; sg.pitch = 0; sg.j0 = origin; sg.i0 = 0;
+        sg.j1 = x; sg.j2 = x; sg.i1 = 0; sg.i2 = 0; sg.nk = kz;
+        v.push_back(sg);
+      }
+    };
+    auto on = [&](int d) { return d < 4; };
+    exchange_generic(fn, on, on);
   }
 
   // ------------------------------------------------------------------ the step
@@ -522,7 +630,7 @@ struct rcmdyn_engine {
 
   void prepare() {
     if (statics_dirty) {
-      xch(FK::MSFX, 1, 2, 0); xch(FK::MSFD, 1, 2, 0); xch(FK::HT, 1, 2, 0); xch(FK::CORIOL, 1, 2, 0);
+      xch({{FK::MSFX, 1}, {FK::MSFD, 1}, {FK::HT, 1}, {FK::CORIOL, 1}}, 2, 0);
       each([&](Tile& t) {
         hipLaunchKernelGGL(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
                            t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
@@ -532,8 +640,8 @@ struct rcmdyn_engine {
     }
     if (bdy_dirty) {
       const int kz = cfg.kz;
-      for (FK f : {FK::UB0, FK::UBT, FK::VB0, FK::VBT, FK::TB0, FK::TBT, FK::QB0, FK::QBT}) xch(f, kz, 1, 0);
-      xch(FK::PB0, 1, 1, 0); xch(FK::PBT, 1, 1, 0);
+      xch({{FK::UB0, kz}, {FK::UBT, kz}, {FK::VB0, kz}, {FK::VBT, kz}}, 1, 0);
+      xch({{FK::TB0, kz}, {FK::TBT, kz}, {FK::QB0, kz}, {FK::QBT, kz}, {FK::PB0, 1}, {FK::PBT, 1}}, 1, 0);
       bdy_dirty = false;
       invalidate_graphs();
     }
@@ -542,22 +650,23 @@ struct rcmdyn_engine {
   void tend() {
     const int kz = cfg.kz, ns = cfg.nsplit;
     // surface_pressures, Main/mod_tendency.F90:815-834
-    xch(FK::PSA, 1, 1, 0); xch(FK::PSB, 1, 2, 0);
+    xch(FK::PSA, 1, 1, 0);
+    xch(FK::PSB, 1, 2, 0);
     each([&](Tile& t) {
       hipLaunchKernelGGL(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, t.psa, t.psb, t.rpsa,
                          t.rpsb, t.psdota, t.psdotb);
     });
     xch(FK::PSDOTA, 1, 1, 0); xch(FK::PSDOTB, 1, 2, 0);
     // decouple, :852-1116
-    for (FK f : {FK::A1U, FK::A1V, FK::A1T, FK::A1QV, FK::A1QC}) xch(f, kz, 1, 0);
+    xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz}, {FK::A1QC, kz}}, 1, 0);
     each([&](Tile& t) {
       const int c = t.cur;
       hipLaunchKernelGGL(k_decouple, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, t.a1u[c], t.a1v[c], t.a1t[c],
                          t.a1qv[c], t.a1qc[c], t.msfd, t.psdota, t.rpsa, t.rpsda, t.umc, t.vmc, t.ud, t.vd, t.xt,
                          t.xqv, t.xqc, t.xtv, hc.ep1);
     });
-    xch(FK::UD, kz, 1, 0); xch(FK::VD, kz, 1, 0);
-    for (FK f : {FK::A2U, FK::A2V, FK::A2T, FK::A2QV, FK::A2QC}) xch(f, kz, 2, 0);
+    xch({{FK::UD, kz}, {FK::VD, kz}}, 1, 0);
+    xch({{FK::A2U, kz}, {FK::A2V, kz}, {FK::A2T, kz}, {FK::A2QV, kz}, {FK::A2QC, kz}}, 2, 0);
     // compute_omega column part, :1118-1156
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -610,7 +719,7 @@ struct rcmdyn_engine {
                          t.xmsf, t.qdot, t.qb0, t.qbt, t.rgcr, t.ibcr, t.xkc, t.qvb, t.qcb, t.cqv, t.cqc, t.qvten,
                          t.qcten);
     });
-    xch(FK::CQV, kz, 1, 0); xch(FK::CQC, kz, 1, 0);
+    xch({{FK::CQV, kz}, {FK::CQC, kz}}, 1, 0);
     each([&](Tile& t) {
       const Geom& g = t.g;
       hipLaunchKernelGGL(k_ps_filter, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, 1), BLK, 0, stream, g, dc,
@@ -632,18 +741,32 @@ struct rcmdyn_engine {
       hipLaunchKernelGGL(k_psc2psd, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, t.psa,
                          t.psdota);
     });
-    for (FK f : {FK::A1U, FK::A1V, FK::A2U, FK::A2V}) xch(f, kz, 1, 2);
+    xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A2U, kz}, {FK::A2V, kz}}, 1, 2);
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur;
       hipLaunchKernelGGL(k_split_project, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
                          dc, t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa, t.psb, t.msfd,
                          t.mapf, t.dstor, t.hstor, t.deld, t.delh);
-      hipLaunchKernelGGL(k_spstep_init, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc,
-                         t.deld, t.delh, t.ddsum, t.dhsum);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
-    for (int l = 1; l <= ns; l++) {
+    bool fused = (ntiles == 1);
+    for (int l = 1; l <= ns; l++) fused = fused && ((int)hc.aam[l - 1] * 2 <= SPH);
+    if (fused) {
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        dim3 gr((g.jce2 - g.jce1 + SPB) / SPB, (g.ice2 - g.ice1 + SPB) / SPB, ns);
+        hipLaunchKernelGGL(k_spstep_fused, gr, dim3(32, 8), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
+                           t.psdota, t.mapf, t.psa, t.ddsum, t.dhsum);
+      });
+    } else {
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        hipLaunchKernelGGL(k_spstep_init, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
+                           dc, t.deld, t.delh, t.ddsum, t.dhsum);
+      });
+    }
+    for (int l = 1; l <= ns && !fused; l++) {
       int n0 = 1, n1 = 2, n2 = n0;
       const int m2 = (int)hc.aam[l - 1] * 2;
       sp_substep(l, n0, n0, n0, n1, 0);
@@ -673,35 +796,12 @@ struct rcmdyn_engine {
       hipLaunchKernelGGL(k_spstep_grad, grid3(g.jdi2 - g.jdi1 + 1, g.idi2 - g.idi1 + 1, 1), BLK, 0, stream, g, dc, l,
                          src, t.delh, t.msfx, t.msfd, t.psdota, t.uu, t.vv);
     });
-    xch(FK::UU, 1, 1, 2); xch(FK::VV, 1, 1, 2);
+    xch({{FK::UU, 1}, {FK::VV, 1}}, 1, 2);
     each([&](Tile& t) {
       const Geom& g = t.g;
       hipLaunchKernelGGL(k_spstep_update, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
                          l, n0, n1, nn, leap, t.uu, t.vv, t.mapf, t.psa, t.deld, t.delh, t.ddsum, t.dhsum);
     });
-  }
-
-  // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
-  void xch_delh_slot(int l, int src) {
-    if (ntiles == 1) return;
-    const long off = ((long)(src - 1) * cfg.nsplit + (l - 1));
-    for (auto& t : tiles) {
-      NbrTable nt{};
-      const int dj9[9] = {-1, 0, 1, -1, 0, 1, -1, 0, 1}, di9[9] = {-1, -1, -1, 0, 0, 0, 1, 1, 1};
-      for (int d = 0; d < 9; d++) {
-        nt.base[d] = nullptr;
-        if (d == 4) continue;
-        int lj = t.lj + dj9[d], li = t.li + di9[d];
-        if (lj < 0 || lj >= cfg.nproc_j || li < 0 || li >= cfg.nproc_i) continue;
-        Tile* nb = local_tile(lj * cfg.nproc_i + li);
-        if (!nb) continue;
-        nt.base[d] = nb->delh + off * nb->g.plane;
-        nt.j0[d] = nb->g.j0; nt.i0[d] = nb->g.i0; nt.pitch[d] = nb->g.pitch; nt.plane[d] = nb->g.plane;
-      }
-      hipLaunchKernelGGL(k_ghost_fill, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, t.delh + off * t.g.plane, 1,
-                         1, 1, nt);
-    }
-    if (comm) comm->exchange(tiles[0], tiles[0].delh + off * tiles[0].g.plane, 1, 1, 1);
   }
 
   void bdyval() {

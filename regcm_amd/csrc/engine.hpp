@@ -93,6 +93,8 @@ struct Tile {
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // boundary slices (Main/mod_bdycod.F90:58-61): [k][frame index]
   double *sl[16];
+  // halo staging buffers
+  double *sbuf = nullptr, *rbuf = nullptr;
   // reduction partials
   double *red;
   int nred;

@@ -34,7 +34,8 @@ __device__ __forceinline__ bool in(int v, int lo, int hi) { return v >= lo && v 
 #define THREAD_POINT(j1, i1)                                   \
   const int j = (j1) + (int)(blockIdx.x * blockDim.x + threadIdx.x); \
   const int i = (i1) + (int)(blockIdx.y * blockDim.y + threadIdx.y); \
-  const int k = (int)blockIdx.z + 1;
+  const int k = (int)blockIdx.z + 1;                              \
+  (void)k;
 
 // psc2psd at one dot point, Main/mpplib/mod_mppparam.F90:13811-13862.
 __device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int j, int i, double& v) {
@@ -871,6 +872,116 @@ __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int
   dhsum[(long)(l - 1) * g.plane + q] = dhsum[(long)(l - 1) * g.plane + q] + HN[q];
 }
 
+// spstep fused, single-tile: every sub-step of one vertical mode in one launch (blockIdx.z =
+// mode).  A workgroup owns SPB x SPB cross points plus a SPH-point halo held in LDS; each
+// sub-step couples delh only within radius 1, so after m2 <= SPH sub-steps the owned block is
+// exact (halo values are recomputed redundantly and the contaminated rim never reaches it).
+// Per point the operations are those of k_spstep_grad/k_spstep_update, so results are
+// bit-identical to the two-kernel-per-substep path (Main/mod_split.F90:463-669).
+constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;
+__global__ __launch_bounds__(256) void k_spstep_fused(
+    Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
+    const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota,
+    const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
+  __shared__ double Ds[2][SPR][SPP], Hs[2][SPR][SPP], U[SPR][SPP], V[SPR][SPP];
+  const int l = blockIdx.z + 1;
+  const int J1 = g.jce1 + blockIdx.x * SPB, I1 = g.ice1 + blockIdx.y * SPB;
+  const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
+  const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 8
+  const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
+  const int m2 = (int)aam * 2;
+  const double dtau2 = dtau * d_two, rdx2 = d_one / c->dx2;
+  const double* D1 = SLOT(deld, l, 1); const double* D2 = SLOT(deld, l, 2); const double* D3 = SLOT(deld, l, 3);
+  const double* H1 = SLOT(delh, l, 1); const double* H2 = SLOT(delh, l, 2); const double* H3 = SLOT(delh, l, 3);
+  // per-thread points: (tx, ty + 8 r), r = 0..3
+  double d3[4], h3[4], ps[4], mf[4], ufac[4], msd[4], sd[4], sh[4];
+  bool ce[4], ci[4], bnd[4], di[4], own[4];
+  for (int r = 0; r < 4; r++) {
+    const int lj = tx, li = ty + 8 * r, j = jr0 + lj, i = ir0 + li;
+    ce[r] = in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
+    ci[r] = in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+    di[r] = in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2);
+    bnd[r] = ce[r] && !ci[r] &&
+             ((g.bl && j == g.jce1 && in(i, g.ici1, g.ici2)) || (g.br && j == g.jce2 && in(i, g.ici1, g.ici2)) ||
+              (g.bb && i == g.ice1) || (g.bt && i == g.ice2));
+    own[r] = in(j, J1, J1 + SPB - 1) && in(i, I1, I1 + SPB - 1);
+    const long q = ce[r] ? g.ix(j, i) : 0;
+    Ds[0][li][lj] = ce[r] ? D1[q] : 0.0; Ds[1][li][lj] = ce[r] ? D2[q] : 0.0;
+    Hs[0][li][lj] = ce[r] ? H1[q] : 0.0; Hs[1][li][lj] = ce[r] ? H2[q] : 0.0;
+    U[li][lj] = 0.0; V[li][lj] = 0.0;
+    d3[r] = ce[r] ? D3[q] : 0.0; h3[r] = ce[r] ? H3[q] : 0.0;
+    ps[r] = ci[r] ? F2(psa, j, i) : 1.0;
+    mf[r] = ci[r] ? F2(mapf, j, i) : 0.0;
+    ufac[r] = di[r] ? c->dx2 * F2(msfx, j, i) : 1.0;
+    msd[r] = di[r] ? F2(msfd, j, i) : 0.0;
+    sd[r] = ce[r] ? Ds[0][li][lj] : 0.0;     // ddsum(ce) = deld(n0)
+    sh[r] = ce[r] ? Hs[0][li][lj] : 0.0;
+  }
+  double pda[4];
+  for (int r = 0; r < 4; r++) {
+    const int j = jr0 + tx, i = ir0 + ty + 8 * r;
+    pda[r] = di[r] ? F2(psdota, j, i) : 0.0;
+  }
+  __syncthreads();
+  int n0 = 0, n1 = 1;                                   // slot indices (reference slots 1, 2)
+  for (int n = 1; n <= m2; n++) {
+    const int src = (n == 1) ? n0 : n1;
+    // gradient of delh(src) at dot points -> (uu, vv)
+    for (int r = 0; r < 4; r++) {
+      const int lj = tx, li = ty + 8 * r;
+      if (di[r] && lj >= 1 && li >= 1) {
+        const double a = Hs[src][li][lj], b = Hs[src][li - 1][lj], cc = Hs[src][li][lj - 1], dd = Hs[src][li - 1][lj - 1];
+        double w1 = (a + b - cc - dd) / ufac[r];
+        double w2 = (a + cc - b - dd) / ufac[r];
+        w1 = w1 * pda[r];
+        w2 = w2 * pda[r];
+        U[li][lj] = w1 * msd[r];
+        V[li][lj] = w2 * msd[r];
+      }
+    }
+    __syncthreads();
+    const int nn = (n == 1) ? n1 : n0;                  // forward writes n1; leapfrog n2 = n0
+    for (int r = 0; r < 4; r++) {
+      const int lj = tx, li = ty + 8 * r;
+      if (ci[r] && lj + 1 < SPR && li + 1 < SPR) {
+        const double w3 = rdx2 * mf[r] *
+            (-U[li + 1][lj] + U[li + 1][lj + 1] - U[li][lj] + U[li][lj + 1] +
+             V[li + 1][lj] + V[li + 1][lj + 1] - V[li][lj] - V[li][lj + 1]);
+        if (n == 1) {
+          const double m2d = (double)m2;
+          const double dn = Ds[n0][li][lj] - dtau * w3 + d3[r] / m2d;
+          const double hn = Hs[n0][li][lj] - dtau * hbar * Ds[n0][li][lj] / ps[r] + h3[r] / m2d;
+          Ds[nn][li][lj] = dn;
+          Hs[nn][li][lj] = hn;
+        } else {
+          const double dn = Ds[n0][li][lj] - dtau2 * w3 + d3[r] / aam;
+          const double hn = Hs[n0][li][lj] - dtau2 * hbar * Ds[n1][li][lj] / ps[r] + h3[r] / aam;
+          Ds[nn][li][lj] = dn;
+          Hs[nn][li][lj] = hn;
+        }
+      } else if (bnd[r]) {
+        if (n == 1) Hs[nn][li][lj] = Hs[n0][li][lj] * ((aam - d_one) / aam);
+        else Hs[nn][li][lj] = d_two * Hs[n1][li][lj] - Hs[n0][li][lj];
+      }
+      if (ce[r]) {
+        sd[r] = sd[r] + Ds[nn][li][lj];
+        sh[r] = sh[r] + Hs[nn][li][lj];
+      }
+    }
+    __syncthreads();
+    if (n >= 2) { const int t0 = n0; n0 = n1; n1 = t0; }
+    else { /* forward step: n0 = 1, n1 = 2 stay; the leapfrog loop starts with n2 = n0 */ }
+  }
+  for (int r = 0; r < 4; r++) {
+    const int j = jr0 + tx, i = ir0 + ty + 8 * r;
+    if (own[r] && in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2)) {
+      const long q = (long)(l - 1) * g.plane + g.ix(j, i);
+      ddsum[q] = ce[r] ? sd[r] : d_zero;
+      dhsum[q] = ce[r] ? sh[r] : d_zero;
+    }
+  }
+}
+
 // splitf corrections, Main/mod_split.F90:417-457 (ps and t on ci, u and v on di)
 __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
@@ -1072,29 +1183,22 @@ __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu
 }
 
 // ---------------------------------------------------------------------------------------
-// Ghost fill between tiles resident on the same device (the local transport of exchange*).
-__global__ void k_ghost_fill(Geom g, double* dst, int nk, int width, int sides, NbrTable nt) {
-  const int j = g.j0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int i = g.i0 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (j < g.jde1 - width || j > g.jde2 + width || i < g.ide1 - width || i > g.ide2 + width) return;
-  const int dj = (j < g.jde1) ? 0 : (j > g.jde2 ? 2 : 1);
-  const int di = (i < g.ide1) ? 0 : (i > g.ide2 ? 2 : 1);
-  if (dj == 1 && di == 1) return;
-  if (sides == 1 && !((dj == 0 && di == 1) || (dj == 1 && di == 0) || (dj == 0 && di == 0))) return;
-  if (sides == 2 && !((dj == 2 && di == 1) || (dj == 1 && di == 2) || (dj == 2 && di == 2))) return;
-  const int nb = di * 3 + dj;
-  const double* src = nt.base[nb];
-  if (!src) return;
-  const long sq = (long)(i - nt.i0[nb]) * nt.pitch[nb] + (j - nt.j0[nb]);
-  for (int k = 1; k <= nk; k++) dst[(long)(k - 1) * g.plane + g.ix(j, i)] = src[(long)(k - 1) * nt.plane[nb] + sq];
-}
-
-__global__ void k_slice_fill(double* dst, const double* __restrict__ src, int dst_off, int src_off, long dslen,
-                             long sslen, int kz) {
-  const int k = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (k > kz) return;
-  dst[(long)(k - 1) * dslen + dst_off] = src[(long)(k - 1) * sslen + src_off];
+// Halo staging: pack owned edge boxes / unpack ghost boxes of several fields in one launch.
+// A segment addresses p + (k-1)*kstride + (i-i0)*pitch + (j-j0) over a box of nk levels and
+// lands at buf[off + ((k-1)*ni + (i-i1))*nj + (j-j1)].  Used by every exchange, whether the
+// peer tile is on this device (device copy) or on another rank (RCCL).
+__global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack) {
+  const Seg sg = L.s[blockIdx.y];
+  const int nj = sg.j2 - sg.j1 + 1, ni = sg.i2 - sg.i1 + 1;
+  const long n = (long)nj * ni * sg.nk;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+    const int j = sg.j1 + (int)(q % nj);
+    const int i = sg.i1 + (int)((q / nj) % ni);
+    const int k = (int)(q / ((long)nj * ni));
+    double* a = sg.p + (long)k * sg.kstride + (long)(i - sg.i0) * sg.pitch + (j - sg.j0);
+    if (unpack) *a = buf[sg.off + q];
+    else buf[sg.off + q] = *a;
+  }
 }
 
 }  // namespace rcm

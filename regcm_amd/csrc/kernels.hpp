@@ -4,11 +4,19 @@
 
 namespace rcm {
 
-// 3x3 neighbourhood table for the same-device ghost fill (index di*3+dj; 4 = self).
-struct NbrTable {
-  const double* base[9];
-  int j0[9], i0[9], pitch[9];
-  long plane[9];
+// one halo staging segment (see k_pack_segs)
+struct Seg {
+  double* p;
+  long kstride;
+  int pitch, j0, i0, j1, j2, i1, i2, nk;
+  long off;
+};
+constexpr int MAXSEG = 64;
+// fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
+constexpr int SPB = 16, SPH = 8;
+struct SegList {
+  Seg s[MAXSEG];
+  int n;
 };
 
 // boundary slices, order documented at k_bdyval_set
@@ -42,7 +50,7 @@ __global__ void k_bdyval_qc_we(Geom g, int kz, double* a1qc, const double* __res
 __global__ void k_bdyval_qc_sn(Geom g, int kz, double* a1qc, const double* __restrict__ psa, Slices sl, long slen);
 __global__ void k_bdyval_time(StepState* s, double dtsec);
 __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu_hgtf, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ ht, double* xmsf, double* dmsf, double* hgfact, double* mapf);
-__global__ void k_ghost_fill(Geom g, double* dst, int nk, int width, int sides, NbrTable nt);
-__global__ void k_slice_fill(double* dst, const double* __restrict__ src, int dst_off, int src_off, long dslen, long sslen, int kz);
+__global__ void k_spstep_fused(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
+__global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack);
 
 }  // namespace rcm

@@ -14,6 +14,7 @@ program test_shim
   real(c_double), pointer, contiguous :: a3(:,:,:), a2(:,:)
   real(c_double), pointer, contiguous :: t(:,:,:), u(:,:,:), ps(:,:)
   character(len=512) :: fin, fout
+  integer(c_int8_t), allocatable :: raw(:)
   integer(c_int64_t) :: lcount
   real(c_double) :: dt, xbc
   call get_command_argument(1, fin)
@@ -22,9 +23,21 @@ program test_shim
     stop
   end if
   call get_command_argument(2, fout)
+  if ( trim(fin) == '--dump' ) then
+    open(10, file=trim(fout), access='stream', form='unformatted', status='old')
+    read(10) jx, iy, kz, nsplit, nsteps
+    allocate(raw(c_sizeof(cfg)))
+    read(10) raw         ! the C struct's memory image (with its alignment padding)
+    cfg = transfer(raw, cfg)
+    close(10)
+    print *, cfg%jx, cfg%kz, cfg%dtsec, cfg%pd, cfg%device, cfg%comm_size, cfg%nsplit
+    stop
+  end if
   open(10, file=trim(fin), access='stream', form='unformatted', status='old')
   read(10) jx, iy, kz, nsplit, nsteps
-  read(10) cfg
+  allocate(raw(c_sizeof(cfg)))
+  read(10) raw           ! the C struct's memory image (with its alignment padding)
+  cfg = transfer(raw, cfg)
   call gpu_dyn_check(c_null_ptr, rcmdyn_create(cfg, h), 'create')
   read(10) nf
   do n = 1 , nf
