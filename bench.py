@@ -22,16 +22,35 @@ sys.path.insert(0, ROOT)
 
 from regcm_amd.config import CONFIGS, set_nproc  # noqa: E402
 from regcm_amd import icbc  # noqa: E402
+from regcm_amd.traffic import kernel_bytes, step_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def algorithmic_bytes_hydro(jx: int, iy: int, kz: int, nspgx: int = 12) -> float:
-    """Compulsory HBM bytes of one hydrostatic step, SURVEY.md section 8(d):
-    B_h = 8 [N3 (20 + 8 f_b) + N2 (19 + 2 f_b)]."""
-    n3, n2 = jx * iy * kz, jx * iy
-    fb = 1.0 - ((jx - 1 - 2 * nspgx) * (iy - 1 - 2 * nspgx)) / ((jx - 1) * (iy - 1))
-    return 8.0 * (n3 * (20 + 8 * fb) + n2 * (19 + 2 * fb))
+def kernels_digest() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("kernels.hip", "kernels.hpp", "engine.hip", "engine.hpp"):
+        with open(os.path.join(ROOT, "regcm_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel: str, config: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py), only if it was measured on this exact kernel source."""
+    try:
+        with open(PMC_FILE) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("digest") != kernels_digest() or d.get("config") != config:
+        return None, None
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_per_launch"], d.get("source")
 
 
 def cpu_baseline(rc, data, budget_s: float = 15.0):
@@ -63,6 +82,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--prof-steps", type=int, default=5,
+                    help="eager steps timed per kernel with HIP events (dominant-kernel roofline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,12 +132,40 @@ def main():
         wall = float(tt.item())
     t_step = wall / args.steps
     sypd = rc.dt / (365.0 * t_step)
-    bstep = algorithmic_bytes_hydro(rc.jx, rc.iy, rc.kz, rc.nspgx)
-    achieved = bstep / t_step / 1e9
+    # per-kernel device time (HIP events around each launch on the engine's stream), on
+    # every rank (the eager steps exchange halos), after the timed region
+    kt = eng.kernel_times(args.prof_steps) if args.prof_steps > 0 else {}
+    barrier()
+    bstep = step_bytes(rc.jx, rc.iy, rc.kz, rc.nspgx)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
+    # dominant kernel = largest device time per step
+    dom = max(kt.items(), key=lambda kv: kv[1][0] * kv[1][1])[0] if kt else None
+    roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+            "traffic": None, "kernel": dom}
+    if dom is not None:
+        launches, avg_ms = kt[dom]
+        tj, ti = rc.jx, rc.iy
+        if world > 1:                   # this rank's tile
+            from regcm_amd.dycore import tile_extent
+            ext, _ = tile_extent(rc.jx, rc.iy, cj, ci, rank)
+            tj, ti = ext[1] - ext[0] + 1, ext[3] - ext[2] + 1
+        b = kernel_bytes(dom, tj, ti, rc.kz, rc.nspgx)
+        traffic, src = pmc_traffic(dom, args.config) if world == 1 else (None, None)
+        roof.update({
+            "avg_launch_us": avg_ms * 1e3,
+            "launches_per_step": launches / args.prof_steps,
+            "algorithmic_bytes_per_launch": b,
+            "timing": f"HIP events around every launch on the engine stream, {args.prof_steps} eager steps "
+                      "(rcmdyn_kernel_times)",
+            "traffic_source": src,
+        })
+        if b is not None:
+            achieved = b / (avg_ms * 1e-3) / 1e9
+            roof.update({"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "traffic": traffic})
+    step_achieved = bstep / t_step / 1e9
     line = {
         "metric": "simulated-years/wall-day, 192x192x23 sigma grid (hydrostatic dyn step)",
         "value": sypd,
@@ -134,10 +183,11 @@ def main():
                                "hydrostatic, upstream adv + 4th-order diff + split-explicit "
                                "(nsplit=2) + iboudy=5 relaxation, physics stubbed",
                    "tiles": f"{cj}x{ci}", "step": "tend + bdyval"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "whole dyn step (hipGraph of ~30 kernels)",
-                     "algorithmic_bytes": bstep},
+        "roofline": roof,
+        "step_roofline": {"achieved": step_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": step_achieved / HBM_PEAK_GBS, "algorithmic_bytes": bstep,
+                          "note": "SURVEY 8(d) B_h per step / wall time per step"},
+        "kernel_us": {k: round(v[1] * 1e3, 2) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0] * kv[1][1])},
         "device_ms_per_step": dev_ms,
     }
     if not args.no_cpu_baseline and world == 1:

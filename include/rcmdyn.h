@@ -159,6 +159,20 @@ int rcmdyn_comm_unique_id(uint8_t out[128]);
  * with HIP events on the engine's compute stream. */
 int rcmdyn_last_step_ms(rcmdyn_t* h, double* ms);
 
+/* Tendency diagnostics (TTEN..QCTEN, OMEGA, XKC of rcmdyn_field): off by default.  When on,
+ * every tend also stores the per-point tendencies the reference accumulates in aten
+ * (Main/mod_tendency.F90:259-400) for rcmdyn_get; when off those gets fail.  The prognostic
+ * results are identical either way. */
+int rcmdyn_set_diagnostics(rcmdyn_t* h, int32_t on);
+
+/* Per-kernel device time (measurement hook, mirrors rocprofv3 --kernel-trace --stats):
+ * runs nsteps steps (tend + bdyval, eagerly, no graph) with a HIP event pair around every
+ * kernel launch on the engine's stream.  For each distinct kernel (at most cap) fills
+ * names[q*48 .. q*48+47] (NUL-terminated), launches[q] and avg_ms[q] (mean duration per
+ * launch); *count = kernels found.  The steps advance the model like rcmdyn_step. */
+int rcmdyn_kernel_times(rcmdyn_t* h, int32_t nsteps, int32_t cap, char* names, int32_t* launches,
+                        double* avg_ms, int32_t* count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,8 @@ Geom make_geom(int jx, int iy, int cj, int ci, int tile) {
   g.ni = (g.ide2 - g.ide1 + 1) + 2 * G;
   g.pitch = (g.nj + 15) / 16 * 16;
   g.plane = (long)g.pitch * g.ni;
+  g.P8 = (uint32_t)g.pitch * 8u;
+  g.L8 = (uint32_t)(g.plane * 8);
   return g;
 }
 
@@ -140,6 +142,42 @@ void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::ve
   }
 }
 
+// Launch with an optional HIP event pair around the kernel (rcmdyn_kernel_times).
+#define KLAUNCH(kern, ...)                                  \
+  do {                                                      \
+    hipEvent_t e0_ = prof ? prof->begin(stream) : nullptr;  \
+    hipLaunchKernelGGL(kern, __VA_ARGS__);                  \
+    if (prof) prof->end(stream, #kern, e0_);                \
+  } while (0)
+
+// per-launch event pairs, aggregated by kernel name after the run
+struct KernelProf {
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> rec;
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("rcmdyn: hipEventCreate failed");
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  hipEvent_t begin(hipStream_t s) {
+    hipEvent_t e = get();
+    hipEventRecord(e, s);
+    return e;
+  }
+  void end(hipStream_t s, const char* name, hipEvent_t e0) {
+    hipEvent_t e1 = get();
+    hipEventRecord(e1, s);
+    rec.push_back({name, {e0, e1}});
+  }
+  ~KernelProf() {
+    for (hipEvent_t e : pool) hipEventDestroy(e);
+  }
+};
+
 inline dim3 grid3(int nj, int ni, int nk) { return dim3((nj + 63) / 64, (ni + 3) / 4, nk); }
 const dim3 BLK(64, 4, 1);
 
@@ -148,7 +186,7 @@ const dim3 BLK(64, 4, 1);
 // Buffers that exchanges refer to, resolved per tile.
 enum class FK {
   A1U, A1V, A1T, A1QV, A1QC, A2U, A2V, A2T, A2QV, A2QC, PSA, PSB, PSDOTA, PSDOTB,
-  UD, VD, QDOT, XKC, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
+  RPSDA, RPSDB, QDOT, XKC, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
   UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR
 };
 
@@ -168,6 +206,11 @@ struct rcmdyn_engine {
   bool capturing = false;
   long slen = 0;
   long staging_cap = 0;
+  double* red = nullptr;     // noise-sum partials of every tile (k_columns)
+  unsigned* ticket = nullptr;
+  int red_total = 0;
+  bool diag = false;         // write the per-tend diagnostic fields
+  KernelProf* prof = nullptr;  // set while rcmdyn_kernel_times runs
   double last_ms = 0.0;
   std::string err;
   std::unique_ptr<Comm> comm;
@@ -267,7 +310,7 @@ struct rcmdyn_engine {
       t.a2u[b] = dalloc(t, P3); t.a2v[b] = dalloc(t, P3); t.a2t[b] = dalloc(t, P3);
       t.a2qv[b] = dalloc(t, P3); t.a2qc[b] = dalloc(t, P3);
     }
-    t.psa = dalloc(t, P); t.psb = dalloc(t, P);
+    for (int b = 0; b < 2; b++) { t.psa_[b] = dalloc(t, P); t.psb_[b] = dalloc(t, P); }
     t.dstor = dalloc(t, P * ns); t.hstor = dalloc(t, P * ns);
     t.msfx = dalloc(t, P); t.msfd = dalloc(t, P); t.coriol = dalloc(t, P); t.ht = dalloc(t, P);
     t.xmsf = dalloc(t, P); t.dmsf = dalloc(t, P); t.hgfact = dalloc(t, P); t.mapf = dalloc(t, P);
@@ -276,15 +319,12 @@ struct rcmdyn_engine {
     t.ub0 = dalloc(t, P3); t.ubt = dalloc(t, P3); t.vb0 = dalloc(t, P3); t.vbt = dalloc(t, P3);
     t.tb0 = dalloc(t, P3); t.tbt = dalloc(t, P3); t.qb0 = dalloc(t, P3); t.qbt = dalloc(t, P3);
     t.pb0 = dalloc(t, P); t.pbt = dalloc(t, P);
-    t.rpsa = dalloc(t, P); t.rpsb = dalloc(t, P); t.rpsc = dalloc(t, P); t.rpsda = dalloc(t, P);
+    t.rpsa = dalloc(t, P); t.rpsb = dalloc(t, P); t.rpsda = dalloc(t, P); t.rpsdb = dalloc(t, P);
     t.psc = dalloc(t, P); t.psdota = dalloc(t, P); t.psdotb = dalloc(t, P); t.pten = dalloc(t, 2 * P);
-    t.umc = dalloc(t, P3); t.vmc = dalloc(t, P3); t.ud = dalloc(t, P3); t.vd = dalloc(t, P3);
-    t.xt = dalloc(t, P3); t.xqv = dalloc(t, P3); t.xqc = dalloc(t, P3); t.xtv = dalloc(t, P3);
     t.qdot = dalloc(t, P * (kz + 1));
-    t.ubd = dalloc(t, P3); t.vbd = dalloc(t, P3); t.tb3d = dalloc(t, P3); t.qvb = dalloc(t, P3);
-    t.qcb = dalloc(t, P3); t.xkc = dalloc(t, P3); t.phi = dalloc(t, P3);
+    t.xkc = dalloc(t, P3); t.phi = dalloc(t, P3);
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
-    t.dep = talloc<uint8_t>(t, 2 * P3); t.depplane = talloc<int>(t, 2 * kz);
+    t.depplane = talloc<int>(t, 2 * kz);
     t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
     t.ddsum = dalloc(t, P * ns); t.dhsum = dalloc(t, P * ns);
     t.uu = dalloc(t, P); t.vv = dalloc(t, P);
@@ -296,9 +336,10 @@ struct rcmdyn_engine {
     staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 2 * (kz + 1) * 8);
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
-    dim3 gr = grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1);
-    t.nred = gr.x * gr.y;
-    t.red = dalloc(t, 2 * (size_t)t.nred + 2);
+    // column blocks of k_columns (one noise partial each)
+    t.nred = ((g.jde2 - g.jde1 + 64) / 64) * ((g.ide2 - g.ide1 + 4) / 4);
+    t.red_off = red_total;
+    red_total += t.nred;
     // boundary masks
     std::vector<int8_t> rg;
     std::vector<int16_t> ib;
@@ -340,7 +381,15 @@ struct rcmdyn_engine {
     HIPCHK(hipMalloc(&ds, sizeof(StepState)));
     HIPCHK(hipMemcpy(ds, &hs, sizeof(StepState), hipMemcpyHostToDevice));
     tiles.resize(cfg.tile_count);
-    for (int t = 0; t < cfg.tile_count; t++) setup_tile(tiles[t], cfg.tile_first + t);
+    for (int t = 0; t < cfg.tile_count; t++) {
+      const Geom& g = all[cfg.tile_first + t];
+      if ((double)g.plane * 8.0 * (cfg.kz + 1) >= 4294967296.0)
+        throw std::runtime_error("rcmdyn: tile too large for 32-bit field offsets");
+      setup_tile(tiles[t], cfg.tile_first + t);
+    }
+    HIPCHK(hipMalloc(&red, sizeof(double) * 2 * (size_t)(red_total + 1)));
+    HIPCHK(hipMalloc(&ticket, sizeof(unsigned)));
+    HIPCHK(hipMemset(ticket, 0, sizeof(unsigned)));
     if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg, stream));
   }
 
@@ -353,6 +402,8 @@ struct rcmdyn_engine {
     comm.reset();
     if (dc) hipFree(dc);
     if (ds) hipFree(ds);
+    if (red) hipFree(red);
+    if (ticket) hipFree(ticket);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -369,9 +420,9 @@ struct rcmdyn_engine {
       case FK::A1QV: return t.a1qv[c]; case FK::A1QC: return t.a1qc[c];
       case FK::A2U: return t.a2u[c]; case FK::A2V: return t.a2v[c]; case FK::A2T: return t.a2t[c];
       case FK::A2QV: return t.a2qv[c]; case FK::A2QC: return t.a2qc[c];
-      case FK::PSA: return t.psa; case FK::PSB: return t.psb;
+      case FK::PSA: return t.psa_[c]; case FK::PSB: return t.psb_[c];
       case FK::PSDOTA: return t.psdota; case FK::PSDOTB: return t.psdotb;
-      case FK::UD: return t.ud; case FK::VD: return t.vd; case FK::QDOT: return t.qdot;
+      case FK::RPSDA: return t.rpsda; case FK::RPSDB: return t.rpsdb; case FK::QDOT: return t.qdot;
       case FK::XKC: return t.xkc; case FK::CQV: return t.cqv; case FK::CQC: return t.cqc;
       case FK::PHI: return t.phi; case FK::UU: return t.uu; case FK::VV: return t.vv;
       case FK::DHSUM: return t.dhsum; case FK::DELH: return t.delh;
@@ -410,7 +461,7 @@ struct rcmdyn_engine {
     }
     nk = 1;
     switch (f) {
-      case RCMDYN_PSA: return t.psa; case RCMDYN_PSB: return t.psb;
+      case RCMDYN_PSA: return t.psa_[c]; case RCMDYN_PSB: return t.psb_[c];
       case RCMDYN_MSFX: return t.msfx; case RCMDYN_MSFD: return t.msfd;
       case RCMDYN_CORIOL: return t.coriol; case RCMDYN_HT: return t.ht;
       case RCMDYN_XPSB_B0: return t.pb0; case RCMDYN_XPSB_BT: return t.pbt;
@@ -441,6 +492,9 @@ struct rcmdyn_engine {
   }
 
   void get(int f, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
+    if (!diag && (f == RCMDYN_TTEN || f == RCMDYN_UTEN || f == RCMDYN_VTEN || f == RCMDYN_QVTEN ||
+                  f == RCMDYN_QCTEN || f == RCMDYN_OMEGA || f == RCMDYN_XKC))
+      throw std::runtime_error("rcmdyn_get: tendency diagnostics are off (rcmdyn_set_diagnostics)");
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -523,7 +577,7 @@ struct rcmdyn_engine {
       SegList L{};
       L.n = (int)std::min<size_t>(MAXSEG, segs.size() - a);
       for (int q = 0; q < L.n; q++) L.s[q] = segs[a + q];
-      hipLaunchKernelGGL(k_pack_segs, dim3(32, L.n), dim3(256), 0, stream, L, buf, unpack);
+      KLAUNCH(k_pack_segs, dim3(32, L.n), dim3(256), 0, stream, L, buf, unpack);
     }
   }
   void exchange_generic(const SegFn& fn, const std::function<bool(int)>& send_on,
@@ -647,107 +701,85 @@ struct rcmdyn_engine {
     }
   }
 
+  // all buffers of one tile for its current parity (see Fields)
+  Fields fields(Tile& t) {
+    const int c = t.cur, n = 1 - c;
+    Fields f{};
+    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[c]; f.a1qv = t.a1qv[c]; f.a1qc = t.a1qc[c];
+    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[c]; f.a2qv = t.a2qv[c]; f.a2qc = t.a2qc[c];
+    f.psa = t.psa_[c]; f.psb = t.psb_[c];
+    f.b1u = t.a1u[n]; f.b1v = t.a1v[n]; f.b1t = t.a1t[n]; f.b1qv = t.a1qv[n]; f.b1qc = t.a1qc[n];
+    f.b2u = t.a2u[n]; f.b2v = t.a2v[n]; f.b2t = t.a2t[n]; f.b2qv = t.a2qv[n]; f.b2qc = t.a2qc[n];
+    f.bpsa = t.psa_[n]; f.bpsb = t.psb_[n];
+    f.msfx = t.msfx; f.msfd = t.msfd; f.coriol = t.coriol; f.ht = t.ht; f.xmsf = t.xmsf; f.dmsf = t.dmsf;
+    f.hgfact = t.hgfact; f.mapf = t.mapf;
+    f.rgcr = t.rgcr; f.rgdt = t.rgdt; f.ibcr = t.ibcr; f.ibdt = t.ibdt;
+    f.ub0 = t.ub0; f.ubt = t.ubt; f.vb0 = t.vb0; f.vbt = t.vbt; f.tb0 = t.tb0; f.tbt = t.tbt;
+    f.qb0 = t.qb0; f.qbt = t.qbt; f.pb0 = t.pb0; f.pbt = t.pbt;
+    f.rpsa = t.rpsa; f.rpsb = t.rpsb; f.rpsda = t.rpsda; f.rpsdb = t.rpsdb; f.psc = t.psc;
+    f.psdota = t.psdota; f.psdotb = t.psdotb; f.pten = t.pten; f.ptenn = t.pten + t.g.plane;
+    f.qdot = t.qdot; f.xkc = t.xkc; f.phi = t.phi; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
+    f.depplane = t.depplane;
+    if (diag) {
+      f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
+      f.omega = t.omega; f.xkcs = t.xkcs;
+    }
+    f.red = red; f.ticket = ticket; f.red_off = t.red_off; f.red_total = red_total;
+    return f;
+  }
+
   void tend() {
     const int kz = cfg.kz, ns = cfg.nsplit;
-    // surface_pressures, Main/mod_tendency.F90:815-834
+    // surface_pressures + 2-D reciprocals, Main/mod_tendency.F90:815-834
     xch(FK::PSA, 1, 1, 0);
     xch(FK::PSB, 1, 2, 0);
     each([&](Tile& t) {
-      hipLaunchKernelGGL(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, t.psa, t.psb, t.rpsa,
-                         t.rpsb, t.psdota, t.psdotb);
+      KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
     });
-    xch(FK::PSDOTA, 1, 1, 0); xch(FK::PSDOTB, 1, 2, 0);
-    // decouple, :852-1116
+    xch({{FK::PSDOTA, 1}, {FK::RPSDA, 1}}, 1, 0);
+    xch({{FK::PSDOTB, 1}, {FK::RPSDB, 1}}, 2, 0);
+    // decouple / mkslice inputs (:852-1116, Main/mod_slice.F90:102-300): the decoupled
+    // fields are recomputed where read, so their exchanges become exchanges of atm1/atm2
     xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz}, {FK::A1QC, kz}}, 1, 0);
-    each([&](Tile& t) {
-      const int c = t.cur;
-      hipLaunchKernelGGL(k_decouple, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, t.a1u[c], t.a1v[c], t.a1t[c],
-                         t.a1qv[c], t.a1qc[c], t.msfd, t.psdota, t.rpsa, t.rpsda, t.umc, t.vmc, t.ud, t.vd, t.xt,
-                         t.xqv, t.xqc, t.xtv, hc.ep1);
-    });
-    xch({{FK::UD, kz}, {FK::VD, kz}}, 1, 0);
     xch({{FK::A2U, kz}, {FK::A2V, kz}, {FK::A2T, kz}, {FK::A2QV, kz}, {FK::A2QC, kz}}, 2, 0);
-    // compute_omega column part, :1118-1156
+    // compute_omega columns, new_pressure, geopotential, calc_coeff (one launch)
     each([&](Tile& t) {
       const Geom& g = t.g;
-      hipLaunchKernelGGL(k_omega_col, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc,
-                         t.umc, t.vmc, t.msfx, t.rpsa, t.pten, t.qdot);
+      const int nxa = (g.jce2 - g.jce1 + 64) / 64, nya = (g.ice2 - g.ice1 + 4) / 4;
+      const int nba = nxa * nya * kz, nxb = (g.jde2 - g.jde1 + 64) / 64;
+      KLAUNCH(k_columns, dim3(nba + t.nred), dim3(256), 0, stream, g, dc, ds, fields(t), nxa, nya, nba,
+                         nxb);
     });
     xch(FK::QDOT, kz + 1, 1, 0);
-    // mkslice, Main/mod_slice.F90:102-300 (dyn subset)
-    each([&](Tile& t) {
-      const int c = t.cur;
-      hipLaunchKernelGGL(k_mkslice, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, t.a2u[c], t.a2v[c], t.a2t[c],
-                         t.a2qv[c], t.a2qc[c], t.psb, t.psdotb, t.ubd, t.vbd, t.tb3d, t.qvb, t.qcb);
-    });
-    // new_pressure, :1428-1460
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      dim3 gr = grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1);
-      hipLaunchKernelGGL(k_new_pressure, gr, BLK, 0, stream, g, dc, ds, t.psa, t.psb, t.pb0, t.pbt, t.rgcr, t.ibcr,
-                         t.pten, t.pten + g.plane, t.psc, t.rpsc, t.red);
-    });
-    each([&](Tile& t) { hipLaunchKernelGGL(k_reduce_noise, dim3(1), dim3(256), 0, stream, t.red, t.nred, ds); });
-    // calc_coeff, Main/mod_diffusion.F90:169-251
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      hipLaunchKernelGGL(k_calc_coeff, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc,
-                         t.ubd, t.vbd, t.hgfact, t.xkc);
-    });
     xch(FK::XKC, kz, 1, 0);
-    // geopotential for the PGF, :2033-2099
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      hipLaunchKernelGGL(k_phi_col, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
-                         t.a1t[t.cur], t.xqv, t.xqc, t.psa, t.rpsa, t.ht, t.phi);
-    });
     xch(FK::PHI, kz, 1, 1);
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {
       const Geom& g = t.g;
-      const int c = t.cur, n = 1 - c;
-      hipLaunchKernelGGL(k_momentum, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, t.a1u[c], t.a1v[c],
-                         t.a2u[c], t.a2v[c], t.a1u[n], t.a1v[n], t.a2u[n], t.a2v[n], t.umc, t.vmc, t.ud, t.vd,
-                         t.qdot, t.coriol, t.dmsf, t.msfd, t.ub0, t.ubt, t.vb0, t.vbt, t.rgdt, t.ibdt, t.xkc,
-                         t.psdotb, t.ubd, t.vbd, t.xtv, t.psdota, t.psa, t.phi, t.uten, t.vten);
-      hipLaunchKernelGGL(k_temperature, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, t.a1t[c], t.a2t[c],
-                         t.a1t[n], t.a2t[n], t.xt, t.umc, t.vmc, t.psa, t.psb, t.xmsf, t.qdot, t.pten, t.ud, t.vd,
-                         t.msfx, t.xqv, t.xtv, t.rpsa, t.tb0, t.tbt, t.rgcr, t.ibcr, t.xkc, t.tb3d, t.tten,
-                         t.omega, t.xkcs);
-      hipLaunchKernelGGL(k_moisture, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc, ds,
-                         t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.xqv, t.xqc, t.umc, t.vmc, t.psa, t.psb,
-                         t.xmsf, t.qdot, t.qb0, t.qbt, t.rgcr, t.ibcr, t.xkc, t.qvb, t.qcb, t.cqv, t.cqc, t.qvten,
-                         t.qcten);
+      const Fields f = fields(t);
+      KLAUNCH(k_momentum, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, f);
+      KLAUNCH(k_temperature, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, f);
+      KLAUNCH(k_moisture, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc, ds,
+                         f);
     });
     xch({{FK::CQV, kz}, {FK::CQC, kz}}, 1, 0);
+    // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     each([&](Tile& t) {
-      const Geom& g = t.g;
-      hipLaunchKernelGGL(k_ps_filter, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, 1), BLK, 0, stream, g, dc,
-                         t.psa, t.psb, t.psc);
-      hipLaunchKernelGGL(k_negfix, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, kz,
-                         t.cqv, t.cqc, t.fqv, t.fqc, t.dep, t.depplane);
-      hipLaunchKernelGGL(k_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, kz, t.cqv, t.cqc, t.fqv, t.fqc,
-                         t.dep, t.depplane);
-      const int c = t.cur, n = 1 - c;
-      hipLaunchKernelGGL(k_moisture_filter, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, t.a1qv[c], t.a1qc[c],
-                         t.a2qv[c], t.a2qc[c], t.a1qv[n], t.a1qc[n], t.a2qv[n], t.a2qc[n], t.fqv, t.fqc, t.psa,
-                         t.psb);
-      t.cur = n;
+      KLAUNCH(k_qfilter, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
+      t.cur = 1 - t.cur;
     });
     // splitf, Main/mod_split.F90:243-461
     xch(FK::PSA, 1, 1, 0);
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      hipLaunchKernelGGL(k_psc2psd, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, t.psa,
-                         t.psdota);
-    });
     xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A2U, kz}, {FK::A2V, kz}}, 1, 2);
     each([&](Tile& t) {
       const Geom& g = t.g;
-      const int c = t.cur;
-      hipLaunchKernelGGL(k_split_project, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
-                         dc, t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa, t.psb, t.msfd,
-                         t.mapf, t.dstor, t.hstor, t.deld, t.delh);
+      const int c = t.cur, o = 1 - c;
+      QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
+             t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.depplane};
+      const int nxp = (g.jde2 - g.jde1 + 64) / 64, nproj = nxp * ((g.ide2 - g.ide1 + 4) / 4);
+      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), BLK, 0, stream, g, dc, t.a1u[c], t.a1v[c],
+                         t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
+                         t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
     bool fused = (ntiles == 1);
@@ -756,13 +788,13 @@ struct rcmdyn_engine {
       each([&](Tile& t) {
         const Geom& g = t.g;
         dim3 gr((g.jce2 - g.jce1 + SPB) / SPB, (g.ice2 - g.ice1 + SPB) / SPB, ns);
-        hipLaunchKernelGGL(k_spstep_fused, gr, dim3(32, 8), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
-                           t.psdota, t.mapf, t.psa, t.ddsum, t.dhsum);
+        KLAUNCH(k_spstep_fused, gr, dim3(32, 8), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
+                           t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
       });
     } else {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        hipLaunchKernelGGL(k_spstep_init, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
+        KLAUNCH(k_spstep_init, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g,
                            dc, t.deld, t.delh, t.ddsum, t.dhsum);
       });
     }
@@ -776,14 +808,15 @@ struct rcmdyn_engine {
       }
     }
     xch(FK::DHSUM, ns, 1, 1);
-    each([&](Tile& t) {
+    // corrections + rcmtimer advance (last tile's launch)
+    for (size_t q = 0; q < tiles.size(); q++) {
+      Tile& t = tiles[q];
       const Geom& g = t.g;
       const int c = t.cur;
-      hipLaunchKernelGGL(k_split_correct, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
-                         dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa, t.psb, t.a1t[c], t.a2t[c], t.a1u[c],
-                         t.a1v[c], t.a2u[c], t.a2v[c]);
-    });
-    hipLaunchKernelGGL(k_advance_time, dim3(1), dim3(1), 0, stream, ds, cfg.dtsec);
+      KLAUNCH(k_split_correct, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
+                         dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
+                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()));
+    }
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
   }
@@ -793,50 +826,50 @@ struct rcmdyn_engine {
     xch_delh_slot(l, src);
     each([&](Tile& t) {
       const Geom& g = t.g;
-      hipLaunchKernelGGL(k_spstep_grad, grid3(g.jdi2 - g.jdi1 + 1, g.idi2 - g.idi1 + 1, 1), BLK, 0, stream, g, dc, l,
+      KLAUNCH(k_spstep_grad, grid3(g.jdi2 - g.jdi1 + 1, g.idi2 - g.idi1 + 1, 1), BLK, 0, stream, g, dc, l,
                          src, t.delh, t.msfx, t.msfd, t.psdota, t.uu, t.vv);
     });
     xch({{FK::UU, 1}, {FK::VV, 1}}, 1, 2);
     each([&](Tile& t) {
       const Geom& g = t.g;
-      hipLaunchKernelGGL(k_spstep_update, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
-                         l, n0, n1, nn, leap, t.uu, t.vv, t.mapf, t.psa, t.deld, t.delh, t.ddsum, t.dhsum);
+      KLAUNCH(k_spstep_update, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
+                         l, n0, n1, nn, leap, t.uu, t.vv, t.mapf, t.psa_[t.cur], t.deld, t.delh, t.ddsum, t.dhsum);
     });
   }
 
   void bdyval() {
     const int kz = cfg.kz;
+    auto slices = [&](Tile& t) {
+      Slices sl;
+      for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
+      return sl;
+    };
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur;
-      Slices sl;
-      for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
-      hipLaunchKernelGGL(k_bdyval_set, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, ds,
+      KLAUNCH(k_bdyval_set, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, ds,
                          t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
-                         t.a2qv[c], t.a2qc[c], t.psa, t.psb, t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt,
-                         t.pb0, t.pbt, sl, slen);
-      hipLaunchKernelGGL(k_bdyval_corners, dim3(1), dim3(64), 0, stream, g, kz, sl, slen);
+                         t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0,
+                         t.qbt, t.pb0, t.pbt, slices(t), slen);
     });
+    for (size_t q = 0; q < tiles.size(); q++)
+      KLAUNCH(k_bdyval_corners, dim3(1), dim3(64), 0, stream, tiles[q].g, kz, slices(tiles[q]), slen, ds,
+                         cfg.dtsec, (int)(q + 1 == tiles.size()));
     xch_slices();
     if (!cfg.present_qc) {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        Slices sl;
-        for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
         if (g.bl || g.br)
-          hipLaunchKernelGGL(k_bdyval_qc_we, dim3((g.ice2 - g.ice1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
-                             t.a1qc[t.cur], t.psa, sl, slen);
+          KLAUNCH(k_bdyval_qc_we, dim3((g.ice2 - g.ice1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
+                             t.a1qc[t.cur], t.psa_[t.cur], slices(t), slen);
       });
       each([&](Tile& t) {
         const Geom& g = t.g;
-        Slices sl;
-        for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
         if (g.bb || g.bt)
-          hipLaunchKernelGGL(k_bdyval_qc_sn, dim3((g.jci2 - g.jci1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
-                             t.a1qc[t.cur], t.psa, sl, slen);
+          KLAUNCH(k_bdyval_qc_sn, dim3((g.jci2 - g.jci1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
+                             t.a1qc[t.cur], t.psa_[t.cur], slices(t), slen);
       });
     }
-    hipLaunchKernelGGL(k_bdyval_time, dim3(1), dim3(1), 0, stream, ds, cfg.dtsec);
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }
 
@@ -890,6 +923,40 @@ struct rcmdyn_engine {
     HIPCHK(hipGraphDestroy(graph));
     hs = save;
     for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
+  }
+
+  void kernel_times(int nsteps, int cap, char* names, int32_t* launches, double* avg, int32_t* count) {
+    prepare();
+    KernelProf kp;
+    HIPCHK(hipStreamSynchronize(stream));
+    prof = &kp;
+    try {
+      for (int s = 0; s < nsteps; s++) { tend(); bdyval(); }
+    } catch (...) {
+      prof = nullptr;
+      throw;
+    }
+    prof = nullptr;
+    HIPCHK(hipStreamSynchronize(stream));
+    std::vector<std::string> order;
+    std::vector<double> tot;
+    std::vector<int> cnt;
+    for (auto& r : kp.rec) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, r.second.first, r.second.second));
+      size_t q = std::find(order.begin(), order.end(), r.first) - order.begin();
+      if (q == order.size()) { order.push_back(r.first); tot.push_back(0.0); cnt.push_back(0); }
+      tot[q] += ms;
+      cnt[q] += 1;
+    }
+    const int n = std::min<int>(cap, (int)order.size());
+    for (int q = 0; q < n; q++) {
+      std::memset(names + 48 * q, 0, 48);
+      std::strncpy(names + 48 * q, order[q].c_str(), 47);
+      launches[q] = cnt[q];
+      avg[q] = tot[q] / cnt[q];
+    }
+    *count = n;
   }
 
   void set_time(long long lcount, double dt, double xbctime) {
@@ -1032,5 +1099,20 @@ int rcmdyn_comm_unique_id(uint8_t out[128]) {
 }
 
 int rcmdyn_last_step_ms(rcmdyn_t* h, double* ms) { return guard(h, [&] { *ms = h->last_ms; }); }
+
+int rcmdyn_set_diagnostics(rcmdyn_t* h, int32_t on) {
+  return guard(h, [&] {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (h->diag != (on != 0)) {
+      h->diag = (on != 0);
+      h->invalidate_graphs();
+    }
+  });
+}
+
+int rcmdyn_kernel_times(rcmdyn_t* h, int32_t nsteps, int32_t cap, char* names, int32_t* launches, double* avg_ms,
+                        int32_t* count) {
+  return guard(h, [&] { h->kernel_times(nsteps, cap, names, launches, avg_ms, count); });
+}
 
 }  // extern "C"

@@ -33,8 +33,16 @@ struct Geom {
   int nj, ni;                      // frame size (nj <= pitch)
   int pitch;
   long plane;
+  uint32_t P8, L8;                 // row and plane strides in bytes (all fields share them)
   __host__ __device__ __forceinline__ long ix(int j, int i) const {
     return (long)(i - i0) * pitch + (j - j0);
+  }
+  // byte offset of (j,i) in a 2-D field / of (j,i,k) in a 3-D field
+  __host__ __device__ __forceinline__ uint32_t o2(int j, int i) const {
+    return (uint32_t)((i - i0) * pitch + (j - j0)) * 8u;
+  }
+  __host__ __device__ __forceinline__ uint32_t o3(int j, int i, int k) const {
+    return o2(j, i) + (uint32_t)(k - 1) * L8;
   }
 };
 
@@ -73,8 +81,9 @@ struct Tile {
   // prognostic state, ping-pong for the 3-D fields written by the fused update kernels
   double *a1u[2], *a1v[2], *a1t[2], *a1qv[2], *a1qc[2];
   double *a2u[2], *a2v[2], *a2t[2], *a2qv[2], *a2qc[2];
+  double *psa_[2], *psb_[2];
   int cur = 0;
-  double *psa, *psb, *dstor, *hstor;
+  double *dstor, *hstor;
   // statics
   double *msfx, *msfd, *coriol, *ht, *xmsf, *dmsf, *hgfact, *mapf;
   int8_t *rgcr, *rgdt;
@@ -82,12 +91,11 @@ struct Tile {
   // boundary data
   double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
   // work
-  double *rpsa, *rpsb, *rpsc, *rpsda, *psc, *psdota, *psdotb, *pten;
-  double *umc, *vmc, *ud, *vd, *xt, *xqv, *xqc, *xtv, *qdot;
-  double *ubd, *vbd, *tb3d, *qvb, *qcb, *xkc, *phi;
+  // 2-D reciprocals of the decoupling (decouple / mkslice, recomputed on the fly from them)
+  double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten;
+  double *qdot, *xkc, *phi;
   double *cqv, *cqc, *fqv, *fqc;
-  uint8_t *dep;                    // negative-moisture dependency flags (2 x kz planes)
-  int *depplane;                   // per (n,k) plane flag
+  int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;
   // diagnostics of the last tend
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
@@ -95,9 +103,7 @@ struct Tile {
   double *sl[16];
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
-  // reduction partials
-  double *red;
-  int nred;
+  int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials
   std::vector<void*> allocs;
 };
 

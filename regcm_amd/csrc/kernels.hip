@@ -7,9 +7,16 @@
 // the same order inside one thread, so transcendental-free results are bit-identical
 // (compiled with -ffp-contract=off).
 //
+// The reference materialises decoupled copies of the state (decouple: umc, vmc, ud, vd, t,
+// qv, qc, tv; mkslice: ubd3d, vbd3d, tb3d, qxb3d).  Each is one product of a state field with
+// a 2-D factor, so the kernels here recompute them where they are read (the same product,
+// hence the same bits) and only the 2-D reciprocals are stored: 13 3-D fields of HBM traffic
+// and two launches per step disappear.
+//
 // Thread mapping: x -> j (west-east, unit stride, coalesced), y -> i, z -> k; blocks of
-// 64 x 4.  Column recurrences (pten/qdot, phi, split projections) use one thread per
-// (j,i) column with the k loop in registers.
+// 64 x 4.  All fields of a tile share one frame, so a point's 32-bit byte offset (plus
+// shared neighbour offsets) addresses every field: loads are SGPR base + VGPR offset.
+// Column recurrences (pten/qdot, phi, split projections) use one thread per (j,i) column.
 #include "engine.hpp"
 #include "kernels.hpp"
 
@@ -19,6 +26,13 @@ namespace rcm {
 #define F3(a, j, i, k) (a)[(long)((k) - 1) * g.plane + g.ix(j, i)]
 #define SLI(s, i, k) (s)[(long)((k) - 1) * slen + ((i) - g.i0)]
 #define SLJ(s, j, k) (s)[(long)((k) - 1) * slen + ((j) - g.j0)]
+// byte-offset access
+#define LD(a, o) (*(const double*)((const char*)(a) + (uint32_t)(o)))
+#define ST(a, o, v) (*(double*)((char*)(a) + (uint32_t)(o)) = (v))
+// neighbour offsets relative to the thread's point (o2: 2-D, o3: 3-D at level k)
+#define O2(dj, di) (o2 + (uint32_t)((dj) * 8) + (uint32_t)(di) * P8)
+#define O3(dj, di) (o3 + (uint32_t)((dj) * 8) + (uint32_t)(di) * P8)
+#define O3K(dj, di, dk) (O3(dj, di) + (uint32_t)(dk) * L8)
 
 static constexpr double d_zero = 0.0, d_one = 1.0, d_two = 2.0, d_four = 4.0;
 static constexpr double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
@@ -30,7 +44,7 @@ __device__ __forceinline__ double dmin(double a, double b) { return (a < b) ? a 
 
 __device__ __forceinline__ bool in(int v, int lo, int hi) { return v >= lo && v <= hi; }
 
-// thread -> (j, i, k) over a box starting at (j1, i1); k = blockIdx.z + kbase
+// thread -> (j, i, k) over a box starting at (j1, i1); k = blockIdx.z + 1
 #define THREAD_POINT(j1, i1)                                   \
   const int j = (j1) + (int)(blockIdx.x * blockDim.x + threadIdx.x); \
   const int i = (i1) + (int)(blockIdx.y * blockDim.y + threadIdx.y); \
@@ -55,132 +69,18 @@ __device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int 
 }
 
 // ---------------------------------------------------------------------------------------
-// surface_pressures, Main/mod_tendency.F90:815-834 (both time levels in one pass)
-__global__ void k_surface_pressures(Geom g, const double* __restrict__ psa, const double* __restrict__ psb,
-                                    double* rpsa, double* rpsb, double* psdota, double* psdotb) {
+// K1. surface_pressures, Main/mod_tendency.F90:815-834, and the 2-D reciprocals of decouple
+// (rpsda, :868-875) and mkslice (1/psdotb, 1/psb, Main/mod_slice.F90:163-183).
+__global__ void k_surface_pressures(Geom g, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga)) F2(rpsa, j, i) = d_one / F2(psa, j, i);
-  if (in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2)) F2(rpsb, j, i) = d_one / F2(psb, j, i);
+  if (in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
+  if (in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
   double v;
-  if (psc2psd_at(g, psa, j, i, v)) F2(psdota, j, i) = v;
-  if (psc2psd_at(g, psb, j, i, v)) F2(psdotb, j, i) = v;
+  if (psc2psd_at(g, f.psa, j, i, v)) { F2(f.psdota, j, i) = v; F2(f.rpsda, j, i) = d_one / v; }
+  if (psc2psd_at(g, f.psb, j, i, v)) { F2(f.psdotb, j, i) = v; F2(f.rpsdb, j, i) = d_one / v; }
 }
 
-// psdota only (splitf, Main/mod_split.F90:259-260)
-__global__ void k_psc2psd(Geom g, const double* __restrict__ pc, double* pd) {
-  THREAD_POINT(g.jde1, g.ide1);
-  if (j > g.jde2 || i > g.ide2) return;
-  double v;
-  if (psc2psd_at(g, pc, j, i, v)) F2(pd, j, i) = v;
-}
-
-// ---------------------------------------------------------------------------------------
-// decouple, Main/mod_tendency.F90:858-1025 (hydrostatic).  ud/vd are atm1*rpsda on the whole
-// dot range: on the boundary rows this equals the reference's boundary-slice assignment
-// (:895-994) because bdyval stores the identical value b0+xt*bt in both atm1 and the slice.
-__global__ void k_decouple(Geom g, const double* __restrict__ a1u, const double* __restrict__ a1v,
-                           const double* __restrict__ a1t, const double* __restrict__ a1qv,
-                           const double* __restrict__ a1qc, const double* __restrict__ msfd,
-                           const double* __restrict__ psdota, const double* __restrict__ rpsa,
-                           double* rpsda, double* umc, double* vmc, double* ud, double* vd,
-                           double* xt, double* xqv, double* xqc, double* xtv, double ep1) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
-    const double r = d_one / F2(psdota, j, i);
-    if (k == 1) F2(rpsda, j, i) = r;
-    const double u = F3(a1u, j, i, k), v = F3(a1v, j, i, k), m = F2(msfd, j, i);
-    F3(umc, j, i, k) = u * m;
-    F3(vmc, j, i, k) = v * m;
-    if (in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2)) {
-      F3(ud, j, i, k) = u * r;
-      F3(vd, j, i, k) = v * r;
-    }
-  }
-  if (in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga)) {
-    const double rp = F2(rpsa, j, i);
-    const double t = F3(a1t, j, i, k) * rp;
-    const double qv = dmax(F3(a1qv, j, i, k) * rp, MINQQ);
-    const double qc = dmax(F3(a1qc, j, i, k) * rp, d_zero);
-    F3(xt, j, i, k) = t;
-    F3(xqv, j, i, k) = qv;
-    F3(xqc, j, i, k) = qc;
-    F3(xtv, j, i, k) = t * (d_one + ep1 * qv);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// compute_omega column part, Main/mod_tendency.F90:1123-1156: pten and qdot (k-scan).
-__device__ __forceinline__ double mass_div(const Geom& g, const double* umc, const double* vmc, int j, int i,
-                                           int k, double dummy) {
-  const double a = F3(umc, j + 1, i + 1, k) + F3(umc, j + 1, i, k) - F3(umc, j, i + 1, k) - F3(umc, j, i, k);
-  const double b = F3(vmc, j + 1, i + 1, k) + F3(vmc, j, i + 1, k) - F3(vmc, j + 1, i, k) - F3(vmc, j, i, k);
-  return (a + b) * dummy;
-}
-
-__global__ void k_omega_col(Geom g, const Consts* __restrict__ c, const double* __restrict__ umc,
-                            const double* __restrict__ vmc, const double* __restrict__ msfx,
-                            const double* __restrict__ rpsa, double* pten, double* qdot) {
-  const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int i = g.ide1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  if (j > g.jde2 || i > g.ide2) return;
-  const int kz = c->kz;
-  if (!(in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2))) {
-    for (int k = 1; k <= kz + 1; k++) F3(qdot, j, i, k) = d_zero;
-    return;
-  }
-  const double mx = F2(msfx, j, i);
-  const double dummy = d_one / (c->dx2 * mx * mx);
-  double pt = d_zero;
-  for (int k = 1; k <= kz; k++) pt = pt - mass_div(g, umc, vmc, j, i, k, dummy) * c->dsigma[k];
-  F2(pten, j, i) = pt;
-  const double rp = F2(rpsa, j, i);
-  double q = d_zero;
-  F3(qdot, j, i, 1) = d_zero;
-  for (int k = 2; k <= kz; k++) {
-    const double crm = mass_div(g, umc, vmc, j, i, k - 1, dummy);
-    q = q - (pt + crm) * c->dsigma[k - 1] * rp;
-    F3(qdot, j, i, k) = q;
-  }
-  F3(qdot, j, i, kz + 1) = d_zero;
-}
-
-// omega at one point, Main/mod_tendency.F90:1200-1214
-__device__ __forceinline__ double omega_at(const Geom& g, const Consts* c, const double* qdot, const double* pten,
-                                           const double* ud, const double* vd, const double* psa,
-                                           const double* msfx, int j, int i, int k) {
-  const double dummy = d_one / (c->dx8 * F2(msfx, j, i));
-  const double su = F3(ud, j, i, k) + F3(ud, j, i + 1, k) + F3(ud, j + 1, i + 1, k) + F3(ud, j + 1, i, k);
-  const double sv = F3(vd, j, i, k) + F3(vd, j, i + 1, k) + F3(vd, j + 1, i + 1, k) + F3(vd, j + 1, i, k);
-  const double x = su * (F2(psa, j + 1, i) - F2(psa, j - 1, i)) + sv * (F2(psa, j, i + 1) - F2(psa, j, i - 1));
-  return d_half * (F3(qdot, j, i, k + 1) + F3(qdot, j, i, k)) * F2(psa, j, i) +
-         c->hsigma[k] * (F2(pten, j, i) + x * dummy);
-}
-
-// ---------------------------------------------------------------------------------------
-// mkslice dyn subset, Main/mod_slice.F90:163-183
-__global__ void k_mkslice(Geom g, const double* __restrict__ a2u, const double* __restrict__ a2v,
-                          const double* __restrict__ a2t, const double* __restrict__ a2qv,
-                          const double* __restrict__ a2qc, const double* __restrict__ psb,
-                          const double* __restrict__ psdotb, double* ubd, double* vbd, double* tb3d,
-                          double* qvb, double* qcb) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (in(j, g.jde1gb, g.jde2gb) && in(i, g.ide1gb, g.ide2gb)) {
-    const double r = d_one / F2(psdotb, j, i);
-    F3(ubd, j, i, k) = F3(a2u, j, i, k) * r;
-    F3(vbd, j, i, k) = F3(a2v, j, i, k) * r;
-  }
-  if (in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb)) {
-    const double r = d_one / F2(psb, j, i);
-    F3(tb3d, j, i, k) = F3(a2t, j, i, k) * r;
-    F3(qvb, j, i, k) = dmax(F3(a2qv, j, i, k) * r, MINQQ);
-    F3(qcb, j, i, k) = dmax(F3(a2qc, j, i, k) * r, d_zero);
-  }
-}
-
-// ---------------------------------------------------------------------------------------
 // generic relaxation contribution (nudge*, Main/mod_bdycod.F90:4262-4263)
 __device__ __forceinline__ double relax(double ften, double xf, double xg, double f0, double f1, double f2,
                                         double f3, double f4) {
@@ -191,58 +91,139 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
   else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
 }
 
-// new_pressure, Main/mod_tendency.F90:1428-1460 (+ nudge2d, Main/mod_bdycod.F90:4597-4766)
-// plus per-block partial sums of the Bleck noise parameters.
-__global__ void k_new_pressure(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s,
-                               const double* __restrict__ psa, const double* __restrict__ psb,
-                               const double* __restrict__ pb0, const double* __restrict__ pbt,
-                               const int8_t* __restrict__ rgcr, const int16_t* __restrict__ ibcr,
-                               const double* __restrict__ pten, double* ptenn, double* psc, double* rpsc,
-                               double* red) {
-  THREAD_POINT(g.jce1, g.ice1);
-  const double dt = s->dt;
-  const double xt = s->xbctime + dt;
-  double a = 0.0, b = 0.0;
-  if (j <= g.jce2 && i <= g.ice2) {
-    double pt = F2(pten, j, i);
-    if (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2) && F2(rgcr, j, i) > 0) {
-      double xf, xg;
-      nudge_coef(c, F2(ibcr, j, i), c->kz, xf, xg);
-#define FG1(J, I) ((F2(pb0, J, I) + xt * F2(pbt, J, I)) - F2(psb, J, I))
-      pt = relax(pt, xf, xg, FG1(j, i), FG1(j - 1, i), FG1(j + 1, i), FG1(j, i - 1), FG1(j, i + 1));
+// ---------------------------------------------------------------------------------------
+// K2. Column work and the Smagorinsky coefficient in one launch (both only read the state):
+//  blocks [0, nba): calc_coeff, Main/mod_diffusion.F90:194-210 (unscaled xkc on jce/ice),
+//    ubd3d/vbd3d = atm2 * (1/psdotb) recomputed;
+//  blocks [nba, ..): one thread per (j,i) column of jde x ide:
+//    compute_omega column part, Main/mod_tendency.F90:1123-1156 (pten, qdot k-scan),
+//    new_pressure + nudge2d, :1428-1460 / Main/mod_bdycod.F90:4597-4766 (psc, nudged pten),
+//    the geopotential of the PGF, :1966-1995, 2033-2097 (alpha_hyd = 0, td == tva),
+//    and the Bleck noise sums, reduced deterministically by the last block to finish.
+__global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+                                                 int nxa, int nya, int nba, int nxb) {
+  const uint32_t P8 = g.P8, L8 = g.L8;
+  const int b = blockIdx.x;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  if (b < nba) {
+    const int r = b % (nxa * nya);
+    const int j = g.jce1 + (r % nxa) * 64 + tx, i = g.ice1 + (r / nxa) * 4 + ty, k = b / (nxa * nya) + 1;
+    if (j > g.jce2 || i > g.ice2) return;
+    const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
+#define UBD(dj, di) (LD(f.a2u, O3(dj, di)) * LD(f.rpsdb, O2(dj, di)))
+#define VBD(dj, di) (LD(f.a2v, O3(dj, di)) * LD(f.rpsdb, O2(dj, di)))
+    const double dudx = UBD(1, 0) + UBD(1, 1) - UBD(0, 0) - UBD(0, 1);
+    const double dvdx = VBD(1, 0) + VBD(1, 1) - VBD(0, 0) - VBD(0, 1);
+    const double dudy = UBD(0, 1) + UBD(1, 1) - UBD(0, 0) - UBD(1, 0);
+    const double dvdy = VBD(0, 1) + VBD(1, 1) - VBD(0, 0) - VBD(1, 0);
+#undef UBD
+#undef VBD
+    const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
+    ST(f.xkc, o3, dmin(LD(f.hgfact, o2) + c->dydc * duv, c->xkhmax));
+    return;
+  }
+  const int bb = b - nba;
+  const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + (bb / nxb) * 4 + ty;
+  const bool valid = j <= g.jde2 && i <= g.ide2;
+  const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
+  const bool ci = ce && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+  const int kz = c->kz;
+  double na = 0.0, nb = 0.0;
+  if (valid) {
+    const uint32_t o2 = g.o2(j, i);
+    if (!ce) {
+      for (int k = 1; k <= kz + 1; k++) ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, d_zero);
+    } else {
+      // compute_omega: mass divergence of umc/vmc = atm1 * msfd (decouple :880-890)
+      const double mx = LD(f.msfx, o2);
+      const double dummy = d_one / (c->dx2 * mx * mx);
+      const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
+      const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
+      auto mass_div = [&](int k) {
+        const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
+        const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
+                         LD(f.a1u, o3) * m00;
+        const double bq = LD(f.a1v, O3(1, 1)) * m11 + LD(f.a1v, O3(0, 1)) * m01 - LD(f.a1v, O3(1, 0)) * m10 -
+                          LD(f.a1v, o3) * m00;
+        return (a + bq) * dummy;
+      };
+      double pt = d_zero;
+      for (int k = 1; k <= kz; k++) pt = pt - mass_div(k) * c->dsigma[k];
+      ST(f.pten, o2, pt);
+      const double rp = LD(f.rpsa, o2);
+      double q = d_zero;
+      ST(f.qdot, o2, d_zero);
+      for (int k = 2; k <= kz; k++) {
+        const double crm = mass_div(k - 1);
+        q = q - (pt + crm) * c->dsigma[k - 1] * rp;
+        ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, q);
+      }
+      ST(f.qdot, o2 + (uint32_t)kz * L8, d_zero);
+      // new_pressure
+      const double dt = s->dt;
+      const double psbv = LD(f.psb, o2);
+      if (ci && f.rgcr[o2 >> 3] > 0) {
+        const double xt = s->xbctime + dt;
+        double xf, xg;
+        nudge_coef(c, f.ibcr[o2 >> 3], kz, xf, xg);
+#define FG1(dj, di) ((LD(f.pb0, O2(dj, di)) + xt * LD(f.pbt, O2(dj, di))) - LD(f.psb, O2(dj, di)))
+        pt = relax(pt, xf, xg, FG1(0, 0), FG1(-1, 0), FG1(1, 0), FG1(0, -1), FG1(0, 1));
 #undef FG1
-    }
-    F2(ptenn, j, i) = pt;
-    const double pc = F2(psb, j, i) + pt * dt;
-    F2(psc, j, i) = pc;
-    F2(rpsc, j, i) = d_one / pc;
-    if (s->lcount > 0 && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2)) {
-      a = fabs(pt);
-      b = fabs((pc + F2(psb, j, i) - d_two * F2(psa, j, i)) / (dt * dt * d_rfour));
+      }
+      ST(f.ptenn, o2, pt);
+      const double pc = psbv + pt * dt;
+      ST(f.psc, o2, pc);
+      if (s->lcount > 0 && ci) {
+        na = fabs(pt);
+        nb = fabs((pc + psbv - d_two * LD(f.psa, o2)) / (dt * dt * d_rfour));
+      }
+      // geopotential column, bottom-up; xqv/xqc = decoupled moisture (decouple :1000-1016)
+      const double ps = LD(f.psa, o2);
+      const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
+      auto xqv = [&](int K) { return dmax(LD(f.a1qv, o2 + (uint32_t)(K - 1) * L8) * rp, MINQQ); };
+      auto xqc = [&](int K) { return dmax(LD(f.a1qc, o2 + (uint32_t)(K - 1) * L8) * rp, d_zero); };
+      auto td = [&](int K) { return LD(f.a1t, o2 + (uint32_t)(K - 1) * L8) * (d_one + ep1 * xqv(K)); };
+      auto tvfac = [&](int K) { return d_one / (d_one + xqc(K) / (d_one + xqv(K))); };
+      double tdk1 = td(kz);
+      const double tv = tdk1 * rp * tvfac(kz);
+      double ph = LD(f.ht, o2) - rgas * tv * log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
+      ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
+      for (int lev = kz - 1; lev >= 1; lev--) {
+        const double tdl = td(lev);
+        const double tvavg = ((tdl * c->dsigma[lev] + tdk1 * c->dsigma[lev + 1]) /
+                              (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * tvfac(lev);
+        ph = ph - rgas * tvavg * log((c->hsigma[lev] + ptop * rp) / (c->hsigma[lev + 1] + ptop * rp));
+        ST(f.phi, o2 + (uint32_t)(lev - 1) * L8, ph);
+        tdk1 = tdl;
+      }
     }
   }
-  // deterministic block reduction (fixed tree order)
+  // deterministic reduction of the noise sums: fixed tree per block, then the last block
+  // (ticket) sums the per-block partials of every tile in index order.
   __shared__ double sa[256], sb[256];
-  const int t = threadIdx.y * blockDim.x + threadIdx.x;
-  sa[t] = a; sb[t] = b;
+  __shared__ int last;
+  const int t = threadIdx.x;
+  sa[t] = na; sb[t] = nb;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
     __syncthreads();
   }
   if (t == 0) {
-    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-    red[2 * blk] = sa[0];
-    red[2 * blk + 1] = sb[0];
+    f.red[2 * (f.red_off + bb)] = sa[0];
+    f.red[2 * (f.red_off + bb) + 1] = sb[0];
+    __threadfence();
+    last = (atomicAdd(f.ticket, 1u) == (unsigned)f.red_total - 1u);
   }
-}
-
-__global__ void k_reduce_noise(const double* __restrict__ red, int nblk, StepState* s) {
-  __shared__ double sa[256], sb[256];
-  const int t = threadIdx.x;
-  double a = 0.0, b = 0.0;
-  for (int q = t; q < nblk; q += 256) { a += red[2 * q]; b += red[2 * q + 1]; }
-  sa[t] = a; sb[t] = b;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double a = 0.0, bsum = 0.0;
+  for (int q = t; q < f.red_total; q += 256) {
+    a += __builtin_nontemporal_load(&f.red[2 * q]);
+    bsum += __builtin_nontemporal_load(&f.red[2 * q + 1]);
+  }
+  sa[t] = a; sb[t] = bsum;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
     if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
@@ -252,160 +233,113 @@ __global__ void k_reduce_noise(const double* __restrict__ red, int nblk, StepSta
     s->ptntot = sa[0];
     s->pt2tot = sb[0];
     if (sa[0] != sa[0]) s->nanflag = 1;
+    *f.ticket = 0u;
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// calc_coeff Smagorinsky part, Main/mod_diffusion.F90:194-210 (unscaled xkc on jce/ice)
-__global__ void k_calc_coeff(Geom g, const Consts* __restrict__ c, const double* __restrict__ ubd,
-                             const double* __restrict__ vbd, const double* __restrict__ hgfact, double* xkc) {
-  THREAD_POINT(g.jce1, g.ice1);
-  if (j > g.jce2 || i > g.ice2) return;
-  const double dudx = F3(ubd, j + 1, i, k) + F3(ubd, j + 1, i + 1, k) - F3(ubd, j, i, k) - F3(ubd, j, i + 1, k);
-  const double dvdx = F3(vbd, j + 1, i, k) + F3(vbd, j + 1, i + 1, k) - F3(vbd, j, i, k) - F3(vbd, j, i + 1, k);
-  const double dudy = F3(ubd, j, i + 1, k) + F3(ubd, j + 1, i + 1, k) - F3(ubd, j, i, k) - F3(ubd, j + 1, i, k);
-  const double dvdy = F3(vbd, j, i + 1, k) + F3(vbd, j + 1, i + 1, k) - F3(vbd, j, i, k) - F3(vbd, j + 1, i, k);
-  const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
-  F3(xkc, j, i, k) = dmin(F2(hgfact, j, i) + c->dydc * duv, c->xkhmax);
-}
-
-// ---------------------------------------------------------------------------------------
-// pressure_gradient_force geopotential column, Main/mod_tendency.F90:1966-1995, 2033-2097.
-// alpha_hyd = 0 (Share/mod_constants.F90:319) makes td == tva bit-for-bit for finite input.
-__global__ void k_phi_col(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1t,
-                          const double* __restrict__ xqv, const double* __restrict__ xqc,
-                          const double* __restrict__ psa, const double* __restrict__ rpsa,
-                          const double* __restrict__ ht, double* phi) {
-  const int j = g.jce1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int i = g.ice1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  if (j > g.jce2 || i > g.ice2) return;
-  const int kz = c->kz;
-  const double rp = F2(rpsa, j, i);
-  const double ps = F2(psa, j, i);
-  const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
-#define TD(K) (F3(a1t, j, i, K) * (d_one + ep1 * F3(xqv, j, i, K)))
-#define TVFAC(K) (d_one / (d_one + F3(xqc, j, i, K) / (d_one + F3(xqv, j, i, K))))
-  double tdk1 = TD(kz);
-  const double tv = tdk1 * rp * TVFAC(kz);
-  double ph = F2(ht, j, i) - rgas * tv * log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
-  F3(phi, j, i, kz) = ph;
-  for (int lev = kz - 1; lev >= 1; lev--) {
-    const double tdl = TD(lev);
-    const double tvavg = ((tdl * c->dsigma[lev] + tdk1 * c->dsigma[lev + 1]) /
-                          (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * TVFAC(lev);
-    ph = ph - rgas * tvavg * log((c->hsigma[lev] + ptop * rp) / (c->hsigma[lev + 1] + ptop * rp));
-    F3(phi, j, i, lev) = ph;
-    tdk1 = tdl;
-  }
-#undef TD
-#undef TVFAC
-}
-
-// ---------------------------------------------------------------------------------------
-// Momentum: hadvuv + vadvuv + curvature + nudgeuv + diffu_d + PGF, then the forecast and the
-// Robert-Asselin filter (Main/mod_advection.F90:203-299, Main/mod_tendency.F90:1829-1838,
+// K3. Momentum: hadvuv + vadvuv + curvature + nudgeuv + diffu_d + PGF, then the forecast and
+// the Robert-Asselin filter (Main/mod_advection.F90:203-299, Main/mod_tendency.F90:1829-1838,
 // Main/mod_bdycod.F90:3581-3823, Main/mod_diffusion.F90:281-385, Main/mod_tendency.F90:
 // 1996-2025, 2103-2115, 404-411, 433-445; Main/mod_timefilter.F90 filter_ra_uv).
-__global__ __launch_bounds__(256) void k_momentum(
-    Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s,
-    const double* __restrict__ a1u, const double* __restrict__ a1v,
-    const double* __restrict__ a2u, const double* __restrict__ a2v,
-    double* __restrict__ n1u, double* __restrict__ n1v, double* __restrict__ n2u, double* __restrict__ n2v,
-    const double* __restrict__ umc, const double* __restrict__ vmc, const double* __restrict__ ud,
-    const double* __restrict__ vd, const double* __restrict__ qdot, const double* __restrict__ coriol,
-    const double* __restrict__ dmsf, const double* __restrict__ msfd,
-    const double* __restrict__ ub0, const double* __restrict__ ubt, const double* __restrict__ vb0,
-    const double* __restrict__ vbt, const int8_t* __restrict__ rgdt, const int16_t* __restrict__ ibdt,
-    const double* __restrict__ xkc, const double* __restrict__ psdotb,
-    const double* __restrict__ ubd, const double* __restrict__ vbd,
-    const double* __restrict__ xtv, const double* __restrict__ psdota, const double* __restrict__ psa,
-    const double* __restrict__ phi, double* uten, double* vten) {
+__global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restrict__ c,
+                                                  const StepState* __restrict__ s, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  const long p = (long)(k - 1) * g.plane + g.ix(j, i);
+  const uint32_t P8 = g.P8, L8 = g.L8;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
   if (!(in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))) {
-    n1u[p] = a1u[p]; n1v[p] = a1v[p]; n2u[p] = a2u[p]; n2v[p] = a2v[p];
+    ST(f.b1u, o3, LD(f.a1u, o3)); ST(f.b1v, o3, LD(f.a1v, o3));
+    ST(f.b2u, o3, LD(f.a2u, o3)); ST(f.b2v, o3, LD(f.a2v, o3));
     return;
   }
   const int kz = c->kz;
   const double dt = s->dt;
+  // decoupled winds (decouple :880-890, :895-994)
+#define UMC(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
+#define VMC(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
+#define UD(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
+#define VD(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
   // hadvuv (upstream, hydrostatic)
   double ut, vt;
   {
-    const double* ua = umc; const double* va = vmc;
-    const double ucmona = F3(ua, j, i + 1, k) + d_two * F3(ua, j, i, k) + F3(ua, j, i - 1, k);
-    double ucmonb = F3(ua, j + 1, i + 1, k) + d_two * F3(ua, j + 1, i, k) + F3(ua, j + 1, i - 1, k);
-    double ucmonc = F3(ua, j - 1, i + 1, k) + d_two * F3(ua, j - 1, i, k) + F3(ua, j - 1, i - 1, k);
-    const double vcmona = F3(va, j + 1, i, k) + d_two * F3(va, j, i, k) + F3(va, j - 1, i, k);
-    double vcmonb = F3(va, j + 1, i + 1, k) + d_two * F3(va, j, i + 1, k) + F3(va, j - 1, i + 1, k);
-    double vcmonc = F3(va, j + 1, i - 1, k) + d_two * F3(va, j, i - 1, k) + F3(va, j - 1, i - 1, k);
-    const double u0 = F3(ud, j, i, k), ue = F3(ud, j + 1, i, k), uw = F3(ud, j - 1, i, k);
-    const double un = F3(ud, j, i + 1, k), us = F3(ud, j, i - 1, k);
-    const double v0 = F3(vd, j, i, k), ve = F3(vd, j + 1, i, k), vw = F3(vd, j - 1, i, k);
-    const double vn = F3(vd, j, i + 1, k), vs = F3(vd, j, i - 1, k);
+    const double ucmona = UMC(0, 1) + d_two * UMC(0, 0) + UMC(0, -1);
+    double ucmonb = UMC(1, 1) + d_two * UMC(1, 0) + UMC(1, -1);
+    double ucmonc = UMC(-1, 1) + d_two * UMC(-1, 0) + UMC(-1, -1);
+    const double vcmona = VMC(1, 0) + d_two * VMC(0, 0) + VMC(-1, 0);
+    double vcmonb = VMC(1, 1) + d_two * VMC(0, 1) + VMC(-1, 1);
+    double vcmonc = VMC(1, -1) + d_two * VMC(0, -1) + VMC(-1, -1);
+    const double u0 = UD(0, 0), ue = UD(1, 0), uw = UD(-1, 0), un = UD(0, 1), us = UD(0, -1);
+    const double v0 = VD(0, 0), ve = VD(1, 0), vw = VD(-1, 0), vn = VD(0, 1), vs = VD(0, -1);
     const double ul = c->ul;
     const double ff1 = ul * (ue + u0), ff2 = ul * (uw + u0), ff3 = ul * (vn + v0), ff4 = ul * (vs + v0);
     ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
     ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
     vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
     vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
-    const double dm = F2(dmsf, j, i);
+    const double dm = LD(f.dmsf, o2);
     ut = d_zero - dm * ((ue + u0) * ucmonb - (u0 + uw) * ucmonc + (un + u0) * vcmonb - (u0 + us) * vcmonc);
     vt = d_zero - dm * ((ve + v0) * ucmonb - (v0 + vw) * ucmonc + (vn + v0) * vcmonb - (v0 + vs) * vcmonc);
   }
+#undef UMC
+#undef VMC
+#undef UD
+#undef VD
   // vadvuv: flux at interface k (from loop index k) then interface k+1 (loop index k+1)
   {
-#define QQ(K) (d_rfour * (F3(qdot, j, i, K) + F3(qdot, j, i - 1, K) + F3(qdot, j - 1, i, K) + F3(qdot, j - 1, i - 1, K)))
+#define QQ(dk) (d_rfour * (LD(f.qdot, O3K(0, 0, dk)) + LD(f.qdot, O3K(0, -1, dk)) + LD(f.qdot, O3K(-1, 0, dk)) + \
+                           LD(f.qdot, O3K(-1, -1, dk))))
     if (k >= 2) {
-      const double qq = QQ(k);
-      const double uu = qq * (c->twt1[k] * F3(a1u, j, i, k) + c->twt2[k] * F3(a1u, j, i, k - 1));
-      const double vv = qq * (c->twt1[k] * F3(a1v, j, i, k) + c->twt2[k] * F3(a1v, j, i, k - 1));
+      const double qq = QQ(0);
+      const double uu = qq * (c->twt1[k] * LD(f.a1u, o3) + c->twt2[k] * LD(f.a1u, O3K(0, 0, -1)));
+      const double vv = qq * (c->twt1[k] * LD(f.a1v, o3) + c->twt2[k] * LD(f.a1v, O3K(0, 0, -1)));
       ut = ut + uu * c->xds[k];
       vt = vt + vv * c->xds[k];
     }
     if (k + 1 <= kz) {
-      const double qq = QQ(k + 1);
-      const double uu = qq * (c->twt1[k + 1] * F3(a1u, j, i, k + 1) + c->twt2[k + 1] * F3(a1u, j, i, k));
-      const double vv = qq * (c->twt1[k + 1] * F3(a1v, j, i, k + 1) + c->twt2[k + 1] * F3(a1v, j, i, k));
+      const double qq = QQ(1);
+      const double uu = qq * (c->twt1[k + 1] * LD(f.a1u, O3K(0, 0, 1)) + c->twt2[k + 1] * LD(f.a1u, o3));
+      const double vv = qq * (c->twt1[k + 1] * LD(f.a1v, O3K(0, 0, 1)) + c->twt2[k + 1] * LD(f.a1v, o3));
       ut = ut - uu * c->xds[k];
       vt = vt - vv * c->xds[k];
     }
 #undef QQ
   }
   // curvature (hydrostatic Coriolis)
-  ut = ut + F2(coriol, j, i) * F3(a1v, j, i, k);
-  vt = vt - F2(coriol, j, i) * F3(a1u, j, i, k);
+  ut = ut + LD(f.coriol, o2) * LD(f.a1v, o3);
+  vt = vt - LD(f.coriol, o2) * LD(f.a1u, o3);
   // nudgeuv
-  if (F2(rgdt, j, i) > 0) {
+  if (f.rgdt[o2 >> 3] > 0) {
     const double xt = s->xbctime + dt;
     double xf, xg;
-    const int ib = F2(ibdt, j, i);
+    const int ib = f.ibdt[o2 >> 3];
     if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; } else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
-#define FGU(J, I) ((F3(ub0, J, I, k) + xt * F3(ubt, J, I, k)) - F3(a2u, J, I, k))
-#define FGV(J, I) ((F3(vb0, J, I, k) + xt * F3(vbt, J, I, k)) - F3(a2v, J, I, k))
-    ut = relax(ut, xf, xg, FGU(j, i), FGU(j - 1, i), FGU(j + 1, i), FGU(j, i - 1), FGU(j, i + 1));
-    vt = relax(vt, xf, xg, FGV(j, i), FGV(j - 1, i), FGV(j + 1, i), FGV(j, i - 1), FGV(j, i + 1));
+#define FGU(dj, di) ((LD(f.ub0, O3(dj, di)) + xt * LD(f.ubt, O3(dj, di))) - LD(f.a2u, O3(dj, di)))
+#define FGV(dj, di) ((LD(f.vb0, O3(dj, di)) + xt * LD(f.vbt, O3(dj, di))) - LD(f.a2v, O3(dj, di)))
+    ut = relax(ut, xf, xg, FGU(0, 0), FGU(-1, 0), FGU(1, 0), FGU(0, -1), FGU(0, 1));
+    vt = relax(vt, xf, xg, FGV(0, 0), FGV(-1, 0), FGV(1, 0), FGV(0, -1), FGV(0, 1));
 #undef FGU
 #undef FGV
   }
-  // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248)
+  // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248);
+  // ubd3d = atm2 * (1/psdotb) (mkslice), divided by msfd as diffu_d does
   {
-    double xkd = d_rfour * (F3(xkc, j, i, k) + F3(xkc, j - 1, i - 1, k) + F3(xkc, j - 1, i, k) + F3(xkc, j, i - 1, k));
-    xkd = xkd * c->rdxsq * F2(psdotb, j, i);
-#define UM(a, J, I) (F3(a, J, I, k) / F2(msfd, J, I))
+    double xkd = d_rfour * (LD(f.xkc, o3) + LD(f.xkc, O3(-1, -1)) + LD(f.xkc, O3(-1, 0)) + LD(f.xkc, O3(0, -1)));
+    xkd = xkd * c->rdxsq * LD(f.psdotb, o2);
+#define UM(a, dj, di) ((LD(a, O3(dj, di)) * LD(f.rpsdb, O2(dj, di))) / LD(f.msfd, O2(dj, di)))
     if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
-      ut = ut - xkd * (z4_c1 * (UM(ubd, j + 2, i) + UM(ubd, j - 2, i) + UM(ubd, j, i + 2) + UM(ubd, j, i - 2)) +
-                       z4_c2 * (UM(ubd, j + 1, i) + UM(ubd, j - 1, i) + UM(ubd, j, i + 1) + UM(ubd, j, i - 1)) +
-                       z4_c3 * (UM(ubd, j, i)));
-      vt = vt - xkd * (z4_c1 * (UM(vbd, j + 2, i) + UM(vbd, j - 2, i) + UM(vbd, j, i + 2) + UM(vbd, j, i - 2)) +
-                       z4_c2 * (UM(vbd, j + 1, i) + UM(vbd, j - 1, i) + UM(vbd, j, i + 1) + UM(vbd, j, i - 1)) +
-                       z4_c3 * (UM(vbd, j, i)));
+      ut = ut - xkd * (z4_c1 * (UM(f.a2u, 2, 0) + UM(f.a2u, -2, 0) + UM(f.a2u, 0, 2) + UM(f.a2u, 0, -2)) +
+                       z4_c2 * (UM(f.a2u, 1, 0) + UM(f.a2u, -1, 0) + UM(f.a2u, 0, 1) + UM(f.a2u, 0, -1)) +
+                       z4_c3 * (UM(f.a2u, 0, 0)));
+      vt = vt - xkd * (z4_c1 * (UM(f.a2v, 2, 0) + UM(f.a2v, -2, 0) + UM(f.a2v, 0, 2) + UM(f.a2v, 0, -2)) +
+                       z4_c2 * (UM(f.a2v, 1, 0) + UM(f.a2v, -1, 0) + UM(f.a2v, 0, 1) + UM(f.a2v, 0, -1)) +
+                       z4_c3 * (UM(f.a2v, 0, 0)));
     }
-#define LAPD()                                                                                              \
-  ut = ut + xkd * (z4_c1 * (UM(ubd, j + 1, i) + UM(ubd, j - 1, i) + UM(ubd, j, i + 1) + UM(ubd, j, i - 1)) + \
-                   z4_c2 * (UM(ubd, j, i)));                                                                \
-  vt = vt + xkd * (z4_c1 * (UM(vbd, j + 1, i) + UM(vbd, j - 1, i) + UM(vbd, j, i + 1) + UM(vbd, j, i - 1)) + \
-                   z4_c2 * (UM(vbd, j, i)));
+#define LAPD()                                                                                                  \
+  ut = ut + xkd * (z4_c1 * (UM(f.a2u, 1, 0) + UM(f.a2u, -1, 0) + UM(f.a2u, 0, 1) + UM(f.a2u, 0, -1)) +          \
+                   z4_c2 * (UM(f.a2u, 0, 0)));                                                                  \
+  vt = vt + xkd * (z4_c1 * (UM(f.a2v, 1, 0) + UM(f.a2v, -1, 0) + UM(f.a2v, 0, 1) + UM(f.a2v, 0, -1)) +          \
+                   z4_c2 * (UM(f.a2v, 0, 0)));
     if (g.bl && j == g.jdi1) { LAPD(); }
     if (g.br && j == g.jdi2) { LAPD(); }
     if (g.bb && i == g.idi1) { LAPD(); }
@@ -413,57 +347,72 @@ __global__ __launch_bounds__(256) void k_momentum(
 #undef LAPD
 #undef UM
   }
-  // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient)
+  // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient);
+  // tv = t * (1 + ep1 * qv) from the decoupled t and qv (decouple :1000-1016)
   {
-    double rtbar = d_rfour * (F3(xtv, j - 1, i - 1, k) + F3(xtv, j - 1, i, k) + F3(xtv, j, i - 1, k) + F3(xtv, j, i, k));
-    rtbar = c->rgas * rtbar * F2(psdota, j, i);
+    const double ep1 = c->ep1;
+    auto xtv = [&](int dj, int di) {
+      const double rp = LD(f.rpsa, O2(dj, di));
+      const double t = LD(f.a1t, O3(dj, di)) * rp;
+      const double qv = dmax(LD(f.a1qv, O3(dj, di)) * rp, MINQQ);
+      return t * (d_one + ep1 * qv);
+    };
+    double rtbar = d_rfour * (xtv(-1, -1) + xtv(-1, 0) + xtv(0, -1) + xtv(0, 0));
+    rtbar = c->rgas * rtbar * LD(f.psdota, o2);
     const double hs = c->hsigma[k], pt = c->ptop;
-    const double den = c->dx * F2(msfd, j, i);
-    const double p00 = F2(psa, j, i), p0m = F2(psa, j, i - 1), pm0 = F2(psa, j - 1, i), pmm = F2(psa, j - 1, i - 1);
+    const double den = c->dx * LD(f.msfd, o2);
+    const double p00 = LD(f.psa, o2), p0m = LD(f.psa, O2(0, -1)), pm0 = LD(f.psa, O2(-1, 0));
+    const double pmm = LD(f.psa, O2(-1, -1));
     ut = ut - rtbar * (log(d_half * (p00 + p0m) * hs + pt) - log(d_half * (pm0 + pmm) * hs + pt)) / den;
     vt = vt - rtbar * (log(d_half * (p00 + pm0) * hs + pt) - log(d_half * (pmm + p0m) * hs + pt)) / den;
-    const double den2 = c->dx2 * F2(msfd, j, i);
-    const double pd = F2(psdota, j, i);
-    ut = ut - pd * (F3(phi, j, i, k) + F3(phi, j, i - 1, k) - F3(phi, j - 1, i, k) - F3(phi, j - 1, i - 1, k)) / den2;
-    vt = vt - pd * (F3(phi, j, i, k) + F3(phi, j - 1, i, k) - F3(phi, j, i - 1, k) - F3(phi, j - 1, i - 1, k)) / den2;
+    const double den2 = c->dx2 * LD(f.msfd, o2);
+    const double pd = LD(f.psdota, o2);
+    const double f00 = LD(f.phi, o3), f0m = LD(f.phi, O3(0, -1)), fm0 = LD(f.phi, O3(-1, 0));
+    const double fmm = LD(f.phi, O3(-1, -1));
+    ut = ut - pd * (f00 + f0m - fm0 - fmm) / den2;
+    vt = vt - pd * (f00 + fm0 - f0m - fmm) / den2;
   }
   // totals (uphy = 0), forecast, RA filter
   ut = (d_zero + ut) + d_zero;
   vt = (d_zero + vt) + d_zero;
-  uten[p] = ut;
-  vten[p] = vt;
+  if (f.uten) { ST(f.uten, o3, ut); ST(f.vten, o3, vt); }
   const double g1 = c->gnu1;
-  const double u1 = a1u[p], u2 = a2u[p], v1 = a1v[p], v2 = a2v[p];
+  const double u1 = LD(f.a1u, o3), u2 = LD(f.a2u, o3), v1 = LD(f.a1v, o3), v2 = LD(f.a2v, o3);
   const double cu = u2 + dt * ut, cv = v2 + dt * vt;
   double d = g1 * (cu + u2 - d_two * u1);
-  n2u[p] = u1 + d;
-  n1u[p] = cu;
+  ST(f.b2u, o3, u1 + d);
+  ST(f.b1u, o3, cu);
   d = g1 * (cv + v2 - d_two * v1);
-  n2v[p] = v1 + d;
-  n1v[p] = cv;
+  ST(f.b2v, o3, v1 + d);
+  ST(f.b1v, o3, cv);
 }
 
 // ---------------------------------------------------------------------------------------
 // Scalar upstream flux-form advection (hadvt/hadvqv/hadvqx, Main/mod_advection.F90:337-386,
-// 547-596, 639-653) for one point; limiter 0 none, 1 t_extrema, 2 q_rel_extrema.
-__device__ __forceinline__ double hadv_point(const Geom& g, const Consts* c, const double* f, const double* umc,
-                                             const double* vmc, const double* psa, const double* xmsf,
-                                             int j, int i, int k, int limiter) {
-  const double uavg1 = F3(umc, j, i + 1, k) + F3(umc, j, i, k);
-  const double uavg2 = F3(umc, j + 1, i + 1, k) + F3(umc, j + 1, i, k);
-  const double vavg1 = F3(vmc, j + 1, i, k) + F3(vmc, j, i, k);
-  const double vavg2 = F3(vmc, j + 1, i + 1, k) + F3(vmc, j, i + 1, k);
-  const double ps = F2(psa, j, i);
+// 547-596, 639-653) at the thread's point; fv(dj,di) is the decoupled scalar; limiter 0 none,
+// 1 t_extrema, 2 q_rel_extrema.
+template <class FV>
+__device__ __forceinline__ double hadv_point(const Consts* c, const Fields& f, uint32_t o2, uint32_t o3,
+                                             uint32_t P8, FV fv, int limiter) {
+#define UMC(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
+#define VMC(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
+  const double uavg1 = UMC(0, 1) + UMC(0, 0);
+  const double uavg2 = UMC(1, 1) + UMC(1, 0);
+  const double vavg1 = VMC(1, 0) + VMC(0, 0);
+  const double vavg2 = VMC(1, 1) + VMC(0, 1);
+#undef UMC
+#undef VMC
+  const double ps = LD(f.psa, o2);
   const double ul = c->ul;
   const double f1 = d_half * ul * (uavg2 + uavg1) / ps;
   const double f2 = d_half * ul * (vavg2 + vavg1) / ps;
-  const double fc = F3(f, j, i, k), fw = F3(f, j - 1, i, k), fe = F3(f, j + 1, i, k);
-  const double fs = F3(f, j, i - 1, k), fn = F3(f, j, i + 1, k);
+  const double fc = fv(0, 0), fw = fv(-1, 0), fe = fv(1, 0);
+  const double fs = fv(0, -1), fn = fv(0, 1);
   const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
   const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
   const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
   const double fy2 = (d_one + f2) * fc + (d_one - f2) * fn;
-  double fg = -F2(xmsf, j, i) * (uavg2 * fx2 - uavg1 * fx1 + vavg2 * fy2 - vavg1 * fy1);
+  double fg = -LD(f.xmsf, o2) * (uavg2 * fx2 - uavg1 * fx1 + vavg2 * fy2 - vavg1 * fy1);
   if (limiter && c->stability_enhance) {
     double den, thr;
     if (limiter == 1) { den = ps; thr = c->t_extrema; } else { den = dmax(fc, DLOWVAL); thr = c->q_rel_extrema; }
@@ -479,17 +428,18 @@ __device__ __forceinline__ double hadv_point(const Geom& g, const Consts* c, con
   return fg;
 }
 
-// diffu_x (idiffu = 1) for one point, Main/mod_diffusion.F90:673-713 / 808-...
-__device__ __forceinline__ double diffu_x_point(const Geom& g, double ften, double xkcs, const double* f,
-                                                int j, int i, int k) {
+// diffu_x (idiffu = 1) at the thread's point, Main/mod_diffusion.F90:673-713 / 808-...;
+// fv(dj,di) is the mkslice field (atm2 * (1/psb), clipped for moisture).
+template <class FV>
+__device__ __forceinline__ double diffu_x_point(const Geom& g, double ften, double xkcs, FV fv, int j, int i) {
   if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2)) {
     ften = ften - d_one * xkcs *
-        (z4_c1 * (F3(f, j + 2, i, k) + F3(f, j - 2, i, k) + F3(f, j, i + 2, k) + F3(f, j, i - 2, k)) +
-         z4_c2 * (F3(f, j + 1, i, k) + F3(f, j - 1, i, k) + F3(f, j, i + 1, k) + F3(f, j, i - 1, k)) +
-         z4_c3 * F3(f, j, i, k));
+        (z4_c1 * (fv(2, 0) + fv(-2, 0) + fv(0, 2) + fv(0, -2)) +
+         z4_c2 * (fv(1, 0) + fv(-1, 0) + fv(0, 1) + fv(0, -1)) +
+         z4_c3 * fv(0, 0));
   }
 #define LAP2() ften = ften + d_one * xkcs * \
-    (z4_c1 * (F3(f, j + 1, i, k) + F3(f, j - 1, i, k) + F3(f, j, i + 1, k) + F3(f, j, i - 1, k)) + z4_c2 * F3(f, j, i, k))
+    (z4_c1 * (fv(1, 0) + fv(-1, 0) + fv(0, 1) + fv(0, -1)) + z4_c2 * fv(0, 0))
   if (g.bl && j == g.jci1) { LAP2(); }
   if (g.br && j == g.jci2) { LAP2(); }
   if (g.bb && i == g.ici1) { LAP2(); }
@@ -498,156 +448,163 @@ __device__ __forceinline__ double diffu_x_point(const Geom& g, double ften, doub
   return ften;
 }
 
-// Temperature: hadvt + vadv3d + adiabatic + nudge3d + diffu_x3d, forecast and RA filter
-// (Main/mod_tendency.F90:1327-1341, 1561-1575, 1469, 1525, 285-287, 368-374, 422).
-__global__ __launch_bounds__(256) void k_temperature(
-    Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s,
-    const double* __restrict__ a1t, const double* __restrict__ a2t, double* __restrict__ n1t,
-    double* __restrict__ n2t, const double* __restrict__ xt, const double* __restrict__ umc,
-    const double* __restrict__ vmc, const double* __restrict__ psa, const double* __restrict__ psb,
-    const double* __restrict__ xmsf, const double* __restrict__ qdot, const double* __restrict__ pten,
-    const double* __restrict__ ud, const double* __restrict__ vd, const double* __restrict__ msfx,
-    const double* __restrict__ xqv, const double* __restrict__ xtv, const double* __restrict__ rpsa,
-    const double* __restrict__ tb0, const double* __restrict__ tbt, const int8_t* __restrict__ rgcr,
-    const int16_t* __restrict__ ibcr, const double* __restrict__ xkc, const double* __restrict__ tb3d,
-    double* tten, double* omegad, double* xkcs_d) {
+// K4. Temperature: hadvt + vadv3d + adiabatic (omega on the fly) + nudge3d + diffu_x3d,
+// forecast and RA filter (Main/mod_tendency.F90:1200-1214, 1327-1341, 1561-1575, 1469, 1525,
+// 285-287, 368-374, 422).
+__global__ __launch_bounds__(256) void k_temperature(Geom g, const Consts* __restrict__ c,
+                                                     const StepState* __restrict__ s, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  const long p = (long)(k - 1) * g.plane + g.ix(j, i);
+  const uint32_t P8 = g.P8, L8 = g.L8;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
   if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
-    n1t[p] = a1t[p]; n2t[p] = a2t[p];
-    if (in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2)) xkcs_d[p] = xkc[p];
+    ST(f.b1t, o3, LD(f.a1t, o3)); ST(f.b2t, o3, LD(f.a2t, o3));
+    if (f.xkcs && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2)) ST(f.xkcs, o3, LD(f.xkc, o3));
     return;
   }
   const int kz = c->kz;
   const double dt = s->dt;
-  double td = d_zero + hadv_point(g, c, xt, umc, vmc, psa, xmsf, j, i, k, 1);
+  const double rp = LD(f.rpsa, o2);
+  double td = d_zero + hadv_point(c, f, o2, o3, P8,
+                                  [&](int dj, int di) { return LD(f.a1t, O3(dj, di)) * LD(f.rpsa, O2(dj, di)); }, 1);
   // vadv3d ind = 1 (Main/mod_advection.F90:771-783): pf/pb from psb (mkslice :263-271)
   {
-    const double pb = F2(psb, j, i), ptop = c->ptop, c287 = c->c287;
+    const double pb = LD(f.psb, o2), ptop = c->ptop, c287 = c->c287;
 #define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
 #define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
-#define DQ(K) (F3(qdot, j, i, K) * (c->twt1[K] * F3(a1t, j, i, K) * pow(PF(K) / PB(K), c287) + \
-                                  c->twt2[K] * F3(a1t, j, i, (K) - 1) * pow(PF(K) / PB((K) - 1), c287)))
-    if (k >= 2) td = td + DQ(k) * c->xds[k];
-    if (k + 1 <= kz) td = td - DQ(k + 1) * c->xds[k];
+#define DQ(K, dk) (LD(f.qdot, O3K(0, 0, dk)) * (c->twt1[K] * LD(f.a1t, O3K(0, 0, dk)) * pow(PF(K) / PB(K), c287) + \
+                                              c->twt2[K] * LD(f.a1t, O3K(0, 0, (dk) - 1)) * pow(PF(K) / PB((K) - 1), c287)))
+    if (k >= 2) td = td + DQ(k, 0) * c->xds[k];
+    if (k + 1 <= kz) td = td - DQ(k + 1, 1) * c->xds[k];
 #undef DQ
 #undef PB
 #undef PF
   }
-  // adiabatic (hydrostatic), cpmf = cpd*(1+0.8 qv)
-  const double om = omega_at(g, c, qdot, pten, ud, vd, psa, msfx, j, i, k);
-  omegad[p] = om;
+  // omega, Main/mod_tendency.F90:1200-1214 (ud/vd = atm1 * rpsda)
+  double om;
   {
-    const double rovcpm = c->rgas / (c->cpd * (d_one + 0.80 * F3(xqv, j, i, k)));
-    td = td + (om * rovcpm * F3(xtv, j, i, k)) / (c->ptop * F2(rpsa, j, i) + c->hsigma[k]);
+#define UD(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
+#define VD(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
+    const double dummy = d_one / (c->dx8 * LD(f.msfx, o2));
+    const double su = UD(0, 0) + UD(0, 1) + UD(1, 1) + UD(1, 0);
+    const double sv = VD(0, 0) + VD(0, 1) + VD(1, 1) + VD(1, 0);
+#undef UD
+#undef VD
+    const double x = su * (LD(f.psa, O2(1, 0)) - LD(f.psa, O2(-1, 0))) +
+                     sv * (LD(f.psa, O2(0, 1)) - LD(f.psa, O2(0, -1)));
+    om = d_half * (LD(f.qdot, O3K(0, 0, 1)) + LD(f.qdot, o3)) * LD(f.psa, o2) +
+         c->hsigma[k] * (LD(f.pten, o2) + x * dummy);
+  }
+  if (f.omega) ST(f.omega, o3, om);
+  // adiabatic (hydrostatic), cpmf = cpd*(1+0.8 qv)
+  {
+    const double t = LD(f.a1t, o3) * rp;
+    const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
+    const double tv = t * (d_one + c->ep1 * qv);
+    const double rovcpm = c->rgas / (c->cpd * (d_one + 0.80 * qv));
+    td = td + (om * rovcpm * tv) / (c->ptop * rp + c->hsigma[k]);
   }
   // nudge3d
-  if (F2(rgcr, j, i) > 0) {
+  if (f.rgcr[o2 >> 3] > 0) {
     const double xtb = s->xbctime + dt;
     double xf, xg;
-    nudge_coef(c, F2(ibcr, j, i), k, xf, xg);
-#define FGT(J, I) ((F3(tb0, J, I, k) + xtb * F3(tbt, J, I, k)) - F3(a2t, J, I, k))
-    td = relax(td, xf, xg, FGT(j, i), FGT(j - 1, i), FGT(j + 1, i), FGT(j, i - 1), FGT(j, i + 1));
+    nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
+#define FGT(dj, di) ((LD(f.tb0, O3(dj, di)) + xtb * LD(f.tbt, O3(dj, di))) - LD(f.a2t, O3(dj, di)))
+    td = relax(td, xf, xg, FGT(0, 0), FGT(-1, 0), FGT(1, 0), FGT(0, -1), FGT(0, 1));
 #undef FGT
   }
-  // diffu_x3d with xkc scaled as calc_coeff does (:241-243)
-  const double xkcs = xkc[p] * c->rdxsq * F2(psb, j, i);
-  xkcs_d[p] = xkcs;
-  td = diffu_x_point(g, td, xkcs, tb3d, j, i, k);
+  // diffu_x3d with xkc scaled as calc_coeff does (:241-243); tb3d = atm2 t * (1/psb)
+  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
+  if (f.xkcs) ST(f.xkcs, o3, xkcs);
+  td = diffu_x_point(g, td, xkcs, [&](int dj, int di) { return LD(f.a2t, O3(dj, di)) * LD(f.rpsb, O2(dj, di)); }, j, i);
   // totals (tphy = 0), forecast, RA filter
   const double tt = ((d_zero + td) + d_zero) + d_zero;
-  tten[p] = tt;
-  const double t1 = a1t[p], t2 = a2t[p];
+  if (f.tten) ST(f.tten, o3, tt);
+  const double t1 = LD(f.a1t, o3), t2 = LD(f.a2t, o3);
   const double ct = t2 + dt * tt;
   const double d = c->gnu1 * (ct + t2 - d_two * t1);
-  n2t[p] = t1 + d;
-  n1t[p] = ct;
+  ST(f.b2t, o3, t1 + d);
+  ST(f.b1t, o3, ct);
 }
 
-// Moisture tendencies and forecast (before the negative-value fix):
+// K5. Moisture tendencies and forecast (before the negative-value fix):
 // hadvqv + vadvqv + nudge4d3d + diffu_x4d (qv); hadvqx + vadv4d(ind=1) + diffu_x4d (qc)
 // (Main/mod_tendency.F90:1361-1392, 1470, 1526, 292-294, 332-349, 375-380).
-__global__ __launch_bounds__(256) void k_moisture(
-    Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s,
-    const double* __restrict__ a1qv, const double* __restrict__ a1qc,
-    const double* __restrict__ a2qv, const double* __restrict__ a2qc,
-    const double* __restrict__ xqv, const double* __restrict__ xqc, const double* __restrict__ umc,
-    const double* __restrict__ vmc, const double* __restrict__ psa, const double* __restrict__ psb,
-    const double* __restrict__ xmsf, const double* __restrict__ qdot, const double* __restrict__ qb0,
-    const double* __restrict__ qbt, const int8_t* __restrict__ rgcr, const int16_t* __restrict__ ibcr,
-    const double* __restrict__ xkc, const double* __restrict__ qvb, const double* __restrict__ qcb,
-    double* cqv, double* cqc, double* qvten, double* qcten) {
+__global__ __launch_bounds__(256) void k_moisture(Geom g, const Consts* __restrict__ c,
+                                                  const StepState* __restrict__ s, Fields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (j > g.jce2 || i > g.ice2) return;
-  const long p = (long)(k - 1) * g.plane + g.ix(j, i);
+  const uint32_t P8 = g.P8, L8 = g.L8;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
   if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
-    cqv[p] = a2qv[p];
-    cqc[p] = a2qc[p];
+    ST(f.cqv, o3, LD(f.a2qv, o3));
+    ST(f.cqc, o3, LD(f.a2qc, o3));
     return;
   }
   const int kz = c->kz;
   const double dt = s->dt;
-  const double ps = F2(psa, j, i);
+  const double ps = LD(f.psa, o2);
   // ---- qv
-  double tq = d_zero + hadv_point(g, c, xqv, umc, vmc, psa, xmsf, j, i, k, 2);
+  double tq = d_zero + hadv_point(c, f, o2, o3, P8, [&](int dj, int di) {
+    return dmax(LD(f.a1qv, O3(dj, di)) * LD(f.rpsa, O2(dj, di)), MINQQ); }, 2);
   {
     const double thr = MINQQ * ps;
-#define FGQ(K) ((F3(a1qv, j, i, K) > thr && F3(a1qv, j, i, (K) - 1) > thr) \
-                ? F3(a1qv, j, i, K) * pow(F3(a1qv, j, i, (K) - 1) / F3(a1qv, j, i, K), c->qcon[K]) : d_zero)
-    if (k >= 2) tq = tq + F3(qdot, j, i, k) * FGQ(k) * c->xds[k];
-    if (k + 1 <= kz) tq = tq - F3(qdot, j, i, k + 1) * FGQ(k + 1) * c->xds[k];
+#define QV(dk) LD(f.a1qv, O3K(0, 0, dk))
+#define FGQ(K, dk) ((QV(dk) > thr && QV((dk) - 1) > thr) ? QV(dk) * pow(QV((dk) - 1) / QV(dk), c->qcon[K]) : d_zero)
+    if (k >= 2) tq = tq + LD(f.qdot, o3) * FGQ(k, 0) * c->xds[k];
+    if (k + 1 <= kz) tq = tq - LD(f.qdot, O3K(0, 0, 1)) * FGQ(k + 1, 1) * c->xds[k];
 #undef FGQ
+#undef QV
   }
-  if (F2(rgcr, j, i) > 0) {
+  if (f.rgcr[o2 >> 3] > 0) {
     const double xtb = s->xbctime + dt;
     const double nfac = 1.0e3, rfac = d_one / nfac;
     double xf, xg;
-    nudge_coef(c, F2(ibcr, j, i), k, xf, xg);
-#define FGQ(J, I) (nfac * (F3(qb0, J, I, k) + xtb * F3(qbt, J, I, k)) - nfac * F3(a2qv, J, I, k))
-    const double f0 = FGQ(j, i), f1 = FGQ(j - 1, i), f2 = FGQ(j + 1, i), f3 = FGQ(j, i - 1), f4 = FGQ(j, i + 1);
+    nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
+#define FGQ(dj, di) (nfac * (LD(f.qb0, O3(dj, di)) + xtb * LD(f.qbt, O3(dj, di))) - nfac * LD(f.a2qv, O3(dj, di)))
+    const double f0 = FGQ(0, 0), f1 = FGQ(-1, 0), f2 = FGQ(1, 0), f3 = FGQ(0, -1), f4 = FGQ(0, 1);
 #undef FGQ
     tq = tq + rfac * (xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0));
   }
-  const double xkcs = xkc[p] * c->rdxsq * F2(psb, j, i);
-  tq = diffu_x_point(g, tq, xkcs, qvb, j, i, k);
+  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
+  tq = diffu_x_point(g, tq, xkcs, [&](int dj, int di) {
+    return dmax(LD(f.a2qv, O3(dj, di)) * LD(f.rpsb, O2(dj, di)), MINQQ); }, j, i);
   // ---- qc
-  double tc = d_zero + hadv_point(g, c, xqc, umc, vmc, psa, xmsf, j, i, k, 0);
+  double tc = d_zero + hadv_point(c, f, o2, o3, P8, [&](int dj, int di) {
+    return dmax(LD(f.a1qc, O3(dj, di)) * LD(f.rpsa, O2(dj, di)), d_zero); }, 0);
   {
     const double thr = MINQQ * MINQQ * ps;
-#define FGC(K) ((F3(qdot, j, i, K) > d_zero)                                                        \
-    ? ((F3(a1qc, j, i, (K) - 1) > thr) ? F3(qdot, j, i, K) * (c->twt1[K] * F3(a1qc, j, i, K) +       \
-                                         c->twt2[K] * F3(a1qc, j, i, (K) - 1)) : d_zero)            \
-    : ((F3(a1qc, j, i, K) > thr) ? F3(qdot, j, i, K) * (c->twt1[K] * F3(a1qc, j, i, K) +             \
-                                   c->twt2[K] * F3(a1qc, j, i, (K) - 1)) : d_zero))
-    if (k >= 2) tc = tc + FGC(k) * c->xds[k];
-    if (k + 1 <= kz) tc = tc - FGC(k + 1) * c->xds[k];
+#define QD(dk) LD(f.qdot, O3K(0, 0, dk))
+#define QC(dk) LD(f.a1qc, O3K(0, 0, dk))
+#define FGC(K, dk) ((QD(dk) > d_zero)                                                                   \
+    ? ((QC((dk) - 1) > thr) ? QD(dk) * (c->twt1[K] * QC(dk) + c->twt2[K] * QC((dk) - 1)) : d_zero)     \
+    : ((QC(dk) > thr) ? QD(dk) * (c->twt1[K] * QC(dk) + c->twt2[K] * QC((dk) - 1)) : d_zero))
+    if (k >= 2) tc = tc + FGC(k, 0) * c->xds[k];
+    if (k + 1 <= kz) tc = tc - FGC(k + 1, 1) * c->xds[k];
 #undef FGC
+#undef QC
+#undef QD
   }
-  tc = diffu_x_point(g, tc, xkcs, qcb, j, i, k);
+  tc = diffu_x_point(g, tc, xkcs, [&](int dj, int di) {
+    return dmax(LD(f.a2qc, O3(dj, di)) * LD(f.rpsb, O2(dj, di)), d_zero); }, j, i);
   tq = ((d_zero + tq) + d_zero) + d_zero;
   tc = ((d_zero + tc) + d_zero) + d_zero;
-  qvten[p] = tq;
-  qcten[p] = tc;
-  cqv[p] = a2qv[p] + dt * tq;
-  cqc[p] = a2qc[p] + dt * tc;
+  if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
+  ST(f.cqv, o3, LD(f.a2qv, o3) + dt * tq);
+  ST(f.cqc, o3, LD(f.a2qc, o3) + dt * tc);
 }
 
-// filter_ra_2d on p*, Main/mod_timefilter.F90 (called at Main/mod_tendency.F90:420)
-__global__ void k_ps_filter(Geom g, const Consts* __restrict__ c, double* psa, double* psb,
-                            const double* __restrict__ psc) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (j > g.jci2 || i > g.ici2) return;
-  const double d = c->gnu1 * (F2(psc, j, i) + F2(psb, j, i) - d_two * F2(psa, j, i));
-  F2(psb, j, i) = F2(psa, j, i) + d;
-  F2(psa, j, i) = F2(psc, j, i);
-}
-
-// Negative-moisture fix, Main/mod_tendency.F90:382-393.  The reference sweeps each (k,n)
-// plane in i-major / j-minor order and a fixed point reads already-fixed predecessors.  A
-// negative point whose four predecessors (j-1,i) (j-1,i-1) (j,i-1) (j+1,i-1) inside the
-// sweep are all non-negative only ever reads original values and is fixed here in parallel;
-// the rare others are flagged and resolved in sweep order by k_negfix_serial.
+// ---------------------------------------------------------------------------------------
+// K6. Negative-moisture fix + the RA filter of p* + the RAW filter of qv/qc, one pass
+// (Main/mod_tendency.F90:382-393, 420, 424-427; Main/mod_timefilter.F90 filter_ra_2d,
+// filter_raw_qv, filter_raw_4d).  The reference sweeps each (k,n) plane in i-major / j-minor
+// order and a fixed point reads already-fixed predecessors.  A negative point whose four
+// predecessors (j-1,i) (j-1,i-1) (j,i-1) (j+1,i-1) inside the sweep are all non-negative
+// only ever reads original values and is fixed (and filtered) here in parallel; the rare
+// others are flagged per plane and resolved in sweep order by the serial blocks of
+// k_split_project (nothing in splitf reads moisture).  Fixed values are stored only for
+// negative points: a fixed predecessor is (cq < 0 ? fq : cq).  p* is filtered on the fly by
+// every thread and stored by the k = 1 threads into the next p* buffers.
 __device__ __forceinline__ double negfix_sum(const Geom& g, const double* sv, const double* fx, int j, int i, int k,
                                              bool use_fixed) {
   double sum = 0.0;
@@ -656,98 +613,113 @@ __device__ __forceinline__ double negfix_sum(const Geom& g, const double* sv, co
       double v = F3(sv, jj, ii, k);
       if (use_fixed) {
         const bool pred = (ii < i) || (ii == i && jj < j);
-        if (pred && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2)) v = F3(fx, jj, ii, k);
+        if (pred && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) v = F3(fx, jj, ii, k);
       }
       sum = sum + fabs(v);
     }
   return 0.01 * sum / 9.0;
 }
 
-__global__ void k_negfix(Geom g, int kz, const double* __restrict__ cqv, const double* __restrict__ cqc,
-                         double* fqv, double* fqc, uint8_t* dep, int* depplane) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (j > g.jci2 || i > g.ici2) return;
-  for (int n = 0; n < 2; n++) {
-    const double* sv = n ? cqc : cqv;
-    double* fx = n ? fqc : fqv;
-    const long p = (long)(k - 1) * g.plane + g.ix(j, i);
-    const double v = sv[p];
-    uint8_t fl = 0;
-    double out = v;
-    if (v < d_zero) {
-      bool negpred = false;
+__device__ __forceinline__ bool negfix_dependent(const Geom& g, const double* sv, int j, int i, int k) {
 #define NEG(J, I) (in(J, g.jci1, g.jci2) && in(I, g.ici1, g.ici2) && F3(sv, J, I, k) < d_zero)
-      negpred = NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
+  return NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
 #undef NEG
-      if (negpred) {
-        fl = 1;
-        atomicOr(&depplane[n * kz + (k - 1)], 1);
-      } else {
-        out = negfix_sum(g, sv, fx, j, i, k, false);
-      }
-    }
-    fx[p] = out;
-    dep[(long)n * kz * g.plane + p] = fl;
+}
+
+// RAW filters of one point (filter_raw_qv / filter_raw_4d) with the filtered p*
+__device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, double o1, double o2v, double pa,
+                                           double pb, double& n1, double& n2) {
+  const double beta = 0.53;
+  if (n == 0) {
+    const double d = c->gnu1 * (fq + o2v - d_two * o1);
+    n2 = dmax(o1 + beta * d, MINQQ * pa);
+    n1 = dmax(fq + (beta - d_one) * d, MINQQ * pb);
+  } else {
+    const double d = c->gnu2 * (fq + o2v - d_two * o1);
+    double m = o1 + beta * d;
+    double q = fq + (beta - d_one) * d;
+    if (m < d_zero) m = d_zero;
+    if (q < d_zero) q = d_zero;
+    n2 = m;
+    n1 = q;
   }
 }
 
-__global__ void k_negfix_serial(Geom g, int kz, const double* __restrict__ cqv, const double* __restrict__ cqc,
-                                double* fqv, double* fqc, const uint8_t* __restrict__ dep, int* depplane) {
-  const int plane_id = blockIdx.x;          // n*kz + (k-1)
-  if (!depplane[plane_id]) return;
-  const int n = plane_id / kz, k = plane_id % kz + 1;
-  const double* sv = n ? cqc : cqv;
-  double* fx = n ? fqc : fqv;
-  const uint8_t* dp = dep + (long)n * kz * g.plane;
-  for (int i = g.ici1; i <= g.ici2; i++) {
-    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
-      const int j = j0 + (int)threadIdx.x;
-      const bool flagged = (j <= g.jci2) && dp[(long)(k - 1) * g.plane + g.ix(j, i)];
-      unsigned long long mask = __ballot(flagged);
-      if (threadIdx.x == 0) {
-        while (mask) {
-          const int b = __ffsll((long long)mask) - 1;
-          mask &= mask - 1;
-          const int jj = j0 + b;
-          F3(fx, jj, i, k) = negfix_sum(g, sv, fx, jj, i, k, true);
-        }
-      }
-      __syncthreads();
-    }
-  }
-  if (threadIdx.x == 0) depplane[plane_id] = 0;
-}
-
-// RAW filter on qv (filter_raw_qv) and qc (filter_raw_4d), Main/mod_timefilter.F90;
-// called at Main/mod_tendency.F90:424-427 with the already-filtered psa/psb.
-__global__ void k_moisture_filter(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1qv,
-                                  const double* __restrict__ a1qc, const double* __restrict__ a2qv,
-                                  const double* __restrict__ a2qc, double* n1qv, double* n1qc, double* n2qv,
-                                  double* n2qc, const double* __restrict__ fqv, const double* __restrict__ fqc,
-                                  const double* __restrict__ psa, const double* __restrict__ psb) {
+__global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  const long p = (long)(k - 1) * g.plane + g.ix(j, i);
-  if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
-    n1qv[p] = a1qv[p]; n1qc[p] = a1qc[p]; n2qv[p] = a2qv[p]; n2qc[p] = a2qc[p];
+  const uint32_t L8 = g.L8;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
+  const bool ci = in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+  double pa = LD(f.psa, o2), pb = LD(f.psb, o2);
+  if (ci) {
+    const double psc = LD(f.psc, o2);
+    const double d = c->gnu1 * (psc + pb - d_two * pa);
+    pb = pa + d;
+    pa = psc;
+  }
+  if (k == 1) { ST(f.bpsa, o2, pa); ST(f.bpsb, o2, pb); }
+  if (!ci) {
+    ST(f.b1qv, o3, LD(f.a1qv, o3)); ST(f.b1qc, o3, LD(f.a1qc, o3));
+    ST(f.b2qv, o3, LD(f.a2qv, o3)); ST(f.b2qc, o3, LD(f.a2qc, o3));
     return;
   }
-  const double beta = 0.53;
-  double d = c->gnu1 * (fqv[p] + a2qv[p] - d_two * a1qv[p]);
-  n2qv[p] = dmax(a1qv[p] + beta * d, MINQQ * F2(psa, j, i));
-  n1qv[p] = dmax(fqv[p] + (beta - d_one) * d, MINQQ * F2(psb, j, i));
-  d = c->gnu2 * (fqc[p] + a2qc[p] - d_two * a1qc[p]);
-  double m = a1qc[p] + beta * d;
-  double q = fqc[p] + (beta - d_one) * d;
-  if (m < d_zero) m = d_zero;
-  if (q < d_zero) q = d_zero;
-  n2qc[p] = m;
-  n1qc[p] = q;
+  for (int n = 0; n < 2; n++) {
+    const double* sv = n ? f.cqc : f.cqv;
+    double* fx = n ? f.fqc : f.fqv;
+    double v = LD(sv, o3);
+    if (v < d_zero) {
+      if (negfix_dependent(g, sv, j, i, k)) {
+        atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+        continue;                       // fixed and filtered by the serial sweep
+      }
+      v = negfix_sum(g, sv, fx, j, i, k, false);
+      ST(fx, o3, v);
+    }
+    double n1, n2;
+    raw_filter(c, n, v, LD(n ? f.a1qc : f.a1qv, o3), LD(n ? f.a2qc : f.a2qv, o3), pa, pb, n1, n2);
+    ST(n ? f.b1qc : f.b1qv, o3, n1);
+    ST(n ? f.b2qc : f.b2qv, o3, n2);
+  }
+}
+
+// serial sweep of one flagged (n,k) plane by one wavefront (see K6)
+__device__ void negfix_serial_plane(const Geom& g, const Consts* c, const QFix& q, int plane_id) {
+  if (!q.depplane[plane_id]) return;
+  const int kz = c->kz;
+  const int n = plane_id / kz, k = plane_id % kz + 1;
+  const double* sv = n ? q.cqc : q.cqv;
+  double* fx = n ? q.fqc : q.fqv;
+  const int lane = threadIdx.x;
+  for (int i = g.ici1; i <= g.ici2; i++) {
+    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
+      const int j = j0 + lane;
+      const bool flagged = (j <= g.jci2) && F3(sv, j, i, k) < d_zero && negfix_dependent(g, sv, j, i, k);
+      unsigned long long mask = __ballot(flagged);
+      if (lane == 0) {
+        while (mask) {
+          const int bidx = __ffsll((long long)mask) - 1;
+          mask &= mask - 1;
+          const int jj = j0 + bidx;
+          const double v = negfix_sum(g, sv, fx, jj, i, k, true);
+          F3(fx, jj, i, k) = v;
+          double n1, n2;
+          raw_filter(c, n, v, F3(n ? q.o1qc : q.o1qv, jj, i, k), F3(n ? q.o2qc : q.o2qv, jj, i, k),
+                     F2(q.psa, jj, i), F2(q.psb, jj, i), n1, n2);
+          F3(n ? q.n1qc : q.n1qv, jj, i, k) = n1;
+          F3(n ? q.n2qc : q.n2qv, jj, i, k) = n2;
+        }
+      }
+    }
+  }
+  if (lane == 0) q.depplane[plane_id] = 0;
 }
 
 // ---------------------------------------------------------------------------------------
-// splitf projections, Main/mod_split.F90:254-409: one thread per (j,i) column builds deld/delh
-// slots 1..3 and refreshes dstor/hstor.  slot(l, s) = base + ((s-1)*nsplit + l-1)*plane.
+// K7. splitf projections, Main/mod_split.F90:254-409: one thread per (j,i) column of blocks
+// [0, nproj) builds psdota (:259-260), deld/delh slots 1..3 and refreshes dstor/hstor;
+// slot(l, s) = base + ((s-1)*nsplit + l-1)*plane.  Blocks [nproj, nproj + 2 kz) run the
+// serial negative-moisture sweeps (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
                                 const double* __restrict__ a1v, const double* __restrict__ a2u,
@@ -755,10 +727,19 @@ __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const doub
                                 const double* __restrict__ a2t, const double* __restrict__ psa,
                                 const double* __restrict__ psb, const double* __restrict__ msfd,
                                 const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
-                                double* delh) {
-  const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int i = g.ide1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+                                double* delh, double* psdota, int nxp, int nproj, QFix qf) {
+  const int b = blockIdx.x;
+  if (b >= nproj) {
+    if (threadIdx.y == 0) negfix_serial_plane(g, c, qf, b - nproj);
+    return;
+  }
+  const int j = g.jde1 + (b % nxp) * 64 + (int)threadIdx.x;
+  const int i = g.ide1 + (b / nxp) * 4 + (int)threadIdx.y;
   if (j > g.jde2 || i > g.ide2) return;
+  {
+    double v;
+    if (psc2psd_at(g, psa, j, i, v)) F2(psdota, j, i) = v;
+  }
   const long q = g.ix(j, i);
   const bool ce = in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const double rdx2 = d_one / c->dx2;
@@ -986,8 +967,14 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
 __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                 const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
-                                double* a2t, double* a1u, double* a1v, double* a2u, double* a2v) {
+                                double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
+                                int advance) {
   THREAD_POINT(g.jde1, g.ide1);
+  // rcmtimer%advance + dt switch, Main/mod_tendency.F90:608-616 (nothing here reads the clock)
+  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
+    s->lcount = s->lcount + 1;
+    if (s->lcount == 2) s->dt = d_two * c->dtsec;
+  }
   if (j > g.jde2 || i > g.ide2) return;
   const long q = g.ix(j, i);
   const long p = (long)(k - 1) * g.plane + q;
@@ -1025,12 +1012,6 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
   }
 }
 #undef SLOT
-
-// rcmtimer%advance + dt switch, Main/mod_tendency.F90:608-616
-__global__ void k_advance_time(StepState* s, double dtsec) {
-  s->lcount = s->lcount + 1;
-  if (s->lcount == 2) s->dt = d_two * dtsec;
-}
 
 // ---------------------------------------------------------------------------------------
 // bdyval, Main/mod_bdycod.F90:1109-1529 (+ bdyuv :896-1061).  Slice order:
@@ -1096,8 +1077,11 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
 }
 
 // bdyuv corner fills, Main/mod_bdycod.F90:1030-1061
-__global__ void k_bdyval_corners(Geom g, int kz, Slices sl, long slen) {
+// + the boundary clock advance xbctime += dtsec (Main/mod_bdycod.F90:2566), after every
+// tile's k_bdyval_set
+__global__ void k_bdyval_corners(Geom g, int kz, Slices sl, long slen, StepState* s, double dtsec, int advance) {
   const int k = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (advance && k == 1) s->xbctime = s->xbctime + dtsec;
   if (k > kz) return;
   if (g.bt && g.bl) {
     SLI(sl.s[1], g.ide2, k) = SLJ(sl.s[10], g.jdi1, k); SLI(sl.s[5], g.ide2, k) = SLJ(sl.s[14], g.jdi1, k);
@@ -1150,8 +1134,6 @@ __global__ void k_bdyval_qc_sn(Geom g, int kz, double* a1qc, const double* __res
     F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * F2(psa, j, g.ice2);
   }
 }
-
-__global__ void k_bdyval_time(StepState* s, double dtsec) { s->xbctime = s->xbctime + dtsec; }
 
 // ---------------------------------------------------------------------------------------
 // static derived fields: Main/mod_params.F90:1993-2001 (xmsf, dmsf), Main/mod_diffusion.F90:

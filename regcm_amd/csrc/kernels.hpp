@@ -1,4 +1,4 @@
-// kernels.hpp -- declarations of the device kernels in kernels.hip (generated list).
+// kernels.hpp -- device kernels of kernels.hip and the argument blocks they share.
 #pragma once
 #include "engine.hpp"
 
@@ -22,35 +22,62 @@ struct SegList {
 // boundary slices, order documented at k_bdyval_set
 struct Slices { double* s[16]; };
 
-__global__ void k_surface_pressures(Geom g, const double* __restrict__ psa, const double* __restrict__ psb, double* rpsa, double* rpsb, double* psdota, double* psdotb);
-__global__ void k_psc2psd(Geom g, const double* __restrict__ pc, double* pd);
-__global__ void k_decouple(Geom g, const double* __restrict__ a1u, const double* __restrict__ a1v, const double* __restrict__ a1t, const double* __restrict__ a1qv, const double* __restrict__ a1qc, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ rpsa, double* rpsda, double* umc, double* vmc, double* ud, double* vd, double* xt, double* xqv, double* xqc, double* xtv, double ep1);
-__global__ void k_omega_col(Geom g, const Consts* __restrict__ c, const double* __restrict__ umc, const double* __restrict__ vmc, const double* __restrict__ msfx, const double* __restrict__ rpsa, double* pten, double* qdot);
-__global__ void k_mkslice(Geom g, const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a2t, const double* __restrict__ a2qv, const double* __restrict__ a2qc, const double* __restrict__ psb, const double* __restrict__ psdotb, double* ubd, double* vbd, double* tb3d, double* qvb, double* qcb);
-__global__ void k_new_pressure(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, const double* __restrict__ psa, const double* __restrict__ psb, const double* __restrict__ pb0, const double* __restrict__ pbt, const int8_t* __restrict__ rgcr, const int16_t* __restrict__ ibcr, const double* __restrict__ pten, double* ptenn, double* psc, double* rpsc, double* red);
-__global__ void k_reduce_noise(const double* __restrict__ red, int nblk, StepState* s);
-__global__ void k_calc_coeff(Geom g, const Consts* __restrict__ c, const double* __restrict__ ubd, const double* __restrict__ vbd, const double* __restrict__ hgfact, double* xkc);
-__global__ void k_phi_col(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1t, const double* __restrict__ xqv, const double* __restrict__ xqc, const double* __restrict__ psa, const double* __restrict__ rpsa, const double* __restrict__ ht, double* phi);
-__global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, const double* __restrict__ a1u, const double* __restrict__ a1v, const double* __restrict__ a2u, const double* __restrict__ a2v, double* __restrict__ n1u, double* __restrict__ n1v, double* __restrict__ n2u, double* __restrict__ n2v, const double* __restrict__ umc, const double* __restrict__ vmc, const double* __restrict__ ud, const double* __restrict__ vd, const double* __restrict__ qdot, const double* __restrict__ coriol, const double* __restrict__ dmsf, const double* __restrict__ msfd, const double* __restrict__ ub0, const double* __restrict__ ubt, const double* __restrict__ vb0, const double* __restrict__ vbt, const int8_t* __restrict__ rgdt, const int16_t* __restrict__ ibdt, const double* __restrict__ xkc, const double* __restrict__ psdotb, const double* __restrict__ ubd, const double* __restrict__ vbd, const double* __restrict__ xtv, const double* __restrict__ psdota, const double* __restrict__ psa, const double* __restrict__ phi, double* uten, double* vten);
-__global__ void k_temperature(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, const double* __restrict__ a1t, const double* __restrict__ a2t, double* __restrict__ n1t, double* __restrict__ n2t, const double* __restrict__ xt, const double* __restrict__ umc, const double* __restrict__ vmc, const double* __restrict__ psa, const double* __restrict__ psb, const double* __restrict__ xmsf, const double* __restrict__ qdot, const double* __restrict__ pten, const double* __restrict__ ud, const double* __restrict__ vd, const double* __restrict__ msfx, const double* __restrict__ xqv, const double* __restrict__ xtv, const double* __restrict__ rpsa, const double* __restrict__ tb0, const double* __restrict__ tbt, const int8_t* __restrict__ rgcr, const int16_t* __restrict__ ibcr, const double* __restrict__ xkc, const double* __restrict__ tb3d, double* tten, double* omegad, double* xkcs_d);
-__global__ void k_moisture(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, const double* __restrict__ a1qv, const double* __restrict__ a1qc, const double* __restrict__ a2qv, const double* __restrict__ a2qc, const double* __restrict__ xqv, const double* __restrict__ xqc, const double* __restrict__ umc, const double* __restrict__ vmc, const double* __restrict__ psa, const double* __restrict__ psb, const double* __restrict__ xmsf, const double* __restrict__ qdot, const double* __restrict__ qb0, const double* __restrict__ qbt, const int8_t* __restrict__ rgcr, const int16_t* __restrict__ ibcr, const double* __restrict__ xkc, const double* __restrict__ qvb, const double* __restrict__ qcb, double* cqv, double* cqc, double* qvten, double* qcten);
-__global__ void k_ps_filter(Geom g, const Consts* __restrict__ c, double* psa, double* psb, const double* __restrict__ psc);
-__global__ void k_negfix(Geom g, int kz, const double* __restrict__ cqv, const double* __restrict__ cqc, double* fqv, double* fqc, uint8_t* dep, int* depplane);
-__global__ void k_negfix_serial(Geom g, int kz, const double* __restrict__ cqv, const double* __restrict__ cqc, double* fqv, double* fqc, const uint8_t* __restrict__ dep, int* depplane);
-__global__ void k_moisture_filter(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1qv, const double* __restrict__ a1qc, const double* __restrict__ a2qv, const double* __restrict__ a2qc, double* n1qv, double* n1qc, double* n2qv, double* n2qc, const double* __restrict__ fqv, const double* __restrict__ fqc, const double* __restrict__ psa, const double* __restrict__ psb);
-__global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v, const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t, const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb, const double* __restrict__ msfd, const double* __restrict__ mapf, double* dstor, double* hstor, double* deld, double* delh);
+// Every device buffer of one tile for one ping-pong parity: a* are the current time levels,
+// b* the buffers the fused update kernels write the next time levels into.  Passed by value
+// (kernel argument segment -> SGPRs); all fields share the frame, so one 32-bit byte offset
+// per point addresses every one of them.  Diagnostic pointers are null when diagnostics are
+// off (rcmdyn_set_diagnostics).
+struct Fields {
+  double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc, *psa, *psb;
+  double *b1u, *b1v, *b1t, *b1qv, *b1qc, *b2u, *b2v, *b2t, *b2qv, *b2qc, *bpsa, *bpsb;
+  double *msfx, *msfd, *coriol, *ht, *xmsf, *dmsf, *hgfact, *mapf;
+  const int8_t *rgcr, *rgdt;
+  const int16_t *ibcr, *ibdt;
+  double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
+  double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten, *ptenn;
+  double *qdot, *xkc, *phi, *cqv, *cqc, *fqv, *fqc;
+  int* depplane;
+  double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
+  double* red;                 // engine-wide reduction partials
+  unsigned* ticket;            // engine-wide block ticket for the last-block reduction
+  int red_off, red_total;      // this launch's first partial, partials over all tiles
+};
+
+// serial negative-moisture fix-up of k_split_project's extra blocks: the q fields before
+// (o*) and after (n*) the RAW filter, the unfiltered forecasts (c*) and fixed values (f*)
+struct QFix {
+  const double *cqv, *cqc;
+  double *fqv, *fqc;
+  const double *o1qv, *o1qc, *o2qv, *o2qc;
+  double *n1qv, *n1qc, *n2qv, *n2qc;
+  const double *psa, *psb;
+  int* depplane;
+};
+
+__global__ void k_surface_pressures(Geom g, Fields f);
+__global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxa, int nya, int nba,
+                          int nxb);
+__global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_temperature(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_moisture(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
+__global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
+                                const double* __restrict__ a1v, const double* __restrict__ a2u,
+                                const double* __restrict__ a2v, const double* __restrict__ a1t,
+                                const double* __restrict__ a2t, const double* __restrict__ psa,
+                                const double* __restrict__ psb, const double* __restrict__ msfd,
+                                const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
+                                double* delh, double* psdota, int nxp, int nproj, QFix qf);
 __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
-__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v);
-__global__ void k_advance_time(StepState* s, double dtsec);
+__global__ void k_spstep_fused(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
+__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance);
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1u, double* a1v, double* a1t, double* a1qv, double* a1qc, double* a2u, double* a2v, double* a2t, double* a2qv, double* a2qc, double* psa, double* psb, const double* __restrict__ ub0, const double* __restrict__ ubt, const double* __restrict__ vb0, const double* __restrict__ vbt, const double* __restrict__ tb0, const double* __restrict__ tbt, const double* __restrict__ qb0, const double* __restrict__ qbt, const double* __restrict__ pb0, const double* __restrict__ pbt, Slices sl, long slen);
-__global__ void k_bdyval_corners(Geom g, int kz, Slices sl, long slen);
+__global__ void k_bdyval_corners(Geom g, int kz, Slices sl, long slen, StepState* s, double dtsec, int advance);
 __global__ void k_bdyval_qc_we(Geom g, int kz, double* a1qc, const double* __restrict__ psa, Slices sl, long slen);
 __global__ void k_bdyval_qc_sn(Geom g, int kz, double* a1qc, const double* __restrict__ psa, Slices sl, long slen);
-__global__ void k_bdyval_time(StepState* s, double dtsec);
 __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu_hgtf, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ ht, double* xmsf, double* dmsf, double* hgfact, double* mapf);
-__global__ void k_spstep_fused(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
 __global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack);
 
 }  // namespace rcm

@@ -27,7 +27,7 @@ EXPORTED = [
     "rcmdyn_create", "rcmdyn_destroy", "rcmdyn_last_error", "rcmdyn_set_nproc",
     "rcmdyn_tile_extent", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
-    "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms",
+    "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
 ]
 
 
@@ -63,6 +63,8 @@ def lib():
     L.rcmdyn_diagnostics.argtypes = [P, dp]
     L.rcmdyn_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
     L.rcmdyn_last_step_ms.argtypes = [P, dp]
+    L.rcmdyn_set_diagnostics.argtypes = [P, i32]
+    L.rcmdyn_kernel_times.argtypes = [P, i32, i32, ctypes.c_char_p, ctypes.POINTER(i32), dp, ctypes.POINTER(i32)]
     _lib = L
     return L
 
@@ -163,3 +165,20 @@ class DynCore:
         v = ctypes.c_double()
         self._check(lib().rcmdyn_last_step_ms(self.h, ctypes.byref(v)))
         return v.value
+
+    def set_diagnostics(self, on: bool = True):
+        self._check(lib().rcmdyn_set_diagnostics(self.h, 1 if on else 0))
+
+    def kernel_times(self, nsteps: int, cap: int = 64) -> dict:
+        """{kernel name: (launches, average ms per launch)} over nsteps eager steps."""
+        names = ctypes.create_string_buffer(cap * 48)
+        launches = (ctypes.c_int32 * cap)()
+        avg = (ctypes.c_double * cap)()
+        n = ctypes.c_int32()
+        self._check(lib().rcmdyn_kernel_times(self.h, nsteps, cap, names, launches, avg, ctypes.byref(n)))
+        raw = names.raw
+        out = {}
+        for q in range(n.value):
+            nm = raw[q * 48:(q + 1) * 48].split(b"\0", 1)[0].decode()
+            out[nm] = (int(launches[q]), float(avg[q]))
+        return out

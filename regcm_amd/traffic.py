@@ -1,0 +1,57 @@
+"""Algorithmic HBM bytes of the dyn-step kernels (the roofline numerators of bench.py).
+
+"Algorithmic" = the compulsory traffic of a kernel: every field it must read or write,
+counted once, at 8 bytes per fp64 value, over the points it updates.  Units are grid
+points: N3 = jx*iy*kz (one 3-D field), N2 = jx*iy (one 2-D field); f_b is the fraction of
+points in the boundary-relaxation band (the nudging kernels read b0/bt only there).
+Whole-step total B_h is SURVEY.md section 8(d): 8 [N3 (20 + 8 f_b) + N2 (19 + 2 f_b)].
+
+Per-kernel field counts (reads + writes of 3-D fields, 2-D fields) follow the kernels of
+regcm_amd/csrc/kernels.hip with tendency diagnostics off:
+  k_momentum    reads atm1 u,v,t,qv, atm2 u,v, qdot, xkc, phi (9) + u,v b0/bt in band (4 f_b);
+                writes next atm1/atm2 u,v (4); 2-D: msfd msfx-derived dmsf coriol rpsa rpsda rpsdb
+                psa psdota psdotb (9)
+  k_temperature reads atm1 t,u,v,qv, atm2 t, qdot, xkc (7) + t b0/bt in band (2 f_b);
+                writes next atm1/atm2 t (2); 2-D: 9
+  k_moisture    reads atm1 qv,qc,u,v, atm2 qv,qc, qdot, xkc (8) + q b0/bt in band (2 f_b);
+                writes cqv, cqc (2); 2-D: 7
+  k_columns     reads atm1 u,v,t,qv,qc, atm2 u,v (7); writes qdot, phi, xkc (3); 2-D: 12
+  k_qfilter     reads cqv,cqc, atm1/atm2 qv,qc (6); writes next atm1/atm2 qv,qc (4); 2-D: 5
+  k_split_project reads atm1/atm2 u,v,t (6); 2-D: 3 nsplit slots x 2 + 8
+  k_split_correct read-modify-write atm1/atm2 t,u,v (12); 2-D: 2 nsplit + 4
+"""
+from __future__ import annotations
+
+
+def band_fraction(jx: int, iy: int, nspgx: int) -> float:
+    return 1.0 - ((jx - 1 - 2 * nspgx) * (iy - 1 - 2 * nspgx)) / ((jx - 1) * (iy - 1))
+
+
+# (3-D fields, 3-D fields in the band only, 2-D fields)
+KERNEL_FIELDS = {
+    "k_momentum": (13, 4, 9),
+    "k_temperature": (9, 2, 9),
+    "k_moisture": (10, 2, 7),
+    "k_columns": (10, 0, 12),
+    "k_qfilter": (10, 0, 5),
+    "k_split_project": (6, 0, 20),
+    "k_split_correct": (12, 0, 8),
+}
+
+
+def kernel_bytes(name: str, jx: int, iy: int, kz: int, nspgx: int) -> float | None:
+    """Algorithmic bytes of one launch of `name` over a jx x iy x kz domain (None if the
+    kernel has no entry)."""
+    if name not in KERNEL_FIELDS:
+        return None
+    f3, fband, f2 = KERNEL_FIELDS[name]
+    n3, n2 = jx * iy * kz, jx * iy
+    fb = band_fraction(jx, iy, nspgx)
+    return 8.0 * (n3 * (f3 + fband * fb) + n2 * f2)
+
+
+def step_bytes(jx: int, iy: int, kz: int, nspgx: int) -> float:
+    """SURVEY.md section 8(d) B_h: compulsory HBM bytes of one hydrostatic step."""
+    n3, n2 = jx * iy * kz, jx * iy
+    fb = band_fraction(jx, iy, nspgx)
+    return 8.0 * (n3 * (20 + 8 * fb) + n2 * (19 + 2 * fb))

@@ -48,6 +48,7 @@ def test_init_bdyval_exact(c1_data):
 def test_one_tend_intermediates(c1_data):
     rc, data = c1_data
     o, e = make_pair(rc, data)
+    e.set_diagnostics(True)
     o.tend()
     e.tend()
     exact = ["QDOT", "PSDOTA", "XKC", "OMEGA", "PTEN", "PSC", "QCTEN"]
@@ -122,3 +123,81 @@ def test_c2_ten_steps():
     for name in STATE_FIELDS:
         err = relerr(e.get(name), o.get(name), rc, name)
         assert err < 1e-10, (name, err)
+
+
+def test_diagnostics_switch_is_transparent(c1_data):
+    """Tendency diagnostics on/off give identical prognostic results; off refuses gets."""
+    rc, data = c1_data
+    from regcm_amd.dycore import DynCore, EngineError
+    e1 = DynCore(rc, data["split"])
+    e2 = DynCore(rc, data["split"])
+    e2.set_diagnostics(True)
+    for e in (e1, e2):
+        e.put_state(data["state"])
+        e.bdyval()
+        e.step(4)
+    for name in STATE_FIELDS:
+        assert np.array_equal(e1.get(name), e2.get(name)), name
+    with pytest.raises(EngineError):
+        e1.get("TTEN")
+    assert np.isfinite(e2.get("TTEN")).all()
+
+
+def test_kernel_times_hook(c1_data):
+    """rcmdyn_kernel_times runs real (eager) steps and reports every kernel of the step."""
+    rc, data = c1_data
+    from regcm_amd.dycore import DynCore
+    e1 = DynCore(rc, data["split"])
+    e2 = DynCore(rc, data["split"])
+    for e in (e1, e2):
+        e.put_state(data["state"])
+        e.bdyval()
+    kt = e1.kernel_times(3)
+    e2.step(3)
+    for name in STATE_FIELDS:
+        assert np.array_equal(e1.get(name), e2.get(name)), name
+    for k in ("k_momentum", "k_temperature", "k_moisture", "k_columns", "k_qfilter", "k_split_project",
+              "k_spstep_fused", "k_split_correct", "k_bdyval_set"):
+        assert k in kt and kt[k][0] == 3 and kt[k][1] > 0.0, k
+
+
+def _dependent_negatives(cq, rc):
+    """(k, i, j) cross points of the interior where the reference's serial sweep reads an
+    already-fixed predecessor (Main/mod_tendency.F90:382-393)."""
+    jci = slice(1, rc.jx - 2)
+    ici = slice(1, rc.iy - 2)
+    neg = np.zeros_like(cq, dtype=bool)
+    neg[:, ici, jci] = cq[:, ici, jci] < 0
+    dep = np.zeros_like(neg)
+    p = np.pad(neg, ((0, 0), (1, 1), (1, 1)))
+    # predecessors (j-1,i) (j-1,i-1) (j,i-1) (j+1,i-1) in padded coordinates (+1)
+    pred = p[:, 1:-1, :-2] | p[:, :-2, :-2] | p[:, :-2, 1:-1] | p[:, :-2, 2:]
+    dep = neg & pred
+    return int(dep.sum())
+
+
+def test_negative_moisture_serial_sweep(c1_data):
+    """A state with clusters of negative qc forecasts: the parallel fix + serial sweep
+    reproduce the reference's order-dependent fix bit-for-bit."""
+    rc, data = c1_data
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    st = {k: v.copy() for k, v in data["state"].items()}
+    rng = np.random.default_rng(7)
+    ps = st["PSA"][0]
+    pat = rng.uniform(0.0, 2.0e-5, size=st["ATM1_QC"].shape) * (rng.uniform(size=st["ATM1_QC"].shape) < 0.5)
+    st["ATM1_QC"] = pat * ps[None]
+    st["ATM2_QC"] = np.zeros_like(pat)
+    o = OracleCore(rc, data["split"])
+    e = DynCore(rc, data["split"])
+    e.set_diagnostics(True)
+    for c in (o, e):
+        c.put_state(st)
+        c.bdyval()
+        c.tend()
+    dt = o.get_time()[1]
+    cqc = dt * o.get("QCTEN")               # atm2 qc is zero in the interior: cqc = 0 + dt * qcten
+    assert _dependent_negatives(cqc, rc) > 0
+    for name in ("ATM1_QC", "ATM2_QC", "QCTEN"):
+        a, b = e.get(name), o.get(name)
+        assert np.array_equal(a[:, 1:rc.iy - 2, 1:rc.jx - 2], b[:, 1:rc.iy - 2, 1:rc.jx - 2]), name
