@@ -207,7 +207,6 @@ struct rcmdyn_engine {
   long slen = 0;
   long staging_cap = 0;
   double* red = nullptr;     // noise-sum partials of every tile (k_columns)
-  unsigned* ticket = nullptr;
   int red_total = 0;
   bool diag = false;         // write the per-tend diagnostic fields
   KernelProf* prof = nullptr;  // set while rcmdyn_kernel_times runs
@@ -337,7 +336,7 @@ struct rcmdyn_engine {
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     // column blocks of k_columns (one noise partial each)
-    t.nred = ((g.jde2 - g.jde1 + 64) / 64) * ((g.ide2 - g.ide1 + 4) / 4);
+    t.nred = ((g.jde2 - g.jde1 + 64) / 64) * (g.ide2 - g.ide1 + 1);
     t.red_off = red_total;
     red_total += t.nred;
     // boundary masks
@@ -388,8 +387,6 @@ struct rcmdyn_engine {
       setup_tile(tiles[t], cfg.tile_first + t);
     }
     HIPCHK(hipMalloc(&red, sizeof(double) * 2 * (size_t)(red_total + 1)));
-    HIPCHK(hipMalloc(&ticket, sizeof(unsigned)));
-    HIPCHK(hipMemset(ticket, 0, sizeof(unsigned)));
     if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg, stream));
   }
 
@@ -403,7 +400,7 @@ struct rcmdyn_engine {
     if (dc) hipFree(dc);
     if (ds) hipFree(ds);
     if (red) hipFree(red);
-    if (ticket) hipFree(ticket);
+
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -701,6 +698,9 @@ struct rcmdyn_engine {
     }
   }
 
+  // dynamic LDS of the two-phase column kernels: 4 x kz x 64 doubles
+  size_t col_lds() const { return sizeof(double) * 4 * 64 * (size_t)cfg.kz; }
+
   // all buffers of one tile for its current parity (see Fields)
   Fields fields(Tile& t) {
     const int c = t.cur, n = 1 - c;
@@ -724,7 +724,7 @@ struct rcmdyn_engine {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
       f.omega = t.omega; f.xkcs = t.xkcs;
     }
-    f.red = red; f.ticket = ticket; f.red_off = t.red_off; f.red_total = red_total;
+    f.red = red; f.red_off = t.red_off;
     return f;
   }
 
@@ -747,7 +747,7 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const int nxa = (g.jce2 - g.jce1 + 64) / 64, nya = (g.ice2 - g.ice1 + 4) / 4;
       const int nba = nxa * nya * kz, nxb = (g.jde2 - g.jde1 + 64) / 64;
-      KLAUNCH(k_columns, dim3(nba + t.nred), dim3(256), 0, stream, g, dc, ds, fields(t), nxa, nya, nba,
+      KLAUNCH(k_columns, dim3(nba + t.nred), dim3(256), col_lds(), stream, g, dc, ds, fields(t), nxa, nya, nba,
                          nxb);
     });
     xch(FK::QDOT, kz + 1, 1, 0);
@@ -776,8 +776,8 @@ struct rcmdyn_engine {
       const int c = t.cur, o = 1 - c;
       QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
              t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.depplane};
-      const int nxp = (g.jde2 - g.jde1 + 64) / 64, nproj = nxp * ((g.ide2 - g.ide1 + 4) / 4);
-      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), BLK, 0, stream, g, dc, t.a1u[c], t.a1v[c],
+      const int nxp = (g.jde2 - g.jde1 + 64) / 64, nproj = nxp * (g.ide2 - g.ide1 + 1);
+      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(256), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
     });
@@ -815,7 +815,7 @@ struct rcmdyn_engine {
       const int c = t.cur;
       KLAUNCH(k_split_correct, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
                          dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
-                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()));
+                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total);
     }
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
@@ -847,28 +847,17 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_bdyval_set, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, ds,
+      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0,
+              stream, g, ds,
                          t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
                          t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0,
                          t.qbt, t.pb0, t.pbt, slices(t), slen);
     });
-    for (size_t q = 0; q < tiles.size(); q++)
-      KLAUNCH(k_bdyval_corners, dim3(1), dim3(64), 0, stream, tiles[q].g, kz, slices(tiles[q]), slen, ds,
-                         cfg.dtsec, (int)(q + 1 == tiles.size()));
     xch_slices();
-    if (!cfg.present_qc) {
-      each([&](Tile& t) {
-        const Geom& g = t.g;
-        if (g.bl || g.br)
-          KLAUNCH(k_bdyval_qc_we, dim3((g.ice2 - g.ice1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
-                             t.a1qc[t.cur], t.psa_[t.cur], slices(t), slen);
-      });
-      each([&](Tile& t) {
-        const Geom& g = t.g;
-        if (g.bb || g.bt)
-          KLAUNCH(k_bdyval_qc_sn, dim3((g.jci2 - g.jci1 + 64) / 64, kz), dim3(64), 0, stream, g, kz,
-                             t.a1qc[t.cur], t.psa_[t.cur], slices(t), slen);
-      });
+    for (size_t q = 0; q < tiles.size(); q++) {
+      Tile& t = tiles[q];
+      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, t.a1qc[t.cur], t.psa_[t.cur],
+              slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()));
     }
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }

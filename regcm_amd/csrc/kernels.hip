@@ -95,13 +95,18 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 // K2. Column work and the Smagorinsky coefficient in one launch (both only read the state):
 //  blocks [0, nba): calc_coeff, Main/mod_diffusion.F90:194-210 (unscaled xkc on jce/ice),
 //    ubd3d/vbd3d = atm2 * (1/psdotb) recomputed;
-//  blocks [nba, ..): one thread per (j,i) column of jde x ide:
+//  blocks [nba, ..): 64 columns (j) of one row i each:
 //    compute_omega column part, Main/mod_tendency.F90:1123-1156 (pten, qdot k-scan),
 //    new_pressure + nudge2d, :1428-1460 / Main/mod_bdycod.F90:4597-4766 (psc, nudged pten),
 //    the geopotential of the PGF, :1966-1995, 2033-2097 (alpha_hyd = 0, td == tva),
-//    and the Bleck noise sums, reduced deterministically by the last block to finish.
+//    and per-block partials of the Bleck noise sums (summed by k_split_correct).
+//  A column block runs in two phases: all four wavefronts compute the independent per-level
+//  terms (mass divergence, td, tvfac, the log ratios of the hypsometric equation) into LDS,
+//  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
+//  geopotential recurrence, each in the reference's sequential order.
 __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxa, int nya, int nba, int nxb) {
+  extern __shared__ double lds[];                        // 4 x kz x 64
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int b = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -123,39 +128,53 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
     return;
   }
   const int bb = b - nba;
-  const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + (bb / nxb) * 4 + ty;
-  const bool valid = j <= g.jde2 && i <= g.ide2;
+  const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + bb / nxb;
+  const bool valid = j <= g.jde2;
   const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const bool ci = ce && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
   const int kz = c->kz;
+  double* sMD = lds;                                      // mass divergence, [k-1][tx]
+  double* sTD = lds + kz * 64;                            // td
+  double* sTV = lds + 2 * kz * 64;                        // tvfac
+  double* sLG = lds + 3 * kz * 64;                        // log ratio of the layer below level k
+  const uint32_t o2 = valid ? g.o2(j, i) : 0u;
+  const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
+  double rp = 0.0;
+  if (ce) {
+    // phase 1: umc/vmc = atm1 * msfd (decouple :880-890); xqv/xqc decoupled moisture (:1000-1016)
+    const double mx = LD(f.msfx, o2);
+    const double dummy = d_one / (c->dx2 * mx * mx);
+    const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
+    const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
+    rp = LD(f.rpsa, o2);
+    for (int k = ty + 1; k <= kz; k += 4) {
+      const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
+      const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
+                       LD(f.a1u, o3) * m00;
+      const double bq = LD(f.a1v, O3(1, 1)) * m11 + LD(f.a1v, O3(0, 1)) * m01 - LD(f.a1v, O3(1, 0)) * m10 -
+                        LD(f.a1v, o3) * m00;
+      sMD[(k - 1) * 64 + tx] = (a + bq) * dummy;
+      const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
+      const double qc = dmax(LD(f.a1qc, o3) * rp, d_zero);
+      sTD[(k - 1) * 64 + tx] = LD(f.a1t, o3) * (d_one + ep1 * qv);
+      sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
+      sLG[(k - 1) * 64 + tx] = (k < kz) ? log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
+                                        : log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
+    }
+  }
+  __syncthreads();
   double na = 0.0, nb = 0.0;
-  if (valid) {
-    const uint32_t o2 = g.o2(j, i);
+  if (valid && ty == 0) {
     if (!ce) {
       for (int k = 1; k <= kz + 1; k++) ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, d_zero);
     } else {
-      // compute_omega: mass divergence of umc/vmc = atm1 * msfd (decouple :880-890)
-      const double mx = LD(f.msfx, o2);
-      const double dummy = d_one / (c->dx2 * mx * mx);
-      const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
-      const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
-      auto mass_div = [&](int k) {
-        const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
-        const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
-                         LD(f.a1u, o3) * m00;
-        const double bq = LD(f.a1v, O3(1, 1)) * m11 + LD(f.a1v, O3(0, 1)) * m01 - LD(f.a1v, O3(1, 0)) * m10 -
-                          LD(f.a1v, o3) * m00;
-        return (a + bq) * dummy;
-      };
       double pt = d_zero;
-      for (int k = 1; k <= kz; k++) pt = pt - mass_div(k) * c->dsigma[k];
+      for (int k = 1; k <= kz; k++) pt = pt - sMD[(k - 1) * 64 + tx] * c->dsigma[k];
       ST(f.pten, o2, pt);
-      const double rp = LD(f.rpsa, o2);
       double q = d_zero;
       ST(f.qdot, o2, d_zero);
       for (int k = 2; k <= kz; k++) {
-        const double crm = mass_div(k - 1);
-        q = q - (pt + crm) * c->dsigma[k - 1] * rp;
+        q = q - (pt + sMD[(k - 2) * 64 + tx]) * c->dsigma[k - 1] * rp;
         ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, q);
       }
       ST(f.qdot, o2 + (uint32_t)kz * L8, d_zero);
@@ -177,31 +196,26 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
         na = fabs(pt);
         nb = fabs((pc + psbv - d_two * LD(f.psa, o2)) / (dt * dt * d_rfour));
       }
-      // geopotential column, bottom-up; xqv/xqc = decoupled moisture (decouple :1000-1016)
-      const double ps = LD(f.psa, o2);
-      const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
-      auto xqv = [&](int K) { return dmax(LD(f.a1qv, o2 + (uint32_t)(K - 1) * L8) * rp, MINQQ); };
-      auto xqc = [&](int K) { return dmax(LD(f.a1qc, o2 + (uint32_t)(K - 1) * L8) * rp, d_zero); };
-      auto td = [&](int K) { return LD(f.a1t, o2 + (uint32_t)(K - 1) * L8) * (d_one + ep1 * xqv(K)); };
-      auto tvfac = [&](int K) { return d_one / (d_one + xqc(K) / (d_one + xqv(K))); };
-      double tdk1 = td(kz);
-      const double tv = tdk1 * rp * tvfac(kz);
-      double ph = LD(f.ht, o2) - rgas * tv * log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
-      ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
-      for (int lev = kz - 1; lev >= 1; lev--) {
-        const double tdl = td(lev);
-        const double tvavg = ((tdl * c->dsigma[lev] + tdk1 * c->dsigma[lev + 1]) /
-                              (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * tvfac(lev);
-        ph = ph - rgas * tvavg * log((c->hsigma[lev] + ptop * rp) / (c->hsigma[lev + 1] + ptop * rp));
-        ST(f.phi, o2 + (uint32_t)(lev - 1) * L8, ph);
-        tdk1 = tdl;
-      }
     }
   }
-  // deterministic reduction of the noise sums: fixed tree per block, then the last block
-  // (ticket) sums the per-block partials of every tile in index order.
+  if (ce && ty == 1) {
+    // geopotential column, bottom-up
+    const double ps = LD(f.psa, o2);
+    double tdk1 = sTD[(kz - 1) * 64 + tx];
+    const double tv = tdk1 * rp * sTV[(kz - 1) * 64 + tx];
+    double ph = LD(f.ht, o2) - rgas * tv * sLG[(kz - 1) * 64 + tx];
+    ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
+    for (int lev = kz - 1; lev >= 1; lev--) {
+      const double tdl = sTD[(lev - 1) * 64 + tx];
+      const double tvavg = ((tdl * c->dsigma[lev] + tdk1 * c->dsigma[lev + 1]) /
+                            (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * sTV[(lev - 1) * 64 + tx];
+      ph = ph - rgas * tvavg * sLG[(lev - 1) * 64 + tx];
+      ST(f.phi, o2 + (uint32_t)(lev - 1) * L8, ph);
+      tdk1 = tdl;
+    }
+  }
+  // per-block partial of the noise sums (fixed tree); k_split_correct sums the partials
   __shared__ double sa[256], sb[256];
-  __shared__ int last;
   const int t = threadIdx.x;
   sa[t] = na; sb[t] = nb;
   __syncthreads();
@@ -212,28 +226,6 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
   if (t == 0) {
     f.red[2 * (f.red_off + bb)] = sa[0];
     f.red[2 * (f.red_off + bb) + 1] = sb[0];
-    __threadfence();
-    last = (atomicAdd(f.ticket, 1u) == (unsigned)f.red_total - 1u);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  double a = 0.0, bsum = 0.0;
-  for (int q = t; q < f.red_total; q += 256) {
-    a += __builtin_nontemporal_load(&f.red[2 * q]);
-    bsum += __builtin_nontemporal_load(&f.red[2 * q + 1]);
-  }
-  sa[t] = a; sb[t] = bsum;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
-    __syncthreads();
-  }
-  if (t == 0) {
-    s->ptntot = sa[0];
-    s->pt2tot = sb[0];
-    if (sa[0] != sa[0]) s->nanflag = 1;
-    *f.ticket = 0u;
   }
 }
 
@@ -716,67 +708,92 @@ __device__ void negfix_serial_plane(const Geom& g, const Consts* c, const QFix& 
 }
 
 // ---------------------------------------------------------------------------------------
-// K7. splitf projections, Main/mod_split.F90:254-409: one thread per (j,i) column of blocks
-// [0, nproj) builds psdota (:259-260), deld/delh slots 1..3 and refreshes dstor/hstor;
-// slot(l, s) = base + ((s-1)*nsplit + l-1)*plane.  Blocks [nproj, nproj + 2 kz) run the
-// serial negative-moisture sweeps (one plane each, usually an immediate exit).
+// K7. splitf projections, Main/mod_split.F90:254-409, for 64 columns (j) of one row i per
+// block: psdota (:259-260), deld/delh slots 1..3 and dstor/hstor refresh; slot(l, s) =
+// base + ((s-1)*nsplit + l-1)*plane.  Phase 1: all four wavefronts compute each level's
+// divergence of atm1/atm2 (shared by every vertical mode) and stage atm1/atm2 t in LDS;
+// phase 2: one wavefront per (mode, divergence|geopotential) sum runs the k loop in the
+// reference's order.  Blocks [nproj, nproj + 2 kz) run the serial negative-moisture sweeps
+// (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
-__global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
-                                const double* __restrict__ a1v, const double* __restrict__ a2u,
-                                const double* __restrict__ a2v, const double* __restrict__ a1t,
-                                const double* __restrict__ a2t, const double* __restrict__ psa,
-                                const double* __restrict__ psb, const double* __restrict__ msfd,
-                                const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
-                                double* delh, double* psdota, int nxp, int nproj, QFix qf) {
+__global__ __launch_bounds__(256) void k_split_project(
+    Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
+    const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
+    const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
+    const double* __restrict__ msfd, const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
+    double* delh, double* psdota, int nxp, int nproj, QFix qf) {
+  extern __shared__ double lds[];                        // 4 x kz x 64
   const int b = blockIdx.x;
   if (b >= nproj) {
-    if (threadIdx.y == 0) negfix_serial_plane(g, c, qf, b - nproj);
+    if (threadIdx.x < 64) negfix_serial_plane(g, c, qf, b - nproj);
     return;
   }
-  const int j = g.jde1 + (b % nxp) * 64 + (int)threadIdx.x;
-  const int i = g.ide1 + (b / nxp) * 4 + (int)threadIdx.y;
-  if (j > g.jde2 || i > g.ide2) return;
-  {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int j = g.jde1 + (b % nxp) * 64 + tx, i = g.ide1 + b / nxp;
+  const bool valid = j <= g.jde2;
+  const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
+  const int kz = c->kz;
+  double* sD1 = lds;
+  double* sD2 = lds + kz * 64;
+  double* sT1 = lds + 2 * kz * 64;
+  double* sT2 = lds + 3 * kz * 64;
+  if (valid && ty == 0) {
     double v;
     if (psc2psd_at(g, psa, j, i, v)) F2(psdota, j, i) = v;
   }
-  const long q = g.ix(j, i);
-  const bool ce = in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
-  const double rdx2 = d_one / c->dx2;
-  const int kz = c->kz;
-  for (int l = 1; l <= c->nsplit; l++) {
-    const double ds = dstor[(long)(l - 1) * g.plane + q];
-    const double hs = hstor[(long)(l - 1) * g.plane + q];
-    double d3 = d_zero, d2 = d_zero, h3 = d_zero, h2 = d_zero;
-    if (ce) {
-      const double mf = F2(mapf, j, i);
-      const double m00 = F2(msfd, j, i), m10 = F2(msfd, j + 1, i), m01 = F2(msfd, j, i + 1), m11 = F2(msfd, j + 1, i + 1);
-      for (int k = 1; k <= kz; k++) {
-        const double zr = c->zmatxr[l - 1][k - 1];
+  if (ce) {
+    const double m00 = F2(msfd, j, i), m10 = F2(msfd, j + 1, i), m01 = F2(msfd, j, i + 1), m11 = F2(msfd, j + 1, i + 1);
+    for (int k = ty + 1; k <= kz; k += 4) {
 #define DIV(U, V) (-(F3(U, j, i + 1, k) * m01) + (F3(U, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) + \
                    (F3(U, j + 1, i, k) * m10) + (F3(V, j, i + 1, k) * m01) + (F3(V, j + 1, i + 1, k) * m11) - \
                    (F3(V, j, i, k) * m00) - (F3(V, j + 1, i, k) * m10))
-        d3 = d3 + zr * rdx2 * mf * DIV(a1u, a1v);
-        d2 = d2 + zr * rdx2 * mf * DIV(a2u, a2v);
+      sD1[(k - 1) * 64 + tx] = DIV(a1u, a1v);
+      sD2[(k - 1) * 64 + tx] = DIV(a2u, a2v);
 #undef DIV
-      }
-      const double pa = F2(psa, j, i), pbv = F2(psb, j, i);
-      h3 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pa - c->pd);
-      h2 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pbv - c->pd);
-      for (int k = 1; k <= kz; k++) {
-        const double ta = c->tau[l - 1][k - 1], pdk = c->pdlog[l - 1][k], ek = c->eps1[l - 1][k];
-        h3 = h3 + pdk + ta * F3(a1t, j, i, k) / pa + ek * (pa - c->pd);
-        h2 = h2 + pdk + ta * F3(a2t, j, i, k) / pbv + ek * (pbv - c->pd);
-      }
+      sT1[(k - 1) * 64 + tx] = F3(a1t, j, i, k);
+      sT2[(k - 1) * 64 + tx] = F3(a2t, j, i, k);
     }
-    SLOT(deld, l, 1)[q] = ds - d2;
-    SLOT(deld, l, 2)[q] = d2;
-    SLOT(deld, l, 3)[q] = d3 - ds;
-    SLOT(delh, l, 1)[q] = hs - h2;
-    SLOT(delh, l, 2)[q] = h2;
-    SLOT(delh, l, 3)[q] = h3 - hs;
-    dstor[(long)(l - 1) * g.plane + q] = d2;
-    hstor[(long)(l - 1) * g.plane + q] = h2;
+  }
+  __syncthreads();
+  if (!valid) return;
+  const long q = g.ix(j, i);
+  const double rdx2 = d_one / c->dx2;
+  const int ns = c->nsplit;
+  for (int w = ty; w < 2 * ns; w += 4) {
+    const int l = w % ns + 1;
+    if (w < ns) {
+      const double ds = dstor[(long)(l - 1) * g.plane + q];
+      double d3 = d_zero, d2 = d_zero;
+      if (ce) {
+        const double mf = F2(mapf, j, i);
+        for (int k = 1; k <= kz; k++) {
+          const double zr = c->zmatxr[l - 1][k - 1];
+          d3 = d3 + zr * rdx2 * mf * sD1[(k - 1) * 64 + tx];
+          d2 = d2 + zr * rdx2 * mf * sD2[(k - 1) * 64 + tx];
+        }
+      }
+      SLOT(deld, l, 1)[q] = ds - d2;
+      SLOT(deld, l, 2)[q] = d2;
+      SLOT(deld, l, 3)[q] = d3 - ds;
+      dstor[(long)(l - 1) * g.plane + q] = d2;
+    } else {
+      const double hs = hstor[(long)(l - 1) * g.plane + q];
+      double h3 = d_zero, h2 = d_zero;
+      if (ce) {
+        const double pa = F2(psa, j, i), pbv = F2(psb, j, i);
+        h3 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pa - c->pd);
+        h2 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pbv - c->pd);
+        for (int k = 1; k <= kz; k++) {
+          const double ta = c->tau[l - 1][k - 1], pdk = c->pdlog[l - 1][k], ek = c->eps1[l - 1][k];
+          h3 = h3 + pdk + ta * sT1[(k - 1) * 64 + tx] / pa + ek * (pa - c->pd);
+          h2 = h2 + pdk + ta * sT2[(k - 1) * 64 + tx] / pbv + ek * (pbv - c->pd);
+        }
+      }
+      SLOT(delh, l, 1)[q] = hs - h2;
+      SLOT(delh, l, 2)[q] = h2;
+      SLOT(delh, l, 3)[q] = h3 - hs;
+      hstor[(long)(l - 1) * g.plane + q] = h2;
+    }
   }
 }
 
@@ -968,12 +985,29 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                 const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
                                 double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
-                                int advance) {
+                                int advance, const double* __restrict__ red, int red_total) {
   THREAD_POINT(g.jde1, g.ide1);
-  // rcmtimer%advance + dt switch, Main/mod_tendency.F90:608-616 (nothing here reads the clock)
-  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0 && threadIdx.y == 0) {
-    s->lcount = s->lcount + 1;
-    if (s->lcount == 2) s->dt = d_two * c->dtsec;
+  // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
+  // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch
+  // (:608-616); nothing else here reads the clock
+  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+    __shared__ double sa[256], sb[256];
+    const int t = threadIdx.y * blockDim.x + threadIdx.x;
+    double a = 0.0, b = 0.0;
+    for (int q = t; q < red_total; q += 256) { a += red[2 * q]; b += red[2 * q + 1]; }
+    sa[t] = a; sb[t] = b;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
+      __syncthreads();
+    }
+    if (t == 0) {
+      s->ptntot = sa[0];
+      s->pt2tot = sb[0];
+      if (sa[0] != sa[0]) s->nanflag = 1;
+      s->lcount = s->lcount + 1;
+      if (s->lcount == 2) s->dt = d_two * c->dtsec;
+    }
   }
   if (j > g.jde2 || i > g.ide2) return;
   const long q = g.ix(j, i);
@@ -1027,8 +1061,24 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
                              const double* __restrict__ tbt, const double* __restrict__ qb0,
                              const double* __restrict__ qbt, const double* __restrict__ pb0,
                              const double* __restrict__ pbt, Slices sl, long slen) {
-  THREAD_POINT(g.jde1, g.ide1);
-  if (j > g.jde2 || i > g.ide2) return;
+  // thread -> one point of the boundary lines: blockIdx.y 0..2 = rows i = ide1 (bottom),
+  // ide2 (top), ice2 (top cross row) over jde; 3..5 = columns j = jde1, jde2, jce2 over ide
+  // minus the points a row owns.  Every point the body modifies lies on these lines.
+  const int line = blockIdx.y, k = (int)blockIdx.z + 1;
+  const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  int j, i;
+  if (line < 3) {
+    if (line == 0 ? !g.bb : !g.bt) return;
+    i = (line == 0) ? g.ide1 : (line == 1) ? g.ide2 : g.ice2;
+    j = g.jde1 + x;
+    if (j > g.jde2) return;
+  } else {
+    if (line == 3 ? !g.bl : !g.br) return;
+    j = (line == 3) ? g.jde1 : (line == 4) ? g.jde2 : g.jce2;
+    i = g.ide1 + x;
+    if (i > g.ide2) return;
+    if ((g.bb && i == g.ide1) || (g.bt && (i == g.ide2 || i == g.ice2))) return;
+  }
   const long q = g.ix(j, i);
   const long p = (long)(k - 1) * g.plane + q;
   const double xt = s->xbctime + s->dt;
@@ -1074,64 +1124,63 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
     if (in(j, g.jdi1, g.jdi2)) { SLJ(sl.s[11], j, k) = F3(a1u, j, g.idi2, k); SLJ(sl.s[15], j, k) = F3(a1v, j, g.idi2, k); }
     SLJ(sl.s[10], j, k) = ub0[p] + xt * ubt[p]; SLJ(sl.s[14], j, k) = vb0[p] + xt * vbt[p];
   }
+  // bdyuv corner fills, Main/mod_bdycod.F90:1030-1061: every corner slice entry is the
+  // boundary value b0 + xt*bt of a known point, written by the thread of that tile corner
+#define UB(J, I) (F3(ub0, J, I, k) + xt * F3(ubt, J, I, k))
+#define VB(J, I) (F3(vb0, J, I, k) + xt * F3(vbt, J, I, k))
+  if (g.bt && g.bl && j == g.jde1 && i == g.ide2) {
+    SLI(sl.s[1], g.ide2, k) = UB(g.jdi1, g.ide2); SLI(sl.s[5], g.ide2, k) = VB(g.jdi1, g.ide2);
+    SLJ(sl.s[11], g.jde1, k) = UB(g.jde1, g.idi2); SLJ(sl.s[15], g.jde1, k) = VB(g.jde1, g.idi2);
+  }
+  if (g.bb && g.bl && j == g.jde1 && i == g.ide1) {
+    SLI(sl.s[1], g.ide1, k) = UB(g.jdi1, g.ide1); SLI(sl.s[5], g.ide1, k) = VB(g.jdi1, g.ide1);
+    SLJ(sl.s[9], g.jde1, k) = UB(g.jde1, g.idi1); SLJ(sl.s[13], g.jde1, k) = VB(g.jde1, g.idi1);
+  }
+  if (g.bt && g.br && j == g.jde2 && i == g.ide2) {
+    SLI(sl.s[3], g.ide2, k) = UB(g.jdi2, g.ide2); SLI(sl.s[7], g.ide2, k) = VB(g.jdi2, g.ide2);
+    SLJ(sl.s[11], g.jde2, k) = UB(g.jde2, g.idi2); SLJ(sl.s[15], g.jde2, k) = VB(g.jde2, g.idi2);
+  }
+  if (g.bb && g.br && j == g.jde2 && i == g.ide1) {
+    SLI(sl.s[3], g.ide1, k) = UB(g.jdi2, g.ide1); SLI(sl.s[7], g.ide1, k) = VB(g.jdi2, g.ide1);
+    SLJ(sl.s[9], g.jde2, k) = UB(g.jde2, g.idi1); SLJ(sl.s[13], g.jde2, k) = VB(g.jde2, g.idi1);
+  }
+#undef UB
+#undef VB
 }
 
-// bdyuv corner fills, Main/mod_bdycod.F90:1030-1061
-// + the boundary clock advance xbctime += dtsec (Main/mod_bdycod.F90:2566), after every
-// tile's k_bdyval_set
-__global__ void k_bdyval_corners(Geom g, int kz, Slices sl, long slen, StepState* s, double dtsec, int advance) {
-  const int k = 1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  if (advance && k == 1) s->xbctime = s->xbctime + dtsec;
-  if (k > kz) return;
-  if (g.bt && g.bl) {
-    SLI(sl.s[1], g.ide2, k) = SLJ(sl.s[10], g.jdi1, k); SLI(sl.s[5], g.ide2, k) = SLJ(sl.s[14], g.jdi1, k);
-    SLJ(sl.s[11], g.jde1, k) = SLI(sl.s[0], g.idi2, k); SLJ(sl.s[15], g.jde1, k) = SLI(sl.s[4], g.idi2, k);
+// qc inflow/outflow (present_qc = .false., bdyflow), Main/mod_bdycod.F90:2153-2220, one
+// block per level: west/east first (they read qc(jci1|jci2, ice1|ice2) before south/north
+// rewrite it), then south/north.  The last tile's launch also advances the boundary clock
+// xbctime += dtsec (Main/mod_bdycod.F90:2566): nothing here reads it.
+__global__ void k_bdyval_qc(Geom g, int do_qc, double* a1qc, const double* __restrict__ psa, Slices sl, long slen,
+                            StepState* s, double dtsec, int advance) {
+  const int k = (int)blockIdx.x + 1;
+  if (advance && k == 1 && threadIdx.x == 0) s->xbctime = s->xbctime + dtsec;
+  if (!do_qc) return;
+  for (int i = g.ice1 + (int)threadIdx.x; i <= g.ice2; i += (int)blockDim.x) {
+    if (g.bl) {
+      const double qxint = F3(a1qc, g.jci1, i, k) / F2(psa, g.jci1, i);
+      const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
+      F3(a1qc, g.jce1, i, k) = (w > d_zero) ? d_zero : qxint * F2(psa, g.jce1, i);
+    }
+    if (g.br) {
+      const double qxint = F3(a1qc, g.jci2, i, k) / F2(psa, g.jci2, i);
+      const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
+      F3(a1qc, g.jce2, i, k) = (w < d_zero) ? d_zero : qxint * F2(psa, g.jce2, i);
+    }
   }
-  if (g.bb && g.bl) {
-    SLI(sl.s[1], g.ide1, k) = SLJ(sl.s[8], g.jdi1, k); SLI(sl.s[5], g.ide1, k) = SLJ(sl.s[12], g.jdi1, k);
-    SLJ(sl.s[9], g.jde1, k) = SLI(sl.s[0], g.idi1, k); SLJ(sl.s[13], g.jde1, k) = SLI(sl.s[4], g.idi1, k);
-  }
-  if (g.bt && g.br) {
-    SLI(sl.s[3], g.ide2, k) = SLJ(sl.s[10], g.jdi2, k); SLI(sl.s[7], g.ide2, k) = SLJ(sl.s[14], g.jdi2, k);
-    SLJ(sl.s[11], g.jde2, k) = SLI(sl.s[2], g.idi2, k); SLJ(sl.s[15], g.jde2, k) = SLI(sl.s[6], g.idi2, k);
-  }
-  if (g.bb && g.br) {
-    SLI(sl.s[3], g.ide1, k) = SLJ(sl.s[8], g.jdi2, k); SLI(sl.s[7], g.ide1, k) = SLJ(sl.s[12], g.jdi2, k);
-    SLJ(sl.s[9], g.jde2, k) = SLI(sl.s[2], g.idi1, k); SLJ(sl.s[13], g.jde2, k) = SLI(sl.s[6], g.idi1, k);
-  }
-}
-
-// qc inflow/outflow (present_qc = .false., bdyflow), Main/mod_bdycod.F90:2153-2220.
-// west/east first (they read qc(jci1|jci2, ice1|ice2) before south/north rewrite it).
-__global__ void k_bdyval_qc_we(Geom g, int kz, double* a1qc, const double* __restrict__ psa, Slices sl, long slen) {
-  const int i = g.ice1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int k = 1 + (int)blockIdx.y;
-  if (i > g.ice2) return;
-  if (g.bl) {
-    const double qxint = F3(a1qc, g.jci1, i, k) / F2(psa, g.jci1, i);
-    const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
-    F3(a1qc, g.jce1, i, k) = (w > d_zero) ? d_zero : qxint * F2(psa, g.jce1, i);
-  }
-  if (g.br) {
-    const double qxint = F3(a1qc, g.jci2, i, k) / F2(psa, g.jci2, i);
-    const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
-    F3(a1qc, g.jce2, i, k) = (w < d_zero) ? d_zero : qxint * F2(psa, g.jce2, i);
-  }
-}
-
-__global__ void k_bdyval_qc_sn(Geom g, int kz, double* a1qc, const double* __restrict__ psa, Slices sl, long slen) {
-  const int j = g.jci1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int k = 1 + (int)blockIdx.y;
-  if (j > g.jci2) return;
-  if (g.bb) {
-    const double qxint = F3(a1qc, j, g.ici1, k) / F2(psa, j, g.ici1);
-    const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
-    F3(a1qc, j, g.ice1, k) = (w > d_zero) ? d_zero : qxint * F2(psa, j, g.ice1);
-  }
-  if (g.bt) {
-    const double qxint = F3(a1qc, j, g.ici2, k) / F2(psa, j, g.ici2);
-    const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
-    F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * F2(psa, j, g.ice2);
+  __syncthreads();
+  for (int j = g.jci1 + (int)threadIdx.x; j <= g.jci2; j += (int)blockDim.x) {
+    if (g.bb) {
+      const double qxint = F3(a1qc, j, g.ici1, k) / F2(psa, j, g.ici1);
+      const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
+      F3(a1qc, j, g.ice1, k) = (w > d_zero) ? d_zero : qxint * F2(psa, j, g.ice1);
+    }
+    if (g.bt) {
+      const double qxint = F3(a1qc, j, g.ici2, k) / F2(psa, j, g.ici2);
+      const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
+      F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * F2(psa, j, g.ice2);
+    }
   }
 }
 
