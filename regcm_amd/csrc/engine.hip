@@ -757,10 +757,10 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const Fields f = fields(t);
-      KLAUNCH(k_momentum, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, f);
-      KLAUNCH(k_temperature, grid3(g.nj, g.ni, kz), BLK, 0, stream, g, dc, ds, f);
-      KLAUNCH(k_moisture, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kz), BLK, 0, stream, g, dc, ds,
-                         f);
+      KLAUNCH(k_momentum, dim3((g.jdi2 - g.jdi1 + MBJ) / MBJ, (g.idi2 - g.idi1 + MBI) / MBI, kz), dim3(MBT), 0,
+              stream, g, dc, ds, f);
+      KLAUNCH(k_scalars, dim3((g.jce2 - g.jce1 + SBJ) / SBJ, (g.ice2 - g.ice1 + SBI) / SBI, kz), dim3(SBT), 0,
+              stream, g, dc, ds, f);
     });
     xch({{FK::CQV, kz}, {FK::CQC, kz}}, 1, 0);
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current

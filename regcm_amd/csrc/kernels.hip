@@ -234,24 +234,78 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
 // the Robert-Asselin filter (Main/mod_advection.F90:203-299, Main/mod_tendency.F90:1829-1838,
 // Main/mod_bdycod.F90:3581-3823, Main/mod_diffusion.F90:281-385, Main/mod_tendency.F90:
 // 1996-2025, 2103-2115, 404-411, 433-445; Main/mod_timefilter.F90 filter_ra_uv).
-__global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restrict__ c,
-                                                  const StepState* __restrict__ s, Fields f) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+// One block = MBJ x MBI dot points of the interior (jdi x idi) at one level.  Every stencil
+// operand is first staged in LDS for the block plus its halo, with the decoupled products
+// formed once per staged point (umc/vmc = atm1*msfd, ud/vd = atm1*rpsda, ubd3d/msfd =
+// (atm2*(1/psdotb))/msfd, tv = t*(1+ep1*qv)): one round of independent global loads per
+// block instead of dependent per-operand rounds, and one division per staged point instead
+// of 13 per output.  Points outside jdi x idi keep their values (copied by k_qfilter).
+constexpr int TW1 = MBJ + 2, TH1 = MBI + 2;   // halo 1 on every side
+constexpr int TW2 = MBJ + 4, TH2 = MBI + 4;   // halo 2 on every side
+constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i-1)
+__global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __restrict__ c,
+                                                     const StepState* __restrict__ s, Fields f) {
+  __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
+  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
+  __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
+  const int tid = threadIdx.x;
+  const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
   const uint32_t P8 = g.P8, L8 = g.L8;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
-  if (!(in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))) {
-    ST(f.b1u, o3, LD(f.a1u, o3)); ST(f.b1v, o3, LD(f.a1v, o3));
-    ST(f.b2u, o3, LD(f.a2u, o3)); ST(f.b2v, o3, LD(f.a2v, o3));
-    return;
-  }
+  const uint32_t kof = (uint32_t)(k - 1) * L8;
+  const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
   const int kz = c->kz;
+  const double ep1 = c->ep1;
+  // ---- stage (all loads independent)
+  for (int t = tid; t < TW1 * TH1; t += MBT) {
+    const int jj = t % TW1, ii = t / TW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0;
+    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
+      umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
+    }
+    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd;
+  }
+  for (int t = tid; t < TW2 * TH2; t += MBT) {
+    const int jj = t % TW2, ii = t / TW2, jg = J0 - 2 + jj, ig = I0 - 2 + ii;
+    double um = 0.0, vm = 0.0;
+    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double r = LD(f.rpsdb, q2), m = LD(f.msfd, q2);
+      um = (LD(f.a2u, q3) * r) / m;
+      vm = (LD(f.a2v, q3) * r) / m;
+    }
+    sUM[ii][jj] = um; sVM[ii][jj] = vm;
+  }
+  for (int t = tid; t < TW0 * TH0; t += MBT) {
+    const int jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+    double tv = 0.0, q0 = 0.0, q1 = 0.0, ph = 0.0, ps = 0.0, xk = 0.0;
+    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double rp = LD(f.rpsa, q2);
+      const double tt = LD(f.a1t, q3) * rp;
+      const double qv = dmax(LD(f.a1qv, q3) * rp, MINQQ);
+      tv = tt * (d_one + ep1 * qv);
+      q0 = LD(f.qdot, q3);
+      q1 = LD(f.qdot, q3 + L8);
+      ph = LD(f.phi, q3);
+      ps = LD(f.psa, q2);
+      xk = LD(f.xkc, q3);
+    }
+    sTV[ii][jj] = tv; sQ0[ii][jj] = q0; sQ1[ii][jj] = q1; sPH[ii][jj] = ph; sPS[ii][jj] = ps; sXK[ii][jj] = xk;
+  }
+  __syncthreads();
+  const int tj = tid % MBJ, ti = tid / MBJ;
+  const int j = J0 + tj, i = I0 + ti;
+  if (j > g.jdi2 || i > g.idi2) return;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + kof;
   const double dt = s->dt;
-  // decoupled winds (decouple :880-890, :895-994)
-#define UMC(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
-#define VMC(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
-#define UD(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
-#define VD(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
+  // tile coordinates of (j,i): halo-1 tiles (b1,a1), halo-2 (b2,a2), low-halo (b0,a0)
+  const int b1 = tj + 1, a1 = ti + 1, b2 = tj + 2, a2 = ti + 2, b0 = tj + 1, a0 = ti + 1;
+#define UMC(dj, di) sUMC[a1 + (di)][b1 + (dj)]
+#define VMC(dj, di) sVMC[a1 + (di)][b1 + (dj)]
+#define UD(dj, di) sUD[a1 + (di)][b1 + (dj)]
+#define VD(dj, di) sVD[a1 + (di)][b1 + (dj)]
   // hadvuv (upstream, hydrostatic)
   double ut, vt;
   {
@@ -277,29 +331,29 @@ __global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restri
 #undef VMC
 #undef UD
 #undef VD
+  const double u1c = LD(f.a1u, o3), v1c = LD(f.a1v, o3);
   // vadvuv: flux at interface k (from loop index k) then interface k+1 (loop index k+1)
   {
-#define QQ(dk) (d_rfour * (LD(f.qdot, O3K(0, 0, dk)) + LD(f.qdot, O3K(0, -1, dk)) + LD(f.qdot, O3K(-1, 0, dk)) + \
-                           LD(f.qdot, O3K(-1, -1, dk))))
+#define QQ(S) (d_rfour * (S[a0][b0] + S[a0][b0 - 1] + S[a0 - 1][b0] + S[a0 - 1][b0 - 1]))
     if (k >= 2) {
-      const double qq = QQ(0);
-      const double uu = qq * (c->twt1[k] * LD(f.a1u, o3) + c->twt2[k] * LD(f.a1u, O3K(0, 0, -1)));
-      const double vv = qq * (c->twt1[k] * LD(f.a1v, o3) + c->twt2[k] * LD(f.a1v, O3K(0, 0, -1)));
+      const double qq = QQ(sQ0);
+      const double uu = qq * (c->twt1[k] * u1c + c->twt2[k] * LD(f.a1u, o3 - L8));
+      const double vv = qq * (c->twt1[k] * v1c + c->twt2[k] * LD(f.a1v, o3 - L8));
       ut = ut + uu * c->xds[k];
       vt = vt + vv * c->xds[k];
     }
     if (k + 1 <= kz) {
-      const double qq = QQ(1);
-      const double uu = qq * (c->twt1[k + 1] * LD(f.a1u, O3K(0, 0, 1)) + c->twt2[k + 1] * LD(f.a1u, o3));
-      const double vv = qq * (c->twt1[k + 1] * LD(f.a1v, O3K(0, 0, 1)) + c->twt2[k + 1] * LD(f.a1v, o3));
+      const double qq = QQ(sQ1);
+      const double uu = qq * (c->twt1[k + 1] * LD(f.a1u, o3 + L8) + c->twt2[k + 1] * u1c);
+      const double vv = qq * (c->twt1[k + 1] * LD(f.a1v, o3 + L8) + c->twt2[k + 1] * v1c);
       ut = ut - uu * c->xds[k];
       vt = vt - vv * c->xds[k];
     }
 #undef QQ
   }
   // curvature (hydrostatic Coriolis)
-  ut = ut + LD(f.coriol, o2) * LD(f.a1v, o3);
-  vt = vt - LD(f.coriol, o2) * LD(f.a1u, o3);
+  ut = ut + LD(f.coriol, o2) * v1c;
+  vt = vt - LD(f.coriol, o2) * u1c;
   // nudgeuv
   if (f.rgdt[o2 >> 3] > 0) {
     const double xt = s->xbctime + dt;
@@ -313,25 +367,24 @@ __global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restri
 #undef FGU
 #undef FGV
   }
-  // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248);
-  // ubd3d = atm2 * (1/psdotb) (mkslice), divided by msfd as diffu_d does
+  // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248)
   {
-    double xkd = d_rfour * (LD(f.xkc, o3) + LD(f.xkc, O3(-1, -1)) + LD(f.xkc, O3(-1, 0)) + LD(f.xkc, O3(0, -1)));
+    double xkd = d_rfour * (sXK[a0][b0] + sXK[a0 - 1][b0 - 1] + sXK[a0 - 1][b0] + sXK[a0][b0 - 1]);
     xkd = xkd * c->rdxsq * LD(f.psdotb, o2);
-#define UM(a, dj, di) ((LD(a, O3(dj, di)) * LD(f.rpsdb, O2(dj, di))) / LD(f.msfd, O2(dj, di)))
+#define UM(S, dj, di) S[a2 + (di)][b2 + (dj)]
     if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
-      ut = ut - xkd * (z4_c1 * (UM(f.a2u, 2, 0) + UM(f.a2u, -2, 0) + UM(f.a2u, 0, 2) + UM(f.a2u, 0, -2)) +
-                       z4_c2 * (UM(f.a2u, 1, 0) + UM(f.a2u, -1, 0) + UM(f.a2u, 0, 1) + UM(f.a2u, 0, -1)) +
-                       z4_c3 * (UM(f.a2u, 0, 0)));
-      vt = vt - xkd * (z4_c1 * (UM(f.a2v, 2, 0) + UM(f.a2v, -2, 0) + UM(f.a2v, 0, 2) + UM(f.a2v, 0, -2)) +
-                       z4_c2 * (UM(f.a2v, 1, 0) + UM(f.a2v, -1, 0) + UM(f.a2v, 0, 1) + UM(f.a2v, 0, -1)) +
-                       z4_c3 * (UM(f.a2v, 0, 0)));
+      ut = ut - xkd * (z4_c1 * (UM(sUM, 2, 0) + UM(sUM, -2, 0) + UM(sUM, 0, 2) + UM(sUM, 0, -2)) +
+                       z4_c2 * (UM(sUM, 1, 0) + UM(sUM, -1, 0) + UM(sUM, 0, 1) + UM(sUM, 0, -1)) +
+                       z4_c3 * (UM(sUM, 0, 0)));
+      vt = vt - xkd * (z4_c1 * (UM(sVM, 2, 0) + UM(sVM, -2, 0) + UM(sVM, 0, 2) + UM(sVM, 0, -2)) +
+                       z4_c2 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +
+                       z4_c3 * (UM(sVM, 0, 0)));
     }
-#define LAPD()                                                                                                  \
-  ut = ut + xkd * (z4_c1 * (UM(f.a2u, 1, 0) + UM(f.a2u, -1, 0) + UM(f.a2u, 0, 1) + UM(f.a2u, 0, -1)) +          \
-                   z4_c2 * (UM(f.a2u, 0, 0)));                                                                  \
-  vt = vt + xkd * (z4_c1 * (UM(f.a2v, 1, 0) + UM(f.a2v, -1, 0) + UM(f.a2v, 0, 1) + UM(f.a2v, 0, -1)) +          \
-                   z4_c2 * (UM(f.a2v, 0, 0)));
+#define LAPD()                                                                                        \
+  ut = ut + xkd * (z4_c1 * (UM(sUM, 1, 0) + UM(sUM, -1, 0) + UM(sUM, 0, 1) + UM(sUM, 0, -1)) +        \
+                   z4_c2 * (UM(sUM, 0, 0)));                                                          \
+  vt = vt + xkd * (z4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +        \
+                   z4_c2 * (UM(sVM, 0, 0)));
     if (g.bl && j == g.jdi1) { LAPD(); }
     if (g.br && j == g.jdi2) { LAPD(); }
     if (g.bb && i == g.idi1) { LAPD(); }
@@ -339,28 +392,19 @@ __global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restri
 #undef LAPD
 #undef UM
   }
-  // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient);
-  // tv = t * (1 + ep1 * qv) from the decoupled t and qv (decouple :1000-1016)
+  // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient)
   {
-    const double ep1 = c->ep1;
-    auto xtv = [&](int dj, int di) {
-      const double rp = LD(f.rpsa, O2(dj, di));
-      const double t = LD(f.a1t, O3(dj, di)) * rp;
-      const double qv = dmax(LD(f.a1qv, O3(dj, di)) * rp, MINQQ);
-      return t * (d_one + ep1 * qv);
-    };
-    double rtbar = d_rfour * (xtv(-1, -1) + xtv(-1, 0) + xtv(0, -1) + xtv(0, 0));
+    double rtbar = d_rfour * (sTV[a0 - 1][b0 - 1] + sTV[a0][b0 - 1] + sTV[a0 - 1][b0] + sTV[a0][b0]);
     rtbar = c->rgas * rtbar * LD(f.psdota, o2);
     const double hs = c->hsigma[k], pt = c->ptop;
-    const double den = c->dx * LD(f.msfd, o2);
-    const double p00 = LD(f.psa, o2), p0m = LD(f.psa, O2(0, -1)), pm0 = LD(f.psa, O2(-1, 0));
-    const double pmm = LD(f.psa, O2(-1, -1));
+    const double mfd = LD(f.msfd, o2);
+    const double den = c->dx * mfd;
+    const double p00 = sPS[a0][b0], p0m = sPS[a0 - 1][b0], pm0 = sPS[a0][b0 - 1], pmm = sPS[a0 - 1][b0 - 1];
     ut = ut - rtbar * (log(d_half * (p00 + p0m) * hs + pt) - log(d_half * (pm0 + pmm) * hs + pt)) / den;
     vt = vt - rtbar * (log(d_half * (p00 + pm0) * hs + pt) - log(d_half * (pmm + p0m) * hs + pt)) / den;
-    const double den2 = c->dx2 * LD(f.msfd, o2);
+    const double den2 = c->dx2 * mfd;
     const double pd = LD(f.psdota, o2);
-    const double f00 = LD(f.phi, o3), f0m = LD(f.phi, O3(0, -1)), fm0 = LD(f.phi, O3(-1, 0));
-    const double fmm = LD(f.phi, O3(-1, -1));
+    const double f00 = sPH[a0][b0], f0m = sPH[a0 - 1][b0], fm0 = sPH[a0][b0 - 1], fmm = sPH[a0 - 1][b0 - 1];
     ut = ut - pd * (f00 + f0m - fm0 - fmm) / den2;
     vt = vt - pd * (f00 + fm0 - f0m - fmm) / den2;
   }
@@ -369,42 +413,45 @@ __global__ __launch_bounds__(256) void k_momentum(Geom g, const Consts* __restri
   vt = (d_zero + vt) + d_zero;
   if (f.uten) { ST(f.uten, o3, ut); ST(f.vten, o3, vt); }
   const double g1 = c->gnu1;
-  const double u1 = LD(f.a1u, o3), u2 = LD(f.a2u, o3), v1 = LD(f.a1v, o3), v2 = LD(f.a2v, o3);
+  const double u2 = LD(f.a2u, o3), v2 = LD(f.a2v, o3);
   const double cu = u2 + dt * ut, cv = v2 + dt * vt;
-  double d = g1 * (cu + u2 - d_two * u1);
-  ST(f.b2u, o3, u1 + d);
+  double d = g1 * (cu + u2 - d_two * u1c);
+  ST(f.b2u, o3, u1c + d);
   ST(f.b1u, o3, cu);
-  d = g1 * (cv + v2 - d_two * v1);
-  ST(f.b2v, o3, v1 + d);
+  d = g1 * (cv + v2 - d_two * v1c);
+  ST(f.b2v, o3, v1c + d);
   ST(f.b1v, o3, cv);
 }
 
 // ---------------------------------------------------------------------------------------
-// Scalar upstream flux-form advection (hadvt/hadvqv/hadvqx, Main/mod_advection.F90:337-386,
-// 547-596, 639-653) at the thread's point; fv(dj,di) is the decoupled scalar; limiter 0 none,
-// 1 t_extrema, 2 q_rel_extrema.
-template <class FV>
-__device__ __forceinline__ double hadv_point(const Consts* c, const Fields& f, uint32_t o2, uint32_t o3,
-                                             uint32_t P8, FV fv, int limiter) {
-#define UMC(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
-#define VMC(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.msfd, O2(dj, di)))
-  const double uavg1 = UMC(0, 1) + UMC(0, 0);
-  const double uavg2 = UMC(1, 1) + UMC(1, 0);
-  const double vavg1 = VMC(1, 0) + VMC(0, 0);
-  const double vavg2 = VMC(1, 1) + VMC(0, 1);
-#undef UMC
-#undef VMC
-  const double ps = LD(f.psa, o2);
+// K4. Scalars at the cross points jce x ice, one level per block of SBJ x SBI points:
+//  temperature: hadvt + vadv3d + omega + adiabatic + nudge3d + diffu_x3d, forecast and RA
+//    filter (Main/mod_tendency.F90:1200-1214, 1327-1341, 1561-1575, 1469, 1525, 285-287,
+//    368-374, 422);
+//  moisture (before the negative-value fix): hadvqv + vadvqv + nudge4d3d + diffu_x4d (qv),
+//    hadvqx + vadv4d(ind=1) + diffu_x4d (qc), forecast (:1361-1392, 1470, 1526, 292-294,
+//    332-349, 375-380).
+// The stencil operands are staged in LDS once for the block and its halo, with the decoupled
+// products formed once per staged point: umc/vmc/ud/vd at the dot points (j..j+1, i..i+1),
+// p*, t, qv, qc (atm1 * rpsa) with halo 1 and the mkslice fields atm2 * (1/psb) with halo 2.
+// The interior ring (jce \ jci) only passes atm2 moisture to the forecast buffers.
+constexpr int SDW = SBJ + 1, SDH = SBI + 1;    // dot points j..j+SBJ, i..i+SBI
+constexpr int SW1 = SBJ + 2, SH1 = SBI + 2;    // halo 1
+constexpr int SW2 = SBJ + 4, SH2 = SBI + 4;    // halo 2
+
+// upstream flux-form advection of one scalar (hadvt/hadvqv/hadvqx, Main/mod_advection.F90:
+// 337-386, 547-596, 639-653); limiter 0 none, 1 t_extrema, 2 q_rel_extrema
+__device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double ps, double uavg1, double uavg2,
+                                            double vavg1, double vavg2, double fc, double fw, double fe, double fs,
+                                            double fn, int limiter) {
   const double ul = c->ul;
   const double f1 = d_half * ul * (uavg2 + uavg1) / ps;
   const double f2 = d_half * ul * (vavg2 + vavg1) / ps;
-  const double fc = fv(0, 0), fw = fv(-1, 0), fe = fv(1, 0);
-  const double fs = fv(0, -1), fn = fv(0, 1);
   const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
   const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
   const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
   const double fy2 = (d_one + f2) * fc + (d_one - f2) * fn;
-  double fg = -LD(f.xmsf, o2) * (uavg2 * fx2 - uavg1 * fx1 + vavg2 * fy2 - vavg1 * fy1);
+  double fg = -xm * (uavg2 * fx2 - uavg1 * fx1 + vavg2 * fy2 - vavg1 * fy1);
   if (limiter && c->stability_enhance) {
     double den, thr;
     if (limiter == 1) { den = ps; thr = c->t_extrema; } else { den = dmax(fc, DLOWVAL); thr = c->q_rel_extrema; }
@@ -420,133 +467,167 @@ __device__ __forceinline__ double hadv_point(const Consts* c, const Fields& f, u
   return fg;
 }
 
-// diffu_x (idiffu = 1) at the thread's point, Main/mod_diffusion.F90:673-713 / 808-...;
-// fv(dj,di) is the mkslice field (atm2 * (1/psb), clipped for moisture).
-template <class FV>
-__device__ __forceinline__ double diffu_x_point(const Geom& g, double ften, double xkcs, FV fv, int j, int i) {
-  if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2)) {
-    ften = ften - d_one * xkcs *
-        (z4_c1 * (fv(2, 0) + fv(-2, 0) + fv(0, 2) + fv(0, -2)) +
-         z4_c2 * (fv(1, 0) + fv(-1, 0) + fv(0, 1) + fv(0, -1)) +
-         z4_c3 * fv(0, 0));
-  }
-#define LAP2() ften = ften + d_one * xkcs * \
-    (z4_c1 * (fv(1, 0) + fv(-1, 0) + fv(0, 1) + fv(0, -1)) + z4_c2 * fv(0, 0))
-  if (g.bl && j == g.jci1) { LAP2(); }
-  if (g.br && j == g.jci2) { LAP2(); }
-  if (g.bb && i == g.ici1) { LAP2(); }
-  if (g.bt && i == g.ici2) { LAP2(); }
-#undef LAP2
-  return ften;
-}
+// diffu_x (idiffu = 1) at one point from a halo-2 LDS tile, Main/mod_diffusion.F90:673-713
+#define H2T(S, dj, di) S[a2 + (di)][b2 + (dj)]
+#define DIFFU_X(ften, S)                                                                          \
+  do {                                                                                            \
+    if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))                                       \
+      ften = ften - d_one * xkcs *                                                                \
+          (z4_c1 * (H2T(S, 2, 0) + H2T(S, -2, 0) + H2T(S, 0, 2) + H2T(S, 0, -2)) +                \
+           z4_c2 * (H2T(S, 1, 0) + H2T(S, -1, 0) + H2T(S, 0, 1) + H2T(S, 0, -1)) +                \
+           z4_c3 * H2T(S, 0, 0));                                                                 \
+    if (g.bl && j == g.jci1) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+        H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
+    if (g.br && j == g.jci2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+        H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
+    if (g.bb && i == g.ici1) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+        H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
+    if (g.bt && i == g.ici2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+        H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
+  } while (0)
 
-// K4. Temperature: hadvt + vadv3d + adiabatic (omega on the fly) + nudge3d + diffu_x3d,
-// forecast and RA filter (Main/mod_tendency.F90:1200-1214, 1327-1341, 1561-1575, 1469, 1525,
-// 285-287, 368-374, 422).
-__global__ __launch_bounds__(256) void k_temperature(Geom g, const Consts* __restrict__ c,
-                                                     const StepState* __restrict__ s, Fields f) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+__global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __restrict__ c,
+                                                    const StepState* __restrict__ s, Fields f) {
+  __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW];
+  __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
+  __shared__ double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
+  const int tid = threadIdx.x;
+  const int J0 = g.jce1 + (int)blockIdx.x * SBJ, I0 = g.ice1 + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
   const uint32_t P8 = g.P8, L8 = g.L8;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
-  if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
-    ST(f.b1t, o3, LD(f.a1t, o3)); ST(f.b2t, o3, LD(f.a2t, o3));
-    if (f.xkcs && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2)) ST(f.xkcs, o3, LD(f.xkc, o3));
-    return;
-  }
+  const uint32_t kof = (uint32_t)(k - 1) * L8;
+  const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
   const int kz = c->kz;
-  const double dt = s->dt;
-  const double rp = LD(f.rpsa, o2);
-  double td = d_zero + hadv_point(c, f, o2, o3, P8,
-                                  [&](int dj, int di) { return LD(f.a1t, O3(dj, di)) * LD(f.rpsa, O2(dj, di)); }, 1);
-  // vadv3d ind = 1 (Main/mod_advection.F90:771-783): pf/pb from psb (mkslice :263-271)
-  {
-    const double pb = LD(f.psb, o2), ptop = c->ptop, c287 = c->c287;
-#define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
-#define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
-#define DQ(K, dk) (LD(f.qdot, O3K(0, 0, dk)) * (c->twt1[K] * LD(f.a1t, O3K(0, 0, dk)) * pow(PF(K) / PB(K), c287) + \
-                                              c->twt2[K] * LD(f.a1t, O3K(0, 0, (dk) - 1)) * pow(PF(K) / PB((K) - 1), c287)))
-    if (k >= 2) td = td + DQ(k, 0) * c->xds[k];
-    if (k + 1 <= kz) td = td - DQ(k + 1, 1) * c->xds[k];
-#undef DQ
-#undef PB
-#undef PF
+  (void)P8;
+  // ---- stage
+  for (int t = tid; t < SDW * SDH; t += SBT) {
+    const int jj = t % SDW, ii = t / SDW, jg = J0 + jj, ig = I0 + ii;
+    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0;
+    if (jg <= jhi && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
+      umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
+    }
+    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd;
   }
-  // omega, Main/mod_tendency.F90:1200-1214 (ud/vd = atm1 * rpsda)
-  double om;
-  {
-#define UD(dj, di) (LD(f.a1u, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
-#define VD(dj, di) (LD(f.a1v, O3(dj, di)) * LD(f.rpsda, O2(dj, di)))
-    const double dummy = d_one / (c->dx8 * LD(f.msfx, o2));
-    const double su = UD(0, 0) + UD(0, 1) + UD(1, 1) + UD(1, 0);
-    const double sv = VD(0, 0) + VD(0, 1) + VD(1, 1) + VD(1, 0);
-#undef UD
-#undef VD
-    const double x = su * (LD(f.psa, O2(1, 0)) - LD(f.psa, O2(-1, 0))) +
-                     sv * (LD(f.psa, O2(0, 1)) - LD(f.psa, O2(0, -1)));
-    om = d_half * (LD(f.qdot, O3K(0, 0, 1)) + LD(f.qdot, o3)) * LD(f.psa, o2) +
-         c->hsigma[k] * (LD(f.pten, o2) + x * dummy);
+  for (int t = tid; t < SW1 * SH1; t += SBT) {
+    const int jj = t % SW1, ii = t / SW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+    double ps = 0.0, xt = 0.0, xqv = 0.0, xqc = 0.0;
+    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double rp = LD(f.rpsa, q2);
+      ps = LD(f.psa, q2);
+      xt = LD(f.a1t, q3) * rp;
+      xqv = dmax(LD(f.a1qv, q3) * rp, MINQQ);
+      xqc = dmax(LD(f.a1qc, q3) * rp, d_zero);
+    }
+    sPS[ii][jj] = ps; sXT[ii][jj] = xt; sXQV[ii][jj] = xqv; sXQC[ii][jj] = xqc;
   }
-  if (f.omega) ST(f.omega, o3, om);
-  // adiabatic (hydrostatic), cpmf = cpd*(1+0.8 qv)
-  {
-    const double t = LD(f.a1t, o3) * rp;
-    const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
-    const double tv = t * (d_one + c->ep1 * qv);
-    const double rovcpm = c->rgas / (c->cpd * (d_one + 0.80 * qv));
-    td = td + (om * rovcpm * tv) / (c->ptop * rp + c->hsigma[k]);
+  for (int t = tid; t < SW2 * SH2; t += SBT) {
+    const int jj = t % SW2, ii = t / SW2, jg = J0 - 2 + jj, ig = I0 - 2 + ii;
+    double tb = 0.0, qvb = 0.0, qcb = 0.0;
+    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
+      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
+      const double r = LD(f.rpsb, q2);
+      tb = LD(f.a2t, q3) * r;
+      qvb = dmax(LD(f.a2qv, q3) * r, MINQQ);
+      qcb = dmax(LD(f.a2qc, q3) * r, d_zero);
+    }
+    sTB[ii][jj] = tb; sQVB[ii][jj] = qvb; sQCB[ii][jj] = qcb;
   }
-  // nudge3d
-  if (f.rgcr[o2 >> 3] > 0) {
-    const double xtb = s->xbctime + dt;
-    double xf, xg;
-    nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
-#define FGT(dj, di) ((LD(f.tb0, O3(dj, di)) + xtb * LD(f.tbt, O3(dj, di))) - LD(f.a2t, O3(dj, di)))
-    td = relax(td, xf, xg, FGT(0, 0), FGT(-1, 0), FGT(1, 0), FGT(0, -1), FGT(0, 1));
-#undef FGT
-  }
-  // diffu_x3d with xkc scaled as calc_coeff does (:241-243); tb3d = atm2 t * (1/psb)
-  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
-  if (f.xkcs) ST(f.xkcs, o3, xkcs);
-  td = diffu_x_point(g, td, xkcs, [&](int dj, int di) { return LD(f.a2t, O3(dj, di)) * LD(f.rpsb, O2(dj, di)); }, j, i);
-  // totals (tphy = 0), forecast, RA filter
-  const double tt = ((d_zero + td) + d_zero) + d_zero;
-  if (f.tten) ST(f.tten, o3, tt);
-  const double t1 = LD(f.a1t, o3), t2 = LD(f.a2t, o3);
-  const double ct = t2 + dt * tt;
-  const double d = c->gnu1 * (ct + t2 - d_two * t1);
-  ST(f.b2t, o3, t1 + d);
-  ST(f.b1t, o3, ct);
-}
-
-// K5. Moisture tendencies and forecast (before the negative-value fix):
-// hadvqv + vadvqv + nudge4d3d + diffu_x4d (qv); hadvqx + vadv4d(ind=1) + diffu_x4d (qc)
-// (Main/mod_tendency.F90:1361-1392, 1470, 1526, 292-294, 332-349, 375-380).
-__global__ __launch_bounds__(256) void k_moisture(Geom g, const Consts* __restrict__ c,
-                                                  const StepState* __restrict__ s, Fields f) {
-  THREAD_POINT(g.jce1, g.ice1);
+  __syncthreads();
+  const int tj = tid % SBJ, ti = tid / SBJ;
+  const int j = J0 + tj, i = I0 + ti;
   if (j > g.jce2 || i > g.ice2) return;
-  const uint32_t P8 = g.P8, L8 = g.L8;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
+  const uint32_t o2 = g.o2(j, i), o3 = o2 + kof;
   if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
     ST(f.cqv, o3, LD(f.a2qv, o3));
     ST(f.cqc, o3, LD(f.a2qc, o3));
+    if (f.xkcs) ST(f.xkcs, o3, LD(f.xkc, o3));
     return;
   }
-  const int kz = c->kz;
   const double dt = s->dt;
-  const double ps = LD(f.psa, o2);
-  // ---- qv
-  double tq = d_zero + hadv_point(c, f, o2, o3, P8, [&](int dj, int di) {
-    return dmax(LD(f.a1qv, O3(dj, di)) * LD(f.rpsa, O2(dj, di)), MINQQ); }, 2);
+  const int b1 = tj + 1, a1 = ti + 1, b2 = tj + 2, a2 = ti + 2;
+#define DT(S, dj, di) S[ti + (di)][tj + (dj)]
+#define H1T(S, dj, di) S[a1 + (di)][b1 + (dj)]
+  // mass fluxes of the cell (shared by the three scalars)
+  const double uavg1 = DT(sUMC, 0, 1) + DT(sUMC, 0, 0);
+  const double uavg2 = DT(sUMC, 1, 1) + DT(sUMC, 1, 0);
+  const double vavg1 = DT(sVMC, 1, 0) + DT(sVMC, 0, 0);
+  const double vavg2 = DT(sVMC, 1, 1) + DT(sVMC, 0, 1);
+  const double ps = H1T(sPS, 0, 0);
+  const double xm = LD(f.xmsf, o2);
+  const double rp = LD(f.rpsa, o2);
+  const double q0 = LD(f.qdot, o3), q1 = LD(f.qdot, o3 + L8);
+  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
+  if (f.xkcs) ST(f.xkcs, o3, xkcs);
+  // ================= temperature
+  {
+    double td = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXT, 0, 0), H1T(sXT, -1, 0),
+                                   H1T(sXT, 1, 0), H1T(sXT, 0, -1), H1T(sXT, 0, 1), 1);
+    const double t1 = LD(f.a1t, o3);
+    // vadv3d ind = 1 (Main/mod_advection.F90:771-783): pf/pb from psb (mkslice :263-271)
+    {
+      const double pb = LD(f.psb, o2), ptop = c->ptop, c287 = c->c287;
+#define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
+#define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
+      if (k >= 2)
+        td = td + (q0 * (c->twt1[k] * t1 * pow(PF(k) / PB(k), c287) +
+                         c->twt2[k] * LD(f.a1t, o3 - L8) * pow(PF(k) / PB(k - 1), c287))) * c->xds[k];
+      if (k + 1 <= kz)
+        td = td - (q1 * (c->twt1[k + 1] * LD(f.a1t, o3 + L8) * pow(PF(k + 1) / PB(k + 1), c287) +
+                         c->twt2[k + 1] * t1 * pow(PF(k + 1) / PB(k), c287))) * c->xds[k];
+#undef PB
+#undef PF
+    }
+    // omega, Main/mod_tendency.F90:1200-1214
+    double om;
+    {
+      const double dummy = d_one / (c->dx8 * LD(f.msfx, o2));
+      const double su = DT(sUD, 0, 0) + DT(sUD, 0, 1) + DT(sUD, 1, 1) + DT(sUD, 1, 0);
+      const double sv = DT(sVD, 0, 0) + DT(sVD, 0, 1) + DT(sVD, 1, 1) + DT(sVD, 1, 0);
+      const double x = su * (H1T(sPS, 1, 0) - H1T(sPS, -1, 0)) + sv * (H1T(sPS, 0, 1) - H1T(sPS, 0, -1));
+      om = d_half * (q1 + q0) * ps + c->hsigma[k] * (LD(f.pten, o2) + x * dummy);
+    }
+    if (f.omega) ST(f.omega, o3, om);
+    // adiabatic (hydrostatic), cpmf = cpd*(1+0.8 qv)
+    {
+      const double qv = H1T(sXQV, 0, 0);
+      const double tv = H1T(sXT, 0, 0) * (d_one + c->ep1 * qv);
+      const double rovcpm = c->rgas / (c->cpd * (d_one + 0.80 * qv));
+      td = td + (om * rovcpm * tv) / (c->ptop * rp + c->hsigma[k]);
+    }
+    // nudge3d
+    if (f.rgcr[o2 >> 3] > 0) {
+      const double xtb = s->xbctime + dt;
+      double xf, xg;
+      nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
+#define FGT(dj, di) ((LD(f.tb0, O3(dj, di)) + xtb * LD(f.tbt, O3(dj, di))) - LD(f.a2t, O3(dj, di)))
+      td = relax(td, xf, xg, FGT(0, 0), FGT(-1, 0), FGT(1, 0), FGT(0, -1), FGT(0, 1));
+#undef FGT
+    }
+    DIFFU_X(td, sTB);
+    const double tt = ((d_zero + td) + d_zero) + d_zero;
+    if (f.tten) ST(f.tten, o3, tt);
+    const double t2 = LD(f.a2t, o3);
+    const double ct = t2 + dt * tt;
+    const double d = c->gnu1 * (ct + t2 - d_two * t1);
+    ST(f.b2t, o3, t1 + d);
+    ST(f.b1t, o3, ct);
+  }
+  // ================= qv
+  double tq = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQV, 0, 0), H1T(sXQV, -1, 0),
+                                 H1T(sXQV, 1, 0), H1T(sXQV, 0, -1), H1T(sXQV, 0, 1), 2);
   {
     const double thr = MINQQ * ps;
-#define QV(dk) LD(f.a1qv, O3K(0, 0, dk))
-#define FGQ(K, dk) ((QV(dk) > thr && QV((dk) - 1) > thr) ? QV(dk) * pow(QV((dk) - 1) / QV(dk), c->qcon[K]) : d_zero)
-    if (k >= 2) tq = tq + LD(f.qdot, o3) * FGQ(k, 0) * c->xds[k];
-    if (k + 1 <= kz) tq = tq - LD(f.qdot, O3K(0, 0, 1)) * FGQ(k + 1, 1) * c->xds[k];
-#undef FGQ
-#undef QV
+    const double qc0 = LD(f.a1qv, o3);
+    if (k >= 2) {
+      const double qm = LD(f.a1qv, o3 - L8);
+      tq = tq + q0 * ((qc0 > thr && qm > thr) ? qc0 * pow(qm / qc0, c->qcon[k]) : d_zero) * c->xds[k];
+    }
+    if (k + 1 <= kz) {
+      const double qp = LD(f.a1qv, o3 + L8);
+      tq = tq - q1 * ((qp > thr && qc0 > thr) ? qp * pow(qc0 / qp, c->qcon[k + 1]) : d_zero) * c->xds[k];
+    }
   }
   if (f.rgcr[o2 >> 3] > 0) {
     const double xtb = s->xbctime + dt;
@@ -558,33 +639,37 @@ __global__ __launch_bounds__(256) void k_moisture(Geom g, const Consts* __restri
 #undef FGQ
     tq = tq + rfac * (xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0));
   }
-  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
-  tq = diffu_x_point(g, tq, xkcs, [&](int dj, int di) {
-    return dmax(LD(f.a2qv, O3(dj, di)) * LD(f.rpsb, O2(dj, di)), MINQQ); }, j, i);
-  // ---- qc
-  double tc = d_zero + hadv_point(c, f, o2, o3, P8, [&](int dj, int di) {
-    return dmax(LD(f.a1qc, O3(dj, di)) * LD(f.rpsa, O2(dj, di)), d_zero); }, 0);
+  DIFFU_X(tq, sQVB);
+  // ================= qc
+  double tc = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQC, 0, 0), H1T(sXQC, -1, 0),
+                                 H1T(sXQC, 1, 0), H1T(sXQC, 0, -1), H1T(sXQC, 0, 1), 0);
   {
     const double thr = MINQQ * MINQQ * ps;
-#define QD(dk) LD(f.qdot, O3K(0, 0, dk))
-#define QC(dk) LD(f.a1qc, O3K(0, 0, dk))
-#define FGC(K, dk) ((QD(dk) > d_zero)                                                                   \
-    ? ((QC((dk) - 1) > thr) ? QD(dk) * (c->twt1[K] * QC(dk) + c->twt2[K] * QC((dk) - 1)) : d_zero)     \
-    : ((QC(dk) > thr) ? QD(dk) * (c->twt1[K] * QC(dk) + c->twt2[K] * QC((dk) - 1)) : d_zero))
-    if (k >= 2) tc = tc + FGC(k, 0) * c->xds[k];
-    if (k + 1 <= kz) tc = tc - FGC(k + 1, 1) * c->xds[k];
-#undef FGC
-#undef QC
-#undef QD
+    const double c0 = LD(f.a1qc, o3);
+    if (k >= 2) {
+      const double cm = LD(f.a1qc, o3 - L8);
+      const double fl = (q0 > d_zero) ? ((cm > thr) ? q0 * (c->twt1[k] * c0 + c->twt2[k] * cm) : d_zero)
+                                      : ((c0 > thr) ? q0 * (c->twt1[k] * c0 + c->twt2[k] * cm) : d_zero);
+      tc = tc + fl * c->xds[k];
+    }
+    if (k + 1 <= kz) {
+      const double cp = LD(f.a1qc, o3 + L8);
+      const double fl = (q1 > d_zero) ? ((c0 > thr) ? q1 * (c->twt1[k + 1] * cp + c->twt2[k + 1] * c0) : d_zero)
+                                      : ((cp > thr) ? q1 * (c->twt1[k + 1] * cp + c->twt2[k + 1] * c0) : d_zero);
+      tc = tc - fl * c->xds[k];
+    }
   }
-  tc = diffu_x_point(g, tc, xkcs, [&](int dj, int di) {
-    return dmax(LD(f.a2qc, O3(dj, di)) * LD(f.rpsb, O2(dj, di)), d_zero); }, j, i);
+  DIFFU_X(tc, sQCB);
+#undef DT
+#undef H1T
   tq = ((d_zero + tq) + d_zero) + d_zero;
   tc = ((d_zero + tc) + d_zero) + d_zero;
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
   ST(f.cqv, o3, LD(f.a2qv, o3) + dt * tq);
   ST(f.cqc, o3, LD(f.a2qc, o3) + dt * tc);
 }
+#undef DIFFU_X
+#undef H2T
 
 // ---------------------------------------------------------------------------------------
 // K6. Negative-moisture fix + the RA filter of p* + the RAW filter of qv/qc, one pass
@@ -651,7 +736,13 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
     pa = psc;
   }
   if (k == 1) { ST(f.bpsa, o2, pa); ST(f.bpsb, o2, pb); }
+  // points k_momentum does not update keep their winds in the next buffers
+  if (!(in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))) {
+    ST(f.b1u, o3, LD(f.a1u, o3)); ST(f.b1v, o3, LD(f.a1v, o3));
+    ST(f.b2u, o3, LD(f.a2u, o3)); ST(f.b2v, o3, LD(f.a2v, o3));
+  }
   if (!ci) {
+    ST(f.b1t, o3, LD(f.a1t, o3)); ST(f.b2t, o3, LD(f.a2t, o3));
     ST(f.b1qv, o3, LD(f.a1qv, o3)); ST(f.b1qc, o3, LD(f.a1qc, o3));
     ST(f.b2qv, o3, LD(f.a2qv, o3)); ST(f.b2qc, o3, LD(f.a2qc, o3));
     return;

@@ -14,6 +14,10 @@ struct Seg {
 constexpr int MAXSEG = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
+// LDS-tiled momentum block (dot points j x i at one level)
+constexpr int MBJ = 64, MBI = 8, MBT = MBJ * MBI;
+// LDS-tiled scalar (t, qv, qc) block (cross points j x i at one level)
+constexpr int SBJ = 64, SBI = 8, SBT = SBJ * SBI;
 struct SegList {
   Seg s[MAXSEG];
   int n;
@@ -57,8 +61,7 @@ __global__ void k_surface_pressures(Geom g, Fields f);
 __global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxa, int nya, int nba,
                           int nxb);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
-__global__ void k_temperature(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
-__global__ void k_moisture(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
                                 const double* __restrict__ a1v, const double* __restrict__ a2u,

@@ -11,10 +11,8 @@ regcm_amd/csrc/kernels.hip with tendency diagnostics off:
   k_momentum    reads atm1 u,v,t,qv, atm2 u,v, qdot, xkc, phi (9) + u,v b0/bt in band (4 f_b);
                 writes next atm1/atm2 u,v (4); 2-D: msfd msfx-derived dmsf coriol rpsa rpsda rpsdb
                 psa psdota psdotb (9)
-  k_temperature reads atm1 t,u,v,qv, atm2 t, qdot, xkc (7) + t b0/bt in band (2 f_b);
-                writes next atm1/atm2 t (2); 2-D: 9
-  k_moisture    reads atm1 qv,qc,u,v, atm2 qv,qc, qdot, xkc (8) + q b0/bt in band (2 f_b);
-                writes cqv, cqc (2); 2-D: 7
+  k_scalars     reads atm1 u,v,t,qv,qc, atm2 t,qv,qc, qdot, xkc (10) + t,q b0/bt in band (4 f_b);
+                writes next atm1/atm2 t, cqv, cqc (4); 2-D: 12
   k_columns     reads atm1 u,v,t,qv,qc, atm2 u,v (7); writes qdot, phi, xkc (3); 2-D: 12
   k_qfilter     reads cqv,cqc, atm1/atm2 qv,qc (6); writes next atm1/atm2 qv,qc (4); 2-D: 5
   k_split_project reads atm1/atm2 u,v,t (6); 2-D: 3 nsplit slots x 2 + 8
@@ -30,8 +28,7 @@ def band_fraction(jx: int, iy: int, nspgx: int) -> float:
 # (3-D fields, 3-D fields in the band only, 2-D fields)
 KERNEL_FIELDS = {
     "k_momentum": (13, 4, 9),
-    "k_temperature": (9, 2, 9),
-    "k_moisture": (10, 2, 7),
+    "k_scalars": (14, 4, 12),
     "k_columns": (10, 0, 12),
     "k_qfilter": (10, 0, 5),
     "k_split_project": (6, 0, 20),
