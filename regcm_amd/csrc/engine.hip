@@ -186,7 +186,7 @@ const dim3 BLK(64, 4, 1);
 // Buffers that exchanges refer to, resolved per tile.
 enum class FK {
   A1U, A1V, A1T, A1QV, A1QC, A2U, A2V, A2T, A2QV, A2QC, PSA, PSB, PSDOTA, PSDOTB,
-  RPSDA, RPSDB, QDOT, XKC, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
+  RPSDA, RPSDB, QDOT, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
   UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR
 };
 
@@ -321,7 +321,7 @@ struct rcmdyn_engine {
     t.rpsa = dalloc(t, P); t.rpsb = dalloc(t, P); t.rpsda = dalloc(t, P); t.rpsdb = dalloc(t, P);
     t.psc = dalloc(t, P); t.psdota = dalloc(t, P); t.psdotb = dalloc(t, P); t.pten = dalloc(t, 2 * P);
     t.qdot = dalloc(t, P * (kz + 1));
-    t.xkc = dalloc(t, P3); t.phi = dalloc(t, P3);
+    t.phi = dalloc(t, P3);
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     t.depplane = talloc<int>(t, 2 * kz);
     t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
@@ -420,7 +420,7 @@ struct rcmdyn_engine {
       case FK::PSA: return t.psa_[c]; case FK::PSB: return t.psb_[c];
       case FK::PSDOTA: return t.psdota; case FK::PSDOTB: return t.psdotb;
       case FK::RPSDA: return t.rpsda; case FK::RPSDB: return t.rpsdb; case FK::QDOT: return t.qdot;
-      case FK::XKC: return t.xkc; case FK::CQV: return t.cqv; case FK::CQC: return t.cqc;
+      case FK::CQV: return t.cqv; case FK::CQC: return t.cqc;
       case FK::PHI: return t.phi; case FK::UU: return t.uu; case FK::VV: return t.vv;
       case FK::DHSUM: return t.dhsum; case FK::DELH: return t.delh;
       case FK::MSFX: return t.msfx; case FK::MSFD: return t.msfd; case FK::HT: return t.ht;
@@ -718,7 +718,7 @@ struct rcmdyn_engine {
     f.qb0 = t.qb0; f.qbt = t.qbt; f.pb0 = t.pb0; f.pbt = t.pbt;
     f.rpsa = t.rpsa; f.rpsb = t.rpsb; f.rpsda = t.rpsda; f.rpsdb = t.rpsdb; f.psc = t.psc;
     f.psdota = t.psdota; f.psdotb = t.psdotb; f.pten = t.pten; f.ptenn = t.pten + t.g.plane;
-    f.qdot = t.qdot; f.xkc = t.xkc; f.phi = t.phi; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
+    f.qdot = t.qdot; f.phi = t.phi; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
     f.depplane = t.depplane;
     if (diag) {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
@@ -742,16 +742,14 @@ struct rcmdyn_engine {
     // fields are recomputed where read, so their exchanges become exchanges of atm1/atm2
     xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz}, {FK::A1QC, kz}}, 1, 0);
     xch({{FK::A2U, kz}, {FK::A2V, kz}, {FK::A2T, kz}, {FK::A2QV, kz}, {FK::A2QC, kz}}, 2, 0);
-    // compute_omega columns, new_pressure, geopotential, calc_coeff (one launch)
+    // compute_omega columns, new_pressure, geopotential (calc_coeff is formed where it is
+    // read, in k_momentum and k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
-      const int nxa = (g.jce2 - g.jce1 + 64) / 64, nya = (g.ice2 - g.ice1 + 4) / 4;
-      const int nba = nxa * nya * kz, nxb = (g.jde2 - g.jde1 + 64) / 64;
-      KLAUNCH(k_columns, dim3(nba + t.nred), dim3(256), col_lds(), stream, g, dc, ds, fields(t), nxa, nya, nba,
-                         nxb);
+      KLAUNCH(k_columns, dim3(t.nred), dim3(256), col_lds(), stream, g, dc, ds, fields(t),
+              (g.jde2 - g.jde1 + 64) / 64);
     });
     xch(FK::QDOT, kz + 1, 1, 0);
-    xch(FK::XKC, kz, 1, 0);
     xch(FK::PHI, kz, 1, 1);
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {

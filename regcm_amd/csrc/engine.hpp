@@ -93,7 +93,7 @@ struct Tile {
   // work
   // 2-D reciprocals of the decoupling (decouple / mkslice, recomputed on the fly from them)
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten;
-  double *qdot, *xkc, *phi;
+  double *qdot, *phi;
   double *cqv, *cqc, *fqv, *fqc;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;

@@ -92,10 +92,7 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 }
 
 // ---------------------------------------------------------------------------------------
-// K2. Column work and the Smagorinsky coefficient in one launch (both only read the state):
-//  blocks [0, nba): calc_coeff, Main/mod_diffusion.F90:194-210 (unscaled xkc on jce/ice),
-//    ubd3d/vbd3d = atm2 * (1/psdotb) recomputed;
-//  blocks [nba, ..): 64 columns (j) of one row i each:
+// K2. Column work, 64 columns (j) of one row i per block:
 //    compute_omega column part, Main/mod_tendency.F90:1123-1156 (pten, qdot k-scan),
 //    new_pressure + nudge2d, :1428-1460 / Main/mod_bdycod.F90:4597-4766 (psc, nudged pten),
 //    the geopotential of the PGF, :1966-1995, 2033-2097 (alpha_hyd = 0, td == tva),
@@ -105,29 +102,12 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
 //  geopotential recurrence, each in the reference's sequential order.
 __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
-                                                 int nxa, int nya, int nba, int nxb) {
+                                                 int nxb) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   const uint32_t P8 = g.P8, L8 = g.L8;
-  const int b = blockIdx.x;
+  const int bb = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  if (b < nba) {
-    const int r = b % (nxa * nya);
-    const int j = g.jce1 + (r % nxa) * 64 + tx, i = g.ice1 + (r / nxa) * 4 + ty, k = b / (nxa * nya) + 1;
-    if (j > g.jce2 || i > g.ice2) return;
-    const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
-#define UBD(dj, di) (LD(f.a2u, O3(dj, di)) * LD(f.rpsdb, O2(dj, di)))
-#define VBD(dj, di) (LD(f.a2v, O3(dj, di)) * LD(f.rpsdb, O2(dj, di)))
-    const double dudx = UBD(1, 0) + UBD(1, 1) - UBD(0, 0) - UBD(0, 1);
-    const double dvdx = VBD(1, 0) + VBD(1, 1) - VBD(0, 0) - VBD(0, 1);
-    const double dudy = UBD(0, 1) + UBD(1, 1) - UBD(0, 0) - UBD(1, 0);
-    const double dvdy = VBD(0, 1) + VBD(1, 1) - VBD(0, 0) - VBD(1, 0);
-#undef UBD
-#undef VBD
-    const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
-    ST(f.xkc, o3, dmin(LD(f.hgfact, o2) + c->dydc * duv, c->xkhmax));
-    return;
-  }
-  const int bb = b - nba;
+
   const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + bb / nxb;
   const bool valid = j <= g.jde2;
   const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
@@ -246,7 +226,7 @@ constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i
 __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __restrict__ c,
                                                      const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
-  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
+  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2], sUB[TH2][TW2], sVB[TH2][TW2];
   __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
   const int tid = threadIdx.x;
   const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
@@ -255,6 +235,18 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
   const int kz = c->kz;
   const double ep1 = c->ep1;
+  // this thread's point and its point operands, loaded before the staging barrier so their
+  // latency overlaps it (threads past the interior read a valid interior address)
+  const int tj = tid % MBJ, ti = tid / MBJ;
+  const int j = J0 + tj, i = I0 + ti;
+  const bool valid = j <= g.jdi2 && i <= g.idi2;
+  const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jdi1, g.idi1), o3 = o2 + kof;
+  const double u1c = LD(f.a1u, o3), v1c = LD(f.a1v, o3), u2c = LD(f.a2u, o3), v2c = LD(f.a2v, o3);
+  const double u1m = (k >= 2) ? LD(f.a1u, o3 - L8) : 0.0, v1m = (k >= 2) ? LD(f.a1v, o3 - L8) : 0.0;
+  const double u1p = (k < kz) ? LD(f.a1u, o3 + L8) : 0.0, v1p = (k < kz) ? LD(f.a1v, o3 + L8) : 0.0;
+  const double dmsf = LD(f.dmsf, o2), cor = LD(f.coriol, o2), pdotb = LD(f.psdotb, o2);
+  const double pdota = LD(f.psdota, o2), mfd = LD(f.msfd, o2);
+  const int rgd = f.rgdt[o2 >> 3];
   // ---- stage (all loads independent)
   for (int t = tid; t < TW1 * TH1; t += MBT) {
     const int jj = t % TW1, ii = t / TW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
@@ -268,18 +260,20 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   }
   for (int t = tid; t < TW2 * TH2; t += MBT) {
     const int jj = t % TW2, ii = t / TW2, jg = J0 - 2 + jj, ig = I0 - 2 + ii;
-    double um = 0.0, vm = 0.0;
+    double um = 0.0, vm = 0.0, ub = 0.0, vb = 0.0;
     if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
       const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
       const double r = LD(f.rpsdb, q2), m = LD(f.msfd, q2);
-      um = (LD(f.a2u, q3) * r) / m;
-      vm = (LD(f.a2v, q3) * r) / m;
+      ub = LD(f.a2u, q3) * r;
+      vb = LD(f.a2v, q3) * r;
+      um = ub / m;
+      vm = vb / m;
     }
-    sUM[ii][jj] = um; sVM[ii][jj] = vm;
+    sUM[ii][jj] = um; sVM[ii][jj] = vm; sUB[ii][jj] = ub; sVB[ii][jj] = vb;
   }
   for (int t = tid; t < TW0 * TH0; t += MBT) {
     const int jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-    double tv = 0.0, q0 = 0.0, q1 = 0.0, ph = 0.0, ps = 0.0, xk = 0.0;
+    double tv = 0.0, q0 = 0.0, q1 = 0.0, ph = 0.0, ps = 0.0;
     if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
       const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
       const double rp = LD(f.rpsa, q2);
@@ -290,15 +284,29 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
       q1 = LD(f.qdot, q3 + L8);
       ph = LD(f.phi, q3);
       ps = LD(f.psa, q2);
-      xk = LD(f.xkc, q3);
     }
-    sTV[ii][jj] = tv; sQ0[ii][jj] = q0; sQ1[ii][jj] = q1; sPH[ii][jj] = ph; sPS[ii][jj] = ps; sXK[ii][jj] = xk;
+    sTV[ii][jj] = tv; sQ0[ii][jj] = q0; sQ1[ii][jj] = q1; sPH[ii][jj] = ph; sPS[ii][jj] = ps;
   }
   __syncthreads();
-  const int tj = tid % MBJ, ti = tid / MBJ;
-  const int j = J0 + tj, i = I0 + ti;
-  if (j > g.jdi2 || i > g.idi2) return;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + kof;
+  // calc_coeff Smagorinsky xkc (Main/mod_diffusion.F90:194-210) at the low-halo tile points from
+  // the staged ubd3d/vbd3d, over the cross points of the tile and its ghost ring toward
+  // neighbouring tiles (the reference's exchanged xkc there is the same computation)
+  for (int t = tid; t < TW0 * TH0; t += MBT) {
+    const int jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+    double xk = 0.0;
+    if (in(jg, g.jce1ga, g.jce2ga) && in(ig, g.ice1ga, g.ice2ga)) {
+      const int y = ii + 1, x = jj + 1;            // (jg, ig) in the halo-2 tiles
+      const double dudx = sUB[y][x + 1] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y + 1][x];
+      const double dvdx = sVB[y][x + 1] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y + 1][x];
+      const double dudy = sUB[y + 1][x] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y][x + 1];
+      const double dvdy = sVB[y + 1][x] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y][x + 1];
+      const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
+      xk = dmin(LD(f.hgfact, g.o2(jg, ig)) + c->dydc * duv, c->xkhmax);
+    }
+    sXK[ii][jj] = xk;
+  }
+  __syncthreads();
+  if (!valid) return;
   const double dt = s->dt;
   // tile coordinates of (j,i): halo-1 tiles (b1,a1), halo-2 (b2,a2), low-halo (b0,a0)
   const int b1 = tj + 1, a1 = ti + 1, b2 = tj + 2, a2 = ti + 2, b0 = tj + 1, a0 = ti + 1;
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
     ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
     vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
     vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
-    const double dm = LD(f.dmsf, o2);
+    const double dm = dmsf;
     ut = d_zero - dm * ((ue + u0) * ucmonb - (u0 + uw) * ucmonc + (un + u0) * vcmonb - (u0 + us) * vcmonc);
     vt = d_zero - dm * ((ve + v0) * ucmonb - (v0 + vw) * ucmonc + (vn + v0) * vcmonb - (v0 + vs) * vcmonc);
   }
@@ -331,31 +339,30 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
 #undef VMC
 #undef UD
 #undef VD
-  const double u1c = LD(f.a1u, o3), v1c = LD(f.a1v, o3);
   // vadvuv: flux at interface k (from loop index k) then interface k+1 (loop index k+1)
   {
 #define QQ(S) (d_rfour * (S[a0][b0] + S[a0][b0 - 1] + S[a0 - 1][b0] + S[a0 - 1][b0 - 1]))
     if (k >= 2) {
       const double qq = QQ(sQ0);
-      const double uu = qq * (c->twt1[k] * u1c + c->twt2[k] * LD(f.a1u, o3 - L8));
-      const double vv = qq * (c->twt1[k] * v1c + c->twt2[k] * LD(f.a1v, o3 - L8));
+      const double uu = qq * (c->twt1[k] * u1c + c->twt2[k] * u1m);
+      const double vv = qq * (c->twt1[k] * v1c + c->twt2[k] * v1m);
       ut = ut + uu * c->xds[k];
       vt = vt + vv * c->xds[k];
     }
     if (k + 1 <= kz) {
       const double qq = QQ(sQ1);
-      const double uu = qq * (c->twt1[k + 1] * LD(f.a1u, o3 + L8) + c->twt2[k + 1] * u1c);
-      const double vv = qq * (c->twt1[k + 1] * LD(f.a1v, o3 + L8) + c->twt2[k + 1] * v1c);
+      const double uu = qq * (c->twt1[k + 1] * u1p + c->twt2[k + 1] * u1c);
+      const double vv = qq * (c->twt1[k + 1] * v1p + c->twt2[k + 1] * v1c);
       ut = ut - uu * c->xds[k];
       vt = vt - vv * c->xds[k];
     }
 #undef QQ
   }
   // curvature (hydrostatic Coriolis)
-  ut = ut + LD(f.coriol, o2) * v1c;
-  vt = vt - LD(f.coriol, o2) * u1c;
+  ut = ut + cor * v1c;
+  vt = vt - cor * u1c;
   // nudgeuv
-  if (f.rgdt[o2 >> 3] > 0) {
+  if (rgd > 0) {
     const double xt = s->xbctime + dt;
     double xf, xg;
     const int ib = f.ibdt[o2 >> 3];
@@ -370,7 +377,7 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248)
   {
     double xkd = d_rfour * (sXK[a0][b0] + sXK[a0 - 1][b0 - 1] + sXK[a0 - 1][b0] + sXK[a0][b0 - 1]);
-    xkd = xkd * c->rdxsq * LD(f.psdotb, o2);
+    xkd = xkd * c->rdxsq * pdotb;
 #define UM(S, dj, di) S[a2 + (di)][b2 + (dj)]
     if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
       ut = ut - xkd * (z4_c1 * (UM(sUM, 2, 0) + UM(sUM, -2, 0) + UM(sUM, 0, 2) + UM(sUM, 0, -2)) +
@@ -395,15 +402,14 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient)
   {
     double rtbar = d_rfour * (sTV[a0 - 1][b0 - 1] + sTV[a0][b0 - 1] + sTV[a0 - 1][b0] + sTV[a0][b0]);
-    rtbar = c->rgas * rtbar * LD(f.psdota, o2);
+    rtbar = c->rgas * rtbar * pdota;
     const double hs = c->hsigma[k], pt = c->ptop;
-    const double mfd = LD(f.msfd, o2);
     const double den = c->dx * mfd;
     const double p00 = sPS[a0][b0], p0m = sPS[a0 - 1][b0], pm0 = sPS[a0][b0 - 1], pmm = sPS[a0 - 1][b0 - 1];
     ut = ut - rtbar * (log(d_half * (p00 + p0m) * hs + pt) - log(d_half * (pm0 + pmm) * hs + pt)) / den;
     vt = vt - rtbar * (log(d_half * (p00 + pm0) * hs + pt) - log(d_half * (pmm + p0m) * hs + pt)) / den;
     const double den2 = c->dx2 * mfd;
-    const double pd = LD(f.psdota, o2);
+    const double pd = pdota;
     const double f00 = sPH[a0][b0], f0m = sPH[a0 - 1][b0], fm0 = sPH[a0][b0 - 1], fmm = sPH[a0 - 1][b0 - 1];
     ut = ut - pd * (f00 + f0m - fm0 - fmm) / den2;
     vt = vt - pd * (f00 + fm0 - f0m - fmm) / den2;
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   vt = (d_zero + vt) + d_zero;
   if (f.uten) { ST(f.uten, o3, ut); ST(f.vten, o3, vt); }
   const double g1 = c->gnu1;
-  const double u2 = LD(f.a2u, o3), v2 = LD(f.a2v, o3);
+  const double u2 = u2c, v2 = v2c;
   const double cu = u2 + dt * ut, cv = v2 + dt * vt;
   double d = g1 * (cu + u2 - d_two * u1c);
   ST(f.b2u, o3, u1c + d);
@@ -488,7 +494,7 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
 
 __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __restrict__ c,
                                                     const StepState* __restrict__ s, Fields f) {
-  __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW];
+  __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
   __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
   __shared__ double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
   const int tid = threadIdx.x;
@@ -498,16 +504,34 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
   const int kz = c->kz;
   (void)P8;
+  // this thread's point and its point operands, loaded before the staging barrier
+  const int tj = tid % SBJ, ti = tid / SBJ;
+  const int j = J0 + tj, i = I0 + ti;
+  const bool valid = j <= g.jce2 && i <= g.ice2;
+  const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jce1, g.ice1), o3 = o2 + kof;
+  const double t1 = LD(f.a1t, o3), t2 = LD(f.a2t, o3), qv2 = LD(f.a2qv, o3), qc2 = LD(f.a2qc, o3);
+  const double qv1 = LD(f.a1qv, o3), qc1 = LD(f.a1qc, o3);
+  const double t1m = (k >= 2) ? LD(f.a1t, o3 - L8) : 0.0, qv1m = (k >= 2) ? LD(f.a1qv, o3 - L8) : 0.0;
+  const double qc1m = (k >= 2) ? LD(f.a1qc, o3 - L8) : 0.0;
+  const double t1p = (k < kz) ? LD(f.a1t, o3 + L8) : 0.0, qv1p = (k < kz) ? LD(f.a1qv, o3 + L8) : 0.0;
+  const double qc1p = (k < kz) ? LD(f.a1qc, o3 + L8) : 0.0;
+  const double q0 = LD(f.qdot, o3), q1 = LD(f.qdot, o3 + L8);
+  const double xm = LD(f.xmsf, o2), rp = LD(f.rpsa, o2), pb = LD(f.psb, o2), mx = LD(f.msfx, o2);
+  const double ptn = LD(f.pten, o2), hgf = LD(f.hgfact, o2);
+  const int rgc = f.rgcr[o2 >> 3];
   // ---- stage
   for (int t = tid; t < SDW * SDH; t += SBT) {
     const int jj = t % SDW, ii = t / SDW, jg = J0 + jj, ig = I0 + ii;
-    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0;
+    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0, ub = 0.0, vb = 0.0;
     if (jg <= jhi && ig <= ihi) {
       const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
       const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
+      const double rb = LD(f.rpsdb, q2);
       umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
+      ub = LD(f.a2u, q3) * rb;
+      vb = LD(f.a2v, q3) * rb;
     }
-    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd;
+    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd; sUB[ii][jj] = ub; sVB[ii][jj] = vb;
   }
   for (int t = tid; t < SW1 * SH1; t += SBT) {
     const int jj = t % SW1, ii = t / SW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
@@ -535,19 +559,26 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
     sTB[ii][jj] = tb; sQVB[ii][jj] = qvb; sQCB[ii][jj] = qcb;
   }
   __syncthreads();
-  const int tj = tid % SBJ, ti = tid / SBJ;
-  const int j = J0 + tj, i = I0 + ti;
-  if (j > g.jce2 || i > g.ice2) return;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + kof;
+  if (!valid) return;
+#define DT(S, dj, di) S[ti + (di)][tj + (dj)]
+  // calc_coeff Smagorinsky xkc, Main/mod_diffusion.F90:194-210 (ubd3d/vbd3d = atm2 * (1/psdotb))
+  double xkc;
+  {
+    const double dudx = DT(sUB, 1, 0) + DT(sUB, 1, 1) - DT(sUB, 0, 0) - DT(sUB, 0, 1);
+    const double dvdx = DT(sVB, 1, 0) + DT(sVB, 1, 1) - DT(sVB, 0, 0) - DT(sVB, 0, 1);
+    const double dudy = DT(sUB, 0, 1) + DT(sUB, 1, 1) - DT(sUB, 0, 0) - DT(sUB, 1, 0);
+    const double dvdy = DT(sVB, 0, 1) + DT(sVB, 1, 1) - DT(sVB, 0, 0) - DT(sVB, 1, 0);
+    const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
+    xkc = dmin(hgf + c->dydc * duv, c->xkhmax);
+  }
   if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
-    ST(f.cqv, o3, LD(f.a2qv, o3));
-    ST(f.cqc, o3, LD(f.a2qc, o3));
-    if (f.xkcs) ST(f.xkcs, o3, LD(f.xkc, o3));
+    ST(f.cqv, o3, qv2);
+    ST(f.cqc, o3, qc2);
+    if (f.xkcs) ST(f.xkcs, o3, xkc);
     return;
   }
   const double dt = s->dt;
   const int b1 = tj + 1, a1 = ti + 1, b2 = tj + 2, a2 = ti + 2;
-#define DT(S, dj, di) S[ti + (di)][tj + (dj)]
 #define H1T(S, dj, di) S[a1 + (di)][b1 + (dj)]
   // mass fluxes of the cell (shared by the three scalars)
   const double uavg1 = DT(sUMC, 0, 1) + DT(sUMC, 0, 0);
@@ -555,26 +586,22 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   const double vavg1 = DT(sVMC, 1, 0) + DT(sVMC, 0, 0);
   const double vavg2 = DT(sVMC, 1, 1) + DT(sVMC, 0, 1);
   const double ps = H1T(sPS, 0, 0);
-  const double xm = LD(f.xmsf, o2);
-  const double rp = LD(f.rpsa, o2);
-  const double q0 = LD(f.qdot, o3), q1 = LD(f.qdot, o3 + L8);
-  const double xkcs = LD(f.xkc, o3) * c->rdxsq * LD(f.psb, o2);
+  const double xkcs = xkc * c->rdxsq * pb;
   if (f.xkcs) ST(f.xkcs, o3, xkcs);
   // ================= temperature
   {
     double td = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXT, 0, 0), H1T(sXT, -1, 0),
                                    H1T(sXT, 1, 0), H1T(sXT, 0, -1), H1T(sXT, 0, 1), 1);
-    const double t1 = LD(f.a1t, o3);
     // vadv3d ind = 1 (Main/mod_advection.F90:771-783): pf/pb from psb (mkslice :263-271)
     {
-      const double pb = LD(f.psb, o2), ptop = c->ptop, c287 = c->c287;
+      const double ptop = c->ptop, c287 = c->c287;
 #define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
 #define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
       if (k >= 2)
         td = td + (q0 * (c->twt1[k] * t1 * pow(PF(k) / PB(k), c287) +
-                         c->twt2[k] * LD(f.a1t, o3 - L8) * pow(PF(k) / PB(k - 1), c287))) * c->xds[k];
+                         c->twt2[k] * t1m * pow(PF(k) / PB(k - 1), c287))) * c->xds[k];
       if (k + 1 <= kz)
-        td = td - (q1 * (c->twt1[k + 1] * LD(f.a1t, o3 + L8) * pow(PF(k + 1) / PB(k + 1), c287) +
+        td = td - (q1 * (c->twt1[k + 1] * t1p * pow(PF(k + 1) / PB(k + 1), c287) +
                          c->twt2[k + 1] * t1 * pow(PF(k + 1) / PB(k), c287))) * c->xds[k];
 #undef PB
 #undef PF
@@ -582,11 +609,11 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
     // omega, Main/mod_tendency.F90:1200-1214
     double om;
     {
-      const double dummy = d_one / (c->dx8 * LD(f.msfx, o2));
+      const double dummy = d_one / (c->dx8 * mx);
       const double su = DT(sUD, 0, 0) + DT(sUD, 0, 1) + DT(sUD, 1, 1) + DT(sUD, 1, 0);
       const double sv = DT(sVD, 0, 0) + DT(sVD, 0, 1) + DT(sVD, 1, 1) + DT(sVD, 1, 0);
       const double x = su * (H1T(sPS, 1, 0) - H1T(sPS, -1, 0)) + sv * (H1T(sPS, 0, 1) - H1T(sPS, 0, -1));
-      om = d_half * (q1 + q0) * ps + c->hsigma[k] * (LD(f.pten, o2) + x * dummy);
+      om = d_half * (q1 + q0) * ps + c->hsigma[k] * (ptn + x * dummy);
     }
     if (f.omega) ST(f.omega, o3, om);
     // adiabatic (hydrostatic), cpmf = cpd*(1+0.8 qv)
@@ -597,7 +624,7 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
       td = td + (om * rovcpm * tv) / (c->ptop * rp + c->hsigma[k]);
     }
     // nudge3d
-    if (f.rgcr[o2 >> 3] > 0) {
+    if (rgc > 0) {
       const double xtb = s->xbctime + dt;
       double xf, xg;
       nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
@@ -608,7 +635,6 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
     DIFFU_X(td, sTB);
     const double tt = ((d_zero + td) + d_zero) + d_zero;
     if (f.tten) ST(f.tten, o3, tt);
-    const double t2 = LD(f.a2t, o3);
     const double ct = t2 + dt * tt;
     const double d = c->gnu1 * (ct + t2 - d_two * t1);
     ST(f.b2t, o3, t1 + d);
@@ -619,17 +645,17 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
                                  H1T(sXQV, 1, 0), H1T(sXQV, 0, -1), H1T(sXQV, 0, 1), 2);
   {
     const double thr = MINQQ * ps;
-    const double qc0 = LD(f.a1qv, o3);
+    const double qc0 = qv1;
     if (k >= 2) {
-      const double qm = LD(f.a1qv, o3 - L8);
+      const double qm = qv1m;
       tq = tq + q0 * ((qc0 > thr && qm > thr) ? qc0 * pow(qm / qc0, c->qcon[k]) : d_zero) * c->xds[k];
     }
     if (k + 1 <= kz) {
-      const double qp = LD(f.a1qv, o3 + L8);
+      const double qp = qv1p;
       tq = tq - q1 * ((qp > thr && qc0 > thr) ? qp * pow(qc0 / qp, c->qcon[k + 1]) : d_zero) * c->xds[k];
     }
   }
-  if (f.rgcr[o2 >> 3] > 0) {
+  if (rgc > 0) {
     const double xtb = s->xbctime + dt;
     const double nfac = 1.0e3, rfac = d_one / nfac;
     double xf, xg;
@@ -645,15 +671,15 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
                                  H1T(sXQC, 1, 0), H1T(sXQC, 0, -1), H1T(sXQC, 0, 1), 0);
   {
     const double thr = MINQQ * MINQQ * ps;
-    const double c0 = LD(f.a1qc, o3);
+    const double c0 = qc1;
     if (k >= 2) {
-      const double cm = LD(f.a1qc, o3 - L8);
+      const double cm = qc1m;
       const double fl = (q0 > d_zero) ? ((cm > thr) ? q0 * (c->twt1[k] * c0 + c->twt2[k] * cm) : d_zero)
                                       : ((c0 > thr) ? q0 * (c->twt1[k] * c0 + c->twt2[k] * cm) : d_zero);
       tc = tc + fl * c->xds[k];
     }
     if (k + 1 <= kz) {
-      const double cp = LD(f.a1qc, o3 + L8);
+      const double cp = qc1p;
       const double fl = (q1 > d_zero) ? ((c0 > thr) ? q1 * (c->twt1[k + 1] * cp + c->twt2[k + 1] * c0) : d_zero)
                                       : ((cp > thr) ? q1 * (c->twt1[k + 1] * cp + c->twt2[k + 1] * c0) : d_zero);
       tc = tc - fl * c->xds[k];
@@ -665,8 +691,8 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   tq = ((d_zero + tq) + d_zero) + d_zero;
   tc = ((d_zero + tc) + d_zero) + d_zero;
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
-  ST(f.cqv, o3, LD(f.a2qv, o3) + dt * tq);
-  ST(f.cqc, o3, LD(f.a2qc, o3) + dt * tc);
+  ST(f.cqv, o3, qv2 + dt * tq);
+  ST(f.cqc, o3, qc2 + dt * tc);
 }
 #undef DIFFU_X
 #undef H2T

@@ -39,7 +39,7 @@ struct Fields {
   const int16_t *ibcr, *ibdt;
   double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten, *ptenn;
-  double *qdot, *xkc, *phi, *cqv, *cqc, *fqv, *fqc;
+  double *qdot, *phi, *cqv, *cqc, *fqv, *fqc;
   int* depplane;
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
@@ -58,8 +58,7 @@ struct QFix {
 };
 
 __global__ void k_surface_pressures(Geom g, Fields f);
-__global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxa, int nya, int nba,
-                          int nxb);
+__global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
