@@ -226,7 +226,14 @@ constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i
 __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __restrict__ c,
                                                      const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
-  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2], sUB[TH2][TW2], sVB[TH2][TW2];
+  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
+  // ubd3d/vbd3d (consumed by xkc) share storage with the PGF log terms formed afterwards
+  __shared__ union {
+    struct { double UB[TH2][TW2], VB[TH2][TW2]; } b;
+    struct { double LU[MBI][TW0], LV[TH0][MBJ]; } l;
+  } sX;
+#define sUB sX.b.UB
+#define sVB sX.b.VB
   __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
   const int tid = threadIdx.x;
   const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
@@ -304,6 +311,23 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
       xk = dmin(LD(f.hgfact, g.o2(jg, ig)) + c->dydc * duv, c->xkhmax);
     }
     sXK[ii][jj] = xk;
+  }
+  __syncthreads();
+#undef sUB
+#undef sVB
+  // PGF log terms (:1996-2025): the u term is LU(j,i) - LU(j-1,i), the v term LV(j,i) - LV(j,i-1),
+  // LU(j,i) = log(0.5*(psa(j,i) + psa(j,i-1))*hs + ptop), LV(j,i) = log(0.5*(psa(j,i) + psa(j-1,i))*hs
+  // + ptop): each log is formed once per staged point instead of twice per output
+  {
+    const double hs = c->hsigma[k], pt = c->ptop;
+    for (int t = tid; t < TW0 * MBI; t += MBT) {
+      const int jj = t % TW0, ii = t / TW0;                  // (J0-1+jj, I0+ii)
+      sX.l.LU[ii][jj] = log(d_half * (sPS[ii + 1][jj] + sPS[ii][jj]) * hs + pt);
+    }
+    for (int t = tid; t < MBJ * TH0; t += MBT) {
+      const int jj = t % MBJ, ii = t / MBJ;                  // (J0+jj, I0-1+ii)
+      sX.l.LV[ii][jj] = log(d_half * (sPS[ii][jj + 1] + sPS[ii][jj]) * hs + pt);
+    }
   }
   __syncthreads();
   if (!valid) return;
@@ -403,11 +427,9 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   {
     double rtbar = d_rfour * (sTV[a0 - 1][b0 - 1] + sTV[a0][b0 - 1] + sTV[a0 - 1][b0] + sTV[a0][b0]);
     rtbar = c->rgas * rtbar * pdota;
-    const double hs = c->hsigma[k], pt = c->ptop;
     const double den = c->dx * mfd;
-    const double p00 = sPS[a0][b0], p0m = sPS[a0 - 1][b0], pm0 = sPS[a0][b0 - 1], pmm = sPS[a0 - 1][b0 - 1];
-    ut = ut - rtbar * (log(d_half * (p00 + p0m) * hs + pt) - log(d_half * (pm0 + pmm) * hs + pt)) / den;
-    vt = vt - rtbar * (log(d_half * (p00 + pm0) * hs + pt) - log(d_half * (pmm + p0m) * hs + pt)) / den;
+    ut = ut - rtbar * (sX.l.LU[ti][tj + 1] - sX.l.LU[ti][tj]) / den;
+    vt = vt - rtbar * (sX.l.LV[ti + 1][tj] - sX.l.LV[ti][tj]) / den;
     const double den2 = c->dx2 * mfd;
     const double pd = pdota;
     const double f00 = sPH[a0][b0], f0m = sPH[a0 - 1][b0], fm0 = sPH[a0][b0 - 1], fmm = sPH[a0 - 1][b0 - 1];
@@ -444,6 +466,11 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
 constexpr int SDW = SBJ + 1, SDH = SBI + 1;    // dot points j..j+SBJ, i..i+SBI
 constexpr int SW1 = SBJ + 2, SH1 = SBI + 2;    // halo 1
 constexpr int SW2 = SBJ + 4, SH2 = SBI + 4;    // halo 2
+
+// x**y for x > 0 as exp(y*log(x)): 140 VALU instructions against 226 for OCML pow, within
+// 2 ulp of it for the arguments here (layer pressure ratios, adjacent-level humidity ratios);
+// the reference's libm pow differs from OCML's by ulps anyway (tests/test_parity_gpu.py bounds)
+__device__ __forceinline__ double powpos(double x, double y) { return exp(y * log(x)); }
 
 // upstream flux-form advection of one scalar (hadvt/hadvqv/hadvqx, Main/mod_advection.F90:
 // 337-386, 547-596, 639-653); limiter 0 none, 1 t_extrema, 2 q_rel_extrema
@@ -598,11 +625,11 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
 #define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
 #define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
       if (k >= 2)
-        td = td + (q0 * (c->twt1[k] * t1 * pow(PF(k) / PB(k), c287) +
-                         c->twt2[k] * t1m * pow(PF(k) / PB(k - 1), c287))) * c->xds[k];
+        td = td + (q0 * (c->twt1[k] * t1 * powpos(PF(k) / PB(k), c287) +
+                         c->twt2[k] * t1m * powpos(PF(k) / PB(k - 1), c287))) * c->xds[k];
       if (k + 1 <= kz)
-        td = td - (q1 * (c->twt1[k + 1] * t1p * pow(PF(k + 1) / PB(k + 1), c287) +
-                         c->twt2[k + 1] * t1 * pow(PF(k + 1) / PB(k), c287))) * c->xds[k];
+        td = td - (q1 * (c->twt1[k + 1] * t1p * powpos(PF(k + 1) / PB(k + 1), c287) +
+                         c->twt2[k + 1] * t1 * powpos(PF(k + 1) / PB(k), c287))) * c->xds[k];
 #undef PB
 #undef PF
     }
@@ -648,11 +675,11 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
     const double qc0 = qv1;
     if (k >= 2) {
       const double qm = qv1m;
-      tq = tq + q0 * ((qc0 > thr && qm > thr) ? qc0 * pow(qm / qc0, c->qcon[k]) : d_zero) * c->xds[k];
+      tq = tq + q0 * ((qc0 > thr && qm > thr) ? qc0 * powpos(qm / qc0, c->qcon[k]) : d_zero) * c->xds[k];
     }
     if (k + 1 <= kz) {
       const double qp = qv1p;
-      tq = tq - q1 * ((qp > thr && qc0 > thr) ? qp * pow(qc0 / qp, c->qcon[k + 1]) : d_zero) * c->xds[k];
+      tq = tq - q1 * ((qp > thr && qc0 > thr) ? qp * powpos(qc0 / qp, c->qcon[k + 1]) : d_zero) * c->xds[k];
     }
   }
   if (rgc > 0) {
