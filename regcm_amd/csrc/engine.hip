@@ -746,7 +746,7 @@ struct rcmdyn_engine {
     // read, in k_momentum and k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
-      KLAUNCH(k_columns, dim3(t.nred), dim3(256), col_lds(), stream, g, dc, ds, fields(t),
+      KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t),
               (g.jde2 - g.jde1 + 64) / 64);
     });
     xch(FK::QDOT, kz + 1, 1, 0);
@@ -763,7 +763,7 @@ struct rcmdyn_engine {
     xch({{FK::CQV, kz}, {FK::CQC, kz}}, 1, 0);
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     each([&](Tile& t) {
-      KLAUNCH(k_qfilter, grid3(t.g.nj, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
+      KLAUNCH(k_qfilter, grid3((t.g.nj + 1) / 2, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
       t.cur = 1 - t.cur;
     });
     // splitf, Main/mod_split.F90:243-461
@@ -775,7 +775,7 @@ struct rcmdyn_engine {
       QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
              t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.depplane};
       const int nxp = (g.jde2 - g.jde1 + 64) / 64, nproj = nxp * (g.ide2 - g.ide1 + 1);
-      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(256), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
+      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
     });
@@ -786,7 +786,7 @@ struct rcmdyn_engine {
       each([&](Tile& t) {
         const Geom& g = t.g;
         dim3 gr((g.jce2 - g.jce1 + SPB) / SPB, (g.ice2 - g.ice1 + SPB) / SPB, ns);
-        KLAUNCH(k_spstep_fused, gr, dim3(32, 8), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
+        KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
                            t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
       });
     } else {
@@ -811,7 +811,7 @@ struct rcmdyn_engine {
       Tile& t = tiles[q];
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_split_correct, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
+      KLAUNCH(k_split_correct, grid3((g.jde2 - g.jde1 + 2) / 2, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
                          dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
                          t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total);
     }

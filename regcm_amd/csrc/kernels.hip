@@ -101,12 +101,12 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  terms (mass divergence, td, tvfac, the log ratios of the hypsometric equation) into LDS,
 //  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
 //  geopotential recurrence, each in the reference's sequential order.
-__global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+__global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxb) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
   const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + bb / nxb;
   const bool valid = j <= g.jde2;
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
     const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
     const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
     rp = LD(f.rpsa, o2);
-    for (int k = ty + 1; k <= kz; k += 4) {
+    for (int k = ty + 1; k <= kz; k += 8) {
       const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
       const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
                        LD(f.a1u, o3) * m00;
@@ -195,11 +195,11 @@ __global__ __launch_bounds__(256) void k_columns(Geom g, const Consts* __restric
     }
   }
   // per-block partial of the noise sums (fixed tree); k_split_correct sums the partials
-  __shared__ double sa[256], sb[256];
+  __shared__ double sa[512], sb[512];
   const int t = threadIdx.x;
   sa[t] = na; sb[t] = nb;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = 256; w > 0; w >>= 1) {
     if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
     __syncthreads();
   }
@@ -775,47 +775,70 @@ __device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, do
   }
 }
 
+// Two adjacent points (j, j+1) per thread with 16-byte accesses (rows start 128-B aligned and
+// pairs start at even j - j0); the second point of a pair may fall in the row padding.
+#define LD2(a, o) (*(const double2*)((const char*)(a) + (uint32_t)(o)))
+#define ST2(a, o, v) (*(double2*)((char*)(a) + (uint32_t)(o)) = (v))
 __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  const uint32_t L8 = g.L8;
-  const uint32_t o2 = g.o2(j, i), o3 = o2 + (uint32_t)(k - 1) * L8;
-  const bool ci = in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
-  double pa = LD(f.psa, o2), pb = LD(f.psb, o2);
-  if (ci) {
-    const double psc = LD(f.psc, o2);
-    const double d = c->gnu1 * (psc + pb - d_two * pa);
-    pb = pa + d;
-    pa = psc;
+  const int jp = g.j0 + 2 * (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int i = g.i0 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int k = (int)blockIdx.z + 1;
+  if (jp >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+  const uint32_t o2 = g.o2(jp, i), o3 = o2 + (uint32_t)(k - 1) * g.L8;
+  const bool ici = in(i, g.ici1, g.ici2), idi = in(i, g.idi1, g.idi2);
+  const bool ci0 = ici && in(jp, g.jci1, g.jci2), ci1 = ici && in(jp + 1, g.jci1, g.jci2);
+  const bool di0 = idi && in(jp, g.jdi1, g.jdi2), di1 = idi && in(jp + 1, g.jdi1, g.jdi2);
+  // p* RA filter on the fly (k = 1 threads store it)
+  double2 pa = LD2(f.psa, o2), pb = LD2(f.psb, o2);
+  if (ci0 || ci1) {
+    const double2 psc = LD2(f.psc, o2);
+    if (ci0) { const double d = c->gnu1 * (psc.x + pb.x - d_two * pa.x); pb.x = pa.x + d; pa.x = psc.x; }
+    if (ci1) { const double d = c->gnu1 * (psc.y + pb.y - d_two * pa.y); pb.y = pa.y + d; pa.y = psc.y; }
   }
-  if (k == 1) { ST(f.bpsa, o2, pa); ST(f.bpsb, o2, pb); }
-  // points k_momentum does not update keep their winds in the next buffers
-  if (!(in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))) {
-    ST(f.b1u, o3, LD(f.a1u, o3)); ST(f.b1v, o3, LD(f.a1v, o3));
-    ST(f.b2u, o3, LD(f.a2u, o3)); ST(f.b2v, o3, LD(f.a2v, o3));
+  if (k == 1) { ST2(f.bpsa, o2, pa); ST2(f.bpsb, o2, pb); }
+  // points k_momentum / k_scalars do not update keep their values in the next buffers
+  {
+    double2 x;
+#define KEEP(dst, src, upd) x = LD2(dst, o3); { const double2 y = LD2(src, o3);              \
+    if (!upd##0) x.x = y.x; if (!upd##1) x.y = y.y; } ST2(dst, o3, x);
+    if (!(di0 && di1)) { KEEP(f.b1u, f.a1u, di) KEEP(f.b1v, f.a1v, di) KEEP(f.b2u, f.a2u, di) KEEP(f.b2v, f.a2v, di) }
+    if (!(ci0 && ci1)) { KEEP(f.b1t, f.a1t, ci) KEEP(f.b2t, f.a2t, ci) }
+#undef KEEP
   }
-  if (!ci) {
-    ST(f.b1t, o3, LD(f.a1t, o3)); ST(f.b2t, o3, LD(f.a2t, o3));
-    ST(f.b1qv, o3, LD(f.a1qv, o3)); ST(f.b1qc, o3, LD(f.a1qc, o3));
-    ST(f.b2qv, o3, LD(f.a2qv, o3)); ST(f.b2qc, o3, LD(f.a2qc, o3));
+  if (!ci0 && !ci1) {
+    ST2(f.b1qv, o3, LD2(f.a1qv, o3)); ST2(f.b1qc, o3, LD2(f.a1qc, o3));
+    ST2(f.b2qv, o3, LD2(f.a2qv, o3)); ST2(f.b2qc, o3, LD2(f.a2qc, o3));
     return;
   }
   for (int n = 0; n < 2; n++) {
     const double* sv = n ? f.cqc : f.cqv;
     double* fx = n ? f.fqc : f.fqv;
-    double v = LD(sv, o3);
-    if (v < d_zero) {
-      if (negfix_dependent(g, sv, j, i, k)) {
-        atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
-        continue;                       // fixed and filtered by the serial sweep
+    const double2 cv = LD2(sv, o3);
+    const double2 o1 = LD2(n ? f.a1qc : f.a1qv, o3), o2v = LD2(n ? f.a2qc : f.a2qv, o3);
+    double2 n1, n2;
+    for (int q = 0; q < 2; q++) {
+      const int j = jp + q;
+      const bool ci = q ? ci1 : ci0;
+      const double a1 = q ? o1.y : o1.x, a2 = q ? o2v.y : o2v.x;
+      double r1 = a1, r2 = a2;                  // ring points keep their values
+      if (ci) {
+        double v = q ? cv.y : cv.x;
+        bool done = true;
+        if (v < d_zero) {
+          if (negfix_dependent(g, sv, j, i, k)) {
+            atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+            done = false;                       // fixed and filtered by the serial sweep
+          } else {
+            v = negfix_sum(g, sv, fx, j, i, k, false);
+            F3(fx, j, i, k) = v;
+          }
+        }
+        if (done) raw_filter(c, n, v, a1, a2, q ? pa.y : pa.x, q ? pb.y : pb.x, r1, r2);
       }
-      v = negfix_sum(g, sv, fx, j, i, k, false);
-      ST(fx, o3, v);
+      if (q) { n1.y = r1; n2.y = r2; } else { n1.x = r1; n2.x = r2; }
     }
-    double n1, n2;
-    raw_filter(c, n, v, LD(n ? f.a1qc : f.a1qv, o3), LD(n ? f.a2qc : f.a2qv, o3), pa, pb, n1, n2);
-    ST(n ? f.b1qc : f.b1qv, o3, n1);
-    ST(n ? f.b2qc : f.b2qv, o3, n2);
+    ST2(n ? f.b1qc : f.b1qv, o3, n1);
+    ST2(n ? f.b2qc : f.b2qv, o3, n2);
   }
 }
 
@@ -860,7 +883,7 @@ __device__ void negfix_serial_plane(const Geom& g, const Consts* c, const QFix& 
 // reference's order.  Blocks [nproj, nproj + 2 kz) run the serial negative-moisture sweeps
 // (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
-__global__ __launch_bounds__(256) void k_split_project(
+__global__ __launch_bounds__(512) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
@@ -887,7 +910,7 @@ __global__ __launch_bounds__(256) void k_split_project(
   }
   if (ce) {
     const double m00 = F2(msfd, j, i), m10 = F2(msfd, j + 1, i), m01 = F2(msfd, j, i + 1), m11 = F2(msfd, j + 1, i + 1);
-    for (int k = ty + 1; k <= kz; k += 4) {
+    for (int k = ty + 1; k <= kz; k += 8) {
 #define DIV(U, V) (-(F3(U, j, i + 1, k) * m01) + (F3(U, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) + \
                    (F3(U, j + 1, i, k) * m10) + (F3(V, j, i + 1, k) * m01) + (F3(V, j + 1, i + 1, k) * m11) - \
                    (F3(V, j, i, k) * m00) - (F3(V, j + 1, i, k) * m10))
@@ -903,7 +926,7 @@ __global__ __launch_bounds__(256) void k_split_project(
   const long q = g.ix(j, i);
   const double rdx2 = d_one / c->dx2;
   const int ns = c->nsplit;
-  for (int w = ty; w < 2 * ns; w += 4) {
+  for (int w = ty; w < 2 * ns; w += 8) {
     const int l = w % ns + 1;
     if (w < ns) {
       const double ds = dstor[(long)(l - 1) * g.plane + q];
@@ -1021,7 +1044,7 @@ __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int
 // Per point the operations are those of k_spstep_grad/k_spstep_update, so results are
 // bit-identical to the two-kernel-per-substep path (Main/mod_split.F90:463-669).
 constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;
-__global__ __launch_bounds__(256) void k_spstep_fused(
+__global__ __launch_bounds__(512) void k_spstep_fused(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
     const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota,
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
@@ -1029,17 +1052,20 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
   const int l = blockIdx.z + 1;
   const int J1 = g.jce1 + blockIdx.x * SPB, I1 = g.ice1 + blockIdx.y * SPB;
   const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
-  const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 8
+  const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 16
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
   const int m2 = (int)aam * 2;
   const double dtau2 = dtau * d_two, rdx2 = d_one / c->dx2;
   const double* D1 = SLOT(deld, l, 1); const double* D2 = SLOT(deld, l, 2); const double* D3 = SLOT(deld, l, 3);
   const double* H1 = SLOT(delh, l, 1); const double* H2 = SLOT(delh, l, 2); const double* H3 = SLOT(delh, l, 3);
-  // per-thread points: (tx, ty + 8 r), r = 0..3
-  double d3[4], h3[4], ps[4], mf[4], ufac[4], msd[4], sd[4], sh[4];
-  bool ce[4], ci[4], bnd[4], di[4], own[4];
-  for (int r = 0; r < 4; r++) {
-    const int lj = tx, li = ty + 8 * r, j = jr0 + lj, i = ir0 + li;
+  // per-thread points: (tx, ty + 16 r), r = 0..1; d3/m2, h3/m2 (forward step) and d3/aam,
+  // h3/aam (leapfrog) are loop-invariant and formed once
+  constexpr int NR = 2;
+  double d3f[NR], h3f[NR], d3l[NR], h3l[NR], ps[NR], mf[NR], ufac[NR], msd[NR], sd[NR], sh[NR];
+  bool ce[NR], ci[NR], bnd[NR], di[NR], own[NR];
+  const double m2d = (double)m2;
+  for (int r = 0; r < NR; r++) {
+    const int lj = tx, li = ty + 16 * r, j = jr0 + lj, i = ir0 + li;
     ce[r] = in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
     ci[r] = in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
     di[r] = in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2);
@@ -1051,7 +1077,8 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
     Ds[0][li][lj] = ce[r] ? D1[q] : 0.0; Ds[1][li][lj] = ce[r] ? D2[q] : 0.0;
     Hs[0][li][lj] = ce[r] ? H1[q] : 0.0; Hs[1][li][lj] = ce[r] ? H2[q] : 0.0;
     U[li][lj] = 0.0; V[li][lj] = 0.0;
-    d3[r] = ce[r] ? D3[q] : 0.0; h3[r] = ce[r] ? H3[q] : 0.0;
+    const double d3 = ce[r] ? D3[q] : 0.0, h3 = ce[r] ? H3[q] : 0.0;
+    d3f[r] = d3 / m2d; h3f[r] = h3 / m2d; d3l[r] = d3 / aam; h3l[r] = h3 / aam;
     ps[r] = ci[r] ? F2(psa, j, i) : 1.0;
     mf[r] = ci[r] ? F2(mapf, j, i) : 0.0;
     ufac[r] = di[r] ? c->dx2 * F2(msfx, j, i) : 1.0;
@@ -1059,9 +1086,9 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
     sd[r] = ce[r] ? Ds[0][li][lj] : 0.0;     // ddsum(ce) = deld(n0)
     sh[r] = ce[r] ? Hs[0][li][lj] : 0.0;
   }
-  double pda[4];
-  for (int r = 0; r < 4; r++) {
-    const int j = jr0 + tx, i = ir0 + ty + 8 * r;
+  double pda[NR];
+  for (int r = 0; r < NR; r++) {
+    const int j = jr0 + tx, i = ir0 + ty + 16 * r;
     pda[r] = di[r] ? F2(psdota, j, i) : 0.0;
   }
   __syncthreads();
@@ -1069,8 +1096,8 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
   for (int n = 1; n <= m2; n++) {
     const int src = (n == 1) ? n0 : n1;
     // gradient of delh(src) at dot points -> (uu, vv)
-    for (int r = 0; r < 4; r++) {
-      const int lj = tx, li = ty + 8 * r;
+    for (int r = 0; r < NR; r++) {
+      const int lj = tx, li = ty + 16 * r;
       if (di[r] && lj >= 1 && li >= 1) {
         const double a = Hs[src][li][lj], b = Hs[src][li - 1][lj], cc = Hs[src][li][lj - 1], dd = Hs[src][li - 1][lj - 1];
         double w1 = (a + b - cc - dd) / ufac[r];
@@ -1083,21 +1110,20 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
     }
     __syncthreads();
     const int nn = (n == 1) ? n1 : n0;                  // forward writes n1; leapfrog n2 = n0
-    for (int r = 0; r < 4; r++) {
-      const int lj = tx, li = ty + 8 * r;
+    for (int r = 0; r < NR; r++) {
+      const int lj = tx, li = ty + 16 * r;
       if (ci[r] && lj + 1 < SPR && li + 1 < SPR) {
         const double w3 = rdx2 * mf[r] *
             (-U[li + 1][lj] + U[li + 1][lj + 1] - U[li][lj] + U[li][lj + 1] +
              V[li + 1][lj] + V[li + 1][lj + 1] - V[li][lj] - V[li][lj + 1]);
         if (n == 1) {
-          const double m2d = (double)m2;
-          const double dn = Ds[n0][li][lj] - dtau * w3 + d3[r] / m2d;
-          const double hn = Hs[n0][li][lj] - dtau * hbar * Ds[n0][li][lj] / ps[r] + h3[r] / m2d;
+          const double dn = Ds[n0][li][lj] - dtau * w3 + d3f[r];
+          const double hn = Hs[n0][li][lj] - dtau * hbar * Ds[n0][li][lj] / ps[r] + h3f[r];
           Ds[nn][li][lj] = dn;
           Hs[nn][li][lj] = hn;
         } else {
-          const double dn = Ds[n0][li][lj] - dtau2 * w3 + d3[r] / aam;
-          const double hn = Hs[n0][li][lj] - dtau2 * hbar * Ds[n1][li][lj] / ps[r] + h3[r] / aam;
+          const double dn = Ds[n0][li][lj] - dtau2 * w3 + d3l[r];
+          const double hn = Hs[n0][li][lj] - dtau2 * hbar * Ds[n1][li][lj] / ps[r] + h3l[r];
           Ds[nn][li][lj] = dn;
           Hs[nn][li][lj] = hn;
         }
@@ -1114,8 +1140,8 @@ __global__ __launch_bounds__(256) void k_spstep_fused(
     if (n >= 2) { const int t0 = n0; n0 = n1; n1 = t0; }
     else { /* forward step: n0 = 1, n1 = 2 stay; the leapfrog loop starts with n2 = n0 */ }
   }
-  for (int r = 0; r < 4; r++) {
-    const int j = jr0 + tx, i = ir0 + ty + 8 * r;
+  for (int r = 0; r < NR; r++) {
+    const int j = jr0 + tx, i = ir0 + ty + 16 * r;
     if (own[r] && in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2)) {
       const long q = (long)(l - 1) * g.plane + g.ix(j, i);
       ddsum[q] = ce[r] ? sd[r] : d_zero;
@@ -1153,40 +1179,60 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
       if (s->lcount == 2) s->dt = d_two * c->dtsec;
     }
   }
-  if (j > g.jde2 || i > g.ide2) return;
-  const long q = g.ix(j, i);
-  const long p = (long)(k - 1) * g.plane + q;
+  // two adjacent points (jp, jp+1) per thread, 16-byte accesses (jp - j0 is even)
+  const int jp = g.jde1 + 2 * (j - g.jde1);
+  if (jp > g.jde2 || i > g.ide2) return;
+  const uint32_t o2 = g.o2(jp, i), o3 = o2 + (uint32_t)(k - 1) * g.L8;
   const double gnu1 = c->gnu1;
   const int ns = c->nsplit;
-  if (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2)) {
+  const bool ici = in(i, g.ici1, g.ici2), idi = in(i, g.idi1, g.idi2);
+  const bool ci0 = ici && in(jp, g.jci1, g.jci2), ci1 = ici && in(jp + 1, g.jci1, g.jci2);
+  const bool di0 = idi && in(jp, g.jdi1, g.jdi2), di1 = idi && in(jp + 1, g.jdi1, g.jdi2);
+  if (ci0 || ci1) {
+    double dd[2][MAXSPLIT];
+    for (int l = 1; l <= ns; l++) {
+      const double2 d = LD2(ddsum, o2 + (uint32_t)(l - 1) * g.L8);
+      dd[0][l - 1] = d.x; dd[1][l - 1] = d.y;
+    }
     if (k == 1) {
-      double pa = psa[q], pb = psb[q];
+      double2 pa = LD2(psa, o2), pb = LD2(psb, o2);
       for (int l = 1; l <= ns; l++) {
-        const double an = c->an[l - 1], dd = ddsum[(long)(l - 1) * g.plane + q];
-        pa = pa - an * dd;
-        pb = pb - gnu1 * an * dd;
+        const double an = c->an[l - 1];
+        if (ci0) { pa.x = pa.x - an * dd[0][l - 1]; pb.x = pb.x - gnu1 * an * dd[0][l - 1]; }
+        if (ci1) { pa.y = pa.y - an * dd[1][l - 1]; pb.y = pb.y - gnu1 * an * dd[1][l - 1]; }
       }
-      psa[q] = pa; psb[q] = pb;
+      ST2(psa, o2, pa); ST2(psb, o2, pb);
     }
-    double t1 = a1t[p], t2 = a2t[p];
+    double2 t1 = LD2(a1t, o3), t2 = LD2(a2t, o3);
     for (int l = 1; l <= ns; l++) {
-      const double am = c->am[l - 1][k - 1], dd = ddsum[(long)(l - 1) * g.plane + q];
-      t1 = t1 + am * dd;
-      t2 = t2 + gnu1 * am * dd;
+      const double am = c->am[l - 1][k - 1];
+      if (ci0) { t1.x = t1.x + am * dd[0][l - 1]; t2.x = t2.x + gnu1 * am * dd[0][l - 1]; }
+      if (ci1) { t1.y = t1.y + am * dd[1][l - 1]; t2.y = t2.y + gnu1 * am * dd[1][l - 1]; }
     }
-    a1t[p] = t1; a2t[p] = t2;
+    ST2(a1t, o3, t1); ST2(a2t, o3, t2);
   }
-  if (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2)) {
-    double u1 = a1u[p], v1 = a1v[p], u2 = a2u[p], v2 = a2v[p];
-    const double fac = F2(psdota, j, i) / (c->dx2 * F2(msfd, j, i));
+  if (di0 || di1) {
+    double2 u1 = LD2(a1u, o3), v1 = LD2(a1v, o3), u2 = LD2(a2u, o3), v2 = LD2(a2v, o3);
+    const double2 pd = LD2(psdota, o2), md = LD2(msfd, o2);
+    const double fac0 = pd.x / (c->dx2 * md.x), fac1 = pd.y / (c->dx2 * md.y);
     for (int l = 1; l <= ns; l++) {
-      const double* dh = dhsum + (long)(l - 1) * g.plane;
+      const uint32_t lo = o2 + (uint32_t)(l - 1) * g.L8;
+      // dhsum at (jp-1..jp+1, i-1..i)
+      const double2 h0 = LD2(dhsum, lo), hs = LD2(dhsum, lo - g.P8);
+      const double hw = LD(dhsum, lo - 8u), hsw = LD(dhsum, lo - g.P8 - 8u);
       const double zm = c->zmatx[l - 1][k - 1], gnuzm = gnu1 * zm;
-      const double x = fac * (F2(dh, j, i) + F2(dh, j, i - 1) - F2(dh, j - 1, i) - F2(dh, j - 1, i - 1));
-      const double y = fac * (F2(dh, j, i) - F2(dh, j, i - 1) + F2(dh, j - 1, i) - F2(dh, j - 1, i - 1));
-      u1 = u1 - zm * x; v1 = v1 - zm * y; u2 = u2 - gnuzm * x; v2 = v2 - gnuzm * y;
+      if (di0) {
+        const double x = fac0 * (h0.x + hs.x - hw - hsw);
+        const double y = fac0 * (h0.x - hs.x + hw - hsw);
+        u1.x = u1.x - zm * x; v1.x = v1.x - zm * y; u2.x = u2.x - gnuzm * x; v2.x = v2.x - gnuzm * y;
+      }
+      if (di1) {
+        const double x = fac1 * (h0.y + hs.y - h0.x - hs.x);
+        const double y = fac1 * (h0.y - hs.y + h0.x - hs.x);
+        u1.y = u1.y - zm * x; v1.y = v1.y - zm * y; u2.y = u2.y - gnuzm * x; v2.y = v2.y - gnuzm * y;
+      }
     }
-    a1u[p] = u1; a1v[p] = v1; a2u[p] = u2; a2v[p] = v2;
+    ST2(a1u, o3, u1); ST2(a1v, o3, v1); ST2(a2u, o3, u2); ST2(a2v, o3, v2);
   }
 }
 #undef SLOT
