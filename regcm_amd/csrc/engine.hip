@@ -68,6 +68,7 @@ Geom make_geom(int jx, int iy, int cj, int ci, int tile) {
   tile_extent(jx, iy, cj, ci, tile, ext, bdy);
   Geom g{};
   g.bl = bdy[0]; g.br = bdy[1]; g.bb = bdy[2]; g.bt = bdy[3];
+  g.gjx = jx; g.giy = iy;
   g.jde1 = g.jdi1 = g.jdii1 = ext[0]; g.jde2 = g.jdi2 = g.jdii2 = ext[1];
   g.ide1 = g.idi1 = g.idii1 = ext[2]; g.ide2 = g.idi2 = g.idii2 = ext[3];
   if (g.bl) { g.jdi1 = g.jde1 + 1; g.jdii1 = g.jde1 + 2; }
@@ -529,7 +530,7 @@ struct rcmdyn_engine {
     int o = idx - cfg.tile_first;
     return (o >= 0 && o < (int)tiles.size()) ? &tiles[o] : nullptr;
   }
-  struct XField { FK f; int nk; };
+  struct XField { FK f; int nk; int width = 0; int sides = -1; };  // 0/-1: the call's default
   // (j1,j2,i1,i2) of the box sent toward d (send) or received from d (recv)
   static void box(const Geom& g, int d, int w, bool send, int b[4]) {
     b[0] = g.jde1; b[1] = g.jde2; b[2] = g.ide1; b[3] = g.ide2;
@@ -623,15 +624,22 @@ struct rcmdyn_engine {
   }
 
   // exchange / exchange_lb / exchange_rt of several fields at once
-  void xch(std::initializer_list<XField> fields, int width, int sides) {
+  // One exchange point: every field travels in the same per-neighbour message, each with its
+  // own width and sides (0 exchange, 1 exchange_lb, 2 exchange_rt).
+  void xch(std::initializer_list<XField> fields, int width = 1, int sides = 0) {
     if (ntiles == 1) return;
     std::vector<XField> fs(fields);
+    for (XField& x : fs) {
+      if (x.width == 0) x.width = width;
+      if (x.sides < 0) x.sides = sides;
+    }
     auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
-      for (const XField& x : fs) v.push_back(field_seg(t, fptr(t, x.f), x.nk, d, width, send));
+      for (const XField& x : fs)
+        if (recv_dir(x.sides, send ? OPP[d] : d)) v.push_back(field_seg(t, fptr(t, x.f), x.nk, d, x.width, send));
     };
-    exchange_generic(fn, [&](int d) { return recv_dir(sides, OPP[d]); }, [&](int d) { return recv_dir(sides, d); });
+    auto all = [](int) { return true; };
+    exchange_generic(fn, all, all);
   }
-  void xch(FK f, int nk, int width, int sides) { xch({XField{f, nk}}, width, sides); }
 
   // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
   void xch_delh_slot(int l, int src) {
@@ -730,18 +738,17 @@ struct rcmdyn_engine {
 
   void tend() {
     const int kz = cfg.kz, ns = cfg.nsplit;
-    // surface_pressures + 2-D reciprocals, Main/mod_tendency.F90:815-834
-    xch(FK::PSA, 1, 1, 0);
-    xch(FK::PSB, 1, 2, 0);
+    // One exchange point for the whole prologue (Main/mod_tendency.F90:815-1116,
+    // Main/mod_slice.F90:102-300): the decoupled fields are recomputed where read, so their
+    // exchanges become exchanges of atm1 (width 1) and atm2 (idif = 2); p* travels 3 wide so
+    // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
+    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz},
+         {FK::A1QC, kz}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, 2},
+         {FK::A2QC, kz, 2}});
+    // surface_pressures + 2-D reciprocals, :815-834
     each([&](Tile& t) {
       KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
     });
-    xch({{FK::PSDOTA, 1}, {FK::RPSDA, 1}}, 1, 0);
-    xch({{FK::PSDOTB, 1}, {FK::RPSDB, 1}}, 2, 0);
-    // decouple / mkslice inputs (:852-1116, Main/mod_slice.F90:102-300): the decoupled
-    // fields are recomputed where read, so their exchanges become exchanges of atm1/atm2
-    xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz}, {FK::A1QC, kz}}, 1, 0);
-    xch({{FK::A2U, kz}, {FK::A2V, kz}, {FK::A2T, kz}, {FK::A2QV, kz}, {FK::A2QC, kz}}, 2, 0);
     // compute_omega columns, new_pressure, geopotential (calc_coeff is formed where it is
     // read, in k_momentum and k_scalars)
     each([&](Tile& t) {
@@ -749,8 +756,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t),
               (g.jde2 - g.jde1 + 64) / 64);
     });
-    xch(FK::QDOT, kz + 1, 1, 0);
-    xch(FK::PHI, kz, 1, 1);
+    xch({{FK::QDOT, kz + 1}, {FK::PHI, kz, 1, 1}});
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -760,15 +766,14 @@ struct rcmdyn_engine {
       KLAUNCH(k_scalars, dim3((g.jce2 - g.jce1 + SBJ) / SBJ, (g.ice2 - g.ice1 + SBI) / SBI, kz), dim3(SBT), 0,
               stream, g, dc, ds, f);
     });
-    xch({{FK::CQV, kz}, {FK::CQC, kz}}, 1, 0);
+    xch({{FK::CQV, kz}, {FK::CQC, kz}});
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     each([&](Tile& t) {
       KLAUNCH(k_qfilter, grid3((t.g.nj + 1) / 2, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
       t.cur = 1 - t.cur;
     });
     // splitf, Main/mod_split.F90:243-461
-    xch(FK::PSA, 1, 1, 0);
-    xch({{FK::A1U, kz}, {FK::A1V, kz}, {FK::A2U, kz}, {FK::A2V, kz}}, 1, 2);
+    xch({{FK::PSA, 1}, {FK::A1U, kz, 1, 2}, {FK::A1V, kz, 1, 2}, {FK::A2U, kz, 1, 2}, {FK::A2V, kz, 1, 2}});
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
@@ -805,7 +810,7 @@ struct rcmdyn_engine {
         n0 = n1; n1 = n2; n2 = n0;
       }
     }
-    xch(FK::DHSUM, ns, 1, 1);
+    xch({{FK::DHSUM, ns}}, 1, 1);
     // corrections + rcmtimer advance (last tile's launch)
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];

@@ -16,7 +16,8 @@
 
 namespace rcm {
 
-constexpr int G = 2;               // ghost width (idif = 2 for idiffu = 1)
+constexpr int G = 4;               // ghost ring of the frame: idif = 2 for idiffu = 1, plus
+                                   // room for the width-3 p* exchange (even: 16-B pairs)
 constexpr int MAXKZ = RCMDYN_MAXKZ;
 constexpr int MAXSPLIT = RCMDYN_MAXSPLIT;
 constexpr int MAXNSP = 256;        // max boundary-band width (nspgx)
@@ -29,6 +30,7 @@ struct Geom {
   int jci1ga, jci2ga, ici1ga, ici2ga;
   int jde1gb, jde2gb, ide1gb, ide2gb, jce1gb, jce2gb, ice1gb, ice2gb;
   int bl, br, bb, bt;              // has_bdyleft/right/bottom/top
+  int gjx, giy;                    // global dot-grid extents
   int j0, i0;                      // global index of frame origin
   int nj, ni;                      // frame size (nj <= pitch)
   int pitch;

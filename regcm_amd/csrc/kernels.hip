@@ -69,16 +69,38 @@ __device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int 
 }
 
 // ---------------------------------------------------------------------------------------
+// psc2psd at any dot point from the global domain extents (tile ghosts included),
+// Main/mpplib/mod_mppparam.F90:13811-13862: 4-point mean inside, 2-point means on the domain
+// edges, corner copies.  Equal to psc2psd_at on every owned point.
+__device__ __forceinline__ double psc2psd_global(const Geom& g, const double* pc, int j, int i) {
+  const int jx = g.gjx, iy = g.giy;
+  const bool jin = j >= 2 && j <= jx - 1, iin = i >= 2 && i <= iy - 1;
+  if (jin && iin) return (F2(pc, j, i) + F2(pc, j, i - 1) + F2(pc, j - 1, i) + F2(pc, j - 1, i - 1)) * d_rfour;
+  if (jin && i == iy) return (F2(pc, j, iy - 1) + F2(pc, j - 1, iy - 1)) * d_half;
+  if (jin && i == 1) return (F2(pc, j, 1) + F2(pc, j - 1, 1)) * d_half;
+  if (iin && j == 1) return (F2(pc, 1, i) + F2(pc, 1, i - 1)) * d_half;
+  if (iin && j == jx) return (F2(pc, jx - 1, i) + F2(pc, jx - 1, i - 1)) * d_half;
+  return F2(pc, (j == 1) ? 1 : jx - 1, (i == 1) ? 1 : iy - 1);
+}
+
 // K1. surface_pressures, Main/mod_tendency.F90:815-834, and the 2-D reciprocals of decouple
-// (rpsda, :868-875) and mkslice (1/psdotb, 1/psb, Main/mod_slice.F90:163-183).
+// (rpsda, :868-875) and mkslice (1/psdotb, 1/psb, Main/mod_slice.F90:163-183), on the owned
+// points and the ghost ring the consumers read (ga for atm1-derived, gb for atm2-derived).
 __global__ void k_surface_pressures(Geom g, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
   if (in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
   if (in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
-  double v;
-  if (psc2psd_at(g, f.psa, j, i, v)) { F2(f.psdota, j, i) = v; F2(f.rpsda, j, i) = d_one / v; }
-  if (psc2psd_at(g, f.psb, j, i, v)) { F2(f.psdotb, j, i) = v; F2(f.rpsdb, j, i) = d_one / v; }
+  if (in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
+    const double v = psc2psd_global(g, f.psa, j, i);
+    F2(f.psdota, j, i) = v;
+    F2(f.rpsda, j, i) = d_one / v;
+  }
+  if (in(j, g.jde1gb, g.jde2gb) && in(i, g.ide1gb, g.ide2gb)) {
+    const double v = psc2psd_global(g, f.psb, j, i);
+    F2(f.psdotb, j, i) = v;
+    F2(f.rpsdb, j, i) = d_one / v;
+  }
 }
 
 // generic relaxation contribution (nudge*, Main/mod_bdycod.F90:4262-4263)
