@@ -63,7 +63,7 @@ void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4
   bdy[0] = (lj == 0); bdy[1] = (lj == cj - 1); bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
 }
 
-Geom make_geom(int jx, int iy, int cj, int ci, int tile) {
+Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G) {
   int ext[8], bdy[4];
   tile_extent(jx, iy, cj, ci, tile, ext, bdy);
   Geom g{};
@@ -87,9 +87,9 @@ Geom make_geom(int jx, int iy, int cj, int ci, int tile) {
   g.jci1ga = g.jci1 - gl; g.jci2ga = g.jci2 + gr; g.ici1ga = g.ici1 - gb; g.ici2ga = g.ici2 + gt;
   g.jde1gb = g.jde1 - 2 * gl; g.jde2gb = g.jde2 + 2 * gr; g.ide1gb = g.ide1 - 2 * gb; g.ide2gb = g.ide2 + 2 * gt;
   g.jce1gb = g.jce1 - 2 * gl; g.jce2gb = g.jce2 + 2 * gr; g.ice1gb = g.ice1 - 2 * gb; g.ice2gb = g.ice2 + 2 * gt;
-  g.j0 = g.jde1 - G; g.i0 = g.ide1 - G;
-  g.nj = (g.jde2 - g.jde1 + 1) + 2 * G;
-  g.ni = (g.ide2 - g.ide1 + 1) + 2 * G;
+  g.j0 = g.jde1 - gh; g.i0 = g.ide1 - gh;
+  g.nj = (g.jde2 - g.jde1 + 1) + 2 * gh;
+  g.ni = (g.ide2 - g.ide1 + 1) + 2 * gh;
   g.pitch = (g.nj + 15) / 16 * 16;
   g.plane = (long)g.pitch * g.ni;
   g.P8 = (uint32_t)g.pitch * 8u;
@@ -330,6 +330,13 @@ struct rcmdyn_engine {
     t.uu = dalloc(t, P); t.vv = dalloc(t, P);
     t.tten = dalloc(t, P3); t.uten = dalloc(t, P3); t.vten = dalloc(t, P3);
     t.qvten = dalloc(t, P3); t.qcten = dalloc(t, P3); t.omega = dalloc(t, P3); t.xkcs = dalloc(t, P3);
+    if (ntiles > 1) {                       // wide frame of the fused split step
+      t.gw = make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, index, SPH + G);
+      const size_t PW = t.gw.plane;
+      t.wdeld = dalloc(t, PW * 3 * ns); t.wdelh = dalloc(t, PW * 3 * ns);
+      t.wpsa = dalloc(t, PW); t.wpsdota = dalloc(t, PW);
+      t.wmsfx = dalloc(t, PW); t.wmsfd = dalloc(t, PW); t.wmapf = dalloc(t, PW);
+    }
     slen = std::max<long>(g.pitch, g.ni);
     for (int s = 0; s < 16; s++) t.sl[s] = dalloc(t, (size_t)slen * kz);
     // halo staging: 8 directions x widest exchange (6 fields x width 2 x (kz+1) levels)
@@ -651,6 +658,36 @@ struct rcmdyn_engine {
     exchange_generic(fn, [&](int d) { return recv_dir(1, OPP[d]); }, [&](int d) { return recv_dir(1, d); });
   }
 
+  // width-w exchange of 2-D planes held in the tiles' wide frames (fused split step)
+  void xch_wide(std::initializer_list<std::pair<double* Tile::*, int>> fields, int w) {
+    if (ntiles == 1) return;
+    std::vector<std::pair<double* Tile::*, int>> fs(fields);
+    auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
+      int b[4];
+      box(t.gw, d, w, send, b);
+      for (auto& x : fs) {
+        Seg sg{};
+        sg.p = t.*(x.first); sg.kstride = t.gw.plane; sg.pitch = t.gw.pitch; sg.j0 = t.gw.j0; sg.i0 = t.gw.i0;
+        sg.j1 = b[0]; sg.j2 = b[1]; sg.i1 = b[2]; sg.i2 = b[3]; sg.nk = x.second;
+        v.push_back(sg);
+      }
+    };
+    auto all = [](int) { return true; };
+    exchange_generic(fn, all, all);
+  }
+  // the fused split step is exact on a decomposition when every tile is at least SPH wide
+  // (its depth-SPH halo then comes from the direct neighbours only)
+  bool wide_ok() const {
+    if (ntiles == 1) return true;
+    for (const Geom& g : all)
+      if (g.jde2 - g.jde1 + 1 < SPH || g.ide2 - g.ide1 + 1 < SPH) return false;
+    return true;
+  }
+  void copy_wide(Tile& t, const double* src, double* dst, int nplanes) {
+    KLAUNCH(k_copy_frame, grid3(t.g.jde2 - t.g.jde1 + 1, t.g.ide2 - t.g.ide1 + 1, 1), BLK, 0, stream, t.g, t.gw,
+            nplanes, src, (long)t.g.plane, dst, (long)t.gw.plane);
+  }
+
   // exchange_bdy_lr / exchange_bdy_bt of the bdyuv slices (Main/mod_bdycod.F90:1063-1089):
   // south/north slices (by j) with the left/right tiles, west/east slices (by i) with the
   // bottom/top tiles; width 1, every level.
@@ -694,6 +731,14 @@ struct rcmdyn_engine {
         hipLaunchKernelGGL(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
                            t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
       });
+      if (ntiles > 1) {
+        each([&](Tile& t) {
+          copy_wide(t, t.msfx, t.wmsfx, 1);
+          copy_wide(t, t.msfd, t.wmsfd, 1);
+          copy_wide(t, t.mapf, t.wmapf, 1);
+        });
+        xch_wide({{&Tile::wmsfx, 1}, {&Tile::wmsfd, 1}, {&Tile::wmapf, 1}}, SPH);
+      }
       statics_dirty = false;
       invalidate_graphs();
     }
@@ -785,14 +830,28 @@ struct rcmdyn_engine {
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
-    bool fused = (ntiles == 1);
+    bool fused = wide_ok();
     for (int l = 1; l <= ns; l++) fused = fused && ((int)hc.aam[l - 1] * 2 <= SPH);
+    if (fused && ntiles > 1) {
+      // one depth-SPH exchange of every split-step input instead of three per sub-step
+      each([&](Tile& t) {
+        copy_wide(t, t.deld, t.wdeld, 3 * ns);
+        copy_wide(t, t.delh, t.wdelh, 3 * ns);
+        copy_wide(t, t.psa_[t.cur], t.wpsa, 1);
+        copy_wide(t, t.psdota, t.wpsdota, 1);
+      });
+      xch_wide({{&Tile::wdeld, 3 * ns}, {&Tile::wdelh, 3 * ns}, {&Tile::wpsa, 1}, {&Tile::wpsdota, 1}}, SPH);
+    }
     if (fused) {
       each([&](Tile& t) {
         const Geom& g = t.g;
         dim3 gr((g.jce2 - g.jce1 + SPB) / SPB, (g.ice2 - g.ice1 + SPB) / SPB, ns);
-        KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, dc, t.deld, t.delh, t.msfx, t.msfd,
-                           t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
+        if (ntiles > 1)
+          KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
+                  t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
+        else
+          KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, g, dc, t.deld, t.delh, t.msfx, t.msfd,
+                  t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
       });
     } else {
       each([&](Tile& t) {

@@ -103,6 +103,10 @@ struct Tile {
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // boundary slices (Main/mod_bdycod.F90:58-61): [k][frame index]
   double *sl[16];
+  // wide frame of the fused split step on a decomposed domain (2-D inputs, ghost depth SPH)
+  Geom gw{};
+  double *wdeld = nullptr, *wdelh = nullptr, *wpsa = nullptr, *wpsdota = nullptr;
+  double *wmsfx = nullptr, *wmsfd = nullptr, *wmapf = nullptr;
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials

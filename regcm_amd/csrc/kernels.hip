@@ -1066,8 +1066,12 @@ __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int
 // Per point the operations are those of k_spstep_grad/k_spstep_update, so results are
 // bit-identical to the two-kernel-per-substep path (Main/mod_split.F90:463-669).
 constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;
+// Inputs (deld/delh slots, msfx, msfd, psdota, mapf, psa) are addressed through frame w, which
+// for a tile of a decomposition is a wide frame whose ghost ring holds its neighbours' values
+// to depth SPH (one width-SPH exchange per step instead of three per sub-step); the masks use
+// global indices so ghost points evolve exactly as on their owning tile.  Outputs use frame g.
 __global__ __launch_bounds__(512) void k_spstep_fused(
-    Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
+    Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
     const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota,
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
   __shared__ double Ds[2][SPR][SPP], Hs[2][SPR][SPP], U[SPR][SPP], V[SPR][SPP];
@@ -1078,8 +1082,11 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
   const int m2 = (int)aam * 2;
   const double dtau2 = dtau * d_two, rdx2 = d_one / c->dx2;
-  const double* D1 = SLOT(deld, l, 1); const double* D2 = SLOT(deld, l, 2); const double* D3 = SLOT(deld, l, 3);
-  const double* H1 = SLOT(delh, l, 1); const double* H2 = SLOT(delh, l, 2); const double* H3 = SLOT(delh, l, 3);
+#define WSLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * w.plane)
+  const double* D1 = WSLOT(deld, l, 1); const double* D2 = WSLOT(deld, l, 2); const double* D3 = WSLOT(deld, l, 3);
+  const double* H1 = WSLOT(delh, l, 1); const double* H2 = WSLOT(delh, l, 2); const double* H3 = WSLOT(delh, l, 3);
+#undef WSLOT
+  const int gjx = g.gjx, giy = g.giy;
   // per-thread points: (tx, ty + 16 r), r = 0..1; d3/m2, h3/m2 (forward step) and d3/aam,
   // h3/aam (leapfrog) are loop-invariant and formed once
   constexpr int NR = 2;
@@ -1088,30 +1095,29 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   const double m2d = (double)m2;
   for (int r = 0; r < NR; r++) {
     const int lj = tx, li = ty + 16 * r, j = jr0 + lj, i = ir0 + li;
-    ce[r] = in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
-    ci[r] = in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
-    di[r] = in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2);
+    ce[r] = in(j, 1, gjx - 1) && in(i, 1, giy - 1);
+    ci[r] = in(j, 2, gjx - 2) && in(i, 2, giy - 2);
+    di[r] = in(j, 2, gjx - 1) && in(i, 2, giy - 1);
     bnd[r] = ce[r] && !ci[r] &&
-             ((g.bl && j == g.jce1 && in(i, g.ici1, g.ici2)) || (g.br && j == g.jce2 && in(i, g.ici1, g.ici2)) ||
-              (g.bb && i == g.ice1) || (g.bt && i == g.ice2));
+             (((j == 1 || j == gjx - 1) && in(i, 2, giy - 2)) || i == 1 || i == giy - 1);
     own[r] = in(j, J1, J1 + SPB - 1) && in(i, I1, I1 + SPB - 1);
-    const long q = ce[r] ? g.ix(j, i) : 0;
+    const long q = ce[r] ? w.ix(j, i) : 0;
     Ds[0][li][lj] = ce[r] ? D1[q] : 0.0; Ds[1][li][lj] = ce[r] ? D2[q] : 0.0;
     Hs[0][li][lj] = ce[r] ? H1[q] : 0.0; Hs[1][li][lj] = ce[r] ? H2[q] : 0.0;
     U[li][lj] = 0.0; V[li][lj] = 0.0;
     const double d3 = ce[r] ? D3[q] : 0.0, h3 = ce[r] ? H3[q] : 0.0;
     d3f[r] = d3 / m2d; h3f[r] = h3 / m2d; d3l[r] = d3 / aam; h3l[r] = h3 / aam;
-    ps[r] = ci[r] ? F2(psa, j, i) : 1.0;
-    mf[r] = ci[r] ? F2(mapf, j, i) : 0.0;
-    ufac[r] = di[r] ? c->dx2 * F2(msfx, j, i) : 1.0;
-    msd[r] = di[r] ? F2(msfd, j, i) : 0.0;
+    ps[r] = ci[r] ? psa[w.ix(j, i)] : 1.0;
+    mf[r] = ci[r] ? mapf[w.ix(j, i)] : 0.0;
+    ufac[r] = di[r] ? c->dx2 * msfx[w.ix(j, i)] : 1.0;
+    msd[r] = di[r] ? msfd[w.ix(j, i)] : 0.0;
     sd[r] = ce[r] ? Ds[0][li][lj] : 0.0;     // ddsum(ce) = deld(n0)
     sh[r] = ce[r] ? Hs[0][li][lj] : 0.0;
   }
   double pda[NR];
   for (int r = 0; r < NR; r++) {
     const int j = jr0 + tx, i = ir0 + ty + 16 * r;
-    pda[r] = di[r] ? F2(psdota, j, i) : 0.0;
+    pda[r] = di[r] ? psdota[w.ix(j, i)] : 0.0;
   }
   __syncthreads();
   int n0 = 0, n1 = 1;                                   // slot indices (reference slots 1, 2)
@@ -1442,6 +1448,15 @@ __global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack) {
     if (unpack) *a = buf[sg.off + q];
     else buf[sg.off + q] = *a;
   }
+}
+
+// Copy the owned points (jde x ide) of nplanes 2-D planes from frame g into frame w (the wide
+// frame of the fused split step); plane strides sstride / dstride.
+__global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restrict__ src, long sstride, double* dst,
+                             long dstride) {
+  THREAD_POINT(g.jde1, g.ide1);
+  if (j > g.jde2 || i > g.ide2) return;
+  for (int p = 0; p < nplanes; p++) dst[p * dstride + w.ix(j, i)] = src[p * sstride + g.ix(j, i)];
 }
 
 }  // namespace rcm
