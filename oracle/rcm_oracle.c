@@ -74,6 +74,7 @@ struct orc {
   double xds[RCMDYN_MAXKZ + 1], dds[RCMDYN_MAXKZ + 2];
   double hefc[256][RCMDYN_MAXKZ + 1], hegc[256][RCMDYN_MAXKZ + 1]; /* (n,k), n=2..nspgx-1 */
   double fcx[256], gcx[256];
+  double wgtx[256], wgtd[256];              /* sponge weights (iboudy = 4), :238-250 */
   double pdlog[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ + 2], eps1[RCMDYN_MAXSPLIT][RCMDYN_MAXKZ + 2];
   /* boundary masks: 0 none, 1 S, 2 N, 3 W, 4 E; ibnd */
   signed char *rg_cr, *rg_dt;
@@ -271,6 +272,13 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
       double xfun = exp(-((double)(n - 2) / an));
       o->hefc[n][k] = o->fnudge * xfun; o->hegc[n][k] = o->gnudge * xfun;
     }
+  }
+  /* sponge weights, Main/mod_bdycod.F90:237-250 (iboudy = 4) */
+  if (cfg->iboudy == 4) {
+    o->wgtd[2] = 0.20; o->wgtd[3] = 0.55; o->wgtd[4] = 0.80; o->wgtd[5] = 0.95;
+    for (int n = 6; n <= cfg->nspgd - 1 && n < 256; n++) o->wgtd[n] = d_one;
+    o->wgtx[2] = 0.4; o->wgtx[3] = 0.7; o->wgtx[4] = 0.9;
+    for (int n = 5; n <= cfg->nspgx - 1 && n < 256; n++) o->wgtx[n] = 1.0;
   }
   /* splitf scalar geopotential terms, Main/mod_split.F90:343-353 */
   for (int l = 1; l <= o->nsplit; l++)
@@ -674,9 +682,20 @@ static void nudge_coef(orc_t* o, int ib, int k, double* xf, double* xg) {
   else { *xf = o->hefc[ib][k]; *xg = o->hegc[ib][k]; }
 }
 
-/* new_pressure, Main/mod_tendency.F90:1428-1460 (+ nudge2d :4597-4766) */
+/* new_pressure, Main/mod_tendency.F90:1428-1460 (+ nudge2d :4597-4766, or sponge2d
+ * Main/mod_bdycod.F90:3065-3122 for iboudy = 4) */
 static void new_pressure(orc_t* o) {
   double xt = o->xbctime + o->dt;
+  if (o->cfg.iboudy == 4) {
+    for (int r = 1; r <= 4; r++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          int ib = A2(o->ib_cr, j, i);
+          A2(o->pten, j, i) = o->wgtx[ib] * A2(o->pten, j, i) + (d_one - o->wgtx[ib]) * A2(o->pbt, j, i);
+        }
+    goto forecast;
+  }
   for (int i = o->ice1ga; i <= o->ice2ga; i++)
     for (int j = o->jce1ga; j <= o->jce2ga; j++)
       A3(o->fg1, j, i, 1) = (A2(o->pb0, j, i) + xt * A2(o->pbt, j, i)) - A2(o->psb, j, i);
@@ -689,6 +708,7 @@ static void new_pressure(orc_t* o) {
         A2(o->pten, j, i) = relax(A2(o->pten, j, i), xf, xg, A3(o->fg1, j, i, 1), A3(o->fg1, j - 1, i, 1),
                                   A3(o->fg1, j + 1, i, 1), A3(o->fg1, j, i - 1, 1), A3(o->fg1, j, i + 1, 1));
       }
+forecast:
   for (int i = o->ice1; i <= o->ice2; i++)
     for (int j = o->jce1; j <= o->jce2; j++) {
       A2(o->psc, j, i) = A2(o->psb, j, i) + A2(o->pten, j, i) * o->dt;
@@ -936,9 +956,42 @@ static void adiabatic(orc_t* o) {
 }
 
 /* boundary, Main/mod_tendency.F90:1462-1471 -> nudge3d/nudge4d3d/nudgeuv */
+/* sponge3d / sponge4d / spongeuv, Main/mod_bdycod.F90:2591-2994 (iboudy = 4): applied to the
+ * total tendencies (pc_total), which are still zero when boundary runs (init_tendencies);
+ * the dynamic terms are added to them afterwards (:285-294). */
+static void sponge_all(orc_t* o) {
+  int kz = o->kz;
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          int ib = A2(o->ib_cr, j, i);
+          A3(o->tten, j, i, k) = o->wgtx[ib] * A3(o->tten, j, i, k) + (d_one - o->wgtx[ib]) * A3(o->tbt, j, i, k);
+        }
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          int ib = A2(o->ib_cr, j, i);
+          A3(o->qten[0], j, i, k) = o->wgtx[ib] * A3(o->qten[0], j, i, k) + (d_one - o->wgtx[ib]) * A3(o->qbt, j, i, k);
+        }
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          if (A2(o->rg_dt, j, i) != r) continue;
+          int ib = A2(o->ib_dt, j, i);
+          A3(o->uten, j, i, k) = o->wgtd[ib] * A3(o->uten, j, i, k) + (d_one - o->wgtd[ib]) * A3(o->ubt, j, i, k);
+          A3(o->vten, j, i, k) = o->wgtd[ib] * A3(o->vten, j, i, k) + (d_one - o->wgtd[ib]) * A3(o->vbt, j, i, k);
+        }
+}
+
 static void boundary(orc_t* o) {
   int kz = o->kz;
   double xt = o->xbctime + o->dt;
+  if (o->cfg.iboudy == 4) { sponge_all(o); return; }
   /* nudge3d(atm2%t, xtb, tdyn), Main/mod_bdycod.F90:4218-4406 */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ice1ga; i <= o->ice2ga; i++)
@@ -1542,6 +1595,31 @@ void orc_bdyval(orc_t* o) {
   if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice1);
   if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice2);
 #undef TQB
+  /* qv inflow/outflow for iboudy = 3 or 4, :1809-1950: west/east on ici, then south/north on
+   * jce (they read the west/east results at the corners) */
+  if (o->cfg.iboudy == 4) {
+    double* q = o->a1q[0];
+    if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) {
+      double qext = A3(q, o->jce1, i, k) / A2(o->psa, o->jce1, i);
+      double qint = A3(q, o->jci1, i, k) / A2(o->psa, o->jci1, i);
+      double w = SI(o->wue, i, k) + SI(o->wue, i + 1, k) + SI(o->wui, i, k) + SI(o->wui, i + 1, k);
+      A3(q, o->jce1, i, k) = (w > d_zero) ? qext * A2(o->psa, o->jce1, i) : qint * A2(o->psa, o->jce1, i); }
+    if (o->br) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) {
+      double qext = A3(q, o->jce2, i, k) / A2(o->psa, o->jce2, i);
+      double qint = A3(q, o->jci2, i, k) / A2(o->psa, o->jci2, i);
+      double w = SI(o->eue, i, k) + SI(o->eue, i + 1, k) + SI(o->eui, i, k) + SI(o->eui, i + 1, k);
+      A3(q, o->jce2, i, k) = (w < d_zero) ? qext * A2(o->psa, o->jce2, i) : qint * A2(o->psa, o->jce2, i); }
+    if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) {
+      double qext = A3(q, j, o->ice1, k) / A2(o->psa, j, o->ice1);
+      double qint = A3(q, j, o->ici1, k) / A2(o->psa, j, o->ici1);
+      double w = SJ(o->sve, j, k) + SJ(o->sve, j + 1, k) + SJ(o->svi, j, k) + SJ(o->svi, j + 1, k);
+      A3(q, j, o->ice1, k) = (w > d_zero) ? qext * A2(o->psa, j, o->ice1) : qint * A2(o->psa, j, o->ice1); }
+    if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) {
+      double qext = A3(q, j, o->ice2, k) / A2(o->psa, j, o->ice2);
+      double qint = A3(q, j, o->ici2, k) / A2(o->psa, j, o->ici2);
+      double w = SJ(o->nve, j, k) + SJ(o->nve, j + 1, k) + SJ(o->nvi, j, k) + SJ(o->nvi, j + 1, k);
+      A3(q, j, o->ice2, k) = (w < d_zero) ? qext * A2(o->psa, j, o->ice2) : qint * A2(o->psa, j, o->ice2); }
+  }
   /* qc inflow/outflow (not present_qc, bdyflow), :2153-2220 */
   if (!o->cfg.present_qc) {
     double* q = o->a1q[1];

@@ -253,6 +253,12 @@ struct rcmdyn_engine {
       double xfun = (double)(cfg.nspgx - n) / (double)(cfg.nspgx - 2);
       c.fcx[n] = fnudge * xfun; c.gcx[n] = gnudge * xfun;
     }
+    if (cfg.iboudy == 4) {                                  // Main/mod_bdycod.F90:237-250
+      c.wgtd[2] = 0.20; c.wgtd[3] = 0.55; c.wgtd[4] = 0.80; c.wgtd[5] = 0.95;
+      for (int n = 6; n <= cfg.nspgd - 1 && n < MAXNSP; n++) c.wgtd[n] = 1.0;
+      c.wgtx[2] = 0.4; c.wgtx[3] = 0.7; c.wgtx[4] = 0.9;
+      for (int n = 5; n <= cfg.nspgx - 1 && n < MAXNSP; n++) c.wgtx[n] = 1.0;
+    }
     for (int k = 1; k <= kz; k++) {
       double an = (c.hsigma[k] < 0.4) ? cfg.high_nudge : (c.hsigma[k] < 0.8) ? cfg.medium_nudge : cfg.low_nudge;
       for (int n = 2; n <= cfg.nspgx - 1 && n < MAXNSP; n++) {
@@ -364,7 +370,8 @@ struct rcmdyn_engine {
     if (cfg.idynamic != 1) throw std::runtime_error("rcmdyn: only idynamic=1 (hydrostatic) is built");
     if (cfg.idiffu != 1) throw std::runtime_error("rcmdyn: only idiffu=1 is built");
     if (cfg.ipgf != 0) throw std::runtime_error("rcmdyn: only ipgf=0 is built");
-    if (cfg.iboudy != 5 && cfg.iboudy != 1) throw std::runtime_error("rcmdyn: iboudy must be 1 or 5");
+    if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
+      throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
     if (cfg.nsplit < 1 || cfg.nsplit > MAXSPLIT) throw std::runtime_error("rcmdyn: nsplit out of range");
     if (cfg.nspgx >= MAXNSP || cfg.nspgd != cfg.nspgx) throw std::runtime_error("rcmdyn: nspgx/nspgd unsupported");
@@ -918,8 +925,9 @@ struct rcmdyn_engine {
     xch_slices();
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
-      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, t.a1qc[t.cur], t.psa_[t.cur],
-              slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()));
+      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
+              t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], slices(t), slen, ds, cfg.dtsec,
+              (int)(q + 1 == tiles.size()));
     }
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }

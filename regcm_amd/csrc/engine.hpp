@@ -58,6 +58,7 @@ struct Consts {
   double twt1[MAXKZ + 1], twt2[MAXKZ + 1], qcon[MAXKZ + 1], xds[MAXKZ + 1];
   double hefc[MAXNSP][MAXKZ + 1], hegc[MAXNSP][MAXKZ + 1];
   double fcx[MAXNSP], gcx[MAXNSP];
+  double wgtx[MAXNSP], wgtd[MAXNSP];   // sponge weights (iboudy = 4)
   double zmatx[MAXSPLIT][MAXKZ], zmatxr[MAXSPLIT][MAXKZ], am[MAXSPLIT][MAXKZ];
   double tau[MAXSPLIT][MAXKZ];
   double an[MAXSPLIT], hbar[MAXSPLIT], aam[MAXSPLIT], dtau[MAXSPLIT];

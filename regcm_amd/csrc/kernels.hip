@@ -183,7 +183,11 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       // new_pressure
       const double dt = s->dt;
       const double psbv = LD(f.psb, o2);
-      if (ci && f.rgcr[o2 >> 3] > 0) {
+      if (ci && f.rgcr[o2 >> 3] > 0 && c->iboudy == 4) {
+        // sponge2d, Main/mod_bdycod.F90:3065-3122
+        const int ib = f.ibcr[o2 >> 3];
+        pt = c->wgtx[ib] * pt + (d_one - c->wgtx[ib]) * LD(f.pbt, o2);
+      } else if (ci && f.rgcr[o2 >> 3] > 0) {
         const double xt = s->xbctime + dt;
         double xf, xg;
         nudge_coef(c, f.ibcr[o2 >> 3], kz, xf, xg);
@@ -407,8 +411,14 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   // curvature (hydrostatic Coriolis)
   ut = ut + cor * v1c;
   vt = vt - cor * u1c;
-  // nudgeuv
-  if (rgd > 0) {
+  // nudgeuv (iboudy 1/5); the sponge of iboudy = 4 (spongeuv, Main/mod_bdycod.F90:2735-2813)
+  // acts on the still-zero total tendency, so it enters as the first summand below
+  double spu = d_zero, spv = d_zero;
+  if (rgd > 0 && c->iboudy == 4) {
+    const int ib = f.ibdt[o2 >> 3];
+    spu = c->wgtd[ib] * d_zero + (d_one - c->wgtd[ib]) * LD(f.ubt, o3);
+    spv = c->wgtd[ib] * d_zero + (d_one - c->wgtd[ib]) * LD(f.vbt, o3);
+  } else if (rgd > 0) {
     const double xt = s->xbctime + dt;
     double xf, xg;
     const int ib = f.ibdt[o2 >> 3];
@@ -459,8 +469,8 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
     vt = vt - pd * (f00 + fm0 - f0m - fmm) / den2;
   }
   // totals (uphy = 0), forecast, RA filter
-  ut = (d_zero + ut) + d_zero;
-  vt = (d_zero + vt) + d_zero;
+  ut = (spu + ut) + d_zero;
+  vt = (spv + vt) + d_zero;
   if (f.uten) { ST(f.uten, o3, ut); ST(f.vten, o3, vt); }
   const double g1 = c->gnu1;
   const double u2 = u2c, v2 = v2c;
@@ -672,8 +682,12 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
       const double rovcpm = c->rgas / (c->cpd * (d_one + 0.80 * qv));
       td = td + (om * rovcpm * tv) / (c->ptop * rp + c->hsigma[k]);
     }
-    // nudge3d
-    if (rgc > 0) {
+    // nudge3d (iboudy 1/5) or the sponge3d summand (iboudy 4, see k_momentum)
+    double spt = d_zero;
+    if (rgc > 0 && c->iboudy == 4) {
+      const int ib = f.ibcr[o2 >> 3];
+      spt = c->wgtx[ib] * d_zero + (d_one - c->wgtx[ib]) * LD(f.tbt, o3);
+    } else if (rgc > 0) {
       const double xtb = s->xbctime + dt;
       double xf, xg;
       nudge_coef(c, f.ibcr[o2 >> 3], k, xf, xg);
@@ -682,7 +696,7 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
 #undef FGT
     }
     DIFFU_X(td, sTB);
-    const double tt = ((d_zero + td) + d_zero) + d_zero;
+    const double tt = ((spt + td) + d_zero) + d_zero;
     if (f.tten) ST(f.tten, o3, tt);
     const double ct = t2 + dt * tt;
     const double d = c->gnu1 * (ct + t2 - d_two * t1);
@@ -704,7 +718,11 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
       tq = tq - q1 * ((qp > thr && qc0 > thr) ? qp * powpos(qc0 / qp, c->qcon[k + 1]) : d_zero) * c->xds[k];
     }
   }
-  if (rgc > 0) {
+  double spq = d_zero;
+  if (rgc > 0 && c->iboudy == 4) {
+    const int ib = f.ibcr[o2 >> 3];
+    spq = c->wgtx[ib] * d_zero + (d_one - c->wgtx[ib]) * LD(f.qbt, o3);
+  } else if (rgc > 0) {
     const double xtb = s->xbctime + dt;
     const double nfac = 1.0e3, rfac = d_one / nfac;
     double xf, xg;
@@ -737,7 +755,7 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   DIFFU_X(tc, sQCB);
 #undef DT
 #undef H1T
-  tq = ((d_zero + tq) + d_zero) + d_zero;
+  tq = ((spq + tq) + d_zero) + d_zero;
   tc = ((d_zero + tc) + d_zero) + d_zero;
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
   ST(f.cqv, o3, qv2 + dt * tq);
@@ -1370,10 +1388,44 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
 // block per level: west/east first (they read qc(jci1|jci2, ice1|ice2) before south/north
 // rewrite it), then south/north.  The last tile's launch also advances the boundary clock
 // xbctime += dtsec (Main/mod_bdycod.F90:2566): nothing here reads it.
-__global__ void k_bdyval_qc(Geom g, int do_qc, double* a1qc, const double* __restrict__ psa, Slices sl, long slen,
-                            StepState* s, double dtsec, int advance) {
+__global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa,
+                            Slices sl, long slen, StepState* s, double dtsec, int advance) {
   const int k = (int)blockIdx.x + 1;
   if (advance && k == 1 && threadIdx.x == 0) s->xbctime = s->xbctime + dtsec;
+  if (do_qv) {
+    // qv inflow/outflow for iboudy = 3 or 4, Main/mod_bdycod.F90:1809-1950: west/east on ici,
+    // then south/north on jce (reading the west/east results at the corners)
+    for (int i = g.ici1 + (int)threadIdx.x; i <= g.ici2; i += (int)blockDim.x) {
+      if (g.bl) {
+        const double qext = F3(a1qv, g.jce1, i, k) / F2(psa, g.jce1, i);
+        const double qint = F3(a1qv, g.jci1, i, k) / F2(psa, g.jci1, i);
+        const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
+        F3(a1qv, g.jce1, i, k) = (w > d_zero) ? qext * F2(psa, g.jce1, i) : qint * F2(psa, g.jce1, i);
+      }
+      if (g.br) {
+        const double qext = F3(a1qv, g.jce2, i, k) / F2(psa, g.jce2, i);
+        const double qint = F3(a1qv, g.jci2, i, k) / F2(psa, g.jci2, i);
+        const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
+        F3(a1qv, g.jce2, i, k) = (w < d_zero) ? qext * F2(psa, g.jce2, i) : qint * F2(psa, g.jce2, i);
+      }
+    }
+    __syncthreads();
+    for (int j = g.jce1 + (int)threadIdx.x; j <= g.jce2; j += (int)blockDim.x) {
+      if (g.bb) {
+        const double qext = F3(a1qv, j, g.ice1, k) / F2(psa, j, g.ice1);
+        const double qint = F3(a1qv, j, g.ici1, k) / F2(psa, j, g.ici1);
+        const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
+        F3(a1qv, j, g.ice1, k) = (w > d_zero) ? qext * F2(psa, j, g.ice1) : qint * F2(psa, j, g.ice1);
+      }
+      if (g.bt) {
+        const double qext = F3(a1qv, j, g.ice2, k) / F2(psa, j, g.ice2);
+        const double qint = F3(a1qv, j, g.ici2, k) / F2(psa, j, g.ici2);
+        const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
+        F3(a1qv, j, g.ice2, k) = (w < d_zero) ? qext * F2(psa, j, g.ice2) : qint * F2(psa, j, g.ice2);
+      }
+    }
+    __syncthreads();
+  }
   if (!do_qc) return;
   for (int i = g.ice1 + (int)threadIdx.x; i <= g.ice2; i += (int)blockDim.x) {
     if (g.bl) {
