@@ -39,6 +39,10 @@ static const double beta_hyd = 1.0 - 2.0 * 0.0; /* :320 */
 /* mod_diffusion.F90:69-71 */
 static const double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
 
+/* reference-atmosphere constants of the ipgf = 1 pressure gradient, Share/mod_constants.F90:359-362 */
+static const double T00PG = 287.0, P00PG = 101.325, ALAM = 6.5e-3;
+static double c_pgfaa1;
+
 static void init_constants(void) {
   double rgasmol = NAVGDR * BOLTZK;          /* :130 */
   c_c287 = rgasmol / AMD;                    /* :132 */
@@ -46,6 +50,7 @@ static void init_constants(void) {
   c_cpd = 3.5 * c_rgas;                      /* :144 */
   c_ep1 = AMD / AMW - d_one;                 /* :303 */
   c_regrav = d_one / EGRAV;                  /* :182 */
+  c_pgfaa1 = ALAM * c_rgas * c_regrav;       /* :362 */
 }
 
 #define GO 3   /* frame ghost width (covers ga/gb/gc halos) */
@@ -1113,11 +1118,23 @@ static void pressure_gradient_force(orc_t* o) {
   if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TDB(j, o->ice1);
   if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TDB(j, o->ice2);
 #undef TDB
+  /* ipgf = 1 (:1893-1964, 2039-2067): td minus the reference-atmosphere temperature.  The
+   * reference loops k = -1..kz over arrays allocated 1..kz (out of bounds below k = 1); the
+   * defined part k = 1..kz is restated. */
+  const int ipgf = o->cfg.ipgf;
+  if (ipgf == 1)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++)
+          A3(o->td, j, i, k) = A3(o->td, j, i, k) - A2(o->psa, j, i) * T00PG *
+              pow((o->hsigma[k] * A2(o->psa, j, i) + o->ptop) / P00PG, c_pgfaa1);
   for (int k = 1; k <= kz; k++)
     for (int i = o->idi1; i <= o->idi2; i++)
       for (int j = o->jdi1; j <= o->jdi2; j++) {
         double rtbar = d_rfour * (A3(o->xtv, j - 1, i - 1, k) + A3(o->xtv, j - 1, i, k) +
                                   A3(o->xtv, j, i - 1, k) + A3(o->xtv, j, i, k));
+        if (ipgf == 1)
+          rtbar = rtbar - T00PG * pow((o->hsigma[k] * A2(o->psdota, j, i) + o->ptop) / P00PG, c_pgfaa1);
         rtbar = c_rgas * rtbar * A2(o->psdota, j, i);
         double hs = o->hsigma[k], pt = o->ptop;
         double den = o->dx * A2(o->msfd, j, i);
@@ -1136,7 +1153,10 @@ static void pressure_gradient_force(orc_t* o) {
     for (int j = o->jce1; j <= o->jce2; j++) {
       double rp = A2(o->rpsa, j, i);
       double tv = A3(o->td, j, i, kz) * rp * A3(o->tvfac, j, i, kz);
-      A3(o->phi, j, i, kz) = A2(o->ht, j, i) - c_rgas * tv *
+      double top = A2(o->ht, j, i);
+      if (ipgf == 1)
+        top = top + c_rgas * T00PG / c_pgfaa1 * pow((A2(o->psa, j, i) + o->ptop) / P00PG, c_pgfaa1);
+      A3(o->phi, j, i, kz) = top - c_rgas * tv *
           log((o->hsigma[kz] + o->ptop * rp) / (d_one + o->ptop * rp));
     }
   for (int k = 1; k <= kz - 1; k++) {

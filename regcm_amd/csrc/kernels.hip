@@ -38,6 +38,7 @@ static constexpr double d_zero = 0.0, d_one = 1.0, d_two = 2.0, d_four = 4.0;
 static constexpr double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
 static constexpr double MINQQ = 1.0e-8, DLOWVAL = 1.0e-20;
 static constexpr double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
+static constexpr double T00PG = 287.0, P00PG = 101.325;   // ipgf = 1, Share/mod_constants.F90:359-360
 
 __device__ __forceinline__ double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }
 __device__ __forceinline__ double dmin(double a, double b) { return (a < b) ? a : (b < a ? b : a); }
@@ -149,6 +150,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
     const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
     rp = LD(f.rpsa, o2);
+    const double psk = LD(f.psa, o2);
     for (int k = ty + 1; k <= kz; k += 8) {
       const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
       const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
@@ -158,7 +160,10 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       sMD[(k - 1) * 64 + tx] = (a + bq) * dummy;
       const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
       const double qc = dmax(LD(f.a1qc, o3) * rp, d_zero);
-      sTD[(k - 1) * 64 + tx] = LD(f.a1t, o3) * (d_one + ep1 * qv);
+      double tdk = LD(f.a1t, o3) * (d_one + ep1 * qv);
+      // ipgf = 1: minus the reference-atmosphere temperature (ttld, :1893-1964)
+      if (c->ipgf == 1) tdk = tdk - psk * T00PG * pow((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
+      sTD[(k - 1) * 64 + tx] = tdk;
       sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
       sLG[(k - 1) * 64 + tx] = (k < kz) ? log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
                                         : log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
@@ -209,7 +214,9 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     const double ps = LD(f.psa, o2);
     double tdk1 = sTD[(kz - 1) * 64 + tx];
     const double tv = tdk1 * rp * sTV[(kz - 1) * 64 + tx];
-    double ph = LD(f.ht, o2) - rgas * tv * sLG[(kz - 1) * 64 + tx];
+    double top = LD(f.ht, o2);
+    if (c->ipgf == 1) top = top + rgas * T00PG / c->pgfaa1 * pow((ps + ptop) / P00PG, c->pgfaa1);  // :2045
+    double ph = top - rgas * tv * sLG[(kz - 1) * 64 + tx];
     ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
     for (int lev = kz - 1; lev >= 1; lev--) {
       const double tdl = sTD[(lev - 1) * 64 + tx];
@@ -458,6 +465,8 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   // pressure gradient force, part 1 (ipgf = 0) and part 2 (geopotential gradient)
   {
     double rtbar = d_rfour * (sTV[a0 - 1][b0 - 1] + sTV[a0][b0 - 1] + sTV[a0 - 1][b0] + sTV[a0][b0]);
+    if (c->ipgf == 1)                       // reference-atmosphere temperature, :1945-1946
+      rtbar = rtbar - T00PG * pow((c->hsigma[k] * pdota + c->ptop) / P00PG, c->pgfaa1);
     rtbar = c->rgas * rtbar * pdota;
     const double den = c->dx * mfd;
     ut = ut - rtbar * (sX.l.LU[ti][tj + 1] - sX.l.LU[ti][tj]) / den;
