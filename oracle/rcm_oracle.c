@@ -38,6 +38,8 @@ static const double alpha_hyd = 0.0;         /* :319 */
 static const double beta_hyd = 1.0 - 2.0 * 0.0; /* :320 */
 /* mod_diffusion.F90:69-71 */
 static const double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
+/* second-order (9-point) scheme of idiffu = 2, Main/mod_diffusion.F90:63-65 */
+static const double o4_c1 = 4.0 / 6.0, o4_c2 = 1.0 / 6.0, o4_c3 = -20.0 / 6.0;
 
 /* reference-atmosphere constants of the ipgf = 1 pressure gradient, Share/mod_constants.F90:359-362 */
 static const double T00PG = 287.0, P00PG = 101.325, ALAM = 6.5e-3;
@@ -1052,6 +1054,18 @@ static void boundary(orc_t* o) {
 
 /* diffusion, Main/mod_tendency.F90:1515-1526 -> diffu_d, diffu_x3d, diffu_x4d */
 static void diffu_x(orc_t* o, double* ften, const double* f, double fac) {
+  if (o->cfg.idiffu == 2) {
+    /* diffu_x3d / diffu_x4d3d idiffu = 2, Main/mod_diffusion.F90:726-735, 881-891 */
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(ften, j, i, k) = A3(ften, j, i, k) + fac * A3(o->xkc, j, i, k) *
+              (o4_c1 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
+               o4_c2 * (A3(f, j + 1, i + 1, k) + A3(f, j - 1, i - 1, k) + A3(f, j - 1, i + 1, k) +
+                        A3(f, j + 1, i - 1, k)) +
+               o4_c3 * A3(f, j, i, k));
+    return;
+  }
   /* diffu_x3d / diffu_x4d3d idiffu = 1, Main/mod_diffusion.F90:673-713, 808-... */
   for (int k = 1; k <= o->kz; k++)
     for (int i = o->icii1; i <= o->icii2; i++)
@@ -1074,6 +1088,23 @@ static void diffu_x(orc_t* o, double* ften, const double* f, double fac) {
 static void diffu_d(orc_t* o) {                                    /* :281-385 */
   const double* m = o->msfd;
 #define UM(a, J, I) (A3(a, J, I, k) / A2(m, J, I))
+  if (o->cfg.idiffu == 2) {                                        /* :386-411 */
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A3(o->xkd, j, i, k) *
+              (o4_c1 * (UM(o->ubd, j + 1, i) + UM(o->ubd, j - 1, i) + UM(o->ubd, j, i + 1) + UM(o->ubd, j, i - 1)) +
+               o4_c2 * (UM(o->ubd, j + 1, i + 1) + UM(o->ubd, j - 1, i - 1) + UM(o->ubd, j - 1, i + 1) +
+                        UM(o->ubd, j + 1, i - 1)) +
+               o4_c3 * (UM(o->ubd, j, i)));
+          A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) + A3(o->xkd, j, i, k) *
+              (o4_c1 * (UM(o->vbd, j + 1, i) + UM(o->vbd, j - 1, i) + UM(o->vbd, j, i + 1) + UM(o->vbd, j, i - 1)) +
+               o4_c2 * (UM(o->vbd, j + 1, i + 1) + UM(o->vbd, j - 1, i - 1) + UM(o->vbd, j - 1, i + 1) +
+                        UM(o->vbd, j + 1, i - 1)) +
+               o4_c3 * (UM(o->vbd, j, i)));
+        }
+    return;
+  }
   for (int k = 1; k <= o->kz; k++)
     for (int i = o->idii1; i <= o->idii2; i++)
       for (int j = o->jdii1; j <= o->jdii2; j++) {

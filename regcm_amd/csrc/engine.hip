@@ -228,6 +228,7 @@ struct rcmdyn_engine {
     c.c287 = rgasmol / AMD; c.rgas = c.c287 * 1000.0; c.cpd = 3.5 * c.rgas;
     c.ep1 = AMD / AMW - 1.0; c.regrav = 1.0 / EGRAV;
     c.ipgf = cfg.ipgf;
+    c.idiffu = cfg.idiffu;
     c.pgfaa1 = 6.5e-3 * c.rgas * c.regrav;                  // Share/mod_constants.F90:359-362
     c.dx = cfg.ds * 1000.0; c.dx2 = 2.0 * c.dx; c.dx4 = 4.0 * c.dx; c.dx8 = 8.0 * c.dx;
     c.dx16 = 16.0 * c.dx; c.dxsq = c.dx * c.dx; c.rdxsq = 1.0 / c.dxsq;
@@ -370,7 +371,7 @@ struct rcmdyn_engine {
     cfg = *c;
     if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
     if (cfg.idynamic != 1) throw std::runtime_error("rcmdyn: only idynamic=1 (hydrostatic) is built");
-    if (cfg.idiffu != 1) throw std::runtime_error("rcmdyn: only idiffu=1 is built");
+    if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");

@@ -50,7 +50,7 @@ struct Geom {
 
 // Run constants (read-only on device, one copy per engine).
 struct Consts {
-  int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc, ipgf;
+  int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc, ipgf, idiffu;
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
   double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;

@@ -38,6 +38,7 @@ static constexpr double d_zero = 0.0, d_one = 1.0, d_two = 2.0, d_four = 4.0;
 static constexpr double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
 static constexpr double MINQQ = 1.0e-8, DLOWVAL = 1.0e-20;
 static constexpr double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
+static constexpr double o4_c1 = 4.0 / 6.0, o4_c2 = 1.0 / 6.0, o4_c3 = -20.0 / 6.0;  // idiffu = 2
 static constexpr double T00PG = 287.0, P00PG = 101.325;   // ipgf = 1, Share/mod_constants.F90:359-360
 
 __device__ __forceinline__ double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }
@@ -442,7 +443,14 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
     double xkd = d_rfour * (sXK[a0][b0] + sXK[a0 - 1][b0 - 1] + sXK[a0 - 1][b0] + sXK[a0][b0 - 1]);
     xkd = xkd * c->rdxsq * pdotb;
 #define UM(S, dj, di) S[a2 + (di)][b2 + (dj)]
-    if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
+    if (c->idiffu == 2) {                   // 9-point scheme on jdi x idi, :386-411
+      ut = ut + xkd * (o4_c1 * (UM(sUM, 1, 0) + UM(sUM, -1, 0) + UM(sUM, 0, 1) + UM(sUM, 0, -1)) +
+                       o4_c2 * (UM(sUM, 1, 1) + UM(sUM, -1, -1) + UM(sUM, -1, 1) + UM(sUM, 1, -1)) +
+                       o4_c3 * (UM(sUM, 0, 0)));
+      vt = vt + xkd * (o4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +
+                       o4_c2 * (UM(sVM, 1, 1) + UM(sVM, -1, -1) + UM(sVM, -1, 1) + UM(sVM, 1, -1)) +
+                       o4_c3 * (UM(sVM, 0, 0)));
+    } else if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
       ut = ut - xkd * (z4_c1 * (UM(sUM, 2, 0) + UM(sUM, -2, 0) + UM(sUM, 0, 2) + UM(sUM, 0, -2)) +
                        z4_c2 * (UM(sUM, 1, 0) + UM(sUM, -1, 0) + UM(sUM, 0, 1) + UM(sUM, 0, -1)) +
                        z4_c3 * (UM(sUM, 0, 0)));
@@ -455,10 +463,12 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
                    z4_c2 * (UM(sUM, 0, 0)));                                                          \
   vt = vt + xkd * (z4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +        \
                    z4_c2 * (UM(sVM, 0, 0)));
-    if (g.bl && j == g.jdi1) { LAPD(); }
-    if (g.br && j == g.jdi2) { LAPD(); }
-    if (g.bb && i == g.idi1) { LAPD(); }
-    if (g.bt && i == g.idi2) { LAPD(); }
+    if (c->idiffu == 1) {
+      if (g.bl && j == g.jdi1) { LAPD(); }
+      if (g.br && j == g.jdi2) { LAPD(); }
+      if (g.bb && i == g.idi1) { LAPD(); }
+      if (g.bt && i == g.idi2) { LAPD(); }
+    }
 #undef LAPD
 #undef UM
   }
@@ -545,6 +555,13 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
 #define H2T(S, dj, di) S[a2 + (di)][b2 + (dj)]
 #define DIFFU_X(ften, S)                                                                          \
   do {                                                                                            \
+    if (c->idiffu == 2) {                   /* 9-point scheme, :726-735, 881-891 */               \
+      ften = ften + d_one * xkcs *                                                                \
+          (o4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + H2T(S, 0, 1) + H2T(S, 0, -1)) +                \
+           o4_c2 * (H2T(S, 1, 1) + H2T(S, -1, -1) + H2T(S, -1, 1) + H2T(S, 1, -1)) +              \
+           o4_c3 * H2T(S, 0, 0));                                                                 \
+      break;                                                                                      \
+    }                                                                                             \
     if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))                                       \
       ften = ften - d_one * xkcs *                                                                \
           (z4_c1 * (H2T(S, 2, 0) + H2T(S, -2, 0) + H2T(S, 0, 2) + H2T(S, 0, -2)) +                \

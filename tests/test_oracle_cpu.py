@@ -162,7 +162,7 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     base.bdyval()
     base.step(10)
     ref = base.get("ATM1_T")
-    for variant in ({"iboudy": 4}, {"ipgf": 1}):
+    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])
         o.put_state(data["state"])

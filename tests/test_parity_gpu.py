@@ -205,7 +205,7 @@ def test_negative_moisture_serial_sweep(c1_data):
 
 
 # namelist options beyond the defaults, each against the oracle and under decomposition
-VARIANTS = [{"iboudy": 4}, {"ipgf": 1}]
+VARIANTS = [{"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}]
 
 
 def _variant_id(v):
