@@ -19,6 +19,7 @@
 // Column recurrences (pten/qdot, phi, split projections) use one thread per (j,i) column.
 #include "engine.hpp"
 #include "kernels.hpp"
+#include "fastmath.hpp"
 
 namespace rcm {
 
@@ -166,8 +167,8 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       if (c->ipgf == 1) tdk = tdk - psk * T00PG * pow((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
       sTD[(k - 1) * 64 + tx] = tdk;
       sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
-      sLG[(k - 1) * 64 + tx] = (k < kz) ? log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
-                                        : log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
+      sLG[(k - 1) * 64 + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
+                                        : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
     }
   }
   __syncthreads();
@@ -356,11 +357,11 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
     const double hs = c->hsigma[k], pt = c->ptop;
     for (int t = tid; t < TW0 * MBI; t += MBT) {
       const int jj = t % TW0, ii = t / TW0;                  // (J0-1+jj, I0+ii)
-      sX.l.LU[ii][jj] = log(d_half * (sPS[ii + 1][jj] + sPS[ii][jj]) * hs + pt);
+      sX.l.LU[ii][jj] = rcm_log(d_half * (sPS[ii + 1][jj] + sPS[ii][jj]) * hs + pt);
     }
     for (int t = tid; t < MBJ * TH0; t += MBT) {
       const int jj = t % MBJ, ii = t / MBJ;                  // (J0+jj, I0-1+ii)
-      sX.l.LV[ii][jj] = log(d_half * (sPS[ii][jj + 1] + sPS[ii][jj]) * hs + pt);
+      sX.l.LV[ii][jj] = rcm_log(d_half * (sPS[ii][jj + 1] + sPS[ii][jj]) * hs + pt);
     }
   }
   __syncthreads();
@@ -518,10 +519,11 @@ constexpr int SDW = SBJ + 1, SDH = SBI + 1;    // dot points j..j+SBJ, i..i+SBI
 constexpr int SW1 = SBJ + 2, SH1 = SBI + 2;    // halo 1
 constexpr int SW2 = SBJ + 4, SH2 = SBI + 4;    // halo 2
 
-// x**y for x > 0 as exp(y*log(x)): 140 VALU instructions against 226 for OCML pow, within
-// 2 ulp of it for the arguments here (layer pressure ratios, adjacent-level humidity ratios);
-// the reference's libm pow differs from OCML's by ulps anyway (tests/test_parity_gpu.py bounds)
-__device__ __forceinline__ double powpos(double x, double y) { return exp(y * log(x)); }
+// x**y for x > 0 as exp(y*log(x)) with the fdlibm-class routines of fastmath.hpp: about 70
+// VALU instructions against 226 for OCML pow, within a few ulp of it for the arguments here
+// (layer pressure ratios, adjacent-level humidity ratios); the reference's libm pow differs
+// from OCML's by ulps anyway (tests/test_parity_gpu.py bounds)
+__device__ __forceinline__ double powpos(double x, double y) { return rcm_powpos(x, y); }
 
 // upstream flux-form advection of one scalar (hadvt/hadvqv/hadvqx, Main/mod_advection.F90:
 // 337-386, 547-596, 639-653); limiter 0 none, 1 t_extrema, 2 q_rel_extrema
