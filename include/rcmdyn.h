@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RCMDYN_ABI_VERSION 1
+#define RCMDYN_ABI_VERSION 2
 #define RCMDYN_MAXKZ 64
 #define RCMDYN_MAXSPLIT 4
 
@@ -52,7 +52,7 @@ typedef struct rcmdyn_config {
   /* tiles owned by this engine instance: [tile_first, tile_first + tile_count) */
   int32_t tile_first, tile_count;
   /* dynamics options (defaults in brackets) */
-  int32_t idynamic;             /* [1] hydrostatic (2 = non-hydrostatic: not yet built) */
+  int32_t idynamic;             /* [1] hydrostatic, 2 = non-hydrostatic (MM5-type, sound) */
   int32_t iboudy;               /* [5] exponential relaxation (1 = linear) */
   int32_t idiffu;               /* [1] 4th-order diffusion */
   int32_t ipgf;                 /* [0] */
@@ -92,6 +92,17 @@ typedef struct rcmdyn_config {
   int32_t comm_rank, comm_size; /* process rank / size in the RCCL communicator */
   int32_t device;               /* HIP device ordinal, -1 = current */
   uint8_t comm_unique_id[128];  /* ncclUniqueId from rcmdyn_comm_unique_id() on rank 0 */
+  /* non-hydrostatic core (idynamic = 2): nonhydroparam, Main/mod_params.F90:115-116,287-296 */
+  int32_t ifupr;                /* [1] upper radiative boundary condition in sound */
+  int32_t ifrayd;               /* [1] Rayleigh damping of the top levels */
+  int32_t rayndamp;             /* [5] number of damped levels */
+  int32_t nh_reserved;
+  double nhbet, nhxkd;          /* [0.4, 0.1] Ikawa beta, divergence damping */
+  double rayalpha0, rayhd;      /* [3e-4 1/s, 10000 m] */
+  /* init_sound outputs (Main/mod_sound.F90:115-161), computed by the host once:
+   * nh_dtsmax = dx / sqrt(gamma R max(t0)) / (1 + nhxkd), nh_xmsf = mean of msfx over the
+   * interior cross points (the global sumall of :143-145) */
+  double nh_dtsmax, nh_xmsf;
 } rcmdyn_config;
 
 /* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */
@@ -112,6 +123,19 @@ enum rcmdyn_field {
   RCMDYN_PSC, RCMDYN_PTEN, RCMDYN_PSDOTA,
   RCMDYN_TTEN, RCMDYN_UTEN, RCMDYN_VTEN, RCMDYN_QVTEN, RCMDYN_QCTEN,
   RCMDYN_OMEGA, RCMDYN_QDOT /* k = 1..kz+1 */, RCMDYN_XKC, RCMDYN_PHI,
+  /* non-hydrostatic state (coupled with p* like t): pressure perturbation (Pa), vertical
+   * velocity on full levels (k = 1..kz+1), their boundary data */
+  RCMDYN_ATM1_PP, RCMDYN_ATM2_PP, RCMDYN_ATM1_W, RCMDYN_ATM2_W,
+  RCMDYN_XPPB_B0, RCMDYN_XPPB_BT, RCMDYN_XWWB_B0, RCMDYN_XWWB_BT,
+  /* non-hydrostatic reference state and statics, as make_reference_atmosphere and
+   * compute_full_coriolis_coefficients leave them (Main/mod_params.F90:2614-2741):
+   * atm0 ps (2-D, p* in Pa), pr, t, rho, z (half levels), pf, rhof, zf (full levels, kz+1),
+   * dpsdxm, dpsdym (2-D), dprddx, dprddy (dot, kz), ef, ddx, ddy, dmdx, dmdy (dot, 2-D),
+   * ex, crx, cry (cross, 2-D) */
+  RCMDYN_ATM0_PS, RCMDYN_ATM0_PR, RCMDYN_ATM0_T, RCMDYN_ATM0_RHO, RCMDYN_ATM0_Z,
+  RCMDYN_ATM0_PF, RCMDYN_ATM0_RHOF, RCMDYN_ATM0_ZF,
+  RCMDYN_DPSDXM, RCMDYN_DPSDYM, RCMDYN_DPRDDX, RCMDYN_DPRDDY,
+  RCMDYN_EF, RCMDYN_DDX, RCMDYN_DDY, RCMDYN_DMDX, RCMDYN_DMDY, RCMDYN_EX, RCMDYN_CRX, RCMDYN_CRY,
   RCMDYN_NFIELDS
 };
 

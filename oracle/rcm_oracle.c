@@ -552,6 +552,13 @@ static void decouple(orc_t* o) {
         A3(o->ud, o->jde1, i, k) = SI(o->wue, i, k) * A2(o->rpsda, o->jde1, i);
         A3(o->vd, o->jde1, i, k) = SI(o->wve, i, k) * A2(o->rpsda, o->jde1, i);
       }
+    if (o->cfg.iboudy == 3 || o->cfg.iboudy == 4)                    /* :908-918 */
+      for (int k = 1; k <= kz; k++)
+        for (int i = o->idi1; i <= o->idi2; i++)
+          if (A3(o->a1u, o->jde1, i, k) <= d_zero) {
+            A3(o->ud, o->jde1, i, k) = A3(o->ud, o->jdi1, i, k);
+            A3(o->vd, o->jde1, i, k) = A3(o->vd, o->jdi1, i, k);
+          }
   }
   if (o->br) {                                                    /* :920-932 */
     for (int k = 1; k <= kz; k++)
@@ -564,6 +571,13 @@ static void decouple(orc_t* o) {
         A3(o->ud, o->jde2, i, k) = SI(o->eue, i, k) * A2(o->rpsda, o->jde2, i);
         A3(o->vd, o->jde2, i, k) = SI(o->eve, i, k) * A2(o->rpsda, o->jde2, i);
       }
+    if (o->cfg.iboudy == 3 || o->cfg.iboudy == 4)                    /* :933-943 */
+      for (int k = 1; k <= kz; k++)
+        for (int i = o->idi1; i <= o->idi2; i++)
+          if (A3(o->a1u, o->jde2, i, k) >= d_zero) {
+            A3(o->ud, o->jde2, i, k) = A3(o->ud, o->jdi2, i, k);
+            A3(o->vd, o->jde2, i, k) = A3(o->vd, o->jdi2, i, k);
+          }
   }
   if (o->bb) {                                                    /* :945-957 */
     for (int k = 1; k <= kz; k++)
@@ -576,6 +590,13 @@ static void decouple(orc_t* o) {
         A3(o->ud, j, o->ide1, k) = SJ(o->sue, j, k) * A2(o->rpsda, j, o->ide1);
         A3(o->vd, j, o->ide1, k) = SJ(o->sve, j, k) * A2(o->rpsda, j, o->ide1);
       }
+    if (o->cfg.iboudy == 3 || o->cfg.iboudy == 4)                    /* :958-968 */
+      for (int k = 1; k <= kz; k++)
+        for (int j = o->jde1; j <= o->jde2; j++)
+          if (A3(o->a1v, j, o->ide1, k) >= d_zero) {
+            A3(o->ud, j, o->ide1, k) = A3(o->ud, j, o->idi1, k);
+            A3(o->vd, j, o->ide1, k) = A3(o->vd, j, o->idi1, k);
+          }
   }
   if (o->bt) {                                                    /* :970-982 */
     for (int k = 1; k <= kz; k++)
@@ -588,6 +609,13 @@ static void decouple(orc_t* o) {
         A3(o->ud, j, o->ide2, k) = SJ(o->nue, j, k) * A2(o->rpsda, j, o->ide2);
         A3(o->vd, j, o->ide2, k) = SJ(o->nve, j, k) * A2(o->rpsda, j, o->ide2);
       }
+    if (o->cfg.iboudy == 3 || o->cfg.iboudy == 4)                    /* :983-993 */
+      for (int k = 1; k <= kz; k++)
+        for (int j = o->jde1; j <= o->jde2; j++)
+          if (A3(o->a1v, j, o->ide2, k) <= d_zero) {
+            A3(o->ud, j, o->ide2, k) = A3(o->ud, j, o->idi2, k);
+            A3(o->vd, j, o->ide2, k) = A3(o->vd, j, o->idi2, k);
+          }
   }
   xch(o, o->ud, kz, 1, 0); xch(o, o->vd, kz, 1, 0);            /* :1003-1004 */
   /* umd/vmd (:1005-1008) feed only non-hydrostatic terms: not needed for idynamic=1 */

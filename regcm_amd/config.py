@@ -17,7 +17,7 @@ import numpy as np
 
 MAXKZ = 64
 MAXSPLIT = 4
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # Share/mod_sigma.F90:88-152 -- the hard-coded sigma tables (data, cited).
 SIGMA_TABLES = {
@@ -67,6 +67,11 @@ class RcmdynConfig(ctypes.Structure):
         ("comm_rank", ctypes.c_int32), ("comm_size", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("comm_unique_id", ctypes.c_uint8 * 128),
+        ("ifupr", ctypes.c_int32), ("ifrayd", ctypes.c_int32), ("rayndamp", ctypes.c_int32),
+        ("nh_reserved", ctypes.c_int32),
+        ("nhbet", ctypes.c_double), ("nhxkd", ctypes.c_double),
+        ("rayalpha0", ctypes.c_double), ("rayhd", ctypes.c_double),
+        ("nh_dtsmax", ctypes.c_double), ("nh_xmsf", ctypes.c_double),
     ]
 
 
@@ -80,10 +85,21 @@ FIELD_NAMES = [
     "XPSB_B0", "XPSB_BT",
     "PSC", "PTEN", "PSDOTA", "TTEN", "UTEN", "VTEN", "QVTEN", "QCTEN",
     "OMEGA", "QDOT", "XKC", "PHI",
+    "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W", "XPPB_B0", "XPPB_BT", "XWWB_B0", "XWWB_BT",
+    "ATM0_PS", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_Z", "ATM0_PF", "ATM0_RHOF", "ATM0_ZF",
+    "DPSDXM", "DPSDYM", "DPRDDX", "DPRDDY", "EF", "DDX", "DDY", "DMDX", "DMDY", "EX", "CRX", "CRY",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
-         "PTEN", "PSDOTA"}
+         "PTEN", "PSDOTA", "ATM0_PS", "DPSDXM", "DPSDYM", "EF", "DDX", "DDY", "DMDX", "DMDY",
+         "EX", "CRX", "CRY"}
+FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM0_RHOF",
+               "ATM0_ZF"}
+NH_STATE_FIELDS = ["ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"]
+NH_BDY_FIELDS = ["XPPB_B0", "XPPB_BT", "XWWB_B0", "XWWB_BT"]
+NH_STATIC_FIELDS = ["ATM0_PS", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_Z", "ATM0_PF",
+                    "ATM0_RHOF", "ATM0_ZF", "DPSDXM", "DPSDYM", "DPRDDX", "DPRDDY",
+                    "EF", "DDX", "DDY", "DMDX", "DMDY", "EX", "CRX", "CRY"]
 STATE_FIELDS = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC",
                 "ATM2_U", "ATM2_V", "ATM2_T", "ATM2_QV", "ATM2_QC",
                 "PSA", "PSB", "DSTOR", "HSTOR"]
@@ -97,14 +113,16 @@ def field_levels(name: str, kz: int, nsplit: int) -> int:
         return 1
     if name in ("DSTOR", "HSTOR"):
         return nsplit
-    if name == "QDOT":
+    if name in FULL_LEVELS:
         return kz + 1
     return kz
 
 
 @dataclasses.dataclass
 class RunConfig:
-    """One BASELINE.json configuration (hydrostatic core, physics stubbed)."""
+    """One BASELINE.json configuration (physics stubbed).  ``idynamic`` 1 = hydrostatic,
+    2 = non-hydrostatic; the NH knobs are nonhydroparam (Main/mod_params.F90:287-296) and
+    referenceatm (Share/mod_dynparam.F90:507-508)."""
 
     jx: int
     iy: int
@@ -134,8 +152,23 @@ class RunConfig:
     ibdyfrq: int = 6
     present_qc: int = 0
     name: str = ""
+    idynamic: int = 1
+    ifupr: int = 1
+    ifrayd: int = 1
+    rayndamp: int = 5
+    rayalpha0: float = 0.0003
+    rayhd: float = 10000.0
+    nhbet: float = 0.4
+    nhxkd: float = 0.1
+    base_state_pressure: float = 101325.0
+    logp_lrate: float = 47.70
+    base_state_ts0: float = 288.15   # domain-file value in the reference; synthetic here
 
     def __post_init__(self):
+        # dynparam defaults per core, Main/mod_params.F90:645-661
+        if self.idynamic == 2:
+            self.gnu1 = self.gnu2 = 0.1
+            self.diffu_hgtf = 0
         # Share/mod_dynparam.F90:664-675
         for attr in ("nspgx", "nspgd"):
             if getattr(self, attr) is None:
@@ -160,6 +193,11 @@ CONFIGS = {
     "C2": RunConfig(jx=96, iy=96, kz=23, ds=50.0, dt=100.0, name="C2 96x96x23 dt=100"),
     "C3": RunConfig(jx=192, iy=192, kz=23, ds=50.0, dt=150.0, name="C3 192x192x23 50km EURO"),
     "C4": RunConfig(jx=384, iy=384, kz=23, ds=50.0, dt=150.0, name="C4 384x384x23"),
+    # non-hydrostatic: C5 is BASELINE's 3 km convection-permitting case; N1/N2 are reduced
+    # grids of the same physics for parity tests
+    "N1": RunConfig(jx=40, iy=36, kz=18, ds=3.0, dt=30.0, idynamic=2, name="N1 40x36x18 NH 3km"),
+    "N2": RunConfig(jx=96, iy=96, kz=41, ds=3.0, dt=30.0, idynamic=2, name="N2 96x96x41 NH 3km"),
+    "C5": RunConfig(jx=768, iy=768, kz=41, ds=3.0, dt=30.0, idynamic=2, name="C5 768x768x41 NH 3km"),
 }
 
 
@@ -174,7 +212,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.nproc_j, c.nproc_i = nproc_j, nproc_i
     c.tile_first = tile_first
     c.tile_count = nproc_j * nproc_i if tile_count is None else tile_count
-    c.idynamic = 1
+    c.idynamic = rc.idynamic
     c.iboudy, c.idiffu, c.ipgf, c.nsplit = rc.iboudy, rc.idiffu, rc.ipgf, rc.nsplit
     c.nspgx, c.nspgd = rc.nspgx, rc.nspgd
     c.diffu_hgtf = rc.diffu_hgtf
@@ -209,6 +247,11 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.comm_rank, c.comm_size, c.device = comm_rank, comm_size, device
     if unique_id is not None:
         ctypes.memmove(c.comm_unique_id, unique_id, 128)
+    c.ifupr, c.ifrayd, c.rayndamp = rc.ifupr, rc.ifrayd, rc.rayndamp
+    c.nhbet, c.nhxkd, c.rayalpha0, c.rayhd = rc.nhbet, rc.nhxkd, rc.rayalpha0, rc.rayhd
+    if rc.idynamic == 2:
+        c.nh_dtsmax = split["nh_dtsmax"]
+        c.nh_xmsf = split["nh_xmsf"]
     return c
 
 

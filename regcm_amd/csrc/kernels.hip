@@ -255,6 +255,31 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
 // (atm2*(1/psdotb))/msfd, tv = t*(1+ep1*qv)): one round of independent global loads per
 // block instead of dependent per-operand rounds, and one division per staged point instead
 // of 13 per output.  Points outside jdi x idi keep their values (copied by k_qfilter).
+// decoupled boundary ud/vd of decouple with the inflow/outflow rule of iboudy = 3/4
+// (Main/mod_tendency.F90:893-994): an outflow boundary point takes the adjacent interior
+// value.  W/E run on the idi columns first, then S/N on the full jde rows, so a corner row
+// point copies the (possibly already replaced) W/E value.  The slice values the reference
+// multiplies (wui, wue, ...) equal atm1 there (bdyuv), so the default is atm1 * rpsda.
+__device__ double2 udvd_bdy(const Geom& g, const Fields& f, int j, int i, uint32_t kof) {
+  auto base = [&](int jj, int ii) {
+    const uint32_t q2 = g.o2(jj, ii);
+    const double r = LD(f.rpsda, q2);
+    return make_double2(LD(f.a1u, q2 + kof) * r, LD(f.a1v, q2 + kof) * r);
+  };
+  auto we = [&](int jj, int ii) {
+    if (in(ii, g.idi1, g.idi2)) {
+      if (g.bl && jj == g.jde1 && LD(f.a1u, g.o2(jj, ii) + kof) <= d_zero) return base(g.jdi1, ii);
+      if (g.br && jj == g.jde2 && LD(f.a1u, g.o2(jj, ii) + kof) >= d_zero) return base(g.jdi2, ii);
+    }
+    return base(jj, ii);
+  };
+  if (in(j, g.jde1, g.jde2)) {
+    if (g.bb && i == g.ide1 && LD(f.a1v, g.o2(j, i) + kof) >= d_zero) return we(j, g.idi1);
+    if (g.bt && i == g.ide2 && LD(f.a1v, g.o2(j, i) + kof) <= d_zero) return we(j, g.idi2);
+  }
+  return we(j, i);
+}
+
 constexpr int TW1 = MBJ + 2, TH1 = MBI + 2;   // halo 1 on every side
 constexpr int TW2 = MBJ + 4, TH2 = MBI + 4;   // halo 2 on every side
 constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i-1)
@@ -297,6 +322,10 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
       const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
       const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
       umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
+      if (c->iboudy == 4 && (jg == g.jde1 || jg == g.jde2 || ig == g.ide1 || ig == g.ide2)) {
+        const double2 b = udvd_bdy(g, f, jg, ig, kof);
+        ud = b.x; vd = b.y;
+      }
     }
     sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd;
   }

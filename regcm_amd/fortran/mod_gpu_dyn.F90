@@ -11,7 +11,7 @@ module mod_gpu_dyn
   implicit none
   private
 
-  integer, parameter, public :: rcmdyn_abi_version = 1
+  integer, parameter, public :: rcmdyn_abi_version = 2
   integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
 
   ! field ids (enum rcmdyn_field)
@@ -23,7 +23,13 @@ module mod_gpu_dyn
     f_xub_b0 = 18, f_xub_bt = 19, f_xvb_b0 = 20, f_xvb_bt = 21, f_xtb_b0 = 22, &
     f_xtb_bt = 23, f_xqb_b0 = 24, f_xqb_bt = 25, f_xpsb_b0 = 26, f_xpsb_bt = 27, &
     f_psc = 28, f_pten = 29, f_psdota = 30, f_tten = 31, f_uten = 32, f_vten = 33, &
-    f_qvten = 34, f_qcten = 35, f_omega = 36, f_qdot = 37, f_xkc = 38, f_phi = 39
+    f_qvten = 34, f_qcten = 35, f_omega = 36, f_qdot = 37, f_xkc = 38, f_phi = 39, &
+    f_atm1_pp = 40, f_atm2_pp = 41, f_atm1_w = 42, f_atm2_w = 43, &
+    f_xppb_b0 = 44, f_xppb_bt = 45, f_xwwb_b0 = 46, f_xwwb_bt = 47, &
+    f_atm0_ps = 48, f_atm0_pr = 49, f_atm0_t = 50, f_atm0_rho = 51, f_atm0_z = 52, &
+    f_atm0_pf = 53, f_atm0_rhof = 54, f_atm0_zf = 55, f_dpsdxm = 56, f_dpsdym = 57, &
+    f_dprddx = 58, f_dprddy = 59, f_ef = 60, f_ddx = 61, f_ddy = 62, f_dmdx = 63, &
+    f_dmdy = 64, f_ex = 65, f_crx = 66, f_cry = 67
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -47,6 +53,9 @@ module mod_gpu_dyn
     real(c_double) :: pd
     integer(c_int32_t) :: comm_rank, comm_size, device
     integer(c_int8_t) :: comm_unique_id(128)
+    ! non-hydrostatic core (nonhydroparam, init_sound outputs)
+    integer(c_int32_t) :: ifupr, ifrayd, rayndamp, nh_reserved
+    real(c_double) :: nhbet, nhxkd, rayalpha0, rayhd, nh_dtsmax, nh_xmsf
   end type rcmdyn_config
 
   interface

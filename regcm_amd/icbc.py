@@ -163,3 +163,120 @@ def spinit_storage(rc: RunConfig, split: dict, st: dict):
             h = ((h + pdlog) + (tau[l, k] * st["ATM2_T"][k][ce]) / psb) + eps
         hstor[l][ce] = h
     return dstor, hstor
+
+
+def nhpp(sigma: np.ndarray, t: np.ndarray, tv: np.ndarray, pr0: np.ndarray, t0: np.ndarray,
+         ps_cb: np.ndarray, ps0_pa: np.ndarray, ptop: float) -> np.ndarray:
+    """Pressure perturbation in hydrostatic balance with t and the p* ps_cb, integrated up from
+    the surface (Share/mod_nhinterp.F90:284-350).  Inputs (kz, ...) on cross points; Pa."""
+    kz = t.shape[0]
+    pp = np.empty_like(t)
+    p0surf = ps0_pa + ptop * 1000.0
+    psp = ps_cb * 1000.0 - ps0_pa
+    k = kz - 1
+    delp0 = p0surf - pr0[k]
+    tvpot = (tv[k] - t0[k]) / t[k]
+    pp[k] = (tvpot * delp0 + psp) / (1.0 + delp0 / pr0[k])
+    for k in range(kz - 2, -1, -1):           # Fortran k = kz-1 .. 1
+        wtl = (sigma[k + 1] - sigma[k]) / (sigma[k + 2] - sigma[k])
+        wtu = 1.0 - wtl
+        aa = C.egrav / (pr0[k + 1] - pr0[k])
+        bb = C.egrav * wtl / pr0[k + 1] * t0[k + 1] / t[k + 1]
+        cc = C.egrav * wtu / pr0[k] * t0[k] / t[k]
+        tvpot = wtl * ((tv[k + 1] - t0[k + 1]) / t[k + 1]) + wtu * ((tv[k] - t0[k]) / t[k])
+        pp[k] = (C.egrav * tvpot + pp[k + 1] * (aa - bb)) / (aa + cc)
+    return pp
+
+
+def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: float = 0.02) -> dict:
+    """Synthetic non-hydrostatic ICBC ("syn-icbc v1", NH variant).
+
+    The reference state comes from the terrain (regcm_amd/nhbase.py); p* is the constant
+    reference p* (``sfs%psa = atm0%ps * 1e-3``, Main/mod_init.F90:144-151); t, qv, u, v are
+    the hydrostatic synthetic profiles on the NH half levels; the pressure perturbation
+    balances them hydrostatically against the US-standard surface pressure (``nhpp``); w is
+    zero on the boundary and small seeded noise inside (so every w term is exercised from
+    the first step).  Boundary time level 1 adds (1 K, 1 m/s, +2 % qv) as in the hydrostatic
+    generator, with its own balanced pp.
+    """
+    from . import nhbase
+    rng = np.random.Generator(np.random.PCG64(seed + 2))
+    jx, iy, kz = rc.jx, rc.iy, rc.kz
+    sigma = rc.sigma
+    hsig = (sigma[1:] + sigma[:-1]) * 0.5
+    ptop = rc.ptop
+    hmax = (800.0 if rc.ds < 10.0 else 1500.0) if hmax is None else hmax
+    jj, ii = np.meshgrid(np.arange(1, jx + 1, dtype=np.float64),
+                         np.arange(1, iy + 1, dtype=np.float64))
+    jc, ic = 0.5 * jx, 0.5 * iy
+    r2 = (jj - jc) ** 2 + (ii - ic) ** 2
+    ht = hmax * np.exp(-r2 / (2.0 * (0.15 * jx) ** 2)) + rng.normal(0.0, 20.0, (iy, jx))
+    ht = np.maximum(ht, 0.0)
+    mf = 1.0 + 0.02 * ((ii - ic) / iy) ** 2
+    dlat = 30.0 + 30.0 * (ii - 1.0) / max(iy - 1.0, 1.0)
+    xlat = 30.0 + 30.0 * (ii - 0.5) / max(iy - 1.0, 1.0)
+    xlon = 10.0 + 20.0 * (jj - 0.5) / max(jx - 1.0, 1.0)
+    coriol = 2.0 * C.eomeg * np.sin(np.deg2rad(dlat))
+    msfx = 1.0 / mf
+    msfd = 1.0 / mf
+    ht_geo = ht * C.egrav
+    ref = nhbase.reference_state(rc, ht_geo, msfx, msfd, xlat, xlon, dlat)
+    F = ref["fields"]
+    ce = (slice(0, iy - 1), slice(0, jx - 1))
+    ps0 = F["ATM0_PS"][0][ce]                         # Pa
+    pr0 = F["ATM0_PR"][:, 0:iy - 1, 0:jx - 1]
+    t0 = F["ATM0_T"][:, 0:iy - 1, 0:jx - 1]
+    pstar = np.zeros((iy, jx))
+    pstar[ce] = ps0 * 1.0e-3                          # Main/mod_init.F90:146
+    pdot = psc2psd_global(pstar)
+    expo = C.egrav / (C.rgas * 0.0065)
+    ps_h = (C.stdpcb * (1.0 - 0.0065 * ht / 288.15) ** expo - ptop)[ce]
+
+    t = np.maximum(288.15 * (pr0 / 101325.0) ** (C.rgas * 0.0065 / C.egrav), 216.65)
+    t = t + rng.normal(0.0, 0.5, t.shape)
+    qv = 0.7 * _qsat(t, pr0)
+    pp = nhpp(sigma, t, t * (1.0 + C.ep1 * qv), pr0, t0, ps_h, ps0, ptop)
+    t1, qv1 = t + 1.0, qv * 1.02
+    pp1 = nhpp(sigma, t1, t1 * (1.0 + C.ep1 * qv1), pr0, t0, ps_h, ps0, ptop)
+    u = (10.0 + 15.0 * np.sin(math.pi * hsig)[:, None, None] *
+         np.cos(math.pi * (ii - ic) / iy)[None]) + rng.normal(0.0, 0.3, (kz, iy, jx))
+    v = (2.0 * np.sin(2.0 * math.pi * jj / jx))[None] + rng.normal(0.0, 0.3, (kz, iy, jx))
+    u1, v1 = u + 1.0, v + 1.0
+    w = np.zeros((kz + 1, iy, jx))
+    w[1:kz, 1:iy - 2, 1:jx - 2] = rng.normal(0.0, w_noise, (kz - 1, iy - 3, jx - 3))
+    rdtbdy = 1.0 / rc.dtbdys
+
+    def cross3(a):
+        out = np.zeros((a.shape[0], iy, jx))
+        out[:, 0:iy - 1, 0:jx - 1] = a
+        return out
+
+    ps3 = pstar[None]
+    tb0, tb1 = cross3(t) * ps3, cross3(t1) * ps3
+    qb0, qb1 = cross3(qv) * ps3, cross3(qv1) * ps3
+    ppb0, ppb1 = cross3(pp) * ps3, cross3(pp1) * ps3
+    ub0, ub1 = u * pdot[None], u1 * pdot[None]
+    vb0, vb1 = v * pdot[None], v1 * pdot[None]
+    st = dict(F)
+    st["MSFX"], st["MSFD"] = msfx[None].copy(), msfd[None].copy()
+    st["CORIOL"], st["HT"] = coriol[None].copy(), ht_geo[None].copy()
+    st["XUB_B0"], st["XUB_BT"] = ub0, (ub1 - ub0) * rdtbdy
+    st["XVB_B0"], st["XVB_BT"] = vb0, (vb1 - vb0) * rdtbdy
+    st["XTB_B0"], st["XTB_BT"] = tb0, (tb1 - tb0) * rdtbdy
+    st["XQB_B0"], st["XQB_BT"] = qb0, (qb1 - qb0) * rdtbdy
+    st["XPPB_B0"], st["XPPB_BT"] = ppb0, (ppb1 - ppb0) * rdtbdy
+    st["XWWB_B0"], st["XWWB_BT"] = np.zeros((kz + 1, iy, jx)), np.zeros((kz + 1, iy, jx))
+    st["XPSB_B0"], st["XPSB_BT"] = pstar[None].copy(), np.zeros((1, iy, jx))
+    for lvl in ("ATM1", "ATM2"):
+        st[f"{lvl}_U"], st[f"{lvl}_V"] = ub0.copy(), vb0.copy()
+        st[f"{lvl}_T"], st[f"{lvl}_QV"] = tb0.copy(), qb0.copy()
+        st[f"{lvl}_QC"] = np.zeros((kz, iy, jx))
+        st[f"{lvl}_PP"] = ppb0.copy()
+        st[f"{lvl}_W"] = w * ps3
+    st["PSA"], st["PSB"] = pstar[None].copy(), pstar[None].copy()
+    split = spinit_constants(sigma, ptop, kz, rc.dt, rc.nsplit)
+    split["nh_dtsmax"] = ref["nh_dtsmax"]
+    split["nh_xmsf"] = ref["nh_xmsf"]
+    st["DSTOR"] = np.zeros((rc.nsplit, iy, jx))
+    st["HSTOR"] = np.zeros((rc.nsplit, iy, jx))
+    return dict(state=st, split=split)
