@@ -106,6 +106,19 @@ struct orc {
   /* boundary slices (Main/mod_bdycod.F90:58-61): indexed by frame j or i, then k */
   double *wue, *wui, *eue, *eui, *wve, *wvi, *eve, *evi;
   double *sue, *sui, *nue, *nui, *sve, *svi, *nve, *nvi;
+  /* non-hydrostatic core (idynamic = 2) */
+  int nh;
+  double *a1pp, *a2pp, *a1w, *a2w, *ppb0, *ppbt, *wwb0, *wwbt;
+  double *ps0, *pr0, *t0, *rho0, *z0, *pf0, *rhof0, *zf0, *dpsdxm, *dpsdym, *dprddx, *dprddy;
+  double *ef, *ddx, *ddy, *dmdx, *dmdy, *ex, *crx, *cry;
+  double *umd, *vmd, *xpp, *xw, *pr1, *rho1, *xpr, *ucc, *vcc, *ppb3d, *wb3d, *xkcf;
+  double *ppten, *ppdyn, *wten, *wdyn, *cpp, *cw, *cdt;
+  double *s_wo, *s_e, *s_f, *s_aa, *s_b, *s_c, *s_rhs, *s_ca, *s_g1, *s_g2, *s_ptend, *s_pxup,
+         *s_pyvp, *s_tk, *s_cc, *s_cdd, *s_cj, *s_pi, *s_ucrs, *s_vcrs;
+  double *estore, *astore, *wpval;
+  double tmask[13][13];                     /* tmask(nsj, nsi), nsj/nsi = -6..6 */
+  int tmask_valid, nh_istep;
+  double nh_cfl;
   /* diagnostics */
   double ptntot, pt2tot;
   /* exchange */
@@ -208,6 +221,10 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   init_constants();
   if (cfg->tile_count != 1 || cfg->kz > RCMDYN_MAXKZ || cfg->nsplit > RCMDYN_MAXSPLIT)
     return NULL;
+  /* the non-hydrostatic restatement covers one tile (the upper radiative condition of sound
+   * gathers estore over the whole domain, Main/mod_sound.F90:496-497) */
+  if (cfg->idynamic == 2 && cfg->nproc_j * cfg->nproc_i != 1) return NULL;
+  if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
   o->cfg = *cfg;
   o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
@@ -265,6 +282,11 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   o->xkhmax = o->dxsq / (64.0 * o->dtsec);
   o->dydc = cfg->adyndif * VONKAR * VONKAR * o->dx * d_rfour;
   o->xkhz = cfg->ckh * 1.5e-3 * o->dxsq / o->dtsec;
+  o->nh = (cfg->idynamic == 2);
+  if (o->nh) {                                /* :108-113 (Xu et al. 2001) */
+    o->xkhz = cfg->ckh * o->dx;
+    o->xkhmax = d_two * o->xkhmax;
+  }
   /* setup_bdycon, Main/mod_bdycod.F90:203-274 */
   o->fnudge = (cfg->bdy_nm > 0) ? cfg->bdy_nm : 0.1 / o->dt;
   o->gnudge = (cfg->bdy_dm > 0) ? cfg->bdy_dm : d_one / (o->dt * 50.0);
@@ -335,6 +357,26 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   o->ddsum = alloc3(o, o->nsplit); o->dhsum = alloc3(o, o->nsplit);
   o->xdelh = alloc3(o, 1); o->work = alloc3(o, 3); o->uu = alloc3(o, 1); o->vv = alloc3(o, 1);
   o->uuu = alloc3(o, kz); o->vvv = alloc3(o, kz);
+  if (o->nh) {
+    o->a1pp = alloc3(o, kz); o->a2pp = alloc3(o, kz); o->a1w = alloc3(o, kp); o->a2w = alloc3(o, kp);
+    o->ppb0 = alloc3(o, kz); o->ppbt = alloc3(o, kz); o->wwb0 = alloc3(o, kp); o->wwbt = alloc3(o, kp);
+    o->ps0 = alloc3(o, 1); o->pr0 = alloc3(o, kz); o->t0 = alloc3(o, kz); o->rho0 = alloc3(o, kz);
+    o->z0 = alloc3(o, kz); o->pf0 = alloc3(o, kp); o->rhof0 = alloc3(o, kp); o->zf0 = alloc3(o, kp);
+    o->dpsdxm = alloc3(o, 1); o->dpsdym = alloc3(o, 1); o->dprddx = alloc3(o, kz); o->dprddy = alloc3(o, kz);
+    o->ef = alloc3(o, 1); o->ddx = alloc3(o, 1); o->ddy = alloc3(o, 1); o->dmdx = alloc3(o, 1);
+    o->dmdy = alloc3(o, 1); o->ex = alloc3(o, 1); o->crx = alloc3(o, 1); o->cry = alloc3(o, 1);
+    o->umd = alloc3(o, kz); o->vmd = alloc3(o, kz); o->xpp = alloc3(o, kz); o->xw = alloc3(o, kp);
+    o->pr1 = alloc3(o, kz); o->rho1 = alloc3(o, kz); o->xpr = alloc3(o, kz);
+    o->ucc = alloc3(o, kz); o->vcc = alloc3(o, kz); o->ppb3d = alloc3(o, kz); o->wb3d = alloc3(o, kp);
+    o->xkcf = alloc3(o, kp);
+    o->ppten = alloc3(o, kz); o->ppdyn = alloc3(o, kz); o->wten = alloc3(o, kp); o->wdyn = alloc3(o, kp);
+    o->cpp = alloc3(o, kz); o->cw = alloc3(o, kp); o->cdt = alloc3(o, kz);
+    double** sc[] = {&o->s_wo, &o->s_e, &o->s_f, &o->s_aa, &o->s_b, &o->s_c, &o->s_rhs, &o->s_ca,
+                     &o->s_g1, &o->s_g2, &o->s_ptend, &o->s_pxup, &o->s_pyvp, &o->s_tk, &o->s_cc,
+                     &o->s_cdd, &o->s_cj, &o->s_pi, &o->s_ucrs, &o->s_vcrs};
+    for (size_t q = 0; q < sizeof(sc) / sizeof(sc[0]); q++) *sc[q] = alloc3(o, kp);
+    o->estore = alloc3(o, 1); o->astore = alloc3(o, 1); o->wpval = alloc3(o, 1);
+  }
   size_t sjn = (size_t)o->nj * kz, sin_ = (size_t)o->ni * kz;
   o->sue = calloc(sjn, 8); o->sui = calloc(sjn, 8); o->nue = calloc(sjn, 8); o->nui = calloc(sjn, 8);
   o->sve = calloc(sjn, 8); o->svi = calloc(sjn, 8); o->nve = calloc(sjn, 8); o->nvi = calloc(sjn, 8);
@@ -359,6 +401,16 @@ void orc_destroy(orc_t* o) {
     &o->sve, &o->svi, &o->nve, &o->nvi, &o->wue, &o->wui, &o->eue, &o->eui, &o->wve, &o->wvi,
     &o->eve, &o->evi};
   for (size_t p = 0; p < sizeof(ptrs) / sizeof(ptrs[0]); p++) free(*ptrs[p]);
+  double** nhp[] = {
+    &o->a1pp, &o->a2pp, &o->a1w, &o->a2w, &o->ppb0, &o->ppbt, &o->wwb0, &o->wwbt, &o->ps0, &o->pr0,
+    &o->t0, &o->rho0, &o->z0, &o->pf0, &o->rhof0, &o->zf0, &o->dpsdxm, &o->dpsdym, &o->dprddx,
+    &o->dprddy, &o->ef, &o->ddx, &o->ddy, &o->dmdx, &o->dmdy, &o->ex, &o->crx, &o->cry, &o->umd,
+    &o->vmd, &o->xpp, &o->xw, &o->pr1, &o->rho1, &o->xpr, &o->ucc, &o->vcc, &o->ppb3d, &o->wb3d,
+    &o->xkcf, &o->ppten, &o->ppdyn, &o->wten, &o->wdyn, &o->cpp, &o->cw, &o->cdt, &o->s_wo, &o->s_e,
+    &o->s_f, &o->s_aa, &o->s_b, &o->s_c, &o->s_rhs, &o->s_ca, &o->s_g1, &o->s_g2, &o->s_ptend,
+    &o->s_pxup, &o->s_pyvp, &o->s_tk, &o->s_cc, &o->s_cdd, &o->s_cj, &o->s_pi, &o->s_ucrs, &o->s_vcrs,
+    &o->estore, &o->astore, &o->wpval};
+  for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
   for (int n = 0; n < 2; n++) {
     free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
     free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
@@ -408,6 +460,18 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     case RCMDYN_PHI: return o->phi;
     case RCMDYN_QDOT: *nk = o->kz + 1; return o->qdot;
     case RCMDYN_DSTOR: *nk = o->nsplit; return o->dstor;
+    case RCMDYN_ATM1_PP: return o->a1pp;  case RCMDYN_ATM2_PP: return o->a2pp;
+    case RCMDYN_XPPB_B0: return o->ppb0;  case RCMDYN_XPPB_BT: return o->ppbt;
+    case RCMDYN_ATM0_PR: return o->pr0;   case RCMDYN_ATM0_T: return o->t0;
+    case RCMDYN_ATM0_RHO: return o->rho0; case RCMDYN_ATM0_Z: return o->z0;
+    case RCMDYN_DPRDDX: return o->dprddx; case RCMDYN_DPRDDY: return o->dprddy;
+    case RCMDYN_ATM1_W: *nk = o->kz + 1; return o->a1w;
+    case RCMDYN_ATM2_W: *nk = o->kz + 1; return o->a2w;
+    case RCMDYN_XWWB_B0: *nk = o->kz + 1; return o->wwb0;
+    case RCMDYN_XWWB_BT: *nk = o->kz + 1; return o->wwbt;
+    case RCMDYN_ATM0_PF: *nk = o->kz + 1; return o->pf0;
+    case RCMDYN_ATM0_RHOF: *nk = o->kz + 1; return o->rhof0;
+    case RCMDYN_ATM0_ZF: *nk = o->kz + 1; return o->zf0;
     case RCMDYN_HSTOR: *nk = o->nsplit; return o->hstor;
     default: break;
   }
@@ -419,6 +483,11 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     case RCMDYN_XPSB_B0: return o->pb0;  case RCMDYN_XPSB_BT: return o->pbt;
     case RCMDYN_PSC: return o->psc;      case RCMDYN_PTEN: return o->pten;
     case RCMDYN_PSDOTA: return o->psdota;
+    case RCMDYN_ATM0_PS: return o->ps0;
+    case RCMDYN_DPSDXM: return o->dpsdxm; case RCMDYN_DPSDYM: return o->dpsdym;
+    case RCMDYN_EF: return o->ef;   case RCMDYN_DDX: return o->ddx;   case RCMDYN_DDY: return o->ddy;
+    case RCMDYN_DMDX: return o->dmdx; case RCMDYN_DMDY: return o->dmdy;
+    case RCMDYN_EX: return o->ex;   case RCMDYN_CRX: return o->crx;   case RCMDYN_CRY: return o->cry;
     default: return NULL;
   }
 }
@@ -1449,8 +1518,958 @@ static void splitf(orc_t* o) {
   }
 }
 
+/* ======================================================================================
+ * Non-hydrostatic core (idynamic = 2): Main/mod_tendency.F90 NH branches, Main/mod_sound.F90,
+ * raydamp (Main/mod_bdycod.F90:4953-5123).  ithadv = 0, ipptls = 1 (qcd aliases atmx%qx(iqc),
+ * Main/mod_tendency.F90:117-121), i_crm = 0, physics stubbed.
+ * ====================================================================================== */
+#define NH_REARTHRAD (d_one / 6.371229e6)            /* Share/mod_constants.F90:282-284 */
+#define NH_MATHPI 3.1415926535897932384626433832795029 /* :254-255 */
+static double nh_xgamma(void) { return d_one / (d_one - c_rgas * (d_one / c_cpd)); } /* mod_sound:77 */
+
+/* surface_pressures NH (:836-848): p* is the constant reference p*; psdota/psdotb as
+ * mod_init leaves them (Main/mod_init.F90:174-178) */
+static void nh_surface_pressures(orc_t* o) {
+  psc2psd(o, o->psa, o->psdota);
+  psc2psd(o, o->psb, o->psdotb);
+  for (int i = o->ice1ga; i <= o->ice2ga; i++)
+    for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->rpsa, j, i) = d_one / A2(o->psa, j, i);
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) A2(o->rpsb, j, i) = d_one / A2(o->psb, j, i);
+  for (int i = o->ide1ga; i <= o->ide2ga; i++)
+    for (int j = o->jde1ga; j <= o->jde2ga; j++) A2(o->rpsda, j, i) = d_one / A2(o->psdota, j, i);
+}
+
+/* decouple NH additions (:1005-1008, :1041-1066, :1081-1084) */
+static void nh_decouple(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  decouple(o);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1ga; i <= o->ide2ga; i++)
+      for (int j = o->jde1ga; j <= o->jde2ga; j++) {
+        A3(o->umd, j, i, k) = A3(o->ud, j, i, k) * A2(o->msfd, j, i);
+        A3(o->vmd, j, i, k) = A3(o->vd, j, i, k) * A2(o->msfd, j, i);
+      }
+  xch(o, o->a1pp, kz, 1, 0); xch(o, o->a1w, kp, 1, 0);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A3(o->xpp, j, i, k) = A3(o->a1pp, j, i, k) * A2(o->rpsa, j, i);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A3(o->xw, j, i, k) = A3(o->a1w, j, i, k) * A2(o->rpsa, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++) {
+        A3(o->pr1, j, i, k) = A3(o->pr0, j, i, k) + A3(o->xpp, j, i, k);
+        A3(o->rho1, j, i, k) = A3(o->pr1, j, i, k) / (c_rgas * A3(o->xtv, j, i, k));
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->xpr, j, i, k) = (A3(o->xtv, j, i, k) - A3(o->t0, j, i, k) -
+                               A3(o->xpp, j, i, k) / (c_cpd * A3(o->rho0, j, i, k))) / A3(o->xt, j, i, k);
+  xch(o, o->a2pp, kz, 2, 0); xch(o, o->a2w, kp, 2, 0);
+}
+
+/* compute_omega NH (:1157-1192, :1216-1223) */
+static void nh_compute_omega(orc_t* o) {
+  int kz = o->kz;
+  memset(o->qdot, 0, sizeof(double) * o->plane * (kz + 1));
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++)
+      A2(o->dummy, j, i) = d_one / (o->dx2 * A2(o->msfx, j, i) * A2(o->msfx, j, i));
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(o->ucc, j, i, k) = A3(o->umd, j, i, k) + A3(o->umd, j, i + 1, k) + A3(o->umd, j + 1, i, k) + A3(o->umd, j + 1, i + 1, k);
+        A3(o->vcc, j, i, k) = A3(o->vmd, j, i, k) + A3(o->vmd, j, i + 1, k) + A3(o->vmd, j + 1, i, k) + A3(o->vmd, j + 1, i + 1, k);
+      }
+  for (int k = 2; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->qdot, j, i, k) = -A3(o->rhof0, j, i, k) * EGRAV * A3(o->xw, j, i, k) / A2(o->ps0, j, i) -
+            o->sigma[k] * (A2(o->dpsdxm, j, i) * (o->twt1[k] * A3(o->ucc, j, i, k) + o->twt2[k] * A3(o->ucc, j, i, k - 1)) +
+                           A2(o->dpsdym, j, i) * (o->twt1[k] * A3(o->vcc, j, i, k) + o->twt2[k] * A3(o->vcc, j, i, k - 1)));
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double a = A3(o->umc, j + 1, i + 1, k) + A3(o->umc, j + 1, i, k) - A3(o->umc, j, i + 1, k) - A3(o->umc, j, i, k);
+        double b = A3(o->vmc, j + 1, i + 1, k) + A3(o->vmc, j, i + 1, k) - A3(o->vmc, j + 1, i, k) - A3(o->vmc, j, i, k);
+        A3(o->cr, j, i, k) = (a + b) * A2(o->dummy, j, i) +
+            (A3(o->qdot, j, i, k + 1) - A3(o->qdot, j, i, k)) * A2(o->psa, j, i) / o->dsigma[k];
+      }
+  xch(o, o->cr, kz, 1, 0);
+  xch(o, o->qdot, kz + 1, 1, 0);
+  memset(o->omega, 0, sizeof(double) * o->plane * kz);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->omega, j, i, k) = -d_half * EGRAV * A3(o->rho0, j, i, k) * A2(o->rpsb, j, i) *
+                                (A3(o->a2w, j, i, k) + A3(o->a2w, j, i, k + 1));
+}
+
+/* mkslice NH subset the dyn core reads (Main/mod_slice.F90:163-183, 215-238, 278-281) */
+static void nh_mkslice(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  mkslice(o);                              /* ubd, vbd, tb3d, qb3d (pb3d/pf3d overwritten below) */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1gb; i <= o->ice2gb; i++)
+      for (int j = o->jce1gb; j <= o->jce2gb; j++)
+        A3(o->ppb3d, j, i, k) = A3(o->a2pp, j, i, k) * A2(o->srpsb, j, i);
+  for (int k = 2; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->pb3d, j, i, k) = A3(o->pr0, j, i, k) + A3(o->ppb3d, j, i, k);
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) {
+      A3(o->pb3d, j, i, 1) = dmax(A3(o->pr0, j, i, 1) + A3(o->ppb3d, j, i, 1), o->ptop * d_1000 + 1.0);
+      double ps2d = A2(o->ps0, j, i) + o->ptop * d_1000 + A3(o->ppb3d, j, i, kz);
+      A3(o->pf3d, j, i, 1) = o->ptop * d_1000;
+      A3(o->pf3d, j, i, kp) = ps2d;
+    }
+  for (int k = 2; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(o->pf3d, j, i, k) = A3(o->pf0, j, i, k) + d_half * (A3(o->ppb3d, j, i, k - 1) + A3(o->ppb3d, j, i, k));
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ice1gb; i <= o->ice2gb; i++)
+      for (int j = o->jce1gb; j <= o->jce2gb; j++)
+        A3(o->wb3d, j, i, k) = A3(o->a2w, j, i, k) * A2(o->srpsb, j, i);
+}
+
+/* calc_coeff NH (Main/mod_diffusion.F90:215-250) */
+static void nh_calc_coeff(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  memset(o->xkc, 0, sizeof(double) * o->plane * kz);
+  memset(o->xkd, 0, sizeof(double) * o->plane * kz);
+  memset(o->xkcf, 0, sizeof(double) * o->plane * kp);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double dudx = A3(o->ubd, j + 1, i, k) + A3(o->ubd, j + 1, i + 1, k) - A3(o->ubd, j, i, k) - A3(o->ubd, j, i + 1, k);
+        double dvdx = A3(o->vbd, j + 1, i, k) + A3(o->vbd, j + 1, i + 1, k) - A3(o->vbd, j, i, k) - A3(o->vbd, j, i + 1, k);
+        double dudy = A3(o->ubd, j, i + 1, k) + A3(o->ubd, j + 1, i + 1, k) - A3(o->ubd, j, i, k) - A3(o->ubd, j + 1, i, k);
+        double dvdy = A3(o->vbd, j, i + 1, k) + A3(o->vbd, j + 1, i + 1, k) - A3(o->vbd, j, i, k) - A3(o->vbd, j + 1, i, k);
+        double dwdz = A3(o->wb3d, j, i, k) - A3(o->wb3d, j, i, k + 1);
+        double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
+        A3(o->xkc, j, i, k) = dmin(A2(o->hgfact, j, i) + o->dydc * duv, o->xkhmax);
+      }
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) A3(o->xkcf, j, i, 1) = A3(o->xkc, j, i, 1);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->xkcf, j, i, k + 1) = A3(o->xkc, j, i, k);
+  xch(o, o->xkc, kz, 1, 0);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++)
+        A3(o->xkd, j, i, k) = d_rfour * (A3(o->xkc, j, i, k) + A3(o->xkc, j - 1, i - 1, k) +
+                                         A3(o->xkc, j - 1, i, k) + A3(o->xkc, j, i - 1, k));
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->xkc, j, i, k) = A3(o->xkc, j, i, k) * o->rdxsq * A2(o->psb, j, i);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->xkcf, j, i, k) = A3(o->xkcf, j, i, k) * o->rdxsq * A2(o->psb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++)
+        A3(o->xkd, j, i, k) = A3(o->xkd, j, i, k) * o->rdxsq * A2(o->psdotb, j, i);
+}
+
+/* hadvuv NH upstream branch (Main/mod_advection.F90:235-264): flux form minus u*divergence */
+static void nh_hadvuv(orc_t* o) {
+  const double* ua = o->umc; const double* va = o->vmc;
+  const double* u = o->ud; const double* v = o->vd;
+  double ul = o->ul;
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double divd = d_rfour * (A3(o->cr, j, i, k) + A3(o->cr, j, i - 1, k) + A3(o->cr, j - 1, i, k) + A3(o->cr, j - 1, i - 1, k));
+        double ucmona = A3(ua, j, i + 1, k) + d_two * A3(ua, j, i, k) + A3(ua, j, i - 1, k);
+        double ucmonb = A3(ua, j + 1, i + 1, k) + d_two * A3(ua, j + 1, i, k) + A3(ua, j + 1, i - 1, k);
+        double ucmonc = A3(ua, j - 1, i + 1, k) + d_two * A3(ua, j - 1, i, k) + A3(ua, j - 1, i - 1, k);
+        double vcmona = A3(va, j + 1, i, k) + d_two * A3(va, j, i, k) + A3(va, j - 1, i, k);
+        double vcmonb = A3(va, j + 1, i + 1, k) + d_two * A3(va, j, i + 1, k) + A3(va, j - 1, i + 1, k);
+        double vcmonc = A3(va, j + 1, i - 1, k) + d_two * A3(va, j, i - 1, k) + A3(va, j - 1, i - 1, k);
+        double dm = A2(o->dmsf, j, i);
+        double diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc));
+        double ff1 = ul * (A3(u, j + 1, i, k) + A3(u, j, i, k));
+        double ff2 = ul * (A3(u, j - 1, i, k) + A3(u, j, i, k));
+        double ff3 = ul * (A3(v, j, i + 1, k) + A3(v, j, i, k));
+        double ff4 = ul * (A3(v, j, i - 1, k) + A3(v, j, i, k));
+        ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+        ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+        vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+        vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A3(u, j, i, k) * diag - dm *
+            (A3(u, j + 1, i, k) * ucmonb - A3(u, j - 1, i, k) * ucmonc + A3(u, j, i + 1, k) * vcmonb - A3(u, j, i - 1, k) * vcmonc);
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) + A3(v, j, i, k) * diag - dm *
+            (A3(v, j + 1, i, k) * ucmonb - A3(v, j - 1, i, k) * ucmonc + A3(v, j, i + 1, k) * vcmonb - A3(v, j, i - 1, k) * vcmonc);
+      }
+}
+
+/* hadv3d ind = 1 upstream (Main/mod_advection.F90:486-507): w on full levels 2..kz */
+static void nh_hadv3d_w(orc_t* o, const double* f, double* ften) {
+  double ul = o->ul;
+  for (int k = 2; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double t1 = o->twt1[k], t2 = o->twt2[k];
+        double uaz1 = (t1 * A3(o->uavg1, j, i, k) + t2 * A3(o->uavg1, j, i, k - 1));
+        double uaz2 = (t1 * A3(o->uavg2, j, i, k) + t2 * A3(o->uavg2, j, i, k - 1));
+        double vaz1 = (t1 * A3(o->vavg1, j, i, k) + t2 * A3(o->vavg1, j, i, k - 1));
+        double vaz2 = (t1 * A3(o->vavg2, j, i, k) + t2 * A3(o->vavg2, j, i, k - 1));
+        double ps = A2(o->psa, j, i);
+        double f1 = d_half * ul * (A3(o->uavg2, j, i, k) + A3(o->uavg1, j, i, k)) / ps;
+        double f2 = d_half * ul * (A3(o->vavg2, j, i, k) + A3(o->vavg1, j, i, k)) / ps;
+        double fx1 = (d_one + f1) * A3(f, j - 1, i, k) + (d_one - f1) * A3(f, j, i, k);
+        double fx2 = (d_one + f1) * A3(f, j, i, k) + (d_one - f1) * A3(f, j + 1, i, k);
+        double fy1 = (d_one + f2) * A3(f, j, i - 1, k) + (d_one - f2) * A3(f, j, i, k);
+        double fy2 = (d_one + f2) * A3(f, j, i, k) + (d_one - f2) * A3(f, j, i + 1, k);
+        A3(ften, j, i, k) = A3(ften, j, i, k) - A2(o->xmsf, j, i) * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
+      }
+}
+
+/* vadv3d ind = 0 (Main/mod_advection.F90:744-766): pp (nk = kz) and w (nk = kz+1) */
+static void nh_vadv3d_lin(orc_t* o, const double* f, double* ften, int full) {
+  int kz = o->kz;
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) {
+      if (!full) {
+        for (int k = 2; k <= kz; k++) {
+          double fx = A3(o->qdot, j, i, k) * (o->twt1[k] * A3(f, j, i, k) + o->twt2[k] * A3(f, j, i, k - 1));
+          A3(ften, j, i, k - 1) = A3(ften, j, i, k - 1) - fx * o->xds[k - 1];
+          A3(ften, j, i, k) = A3(ften, j, i, k) + fx * o->xds[k];
+        }
+      } else {
+        for (int k = 1; k <= kz; k++) {
+          double qq = d_half * (A3(o->qdot, j, i, k) + A3(o->qdot, j, i, k + 1));
+          double fx = qq * ((A3(f, j, i, k) + A3(f, j, i, k + 1)));
+          A3(ften, j, i, k + 1) = A3(ften, j, i, k + 1) + fx * o->dds[k + 1];
+          A3(ften, j, i, k) = A3(ften, j, i, k) - fx * o->dds[k];
+        }
+      }
+    }
+}
+
+/* vadv3d ind = 1, non-hydrostatic form (Main/mod_advection.F90:784-803) */
+static void nh_vadv3d_t(orc_t* o) {
+  const double* f = o->a1t;
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) {
+      double rdphf = exp(-c_c287 * log(A3(o->pb3d, j, i, 1)));
+      A3(o->dotqdot, j, i, 1) = A3(f, j, i, 1) * rdphf;
+    }
+  for (int k = 2; k <= o->kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double rdphf = exp(-c_c287 * log(A3(o->pb3d, j, i, k)));
+        double rdplf = exp(c_c287 * log(A3(o->pf3d, j, i, k)));
+        A3(o->dotqdot, j, i, k) = A3(f, j, i, k) * rdphf;
+        double fx = rdplf * A3(o->qdot, j, i, k) *
+                    (o->twt1[k] * A3(o->dotqdot, j, i, k) + o->twt2[k] * A3(o->dotqdot, j, i, k - 1));
+        A3(o->tdyn, j, i, k - 1) = A3(o->tdyn, j, i, k - 1) - fx * o->xds[k - 1];
+        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + fx * o->xds[k];
+      }
+}
+
+/* advection NH (Main/mod_tendency.F90:1270-1392) */
+static void nh_advection(orc_t* o) {
+  start_advect(o);
+  nh_hadvuv(o);
+  vadvuv(o);
+  hadv_scalar(o, o->xpp, o->ppdyn, 0);        /* hadv3d ind = 0 */
+  nh_vadv3d_lin(o, o->a1pp, o->ppdyn, 0);
+  nh_hadv3d_w(o, o->xw, o->wdyn);
+  nh_vadv3d_lin(o, o->a1w, o->wdyn, 1);
+  hadv_scalar(o, o->xt, o->tdyn, 1);          /* hadvt */
+  nh_vadv3d_t(o);
+  hadv_scalar(o, o->xq[0], o->qdyn[0], 2);
+  vadvqv(o);
+  hadv_scalar(o, o->xq[1], o->qdyn[1], 0);
+  vadv4d_qc(o);
+}
+
+/* curvature NH (:1839-1879) */
+static void nh_curvature(orc_t* o) {
+  for (int k = 1; k <= o->kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double wadot = 0.125 * (A3(o->a1w, j - 1, i - 1, k) + A3(o->a1w, j - 1, i, k) +
+                                A3(o->a1w, j, i - 1, k) + A3(o->a1w, j, i, k));
+        double wadotp1 = 0.125 * (A3(o->a1w, j - 1, i - 1, k + 1) + A3(o->a1w, j - 1, i, k + 1) +
+                                  A3(o->a1w, j, i - 1, k + 1) + A3(o->a1w, j, i, k + 1));
+        double wabar = wadot + wadotp1;
+        double amfac = wabar * A2(o->rpsda, j, i) * NH_REARTHRAD;
+        double uc = A3(o->uc, j, i, k), vc = A3(o->vc, j, i, k);
+        double duv = uc * A2(o->dmdy, j, i) - vc * A2(o->dmdx, j, i);
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A2(o->coriol, j, i) * vc -
+            A2(o->ef, j, i) * A2(o->ddx, j, i) * wabar + A3(o->vmd, j, i, k) * duv - uc * amfac;
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) - A2(o->coriol, j, i) * uc +
+            A2(o->ef, j, i) * A2(o->ddy, j, i) * wabar - A3(o->umd, j, i, k) * duv - vc * amfac;
+      }
+}
+
+/* adiabatic NH (:1581-1593, 1612-1671), ithadv = 0, ipptls > 0 */
+static void nh_adiabatic(orc_t* o) {
+  int kz = o->kz;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double cpm = c_cpd * (d_one + 0.80 * A3(o->xq[0], j, i, k));
+        double scr1 = d_half * EGRAV * A3(o->rho0, j, i, k) * (A3(o->a1w, j, i, k) + A3(o->a1w, j, i, k + 1));
+        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + A3(o->xt, j, i, k) * A3(o->cr, j, i, k) -
+            (scr1 + A3(o->ppdyn, j, i, k) + A3(o->ppten, j, i, k) + A3(o->xpp, j, i, k) * A3(o->cr, j, i, k)) /
+            (A3(o->rho1, j, i, k) * cpm);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->ppdyn, j, i, k) = A3(o->ppdyn, j, i, k) + A3(o->xpp, j, i, k) * A3(o->cr, j, i, k);
+  for (int n = 0; n < 2; n++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->qdyn[n], j, i, k) = A3(o->qdyn[n], j, i, k) + A3(o->xq[n], j, i, k) * A3(o->cr, j, i, k);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(o->ucc, j, i, k) = A3(o->uc, j, i, k) + A3(o->uc, j, i + 1, k) + A3(o->uc, j + 1, i, k) + A3(o->uc, j + 1, i + 1, k);
+        A3(o->vcc, j, i, k) = A3(o->vc, j, i, k) + A3(o->vc, j, i + 1, k) + A3(o->vc, j + 1, i, k) + A3(o->vc, j + 1, i + 1, k);
+      }
+  for (int k = 2; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double rofac = (o->dsigma[k - 1] * A3(o->rho0, j, i, k) + o->dsigma[k] * A3(o->rho0, j, i, k - 1)) /
+                       (o->dsigma[k - 1] * A3(o->rho1, j, i, k) + o->dsigma[k] * A3(o->rho1, j, i, k - 1));
+        double uaq = d_rfour * (o->twt1[k] * A3(o->ucc, j, i, k) + o->twt2[k] * A3(o->ucc, j, i, k - 1));
+        double vaq = d_rfour * (o->twt1[k] * A3(o->vcc, j, i, k) + o->twt2[k] * A3(o->vcc, j, i, k - 1));
+        A3(o->wdyn, j, i, k) = A3(o->wdyn, j, i, k) +
+            (o->twt2[k] * A3(o->xpr, j, i, k - 1) + o->twt1[k] * A3(o->xpr, j, i, k)) * rofac * EGRAV * A2(o->psa, j, i) +
+            A2(o->ex, j, i) * (uaq * A2(o->crx, j, i) - vaq * A2(o->cry, j, i)) +
+            (uaq * uaq + vaq * vaq) * NH_REARTHRAD * A2(o->rpsa, j, i) +
+            A3(o->xw, j, i, k) * (o->twt1[k] * A3(o->cr, j, i, k) + o->twt2[k] * A3(o->cr, j, i, k - 1));
+      }
+  for (int k = 2; k <= kz; k++)                 /* water loading, qcd = atmx%qx(iqc) */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->wdyn, j, i, k) = A3(o->wdyn, j, i, k) - EGRAV * A2(o->psa, j, i) *
+            (o->twt2[k] * A3(o->xq[1], j, i, k - 1) + o->twt1[k] * A3(o->xq[1], j, i, k));
+}
+
+/* nudge3d on nk levels (Main/mod_bdycod.F90:4218-4406; hefc(ib, min(k,kz)) for kz+1) */
+static void nh_nudge3d(orc_t* o, const double* f, const double* b0, const double* bt, double* ften, int nk) {
+  double xt = o->xbctime + o->dt;
+  for (int k = 1; k <= nk; k++)
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A3(o->fg1, j, i, k) = (A3(b0, j, i, k) + xt * A3(bt, j, i, k)) - A3(f, j, i, k);
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= nk; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          double xf, xg; nudge_coef(o, A2(o->ib_cr, j, i), (k < o->kz) ? k : o->kz, &xf, &xg);
+          A3(ften, j, i, k) = relax(A3(ften, j, i, k), xf, xg, A3(o->fg1, j, i, k),
+              A3(o->fg1, j - 1, i, k), A3(o->fg1, j + 1, i, k), A3(o->fg1, j, i - 1, k), A3(o->fg1, j, i + 1, k));
+        }
+}
+
+/* sponge3d on nk levels (Main/mod_bdycod.F90:2926-2994) */
+static void nh_sponge3d(orc_t* o, const double* bt, double* ften, int nk) {
+  for (int r = 1; r <= 4; r++)
+    for (int k = 1; k <= nk; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          if (A2(o->rg_cr, j, i) != r) continue;
+          int ib = A2(o->ib_cr, j, i);
+          A3(ften, j, i, k) = o->wgtx[ib] * A3(ften, j, i, k) + (d_one - o->wgtx[ib]) * A3(bt, j, i, k);
+        }
+}
+
+/* diffu_x3d / diffu_x3df on nk levels with coefficient xk (Main/mod_diffusion.F90:523-790) */
+static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* xk, int nk) {
+  if (o->cfg.idiffu == 2) {
+    for (int k = 1; k <= nk; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(ften, j, i, k) = A3(ften, j, i, k) + d_one * A3(xk, j, i, k) *
+              (o4_c1 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
+               o4_c2 * (A3(f, j + 1, i + 1, k) + A3(f, j - 1, i - 1, k) + A3(f, j - 1, i + 1, k) + A3(f, j + 1, i - 1, k)) +
+               o4_c3 * A3(f, j, i, k));
+    return;
+  }
+  for (int k = 1; k <= nk; k++)
+    for (int i = o->icii1; i <= o->icii2; i++)
+      for (int j = o->jcii1; j <= o->jcii2; j++)
+        A3(ften, j, i, k) = A3(ften, j, i, k) - d_one * A3(xk, j, i, k) *
+            (z4_c1 * (A3(f, j + 2, i, k) + A3(f, j - 2, i, k) + A3(f, j, i + 2, k) + A3(f, j, i - 2, k)) +
+             z4_c2 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
+             z4_c3 * A3(f, j, i, k));
+#define LAP2(J, I) \
+  A3(ften, J, I, k) = A3(ften, J, I, k) + d_one * A3(xk, J, I, k) * \
+      (z4_c1 * (A3(f, (J) + 1, I, k) + A3(f, (J) - 1, I, k) + A3(f, J, (I) + 1, k) + A3(f, J, (I) - 1, k)) + \
+       z4_c2 * A3(f, J, I, k))
+  if (o->bl) for (int k = 1; k <= nk; k++) for (int i = o->ici1; i <= o->ici2; i++) LAP2(o->jci1, i);
+  if (o->br) for (int k = 1; k <= nk; k++) for (int i = o->ici1; i <= o->ici2; i++) LAP2(o->jci2, i);
+  if (o->bb) for (int k = 1; k <= nk; k++) for (int j = o->jci1; j <= o->jci2; j++) LAP2(j, o->ici1);
+  if (o->bt) for (int k = 1; k <= nk; k++) for (int j = o->jci1; j <= o->jci2; j++) LAP2(j, o->ici2);
+#undef LAP2
+}
+
+/* tau, Main/mod_bdycod.F90:5115-5123 */
+static double nh_tau(orc_t* o, double z, double zmax) {
+  double rayhd = o->cfg.rayhd;
+  if (z > zmax - rayhd) {
+    double s = sin((NH_MATHPI * d_half) * (d_one - (zmax - z) / rayhd));
+    return o->cfg.rayalpha0 * (s * s);
+  }
+  return d_zero;
+}
+
+/* raydamp3 / raydampqv (cross, coupled bounds) and raydamp3f (toward 0), :5021-5085 */
+static void nh_raydamp_x(orc_t* o, const double* z, const double* var, double* vten,
+                         const double* b0, const double* bt, int nk) {
+  double xt = o->xbctime + o->dt;
+  int kmax = (nk < o->cfg.rayndamp) ? nk : o->cfg.rayndamp;
+  for (int k = 1; k <= kmax; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double bval = b0 ? (A3(b0, j, i, k) + xt * A3(bt, j, i, k)) : d_zero;
+        A3(vten, j, i, k) = A3(vten, j, i, k) + nh_tau(o, A3(z, j, i, k), A3(z, j, i, 1)) * (bval - A3(var, j, i, k));
+      }
+}
+
+/* raydampuv (dot points, z averaged from the four cross neighbours), :4953-4983 */
+static void nh_raydamp_uv(orc_t* o) {
+  double xt = o->xbctime + o->dt;
+  const double* z = o->z0;
+  int kmax = (o->kz < o->cfg.rayndamp) ? o->kz : o->cfg.rayndamp;
+  for (int pass = 0; pass < 2; pass++) {
+    const double* b0 = pass ? o->vb0 : o->ub0; const double* bt = pass ? o->vbt : o->ubt;
+    const double* var = pass ? o->a2v : o->a2u; double* ten = pass ? o->vten : o->uten;
+    for (int k = 1; k <= kmax; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          double bval = A3(b0, j, i, k) + xt * A3(bt, j, i, k);
+          double zz = d_rfour * (A3(z, j, i, k) + A3(z, j - 1, i, k) + A3(z, j, i - 1, k) + A3(z, j - 1, i - 1, k));
+          double zm = d_rfour * (A3(z, j, i, 1) + A3(z, j - 1, i, 1) + A3(z, j, i - 1, 1) + A3(z, j - 1, i - 1, 1));
+          A3(ten, j, i, k) = A3(ten, j, i, k) + nh_tau(o, zz, zm) * (bval - A3(var, j, i, k));
+        }
+  }
+}
+
+/* upper radiative boundary coefficients, Main/mod_sound.F90:500-543 (computed on the
+ * day alarm at the first acoustic step) */
+static void nh_tmask(orc_t* o, const double* rpsb) {
+  double fi[13], fk[7];
+  for (int n = 0; n < 13; n++) fi[n] = d_one;
+  fi[0] = d_half; fi[12] = d_half;
+  for (int n = 1; n <= 5; n++) fk[n] = d_two;
+  fk[0] = d_one; fk[6] = d_one;
+  double atot = d_zero, rhontot = d_zero;
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) {
+      atot = atot + A2(o->astore, j, i);
+      double ensq = EGRAV * EGRAV / c_cpd / (A3(o->a2t, j, i, 1) * A2(rpsb, j, i));
+      rhontot = rhontot + A3(o->rho1, j, i, 1) * sqrt(ensq);
+    }
+  double rnpts = d_one / (double)((o->iy - 3) * (o->jx - 3));
+  double abar = atot * rnpts, rhon = rhontot * rnpts;
+  double dxmsfb = d_two / o->dxsq / o->cfg.nh_xmsf;
+  memset(o->tmask, 0, sizeof(o->tmask));
+  for (int kk = 0; kk <= 6; kk++) {
+    double rkk = (double)kk;
+    for (int ll = 0; ll <= 6; ll++) {
+      double rll = (double)ll;
+      double xkeff = dxmsfb * sin(NH_MATHPI * rkk / 12.0) * cos(NH_MATHPI * rll / 12.0);
+      double xleff = dxmsfb * sin(NH_MATHPI * rll / 12.0) * cos(NH_MATHPI * rkk / 12.0);
+      double xkleff = sqrt(xkeff * xkeff + xleff * xleff);
+      for (int ii = -6; ii <= 6; ii++) {
+        double ri = (double)ii;
+        for (int jj = -6; jj <= 6; jj++) {
+          double rj = (double)jj;
+          o->tmask[jj + 6][ii + 6] = o->tmask[jj + 6][ii + 6] +
+              (fi[ii + 6] * fi[jj + 6] * fk[kk] * fk[ll]) / 144.0 *
+              cos(2.0 * NH_MATHPI * rkk * ri / 12.0) * cos(2.0 * NH_MATHPI * rll * rj / 12.0) *
+              xkleff / (rhon - abar * xkleff);
+        }
+      }
+    }
+  }
+  o->tmask_valid = 1;
+}
+
+/* sound, Main/mod_sound.F90:163-718 */
+static int nh_sound(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  const double xgamma = nh_xgamma();
+  double dt = o->dt;
+  int istep = (int)(dt / o->cfg.nh_dtsmax);
+  if (istep < 2) istep = 2;
+  if (o->lcount > 0 && istep < 4) istep = 4;
+  o->nh_istep = istep;
+  double dts = dt / (double)istep;
+  double bet = o->cfg.nhbet, xkd = o->cfg.nhxkd;
+  double bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
+  double bpxbp = bp * bp, bpxbm = bp * bm;
+  double* rpsb = o->srpsb;                     /* sound's own 1/psb (same values) */
+  double* cu = o->cu; double* cv = o->cv;
+  double* pp = o->cpp; double* w = o->cw;
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++) A2(rpsb, j, i) = d_one / A2(o->psb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(cu, j, i, k) = A3(o->a2u, j, i, k) / A2(o->psdotb, j, i);
+        A3(cv, j, i, k) = A3(o->a2v, j, i, k) / A2(o->psdotb, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) * dts;
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) * dts;
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->cq[0], j, i, k) = A3(o->a2q[0], j, i, k) * A2(rpsb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A3(pp, j, i, k) = A3(o->a2pp, j, i, k) * A2(rpsb, j, i);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) * dts;
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A3(w, j, i, k) = A3(o->a2w, j, i, k) * A2(rpsb, j, i);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->wten, j, i, k) = A3(o->wten, j, i, k) * dts;
+  /* day alarm (Main/mpplib/mod_timer.F90:306-337): acts at the start and at the first step
+   * whose start time reaches the next multiple of a day */
+  double tnow = (double)o->lcount * o->dtsec;
+  int day_alarm = (o->lcount == 0) || !o->tmask_valid ||
+                  (floor(tnow / 86400.0) != floor((tnow - o->dtsec) / 86400.0));
+  double cflmax = d_zero;
+  double* e = o->s_e; double* f = o->s_f; double* wo = o->s_wo; double* spi = o->s_pi;
+  double *aa = o->s_aa, *b = o->s_b, *c = o->s_c, *rhs = o->s_rhs, *ca = o->s_ca, *g1 = o->s_g1, *g2 = o->s_g2;
+  double *ptend = o->s_ptend, *pxup = o->s_pxup, *pyvp = o->s_pyvp, *tk = o->s_tk, *cc = o->s_cc;
+  double *cdd = o->s_cdd, *cj = o->s_cj;
+  for (int it = 1; it <= istep; it++) {
+    if (it > 1)
+      for (int k = 1; k <= kz; k++)
+        for (int i = o->ici1; i <= o->ici2; i++)
+          for (int j = o->jci1; j <= o->jci2; j++) A3(pp, j, i, k) = A3(pp, j, i, k) + xkd * A3(spi, j, i, k);
+    for (int k = 1; k <= kz; k++) {
+      int kp1 = (kz < k + 1) ? kz : k + 1, km1 = (1 > k - 1) ? 1 : k - 1;
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++)
+          A3(o->cdt, j, i, k) = (A3(pp, j, i, km1) - A3(pp, j, i, kp1)) / (A3(o->pr0, j, i, km1) - A3(o->pr0, j, i, kp1));
+    }
+    xch(o, o->cdt, kz, 1, 0); xch(o, pp, kz, 1, 0);
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          double rho = d_rfour * (A3(o->rho1, j, i, k) + A3(o->rho1, j - 1, i, k) + A3(o->rho1, j, i - 1, k) + A3(o->rho1, j - 1, i - 1, k));
+          double dppdp0 = d_rfour * (A3(o->cdt, j, i, k) + A3(o->cdt, j - 1, i, k) + A3(o->cdt, j, i - 1, k) + A3(o->cdt, j - 1, i - 1, k));
+          double chh = d_half * dts / (rho * o->dx) / A2(o->msfd, j, i);
+          A3(cu, j, i, k) = A3(cu, j, i, k) - chh * (A3(pp, j, i, k) - A3(pp, j - 1, i, k) + A3(pp, j, i - 1, k) -
+                                                     A3(pp, j - 1, i - 1, k) - A3(o->dprddx, j, i, k) * dppdp0);
+          A3(cv, j, i, k) = A3(cv, j, i, k) - chh * (A3(pp, j, i, k) - A3(pp, j, i - 1, k) + A3(pp, j - 1, i, k) -
+                                                     A3(pp, j - 1, i - 1, k) - A3(o->dprddy, j, i, k) * dppdp0);
+        }
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++)
+        for (int j = o->jdi1; j <= o->jdi2; j++) {
+          A3(cu, j, i, k) = A3(cu, j, i, k) + A3(o->uten, j, i, k);
+          A3(cv, j, i, k) = A3(cv, j, i, k) + A3(o->vten, j, i, k);
+        }
+    xch(o, cu, kz, 1, 0); xch(o, cv, kz, 1, 0);
+    if (it > 1)
+      for (int k = 1; k <= kz; k++)
+        for (int i = o->ici1; i <= o->ici2; i++)
+          for (int j = o->jci1; j <= o->jci2; j++) A3(pp, j, i, k) = A3(pp, j, i, k) - xkd * A3(spi, j, i, k);
+    for (int k = 1; k <= kp; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) A3(wo, j, i, k) = A3(w, j, i, k);
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(w, j, i, kp) = d_half * d_rfour * c_regrav *
+            ((A3(cv, j, i + 1, kz) + A3(cv, j, i, kz) + A3(cv, j + 1, i + 1, kz) + A3(cv, j + 1, i, kz)) *
+                 (A2(o->ht, j, i + 1) - A2(o->ht, j, i - 1)) +
+             (A3(cu, j, i + 1, kz) + A3(cu, j, i, kz) + A3(cu, j + 1, i + 1, kz) + A3(cu, j + 1, i, kz)) *
+                 (A2(o->ht, j + 1, i) - A2(o->ht, j - 1, i))) /
+            (o->dx * A2(o->msfx, j, i));
+        A3(e, j, i, kz) = d_zero;
+        A3(f, j, i, kz) = A3(w, j, i, kp);
+      }
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double pr1 = A3(o->pr1, j, i, 1), rho0 = A3(o->rho0, j, i, 1), ps0 = A2(o->ps0, j, i);
+        A3(cc, j, i, 1) = xgamma * pr1 * dts / (o->dx * A2(o->msfx, j, i));
+        A3(cdd, j, i, 1) = xgamma * pr1 * rho0 * EGRAV * dts / (ps0 * o->dsigma[1]);
+        A3(cj, j, i, 1) = d_half * rho0 * EGRAV * dts;
+        A3(pxup, j, i, 1) = 0.0625 * (A3(o->pr0, j + 1, i, 1) - A3(o->pr0, j - 1, i, 1)) *
+            (A3(cu, j, i, 1) + A3(cu, j + 1, i, 1) + A3(cu, j, i + 1, 1) + A3(cu, j + 1, i + 1, 1) -
+             A3(cu, j, i, 2) - A3(cu, j + 1, i, 2) - A3(cu, j, i + 1, 2) - A3(cu, j + 1, i + 1, 2)) /
+            (A3(o->pr0, j, i, 1) - A3(o->pr0, j, i, 2));
+        A3(pyvp, j, i, 1) = 0.0625 * (A3(o->pr0, j, i + 1, 1) - A3(o->pr0, j, i - 1, 1)) *
+            (A3(cv, j, i, 1) + A3(cv, j + 1, i, 1) + A3(cv, j, i + 1, 1) + A3(cv, j + 1, i + 1, 1) -
+             A3(cv, j, i, 2) - A3(cv, j + 1, i, 2) - A3(cv, j, i + 1, 2) - A3(cv, j + 1, i + 1, 2)) /
+            (A3(o->pr0, j, i, 1) - A3(o->pr0, j, i, 2));
+        A3(ptend, j, i, 1) = A3(o->ppten, j, i, 1) - d_half * A3(cc, j, i, 1) *
+            ((A3(cv, j, i + 1, 1) * A2(o->msfd, j, i + 1) - A3(cv, j, i, 1) * A2(o->msfd, j, i) +
+              A3(cv, j + 1, i + 1, 1) * A2(o->msfd, j + 1, i + 1) - A3(cv, j + 1, i, 1) * A2(o->msfd, j + 1, i) +
+              A3(cu, j + 1, i, 1) * A2(o->msfd, j + 1, i) - A3(cu, j, i, 1) * A2(o->msfd, j, i) +
+              A3(cu, j + 1, i + 1, 1) * A2(o->msfd, j + 1, i + 1) - A3(cu, j, i + 1, 1) * A2(o->msfd, j, i + 1)) /
+                 A2(o->msfx, j, i) - d_two * (A3(pyvp, j, i, 1) + A3(pxup, j, i, 1)));
+        A3(tk, j, i, 1) = (d_half * ps0 * A3(o->t0, j, i, 1)) /
+                          (xgamma * A3(o->pr0, j, i, 1) * A3(o->a2t, j, i, 1) * A2(rpsb, j, i));
+      }
+    for (int k = 2; k <= kz; k++) {
+      int kp1 = (k + 1 < kz) ? k + 1 : kz, km1 = k - 1;
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double ps0 = A2(o->ps0, j, i);
+          A3(tk, j, i, k) = (d_half * ps0 * A3(o->t0, j, i, k)) /
+                            (xgamma * A3(o->pr0, j, i, k) * A3(o->a2t, j, i, k) * A2(rpsb, j, i));
+          double rofac = (o->dsigma[km1] * A3(o->rho0, j, i, k) + o->dsigma[k] * A3(o->rho0, j, i, km1)) /
+                         (o->dsigma[km1] * A3(o->rho1, j, i, k) + o->dsigma[k] * A3(o->rho1, j, i, km1));
+          A3(cc, j, i, k) = xgamma * A3(o->pr1, j, i, k) * dts / (o->dx * A2(o->msfx, j, i));
+          A3(cdd, j, i, k) = xgamma * A3(o->pr1, j, i, k) * A3(o->rho0, j, i, k) * EGRAV * dts / (ps0 * o->dsigma[k]);
+          A3(cj, j, i, k) = d_half * A3(o->rho0, j, i, k) * EGRAV * dts;
+          A3(ca, j, i, k) = EGRAV * dts / (A3(o->pr0, j, i, k) - A3(o->pr0, j, i, km1)) * rofac;
+          A3(g1, j, i, k) = d_one - o->dsigma[km1] * A3(tk, j, i, k);
+          A3(g2, j, i, k) = d_one + o->dsigma[k] * A3(tk, j, i, km1);
+          A3(c, j, i, k) = -A3(ca, j, i, k) * (A3(cdd, j, i, km1) - A3(cj, j, i, km1)) * A3(g2, j, i, k) * bpxbp;
+          A3(b, j, i, k) = d_one + A3(ca, j, i, k) * (A3(g1, j, i, k) * (A3(cdd, j, i, k) - A3(cj, j, i, k)) +
+                                                      A3(g2, j, i, k) * (A3(cdd, j, i, km1) + A3(cj, j, i, km1))) * bpxbp;
+          A3(aa, j, i, k) = -A3(ca, j, i, k) * (A3(cdd, j, i, k) + A3(cj, j, i, k)) * A3(g1, j, i, k) * bpxbp;
+          A3(pyvp, j, i, k) = 0.125 * (A3(o->pr0, j, i + 1, k) - A3(o->pr0, j, i - 1, k)) *
+              (A3(cv, j, i, km1) + A3(cv, j + 1, i, km1) + A3(cv, j, i + 1, km1) + A3(cv, j + 1, i + 1, km1) -
+               A3(cv, j, i, kp1) - A3(cv, j + 1, i, kp1) - A3(cv, j, i + 1, kp1) - A3(cv, j + 1, i + 1, kp1)) /
+              (A3(o->pr0, j, i, km1) - A3(o->pr0, j, i, kp1));
+          A3(pxup, j, i, k) = 0.125 * (A3(o->pr0, j + 1, i, k) - A3(o->pr0, j - 1, i, k)) *
+              (A3(cu, j, i, km1) + A3(cu, j + 1, i, km1) + A3(cu, j, i + 1, km1) + A3(cu, j + 1, i + 1, km1) -
+               A3(cu, j, i, kp1) - A3(cu, j + 1, i, kp1) - A3(cu, j, i + 1, kp1) - A3(cu, j + 1, i + 1, kp1)) /
+              (A3(o->pr0, j, i, km1) - A3(o->pr0, j, i, kp1));
+        }
+    }
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(pyvp, j, i, kz) = A3(pyvp, j, i, kz) * d_half;
+        A3(pxup, j, i, kz) = A3(pxup, j, i, kz) * d_half;
+      }
+    for (int k = 2; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          A3(ptend, j, i, k) = A3(o->ppten, j, i, k) - d_half * A3(cc, j, i, k) *
+              ((A3(cv, j, i + 1, k) * A2(o->msfd, j, i + 1) - A3(cv, j, i, k) * A2(o->msfd, j, i) +
+                A3(cv, j + 1, i + 1, k) * A2(o->msfd, j + 1, i + 1) - A3(cv, j + 1, i, k) * A2(o->msfd, j + 1, i) +
+                A3(cu, j + 1, i, k) * A2(o->msfd, j + 1, i) - A3(cu, j, i, k) * A2(o->msfd, j, i) +
+                A3(cu, j + 1, i + 1, k) * A2(o->msfd, j + 1, i + 1) - A3(cu, j, i + 1, k) * A2(o->msfd, j, i + 1)) /
+                   A2(o->msfx, j, i) - d_two * (A3(pyvp, j, i, k) + A3(pxup, j, i, k)));
+          double cdm = A3(cdd, j, i, k - 1), cjm = A3(cj, j, i, k - 1), cdk = A3(cdd, j, i, k), cjk = A3(cj, j, i, k);
+          double gg1 = A3(g1, j, i, k), gg2 = A3(g2, j, i, k);
+          A3(rhs, j, i, k) = A3(w, j, i, k) + A3(o->wten, j, i, k) + A3(ca, j, i, k) *
+              (bpxbm * ((cdm - cjm) * gg2 * A3(wo, j, i, k - 1) -
+                        ((cdm + cjm) * gg2 + (cdk - cjk) * gg1) * A3(wo, j, i, k) +
+                        (cdk + cjk) * gg1 * A3(wo, j, i, k + 1)) +
+               (A3(pp, j, i, k) * gg1 - A3(pp, j, i, k - 1) * gg2) +
+               (gg1 * A3(ptend, j, i, k) - gg2 * A3(ptend, j, i, k - 1)) * bp);
+        }
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          A3(spi, j, i, k) = A3(pp, j, i, k);
+          A3(pp, j, i, k) = A3(pp, j, i, k) + A3(ptend, j, i, k) +
+              (A3(cj, j, i, k) * (A3(wo, j, i, k + 1) + A3(wo, j, i, k)) +
+               A3(cdd, j, i, k) * (A3(wo, j, i, k + 1) - A3(wo, j, i, k))) * bm;
+        }
+    for (int k = kz; k >= 2; k--)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double denom = A3(aa, j, i, k) * A3(e, j, i, k) + A3(b, j, i, k);
+          A3(e, j, i, k - 1) = -A3(c, j, i, k) / denom;
+          A3(f, j, i, k - 1) = (A3(rhs, j, i, k) - A3(f, j, i, k) * A3(aa, j, i, k)) / denom;
+        }
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A2(o->wpval, j, i) = d_zero;
+    if (o->cfg.ifupr == 1) {
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double denom = (A3(cdd, j, i, 1) + A3(cj, j, i, 1)) * bp;
+          A2(o->estore, j, i) = A3(pp, j, i, 1) + A3(f, j, i, 1) * denom;
+          A2(o->astore, j, i) = denom * A3(e, j, i, 1) + (A3(cj, j, i, 1) - A3(cdd, j, i, 1)) * bp;
+        }
+      if (day_alarm && it == 1) nh_tmask(o, rpsb);
+      int ilo = 2, ihi = o->iy - 2, jlo = 2, jhi = o->jx - 2;  /* icross1+1 .. icross2-1 */
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double acc = A2(o->wpval, j, i);
+          for (int nsi = -6; nsi <= 6; nsi++) {
+            int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
+            for (int nsj = -6; nsj <= 6; nsj++) {
+              int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
+              acc = acc + A2(o->estore, jnn, inn) * o->tmask[nsj + 6][nsi + 6];
+            }
+          }
+          A2(o->wpval, j, i) = acc;
+        }
+    }
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(w, j, i, 1) = A2(o->wpval, j, i);
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        for (int k = 1; k <= kz; k++)
+          A3(w, j, i, k + 1) = A3(e, j, i, k) * A3(w, j, i, k) + A3(f, j, i, k);
+    /* zero-gradient w on the boundary cross points (:586-617) */
+    if (o->bb) {
+      for (int k = 1; k <= kp; k++) for (int j = o->jci1; j <= o->jci2; j++) A3(w, j, o->ice1, k) = A3(w, j, o->ici1, k);
+      if (o->bl) for (int k = 1; k <= kp; k++) A3(w, o->jce1, o->ice1, k) = A3(w, o->jci1, o->ici1, k);
+      if (o->br) for (int k = 1; k <= kp; k++) A3(w, o->jce2, o->ice1, k) = A3(w, o->jci2, o->ici1, k);
+    }
+    if (o->bt) {
+      for (int k = 1; k <= kp; k++) for (int j = o->jci1; j <= o->jci2; j++) A3(w, j, o->ice2, k) = A3(w, j, o->ici2, k);
+      if (o->bl) for (int k = 1; k <= kp; k++) A3(w, o->jce1, o->ice2, k) = A3(w, o->jci1, o->ici2, k);
+      if (o->br) for (int k = 1; k <= kp; k++) A3(w, o->jce2, o->ice2, k) = A3(w, o->jci2, o->ici2, k);
+    }
+    if (o->bl) for (int k = 1; k <= kp; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(w, o->jce1, i, k) = A3(w, o->jci1, i, k);
+    if (o->br) for (int k = 1; k <= kp; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(w, o->jce2, i, k) = A3(w, o->jci2, i, k);
+    /* CFL check (:622-682) */
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          A3(o->s_ucrs, j, i, k) = A3(cu, j, i, k) + A3(cu, j, i + 1, k) + A3(cu, j + 1, i, k) + A3(cu, j + 1, i + 1, k);
+          A3(o->s_vcrs, j, i, k) = A3(cv, j, i, k) + A3(cv, j, i + 1, k) + A3(cv, j + 1, i, k) + A3(cv, j + 1, i + 1, k);
+        }
+    double cfl = d_zero;
+    for (int k = kz; k >= 2; k--)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double sigdot = -A3(o->rhof0, j, i, k) * EGRAV * A3(w, j, i, k) / A2(o->ps0, j, i) -
+              o->sigma[k] * (A2(o->dpsdxm, j, i) * (o->twt1[k] * A3(o->s_ucrs, j, i, k) + o->twt2[k] * A3(o->s_ucrs, j, i, k - 1)) +
+                             A2(o->dpsdym, j, i) * (o->twt1[k] * A3(o->s_vcrs, j, i, k) + o->twt2[k] * A3(o->s_vcrs, j, i, k - 1)));
+          double check = fabs(sigdot) * dt / (o->dsigma[k] + o->dsigma[k - 1]);
+          cfl = dmax(check, cfl);
+        }
+    if (cfl > cflmax) cflmax = cfl;
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double ppold = A3(spi, j, i, k);
+          double rho0 = A3(o->rho0, j, i, k);
+          double cddtmp = xgamma * A3(o->pr1, j, i, k) * rho0 * EGRAV * dts / (A2(o->ps0, j, i) * o->dsigma[k]);
+          double cjtmp = rho0 * EGRAV * dts * d_half;
+          A3(pp, j, i, k) = A3(pp, j, i, k) +
+              (cjtmp * (A3(w, j, i, k + 1) + A3(w, j, i, k)) + cddtmp * (A3(w, j, i, k + 1) - A3(w, j, i, k))) * bp;
+          A3(spi, j, i, k) = A3(pp, j, i, k) - ppold - A3(o->ppten, j, i, k);
+          double cpm = c_cpd * (d_one + 0.80 * A3(o->cq[0], j, i, k));
+          double dpterm = A2(o->psb, j, i) * (A3(pp, j, i, k) - ppold) / (cpm * A3(o->rho1, j, i, k));
+          A3(o->a2t, j, i, k) = A3(o->a2t, j, i, k) + o->cfg.gnu1 * dpterm;
+          A3(o->a1t, j, i, k) = A3(o->a1t, j, i, k) + dpterm;
+        }
+  }
+  o->nh_cfl = cflmax;
+  /* time filters (:686-702) */
+  double g1f = o->cfg.gnu1, g2f = o->cfg.gnu2;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(cu, j, i, k) = A2(o->psdotb, j, i) * A3(cu, j, i, k);
+        A3(cv, j, i, k) = A2(o->psdotb, j, i) * A3(cv, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        double d = g1f * (A3(cu, j, i, k) + A3(o->a2u, j, i, k) - d_two * A3(o->a1u, j, i, k));
+        A3(o->a2u, j, i, k) = A3(o->a1u, j, i, k) + d;
+        A3(o->a1u, j, i, k) = A3(cu, j, i, k);
+        d = g1f * (A3(cv, j, i, k) + A3(o->a2v, j, i, k) - d_two * A3(o->a1v, j, i, k));
+        A3(o->a2v, j, i, k) = A3(o->a1v, j, i, k) + d;
+        A3(o->a1v, j, i, k) = A3(cv, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(pp, j, i, k) = A2(o->psb, j, i) * A3(pp, j, i, k);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g1f * (A3(pp, j, i, k) + A3(o->a2pp, j, i, k) - d_two * A3(o->a1pp, j, i, k));
+        A3(o->a2pp, j, i, k) = A3(o->a1pp, j, i, k) + d;
+        A3(o->a1pp, j, i, k) = A3(pp, j, i, k);
+      }
+  size_t nw = o->plane * (size_t)kp;
+  for (size_t q = 0; q < nw; q++) if (fabs(w[q]) < DLOWVAL) w[q] = d_zero;
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(w, j, i, k) = A2(o->psb, j, i) * A3(w, j, i, k);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g2f * (A3(w, j, i, k) + A3(o->a2w, j, i, k) - d_two * A3(o->a1w, j, i, k));
+        A3(o->a2w, j, i, k) = A3(o->a1w, j, i, k) + d;
+        A3(o->a1w, j, i, k) = A3(w, j, i, k);
+      }
+  for (size_t q = 0; q < nw; q++) if (fabs(o->a2w[q]) < DLOWVAL) o->a2w[q] = d_zero;
+  for (size_t q = 0; q < nw; q++) if (fabs(o->a1w[q]) < DLOWVAL) o->a1w[q] = d_zero;
+  return (cflmax > d_one) ? 1 : 0;
+}
+
+/* tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2) */
+static int nh_tend(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  size_t n3 = o->plane * (size_t)kz, n3p = o->plane * (size_t)kp;
+  nh_surface_pressures(o);
+  nh_decouple(o);
+  nh_compute_omega(o);
+  nh_mkslice(o);
+  nh_calc_coeff(o);
+  memset(o->tten, 0, n3 * 8); memset(o->tdyn, 0, n3 * 8);
+  memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
+  memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
+  for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
+  memset(o->ppten, 0, n3 * 8); memset(o->ppdyn, 0, n3 * 8);
+  memset(o->wten, 0, n3p * 8); memset(o->wdyn, 0, n3p * 8);
+  nh_advection(o);
+  nh_curvature(o);
+  nh_adiabatic(o);
+  /* boundary (:1462-1501) */
+  if (o->cfg.iboudy == 4) {
+    sponge_all(o);
+    nh_sponge3d(o, o->ppbt, o->ppten, kz);
+    nh_sponge3d(o, o->wwbt, o->wten, kp);
+  } else {
+    boundary(o);
+    nh_nudge3d(o, o->a2pp, o->ppb0, o->ppbt, o->ppdyn, kz);
+    nh_nudge3d(o, o->a2w, o->wwb0, o->wwbt, o->wdyn, kp);
+  }
+  /* diffusion (:1515-1538) */
+  diffu_d(o);
+  diffu_x(o, o->tdyn, o->tb3d, d_one);
+  diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
+  diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
+  nh_diffu_xk(o, o->ppdyn, o->ppb3d, o->xkc, kz);
+  nh_diffu_xk(o, o->wdyn, o->wb3d, o->xkcf, kp);
+  /* sums (:285-314, 332-335) */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + 0.0;
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + 0.0;
+      }
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->wten, j, i, k) = A3(o->wten, j, i, k) + A3(o->wdyn, j, i, k) + 0.0;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) + A3(o->ppdyn, j, i, k) + 0.0;
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + 0.0;
+      }
+  /* condtq (:336-350) is physics: stubbed, tphy = qxphy = 0 */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + 0.0;
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
+      }
+  if (o->cfg.ifrayd == 1) {                   /* :356-364 */
+    nh_raydamp_x(o, o->z0, o->a2t, o->tten, o->tb0, o->tbt, kz);
+    nh_raydamp_x(o, o->z0, o->a2q[0], o->qten[0], o->qb0, o->qbt, kz);
+  }
+  /* forecast t, qx (:368-393) */
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++)
+        A3(o->ct, j, i, k) = A3(o->a2t, j, i, k) + o->dt * A3(o->tten, j, i, k);
+  for (int n = 0; n < 2; n++) {
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(o->cq[n], j, i, k) = A3(o->a2q[n], j, i, k);
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->cq[n], j, i, k) = A3(o->cq[n], j, i, k) + o->dt * A3(o->qten[n], j, i, k);
+  }
+  xch(o, o->cq[0], kz, 1, 0); xch(o, o->cq[1], kz, 1, 0);
+  for (int n = 0; n < 2; n++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          if (A3(o->cq[n], j, i, k) < d_zero) {
+            double s = 0.0;
+            for (int ii = i - 1; ii <= i + 1; ii++)
+              for (int jj = j - 1; jj <= j + 1; jj++) s = s + fabs(A3(o->cq[n], jj, ii, k));
+            A3(o->cq[n], j, i, k) = 0.01 * s / 9.0;
+          }
+  for (int k = 1; k <= kz; k++)                                     /* :404-411 */
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + 0.0;
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + 0.0;
+      }
+  /* time filters t, qx (:422-427) */
+  double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g1 * (A3(o->ct, j, i, k) + A3(o->a2t, j, i, k) - d_two * A3(o->a1t, j, i, k));
+        A3(o->a2t, j, i, k) = A3(o->a1t, j, i, k) + d;
+        A3(o->a1t, j, i, k) = A3(o->ct, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g1 * (A3(o->cq[0], j, i, k) + A3(o->a2q[0], j, i, k) - d_two * A3(o->a1q[0], j, i, k));
+        A3(o->a2q[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) + beta * d, MINQQ * A2(o->psa, j, i));
+        A3(o->a1q[0], j, i, k) = dmax(A3(o->cq[0], j, i, k) + (beta - d_one) * d, MINQQ * A2(o->psb, j, i));
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = g2 * (A3(o->cq[1], j, i, k) + A3(o->a2q[1], j, i, k) - d_two * A3(o->a1q[1], j, i, k));
+        A3(o->a2q[1], j, i, k) = A3(o->a1q[1], j, i, k) + beta * d;
+        A3(o->a1q[1], j, i, k) = A3(o->cq[1], j, i, k) + (beta - d_one) * d;
+        if (A3(o->a2q[1], j, i, k) < d_zero) A3(o->a2q[1], j, i, k) = d_zero;
+        if (A3(o->a1q[1], j, i, k) < d_zero) A3(o->a1q[1], j, i, k) = d_zero;
+      }
+  /* Rayleigh damping of u, v, pp, w and decoupling of the tendencies (:466-499) */
+  if (o->cfg.ifrayd == 1) {
+    nh_raydamp_uv(o);
+    nh_raydamp_x(o, o->z0, o->a2pp, o->ppten, o->ppb0, o->ppbt, kz);
+    nh_raydamp_x(o, o->zf0, o->a2w, o->wten, NULL, NULL, kp);
+  }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) {
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) * A2(o->rpsda, j, i);
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) * A2(o->rpsda, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) * A2(o->rpsa, j, i);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->wten, j, i, k) = A3(o->wten, j, i, k) * A2(o->rpsa, j, i);
+  int err = nh_sound(o);
+  /* atm2%pr (:507-513) feeds only physics: skipped */
+  o->lcount += 1;
+  if (o->lcount == 2) o->dt = d_two * o->dtsec;
+  o->ptntot = 0; o->pt2tot = 0;
+  return err;
+}
+
 /* tend, Main/mod_tendency.F90:212-726 (hydrostatic, physics stubbed) */
 int orc_tend(orc_t* o) {
+  if (o->nh) return nh_tend(o);
   int kz = o->kz;
   size_t n3 = o->plane * (size_t)kz;
   surface_pressures(o);
@@ -1624,7 +2643,11 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce1, i, k) = A3(o->a1t, o->jce1, i, k);
       for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
         A3(o->a2q[n], o->jce1, i, k) = A3(o->a1q[n], o->jce1, i, k);
-      for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce1, i) = A2(o->psa, o->jce1, i);
+      if (o->nh) {
+        for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2pp, o->jce1, i, k) = A3(o->a1pp, o->jce1, i, k);
+        for (int k = 1; k <= kz + 1; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2w, o->jce1, i, k) = A3(o->a1w, o->jce1, i, k);
+      } else
+        for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce1, i) = A2(o->psa, o->jce1, i);
     }
     if (o->br) {
       for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
@@ -1632,7 +2655,11 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce2, i, k) = A3(o->a1t, o->jce2, i, k);
       for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
         A3(o->a2q[n], o->jce2, i, k) = A3(o->a1q[n], o->jce2, i, k);
-      for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce2, i) = A2(o->psa, o->jce2, i);
+      if (o->nh) {
+        for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2pp, o->jce2, i, k) = A3(o->a1pp, o->jce2, i, k);
+        for (int k = 1; k <= kz + 1; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2w, o->jce2, i, k) = A3(o->a1w, o->jce2, i, k);
+      } else
+        for (int i = o->ici1; i <= o->ici2; i++) A2(o->psb, o->jce2, i) = A2(o->psa, o->jce2, i);
     }
     if (o->bb) {
       for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
@@ -1640,7 +2667,11 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice1, k) = A3(o->a1t, j, o->ice1, k);
       for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
         A3(o->a2q[n], j, o->ice1, k) = A3(o->a1q[n], j, o->ice1, k);
-      for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice1) = A2(o->psa, j, o->ice1);
+      if (o->nh) {
+        for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2pp, j, o->ice1, k) = A3(o->a1pp, j, o->ice1, k);
+        for (int k = 1; k <= kz + 1; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2w, j, o->ice1, k) = A3(o->a1w, j, o->ice1, k);
+      } else
+        for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice1) = A2(o->psa, j, o->ice1);
     }
     if (o->bt) {
       for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
@@ -1648,14 +2679,20 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice2, k) = A3(o->a1t, j, o->ice2, k);
       for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
         A3(o->a2q[n], j, o->ice2, k) = A3(o->a1q[n], j, o->ice2, k);
-      for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice2) = A2(o->psa, j, o->ice2);
+      if (o->nh) {
+        for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2pp, j, o->ice2, k) = A3(o->a1pp, j, o->ice2, k);
+        for (int k = 1; k <= kz + 1; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2w, j, o->ice2, k) = A3(o->a1w, j, o->ice2, k);
+      } else
+        for (int j = o->jce1; j <= o->jce2; j++) A2(o->psb, j, o->ice2) = A2(o->psa, j, o->ice2);
     }
   }
-  /* p* and p*u, p*v boundary values, :1430-1526 */
+  /* p* and p*u, p*v boundary values, :1430-1526 (p* only for the hydrostatic core) */
+  if (!o->nh) {
   if (o->bl) for (int i = o->ici1; i <= o->ici2; i++) A2(o->psa, o->jce1, i) = A2(o->pb0, o->jce1, i) + xt * A2(o->pbt, o->jce1, i);
   if (o->br) for (int i = o->ici1; i <= o->ici2; i++) A2(o->psa, o->jce2, i) = A2(o->pb0, o->jce2, i) + xt * A2(o->pbt, o->jce2, i);
   if (o->bb) for (int j = o->jce1; j <= o->jce2; j++) A2(o->psa, j, o->ice1) = A2(o->pb0, j, o->ice1) + xt * A2(o->pbt, j, o->ice1);
   if (o->bt) for (int j = o->jce1; j <= o->jce2; j++) A2(o->psa, j, o->ice2) = A2(o->pb0, j, o->ice2) + xt * A2(o->pbt, j, o->ice2);
+  }
 #define UVB(J, I) do { \
   A3(o->a1u, J, I, k) = A3(o->ub0, J, I, k) + xt * A3(o->ubt, J, I, k); \
   A3(o->a1v, J, I, k) = A3(o->vb0, J, I, k) + xt * A3(o->vbt, J, I, k); } while (0)
@@ -1674,6 +2711,28 @@ void orc_bdyval(orc_t* o) {
   if (o->bb) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice1);
   if (o->bt) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) TQB(j, o->ice2);
 #undef TQB
+  if (o->nh) {                                                      /* :1707-1790 */
+#define PPW(J, I, JI, II) do { \
+  for (int k = 1; k <= kz; k++) A3(o->a1pp, J, I, k) = A3(o->ppb0, J, I, k) + xt * A3(o->ppbt, J, I, k); \
+  for (int k = 1; k <= kz + 1; k++) A3(o->a1w, J, I, k) = A3(o->wwb0, J, I, k) + xt * A3(o->wwbt, J, I, k); } while (0)
+    if (o->bl) {
+      for (int i = o->ici1; i <= o->ici2; i++) PPW(o->jce1, i, 0, 0);
+      for (int i = o->ici1; i <= o->ici2; i++) A3(o->a1w, o->jce1, i, 1) = A3(o->a1w, o->jci1, i, 1);
+    }
+    if (o->br) {
+      for (int i = o->ici1; i <= o->ici2; i++) PPW(o->jce2, i, 0, 0);
+      for (int i = o->ici1; i <= o->ici2; i++) A3(o->a1w, o->jce2, i, 1) = A3(o->a1w, o->jci2, i, 1);
+    }
+    if (o->bb) {
+      for (int j = o->jce1; j <= o->jce2; j++) PPW(j, o->ice1, 0, 0);
+      for (int j = o->jce1; j <= o->jce2; j++) A3(o->a1w, j, o->ice1, 1) = A3(o->a1w, j, o->ici1, 1);
+    }
+    if (o->bt) {
+      for (int j = o->jce1; j <= o->jce2; j++) PPW(j, o->ice2, 0, 0);
+      for (int j = o->jce1; j <= o->jce2; j++) A3(o->a1w, j, o->ice2, 1) = A3(o->a1w, j, o->ici2, 1);
+    }
+#undef PPW
+  }
   /* qv inflow/outflow for iboudy = 3 or 4, :1809-1950: west/east on ici, then south/north on
    * jce (they read the west/east results at the corners) */
   if (o->cfg.iboudy == 4) {

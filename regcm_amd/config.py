@@ -193,11 +193,13 @@ CONFIGS = {
     "C2": RunConfig(jx=96, iy=96, kz=23, ds=50.0, dt=100.0, name="C2 96x96x23 dt=100"),
     "C3": RunConfig(jx=192, iy=192, kz=23, ds=50.0, dt=150.0, name="C3 192x192x23 50km EURO"),
     "C4": RunConfig(jx=384, iy=384, kz=23, ds=50.0, dt=150.0, name="C4 384x384x23"),
-    # non-hydrostatic: C5 is BASELINE's 3 km convection-permitting case; N1/N2 are reduced
-    # grids of the same physics for parity tests
-    "N1": RunConfig(jx=40, iy=36, kz=18, ds=3.0, dt=30.0, idynamic=2, name="N1 40x36x18 NH 3km"),
-    "N2": RunConfig(jx=96, iy=96, kz=41, ds=3.0, dt=30.0, idynamic=2, name="N2 96x96x41 NH 3km"),
-    "C5": RunConfig(jx=768, iy=768, kz=41, ds=3.0, dt=30.0, idynamic=2, name="C5 768x768x41 NH 3km"),
+    # non-hydrostatic: C5 is BASELINE's 3 km convection-permitting grid; N1/N2 are reduced
+    # grids of the same core for parity tests.  dt = 9 s = 3 x ds(km), the reference's own
+    # CFL rule of thumb (Doc/UserGuide/AdvancedConfig.tex:478-486; its only NH namelist,
+    # PreProc/CRM/crm_test.in, runs 3 km at 5 s): SURVEY's 30 s diverges within 7 steps.
+    "N1": RunConfig(jx=40, iy=36, kz=18, ds=3.0, dt=9.0, idynamic=2, name="N1 40x36x18 NH 3km"),
+    "N2": RunConfig(jx=96, iy=96, kz=41, ds=3.0, dt=9.0, idynamic=2, name="N2 96x96x41 NH 3km"),
+    "C5": RunConfig(jx=768, iy=768, kz=41, ds=3.0, dt=9.0, idynamic=2, name="C5 768x768x41 NH 3km"),
 }
 
 

@@ -188,7 +188,8 @@ def nhpp(sigma: np.ndarray, t: np.ndarray, tv: np.ndarray, pr0: np.ndarray, t0: 
     return pp
 
 
-def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: float = 0.02) -> dict:
+def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: float = 0.02,
+                rest: bool = False) -> dict:
     """Synthetic non-hydrostatic ICBC ("syn-icbc v1", NH variant).
 
     The reference state comes from the terrain (regcm_amd/nhbase.py); p* is the constant
@@ -198,6 +199,9 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
     zero on the boundary and small seeded noise inside (so every w term is exercised from
     the first step).  Boundary time level 1 adds (1 K, 1 m/s, +2 % qv) as in the hydrostatic
     generator, with its own balanced pp.
+
+    ``rest=True`` builds the resting reference atmosphere instead (flat terrain, t = t0,
+    qv = 0, u = v = pp = w = 0, constant boundaries): the balance test of the NH core.
     """
     from . import nhbase
     rng = np.random.Generator(np.random.PCG64(seed + 2))
@@ -212,6 +216,8 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
     r2 = (jj - jc) ** 2 + (ii - ic) ** 2
     ht = hmax * np.exp(-r2 / (2.0 * (0.15 * jx) ** 2)) + rng.normal(0.0, 20.0, (iy, jx))
     ht = np.maximum(ht, 0.0)
+    if rest:
+        ht = np.zeros((iy, jx))
     mf = 1.0 + 0.02 * ((ii - ic) / iy) ** 2
     dlat = 30.0 + 30.0 * (ii - 1.0) / max(iy - 1.0, 1.0)
     xlat = 30.0 + 30.0 * (ii - 0.5) / max(iy - 1.0, 1.0)
@@ -244,6 +250,13 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
     u1, v1 = u + 1.0, v + 1.0
     w = np.zeros((kz + 1, iy, jx))
     w[1:kz, 1:iy - 2, 1:jx - 2] = rng.normal(0.0, w_noise, (kz - 1, iy - 3, jx - 3))
+    if rest:
+        t, t1 = t0.copy(), t0.copy()
+        qv, qv1 = np.zeros_like(t0), np.zeros_like(t0)
+        pp, pp1 = np.zeros_like(t0), np.zeros_like(t0)
+        u = np.zeros((kz, iy, jx)); v = np.zeros((kz, iy, jx))
+        u1, v1 = u, v
+        w[:] = 0.0
     rdtbdy = 1.0 / rc.dtbdys
 
     def cross3(a):

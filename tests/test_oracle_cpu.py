@@ -171,3 +171,72 @@ def test_oracle_option_variants_change_the_solution(c1_data):
         t = o.get("ATM1_T")
         assert np.isfinite(t).all(), variant
         assert not np.array_equal(t, ref), variant
+
+
+# ---- non-hydrostatic core (idynamic = 2) ---------------------------------------------------
+
+def _nh_oracle(rest=False, **kw):
+    from oracle.oracle import OracleCore
+    rc = CONFIGS["N1"]
+    data = icbc.generate_nh(rc, rest=rest, **kw)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    return rc, data, o
+
+
+def test_nh_reference_state_consistency():
+    """nhbase (Share/mod_nhinterp.F90:74-106): hydrostatic, monotone reference profiles;
+    init_sound short-step limit from max t0; istep rule of sound (:201-205)."""
+    from regcm_amd import nhbase
+    rc = CONFIGS["N1"]
+    d = icbc.generate_nh(rc)
+    st = d["state"]
+    ce = (slice(None), slice(0, rc.iy - 1), slice(0, rc.jx - 1))
+    pr, t0, rho, z = st["ATM0_PR"][ce], st["ATM0_T"][ce], st["ATM0_RHO"][ce], st["ATM0_Z"][ce]
+    assert np.all(np.diff(pr, axis=0) > 0) and np.all(np.diff(z, axis=0) < 0)
+    assert np.allclose(rho * 287.0 * t0 / pr, 1.0, atol=2e-3)
+    assert np.all(t0 >= nhbase.TISO)
+    # hydrostatic: dp/dz = -rho g between half levels (centred estimate), below the levels
+    # where t0 is clamped to tiso (z0 keeps the unclamped log-linear profile there); z0
+    # integrates from the local surface pressure while t0 uses p0, a ~1 % offset in the
+    # reference's own formulas
+    dpdz = (pr[1:] - pr[:-1]) / (z[1:] - z[:-1])
+    rhom = 0.5 * (rho[1:] + rho[:-1])
+    warm = (t0[1:] > nhbase.TISO + 1.0) & (t0[:-1] > nhbase.TISO + 1.0)
+    assert warm.sum() > warm.size // 2
+    assert np.allclose((dpdz / (-rhom * 9.80665))[warm], 1.0, atol=3e-2)
+    assert 7.0 < d["split"]["nh_dtsmax"] < 9.0
+    assert nhbase.acoustic_substeps(rc, d["split"]["nh_dtsmax"], 2 * rc.dt, 5) == 4
+    assert nhbase.acoustic_substeps(rc, d["split"]["nh_dtsmax"], rc.dt, 0) == 2
+
+
+def test_nh_oracle_rest_state_stays_at_rest():
+    """A resting atmosphere equal to the reference state over flat terrain is a fixed point
+    of the NH step up to the minqq floor: buoyancy, acoustic pressure gradient and the
+    semi-implicit w/pp solve balance (Main/mod_sound.F90, Main/mod_tendency.F90:1639-1671)."""
+    rc, data, o = _nh_oracle(rest=True)
+    o.step(10)
+    ps = o.get("PSA")[0][None, :-1, :-1]
+    for n, lim in (("ATM1_U", 1e-4), ("ATM1_V", 1e-4), ("ATM1_W", 1e-4), ("ATM1_PP", 0.05)):
+        assert np.abs(o.get(n)[:, :-1, :-1] / ps).max() < lim, n
+    t = o.get("ATM1_T")[:, :-1, :-1] / ps
+    assert np.abs(t - data["state"]["ATM0_T"][:, :-1, :-1]).max() < 1e-4
+
+
+def test_nh_oracle_stable_and_active():
+    """N1 at dt = 3 ds: 40 steps without a CFL stop, bounded w and pp; every NH prognostic
+    moves, p* stays constant (the NH core keeps p* = ps0, Main/mod_tendency.F90:836-848)."""
+    rc, data, o = _nh_oracle()
+    st = data["state"]
+    o.step(40)
+    assert o.get_time()[0] == 40
+    ps = o.get("PSA")[0]
+    assert np.array_equal(ps, st["PSA"][0])
+    psn = ps[None, :-1, :-1]
+    w = o.get("ATM1_W")[:, :-1, :-1] / psn
+    pp = o.get("ATM1_PP")[:, :-1, :-1] / psn
+    assert np.all(np.isfinite(w)) and np.abs(w).max() < 5.0
+    assert np.abs(pp - st["ATM1_PP"][:, :-1, :-1] / psn).max() < 2000.0
+    for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_PP", "ATM1_W", "ATM2_W"):
+        assert not np.array_equal(o.get(n), st[n]), n
