@@ -1,0 +1,71 @@
+// devcommon.hpp -- device helpers shared by the hydrostatic (kernels.hip) and the
+// non-hydrostatic (kernels_nh.hip) kernels: frame indexing, reference constants, psc2psd.
+#pragma once
+#include "engine.hpp"
+
+namespace rcm {
+
+#define F2(a, j, i) (a)[g.ix(j, i)]
+#define F3(a, j, i, k) (a)[(long)((k) - 1) * g.plane + g.ix(j, i)]
+#define SLI(s, i, k) (s)[(long)((k) - 1) * slen + ((i) - g.i0)]
+#define SLJ(s, j, k) (s)[(long)((k) - 1) * slen + ((j) - g.j0)]
+// byte-offset access
+#define LD(a, o) (*(const double*)((const char*)(a) + (uint32_t)(o)))
+#define ST(a, o, v) (*(double*)((char*)(a) + (uint32_t)(o)) = (v))
+// neighbour offsets relative to the thread's point (o2: 2-D, o3: 3-D at level k)
+#define O2(dj, di) (o2 + (uint32_t)((dj) * 8) + (uint32_t)(di) * P8)
+#define O3(dj, di) (o3 + (uint32_t)((dj) * 8) + (uint32_t)(di) * P8)
+#define O3K(dj, di, dk) (O3(dj, di) + (uint32_t)(dk) * L8)
+
+static constexpr double d_zero = 0.0, d_one = 1.0, d_two = 2.0, d_four = 4.0;
+static constexpr double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
+static constexpr double MINQQ = 1.0e-8, DLOWVAL = 1.0e-20;
+static constexpr double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
+static constexpr double o4_c1 = 4.0 / 6.0, o4_c2 = 1.0 / 6.0, o4_c3 = -20.0 / 6.0;  // idiffu = 2
+static constexpr double T00PG = 287.0, P00PG = 101.325;   // ipgf = 1, Share/mod_constants.F90:359-360
+
+__device__ __forceinline__ double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }
+__device__ __forceinline__ double dmin(double a, double b) { return (a < b) ? a : (b < a ? b : a); }
+
+__device__ __forceinline__ bool in(int v, int lo, int hi) { return v >= lo && v <= hi; }
+
+// thread -> (j, i, k) over a box starting at (j1, i1); k = blockIdx.z + 1
+#define THREAD_POINT(j1, i1)                                   \
+  const int j = (j1) + (int)(blockIdx.x * blockDim.x + threadIdx.x); \
+  const int i = (i1) + (int)(blockIdx.y * blockDim.y + threadIdx.y); \
+  const int k = (int)blockIdx.z + 1;                              \
+  (void)k;
+
+// psc2psd at one dot point, Main/mpplib/mod_mppparam.F90:13811-13862.
+__device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int j, int i, double& v) {
+  if (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2)) {
+    v = (F2(pc, j, i) + F2(pc, j, i - 1) + F2(pc, j - 1, i) + F2(pc, j - 1, i - 1)) * d_rfour;
+    return true;
+  }
+  if (g.bt && i == g.ide2 && in(j, g.jdi1, g.jdi2)) { v = (F2(pc, j, g.ice2) + F2(pc, j - 1, g.ice2)) * d_half; return true; }
+  if (g.bb && i == g.ide1 && in(j, g.jdi1, g.jdi2)) { v = (F2(pc, j, g.ice1) + F2(pc, j - 1, g.ice1)) * d_half; return true; }
+  if (g.bl && j == g.jde1 && in(i, g.idi1, g.idi2)) { v = (F2(pc, g.jce1, i) + F2(pc, g.jce1, i - 1)) * d_half; return true; }
+  if (g.br && j == g.jde2 && in(i, g.idi1, g.idi2)) { v = (F2(pc, g.jce2, i) + F2(pc, g.jce2, i - 1)) * d_half; return true; }
+  if (g.bb && g.bl && j == g.jde1 && i == g.ide1) { v = F2(pc, g.jce1, g.ice1); return true; }
+  if (g.bt && g.bl && j == g.jde1 && i == g.ide2) { v = F2(pc, g.jce1, g.ice2); return true; }
+  if (g.bb && g.br && j == g.jde2 && i == g.ide1) { v = F2(pc, g.jce2, g.ice1); return true; }
+  if (g.bt && g.br && j == g.jde2 && i == g.ide2) { v = F2(pc, g.jce2, g.ice2); return true; }
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------
+// psc2psd at any dot point from the global domain extents (tile ghosts included),
+// Main/mpplib/mod_mppparam.F90:13811-13862: 4-point mean inside, 2-point means on the domain
+// edges, corner copies.  Equal to psc2psd_at on every owned point.
+__device__ __forceinline__ double psc2psd_global(const Geom& g, const double* pc, int j, int i) {
+  const int jx = g.gjx, iy = g.giy;
+  const bool jin = j >= 2 && j <= jx - 1, iin = i >= 2 && i <= iy - 1;
+  if (jin && iin) return (F2(pc, j, i) + F2(pc, j, i - 1) + F2(pc, j - 1, i) + F2(pc, j - 1, i - 1)) * d_rfour;
+  if (jin && i == iy) return (F2(pc, j, iy - 1) + F2(pc, j - 1, iy - 1)) * d_half;
+  if (jin && i == 1) return (F2(pc, j, 1) + F2(pc, j - 1, 1)) * d_half;
+  if (iin && j == 1) return (F2(pc, 1, i) + F2(pc, 1, i - 1)) * d_half;
+  if (iin && j == jx) return (F2(pc, jx - 1, i) + F2(pc, jx - 1, i - 1)) * d_half;
+  return F2(pc, (j == 1) ? 1 : jx - 1, (i == 1) ? 1 : iy - 1);
+}
+
+}  // namespace rcm

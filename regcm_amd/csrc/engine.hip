@@ -22,6 +22,7 @@
 #include "comm.hpp"
 #include "engine.hpp"
 #include "kernels.hpp"
+#include "kernels_nh.hpp"
 
 using namespace rcm;
 
@@ -216,6 +217,8 @@ struct rcmdyn_engine {
   std::unique_ptr<Comm> comm;
   int device = 0;
 
+  std::vector<NHFields> nhf;   // non-hydrostatic buffers of each owned tile (idynamic = 2)
+
   int nsplit() const { return cfg.nsplit; }
 
   // ------------------------------------------------------------------ setup
@@ -282,6 +285,18 @@ struct rcmdyn_engine {
       }
     }
     c.pd = cfg.pd;
+    // non-hydrostatic core: diffusion constants (Main/mod_diffusion.F90:108-113), sound
+    c.idynamic = cfg.idynamic;
+    if (cfg.idynamic == 2) {
+      c.xkhz = cfg.ckh * c.dx;
+      c.xkhmax = 2.0 * c.xkhmax;
+      c.ifupr = cfg.ifupr; c.ifrayd = cfg.ifrayd; c.rayndamp = cfg.rayndamp;
+      c.rayalpha0 = cfg.rayalpha0; c.rayhd = cfg.rayhd; c.nhbet = cfg.nhbet; c.nhxkd = cfg.nhxkd;
+      c.nh_dtsmax = cfg.nh_dtsmax; c.nh_xmsf = cfg.nh_xmsf;
+      c.xgamma = 1.0 / (1.0 - c.rgas * (1.0 / c.cpd));           // Main/mod_sound.F90:77
+      c.dds[1] = 0.0; c.dds[kz + 1] = 0.0;                          // Main/mod_advection.F90:101-105
+      for (int k = 2; k <= kz; k++) c.dds[k] = 1.0 / (c.dsigma[k] + c.dsigma[k - 1]);
+    }
   }
 
   double* dalloc(Tile& t, size_t n) {
@@ -356,6 +371,7 @@ struct rcmdyn_engine {
     t.nred = ((g.jde2 - g.jde1 + 64) / 64) * (g.ide2 - g.ide1 + 1);
     t.red_off = red_total;
     red_total += t.nred;
+    if (cfg.idynamic == 2) setup_nh(t);
     // boundary masks
     std::vector<int8_t> rg;
     std::vector<int16_t> ib;
@@ -367,10 +383,60 @@ struct rcmdyn_engine {
     HIPCHK(hipMemcpy(t.ibdt, ib.data(), P * 2, hipMemcpyHostToDevice));
   }
 
+  // non-hydrostatic buffers (kernels_nh.hpp NHFields); shared hydrostatic buffers are
+  // filled per call by nhfields()
+  void setup_nh(Tile& t) {
+    const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
+    NHFields f{};
+    for (double** p : {&f.a1pp, &f.a2pp, &f.umc, &f.vmc, &f.ud, &f.vd, &f.umd, &f.vmd, &f.xt, &f.xqv, &f.xqc,
+                       &f.xtv, &f.xpp, &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.ubd, &f.vbd, &f.tb3d, &f.qvb3d, &f.qcb3d,
+                       &f.ppb3d, &f.pb3d, &f.xkcr, &f.xkc, &f.xkd, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
+                       &f.ppten, &f.ppdyn, &f.ct, &f.cu, &f.cv, &f.cpp, &f.cdt, &f.se, &f.sf, &f.saa, &f.sb,
+                       &f.sc, &f.rhs, &f.sca, &f.sg1, &f.sg2, &f.ptend, &f.pxup, &f.pyvp, &f.tk, &f.scc, &f.scdd,
+                       &f.scj, &f.spi})
+      *p = dalloc(t, P3);
+    for (double** p : {&f.a1w, &f.a2w, &f.xw, &f.wb3d, &f.pf3d, &f.xkcf, &f.wten, &f.wdyn, &f.cw, &f.wo})
+      *p = dalloc(t, P4);
+    f.ppb0 = dalloc(t, P3); f.ppbt = dalloc(t, P3); f.wwb0 = dalloc(t, P4); f.wwbt = dalloc(t, P4);
+    f.pr0 = dalloc(t, P3); f.t0 = dalloc(t, P3); f.rho0 = dalloc(t, P3); f.z0 = dalloc(t, P3);
+    f.dprddx = dalloc(t, P3); f.dprddy = dalloc(t, P3);
+    f.pf0 = dalloc(t, P4); f.rhof0 = dalloc(t, P4); f.zf0 = dalloc(t, P4);
+    f.ps0 = dalloc(t, P); f.dpsdxm = dalloc(t, P); f.dpsdym = dalloc(t, P);
+    f.ef = dalloc(t, P); f.ddx = dalloc(t, P); f.ddy = dalloc(t, P); f.dmdx = dalloc(t, P); f.dmdy = dalloc(t, P);
+    f.ex = dalloc(t, P); f.crx = dalloc(t, P); f.cry = dalloc(t, P);
+    f.estore = dalloc(t, P); f.astore = dalloc(t, P); f.tmask = dalloc(t, 169);
+    f.cfl = talloc<unsigned long long>(t, 1);
+    nhf.push_back(f);
+  }
+
+  NHFields nhfields(Tile& t) {
+    NHFields f = nhf[&t - tiles.data()];
+    const int c = t.cur;
+    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[c]; f.a1qv = t.a1qv[c]; f.a1qc = t.a1qc[c];
+    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[c]; f.a2qv = t.a2qv[c]; f.a2qc = t.a2qc[c];
+    f.psa = t.psa_[c]; f.psb = t.psb_[c];
+    f.msfx = t.msfx; f.msfd = t.msfd; f.coriol = t.coriol; f.ht = t.ht; f.xmsf = t.xmsf; f.dmsf = t.dmsf;
+    f.hgfact = t.hgfact; f.rgcr = t.rgcr; f.rgdt = t.rgdt; f.ibcr = t.ibcr; f.ibdt = t.ibdt;
+    f.ub0 = t.ub0; f.ubt = t.ubt; f.vb0 = t.vb0; f.vbt = t.vbt; f.tb0 = t.tb0; f.tbt = t.tbt;
+    f.qb0 = t.qb0; f.qbt = t.qbt;
+    f.rpsa = t.rpsa; f.rpsb = t.rpsb; f.rpsda = t.rpsda; f.rpsdb = t.rpsdb; f.psdota = t.psdota;
+    f.psdotb = t.psdotb; f.qdot = t.qdot;
+    f.tten = t.tten; f.qvten = t.qvten; f.qcten = t.qcten; f.uten = t.uten; f.vten = t.vten;
+    f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc; f.depplane = t.depplane;
+    return f;
+  }
+
   void create(const rcmdyn_config* c) {
     cfg = *c;
     if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
-    if (cfg.idynamic != 1) throw std::runtime_error("rcmdyn: only idynamic=1 (hydrostatic) is built");
+    if (cfg.idynamic != 1 && cfg.idynamic != 2) throw std::runtime_error("rcmdyn: idynamic must be 1 or 2");
+    if (cfg.idynamic == 2) {
+      if (cfg.nproc_j * cfg.nproc_i != 1)
+        throw std::runtime_error("rcmdyn: the non-hydrostatic core runs on one tile (the upper radiative "
+                                 "condition of sound gathers the whole domain, Main/mod_sound.F90:496-497)");
+      if (!(cfg.nh_dtsmax > 0.0) || !(cfg.nh_xmsf > 0.0))
+        throw std::runtime_error("rcmdyn: nh_dtsmax / nh_xmsf (init_sound) must be set for idynamic=2");
+    }
     if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
@@ -455,6 +521,36 @@ struct rcmdyn_engine {
   double* field_ptr(Tile& t, int f, int& nk) {
     nk = cfg.kz;
     const int c = t.cur;
+    if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
+      if (cfg.idynamic != 2) return nullptr;
+      NHFields& h = nhf[&t - tiles.data()];
+      auto cst = [](const double* p) { return const_cast<double*>(p); };
+      switch (f) {
+        case RCMDYN_ATM1_PP: return h.a1pp;  case RCMDYN_ATM2_PP: return h.a2pp;
+        case RCMDYN_XPPB_B0: return cst(h.ppb0); case RCMDYN_XPPB_BT: return cst(h.ppbt);
+        case RCMDYN_ATM0_PR: return cst(h.pr0); case RCMDYN_ATM0_T: return cst(h.t0);
+        case RCMDYN_ATM0_RHO: return cst(h.rho0); case RCMDYN_ATM0_Z: return cst(h.z0);
+        case RCMDYN_DPRDDX: return cst(h.dprddx); case RCMDYN_DPRDDY: return cst(h.dprddy);
+        default: break;
+      }
+      nk = cfg.kz + 1;
+      switch (f) {
+        case RCMDYN_ATM1_W: return h.a1w;  case RCMDYN_ATM2_W: return h.a2w;
+        case RCMDYN_XWWB_B0: return cst(h.wwb0); case RCMDYN_XWWB_BT: return cst(h.wwbt);
+        case RCMDYN_ATM0_PF: return cst(h.pf0); case RCMDYN_ATM0_RHOF: return cst(h.rhof0);
+        case RCMDYN_ATM0_ZF: return cst(h.zf0);
+        default: break;
+      }
+      nk = 1;
+      switch (f) {
+        case RCMDYN_ATM0_PS: return cst(h.ps0);
+        case RCMDYN_DPSDXM: return cst(h.dpsdxm); case RCMDYN_DPSDYM: return cst(h.dpsdym);
+        case RCMDYN_EF: return cst(h.ef); case RCMDYN_DDX: return cst(h.ddx); case RCMDYN_DDY: return cst(h.ddy);
+        case RCMDYN_DMDX: return cst(h.dmdx); case RCMDYN_DMDY: return cst(h.dmdy);
+        case RCMDYN_EX: return cst(h.ex); case RCMDYN_CRX: return cst(h.crx); case RCMDYN_CRY: return cst(h.cry);
+        default: return nullptr;
+      }
+    }
     switch (f) {
       case RCMDYN_ATM1_U: return t.a1u[c]; case RCMDYN_ATM1_V: return t.a1v[c];
       case RCMDYN_ATM1_T: return t.a1t[c]; case RCMDYN_ATM1_QV: return t.a1qv[c];
@@ -487,7 +583,10 @@ struct rcmdyn_engine {
   }
 
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
-    if (f < 0 || f > RCMDYN_XPSB_BT) throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
+    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || f > RCMDYN_CRY)
+      throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
+    if (f >= RCMDYN_ATM1_PP && cfg.idynamic != 2)
+      throw std::runtime_error("rcmdyn_put: non-hydrostatic field on a hydrostatic engine");
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -503,7 +602,8 @@ struct rcmdyn_engine {
       HIPCHK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
-    if (f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) bdy_dirty = true;
+    if ((f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) || (f >= RCMDYN_XPPB_B0 && f <= RCMDYN_XWWB_BT)) bdy_dirty = true;
+    if (f >= RCMDYN_ATM0_PS) invalidate_graphs();
   }
 
   void get(int f, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
@@ -791,7 +891,97 @@ struct rcmdyn_engine {
     return f;
   }
 
+  // istep of sound (Main/mod_sound.F90:201-205) for the host time mirror
+  int nh_istep() const {
+    int istep = (int)(hs.dt / cfg.nh_dtsmax);
+    if (istep < 2) istep = 2;
+    if (hs.lcount > 0 && istep < 4) istep = 4;
+    return istep;
+  }
+  // alarm_day (Main/mpplib/mod_timer.F90:277-337): active at the start and at the first step
+  // whose start time reaches the next multiple of a day
+  bool nh_day_alarm() const {
+    const double tnow = (double)hs.lcount * cfg.dtsec;
+    return hs.lcount == 0 || !nh_tmask_valid ||
+           std::floor(tnow / 86400.0) != std::floor((tnow - cfg.dtsec) / 86400.0);
+  }
+  bool nh_tmask_valid = false;
+
+  // tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2)
+  void nh_tend() {
+    const int kz = cfg.kz, kp = kz + 1;
+    Tile& t = tiles[0];
+    const Geom& g = t.g;
+    const NHFields f = nhfields(t);
+    const int istep = nh_istep();
+    const bool alarm = nh_day_alarm();
+    const dim3 fr = grid3(g.nj, g.ni, kp), frk = grid3(g.nj, g.ni, kz);
+    const int nce_j = g.jce2 - g.jce1 + 1, nce_i = g.ice2 - g.ice1 + 1;
+    const int nci_j = g.jci2 - g.jci1 + 1, nci_i = g.ici2 - g.ici1 + 1;
+    const int ndi_j = g.jdi2 - g.jdi1 + 1, ndi_i = g.idi2 - g.idi1 + 1;
+    (void)frk;
+    KLAUNCH(k_surface_pressures, grid3(g.nj, g.ni, 1), BLK, 0, stream, g, fields(t));
+    KLAUNCH(k_nh_decouple, fr, BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_omega, grid3(nce_j, nce_i, 1), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_mkslice, fr, BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_coeff_raw, grid3(nce_j, nce_i, kz), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_coeff_scale, fr, BLK, 0, stream, g, dc, f);
+    // init_tendencies (:1227-1240)
+    const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
+    for (double* p : {f.tten, f.tdyn, f.qvten, f.qvdyn, f.qcten, f.qcdyn, f.uten, f.udyn, f.vten, f.vdyn,
+                      f.ppten, f.ppdyn})
+      HIPCHK(hipMemsetAsync(p, 0, b3, stream));
+    for (double* p : {f.wten, f.wdyn}) HIPCHK(hipMemsetAsync(p, 0, b4, stream));
+    KLAUNCH(k_nh_uv_adv, grid3(ndi_j, ndi_i, 1), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_scalar_adv, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_curvature, grid3(ndi_j, ndi_i, kz), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_adiabatic, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_boundary, fr, BLK, 0, stream, g, dc, ds, f);
+    KLAUNCH(k_nh_diffusion, fr, BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_forecast, fr, BLK, 0, stream, g, dc, ds, f);
+    KLAUNCH(k_nh_negfix, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
+    KLAUNCH(k_nh_tfilter, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_raydamp, fr, BLK, 0, stream, g, dc, ds, f);
+    // sound, Main/mod_sound.F90:163-718
+    KLAUNCH(k_nh_sound_init, fr, BLK, 0, stream, g, dc, ds, f, istep);
+    for (int it = 1; it <= istep; it++) {
+      KLAUNCH(k_nh_sound_a, grid3(nce_j, nce_i, 1), BLK, 0, stream, g, dc, f, it);
+      KLAUNCH(k_nh_sound_uv, grid3(ndi_j, ndi_i, kz), BLK, 0, stream, g, dc, ds, f, istep);
+      KLAUNCH(k_nh_sound_b, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, ds, f, istep, it);
+      if (cfg.ifupr == 1 && it == 1 && alarm) {
+        KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, g, dc, f);
+        nh_tmask_valid = true;
+      }
+      KLAUNCH(k_nh_sound_c, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, ds, f, istep);
+    }
+    KLAUNCH(k_nh_sound_final, fr, BLK, 0, stream, g, dc, f);
+    KLAUNCH(k_nh_advance, dim3(1), dim3(1), 0, stream, dc, ds, f);
+    hs.lcount += 1;
+    if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+
+  // bdyval, non-hydrostatic: u, v, t, qv as the hydrostatic core (p* untouched), pp and w,
+  // then the moisture inflow/outflow rules and the clock
+  void nh_bdyval() {
+    const int kz = cfg.kz;
+    Tile& t = tiles[0];
+    const Geom& g = t.g;
+    const int c = t.cur;
+    Slices sl;
+    for (int q = 0; q < 16; q++) sl.s[q] = t.sl[q];
+    KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0, stream,
+            g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c], t.a2qv[c],
+            t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt, t.pb0, t.pbt,
+            sl, slen, 0);
+    KLAUNCH(k_nh_bdyval, dim3(1), dim3(256), 0, stream, g, kz, ds, nhfields(t));
+    KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
+            t.a1qc[c], t.a1qv[c], t.psa_[c], sl, slen, ds, cfg.dtsec, 1);
+    hs.xbctime = hs.xbctime + cfg.dtsec;
+  }
+
   void tend() {
+    if (cfg.idynamic == 2) { nh_tend(); return; }
     const int kz = cfg.kz, ns = cfg.nsplit;
     // One exchange point for the whole prologue (Main/mod_tendency.F90:815-1116,
     // Main/mod_slice.F90:102-300): the decoupled fields are recomputed where read, so their
@@ -910,6 +1100,7 @@ struct rcmdyn_engine {
   }
 
   void bdyval() {
+    if (cfg.idynamic == 2) { nh_bdyval(); return; }
     const int kz = cfg.kz;
     auto slices = [&](Tile& t) {
       Slices sl;
@@ -923,7 +1114,7 @@ struct rcmdyn_engine {
               stream, g, ds,
                          t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
                          t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0,
-                         t.qbt, t.pb0, t.pbt, slices(t), slen);
+                         t.qbt, t.pb0, t.pbt, slices(t), slen, (int)(cfg.idynamic == 1));
     });
     xch_slices();
     for (size_t q = 0; q < tiles.size(); q++) {
@@ -945,11 +1136,15 @@ struct rcmdyn_engine {
     HIPCHK(hipEventRecord(e0, stream));
     for (int s = 0; s < n; s++) {
       const int par = tiles[0].cur;
-      if (use_graph) {
+      const bool nh = cfg.idynamic == 2;
+      // the NH step changes shape on the first two steps (istep) and on the day alarm (upper
+      // radiative coefficients): those run eagerly, the steady step is graph-replayed
+      const bool eager_nh = nh && (hs.lcount < 2 || nh_day_alarm());
+      if (use_graph && !eager_nh) {
         if (!gexec[par]) capture(par);
         HIPCHK(hipGraphLaunch(gexec[par], stream));
         // replay the host-side bookkeeping of one tend + bdyval
-        for (auto& t : tiles) t.cur = 1 - t.cur;
+        if (!nh) for (auto& t : tiles) t.cur = 1 - t.cur;
         hs.lcount += 1;
         if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
         hs.xbctime = hs.xbctime + cfg.dtsec;

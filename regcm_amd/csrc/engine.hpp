@@ -64,6 +64,9 @@ struct Consts {
   double tau[MAXSPLIT][MAXKZ];
   double an[MAXSPLIT], hbar[MAXSPLIT], aam[MAXSPLIT], dtau[MAXSPLIT];
   double pdlog[MAXSPLIT][MAXKZ + 2], eps1[MAXSPLIT][MAXKZ + 2], pd;
+  // non-hydrostatic core (idynamic = 2): nonhydroparam and init_sound scalars
+  int idynamic, ifupr, ifrayd, rayndamp;
+  double rayalpha0, rayhd, nhbet, nhxkd, nh_dtsmax, nh_xmsf, xgamma, dds[MAXKZ + 2];
 };
 
 // rcm_timer state on the device, advanced by kernels so one captured step is replayable.

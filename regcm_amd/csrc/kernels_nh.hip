@@ -1,0 +1,1077 @@
+// kernels_nh.hip -- HIP/CDNA4 kernels of the non-hydrostatic (MM5-type) dynamical-core step
+// (idynamic = 2): the NH branches of tend (Main/mod_tendency.F90), the acoustic sub-stepping
+// of sound (Main/mod_sound.F90:163-718), Rayleigh damping (Main/mod_bdycod.F90:4953-5123)
+// and the NH boundary values.  ithadv = 0, ipptls = 1, i_crm = 0, physics stubbed.
+//
+// Each kernel restates one reference loop nest (or the whole vertical recurrence of a column,
+// one thread per column) with the same floating-point operation order as oracle/rcm_oracle.c
+// (compiled with -ffp-contract=off), so transcendental-free results are bit-identical.  The
+// state is updated in place (the reference's own in-place semantics); intermediates the
+// reference keeps in module arrays live in HBM (NHFields).  This first NH path favours a
+// literal, verifiable structure over fusion: see DESIGN.md section 4 for its kernels and the
+// fusion plan.
+#include "engine.hpp"
+#include "kernels_nh.hpp"
+#include "fastmath.hpp"
+#include "devcommon.hpp"
+
+namespace rcm {
+
+static constexpr double EGRAV_NH = 9.80665;                 // Share/mod_constants.F90:85
+static constexpr double REARTHRAD = 1.0 / 6.371229e6;       // :282-284
+static constexpr double MATHPI = 3.1415926535897932384626433832795029;
+
+#define IN_CE(j, i) (in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2))
+#define IN_CI(j, i) (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))
+#define IN_DI(j, i) (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))
+#define IN_DE(j, i) (in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2))
+#define FRAME_POINT()                                                  \
+  THREAD_POINT(g.j0, g.i0);                                             \
+  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+
+// decoupled boundary ud/vd with the iboudy = 3/4 inflow/outflow rule (see udvd_bdy in
+// kernels.hip; Main/mod_tendency.F90:893-994)
+__device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const double* a1v, const double* rpsda,
+                           int j, int i, int k) {
+  auto base = [&](int jj, int ii) {
+    const double r = F2(rpsda, jj, ii);
+    return make_double2(F3(a1u, jj, ii, k) * r, F3(a1v, jj, ii, k) * r);
+  };
+  if (iboudy != 4) return base(j, i);
+  auto we = [&](int jj, int ii) {
+    if (in(ii, g.idi1, g.idi2)) {
+      if (g.bl && jj == g.jde1 && F3(a1u, jj, ii, k) <= d_zero) return base(g.jdi1, ii);
+      if (g.br && jj == g.jde2 && F3(a1u, jj, ii, k) >= d_zero) return base(g.jdi2, ii);
+    }
+    return base(jj, ii);
+  };
+  if (in(j, g.jde1, g.jde2)) {
+    if (g.bb && i == g.ide1 && F3(a1v, j, i, k) >= d_zero) return we(j, g.idi1);
+    if (g.bt && i == g.ide2 && F3(a1v, j, i, k) <= d_zero) return we(j, g.idi2);
+  }
+  return we(j, i);
+}
+
+// ---------------------------------------------------------------------------------------
+// decouple NH (Main/mod_tendency.F90:852-1066): coupled/decoupled winds on the dot frame
+// (umc, vmc, ud, vd, umd, vmd), decoupled t, q, tv, pp, w, atm1 pr/rho and the buoyancy
+// helper atmx%pr on the cross frame.  k = 1..kz+1 (w only on kz+1).
+__global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  if (k <= kz && in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
+    const double m = F2(f.msfd, j, i);
+    F3(f.umc, j, i, k) = F3(f.a1u, j, i, k) * m;
+    F3(f.vmc, j, i, k) = F3(f.a1v, j, i, k) * m;
+    const double2 d = udvd_nh(g, c->iboudy, f.a1u, f.a1v, f.rpsda, j, i, k);
+    F3(f.ud, j, i, k) = d.x;
+    F3(f.vd, j, i, k) = d.y;
+    F3(f.umd, j, i, k) = d.x * m;
+    F3(f.vmd, j, i, k) = d.y * m;
+  }
+  if (!(in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga))) return;
+  const double rp = F2(f.rpsa, j, i);
+  F3(f.xw, j, i, k) = F3(f.a1w, j, i, k) * rp;
+  if (k > kz) return;
+  const double xt = F3(f.a1t, j, i, k) * rp;
+  const double xqv = dmax(F3(f.a1qv, j, i, k) * rp, MINQQ);
+  const double xqc = dmax(F3(f.a1qc, j, i, k) * rp, d_zero);
+  const double xtv = xt * (d_one + c->ep1 * xqv);
+  const double xpp = F3(f.a1pp, j, i, k) * rp;
+  const double pr1 = F3(f.pr0, j, i, k) + xpp;
+  F3(f.xt, j, i, k) = xt; F3(f.xqv, j, i, k) = xqv; F3(f.xqc, j, i, k) = xqc; F3(f.xtv, j, i, k) = xtv;
+  F3(f.xpp, j, i, k) = xpp; F3(f.pr1, j, i, k) = pr1;
+  F3(f.rho1, j, i, k) = pr1 / (c->rgas * xtv);
+  if (IN_CI(j, i))
+    F3(f.xpr, j, i, k) = (xtv - F3(f.t0, j, i, k) - xpp / (c->cpd * F3(f.rho0, j, i, k))) / xt;
+}
+
+// compute_omega NH (:1157-1191), one thread per cross column: qdot from w and the terrain
+// slopes of the reference p*, then the mass divergence with the qdot term
+__global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  const int kz = c->kz;
+  const double dummy = d_one / (c->dx2 * F2(f.msfx, j, i) * F2(f.msfx, j, i));
+  auto ucc = [&](int kk) {
+    return F3(f.umd, j, i, kk) + F3(f.umd, j, i + 1, kk) + F3(f.umd, j + 1, i, kk) + F3(f.umd, j + 1, i + 1, kk);
+  };
+  auto vcc = [&](int kk) {
+    return F3(f.vmd, j, i, kk) + F3(f.vmd, j, i + 1, kk) + F3(f.vmd, j + 1, i, kk) + F3(f.vmd, j + 1, i + 1, kk);
+  };
+  const double ps0 = F2(f.ps0, j, i), dx = F2(f.dpsdxm, j, i), dy = F2(f.dpsdym, j, i);
+  F3(f.qdot, j, i, 1) = d_zero;
+  F3(f.qdot, j, i, kz + 1) = d_zero;
+  double um = ucc(1), vm = vcc(1);
+  for (int k = 2; k <= kz; k++) {
+    const double uk = ucc(k), vk = vcc(k);
+    F3(f.qdot, j, i, k) = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(f.xw, j, i, k) / ps0 -
+                          c->sigma[k] * (dx * (c->twt1[k] * uk + c->twt2[k] * um) +
+                                         dy * (c->twt1[k] * vk + c->twt2[k] * vm));
+    um = uk; vm = vk;
+  }
+  const double ps = F2(f.psa, j, i);
+  for (int k = 1; k <= kz; k++) {
+    const double a = F3(f.umc, j + 1, i + 1, k) + F3(f.umc, j + 1, i, k) - F3(f.umc, j, i + 1, k) - F3(f.umc, j, i, k);
+    const double b = F3(f.vmc, j + 1, i + 1, k) + F3(f.vmc, j, i + 1, k) - F3(f.vmc, j + 1, i, k) - F3(f.vmc, j, i, k);
+    F3(f.cr, j, i, k) = (a + b) * dummy + (F3(f.qdot, j, i, k + 1) - F3(f.qdot, j, i, k)) * ps / c->dsigma[k];
+  }
+}
+
+// mkslice NH subset (Main/mod_slice.F90:163-183, 215-238, 278-281): b-level decoupled winds,
+// t, q, pp, w and the NH half/full level pressures
+__global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  if (k <= kz && in(j, g.jde1gb, g.jde2gb) && in(i, g.ide1gb, g.ide2gb)) {
+    const double r = F2(f.rpsdb, j, i);
+    F3(f.ubd, j, i, k) = F3(f.a2u, j, i, k) * r;
+    F3(f.vbd, j, i, k) = F3(f.a2v, j, i, k) * r;
+  }
+  if (!(in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb))) return;
+  const double rp = F2(f.rpsb, j, i);
+  F3(f.wb3d, j, i, k) = F3(f.a2w, j, i, k) * rp;
+  const double ptoppa = c->ptop * d_1000;
+  if (k <= kz) {
+    F3(f.tb3d, j, i, k) = F3(f.a2t, j, i, k) * rp;
+    F3(f.qvb3d, j, i, k) = dmax(F3(f.a2qv, j, i, k) * rp, MINQQ);
+    F3(f.qcb3d, j, i, k) = dmax(F3(f.a2qc, j, i, k) * rp, d_zero);
+    const double ppb = F3(f.a2pp, j, i, k) * rp;
+    F3(f.ppb3d, j, i, k) = ppb;
+    if (IN_CE(j, i)) {
+      if (k >= 2) {
+        F3(f.pb3d, j, i, k) = F3(f.pr0, j, i, k) + ppb;
+        const double ppm = F3(f.a2pp, j, i, k - 1) * rp;
+        F3(f.pf3d, j, i, k) = F3(f.pf0, j, i, k) + d_half * (ppm + ppb);
+      } else {
+        F3(f.pb3d, j, i, 1) = dmax(F3(f.pr0, j, i, 1) + ppb, ptoppa + 1.0);
+        F3(f.pf3d, j, i, 1) = ptoppa;
+      }
+    }
+  } else if (IN_CE(j, i)) {
+    const double ppkz = F3(f.a2pp, j, i, kz) * rp;
+    F3(f.pf3d, j, i, kz + 1) = F2(f.ps0, j, i) + ptoppa + ppkz;
+  }
+}
+
+// calc_coeff NH (Main/mod_diffusion.F90:215-250): Smagorinsky coefficient with the
+// vertical-velocity term, unscaled (xkcr) ...
+__global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  const double* ud = f.ubd; const double* vd = f.vbd;
+  const double dudx = F3(ud, j + 1, i, k) + F3(ud, j + 1, i + 1, k) - F3(ud, j, i, k) - F3(ud, j, i + 1, k);
+  const double dvdx = F3(vd, j + 1, i, k) + F3(vd, j + 1, i + 1, k) - F3(vd, j, i, k) - F3(vd, j, i + 1, k);
+  const double dudy = F3(ud, j, i + 1, k) + F3(ud, j + 1, i + 1, k) - F3(ud, j, i, k) - F3(ud, j + 1, i, k);
+  const double dvdy = F3(vd, j, i + 1, k) + F3(vd, j + 1, i + 1, k) - F3(vd, j, i, k) - F3(vd, j + 1, i, k);
+  const double dwdz = F3(f.wb3d, j, i, k) - F3(f.wb3d, j, i, k + 1);
+  const double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
+  F3(f.xkcr, j, i, k) = dmin(F2(f.hgfact, j, i) + c->dydc * duv, c->xkhmax);
+}
+
+// ... then xkc, xkcf (cross interior, full levels) and xkd (dot interior), scaled
+__global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  if (IN_CI(j, i)) {
+    const double pb = F2(f.psb, j, i);
+    if (k <= kz) F3(f.xkc, j, i, k) = F3(f.xkcr, j, i, k) * c->rdxsq * pb;
+    F3(f.xkcf, j, i, k) = F3(f.xkcr, j, i, (k == 1) ? 1 : k - 1) * c->rdxsq * pb;
+  }
+  if (k <= kz && IN_DI(j, i)) {
+    const double x = d_rfour * (F3(f.xkcr, j, i, k) + F3(f.xkcr, j - 1, i - 1, k) + F3(f.xkcr, j - 1, i, k) +
+                                F3(f.xkcr, j, i - 1, k));
+    F3(f.xkd, j, i, k) = x * c->rdxsq * F2(f.psdotb, j, i);
+  }
+}
+
+// hadvuv NH upstream branch (Main/mod_advection.F90:235-264) + vadvuv (:286-299), one thread
+// per dot column
+__global__ void k_nh_uv_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jdi1, g.idi1);
+  if (!IN_DI(j, i)) return;
+  const int kz = c->kz;
+  const double ul = c->ul, dm = F2(f.dmsf, j, i);
+  const double* ua = f.umc; const double* va = f.vmc; const double* u = f.ud; const double* v = f.vd;
+  for (int k = 1; k <= kz; k++) {
+    const double divd = d_rfour * (F3(f.cr, j, i, k) + F3(f.cr, j, i - 1, k) + F3(f.cr, j - 1, i, k) +
+                                   F3(f.cr, j - 1, i - 1, k));
+    const double ucmona = F3(ua, j, i + 1, k) + d_two * F3(ua, j, i, k) + F3(ua, j, i - 1, k);
+    double ucmonb = F3(ua, j + 1, i + 1, k) + d_two * F3(ua, j + 1, i, k) + F3(ua, j + 1, i - 1, k);
+    double ucmonc = F3(ua, j - 1, i + 1, k) + d_two * F3(ua, j - 1, i, k) + F3(ua, j - 1, i - 1, k);
+    const double vcmona = F3(va, j + 1, i, k) + d_two * F3(va, j, i, k) + F3(va, j - 1, i, k);
+    double vcmonb = F3(va, j + 1, i + 1, k) + d_two * F3(va, j, i + 1, k) + F3(va, j - 1, i + 1, k);
+    double vcmonc = F3(va, j + 1, i - 1, k) + d_two * F3(va, j, i - 1, k) + F3(va, j - 1, i - 1, k);
+    const double diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc));
+    const double u0 = F3(u, j, i, k), ue = F3(u, j + 1, i, k), uw = F3(u, j - 1, i, k);
+    const double un = F3(u, j, i + 1, k), us = F3(u, j, i - 1, k);
+    const double v0 = F3(v, j, i, k), ve = F3(v, j + 1, i, k), vw = F3(v, j - 1, i, k);
+    const double vn = F3(v, j, i + 1, k), vs = F3(v, j, i - 1, k);
+    const double ff1 = ul * (ue + u0), ff2 = ul * (uw + u0);
+    const double ff3 = ul * (vn + v0), ff4 = ul * (vs + v0);
+    ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+    ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+    vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+    vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+    F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + u0 * diag - dm * (ue * ucmonb - uw * ucmonc + un * vcmonb - us * vcmonc);
+    F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) + v0 * diag - dm * (ve * ucmonb - vw * ucmonc + vn * vcmonb - vs * vcmonc);
+  }
+  for (int k = 2; k <= kz; k++) {
+    const double qq = d_rfour * (F3(f.qdot, j, i, k) + F3(f.qdot, j, i - 1, k) + F3(f.qdot, j - 1, i, k) +
+                                 F3(f.qdot, j - 1, i - 1, k));
+    const double uu = qq * (c->twt1[k] * F3(f.a1u, j, i, k) + c->twt2[k] * F3(f.a1u, j, i, k - 1));
+    const double vv = qq * (c->twt1[k] * F3(f.a1v, j, i, k) + c->twt2[k] * F3(f.a1v, j, i, k - 1));
+    F3(f.udyn, j, i, k - 1) = F3(f.udyn, j, i, k - 1) - uu * c->xds[k - 1];
+    F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + uu * c->xds[k];
+    F3(f.vdyn, j, i, k - 1) = F3(f.vdyn, j, i, k - 1) - vv * c->xds[k - 1];
+    F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) + vv * c->xds[k];
+  }
+}
+
+// upstream flux form of hadvt/hadvqv/hadvqx/hadv3d ind 0 at one cross point
+// (Main/mod_advection.F90:337-386, 547-596, 639-653, 466-480); limiter 0 none, 1 t, 2 q
+__device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const double* fa, int j, int i, int k,
+                                          double u1, double u2, double v1, double v2, double xmf, double ps,
+                                          int limiter) {
+  const double f1 = d_half * c->ul * (u2 + u1) / ps;
+  const double f2 = d_half * c->ul * (v2 + v1) / ps;
+  const double fc = F3(fa, j, i, k), fw = F3(fa, j - 1, i, k), fe = F3(fa, j + 1, i, k);
+  const double fs = F3(fa, j, i - 1, k), fn = F3(fa, j, i + 1, k);
+  const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
+  const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
+  const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
+  const double fy2 = (d_one + f2) * fc + (d_one - f2) * fn;
+  double fg = -xmf * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1);
+  if (limiter && c->stability_enhance) {
+    double den, thr;
+    if (limiter == 1) { den = ps; thr = c->t_extrema; }
+    else { den = dmax(fc, DLOWVAL); thr = c->q_rel_extrema; }
+    if (fabs(fn + fs - d_two * fc) / den > thr) {
+      if (fc > fn && fc > fs) fg = dmin(fg, d_zero);
+      else if (fc < fn && fc < fs) fg = dmax(fg, d_zero);
+    }
+    if (fabs(fe + fw - d_two * fc) / den > thr) {
+      if (fc > fe && fc > fw) fg = dmin(fg, d_zero);
+      else if (fc < fe && fc < fw) fg = dmax(fg, d_zero);
+    }
+  }
+  return fg;
+}
+
+// scalar advection of the NH core, one thread per interior cross column (advection driver
+// Main/mod_tendency.F90:1308-1392): pp (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 +
+// vadv3d ind 0 on full levels), t (hadvt + vadv3d ind 1 NH form), qv (hadvqv + vadvqv),
+// qc (hadvqx + vadv4d ind 1)
+__global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const int kz = c->kz;
+  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
+  auto avg = [&](int k, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
+    u1 = F3(f.umc, j, i + 1, k) + F3(f.umc, j, i, k);
+    u2 = F3(f.umc, j + 1, i + 1, k) + F3(f.umc, j + 1, i, k);
+    v1 = F3(f.vmc, j + 1, i, k) + F3(f.vmc, j, i, k);
+    v2 = F3(f.vmc, j + 1, i + 1, k) + F3(f.vmc, j, i + 1, k);
+  };
+  double pu1 = 0, pu2 = 0, pv1 = 0, pv2 = 0;
+  for (int k = 1; k <= kz; k++) {
+    double u1, u2, v1, v2;
+    avg(k, u1, u2, v1, v2);
+    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + hadv_fg(g, c, f.xt, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
+    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2);
+    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    if (k >= 2) {                                  // hadv3d ind = 1, :486-507
+      const double t1 = c->twt1[k], t2 = c->twt2[k];
+      const double uaz1 = (t1 * u1 + t2 * pu1), uaz2 = (t1 * u2 + t2 * pu2);
+      const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
+      const double f1 = d_half * ul * (u2 + u1) / ps;
+      const double f2 = d_half * ul * (v2 + v1) / ps;
+      const double* w = f.xw;
+      const double fx1 = (d_one + f1) * F3(w, j - 1, i, k) + (d_one - f1) * F3(w, j, i, k);
+      const double fx2 = (d_one + f1) * F3(w, j, i, k) + (d_one - f1) * F3(w, j + 1, i, k);
+      const double fy1 = (d_one + f2) * F3(w, j, i - 1, k) + (d_one - f2) * F3(w, j, i, k);
+      const double fy2 = (d_one + f2) * F3(w, j, i, k) + (d_one - f2) * F3(w, j, i + 1, k);
+      F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
+    }
+    pu1 = u1; pu2 = u2; pv1 = v1; pv2 = v2;
+  }
+  // vadv3d ind = 0, nk = kz (pp), :746-754
+  for (int k = 2; k <= kz; k++) {
+    const double fx = F3(f.qdot, j, i, k) * (c->twt1[k] * F3(f.a1pp, j, i, k) + c->twt2[k] * F3(f.a1pp, j, i, k - 1));
+    F3(f.ppdyn, j, i, k - 1) = F3(f.ppdyn, j, i, k - 1) - fx * c->xds[k - 1];
+    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + fx * c->xds[k];
+  }
+  // vadv3d ind = 0, nk = kz+1 (w), :756-765
+  for (int k = 1; k <= kz; k++) {
+    const double qq = d_half * (F3(f.qdot, j, i, k) + F3(f.qdot, j, i, k + 1));
+    const double fx = qq * ((F3(f.a1w, j, i, k) + F3(f.a1w, j, i, k + 1)));
+    F3(f.wdyn, j, i, k + 1) = F3(f.wdyn, j, i, k + 1) + fx * c->dds[k + 1];
+    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - fx * c->dds[k];
+  }
+  // vadv3d ind = 1, non-hydrostatic form, :784-803
+  {
+    double dq = F3(f.a1t, j, i, 1) * exp(-c->c287 * log(F3(f.pb3d, j, i, 1)));
+    for (int k = 2; k <= kz; k++) {
+      const double rdphf = exp(-c->c287 * log(F3(f.pb3d, j, i, k)));
+      const double rdplf = exp(c->c287 * log(F3(f.pf3d, j, i, k)));
+      const double dk = F3(f.a1t, j, i, k) * rdphf;
+      const double fx = rdplf * F3(f.qdot, j, i, k) * (c->twt1[k] * dk + c->twt2[k] * dq);
+      F3(f.tdyn, j, i, k - 1) = F3(f.tdyn, j, i, k - 1) - fx * c->xds[k - 1];
+      F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + fx * c->xds[k];
+      dq = dk;
+    }
+  }
+  // vadvqv, :811-836
+  {
+    const double thr = MINQQ * ps;
+    for (int k = 2; k <= kz; k++) {
+      const double fk = F3(f.a1qv, j, i, k), fkm = F3(f.a1qv, j, i, k - 1);
+      double fg = d_zero;
+      if (fk > thr && fkm > thr) fg = fk * rcm_powpos(fkm / fk, c->qcon[k]);
+      const double q = F3(f.qdot, j, i, k);
+      F3(f.qvdyn, j, i, k - 1) = F3(f.qvdyn, j, i, k - 1) - q * fg * c->xds[k - 1];
+      F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + q * fg * c->xds[k];
+    }
+  }
+  // vadv4d ind = 1 (qc), :873-894, 958-961
+  {
+    const double thr = MINQQ * MINQQ * ps;
+    for (int k = 2; k <= kz; k++) {
+      const double svv = F3(f.qdot, j, i, k);
+      const double fk = F3(f.a1qc, j, i, k), fkm = F3(f.a1qc, j, i, k - 1);
+      double fg;
+      if (svv > d_zero) fg = (fkm > thr) ? svv * (c->twt1[k] * fk + c->twt2[k] * fkm) : d_zero;
+      else fg = (fk > thr) ? svv * (c->twt1[k] * fk + c->twt2[k] * fkm) : d_zero;
+      F3(f.qcdyn, j, i, k - 1) = F3(f.qcdyn, j, i, k - 1) - fg * c->xds[k - 1];
+      F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + fg * c->xds[k];
+    }
+  }
+}
+
+// curvature NH (Main/mod_tendency.F90:1839-1879): horizontal and vertical Coriolis,
+// horizontal and vertical curvature
+__global__ void k_nh_curvature(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jdi1, g.idi1);
+  if (!IN_DI(j, i)) return;
+  const double* w = f.a1w;
+  const double wadot = 0.125 * (F3(w, j - 1, i - 1, k) + F3(w, j - 1, i, k) + F3(w, j, i - 1, k) + F3(w, j, i, k));
+  const double wadotp1 = 0.125 * (F3(w, j - 1, i - 1, k + 1) + F3(w, j - 1, i, k + 1) + F3(w, j, i - 1, k + 1) +
+                                  F3(w, j, i, k + 1));
+  const double wabar = wadot + wadotp1;
+  const double amfac = wabar * F2(f.rpsda, j, i) * REARTHRAD;
+  const double uc = F3(f.a1u, j, i, k), vc = F3(f.a1v, j, i, k);
+  const double duv = uc * F2(f.dmdy, j, i) - vc * F2(f.dmdx, j, i);
+  const double cor = F2(f.coriol, j, i), ef = F2(f.ef, j, i);
+  F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + cor * vc - ef * F2(f.ddx, j, i) * wabar + F3(f.vmd, j, i, k) * duv -
+                        uc * amfac;
+  F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) - cor * uc + ef * F2(f.ddy, j, i) * wabar - F3(f.umd, j, i, k) * duv -
+                        vc * amfac;
+}
+
+// adiabatic NH (:1581-1593, 1612-1671), one thread per interior cross column
+__global__ void k_nh_adiabatic(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const int kz = c->kz;
+  for (int k = 1; k <= kz; k++) {
+    const double cpm = c->cpd * (d_one + 0.80 * F3(f.xqv, j, i, k));
+    const double scr1 = d_half * EGRAV_NH * F3(f.rho0, j, i, k) * (F3(f.a1w, j, i, k) + F3(f.a1w, j, i, k + 1));
+    const double cr = F3(f.cr, j, i, k), xpp = F3(f.xpp, j, i, k);
+    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + F3(f.xt, j, i, k) * cr -
+                          (scr1 + F3(f.ppdyn, j, i, k) + F3(f.ppten, j, i, k) + xpp * cr) /
+                              (F3(f.rho1, j, i, k) * cpm);
+    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + xpp * cr;
+    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + F3(f.xqv, j, i, k) * cr;
+    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + F3(f.xqc, j, i, k) * cr;
+  }
+  auto ucc = [&](int k) {
+    return F3(f.a1u, j, i, k) + F3(f.a1u, j, i + 1, k) + F3(f.a1u, j + 1, i, k) + F3(f.a1u, j + 1, i + 1, k);
+  };
+  auto vcc = [&](int k) {
+    return F3(f.a1v, j, i, k) + F3(f.a1v, j, i + 1, k) + F3(f.a1v, j + 1, i, k) + F3(f.a1v, j + 1, i + 1, k);
+  };
+  const double ps = F2(f.psa, j, i), rps = F2(f.rpsa, j, i);
+  const double ex = F2(f.ex, j, i), crx = F2(f.crx, j, i), cry = F2(f.cry, j, i);
+  double um = ucc(1), vm = vcc(1);
+  for (int k = 2; k <= kz; k++) {
+    const double uk = ucc(k), vk = vcc(k);
+    const double rofac = (c->dsigma[k - 1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, k - 1)) /
+                         (c->dsigma[k - 1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, k - 1));
+    const double uaq = d_rfour * (c->twt1[k] * uk + c->twt2[k] * um);
+    const double vaq = d_rfour * (c->twt1[k] * vk + c->twt2[k] * vm);
+    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) +
+        (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
+        ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
+        F3(f.xw, j, i, k) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
+    um = uk; vm = vk;
+  }
+  for (int k = 2; k <= kz; k++)                 // water loading, qcd = atmx%qx(iqc)
+    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - EGRAV_NH * ps *
+                          (c->twt2[k] * F3(f.xqc, j, i, k - 1) + c->twt1[k] * F3(f.xqc, j, i, k));
+}
+
+__device__ __forceinline__ double nh_relax(double ften, double xf, double xg, double f0, double f1, double f2,
+                                           double f3, double f4) {
+  return ften + xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0);
+}
+
+// boundary (Main/mod_tendency.F90:1462-1501): nudge3d/nudge4d3d/nudgeuv of t, qv, u, v, pp
+// and w (hefc(ib, min(k,kz)) on the w top level, Main/mod_bdycod.F90:4332-4333), or the
+// sponges of iboudy = 4 on the total tendencies.  k = 1..kz+1.
+__global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  const double xt = s->xbctime + s->dt;
+  const int kc = (k < kz) ? k : kz;
+  if (IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0) {
+    const int ib = f.ibcr[g.ix(j, i)];
+    if (c->iboudy == 4) {
+      const double w = c->wgtx[ib];
+      if (k <= kz) {
+        F3(f.tten, j, i, k) = w * F3(f.tten, j, i, k) + (d_one - w) * F3(f.tbt, j, i, k);
+        F3(f.qvten, j, i, k) = w * F3(f.qvten, j, i, k) + (d_one - w) * F3(f.qbt, j, i, k);
+        F3(f.ppten, j, i, k) = w * F3(f.ppten, j, i, k) + (d_one - w) * F3(f.ppbt, j, i, k);
+      }
+      F3(f.wten, j, i, k) = w * F3(f.wten, j, i, k) + (d_one - w) * F3(f.wwbt, j, i, k);
+    } else {
+      double xf, xg;
+      if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
+      else { xf = c->hefc[ib][kc]; xg = c->hegc[ib][kc]; }
+#define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
+#define RELAX5(ten, b0, bt, a)                                                                    \
+  F3(ten, j, i, k) = nh_relax(F3(ten, j, i, k), xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), \
+                              FG(b0, bt, a, j + 1, i), FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
+      if (k <= kz) {
+        RELAX5(f.tdyn, f.tb0, f.tbt, f.a2t);
+        const double nfac = 1.0e3, rfac = d_one / nfac;
+#define FQ(J, I) (nfac * (F3(f.qb0, J, I, k) + xt * F3(f.qbt, J, I, k)) - nfac * F3(f.a2qv, J, I, k))
+        const double q0 = FQ(j, i), q1 = FQ(j - 1, i), q2 = FQ(j + 1, i), q3 = FQ(j, i - 1), q4 = FQ(j, i + 1);
+#undef FQ
+        F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
+        RELAX5(f.ppdyn, f.ppb0, f.ppbt, f.a2pp);
+      }
+      RELAX5(f.wdyn, f.wwb0, f.wwbt, f.a2w);
+    }
+  }
+  if (k <= kz && IN_DI(j, i) && f.rgdt[g.ix(j, i)] > 0) {
+    const int ib = f.ibdt[g.ix(j, i)];
+    if (c->iboudy == 4) {
+      const double w = c->wgtd[ib];
+      F3(f.uten, j, i, k) = w * F3(f.uten, j, i, k) + (d_one - w) * F3(f.ubt, j, i, k);
+      F3(f.vten, j, i, k) = w * F3(f.vten, j, i, k) + (d_one - w) * F3(f.vbt, j, i, k);
+    } else {
+      double xf, xg;
+      if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
+      else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
+      RELAX5(f.udyn, f.ub0, f.ubt, f.a2u);
+      RELAX5(f.vdyn, f.vb0, f.vbt, f.a2v);
+    }
+  }
+#undef RELAX5
+#undef FG
+}
+
+// 4th-order (idiffu = 1) / 9-point (idiffu = 2) diffusion of one cross field at (j,i,k)
+// (diffu_x3d / diffu_x3df / diffu_x4d3d, Main/mod_diffusion.F90:523-790)
+__device__ __forceinline__ double diffx_at(const Geom& g, const Consts* c, double ften, const double* fa,
+                                           const double* xk, int j, int i, int k) {
+  if (c->idiffu == 2) {
+    return ften + d_one * F3(xk, j, i, k) *
+        (o4_c1 * (F3(fa, j + 1, i, k) + F3(fa, j - 1, i, k) + F3(fa, j, i + 1, k) + F3(fa, j, i - 1, k)) +
+         o4_c2 * (F3(fa, j + 1, i + 1, k) + F3(fa, j - 1, i - 1, k) + F3(fa, j - 1, i + 1, k) + F3(fa, j + 1, i - 1, k)) +
+         o4_c3 * F3(fa, j, i, k));
+  }
+  if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))
+    ften = ften - d_one * F3(xk, j, i, k) *
+        (z4_c1 * (F3(fa, j + 2, i, k) + F3(fa, j - 2, i, k) + F3(fa, j, i + 2, k) + F3(fa, j, i - 2, k)) +
+         z4_c2 * (F3(fa, j + 1, i, k) + F3(fa, j - 1, i, k) + F3(fa, j, i + 1, k) + F3(fa, j, i - 1, k)) +
+         z4_c3 * F3(fa, j, i, k));
+  const double lap = z4_c1 * (F3(fa, j + 1, i, k) + F3(fa, j - 1, i, k) + F3(fa, j, i + 1, k) + F3(fa, j, i - 1, k)) +
+                     z4_c2 * F3(fa, j, i, k);
+  const int nb = (g.bl && j == g.jci1) + (g.br && j == g.jci2) + (g.bb && i == g.ici1) + (g.bt && i == g.ici2);
+  for (int q = 0; q < nb; q++) ften = ften + d_one * F3(xk, j, i, k) * lap;
+  return ften;
+}
+
+// diffusion (Main/mod_tendency.F90:1515-1538): diffu_d for u, v; diffu_x for t, qv, qc, pp
+// (xkc) and w (xkcf, full levels)
+__global__ void k_nh_diffusion(Geom g, const Consts* __restrict__ c, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  if (IN_CI(j, i)) {
+    if (k <= kz) {
+      F3(f.tdyn, j, i, k) = diffx_at(g, c, F3(f.tdyn, j, i, k), f.tb3d, f.xkc, j, i, k);
+      F3(f.qvdyn, j, i, k) = diffx_at(g, c, F3(f.qvdyn, j, i, k), f.qvb3d, f.xkc, j, i, k);
+      F3(f.qcdyn, j, i, k) = diffx_at(g, c, F3(f.qcdyn, j, i, k), f.qcb3d, f.xkc, j, i, k);
+      F3(f.ppdyn, j, i, k) = diffx_at(g, c, F3(f.ppdyn, j, i, k), f.ppb3d, f.xkc, j, i, k);
+    }
+    F3(f.wdyn, j, i, k) = diffx_at(g, c, F3(f.wdyn, j, i, k), f.wb3d, f.xkcf, j, i, k);
+  }
+  if (k > kz || !IN_DI(j, i)) return;
+  // diffu_d, Main/mod_diffusion.F90:281-411
+  const double* m = f.msfd;
+#define UM(a, J, I) (F3(a, J, I, k) / F2(m, J, I))
+  for (int pass = 0; pass < 2; pass++) {
+    const double* b = pass ? f.vbd : f.ubd;
+    double* ten = pass ? f.vdyn : f.udyn;
+    double t = F3(ten, j, i, k);
+    const double xkd = F3(f.xkd, j, i, k);
+    if (c->idiffu == 2) {
+      t = t + xkd * (o4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                     o4_c2 * (UM(b, j + 1, i + 1) + UM(b, j - 1, i - 1) + UM(b, j - 1, i + 1) + UM(b, j + 1, i - 1)) +
+                     o4_c3 * (UM(b, j, i)));
+    } else {
+      if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2))
+        t = t - xkd * (z4_c1 * (UM(b, j + 2, i) + UM(b, j - 2, i) + UM(b, j, i + 2) + UM(b, j, i - 2)) +
+                       z4_c2 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                       z4_c3 * (UM(b, j, i)));
+      const int nb = (g.bl && j == g.jdi1) + (g.br && j == g.jdi2) + (g.bb && i == g.idi1) + (g.bt && i == g.idi2);
+      for (int q = 0; q < nb; q++)
+        t = t + xkd * (z4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                       z4_c2 * (UM(b, j, i)));
+    }
+    F3(ten, j, i, k) = t;
+  }
+#undef UM
+}
+
+// tau, Main/mod_bdycod.F90:5115-5123
+__device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax) {
+  if (z > zmax - c->rayhd) {
+    const double s = sin((MATHPI * d_half) * (d_one - (zmax - z) / c->rayhd));
+    return c->rayalpha0 * (s * s);
+  }
+  return d_zero;
+}
+
+// tendency sums (:285-314, 332-349), Rayleigh damping of t and qv (:356-364), forecast of t
+// and moisture (:368-380) and the momentum sums (:404-411).  k = 1..kz+1.
+__global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  const double dt = s->dt;
+  if (IN_CI(j, i)) {
+    F3(f.wten, j, i, k) = F3(f.wten, j, i, k) + F3(f.wdyn, j, i, k) + 0.0;
+    if (k <= kz) {
+      double tt = F3(f.tten, j, i, k) + F3(f.tdyn, j, i, k) + 0.0;
+      double qv = F3(f.qvten, j, i, k) + F3(f.qvdyn, j, i, k) + 0.0;
+      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) + F3(f.ppdyn, j, i, k) + 0.0;
+      double qc = F3(f.qcten, j, i, k) + F3(f.qcdyn, j, i, k) + 0.0;
+      tt = tt + 0.0; qv = qv + 0.0; qc = qc + 0.0;
+      if (c->ifrayd == 1 && k <= c->rayndamp) {
+        const double xt = s->xbctime + dt;
+        const double tau = nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1));
+        tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
+        qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
+      }
+      F3(f.tten, j, i, k) = tt; F3(f.qvten, j, i, k) = qv; F3(f.qcten, j, i, k) = qc;
+      F3(f.ct, j, i, k) = F3(f.a2t, j, i, k) + dt * tt;
+    }
+  }
+  if (k > kz) return;
+  if (IN_CE(j, i)) {
+    double qv = F3(f.a2qv, j, i, k), qc = F3(f.a2qc, j, i, k);
+    if (IN_CI(j, i)) {
+      qv = qv + dt * F3(f.qvten, j, i, k);
+      qc = qc + dt * F3(f.qcten, j, i, k);
+    }
+    F3(f.cqv, j, i, k) = qv;
+    F3(f.cqc, j, i, k) = qc;
+  }
+  if (IN_DI(j, i)) {
+    F3(f.uten, j, i, k) = F3(f.uten, j, i, k) + F3(f.udyn, j, i, k) + 0.0;
+    F3(f.vten, j, i, k) = F3(f.vten, j, i, k) + F3(f.vdyn, j, i, k) + 0.0;
+  }
+}
+
+// negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points
+// whose sweep predecessors are non-negative, serial sweep of the flagged planes after it.
+__device__ __forceinline__ double nh_negfix_sum(const Geom& g, const double* sv, const double* fx, int j, int i,
+                                                int k, bool use_fixed) {
+  double sum = 0.0;
+  for (int ii = i - 1; ii <= i + 1; ii++)
+    for (int jj = j - 1; jj <= j + 1; jj++) {
+      double v = F3(sv, jj, ii, k);
+      if (use_fixed) {
+        const bool pred = (ii < i) || (ii == i && jj < j);
+        if (pred && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) v = F3(fx, jj, ii, k);
+      }
+      sum = sum + fabs(v);
+    }
+  return 0.01 * sum / 9.0;
+}
+__device__ __forceinline__ bool nh_negfix_dependent(const Geom& g, const double* sv, int j, int i, int k) {
+#define NEG(J, I) (in(J, g.jci1, g.jci2) && in(I, g.ici1, g.ici2) && F3(sv, J, I, k) < d_zero)
+  return NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
+#undef NEG
+}
+
+__global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  for (int n = 0; n < 2; n++) {
+    const double* sv = n ? f.cqc : f.cqv;
+    double* fx = n ? f.fqc : f.fqv;
+    if (F3(sv, j, i, k) < d_zero) {
+      if (nh_negfix_dependent(g, sv, j, i, k)) atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+      else F3(fx, j, i, k) = nh_negfix_sum(g, sv, fx, j, i, k, false);
+    }
+  }
+}
+
+// one 64-lane block per (n, k) plane; flagged planes swept in the reference order
+__global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f) {
+  const int plane = blockIdx.x;
+  if (!f.depplane[plane]) return;
+  const int kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  const double* sv = n ? f.cqc : f.cqv;
+  double* fx = n ? f.fqc : f.fqv;
+  const int lane = threadIdx.x;
+  for (int i = g.ici1; i <= g.ici2; i++)
+    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
+      const int j = j0 + lane;
+      const bool flagged = (j <= g.jci2) && F3(sv, j, i, k) < d_zero && nh_negfix_dependent(g, sv, j, i, k);
+      unsigned long long mask = __ballot(flagged);
+      if (lane == 0) {
+        while (mask) {
+          const int b = __ffsll((long long)mask) - 1;
+          mask &= mask - 1;
+          F3(fx, j0 + b, i, k) = nh_negfix_sum(g, sv, fx, j0 + b, i, k, true);
+        }
+      }
+    }
+  if (lane == 0) f.depplane[plane] = 0;
+}
+
+// time filters of t (RA), qv and qc (RAW), Main/mod_tendency.F90:422-427; p* is constant
+__global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  {
+    const double o1 = F3(f.a1t, j, i, k), o2 = F3(f.a2t, j, i, k), nw = F3(f.ct, j, i, k);
+    const double d = c->gnu1 * (nw + o2 - d_two * o1);
+    F3(f.a2t, j, i, k) = o1 + d;
+    F3(f.a1t, j, i, k) = nw;
+  }
+  const double beta = 0.53;
+  {
+    double v = F3(f.cqv, j, i, k);
+    if (v < d_zero) v = F3(f.fqv, j, i, k);
+    const double o1 = F3(f.a1qv, j, i, k), o2 = F3(f.a2qv, j, i, k);
+    const double d = c->gnu1 * (v + o2 - d_two * o1);
+    F3(f.a2qv, j, i, k) = dmax(o1 + beta * d, MINQQ * F2(f.psa, j, i));
+    F3(f.a1qv, j, i, k) = dmax(v + (beta - d_one) * d, MINQQ * F2(f.psb, j, i));
+  }
+  {
+    double v = F3(f.cqc, j, i, k);
+    if (v < d_zero) v = F3(f.fqc, j, i, k);
+    const double o1 = F3(f.a1qc, j, i, k), o2 = F3(f.a2qc, j, i, k);
+    const double d = c->gnu2 * (v + o2 - d_two * o1);
+    double m = o1 + beta * d, q = v + (beta - d_one) * d;
+    if (m < d_zero) m = d_zero;
+    if (q < d_zero) q = d_zero;
+    F3(f.a2qc, j, i, k) = m;
+    F3(f.a1qc, j, i, k) = q;
+  }
+}
+
+// Rayleigh damping of u, v, pp, w and decoupling of the tendencies before sound
+// (:466-499; raydampuv/raydamp3/raydamp3f, Main/mod_bdycod.F90:4953-5045).  k = 1..kz+1.
+__global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  const bool ray = c->ifrayd == 1 && k <= c->rayndamp;
+  const double xt = s->xbctime + s->dt;
+  if (k <= kz && IN_DI(j, i)) {
+    double ut = F3(f.uten, j, i, k), vt = F3(f.vten, j, i, k);
+    if (ray) {
+      const double* z = f.z0;
+      const double zz = d_rfour * (F3(z, j, i, k) + F3(z, j - 1, i, k) + F3(z, j, i - 1, k) + F3(z, j - 1, i - 1, k));
+      const double zm = d_rfour * (F3(z, j, i, 1) + F3(z, j - 1, i, 1) + F3(z, j, i - 1, 1) + F3(z, j - 1, i - 1, 1));
+      const double tau = nh_tau(c, zz, zm);
+      ut = ut + tau * ((F3(f.ub0, j, i, k) + xt * F3(f.ubt, j, i, k)) - F3(f.a2u, j, i, k));
+      vt = vt + tau * ((F3(f.vb0, j, i, k) + xt * F3(f.vbt, j, i, k)) - F3(f.a2v, j, i, k));
+    }
+    F3(f.uten, j, i, k) = ut * F2(f.rpsda, j, i);
+    F3(f.vten, j, i, k) = vt * F2(f.rpsda, j, i);
+  }
+  if (!IN_CI(j, i)) return;
+  if (k <= kz) {
+    double pt = F3(f.ppten, j, i, k);
+    if (ray)
+      pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
+                    ((F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k)) - F3(f.a2pp, j, i, k));
+    F3(f.ppten, j, i, k) = pt * F2(f.rpsa, j, i);
+  }
+  double wt = F3(f.wten, j, i, k);
+  if (ray) wt = wt + nh_tau(c, F3(f.zf0, j, i, k), F3(f.zf0, j, i, 1)) * (d_zero - F3(f.a2w, j, i, k));
+  F3(f.wten, j, i, k) = wt * F2(f.rpsa, j, i);
+}
+
+// ======================================================================= sound
+// initial arrays of the acoustic loop (Main/mod_sound.F90:217-245).  k = 1..kz+1.
+__global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                                int istep) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  const double dts = s->dt / (double)istep;
+  const double rpb = IN_CE(j, i) ? F2(f.rpsb, j, i) : 0.0;
+  if (k <= kz) {
+    if (IN_DE(j, i)) {
+      F3(f.cu, j, i, k) = F3(f.a2u, j, i, k) / F2(f.psdotb, j, i);
+      F3(f.cv, j, i, k) = F3(f.a2v, j, i, k) / F2(f.psdotb, j, i);
+    }
+    if (IN_DI(j, i)) {
+      F3(f.uten, j, i, k) = F3(f.uten, j, i, k) * dts;
+      F3(f.vten, j, i, k) = F3(f.vten, j, i, k) * dts;
+    }
+    if (IN_CE(j, i)) F3(f.cpp, j, i, k) = F3(f.a2pp, j, i, k) * rpb;
+    if (IN_CI(j, i)) {
+      F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) * rpb;
+      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) * dts;
+    }
+  }
+  if (IN_CE(j, i)) F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
+  if (IN_CI(j, i)) F3(f.wten, j, i, k) = F3(f.wten, j, i, k) * dts;
+}
+
+// substep part A (:250-262), one thread per cross column: pp += xkd*pi, then dp'/dp0
+__global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  const int kz = c->kz;
+  if (it > 1 && IN_CI(j, i))
+    for (int k = 1; k <= kz; k++) F3(f.cpp, j, i, k) = F3(f.cpp, j, i, k) + c->nhxkd * F3(f.spi, j, i, k);
+  for (int k = 1; k <= kz; k++) {
+    const int kp1 = (kz < k + 1) ? kz : k + 1, km1 = (1 > k - 1) ? 1 : k - 1;
+    F3(f.cdt, j, i, k) = (F3(f.cpp, j, i, km1) - F3(f.cpp, j, i, kp1)) / (F3(f.pr0, j, i, km1) - F3(f.pr0, j, i, kp1));
+  }
+}
+
+// substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
+__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep) {
+  THREAD_POINT(g.jdi1, g.idi1);
+  if (!IN_DI(j, i)) return;
+  const double dts = s->dt / (double)istep;
+  const double rho = d_rfour * (F3(f.rho1, j, i, k) + F3(f.rho1, j - 1, i, k) + F3(f.rho1, j, i - 1, k) +
+                                F3(f.rho1, j - 1, i - 1, k));
+  const double dppdp0 = d_rfour * (F3(f.cdt, j, i, k) + F3(f.cdt, j - 1, i, k) + F3(f.cdt, j, i - 1, k) +
+                                   F3(f.cdt, j - 1, i - 1, k));
+  const double chh = d_half * dts / (rho * c->dx) / F2(f.msfd, j, i);
+  const double* pp = f.cpp;
+  double u = F3(f.cu, j, i, k) - chh * (F3(pp, j, i, k) - F3(pp, j - 1, i, k) + F3(pp, j, i - 1, k) -
+                                        F3(pp, j - 1, i - 1, k) - F3(f.dprddx, j, i, k) * dppdp0);
+  double v = F3(f.cv, j, i, k) - chh * (F3(pp, j, i, k) - F3(pp, j, i - 1, k) + F3(pp, j - 1, i, k) -
+                                        F3(pp, j - 1, i - 1, k) - F3(f.dprddy, j, i, k) * dppdp0);
+  F3(f.cu, j, i, k) = u + F3(f.uten, j, i, k);
+  F3(f.cv, j, i, k) = v + F3(f.vten, j, i, k);
+}
+
+// substep part C (:297-483), one thread per interior cross column: undo the divergence
+// damping, lower boundary w, Ikawa coefficients, pp predictor, upward sweep of the
+// tridiagonal w system, upper radiative condition inputs
+__global__ void k_nh_sound_b(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                             int istep, int it) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const int kz = c->kz;
+  const double dts = s->dt / (double)istep;
+  const double bet = c->nhbet, xg = c->xgamma;
+  const double bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
+  const double bpxbp = bp * bp, bpxbm = bp * bm;
+  double* pp = f.cpp;
+  double* w = f.cw;
+  const double* cu = f.cu;
+  const double* cv = f.cv;
+  if (it > 1)
+    for (int k = 1; k <= kz; k++) F3(pp, j, i, k) = F3(pp, j, i, k) - c->nhxkd * F3(f.spi, j, i, k);
+  for (int k = 1; k <= kz + 1; k++) F3(f.wo, j, i, k) = F3(w, j, i, k);
+  const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
+  F3(w, j, i, kz + 1) = d_half * d_rfour * c->regrav *
+      ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
+           (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
+       (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
+           (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
+      (c->dx * msfx);
+  F3(f.se, j, i, kz) = d_zero;
+  F3(f.sf, j, i, kz) = F3(w, j, i, kz + 1);
+  const double* pr0 = f.pr0;
+  auto divterm = [&](int k) {
+    const double* m = f.msfd;
+    return (F3(cv, j, i + 1, k) * F2(m, j, i + 1) - F3(cv, j, i, k) * F2(m, j, i) +
+            F3(cv, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cv, j + 1, i, k) * F2(m, j + 1, i) +
+            F3(cu, j + 1, i, k) * F2(m, j + 1, i) - F3(cu, j, i, k) * F2(m, j, i) +
+            F3(cu, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cu, j, i + 1, k) * F2(m, j, i + 1)) / msfx;
+  };
+  {
+    const double pr1 = F3(f.pr1, j, i, 1), rho0 = F3(f.rho0, j, i, 1);
+    const double cc = xg * pr1 * dts / (c->dx * msfx);
+    F3(f.scc, j, i, 1) = cc;
+    F3(f.scdd, j, i, 1) = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[1]);
+    F3(f.scj, j, i, 1) = d_half * rho0 * EGRAV_NH * dts;
+    const double pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
+        (F3(cu, j, i, 1) + F3(cu, j + 1, i, 1) + F3(cu, j, i + 1, 1) + F3(cu, j + 1, i + 1, 1) -
+         F3(cu, j, i, 2) - F3(cu, j + 1, i, 2) - F3(cu, j, i + 1, 2) - F3(cu, j + 1, i + 1, 2)) /
+        (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
+    const double pyvp = 0.0625 * (F3(pr0, j, i + 1, 1) - F3(pr0, j, i - 1, 1)) *
+        (F3(cv, j, i, 1) + F3(cv, j + 1, i, 1) + F3(cv, j, i + 1, 1) + F3(cv, j + 1, i + 1, 1) -
+         F3(cv, j, i, 2) - F3(cv, j + 1, i, 2) - F3(cv, j, i + 1, 2) - F3(cv, j + 1, i + 1, 2)) /
+        (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
+    F3(f.pxup, j, i, 1) = pxup; F3(f.pyvp, j, i, 1) = pyvp;
+    F3(f.ptend, j, i, 1) = F3(f.ppten, j, i, 1) - d_half * cc * (divterm(1) - d_two * (pyvp + pxup));
+    F3(f.tk, j, i, 1) = (d_half * ps0 * F3(f.t0, j, i, 1)) / (xg * F3(pr0, j, i, 1) * F3(f.a2t, j, i, 1) * rpb);
+  }
+  for (int k = 2; k <= kz; k++) {
+    const int kp1 = (k + 1 < kz) ? k + 1 : kz, km1 = k - 1;
+    F3(f.tk, j, i, k) = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
+    const double rofac = (c->dsigma[km1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, km1)) /
+                         (c->dsigma[km1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, km1));
+    const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
+    const double cc = xg * pr1 * dts / (c->dx * msfx);
+    const double cdd = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+    const double cj = d_half * rho0 * EGRAV_NH * dts;
+    F3(f.scc, j, i, k) = cc; F3(f.scdd, j, i, k) = cdd; F3(f.scj, j, i, k) = cj;
+    const double ca = EGRAV_NH * dts / (F3(pr0, j, i, k) - F3(pr0, j, i, km1)) * rofac;
+    const double g1 = d_one - c->dsigma[km1] * F3(f.tk, j, i, k);
+    const double g2 = d_one + c->dsigma[k] * F3(f.tk, j, i, km1);
+    const double cdm = F3(f.scdd, j, i, km1), cjm = F3(f.scj, j, i, km1);
+    F3(f.sca, j, i, k) = ca; F3(f.sg1, j, i, k) = g1; F3(f.sg2, j, i, k) = g2;
+    F3(f.sc, j, i, k) = -ca * (cdm - cjm) * g2 * bpxbp;
+    F3(f.sb, j, i, k) = d_one + ca * (g1 * (cdd - cj) + g2 * (cdm + cjm)) * bpxbp;
+    F3(f.saa, j, i, k) = -ca * (cdd + cj) * g1 * bpxbp;
+    F3(f.pyvp, j, i, k) = 0.125 * (F3(pr0, j, i + 1, k) - F3(pr0, j, i - 1, k)) *
+        (F3(cv, j, i, km1) + F3(cv, j + 1, i, km1) + F3(cv, j, i + 1, km1) + F3(cv, j + 1, i + 1, km1) -
+         F3(cv, j, i, kp1) - F3(cv, j + 1, i, kp1) - F3(cv, j, i + 1, kp1) - F3(cv, j + 1, i + 1, kp1)) /
+        (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
+    F3(f.pxup, j, i, k) = 0.125 * (F3(pr0, j + 1, i, k) - F3(pr0, j - 1, i, k)) *
+        (F3(cu, j, i, km1) + F3(cu, j + 1, i, km1) + F3(cu, j, i + 1, km1) + F3(cu, j + 1, i + 1, km1) -
+         F3(cu, j, i, kp1) - F3(cu, j + 1, i, kp1) - F3(cu, j, i + 1, kp1) - F3(cu, j + 1, i + 1, kp1)) /
+        (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
+  }
+  F3(f.pyvp, j, i, kz) = F3(f.pyvp, j, i, kz) * d_half;
+  F3(f.pxup, j, i, kz) = F3(f.pxup, j, i, kz) * d_half;
+  for (int k = 2; k <= kz; k++) {
+    const double pt = F3(f.ppten, j, i, k) - d_half * F3(f.scc, j, i, k) *
+                      (divterm(k) - d_two * (F3(f.pyvp, j, i, k) + F3(f.pxup, j, i, k)));
+    F3(f.ptend, j, i, k) = pt;
+    const double cdm = F3(f.scdd, j, i, k - 1), cjm = F3(f.scj, j, i, k - 1);
+    const double cdk = F3(f.scdd, j, i, k), cjk = F3(f.scj, j, i, k);
+    const double g1 = F3(f.sg1, j, i, k), g2 = F3(f.sg2, j, i, k);
+    F3(f.rhs, j, i, k) = F3(w, j, i, k) + F3(f.wten, j, i, k) + F3(f.sca, j, i, k) *
+        (bpxbm * ((cdm - cjm) * g2 * F3(f.wo, j, i, k - 1) - ((cdm + cjm) * g2 + (cdk - cjk) * g1) * F3(f.wo, j, i, k) +
+                  (cdk + cjk) * g1 * F3(f.wo, j, i, k + 1)) +
+         (F3(pp, j, i, k) * g1 - F3(pp, j, i, k - 1) * g2) + (g1 * pt - g2 * F3(f.ptend, j, i, k - 1)) * bp);
+  }
+  for (int k = 1; k <= kz; k++) {
+    const double p = F3(pp, j, i, k);
+    F3(f.spi, j, i, k) = p;
+    F3(pp, j, i, k) = p + F3(f.ptend, j, i, k) +
+        (F3(f.scj, j, i, k) * (F3(f.wo, j, i, k + 1) + F3(f.wo, j, i, k)) +
+         F3(f.scdd, j, i, k) * (F3(f.wo, j, i, k + 1) - F3(f.wo, j, i, k))) * bm;
+  }
+  for (int k = kz; k >= 2; k--) {
+    const double denom = F3(f.saa, j, i, k) * F3(f.se, j, i, k) + F3(f.sb, j, i, k);
+    F3(f.se, j, i, k - 1) = -F3(f.sc, j, i, k) / denom;
+    F3(f.sf, j, i, k - 1) = (F3(f.rhs, j, i, k) - F3(f.sf, j, i, k) * F3(f.saa, j, i, k)) / denom;
+  }
+  if (c->ifupr == 1) {
+    const double cdd1 = F3(f.scdd, j, i, 1), cj1 = F3(f.scj, j, i, 1);
+    const double denom = (cdd1 + cj1) * bp;
+    F2(f.estore, j, i) = F3(pp, j, i, 1) + F3(f.sf, j, i, 1) * denom;
+    F2(f.astore, j, i) = denom * F3(f.se, j, i, 1) + (cj1 - cdd1) * bp;
+  }
+}
+
+// upper radiative condition coefficients (:500-543), one block: the domain means in the
+// reference's summation order by one thread, then one thread per mask entry
+__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f) {
+  __shared__ double sh[2];
+  if (threadIdx.x == 0) {
+    double atot = d_zero, rhontot = d_zero;
+    for (int i = g.ici1; i <= g.ici2; i++)
+      for (int j = g.jci1; j <= g.jci2; j++) {
+        atot = atot + F2(f.astore, j, i);
+        const double ensq = EGRAV_NH * EGRAV_NH / c->cpd / (F3(f.a2t, j, i, 1) * F2(f.rpsb, j, i));
+        rhontot = rhontot + F3(f.rho1, j, i, 1) * sqrt(ensq);
+      }
+    const double rnpts = d_one / (double)((g.giy - 3) * (g.gjx - 3));
+    sh[0] = atot * rnpts;
+    sh[1] = rhontot * rnpts;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= 169) return;
+  const int jj = t / 13 - 6, ii = t % 13 - 6;       // tmask(jj, ii) stored at [jj+6][ii+6]
+  const double abar = sh[0], rhon = sh[1];
+  const double dxmsfb = d_two / c->dxsq / c->nh_xmsf;
+  const double fi = (ii == -6 || ii == 6) ? d_half : d_one, fj = (jj == -6 || jj == 6) ? d_half : d_one;
+  const double ri = (double)ii, rj = (double)jj;
+  double acc = d_zero;
+  for (int kk = 0; kk <= 6; kk++) {
+    const double rkk = (double)kk, fk = (kk == 0 || kk == 6) ? d_one : d_two;
+    for (int ll = 0; ll <= 6; ll++) {
+      const double rll = (double)ll, fl = (ll == 0 || ll == 6) ? d_one : d_two;
+      const double xkeff = dxmsfb * sin(MATHPI * rkk / 12.0) * cos(MATHPI * rll / 12.0);
+      const double xleff = dxmsfb * sin(MATHPI * rll / 12.0) * cos(MATHPI * rkk / 12.0);
+      const double xkleff = sqrt(xkeff * xkeff + xleff * xleff);
+      acc = acc + (fi * fj * fk * fl) / 144.0 * cos(2.0 * MATHPI * rkk * ri / 12.0) *
+                      cos(2.0 * MATHPI * rll * rj / 12.0) * xkleff / (rhon - abar * xkleff);
+    }
+  }
+  f.tmask[t] = acc;
+}
+
+__device__ __forceinline__ void atomic_max_nonneg(unsigned long long* a, double v) {
+  atomicMax(a, (unsigned long long)__double_as_longlong(v));
+}
+
+// substep part D (:488-685), one thread per interior cross column: upper boundary value,
+// downward sweep of w, CFL of the sigma velocity, new pp and its temperature correction
+__global__ void k_nh_sound_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                             int istep) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const int kz = c->kz;
+  const double dt = s->dt, dts = dt / (double)istep;
+  const double bet = c->nhbet, bp = (d_one + bet) * d_half;
+  double* w = f.cw;
+  double* pp = f.cpp;
+  double wpval = d_zero;
+  if (c->ifupr == 1) {
+    const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
+    for (int nsi = -6; nsi <= 6; nsi++) {
+      int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
+      for (int nsj = -6; nsj <= 6; nsj++) {
+        int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
+        wpval = wpval + F2(f.estore, jnn, inn) * f.tmask[(nsj + 6) * 13 + (nsi + 6)];
+      }
+    }
+  }
+  F3(w, j, i, 1) = wpval;
+  double wk = wpval;
+  for (int k = 1; k <= kz; k++) {
+    wk = F3(f.se, j, i, k) * wk + F3(f.sf, j, i, k);
+    F3(w, j, i, k + 1) = wk;
+  }
+  // CFL (:624-640)
+  {
+    auto ucrs = [&](const double* a, int k) {
+      return F3(a, j, i, k) + F3(a, j, i + 1, k) + F3(a, j + 1, i, k) + F3(a, j + 1, i + 1, k);
+    };
+    double cfl = d_zero;
+    double uk = ucrs(f.cu, kz), vk = ucrs(f.cv, kz);
+    for (int k = kz; k >= 2; k--) {
+      const double um = ucrs(f.cu, k - 1), vm = ucrs(f.cv, k - 1);
+      const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(w, j, i, k) / F2(f.ps0, j, i) -
+          c->sigma[k] * (F2(f.dpsdxm, j, i) * (c->twt1[k] * uk + c->twt2[k] * um) +
+                         F2(f.dpsdym, j, i) * (c->twt1[k] * vk + c->twt2[k] * vm));
+      const double check = fabs(sigdot) * dt / (c->dsigma[k] + c->dsigma[k - 1]);
+      cfl = dmax(check, cfl);
+      uk = um; vk = vm;
+    }
+    atomic_max_nonneg(f.cfl, cfl);
+  }
+  const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i);
+  for (int k = 1; k <= kz; k++) {
+    const double ppold = F3(f.spi, j, i, k);
+    const double rho0 = F3(f.rho0, j, i, k);
+    const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+    const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
+    const double wp = F3(w, j, i, k + 1), wm = F3(w, j, i, k);
+    const double p = F3(pp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
+    F3(pp, j, i, k) = p;
+    F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
+    const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
+    const double dpterm = psb * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
+    F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
+    F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
+  }
+}
+
+// time filters after the acoustic loop (:686-702).  k = 1..kz+1.
+__global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f) {
+  FRAME_POINT();
+  const int kz = c->kz;
+  if (k <= kz && IN_DI(j, i)) {
+    const double pd = F2(f.psdotb, j, i);
+    const double u = pd * F3(f.cu, j, i, k), v = pd * F3(f.cv, j, i, k);
+    double d = c->gnu1 * (u + F3(f.a2u, j, i, k) - d_two * F3(f.a1u, j, i, k));
+    F3(f.a2u, j, i, k) = F3(f.a1u, j, i, k) + d;
+    F3(f.a1u, j, i, k) = u;
+    d = c->gnu1 * (v + F3(f.a2v, j, i, k) - d_two * F3(f.a1v, j, i, k));
+    F3(f.a2v, j, i, k) = F3(f.a1v, j, i, k) + d;
+    F3(f.a1v, j, i, k) = v;
+  }
+  if (k <= kz && IN_CI(j, i)) {
+    const double p = F2(f.psb, j, i) * F3(f.cpp, j, i, k);
+    const double d = c->gnu1 * (p + F3(f.a2pp, j, i, k) - d_two * F3(f.a1pp, j, i, k));
+    F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k) + d;
+    F3(f.a1pp, j, i, k) = p;
+  }
+  double w = F3(f.cw, j, i, k);
+  if (fabs(w) < DLOWVAL) w = d_zero;
+  if (IN_CI(j, i)) {
+    w = F2(f.psb, j, i) * w;
+    const double d = c->gnu2 * (w + F3(f.a2w, j, i, k) - d_two * F3(f.a1w, j, i, k));
+    F3(f.a2w, j, i, k) = F3(f.a1w, j, i, k) + d;
+    F3(f.a1w, j, i, k) = w;
+  }
+  F3(f.cw, j, i, k) = w;
+  if (fabs(F3(f.a2w, j, i, k)) < DLOWVAL) F3(f.a2w, j, i, k) = d_zero;
+  if (fabs(F3(f.a1w, j, i, k)) < DLOWVAL) F3(f.a1w, j, i, k) = d_zero;
+}
+
+// rcmtimer advance and the sound CFL stop (Main/mod_sound.F90:661-682,
+// Main/mod_tendency.F90:608-616)
+__global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f) {
+  const double cfl = __longlong_as_double((long long)*f.cfl);
+  if (cfl > d_one || cfl != cfl) s->nanflag = 1;
+  *f.cfl = 0ull;
+  s->lcount += 1;
+  if (s->lcount == 2) s->dt = d_two * c->dtsec;
+  s->ptntot = 0.0;
+  s->pt2tot = 0.0;
+}
+
+// pp and w boundary values of bdyval (Main/mod_bdycod.F90:1150-1160, 1196-1206, 1242-1252,
+// 1285-1295, 1707-1790), one block: copies and time interpolation first, then the w(k=1)
+// copies W/E on ici followed by S/N on jce (they read the W/E results at the corners)
+__global__ void k_nh_bdyval(Geom g, int KZ, const StepState* __restrict__ s, NHFields f) {
+  const double xt = s->xbctime + s->dt;
+  const bool integ = s->lcount > 0;
+  auto setp = [&](int j, int i) {
+    for (int k = 1; k <= KZ; k++) {
+      if (integ) F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k);
+      F3(f.a1pp, j, i, k) = F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k);
+    }
+    for (int k = 1; k <= KZ + 1; k++) {
+      if (integ) F3(f.a2w, j, i, k) = F3(f.a1w, j, i, k);
+      F3(f.a1w, j, i, k) = F3(f.wwb0, j, i, k) + xt * F3(f.wwbt, j, i, k);
+    }
+  };
+  const int nci = g.ici2 - g.ici1 + 1, ncj = g.jce2 - g.jce1 + 1;
+  for (int t = threadIdx.x; t < nci; t += blockDim.x) {
+    if (g.bl) setp(g.jce1, g.ici1 + t);
+    if (g.br) setp(g.jce2, g.ici1 + t);
+  }
+  for (int t = threadIdx.x; t < ncj; t += blockDim.x) {
+    if (g.bb) setp(g.jce1 + t, g.ice1);
+    if (g.bt) setp(g.jce1 + t, g.ice2);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < nci; t += blockDim.x) {
+    const int i = g.ici1 + t;
+    if (g.bl) F3(f.a1w, g.jce1, i, 1) = F3(f.a1w, g.jci1, i, 1);
+    if (g.br) F3(f.a1w, g.jce2, i, 1) = F3(f.a1w, g.jci2, i, 1);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ncj; t += blockDim.x) {
+    const int j = g.jce1 + t;
+    if (g.bb) F3(f.a1w, j, g.ice1, 1) = F3(f.a1w, j, g.ici1, 1);
+    if (g.bt) F3(f.a1w, j, g.ice2, 1) = F3(f.a1w, j, g.ici2, 1);
+  }
+}
+
+}  // namespace rcm

@@ -1,0 +1,67 @@
+// kernels_nh.hpp -- device kernels of the non-hydrostatic step (kernels_nh.hip) and the
+// argument block they share.
+#pragma once
+#include "engine.hpp"
+
+namespace rcm {
+
+// Every buffer of the non-hydrostatic step of one tile.  The NH core updates its state in
+// place (no ping-pong), one kernel per reference loop nest or per column recurrence, with
+// the intermediates the reference keeps in module arrays held in HBM.  Passed by value.
+struct NHFields {
+  // state (coupled with p*, as the reference stores it)
+  double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc;
+  double *a1pp, *a2pp, *a1w, *a2w, *psa, *psb;
+  // statics
+  const double *msfx, *msfd, *coriol, *ht, *xmsf, *dmsf, *hgfact;
+  const int8_t *rgcr, *rgdt;
+  const int16_t *ibcr, *ibdt;
+  const double *ps0, *pr0, *t0, *rho0, *z0, *pf0, *rhof0, *zf0, *dpsdxm, *dpsdym, *dprddx, *dprddy;
+  const double *ef, *ddx, *ddy, *dmdx, *dmdy, *ex, *crx, *cry;
+  // boundary data
+  const double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *ppb0, *ppbt, *wwb0, *wwbt;
+  // 2-D reciprocals (k_surface_pressures)
+  const double *rpsa, *rpsb, *rpsda, *rpsdb, *psdota, *psdotb;
+  // decoupled / derived fields of the step
+  double *umc, *vmc, *ud, *vd, *umd, *vmd, *xt, *xqv, *xqc, *xtv, *xpp, *xw, *pr1, *rho1, *xpr;
+  double *cr, *qdot, *ubd, *vbd, *tb3d, *qvb3d, *qcb3d, *ppb3d, *wb3d, *pb3d, *pf3d;
+  double *xkcr, *xkc, *xkd, *xkcf, *uavg1, *uavg2, *vavg1, *vavg2;
+  // tendencies: total (pc_total) and dynamic (pc_dynamic)
+  double *tten, *tdyn, *qvten, *qvdyn, *qcten, *qcdyn, *uten, *udyn, *vten, *vdyn;
+  double *ppten, *ppdyn, *wten, *wdyn;
+  // forecasts (atmc) and fixed moisture
+  double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
+  int* depplane;
+  // sound work (Main/mod_sound.F90:40-60)
+  double *wo, *se, *sf, *saa, *sb, *sc, *rhs, *sca, *sg1, *sg2, *ptend, *pxup, *pyvp, *tk;
+  double *scc, *scdd, *scj, *spi, *estore, *astore, *tmask;
+  unsigned long long* cfl;       // max CFL of the step (non-negative doubles as ordered bits)
+};
+
+__global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_uv_adv(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_curvature(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_adiabatic(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_diffusion(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it);
+__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_b(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
+__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_sound_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
+__global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);
+
+}  // namespace rcm
