@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 from regcm_amd.config import CONFIGS, set_nproc  # noqa: E402
 from regcm_amd import icbc  # noqa: E402
-from regcm_amd.traffic import kernel_bytes, step_bytes  # noqa: E402
+from regcm_amd.traffic import kernel_bytes, step_bytes, step_bytes_nh  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -92,7 +92,8 @@ def main():
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rc = CONFIGS[args.config]
-    data = icbc.generate(rc)
+    nh = rc.idynamic == 2
+    data = icbc.generate_nh(rc) if nh else icbc.generate(rc)
     cj, ci = set_nproc(world, rc.jx, rc.iy)
 
     from regcm_amd.dycore import DynCore, comm_unique_id
@@ -136,7 +137,13 @@ def main():
     # every rank (the eager steps exchange halos), after the timed region
     kt = eng.kernel_times(args.prof_steps) if args.prof_steps > 0 else {}
     barrier()
-    bstep = step_bytes(rc.jx, rc.iy, rc.kz, rc.nspgx)
+    if nh:
+        from regcm_amd.nhbase import acoustic_substeps
+        istep = acoustic_substeps(rc, data["split"]["nh_dtsmax"], 2.0 * rc.dt, 2)
+        bstep = step_bytes_nh(rc.jx, rc.iy, rc.kz, rc.nspgx, istep)
+    else:
+        istep = None
+        bstep = step_bytes(rc.jx, rc.iy, rc.kz, rc.nspgx)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -166,8 +173,9 @@ def main():
             achieved = b / (avg_ms * 1e-3) / 1e9
             roof.update({"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "traffic": traffic})
     step_achieved = bstep / t_step / 1e9
+    core = "non-hydrostatic" if nh else "hydrostatic"
     line = {
-        "metric": "simulated-years/wall-day, 192x192x23 sigma grid (hydrostatic dyn step)",
+        "metric": f"simulated-years/wall-day, {rc.jx}x{rc.iy}x{rc.kz} sigma grid ({core} dyn step)",
         "value": sypd,
         "unit": "simulated-years/wall-day",
         "n_gpus": world,
@@ -178,15 +186,19 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (syn-icbc v1, PCG64 seed 20261015): no DOMAIN/ICBC files offline",
-        "config": {"workload": f"{args.config} {rc.jx}x{rc.iy}x{rc.kz} ds={rc.ds}km dt={rc.dt}s "
-                               "hydrostatic, upstream adv + 4th-order diff + split-explicit "
-                               "(nsplit=2) + iboudy=5 relaxation, physics stubbed",
+        "data": ("synthetic (syn-icbc v1" + (" NH variant" if nh else "") +
+                 ", PCG64 seed 20261015): no DOMAIN/ICBC files offline"),
+        "config": {"workload": (f"{args.config} {rc.jx}x{rc.iy}x{rc.kz} ds={rc.ds}km dt={rc.dt}s " +
+                                ("non-hydrostatic (MM5 core), upstream adv + 4th-order diff + sound "
+                                 f"({istep} acoustic sub-steps, upper radiative BC, Rayleigh damping) "
+                                 "+ iboudy=5 relaxation, physics stubbed" if nh else
+                                 "hydrostatic, upstream adv + 4th-order diff + split-explicit "
+                                 "(nsplit=2) + iboudy=5 relaxation, physics stubbed")),
                    "tiles": f"{cj}x{ci}", "step": "tend + bdyval"},
         "roofline": roof,
         "step_roofline": {"achieved": step_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": step_achieved / HBM_PEAK_GBS, "algorithmic_bytes": bstep,
-                          "note": "SURVEY 8(d) B_h per step / wall time per step"},
+                          "note": "SURVEY 8(d) " + ("B_nh" if nh else "B_h") + " per step / wall time per step"},
         "kernel_us": {k: round(v[1] * 1e3, 2) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0] * kv[1][1])},
         "device_ms_per_step": dev_ms,
     }

@@ -405,7 +405,7 @@ struct rcmdyn_engine {
     f.ef = dalloc(t, P); f.ddx = dalloc(t, P); f.ddy = dalloc(t, P); f.dmdx = dalloc(t, P); f.dmdy = dalloc(t, P);
     f.ex = dalloc(t, P); f.crx = dalloc(t, P); f.cry = dalloc(t, P);
     f.estore = dalloc(t, P); f.astore = dalloc(t, P); f.tmask = dalloc(t, 169);
-    f.cfl = talloc<unsigned long long>(t, 1);
+    f.cfl = talloc<unsigned long long>(t, NH_CFL_SLOTS);
     nhf.push_back(f);
   }
 
@@ -948,15 +948,18 @@ struct rcmdyn_engine {
     for (int it = 1; it <= istep; it++) {
       KLAUNCH(k_nh_sound_a, grid3(nce_j, nce_i, 1), BLK, 0, stream, g, dc, f, it);
       KLAUNCH(k_nh_sound_uv, grid3(ndi_j, ndi_i, kz), BLK, 0, stream, g, dc, ds, f, istep);
-      KLAUNCH(k_nh_sound_b, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, ds, f, istep, it);
+      KLAUNCH(k_nh_sound_b1, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, ds, f, istep, it);
+      KLAUNCH(k_nh_sound_b2, grid3(nci_j, nci_i, kz - 1), BLK, 0, stream, g, dc, ds, f, istep);
+      KLAUNCH(k_nh_sound_b3, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
       if (cfg.ifupr == 1 && it == 1 && alarm) {
         KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, g, dc, f);
         nh_tmask_valid = true;
       }
-      KLAUNCH(k_nh_sound_c, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, ds, f, istep);
+      KLAUNCH(k_nh_sound_c1, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_sound_c2, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, ds, f, istep);
     }
     KLAUNCH(k_nh_sound_final, fr, BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_advance, dim3(1), dim3(1), 0, stream, dc, ds, f);
+    KLAUNCH(k_nh_advance, dim3(1), dim3(256), 0, stream, dc, ds, f);
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
   }
@@ -974,7 +977,9 @@ struct rcmdyn_engine {
             g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c], t.a2qv[c],
             t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt, t.pb0, t.pbt,
             sl, slen, 0);
-    KLAUNCH(k_nh_bdyval, dim3(1), dim3(256), 0, stream, g, kz, ds, nhfields(t));
+    const int nperim = 2 * (g.ici2 - g.ici1 + 1) + 2 * (g.jce2 - g.jce1 + 1);
+    KLAUNCH(k_nh_bdyval, dim3((nperim + 63) / 64, kz + 1), dim3(64), 0, stream, g, kz, ds, nhfields(t));
+    KLAUNCH(k_nh_bdyval_w1, dim3(1), dim3(256), 0, stream, g, nhfields(t));
     KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
             t.a1qc[c], t.a1qv[c], t.psa_[c], sl, slen, ds, cfg.dtsec, 1);
     hs.xbctime = hs.xbctime + cfg.dtsec;

@@ -769,118 +769,131 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
   F3(f.cv, j, i, k) = v + F3(f.vten, j, i, k);
 }
 
-// substep part C (:297-483), one thread per interior cross column: undo the divergence
-// damping, lower boundary w, Ikawa coefficients, pp predictor, upward sweep of the
-// tridiagonal w system, upper radiative condition inputs
-__global__ void k_nh_sound_b(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                             int istep, int it) {
+// substep part C (:297-483) in three launches: level-parallel coefficients (C1, C2), then
+// the column work (C3).
+// C1, one thread per interior cross point and level: undo the divergence damping of pp,
+// lower-boundary w (k = 1 threads: it seeds the sweep), Ikawa coefficients cc/cdd/cj, the
+// temperature factor tk, the horizontal pressure-advection terms and ptend
+__global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep, int it) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double dts = s->dt / (double)istep;
-  const double bet = c->nhbet, xg = c->xgamma;
-  const double bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
-  const double bpxbp = bp * bp, bpxbm = bp * bm;
-  double* pp = f.cpp;
-  double* w = f.cw;
+  const double xg = c->xgamma;
   const double* cu = f.cu;
   const double* cv = f.cv;
-  if (it > 1)
-    for (int k = 1; k <= kz; k++) F3(pp, j, i, k) = F3(pp, j, i, k) - c->nhxkd * F3(f.spi, j, i, k);
-  for (int k = 1; k <= kz + 1; k++) F3(f.wo, j, i, k) = F3(w, j, i, k);
-  const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
-  F3(w, j, i, kz + 1) = d_half * d_rfour * c->regrav *
-      ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
-           (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
-       (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
-           (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
-      (c->dx * msfx);
-  F3(f.se, j, i, kz) = d_zero;
-  F3(f.sf, j, i, kz) = F3(w, j, i, kz + 1);
   const double* pr0 = f.pr0;
-  auto divterm = [&](int k) {
-    const double* m = f.msfd;
-    return (F3(cv, j, i + 1, k) * F2(m, j, i + 1) - F3(cv, j, i, k) * F2(m, j, i) +
-            F3(cv, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cv, j + 1, i, k) * F2(m, j + 1, i) +
-            F3(cu, j + 1, i, k) * F2(m, j + 1, i) - F3(cu, j, i, k) * F2(m, j, i) +
-            F3(cu, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cu, j, i + 1, k) * F2(m, j, i + 1)) / msfx;
-  };
-  {
-    const double pr1 = F3(f.pr1, j, i, 1), rho0 = F3(f.rho0, j, i, 1);
-    const double cc = xg * pr1 * dts / (c->dx * msfx);
-    F3(f.scc, j, i, 1) = cc;
-    F3(f.scdd, j, i, 1) = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[1]);
-    F3(f.scj, j, i, 1) = d_half * rho0 * EGRAV_NH * dts;
-    const double pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
+  if (it > 1) F3(f.cpp, j, i, k) = F3(f.cpp, j, i, k) - c->nhxkd * F3(f.spi, j, i, k);
+  const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
+  if (k == 1) {
+    F3(f.se, j, i, kz) = d_zero;
+    F3(f.sf, j, i, kz) = d_half * d_rfour * c->regrav *
+        ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
+             (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
+         (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
+             (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
+        (c->dx * msfx);
+  }
+  const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
+  const double cc = xg * pr1 * dts / (c->dx * msfx);
+  F3(f.scc, j, i, k) = cc;
+  F3(f.scdd, j, i, k) = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+  F3(f.scj, j, i, k) = d_half * rho0 * EGRAV_NH * dts;
+  F3(f.tk, j, i, k) = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
+  double pxup, pyvp;
+  if (k == 1) {
+    pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
         (F3(cu, j, i, 1) + F3(cu, j + 1, i, 1) + F3(cu, j, i + 1, 1) + F3(cu, j + 1, i + 1, 1) -
          F3(cu, j, i, 2) - F3(cu, j + 1, i, 2) - F3(cu, j, i + 1, 2) - F3(cu, j + 1, i + 1, 2)) /
         (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
-    const double pyvp = 0.0625 * (F3(pr0, j, i + 1, 1) - F3(pr0, j, i - 1, 1)) *
+    pyvp = 0.0625 * (F3(pr0, j, i + 1, 1) - F3(pr0, j, i - 1, 1)) *
         (F3(cv, j, i, 1) + F3(cv, j + 1, i, 1) + F3(cv, j, i + 1, 1) + F3(cv, j + 1, i + 1, 1) -
          F3(cv, j, i, 2) - F3(cv, j + 1, i, 2) - F3(cv, j, i + 1, 2) - F3(cv, j + 1, i + 1, 2)) /
         (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
-    F3(f.pxup, j, i, 1) = pxup; F3(f.pyvp, j, i, 1) = pyvp;
-    F3(f.ptend, j, i, 1) = F3(f.ppten, j, i, 1) - d_half * cc * (divterm(1) - d_two * (pyvp + pxup));
-    F3(f.tk, j, i, 1) = (d_half * ps0 * F3(f.t0, j, i, 1)) / (xg * F3(pr0, j, i, 1) * F3(f.a2t, j, i, 1) * rpb);
-  }
-  for (int k = 2; k <= kz; k++) {
+  } else {
     const int kp1 = (k + 1 < kz) ? k + 1 : kz, km1 = k - 1;
-    F3(f.tk, j, i, k) = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
-    const double rofac = (c->dsigma[km1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, km1)) /
-                         (c->dsigma[km1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, km1));
-    const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
-    const double cc = xg * pr1 * dts / (c->dx * msfx);
-    const double cdd = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
-    const double cj = d_half * rho0 * EGRAV_NH * dts;
-    F3(f.scc, j, i, k) = cc; F3(f.scdd, j, i, k) = cdd; F3(f.scj, j, i, k) = cj;
-    const double ca = EGRAV_NH * dts / (F3(pr0, j, i, k) - F3(pr0, j, i, km1)) * rofac;
-    const double g1 = d_one - c->dsigma[km1] * F3(f.tk, j, i, k);
-    const double g2 = d_one + c->dsigma[k] * F3(f.tk, j, i, km1);
-    const double cdm = F3(f.scdd, j, i, km1), cjm = F3(f.scj, j, i, km1);
-    F3(f.sca, j, i, k) = ca; F3(f.sg1, j, i, k) = g1; F3(f.sg2, j, i, k) = g2;
-    F3(f.sc, j, i, k) = -ca * (cdm - cjm) * g2 * bpxbp;
-    F3(f.sb, j, i, k) = d_one + ca * (g1 * (cdd - cj) + g2 * (cdm + cjm)) * bpxbp;
-    F3(f.saa, j, i, k) = -ca * (cdd + cj) * g1 * bpxbp;
-    F3(f.pyvp, j, i, k) = 0.125 * (F3(pr0, j, i + 1, k) - F3(pr0, j, i - 1, k)) *
+    pyvp = 0.125 * (F3(pr0, j, i + 1, k) - F3(pr0, j, i - 1, k)) *
         (F3(cv, j, i, km1) + F3(cv, j + 1, i, km1) + F3(cv, j, i + 1, km1) + F3(cv, j + 1, i + 1, km1) -
          F3(cv, j, i, kp1) - F3(cv, j + 1, i, kp1) - F3(cv, j, i + 1, kp1) - F3(cv, j + 1, i + 1, kp1)) /
         (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
-    F3(f.pxup, j, i, k) = 0.125 * (F3(pr0, j + 1, i, k) - F3(pr0, j - 1, i, k)) *
+    pxup = 0.125 * (F3(pr0, j + 1, i, k) - F3(pr0, j - 1, i, k)) *
         (F3(cu, j, i, km1) + F3(cu, j + 1, i, km1) + F3(cu, j, i + 1, km1) + F3(cu, j + 1, i + 1, km1) -
          F3(cu, j, i, kp1) - F3(cu, j + 1, i, kp1) - F3(cu, j, i + 1, kp1) - F3(cu, j + 1, i + 1, kp1)) /
         (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
+    if (k == kz) { pyvp = pyvp * d_half; pxup = pxup * d_half; }
   }
-  F3(f.pyvp, j, i, kz) = F3(f.pyvp, j, i, kz) * d_half;
-  F3(f.pxup, j, i, kz) = F3(f.pxup, j, i, kz) * d_half;
-  for (int k = 2; k <= kz; k++) {
-    const double pt = F3(f.ppten, j, i, k) - d_half * F3(f.scc, j, i, k) *
-                      (divterm(k) - d_two * (F3(f.pyvp, j, i, k) + F3(f.pxup, j, i, k)));
-    F3(f.ptend, j, i, k) = pt;
-    const double cdm = F3(f.scdd, j, i, k - 1), cjm = F3(f.scj, j, i, k - 1);
-    const double cdk = F3(f.scdd, j, i, k), cjk = F3(f.scj, j, i, k);
-    const double g1 = F3(f.sg1, j, i, k), g2 = F3(f.sg2, j, i, k);
-    F3(f.rhs, j, i, k) = F3(w, j, i, k) + F3(f.wten, j, i, k) + F3(f.sca, j, i, k) *
-        (bpxbm * ((cdm - cjm) * g2 * F3(f.wo, j, i, k - 1) - ((cdm + cjm) * g2 + (cdk - cjk) * g1) * F3(f.wo, j, i, k) +
-                  (cdk + cjk) * g1 * F3(f.wo, j, i, k + 1)) +
-         (F3(pp, j, i, k) * g1 - F3(pp, j, i, k - 1) * g2) + (g1 * pt - g2 * F3(f.ptend, j, i, k - 1)) * bp);
-  }
+  const double* m = f.msfd;
+  const double div = (F3(cv, j, i + 1, k) * F2(m, j, i + 1) - F3(cv, j, i, k) * F2(m, j, i) +
+                      F3(cv, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cv, j + 1, i, k) * F2(m, j + 1, i) +
+                      F3(cu, j + 1, i, k) * F2(m, j + 1, i) - F3(cu, j, i, k) * F2(m, j, i) +
+                      F3(cu, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cu, j, i + 1, k) * F2(m, j, i + 1)) / msfx;
+  F3(f.ptend, j, i, k) = F3(f.ppten, j, i, k) - d_half * cc * (div - d_two * (pyvp + pxup));
+}
+
+// C2, one thread per interior cross point and level k = 2..kz: tridiagonal coefficients and
+// right-hand side of the implicit w equation (Ikawa), Main/mod_sound.F90:400-457
+__global__ void k_nh_sound_b2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep) {
+  const int j = g.jci1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int i = g.ici1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int k = (int)blockIdx.z + 2;
+  if (!IN_CI(j, i) || k > c->kz) return;
+  const double dts = s->dt / (double)istep;
+  const double bet = c->nhbet;
+  const double bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
+  const double bpxbp = bp * bp, bpxbm = bp * bm;
+  const int km1 = k - 1;
+  const double rofac = (c->dsigma[km1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, km1)) /
+                       (c->dsigma[km1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, km1));
+  const double ca = EGRAV_NH * dts / (F3(f.pr0, j, i, k) - F3(f.pr0, j, i, km1)) * rofac;
+  const double g1 = d_one - c->dsigma[km1] * F3(f.tk, j, i, k);
+  const double g2 = d_one + c->dsigma[k] * F3(f.tk, j, i, km1);
+  const double cdm = F3(f.scdd, j, i, km1), cjm = F3(f.scj, j, i, km1);
+  const double cdk = F3(f.scdd, j, i, k), cjk = F3(f.scj, j, i, k);
+  F3(f.sc, j, i, k) = -ca * (cdm - cjm) * g2 * bpxbp;
+  F3(f.sb, j, i, k) = d_one + ca * (g1 * (cdk - cjk) + g2 * (cdm + cjm)) * bpxbp;
+  F3(f.saa, j, i, k) = -ca * (cdk + cjk) * g1 * bpxbp;
+  const double* w = f.cw;                       // still the old w (wo) on levels 1..kz+1
+  F3(f.rhs, j, i, k) = F3(w, j, i, k) + F3(f.wten, j, i, k) + ca *
+      (bpxbm * ((cdm - cjm) * g2 * F3(w, j, i, k - 1) - ((cdm + cjm) * g2 + (cdk - cjk) * g1) * F3(w, j, i, k) +
+                (cdk + cjk) * g1 * F3(w, j, i, k + 1)) +
+       (F3(f.cpp, j, i, k) * g1 - F3(f.cpp, j, i, k - 1) * g2) +
+       (g1 * F3(f.ptend, j, i, k) - g2 * F3(f.ptend, j, i, k - 1)) * bp);
+  (void)bm;
+}
+
+// C3, one thread per interior cross column: pp predictor (:458-464), upward sweep of the
+// tridiagonal system (:468-476), inputs of the upper radiative condition (:488-494)
+__global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const int kz = c->kz;
+  const double bet = c->nhbet, bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
+  const double* w = f.cw;
+  double wk = F3(w, j, i, 1);
   for (int k = 1; k <= kz; k++) {
-    const double p = F3(pp, j, i, k);
+    const double wk1 = F3(w, j, i, k + 1);
+    const double p = F3(f.cpp, j, i, k);
     F3(f.spi, j, i, k) = p;
-    F3(pp, j, i, k) = p + F3(f.ptend, j, i, k) +
-        (F3(f.scj, j, i, k) * (F3(f.wo, j, i, k + 1) + F3(f.wo, j, i, k)) +
-         F3(f.scdd, j, i, k) * (F3(f.wo, j, i, k + 1) - F3(f.wo, j, i, k))) * bm;
+    F3(f.cpp, j, i, k) = p + F3(f.ptend, j, i, k) +
+        (F3(f.scj, j, i, k) * (wk1 + wk) + F3(f.scdd, j, i, k) * (wk1 - wk)) * bm;
+    wk = wk1;
   }
+  double e = F3(f.se, j, i, kz), ff = F3(f.sf, j, i, kz);
   for (int k = kz; k >= 2; k--) {
-    const double denom = F3(f.saa, j, i, k) * F3(f.se, j, i, k) + F3(f.sb, j, i, k);
-    F3(f.se, j, i, k - 1) = -F3(f.sc, j, i, k) / denom;
-    F3(f.sf, j, i, k - 1) = (F3(f.rhs, j, i, k) - F3(f.sf, j, i, k) * F3(f.saa, j, i, k)) / denom;
+    const double aa = F3(f.saa, j, i, k);
+    const double denom = aa * e + F3(f.sb, j, i, k);
+    e = -F3(f.sc, j, i, k) / denom;
+    ff = (F3(f.rhs, j, i, k) - ff * aa) / denom;
+    F3(f.se, j, i, k - 1) = e;
+    F3(f.sf, j, i, k - 1) = ff;
   }
   if (c->ifupr == 1) {
     const double cdd1 = F3(f.scdd, j, i, 1), cj1 = F3(f.scj, j, i, 1);
     const double denom = (cdd1 + cj1) * bp;
-    F2(f.estore, j, i) = F3(pp, j, i, 1) + F3(f.sf, j, i, 1) * denom;
-    F2(f.astore, j, i) = denom * F3(f.se, j, i, 1) + (cj1 - cdd1) * bp;
+    F2(f.estore, j, i) = F3(f.cpp, j, i, 1) + ff * denom;
+    F2(f.astore, j, i) = denom * e + (cj1 - cdd1) * bp;
   }
 }
 
@@ -923,71 +936,99 @@ __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f) {
   f.tmask[t] = acc;
 }
 
-__device__ __forceinline__ void atomic_max_nonneg(unsigned long long* a, double v) {
-  atomicMax(a, (unsigned long long)__double_as_longlong(v));
-}
 
-// substep part D (:488-685), one thread per interior cross column: upper boundary value,
-// downward sweep of w, CFL of the sigma velocity, new pp and its temperature correction
-__global__ void k_nh_sound_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                             int istep) {
-  THREAD_POINT(g.jci1, g.ici1);
+// substep part D (:488-685) in two launches.
+// D1, 64 x 4 interior columns per block: upper boundary value from the 13 x 13 convolution
+// of estore (staged in LDS, clamped to the interior) and the downward sweep of w
+__global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, const Consts* __restrict__ c, NHFields f) {
+  __shared__ double sE[4 + 12][64 + 12];
+  __shared__ double sM[169];
+  const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
+  const int J0 = g.jci1 + (int)blockIdx.x * 64, I0 = g.ici1 + (int)blockIdx.y * 4;
+  const int tid = threadIdx.y * 64 + threadIdx.x;
+  const bool upr = c->ifupr == 1;
+  if (upr) {
+    for (int q = tid; q < 16 * 76; q += 256) {
+      const int jj = q % 76, ii = q / 76;
+      int jn = J0 - 6 + jj, in_ = I0 - 6 + ii;
+      jn = (jn < jlo) ? jlo : (jn > jhi ? jhi : jn);
+      in_ = (in_ < ilo) ? ilo : (in_ > ihi ? ihi : in_);
+      sE[ii][jj] = F2(f.estore, jn, in_);
+    }
+    if (tid < 169) sM[tid] = f.tmask[tid];
+    __syncthreads();
+  }
+  const int j = J0 + (int)threadIdx.x, i = I0 + (int)threadIdx.y;
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
-  const double dt = s->dt, dts = dt / (double)istep;
-  const double bet = c->nhbet, bp = (d_one + bet) * d_half;
-  double* w = f.cw;
-  double* pp = f.cpp;
   double wpval = d_zero;
-  if (c->ifupr == 1) {
-    const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
+  if (upr) {
     for (int nsi = -6; nsi <= 6; nsi++) {
       int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
       for (int nsj = -6; nsj <= 6; nsj++) {
         int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
-        wpval = wpval + F2(f.estore, jnn, inn) * f.tmask[(nsj + 6) * 13 + (nsi + 6)];
+        wpval = wpval + sE[inn - I0 + 6][jnn - J0 + 6] * sM[(nsj + 6) * 13 + (nsi + 6)];
       }
     }
   }
+  double* w = f.cw;
   F3(w, j, i, 1) = wpval;
   double wk = wpval;
   for (int k = 1; k <= kz; k++) {
     wk = F3(f.se, j, i, k) * wk + F3(f.sf, j, i, k);
     F3(w, j, i, k + 1) = wk;
   }
-  // CFL (:624-640)
-  {
-    auto ucrs = [&](const double* a, int k) {
-      return F3(a, j, i, k) + F3(a, j, i + 1, k) + F3(a, j + 1, i, k) + F3(a, j + 1, i + 1, k);
+}
+
+// D2, one thread per interior cross point and level: CFL of the sigma velocity (:624-640),
+// the new pp (:661-674) and its temperature correction (:675-681)
+__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep) {
+  THREAD_POINT(g.jci1, g.ici1);
+  const bool active = IN_CI(j, i);
+  const double dt = s->dt, dts = dt / (double)istep;
+  const double bet = c->nhbet, bp = (d_one + bet) * d_half;
+  const double* w = f.cw;
+  // CFL maximum: wavefront reduction, one atomic per wavefront (non-negative doubles order
+  // like their bit patterns; a NaN sorts above every finite value and raises the stop)
+  double cfl = d_zero;
+  if (active && k >= 2) {
+    auto crs = [&](const double* a, int kk) {
+      return F3(a, j, i, kk) + F3(a, j, i + 1, kk) + F3(a, j + 1, i, kk) + F3(a, j + 1, i + 1, kk);
     };
-    double cfl = d_zero;
-    double uk = ucrs(f.cu, kz), vk = ucrs(f.cv, kz);
-    for (int k = kz; k >= 2; k--) {
-      const double um = ucrs(f.cu, k - 1), vm = ucrs(f.cv, k - 1);
-      const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(w, j, i, k) / F2(f.ps0, j, i) -
-          c->sigma[k] * (F2(f.dpsdxm, j, i) * (c->twt1[k] * uk + c->twt2[k] * um) +
-                         F2(f.dpsdym, j, i) * (c->twt1[k] * vk + c->twt2[k] * vm));
-      const double check = fabs(sigdot) * dt / (c->dsigma[k] + c->dsigma[k - 1]);
-      cfl = dmax(check, cfl);
-      uk = um; vk = vm;
-    }
-    atomic_max_nonneg(f.cfl, cfl);
+    const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(w, j, i, k) / F2(f.ps0, j, i) -
+        c->sigma[k] * (F2(f.dpsdxm, j, i) * (c->twt1[k] * crs(f.cu, k) + c->twt2[k] * crs(f.cu, k - 1)) +
+                       F2(f.dpsdym, j, i) * (c->twt1[k] * crs(f.cv, k) + c->twt2[k] * crs(f.cv, k - 1)));
+    cfl = dmax(fabs(sigdot) * dt / (c->dsigma[k] + c->dsigma[k - 1]), d_zero);
   }
-  const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i);
-  for (int k = 1; k <= kz; k++) {
-    const double ppold = F3(f.spi, j, i, k);
-    const double rho0 = F3(f.rho0, j, i, k);
-    const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
-    const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
-    const double wp = F3(w, j, i, k + 1), wm = F3(w, j, i, k);
-    const double p = F3(pp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
-    F3(pp, j, i, k) = p;
-    F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
-    const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
-    const double dpterm = psb * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
-    F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
-    F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
+  unsigned long long bits = (unsigned long long)__double_as_longlong(cfl);
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(bits, off);
+    bits = (o > bits) ? o : bits;
   }
+  __shared__ unsigned long long sred[4];
+  const int wv = threadIdx.y;                          // blockDim = 64 x 4: one wavefront per row
+  if (threadIdx.x == 0) sred[wv] = bits;
+  __syncthreads();
+  if (threadIdx.x == 0 && wv == 0) {
+    unsigned long long b = sred[0];
+    for (int q = 1; q < 4; q++) b = (sred[q] > b) ? sred[q] : b;
+    const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * 7919u) & (NH_CFL_SLOTS - 1);
+    if (b != 0ull) atomicMax(&f.cfl[slot], b);
+  }
+  if (!active) return;
+  const double ppold = F3(f.spi, j, i, k);
+  const double rho0 = F3(f.rho0, j, i, k);
+  const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (F2(f.ps0, j, i) * c->dsigma[k]);
+  const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
+  const double wp = F3(w, j, i, k + 1), wm = F3(w, j, i, k);
+  const double p = F3(f.cpp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
+  F3(f.cpp, j, i, k) = p;
+  F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
+  const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
+  const double dpterm = F2(f.psb, j, i) * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
+  F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
+  F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
 }
 
 // time filters after the acoustic loop (:686-702).  k = 1..kz+1.
@@ -1026,9 +1067,22 @@ __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields 
 // rcmtimer advance and the sound CFL stop (Main/mod_sound.F90:661-682,
 // Main/mod_tendency.F90:608-616)
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f) {
-  const double cfl = __longlong_as_double((long long)*f.cfl);
+  __shared__ unsigned long long sm[256];
+  unsigned long long b = 0ull;
+  for (int q = threadIdx.x; q < NH_CFL_SLOTS; q += blockDim.x) {
+    const unsigned long long v = f.cfl[q];
+    b = (v > b) ? v : b;
+    f.cfl[q] = 0ull;
+  }
+  sm[threadIdx.x] = b;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sm[threadIdx.x] = (sm[threadIdx.x + w] > sm[threadIdx.x]) ? sm[threadIdx.x + w] : sm[threadIdx.x];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double cfl = __longlong_as_double((long long)sm[0]);
   if (cfl > d_one || cfl != cfl) s->nanflag = 1;
-  *f.cfl = 0ull;
   s->lcount += 1;
   if (s->lcount == 2) s->dt = d_two * c->dtsec;
   s->ptntot = 0.0;
@@ -1036,31 +1090,30 @@ __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHField
 }
 
 // pp and w boundary values of bdyval (Main/mod_bdycod.F90:1150-1160, 1196-1206, 1242-1252,
-// 1285-1295, 1707-1790), one block: copies and time interpolation first, then the w(k=1)
-// copies W/E on ici followed by S/N on jce (they read the W/E results at the corners)
-__global__ void k_nh_bdyval(Geom g, int KZ, const StepState* __restrict__ s, NHFields f) {
+// 1285-1295, 1707-1790).  A: copies and time interpolation, one thread per boundary cross
+// point and level; B (one block): the w(k=1) copies W/E on ici, then S/N on jce (they read
+// the W/E results at the corners).
+__global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f) {
+  const int nci = g.ici2 - g.ici1 + 1, ncj = g.jce2 - g.jce1 + 1;
+  const int p = (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
+  int j, i;
+  if (p < nci) { if (!g.bl) return; j = g.jce1; i = g.ici1 + p; }
+  else if (p < 2 * nci) { if (!g.br) return; j = g.jce2; i = g.ici1 + p - nci; }
+  else if (p < 2 * nci + ncj) { if (!g.bb) return; j = g.jce1 + p - 2 * nci; i = g.ice1; }
+  else if (p < 2 * nci + 2 * ncj) { if (!g.bt) return; j = g.jce1 + p - 2 * nci - ncj; i = g.ice2; }
+  else return;
   const double xt = s->xbctime + s->dt;
   const bool integ = s->lcount > 0;
-  auto setp = [&](int j, int i) {
-    for (int k = 1; k <= KZ; k++) {
-      if (integ) F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k);
-      F3(f.a1pp, j, i, k) = F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k);
-    }
-    for (int k = 1; k <= KZ + 1; k++) {
-      if (integ) F3(f.a2w, j, i, k) = F3(f.a1w, j, i, k);
-      F3(f.a1w, j, i, k) = F3(f.wwb0, j, i, k) + xt * F3(f.wwbt, j, i, k);
-    }
-  };
+  if (k <= kz) {
+    if (integ) F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k);
+    F3(f.a1pp, j, i, k) = F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k);
+  }
+  if (integ) F3(f.a2w, j, i, k) = F3(f.a1w, j, i, k);
+  F3(f.a1w, j, i, k) = F3(f.wwb0, j, i, k) + xt * F3(f.wwbt, j, i, k);
+}
+
+__global__ void k_nh_bdyval_w1(Geom g, NHFields f) {
   const int nci = g.ici2 - g.ici1 + 1, ncj = g.jce2 - g.jce1 + 1;
-  for (int t = threadIdx.x; t < nci; t += blockDim.x) {
-    if (g.bl) setp(g.jce1, g.ici1 + t);
-    if (g.br) setp(g.jce2, g.ici1 + t);
-  }
-  for (int t = threadIdx.x; t < ncj; t += blockDim.x) {
-    if (g.bb) setp(g.jce1 + t, g.ice1);
-    if (g.bt) setp(g.jce1 + t, g.ice2);
-  }
-  __syncthreads();
   for (int t = threadIdx.x; t < nci; t += blockDim.x) {
     const int i = g.ici1 + t;
     if (g.bl) F3(f.a1w, g.jce1, i, 1) = F3(f.a1w, g.jci1, i, 1);

@@ -35,8 +35,10 @@ struct NHFields {
   // sound work (Main/mod_sound.F90:40-60)
   double *wo, *se, *sf, *saa, *sb, *sc, *rhs, *sca, *sg1, *sg2, *ptend, *pxup, *pyvp, *tk;
   double *scc, *scdd, *scj, *spi, *estore, *astore, *tmask;
-  unsigned long long* cfl;       // max CFL of the step (non-negative doubles as ordered bits)
+  unsigned long long* cfl;       // NH_CFL_SLOTS partial maxima of the step's CFL (non-negative
+                                 // doubles as ordered bits), reduced by k_nh_advance
 };
+constexpr int NH_CFL_SLOTS = 1024;
 
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
@@ -57,11 +59,15 @@ __global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepSta
 __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it);
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
-__global__ void k_nh_sound_b(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
+__global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
+__global__ void k_nh_sound_b2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_sound_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_c1(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
 __global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_bdyval_w1(Geom g, NHFields f);
 
 }  // namespace rcm

@@ -52,3 +52,11 @@ def step_bytes(jx: int, iy: int, kz: int, nspgx: int) -> float:
     n3, n2 = jx * iy * kz, jx * iy
     fb = band_fraction(jx, iy, nspgx)
     return 8.0 * (n3 * (20 + 8 * fb) + n2 * (19 + 2 * fb))
+
+
+def step_bytes_nh(jx: int, iy: int, kz: int, nspgx: int, istep: int) -> float:
+    """SURVEY.md section 8(d) B_nh: compulsory HBM bytes of one non-hydrostatic step,
+    8 [N3 (34 + 12 f_b + 22 istep) + 21 N2]."""
+    n3, n2 = jx * iy * kz, jx * iy
+    fb = band_fraction(jx, iy, nspgx)
+    return 8.0 * (n3 * (34 + 12 * fb + 22 * istep) + n2 * 21)
