@@ -37,6 +37,9 @@ class RcclComm final : public Comm {
     for (const Xfer& x : recvs) NCCLCHK(ncclRecv(x.ptr, x.count, ncclDouble, x.peer, comm_, stream_));
     NCCLCHK(ncclGroupEnd());
   }
+  void allreduce_sum(double* p, size_t count) override {
+    NCCLCHK(ncclAllReduce(p, p, count, ncclDouble, ncclSum, comm_, stream_));
+  }
   bool graph_safe() const override { return false; }
 
  private:

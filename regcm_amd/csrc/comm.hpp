@@ -27,6 +27,9 @@ class Comm {
  public:
   virtual ~Comm() = default;
   virtual void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs) = 0;
+  // in-place element-wise sum over all ranks (ncclAllReduce); the engine only reduces arrays
+  // in which each element has one non-zero contributor, so the result is exact
+  virtual void allreduce_sum(double* p, size_t count) = 0;
   virtual bool graph_safe() const = 0;
 };
 

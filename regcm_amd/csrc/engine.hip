@@ -189,7 +189,9 @@ const dim3 BLK(64, 4, 1);
 enum class FK {
   A1U, A1V, A1T, A1QV, A1QC, A2U, A2V, A2T, A2QV, A2QC, PSA, PSB, PSDOTA, PSDOTB,
   RPSDA, RPSDB, QDOT, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
-  UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR
+  UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR,
+  // non-hydrostatic core
+  A1PP, A2PP, A1W, A2W, NCR, NXKCR, NCDT, NCPP, NCU, NCV
 };
 
 struct rcmdyn_engine {
@@ -218,6 +220,7 @@ struct rcmdyn_engine {
   int device = 0;
 
   std::vector<NHFields> nhf;   // non-hydrostatic buffers of each owned tile (idynamic = 2)
+  double* nh_gbuf = nullptr;   // global-indexed day-alarm terms of the radiative condition
 
   int nsplit() const { return cfg.nsplit; }
 
@@ -404,8 +407,16 @@ struct rcmdyn_engine {
     f.ps0 = dalloc(t, P); f.dpsdxm = dalloc(t, P); f.dpsdym = dalloc(t, P);
     f.ef = dalloc(t, P); f.ddx = dalloc(t, P); f.ddy = dalloc(t, P); f.dmdx = dalloc(t, P); f.dmdy = dalloc(t, P);
     f.ex = dalloc(t, P); f.crx = dalloc(t, P); f.cry = dalloc(t, P);
-    f.estore = dalloc(t, P); f.astore = dalloc(t, P); f.tmask = dalloc(t, 169);
-    f.cfl = talloc<unsigned long long>(t, NH_CFL_SLOTS);
+    f.estore = dalloc(t, P); f.astore = dalloc(t, P);
+    if (nhf.empty()) {                 // engine-wide: mask, CFL slots, day-alarm gather buffer
+      f.tmask = dalloc(t, 169);
+      f.cfl = talloc<unsigned long long>(t, NH_CFL_SLOTS);
+      nh_gbuf = dalloc(t, 2 * (size_t)cfg.jx * cfg.iy);
+    } else {
+      f.tmask = nhf[0].tmask;
+      f.cfl = nhf[0].cfl;
+    }
+    if (ntiles > 1) t.westore = dalloc(t, t.gw.plane);
     nhf.push_back(f);
   }
 
@@ -431,9 +442,6 @@ struct rcmdyn_engine {
     if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
     if (cfg.idynamic != 1 && cfg.idynamic != 2) throw std::runtime_error("rcmdyn: idynamic must be 1 or 2");
     if (cfg.idynamic == 2) {
-      if (cfg.nproc_j * cfg.nproc_i != 1)
-        throw std::runtime_error("rcmdyn: the non-hydrostatic core runs on one tile (the upper radiative "
-                                 "condition of sound gathers the whole domain, Main/mod_sound.F90:496-497)");
       if (!(cfg.nh_dtsmax > 0.0) || !(cfg.nh_xmsf > 0.0))
         throw std::runtime_error("rcmdyn: nh_dtsmax / nh_xmsf (init_sound) must be set for idynamic=2");
     }
@@ -454,6 +462,9 @@ struct rcmdyn_engine {
       const Geom& g = all.back();
       if (g.jde2 - g.jde1 + 1 < 3 || g.ide2 - g.ide1 + 1 < 3)
         throw std::runtime_error("rcmdyn: Too much processors (tile < 3x3), mod_mppparam.F90:1365");
+      // the NH radiative condition reaches 6 points: its halo must come from direct neighbours
+      if (cfg.idynamic == 2 && cfg.nproc_j * cfg.nproc_i > 1 && (g.jde2 - g.jde1 + 1 < 6 || g.ide2 - g.ide1 + 1 < 6))
+        throw std::runtime_error("rcmdyn: non-hydrostatic tiles must be at least 6x6 points");
     }
     compute_constants();
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -513,6 +524,14 @@ struct rcmdyn_engine {
       case FK::VBT: return t.vbt; case FK::TB0: return t.tb0; case FK::TBT: return t.tbt;
       case FK::QB0: return t.qb0; case FK::QBT: return t.qbt; case FK::PB0: return t.pb0;
       case FK::PBT: return t.pbt; case FK::DSTOR: return t.dstor; case FK::HSTOR: return t.hstor;
+      default: break;
+    }
+    const NHFields& h = nhf[&t - tiles.data()];
+    switch (f) {
+      case FK::A1PP: return h.a1pp; case FK::A2PP: return h.a2pp; case FK::A1W: return h.a1w;
+      case FK::A2W: return h.a2w; case FK::NCR: return h.cr; case FK::NXKCR: return h.xkcr;
+      case FK::NCDT: return h.cdt; case FK::NCPP: return h.cpp; case FK::NCU: return h.cu; case FK::NCV: return h.cv;
+      default: break;
     }
     return nullptr;
   }
@@ -907,59 +926,115 @@ struct rcmdyn_engine {
   }
   bool nh_tmask_valid = false;
 
-  // tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2)
+  // tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2).  Exchange points
+  // follow the reference's exchange calls: decouple (atm1 width 1, atm2 width idif, pp, w),
+  // compute_omega (cr, qdot), calc_coeff (xkc), the moisture forecast (atmc%qx), and per
+  // acoustic sub-step dp'/dp0 with pp, then u and v (Main/mod_sound.F90:262-263, 294-295);
+  // the upper radiative condition's estore gather (:496-497) becomes a 6-deep halo.
   void nh_tend() {
     const int kz = cfg.kz, kp = kz + 1;
-    Tile& t = tiles[0];
-    const Geom& g = t.g;
-    const NHFields f = nhfields(t);
     const int istep = nh_istep();
     const bool alarm = nh_day_alarm();
-    const dim3 fr = grid3(g.nj, g.ni, kp), frk = grid3(g.nj, g.ni, kz);
-    const int nce_j = g.jce2 - g.jce1 + 1, nce_i = g.ice2 - g.ice1 + 1;
-    const int nci_j = g.jci2 - g.jci1 + 1, nci_i = g.ici2 - g.ici1 + 1;
-    const int ndi_j = g.jdi2 - g.jdi1 + 1, ndi_i = g.idi2 - g.idi1 + 1;
-    (void)frk;
-    KLAUNCH(k_surface_pressures, grid3(g.nj, g.ni, 1), BLK, 0, stream, g, fields(t));
-    KLAUNCH(k_nh_decouple, fr, BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_omega, grid3(nce_j, nce_i, 1), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_mkslice, fr, BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_coeff_raw, grid3(nce_j, nce_i, kz), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_coeff_scale, fr, BLK, 0, stream, g, dc, f);
-    // init_tendencies (:1227-1240)
-    const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
-    for (double* p : {f.tten, f.tdyn, f.qvten, f.qvdyn, f.qcten, f.qcdyn, f.uten, f.udyn, f.vten, f.vdyn,
-                      f.ppten, f.ppdyn})
-      HIPCHK(hipMemsetAsync(p, 0, b3, stream));
-    for (double* p : {f.wten, f.wdyn}) HIPCHK(hipMemsetAsync(p, 0, b4, stream));
-    KLAUNCH(k_nh_uv_adv, grid3(ndi_j, ndi_i, 1), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_scalar_adv, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_curvature, grid3(ndi_j, ndi_i, kz), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_adiabatic, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_boundary, fr, BLK, 0, stream, g, dc, ds, f);
-    KLAUNCH(k_nh_diffusion, fr, BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_forecast, fr, BLK, 0, stream, g, dc, ds, f);
-    KLAUNCH(k_nh_negfix, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
-    KLAUNCH(k_nh_tfilter, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_raydamp, fr, BLK, 0, stream, g, dc, ds, f);
-    // sound, Main/mod_sound.F90:163-718
-    KLAUNCH(k_nh_sound_init, fr, BLK, 0, stream, g, dc, ds, f, istep);
+    struct Grids { dim3 fr, ce1, cek, ci1, cik, cik1, di1, dik; };
+    auto grids = [&](const Geom& g) {
+      const int nce_j = g.jce2 - g.jce1 + 1, nce_i = g.ice2 - g.ice1 + 1;
+      const int nci_j = g.jci2 - g.jci1 + 1, nci_i = g.ici2 - g.ici1 + 1;
+      const int ndi_j = g.jdi2 - g.jdi1 + 1, ndi_i = g.idi2 - g.idi1 + 1;
+      return Grids{grid3(g.nj, g.ni, kp), grid3(nce_j, nce_i, 1), grid3(nce_j, nce_i, kz),
+                   grid3(nci_j, nci_i, 1), grid3(nci_j, nci_i, kz), grid3(nci_j, nci_i, kz - 1),
+                   grid3(ndi_j, ndi_i, 1), grid3(ndi_j, ndi_i, kz)};
+    };
+    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz},
+         {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2},
+         {FK::A2QV, kz, 2}, {FK::A2QC, kz, 2}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}});
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const NHFields f = nhfields(t);
+      const Grids q = grids(g);
+      KLAUNCH(k_surface_pressures, grid3(g.nj, g.ni, 1), BLK, 0, stream, g, fields(t));
+      KLAUNCH(k_nh_decouple, q.fr, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_omega, q.ce1, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_mkslice, q.fr, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
+    });
+    xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const NHFields f = nhfields(t);
+      const Grids q = grids(g);
+      KLAUNCH(k_nh_coeff_scale, q.fr, BLK, 0, stream, g, dc, f);
+      // init_tendencies (:1227-1240)
+      const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
+      for (double* p : {f.tten, f.tdyn, f.qvten, f.qvdyn, f.qcten, f.qcdyn, f.uten, f.udyn, f.vten, f.vdyn,
+                        f.ppten, f.ppdyn})
+        HIPCHK(hipMemsetAsync(p, 0, b3, stream));
+      for (double* p : {f.wten, f.wdyn}) HIPCHK(hipMemsetAsync(p, 0, b4, stream));
+      KLAUNCH(k_nh_uv_adv, q.di1, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_scalar_adv, q.ci1, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_curvature, q.dik, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_adiabatic, q.ci1, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_boundary, q.fr, BLK, 0, stream, g, dc, ds, f);
+      KLAUNCH(k_nh_diffusion, q.fr, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_forecast, q.fr, BLK, 0, stream, g, dc, ds, f);
+    });
+    xch({{FK::CQV, kz}, {FK::CQC, kz}});
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const NHFields f = nhfields(t);
+      const Grids q = grids(g);
+      KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
+      KLAUNCH(k_nh_tfilter, q.cik, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_raydamp, q.fr, BLK, 0, stream, g, dc, ds, f);
+      // sound, Main/mod_sound.F90:163-718
+      KLAUNCH(k_nh_sound_init, q.fr, BLK, 0, stream, g, dc, ds, f, istep);
+    });
     for (int it = 1; it <= istep; it++) {
-      KLAUNCH(k_nh_sound_a, grid3(nce_j, nce_i, 1), BLK, 0, stream, g, dc, f, it);
-      KLAUNCH(k_nh_sound_uv, grid3(ndi_j, ndi_i, kz), BLK, 0, stream, g, dc, ds, f, istep);
-      KLAUNCH(k_nh_sound_b1, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, ds, f, istep, it);
-      KLAUNCH(k_nh_sound_b2, grid3(nci_j, nci_i, kz - 1), BLK, 0, stream, g, dc, ds, f, istep);
-      KLAUNCH(k_nh_sound_b3, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
-      if (cfg.ifupr == 1 && it == 1 && alarm) {
-        KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, g, dc, f);
-        nh_tmask_valid = true;
+      each([&](Tile& t) {
+        KLAUNCH(k_nh_sound_a, grids(t.g).ce1, BLK, 0, stream, t.g, dc, nhfields(t), it);
+      });
+      xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
+      each([&](Tile& t) {
+        KLAUNCH(k_nh_sound_uv, grids(t.g).dik, BLK, 0, stream, t.g, dc, ds, nhfields(t), istep);
+      });
+      xch({{FK::NCU, kz}, {FK::NCV, kz}});
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        const NHFields f = nhfields(t);
+        const Grids q = grids(g);
+        KLAUNCH(k_nh_sound_b1, q.cik, BLK, 0, stream, g, dc, ds, f, istep, it);
+        KLAUNCH(k_nh_sound_b2, q.cik1, BLK, 0, stream, g, dc, ds, f, istep);
+        KLAUNCH(k_nh_sound_b3, q.ci1, BLK, 0, stream, g, dc, f);
+      });
+      if (cfg.ifupr == 1) {
+        if (it == 1 && alarm) {
+          each([&](Tile& t) {
+            KLAUNCH(k_nh_tmask_gather, grids(t.g).ci1, BLK, 0, stream, t.g, dc, nhfields(t), nh_gbuf);
+          });
+          if (comm) comm->allreduce_sum(nh_gbuf, 2 * (size_t)cfg.jx * cfg.iy);
+          KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, tiles[0].g, dc, nh_gbuf, nhf[0].tmask);
+          nh_tmask_valid = true;
+        }
+        if (ntiles > 1) {
+          each([&](Tile& t) { copy_wide(t, nhf[&t - tiles.data()].estore, t.westore, 1); });
+          xch_wide({{&Tile::westore, 1}}, 6);
+        }
       }
-      KLAUNCH(k_nh_sound_c1, grid3(nci_j, nci_i, 1), BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_sound_c2, grid3(nci_j, nci_i, kz), BLK, 0, stream, g, dc, ds, f, istep);
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        const NHFields f = nhfields(t);
+        const Grids q = grids(g);
+        if (ntiles > 1)
+          KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, f);
+        else
+          KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, g, f.estore, dc, f);
+        KLAUNCH(k_nh_sound_c2, q.cik, BLK, 0, stream, g, dc, ds, f, istep);
+      });
     }
-    KLAUNCH(k_nh_sound_final, fr, BLK, 0, stream, g, dc, f);
-    KLAUNCH(k_nh_advance, dim3(1), dim3(256), 0, stream, dc, ds, f);
+    each([&](Tile& t) {
+      KLAUNCH(k_nh_sound_final, grids(t.g).fr, BLK, 0, stream, t.g, dc, nhfields(t));
+    });
+    KLAUNCH(k_nh_advance, dim3(1), dim3(256), 0, stream, dc, ds, nhf[0]);
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
   }
@@ -968,20 +1043,29 @@ struct rcmdyn_engine {
   // then the moisture inflow/outflow rules and the clock
   void nh_bdyval() {
     const int kz = cfg.kz;
-    Tile& t = tiles[0];
-    const Geom& g = t.g;
-    const int c = t.cur;
-    Slices sl;
-    for (int q = 0; q < 16; q++) sl.s[q] = t.sl[q];
-    KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0, stream,
-            g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c], t.a2qv[c],
-            t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt, t.pb0, t.pbt,
-            sl, slen, 0);
-    const int nperim = 2 * (g.ici2 - g.ici1 + 1) + 2 * (g.jce2 - g.jce1 + 1);
-    KLAUNCH(k_nh_bdyval, dim3((nperim + 63) / 64, kz + 1), dim3(64), 0, stream, g, kz, ds, nhfields(t));
-    KLAUNCH(k_nh_bdyval_w1, dim3(1), dim3(256), 0, stream, g, nhfields(t));
-    KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
-            t.a1qc[c], t.a1qv[c], t.psa_[c], sl, slen, ds, cfg.dtsec, 1);
+    auto slices = [&](Tile& t) {
+      Slices sl;
+      for (int q = 0; q < 16; q++) sl.s[q] = t.sl[q];
+      return sl;
+    };
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur;
+      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0,
+              stream, g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
+              t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt,
+              t.pb0, t.pbt, slices(t), slen, 0);
+      const int nperim = 2 * (g.ici2 - g.ici1 + 1) + 2 * (g.jce2 - g.jce1 + 1);
+      KLAUNCH(k_nh_bdyval, dim3((nperim + 63) / 64, kz + 1), dim3(64), 0, stream, g, kz, ds, nhfields(t));
+      KLAUNCH(k_nh_bdyval_w1, dim3(1), dim3(256), 0, stream, g, nhfields(t));
+    });
+    xch_slices();
+    for (size_t q = 0; q < tiles.size(); q++) {
+      Tile& t = tiles[q];
+      const int c = t.cur;
+      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
+              t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()));
+    }
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }
 

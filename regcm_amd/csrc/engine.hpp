@@ -112,6 +112,7 @@ struct Tile {
   Geom gw{};
   double *wdeld = nullptr, *wdelh = nullptr, *wpsa = nullptr, *wpsdota = nullptr;
   double *wmsfx = nullptr, *wmsfd = nullptr, *wmapf = nullptr;
+  double *westore = nullptr;       // NH: estore of sound on the wide frame (6-deep halo)
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials

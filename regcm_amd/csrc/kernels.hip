@@ -205,16 +205,18 @@ __device__ double2 udvd_bdy(const Geom& g, const Fields& f, int j, int i, uint32
     const double r = LD(f.rpsda, q2);
     return make_double2(LD(f.a1u, q2 + kof) * r, LD(f.a1v, q2 + kof) * r);
   };
+  // global boundary lines (a ghost point on them carries the value its owner computes and
+  // the reference exchanges)
   auto we = [&](int jj, int ii) {
-    if (in(ii, g.idi1, g.idi2)) {
-      if (g.bl && jj == g.jde1 && LD(f.a1u, g.o2(jj, ii) + kof) <= d_zero) return base(g.jdi1, ii);
-      if (g.br && jj == g.jde2 && LD(f.a1u, g.o2(jj, ii) + kof) >= d_zero) return base(g.jdi2, ii);
+    if (in(ii, 2, g.giy - 1)) {
+      if (jj == 1 && LD(f.a1u, g.o2(jj, ii) + kof) <= d_zero) return base(2, ii);
+      if (jj == g.gjx && LD(f.a1u, g.o2(jj, ii) + kof) >= d_zero) return base(g.gjx - 1, ii);
     }
     return base(jj, ii);
   };
-  if (in(j, g.jde1, g.jde2)) {
-    if (g.bb && i == g.ide1 && LD(f.a1v, g.o2(j, i) + kof) >= d_zero) return we(j, g.idi1);
-    if (g.bt && i == g.ide2 && LD(f.a1v, g.o2(j, i) + kof) <= d_zero) return we(j, g.idi2);
+  if (in(j, 1, g.gjx)) {
+    if (i == 1 && LD(f.a1v, g.o2(j, i) + kof) >= d_zero) return we(j, 2);
+    if (i == g.giy && LD(f.a1v, g.o2(j, i) + kof) <= d_zero) return we(j, g.giy - 1);
   }
   return we(j, i);
 }
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
       const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
       const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
       umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
-      if (c->iboudy == 4 && (jg == g.jde1 || jg == g.jde2 || ig == g.ide1 || ig == g.ide2)) {
+      if (c->iboudy == 4 && (jg == 1 || jg == g.gjx || ig == 1 || ig == g.giy)) {
         const double2 b = udvd_bdy(g, f, jg, ig, kof);
         ud = b.x; vd = b.y;
       }

@@ -38,16 +38,18 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
     return make_double2(F3(a1u, jj, ii, k) * r, F3(a1v, jj, ii, k) * r);
   };
   if (iboudy != 4) return base(j, i);
+  // global boundary lines (a ghost point on them carries the value its owner computes and
+  // the reference exchanges)
   auto we = [&](int jj, int ii) {
-    if (in(ii, g.idi1, g.idi2)) {
-      if (g.bl && jj == g.jde1 && F3(a1u, jj, ii, k) <= d_zero) return base(g.jdi1, ii);
-      if (g.br && jj == g.jde2 && F3(a1u, jj, ii, k) >= d_zero) return base(g.jdi2, ii);
+    if (in(ii, 2, g.giy - 1)) {
+      if (jj == 1 && F3(a1u, jj, ii, k) <= d_zero) return base(2, ii);
+      if (jj == g.gjx && F3(a1u, jj, ii, k) >= d_zero) return base(g.gjx - 1, ii);
     }
     return base(jj, ii);
   };
-  if (in(j, g.jde1, g.jde2)) {
-    if (g.bb && i == g.ide1 && F3(a1v, j, i, k) >= d_zero) return we(j, g.idi1);
-    if (g.bt && i == g.ide2 && F3(a1v, j, i, k) <= d_zero) return we(j, g.idi2);
+  if (in(j, 1, g.gjx)) {
+    if (i == 1 && F3(a1v, j, i, k) >= d_zero) return we(j, 2);
+    if (i == g.giy && F3(a1v, j, i, k) <= d_zero) return we(j, g.giy - 1);
   }
   return we(j, i);
 }
@@ -897,17 +899,29 @@ __global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f) 
   }
 }
 
-// upper radiative condition coefficients (:500-543), one block: the domain means in the
-// reference's summation order by one thread, then one thread per mask entry
-__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f) {
+// upper radiative condition coefficients (:500-543), on the day alarm.  The domain means
+// are sequential sums over the interior cross points in the reference's i-major order; each
+// tile first scatters its points' terms into a global-indexed buffer (gbuf: astore, then
+// rho*sqrt(N^2)), so every decomposition sums the same values in the same order.
+__global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (!IN_CI(j, i)) return;
+  const long q = (long)(i - 1) * g.gjx + (j - 1), n = (long)g.gjx * g.giy;
+  const double ensq = EGRAV_NH * EGRAV_NH / c->cpd / (F3(f.a2t, j, i, 1) * F2(f.rpsb, j, i));
+  gbuf[q] = F2(f.astore, j, i);
+  gbuf[n + q] = F3(f.rho1, j, i, 1) * sqrt(ensq);
+}
+
+__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask) {
   __shared__ double sh[2];
   if (threadIdx.x == 0) {
+    const long n = (long)g.gjx * g.giy;
     double atot = d_zero, rhontot = d_zero;
-    for (int i = g.ici1; i <= g.ici2; i++)
-      for (int j = g.jci1; j <= g.jci2; j++) {
-        atot = atot + F2(f.astore, j, i);
-        const double ensq = EGRAV_NH * EGRAV_NH / c->cpd / (F3(f.a2t, j, i, 1) * F2(f.rpsb, j, i));
-        rhontot = rhontot + F3(f.rho1, j, i, 1) * sqrt(ensq);
+    for (int i = 2; i <= g.giy - 2; i++)
+      for (int j = 2; j <= g.gjx - 2; j++) {
+        const long q = (long)(i - 1) * g.gjx + (j - 1);
+        atot = atot + gbuf[q];
+        rhontot = rhontot + gbuf[n + q];
       }
     const double rnpts = d_one / (double)((g.giy - 3) * (g.gjx - 3));
     sh[0] = atot * rnpts;
@@ -933,14 +947,16 @@ __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f) {
                       cos(2.0 * MATHPI * rll * rj / 12.0) * xkleff / (rhon - abar * xkleff);
     }
   }
-  f.tmask[t] = acc;
+  tmask[t] = acc;
 }
-
 
 // substep part D (:488-685) in two launches.
 // D1, 64 x 4 interior columns per block: upper boundary value from the 13 x 13 convolution
 // of estore (staged in LDS, clamped to the interior) and the downward sweep of w
-__global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, const Consts* __restrict__ c, NHFields f) {
+// estore is read from the frame ge (the tile frame, or on a decomposed domain the wide frame
+// filled by a 6-deep exchange: the convolution reaches 6 points, clamped to the interior).
+__global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, Geom ge, const double* __restrict__ est,
+                                                     const Consts* __restrict__ c, NHFields f) {
   __shared__ double sE[4 + 12][64 + 12];
   __shared__ double sM[169];
   const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
@@ -953,7 +969,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, const Consts* __res
       int jn = J0 - 6 + jj, in_ = I0 - 6 + ii;
       jn = (jn < jlo) ? jlo : (jn > jhi ? jhi : jn);
       in_ = (in_ < ilo) ? ilo : (in_ > ihi ? ihi : in_);
-      sE[ii][jj] = F2(f.estore, jn, in_);
+      sE[ii][jj] = est[ge.ix(jn, in_)];
     }
     if (tid < 169) sM[tid] = f.tmask[tid];
     __syncthreads();

@@ -62,8 +62,9 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
 __global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_sound_b2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_sound_c1(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
+__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
+__global__ void k_nh_sound_c1(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
