@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -215,6 +216,8 @@ struct rcmdyn_engine {
   bool diag = false;         // write the per-tend diagnostic fields
   KernelProf* prof = nullptr;  // set while rcmdyn_kernel_times runs
   double last_ms = 0.0;
+  // RCMDYN_NO_GRAPH=1 runs rcmdyn_step eagerly (the path of RCCL-decomposed runs), for timing
+  const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
   std::string err;
   std::unique_ptr<Comm> comm;
   int device = 0;
@@ -1221,7 +1224,7 @@ struct rcmdyn_engine {
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    const bool use_graph = !(comm && !comm->graph_safe());
+    const bool use_graph = !no_graph && !(comm && !comm->graph_safe());
     HIPCHK(hipEventRecord(e0, stream));
     for (int s = 0; s < n; s++) {
       const int par = tiles[0].cur;

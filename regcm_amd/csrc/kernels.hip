@@ -224,7 +224,7 @@ __device__ double2 udvd_bdy(const Geom& g, const Fields& f, int j, int i, uint32
 constexpr int TW1 = MBJ + 2, TH1 = MBI + 2;   // halo 1 on every side
 constexpr int TW2 = MBJ + 4, TH2 = MBI + 4;   // halo 2 on every side
 constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i-1)
-__global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __restrict__ c,
+__global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __restrict__ c,
                                                      const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
   __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
@@ -255,67 +255,98 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
   const double dmsf = LD(f.dmsf, o2), cor = LD(f.coriol, o2), pdotb = LD(f.psdotb, o2);
   const double pdota = LD(f.psdota, o2), mfd = LD(f.msfd, o2);
   const int rgd = f.rgdt[o2 >> 3];
-  // ---- stage (all loads independent)
-  for (int t = tid; t < TW1 * TH1; t += MBT) {
-    const int jj = t % TW1, ii = t / TW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0;
-    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
-      umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
-      if (c->iboudy == 4 && (jg == 1 || jg == g.gjx || ig == 1 || ig == g.giy)) {
-        const double2 b = udvd_bdy(g, f, jg, ig, kof);
-        ud = b.x; vd = b.y;
+  // ---- stage.  Every global load of the three staging sets (and hgfact for xkc) is issued
+  // before the first LDS write: one memory latency per block.  Lanes past the tile or the frame
+  // read this thread's own (valid) address and stage zero.
+  constexpr int N1 = (TW1 * TH1 + MBT - 1) / MBT, N2 = (TW2 * TH2 + MBT - 1) / MBT;
+  constexpr int N0 = (TW0 * TH0 + MBT - 1) / MBT;
+  double au[N1], av[N1], am[N1], ar[N1];
+  double br[N2], bm[N2], bu[N2], bv[N2];
+  double crp[N0], ct[N0], cqv[N0], cq0[N0], cq1[N0], cph[N0], cps[N0], chg[N0];
+  bool aok[N1], bok[N2], cok[N0];
+#pragma unroll
+  for (int n = 0; n < N1; n++) {
+    const int t = tid + n * MBT, jg = J0 - 1 + t % TW1, ig = I0 - 1 + t / TW1;
+    aok[n] = t < TW1 * TH1 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
+    const uint32_t q2 = aok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
+  }
+#pragma unroll
+  for (int n = 0; n < N2; n++) {
+    const int t = tid + n * MBT, jg = J0 - 2 + t % TW2, ig = I0 - 2 + t / TW2;
+    bok[n] = t < TW2 * TH2 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
+    const uint32_t q2 = bok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    br[n] = LD(f.rpsdb, q2); bm[n] = LD(f.msfd, q2); bu[n] = LD(f.a2u, q3); bv[n] = LD(f.a2v, q3);
+  }
+#pragma unroll
+  for (int n = 0; n < N0; n++) {
+    const int t = tid + n * MBT, jg = J0 - 1 + t % TW0, ig = I0 - 1 + t / TW0;
+    cok[n] = t < TW0 * TH0 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
+    const uint32_t q2 = cok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    crp[n] = LD(f.rpsa, q2); ct[n] = LD(f.a1t, q3); cqv[n] = LD(f.a1qv, q3);
+    cq0[n] = LD(f.qdot, q3); cq1[n] = LD(f.qdot, q3 + L8); cph[n] = LD(f.phi, q3); cps[n] = LD(f.psa, q2);
+    chg[n] = LD(f.hgfact, q2);
+  }
+#pragma unroll
+  for (int n = 0; n < N1; n++) {
+    const int t = tid + n * MBT, jj = t % TW1, ii = t / TW1;
+    if (t < TW1 * TH1) {
+      const bool ok = aok[n];
+      double ud = ok ? au[n] * ar[n] : 0.0, vd = ok ? av[n] * ar[n] : 0.0;
+      if (c->iboudy == 4 && ok) {
+        const int jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+        if (jg == 1 || jg == g.gjx || ig == 1 || ig == g.giy) {
+          const double2 bb = udvd_bdy(g, f, jg, ig, kof);
+          ud = bb.x; vd = bb.y;
+        }
       }
+      sUMC[ii][jj] = ok ? au[n] * am[n] : 0.0; sVMC[ii][jj] = ok ? av[n] * am[n] : 0.0;
+      sUD[ii][jj] = ud; sVD[ii][jj] = vd;
     }
-    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd;
   }
-  for (int t = tid; t < TW2 * TH2; t += MBT) {
-    const int jj = t % TW2, ii = t / TW2, jg = J0 - 2 + jj, ig = I0 - 2 + ii;
-    double um = 0.0, vm = 0.0, ub = 0.0, vb = 0.0;
-    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double r = LD(f.rpsdb, q2), m = LD(f.msfd, q2);
-      ub = LD(f.a2u, q3) * r;
-      vb = LD(f.a2v, q3) * r;
-      um = ub / m;
-      vm = vb / m;
+#pragma unroll
+  for (int n = 0; n < N2; n++) {
+    const int t = tid + n * MBT, jj = t % TW2, ii = t / TW2;
+    if (t < TW2 * TH2) {
+      const bool ok = bok[n];
+      const double ub = bu[n] * br[n], vb = bv[n] * br[n];
+      sUM[ii][jj] = ok ? ub / bm[n] : 0.0; sVM[ii][jj] = ok ? vb / bm[n] : 0.0;
+      sUB[ii][jj] = ok ? ub : 0.0; sVB[ii][jj] = ok ? vb : 0.0;
     }
-    sUM[ii][jj] = um; sVM[ii][jj] = vm; sUB[ii][jj] = ub; sVB[ii][jj] = vb;
   }
-  for (int t = tid; t < TW0 * TH0; t += MBT) {
-    const int jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-    double tv = 0.0, q0 = 0.0, q1 = 0.0, ph = 0.0, ps = 0.0;
-    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double rp = LD(f.rpsa, q2);
-      const double tt = LD(f.a1t, q3) * rp;
-      const double qv = dmax(LD(f.a1qv, q3) * rp, MINQQ);
-      tv = tt * (d_one + ep1 * qv);
-      q0 = LD(f.qdot, q3);
-      q1 = LD(f.qdot, q3 + L8);
-      ph = LD(f.phi, q3);
-      ps = LD(f.psa, q2);
+#pragma unroll
+  for (int n = 0; n < N0; n++) {
+    const int t = tid + n * MBT, jj = t % TW0, ii = t / TW0;
+    if (t < TW0 * TH0) {
+      const bool ok = cok[n];
+      const double rp = crp[n];
+      const double tt = ct[n] * rp;
+      const double qv = dmax(cqv[n] * rp, MINQQ);
+      sTV[ii][jj] = ok ? tt * (d_one + ep1 * qv) : 0.0;
+      sQ0[ii][jj] = ok ? cq0[n] : 0.0; sQ1[ii][jj] = ok ? cq1[n] : 0.0;
+      sPH[ii][jj] = ok ? cph[n] : 0.0; sPS[ii][jj] = ok ? cps[n] : 0.0;
     }
-    sTV[ii][jj] = tv; sQ0[ii][jj] = q0; sQ1[ii][jj] = q1; sPH[ii][jj] = ph; sPS[ii][jj] = ps;
   }
   __syncthreads();
   // calc_coeff Smagorinsky xkc (Main/mod_diffusion.F90:194-210) at the low-halo tile points from
   // the staged ubd3d/vbd3d, over the cross points of the tile and its ghost ring toward
   // neighbouring tiles (the reference's exchanged xkc there is the same computation)
-  for (int t = tid; t < TW0 * TH0; t += MBT) {
-    const int jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-    double xk = 0.0;
-    if (in(jg, g.jce1ga, g.jce2ga) && in(ig, g.ice1ga, g.ice2ga)) {
-      const int y = ii + 1, x = jj + 1;            // (jg, ig) in the halo-2 tiles
-      const double dudx = sUB[y][x + 1] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y + 1][x];
-      const double dvdx = sVB[y][x + 1] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y + 1][x];
-      const double dudy = sUB[y + 1][x] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y][x + 1];
-      const double dvdy = sVB[y + 1][x] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y][x + 1];
-      const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
-      xk = dmin(LD(f.hgfact, g.o2(jg, ig)) + c->dydc * duv, c->xkhmax);
+#pragma unroll
+  for (int n = 0; n < N0; n++) {
+    const int t = tid + n * MBT, jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
+    if (t < TW0 * TH0) {
+      double xk = 0.0;
+      if (in(jg, g.jce1ga, g.jce2ga) && in(ig, g.ice1ga, g.ice2ga)) {
+        const int y = ii + 1, x = jj + 1;            // (jg, ig) in the halo-2 tiles
+        const double dudx = sUB[y][x + 1] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y + 1][x];
+        const double dvdx = sVB[y][x + 1] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y + 1][x];
+        const double dudy = sUB[y + 1][x] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y][x + 1];
+        const double dvdy = sVB[y + 1][x] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y][x + 1];
+        const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
+        xk = dmin(chg[n] + c->dydc * duv, c->xkhmax);
+      }
+      sXK[ii][jj] = xk;
     }
-    sXK[ii][jj] = xk;
   }
   __syncthreads();
 #undef sUB
@@ -485,6 +516,9 @@ __global__ __launch_bounds__(MBT, 2) void k_momentum(Geom g, const Consts* __res
 // products formed once per staged point: umc/vmc/ud/vd at the dot points (j..j+1, i..i+1),
 // p*, t, qv, qc (atm1 * rpsa) with halo 1 and the mkslice fields atm2 * (1/psb) with halo 2.
 // The interior ring (jce \ jci) only passes atm2 moisture to the forecast buffers.
+#ifdef RCM_PHASE_TIMING
+__device__ int rcm_phase_count = 0;
+#endif
 constexpr int SDW = SBJ + 1, SDH = SBI + 1;    // dot points j..j+SBJ, i..i+SBI
 constexpr int SW1 = SBJ + 2, SH1 = SBI + 2;    // halo 1
 constexpr int SW2 = SBJ + 4, SH2 = SBI + 4;    // halo 2
@@ -549,12 +583,15 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
   } while (0)
 
-__global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __restrict__ c,
+__global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __restrict__ c,
                                                     const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
   __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
   __shared__ double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
   const int tid = threadIdx.x;
+#ifdef RCM_PHASE_TIMING
+  const long long pt0 = wall_clock64();
+#endif
   const int J0 = g.jce1 + (int)blockIdx.x * SBJ, I0 = g.ice1 + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -576,46 +613,75 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   const double xm = LD(f.xmsf, o2), rp = LD(f.rpsa, o2), pb = LD(f.psb, o2), mx = LD(f.msfx, o2);
   const double ptn = LD(f.pten, o2), hgf = LD(f.hgfact, o2);
   const int rgc = f.rgcr[o2 >> 3];
-  // ---- stage
-  for (int t = tid; t < SDW * SDH; t += SBT) {
-    const int jj = t % SDW, ii = t / SDW, jg = J0 + jj, ig = I0 + ii;
-    double umc = 0.0, vmc = 0.0, ud = 0.0, vd = 0.0, ub = 0.0, vb = 0.0;
-    if (jg <= jhi && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double u = LD(f.a1u, q3), v = LD(f.a1v, q3), m = LD(f.msfd, q2), r = LD(f.rpsda, q2);
-      const double rb = LD(f.rpsdb, q2);
-      umc = u * m; vmc = v * m; ud = u * r; vd = v * r;
-      ub = LD(f.a2u, q3) * rb;
-      vb = LD(f.a2v, q3) * rb;
-    }
-    sUMC[ii][jj] = umc; sVMC[ii][jj] = vmc; sUD[ii][jj] = ud; sVD[ii][jj] = vd; sUB[ii][jj] = ub; sVB[ii][jj] = vb;
+  // ---- stage.  Every global load of the three staging sets is issued before the first LDS
+  // write, so the block waits one memory latency instead of one per set and slot; lanes past
+  // the tile or the frame read this thread's own (valid) address and stage zero.
+  constexpr int NA = (SDW * SDH + SBT - 1) / SBT, NB = (SW1 * SH1 + SBT - 1) / SBT;
+  constexpr int NC = (SW2 * SH2 + SBT - 1) / SBT;
+  double au[NA], av[NA], am[NA], ar[NA], arb[NA], au2[NA], av2[NA];
+  double bps[NB], brp[NB], bt[NB], bqv[NB], bqc[NB];
+  double crb[NC], ct2[NC], cqv[NC], cqc[NC];
+  bool aok[NA], bok[NB], cok[NC];
+#pragma unroll
+  for (int n = 0; n < NA; n++) {
+    const int t = tid + n * SBT, jg = J0 + t % SDW, ig = I0 + t / SDW;
+    aok[n] = t < SDW * SDH && jg <= jhi && ig <= ihi;
+    const uint32_t q2 = aok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
+    arb[n] = LD(f.rpsdb, q2); au2[n] = LD(f.a2u, q3); av2[n] = LD(f.a2v, q3);
   }
-  for (int t = tid; t < SW1 * SH1; t += SBT) {
-    const int jj = t % SW1, ii = t / SW1, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-    double ps = 0.0, xt = 0.0, xqv = 0.0, xqc = 0.0;
-    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double rp = LD(f.rpsa, q2);
-      ps = LD(f.psa, q2);
-      xt = LD(f.a1t, q3) * rp;
-      xqv = dmax(LD(f.a1qv, q3) * rp, MINQQ);
-      xqc = dmax(LD(f.a1qc, q3) * rp, d_zero);
-    }
-    sPS[ii][jj] = ps; sXT[ii][jj] = xt; sXQV[ii][jj] = xqv; sXQC[ii][jj] = xqc;
+#pragma unroll
+  for (int n = 0; n < NB; n++) {
+    const int t = tid + n * SBT, jg = J0 - 1 + t % SW1, ig = I0 - 1 + t / SW1;
+    bok[n] = t < SW1 * SH1 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
+    const uint32_t q2 = bok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    bps[n] = LD(f.psa, q2); brp[n] = LD(f.rpsa, q2);
+    bt[n] = LD(f.a1t, q3); bqv[n] = LD(f.a1qv, q3); bqc[n] = LD(f.a1qc, q3);
   }
-  for (int t = tid; t < SW2 * SH2; t += SBT) {
-    const int jj = t % SW2, ii = t / SW2, jg = J0 - 2 + jj, ig = I0 - 2 + ii;
-    double tb = 0.0, qvb = 0.0, qcb = 0.0;
-    if (jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi) {
-      const uint32_t q2 = g.o2(jg, ig), q3 = q2 + kof;
-      const double r = LD(f.rpsb, q2);
-      tb = LD(f.a2t, q3) * r;
-      qvb = dmax(LD(f.a2qv, q3) * r, MINQQ);
-      qcb = dmax(LD(f.a2qc, q3) * r, d_zero);
+#pragma unroll
+  for (int n = 0; n < NC; n++) {
+    const int t = tid + n * SBT, jg = J0 - 2 + t % SW2, ig = I0 - 2 + t / SW2;
+    cok[n] = t < SW2 * SH2 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
+    const uint32_t q2 = cok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
+    crb[n] = LD(f.rpsb, q2); ct2[n] = LD(f.a2t, q3); cqv[n] = LD(f.a2qv, q3); cqc[n] = LD(f.a2qc, q3);
+  }
+#pragma unroll
+  for (int n = 0; n < NA; n++) {
+    const int t = tid + n * SBT, jj = t % SDW, ii = t / SDW;
+    if (t < SDW * SDH) {
+      const bool ok = aok[n];
+      sUMC[ii][jj] = ok ? au[n] * am[n] : 0.0; sVMC[ii][jj] = ok ? av[n] * am[n] : 0.0;
+      sUD[ii][jj] = ok ? au[n] * ar[n] : 0.0; sVD[ii][jj] = ok ? av[n] * ar[n] : 0.0;
+      sUB[ii][jj] = ok ? au2[n] * arb[n] : 0.0; sVB[ii][jj] = ok ? av2[n] * arb[n] : 0.0;
     }
-    sTB[ii][jj] = tb; sQVB[ii][jj] = qvb; sQCB[ii][jj] = qcb;
+  }
+#pragma unroll
+  for (int n = 0; n < NB; n++) {
+    const int t = tid + n * SBT, jj = t % SW1, ii = t / SW1;
+    if (t < SW1 * SH1) {
+      const bool ok = bok[n];
+      const double rp = brp[n];
+      sPS[ii][jj] = ok ? bps[n] : 0.0;
+      sXT[ii][jj] = ok ? bt[n] * rp : 0.0;
+      sXQV[ii][jj] = ok ? dmax(bqv[n] * rp, MINQQ) : 0.0;
+      sXQC[ii][jj] = ok ? dmax(bqc[n] * rp, d_zero) : 0.0;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NC; n++) {
+    const int t = tid + n * SBT, jj = t % SW2, ii = t / SW2;
+    if (t < SW2 * SH2) {
+      const bool ok = cok[n];
+      const double r = crb[n];
+      sTB[ii][jj] = ok ? ct2[n] * r : 0.0;
+      sQVB[ii][jj] = ok ? dmax(cqv[n] * r, MINQQ) : 0.0;
+      sQCB[ii][jj] = ok ? dmax(cqc[n] * r, d_zero) : 0.0;
+    }
   }
   __syncthreads();
+#ifdef RCM_PHASE_TIMING
+  const long long pt1 = wall_clock64();
+#endif
   if (!valid) return;
 #define DT(S, dj, di) S[ti + (di)][tj + (dj)]
   // calc_coeff Smagorinsky xkc, Main/mod_diffusion.F90:194-210 (ubd3d/vbd3d = atm2 * (1/psdotb))
@@ -758,6 +824,14 @@ __global__ __launch_bounds__(SBT, 2) void k_scalars(Geom g, const Consts* __rest
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
   ST(f.cqv, o3, qv2 + dt * tq);
   ST(f.cqc, o3, qc2 + dt * tc);
+#ifdef RCM_PHASE_TIMING
+  if (tid == 0) {
+    const long long pt2 = wall_clock64();
+    const int n = atomicAdd(&rcm_phase_count, 1);
+    if (n < 400) printf("PT k_scalars blk %d %d %d t0 %lld stage %lld compute %lld\n", (int)blockIdx.x, (int)blockIdx.y,
+                        (int)blockIdx.z, pt0, pt1 - pt0, pt2 - pt1);
+  }
+#endif
 }
 #undef DIFFU_X
 #undef H2T
