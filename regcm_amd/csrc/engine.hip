@@ -374,7 +374,9 @@ struct rcmdyn_engine {
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     // column blocks of k_columns (one noise partial each)
-    t.nred = ((g.jde2 - g.jde1 + 64) / 64) * (g.ide2 - g.ide1 + 1);
+    // k_columns blocks: 64 columns x one row, over the tile and its left/bottom ghost ring
+    t.ncolx = (g.jde2 - (g.jde1 - (g.bl ? 0 : 1)) + 64) / 64;
+    t.nred = t.ncolx * (g.ide2 - (g.ide1 - (g.bb ? 0 : 1)) + 1);
     t.red_off = red_total;
     red_total += t.nred;
     if (cfg.idynamic == 2) setup_nh(t);
@@ -807,12 +809,12 @@ struct rcmdyn_engine {
     auto all = [](int) { return true; };
     exchange_generic(fn, all, all);
   }
-  // the fused split step is exact on a decomposition when every tile is at least SPH wide
-  // (its depth-SPH halo then comes from the direct neighbours only)
+  // the fused split step is exact on a decomposition when every tile is at least SPX wide
+  // (its depth-SPX halo then comes from the direct neighbours only)
   bool wide_ok() const {
     if (ntiles == 1) return true;
     for (const Geom& g : all)
-      if (g.jde2 - g.jde1 + 1 < SPH || g.ide2 - g.ide1 + 1 < SPH) return false;
+      if (g.jde2 - g.jde1 + 1 < SPX || g.ide2 - g.ide1 + 1 < SPX) return false;
     return true;
   }
   void copy_wide(Tile& t, const double* src, double* dst, int nplanes) {
@@ -869,7 +871,7 @@ struct rcmdyn_engine {
           copy_wide(t, t.msfd, t.wmsfd, 1);
           copy_wide(t, t.mapf, t.wmapf, 1);
         });
-        xch_wide({{&Tile::wmsfx, 1}, {&Tile::wmsfd, 1}, {&Tile::wmapf, 1}}, SPH);
+        xch_wide({{&Tile::wmsfx, 1}, {&Tile::wmsfd, 1}, {&Tile::wmapf, 1}}, SPX);
       }
       statics_dirty = false;
       invalidate_graphs();
@@ -1090,10 +1092,8 @@ struct rcmdyn_engine {
     // read, in k_momentum and k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
-      KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t),
-              (g.jde2 - g.jde1 + 64) / 64);
+      KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);
     });
-    xch({{FK::QDOT, kz + 1}, {FK::PHI, kz, 1, 1}});
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1125,19 +1125,20 @@ struct rcmdyn_engine {
     bool fused = wide_ok();
     for (int l = 1; l <= ns; l++) fused = fused && ((int)hc.aam[l - 1] * 2 <= SPH);
     if (fused && ntiles > 1) {
-      // one depth-SPH exchange of every split-step input instead of three per sub-step
+      // one depth-SPX exchange of every split-step input instead of three per sub-step
       each([&](Tile& t) {
         copy_wide(t, t.deld, t.wdeld, 3 * ns);
         copy_wide(t, t.delh, t.wdelh, 3 * ns);
         copy_wide(t, t.psa_[t.cur], t.wpsa, 1);
         copy_wide(t, t.psdota, t.wpsdota, 1);
       });
-      xch_wide({{&Tile::wdeld, 3 * ns}, {&Tile::wdelh, 3 * ns}, {&Tile::wpsa, 1}, {&Tile::wpsdota, 1}}, SPH);
+      xch_wide({{&Tile::wdeld, 3 * ns}, {&Tile::wdelh, 3 * ns}, {&Tile::wpsa, 1}, {&Tile::wpsdota, 1}}, SPX);
     }
     if (fused) {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        dim3 gr((g.jce2 - g.jce1 + SPB) / SPB, (g.ice2 - g.ice1 + SPB) / SPB, ns);
+        const int jlo = g.jce1 - (g.bl ? 0 : 1), ilo = g.ice1 - (g.bb ? 0 : 1);
+        dim3 gr((g.jce2 - jlo + SPB) / SPB, (g.ice2 - ilo + SPB) / SPB, ns);
         if (ntiles > 1)
           KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
                   t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
@@ -1161,7 +1162,8 @@ struct rcmdyn_engine {
         n0 = n1; n1 = n2; n2 = n0;
       }
     }
-    xch({{FK::DHSUM, ns}}, 1, 1);
+    // the fused split step also produced ddsum/dhsum on the left/bottom ghost ring
+    if (!fused) xch({{FK::DHSUM, ns}}, 1, 1);
     // corrections + rcmtimer advance (last tile's launch)
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];

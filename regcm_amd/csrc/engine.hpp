@@ -116,6 +116,7 @@ struct Tile {
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials
+  int ncolx = 0;                   // k_columns blocks per row
   std::vector<void*> allocs;
 };
 

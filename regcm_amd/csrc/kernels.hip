@@ -72,10 +72,15 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
   const int bb = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
-  const int j = g.jde1 + (bb % nxb) * 64 + tx, i = g.ide1 + bb / nxb;
+  // columns of the tile plus its ghost ring toward left/bottom neighbours: k_momentum reads
+  // qdot and phi there, and the ghost columns compute exactly what their owners do (no
+  // qdot/phi exchange)
+  const int jlo = g.jde1 - (g.bl ? 0 : 1), ilo = g.ide1 - (g.bb ? 0 : 1);
+  const int j = jlo + (bb % nxb) * 64 + tx, i = ilo + bb / nxb;
   const bool valid = j <= g.jde2;
-  const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
-  const bool ci = ce && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+  const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
+  const bool ce = own || (valid && in(j, jlo, g.jce2) && in(i, ilo, g.ice2));
+  const bool ci = own && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
   const int kz = c->kz;
   double* sMD = lds;                                      // mass divergence, [k-1][tx]
   double* sTD = lds + kz * 64;                            // td
@@ -113,10 +118,10 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
   __syncthreads();
   double na = 0.0, nb = 0.0;
   if (valid && ty == 0) {
+    double pt = d_zero;
     if (!ce) {
       for (int k = 1; k <= kz + 1; k++) ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, d_zero);
     } else {
-      double pt = d_zero;
       for (int k = 1; k <= kz; k++) pt = pt - sMD[(k - 1) * 64 + tx] * c->dsigma[k];
       ST(f.pten, o2, pt);
       double q = d_zero;
@@ -126,6 +131,8 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
         ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, q);
       }
       ST(f.qdot, o2 + (uint32_t)kz * L8, d_zero);
+    }
+    if (own) {
       // new_pressure
       const double dt = s->dt;
       const double psbv = LD(f.psb, o2);
@@ -1166,7 +1173,11 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
   __shared__ double Ds[2][SPR][SPP], Hs[2][SPR][SPP], U[SPR][SPP], V[SPR][SPP];
   const int l = blockIdx.z + 1;
-  const int J1 = g.jce1 + blockIdx.x * SPB, I1 = g.ice1 + blockIdx.y * SPB;
+  // owned blocks tile the tile's cross points plus its ghost ring toward left/bottom
+  // neighbours (k_split_correct reads ddsum/dhsum there; no dhsum exchange).  The first block's
+  // region then starts SPH + 1 points below the tile, the depth of the wide exchange.
+  const int jlo = g.jce1 - (g.bl ? 0 : 1), ilo = g.ice1 - (g.bb ? 0 : 1);
+  const int J1 = jlo + blockIdx.x * SPB, I1 = ilo + blockIdx.y * SPB;
   const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
   const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 16
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
@@ -1185,9 +1196,12 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   const double m2d = (double)m2;
   for (int r = 0; r < NR; r++) {
     const int lj = tx, li = ty + 16 * r, j = jr0 + lj, i = ir0 + li;
-    ce[r] = in(j, 1, gjx - 1) && in(i, 1, giy - 1);
-    ci[r] = in(j, 2, gjx - 2) && in(i, 2, giy - 2);
-    di[r] = in(j, 2, gjx - 1) && in(i, 2, giy - 1);
+    // region points outside frame w (a partial last block) lie in the contaminated rim: they
+    // are read as zero and never reach an output point
+    const bool inw = in(j, w.j0, w.j0 + w.nj - 1) && in(i, w.i0, w.i0 + w.ni - 1);
+    ce[r] = inw && in(j, 1, gjx - 1) && in(i, 1, giy - 1);
+    ci[r] = inw && in(j, 2, gjx - 2) && in(i, 2, giy - 2);
+    di[r] = inw && in(j, 2, gjx - 1) && in(i, 2, giy - 1);
     bnd[r] = ce[r] && !ci[r] &&
              (((j == 1 || j == gjx - 1) && in(i, 2, giy - 2)) || i == 1 || i == giy - 1);
     own[r] = in(j, J1, J1 + SPB - 1) && in(i, I1, I1 + SPB - 1);
@@ -1260,7 +1274,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   }
   for (int r = 0; r < NR; r++) {
     const int j = jr0 + tx, i = ir0 + ty + 16 * r;
-    if (own[r] && in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2)) {
+    if (own[r] && in(j, g.jde1 - (g.bl ? 0 : 1), g.jde2) && in(i, g.ide1 - (g.bb ? 0 : 1), g.ide2)) {
       const long q = (long)(l - 1) * g.plane + g.ix(j, i);
       ddsum[q] = ce[r] ? sd[r] : d_zero;
       dhsum[q] = ce[r] ? sh[r] : d_zero;

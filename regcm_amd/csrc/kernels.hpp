@@ -14,6 +14,8 @@ struct Seg {
 constexpr int MAXSEG = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
+// depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
+constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level)
 constexpr int MBJ = 64, MBI = 8, MBT = MBJ * MBI;
 // LDS-tiled scalar (t, qv, qc) block (cross points j x i at one level)

@@ -115,6 +115,23 @@ def test_decomposition_invariance(c1_data, nproc):
         assert np.array_equal(ref.get(name), til.get(name)), name
 
 
+@pytest.mark.parametrize("nproc", [(2, 1), (2, 2), (2, 4)])
+def test_decomposition_invariance_c3(nproc):
+    """The headline domain on the set_nproc tilings of 2/4/8 GPUs (local tiles): bit-identical
+    to one tile, including the partial blocks the ghost-ring kernels run on 96 x 48 tiles."""
+    from regcm_amd.dycore import DynCore
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    ref = DynCore(rc, data["split"])
+    til = DynCore(rc, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    for e in (ref, til):
+        e.put_state(data["state"])
+        e.bdyval()
+        e.step(5)
+    for name in STATE_FIELDS:
+        assert np.array_equal(ref.get(name), til.get(name)), name
+
+
 def test_c2_ten_steps():
     rc = CONFIGS["C2"]
     data = icbc.generate(rc)
