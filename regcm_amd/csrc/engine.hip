@@ -109,34 +109,38 @@ void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::ve
   rg.assign(g.plane, 0);
   ib.assign(g.plane, -1);
   auto set = [&](int j, int i, int r, int b) { rg[g.ix(j, i)] = (int8_t)r; ib[g.ix(j, i)] = (int16_t)b; };
-  for (int i = g.ide1; i <= g.ide2; i++)
+  // every frame point of the global domain (owned and ghost): the masks are functions of the
+  // global index, so ghost points carry their owners' values
+  const int fi1 = std::max(1, g.i0), fi2 = std::min(iy, g.i0 + g.ni - 1);
+  const int fj1 = std::max(1, g.j0), fj2 = std::min(jx, g.j0 + g.nj - 1);
+  for (int i = fi1; i <= fi2; i++)
     if (i >= igbb1 && i <= igbb2)
-      for (int j = g.jde1; j <= g.jde2; j++)
+      for (int j = fj1; j <= fj2; j++)
         if (j >= jgbl1 && j <= jgbr2) {
           if (j <= jgbl2 && i >= j) continue;
           if (j >= jgbr1 && i >= (jgbr2 - j + 2)) continue;
           set(j, i, 1, i - igbb1 + 2);
         }
-  for (int i = g.ide1; i <= g.ide2; i++)
+  for (int i = fi1; i <= fi2; i++)
     if (i >= igbt1 && i <= igbt2)
-      for (int j = g.jde1; j <= g.jde2; j++)
+      for (int j = fj1; j <= fj2; j++)
         if (j >= jgbl1 && j <= jgbr2) {
           if (j <= jgbl2 && (igbt2 - i + 2) >= j) continue;
           if (j >= jgbr1 && (igbt2 - i) >= (jgbr2 - j)) continue;
           set(j, i, 2, igbt2 - i + 2);
         }
-  for (int i = g.ide1; i <= g.ide2; i++) {
+  for (int i = fi1; i <= fi2; i++) {
     if (i < igbb1 || i > igbt2) continue;
-    for (int j = g.jde1; j <= g.jde2; j++)
+    for (int j = fj1; j <= fj2; j++)
       if (j >= jgbl1 && j <= jgbl2) {
         if (i < igbb2 && j > i) continue;
         if (i > igbt1 && j > (igbt2 - i + 2)) continue;
         set(j, i, 3, j - jgbl1 + 2);
       }
   }
-  for (int i = g.ide1; i <= g.ide2; i++) {
+  for (int i = fi1; i <= fi2; i++) {
     if (i < igbb1 || i > igbt2) continue;
-    for (int j = g.jde1; j <= g.jde2; j++)
+    for (int j = fj1; j <= fj2; j++)
       if (j >= jgbr1 && j <= jgbr2) {
         if (i < igbb2 && (jgbr2 - j + 2) > i) continue;
         if (i > igbt1 && (jgbr2 - j) > (igbt2 - i)) continue;
@@ -208,6 +212,7 @@ struct rcmdyn_engine {
   hipGraphExec_t gexec[2] = {nullptr, nullptr};
   bool statics_dirty = true;
   bool bdy_dirty = true;
+  bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
   bool capturing = false;
   long slen = 0;
   long staging_cap = 0;
@@ -369,14 +374,15 @@ struct rcmdyn_engine {
     }
     slen = std::max<long>(g.pitch, g.ni);
     for (int s = 0; s < 16; s++) t.sl[s] = dalloc(t, (size_t)slen * kz);
-    // halo staging: 8 directions x widest exchange (6 fields x width 2 x (kz+1) levels)
-    staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 2 * (kz + 1) * 8);
+    // halo staging: 8 directions x widest exchange (the hydrostatic prologue: 5 fields 2 wide
+    // + 5 fields 3 wide + p*; at most 32 field-widths of kz+1 levels)
+    staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 32 * (kz + 1));
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     // column blocks of k_columns (one noise partial each)
-    // k_columns blocks: 64 columns x one row, over the tile and its left/bottom ghost ring
-    t.ncolx = (g.jde2 - (g.jde1 - (g.bl ? 0 : 1)) + 64) / 64;
-    t.nred = t.ncolx * (g.ide2 - (g.ide1 - (g.bb ? 0 : 1)) + 1);
+    // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
+    t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
+    t.nred = t.ncolx * (g.idx2() - g.idx1() + 1);
     t.red_off = red_total;
     red_total += t.nred;
     if (cfg.idynamic == 2) setup_nh(t);
@@ -627,6 +633,7 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
     if ((f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) || (f >= RCMDYN_XPPB_B0 && f <= RCMDYN_XWWB_BT)) bdy_dirty = true;
+    ghosts_stale = true;
     if (f >= RCMDYN_ATM0_PS) invalidate_graphs();
   }
 
@@ -817,6 +824,14 @@ struct rcmdyn_engine {
       if (g.jde2 - g.jde1 + 1 < SPX || g.ide2 - g.ide1 + 1 < SPX) return false;
     return true;
   }
+  // The decomposed hydrostatic step runs without the post-prologue exchanges when the fused
+  // split step applies (every tile at least SPX wide, every mode within SPH sub-steps): its
+  // kernels then compute the ghost rings their consumers read.
+  bool split_fused() const {
+    bool f = wide_ok();
+    for (int l = 1; l <= cfg.nsplit; l++) f = f && ((int)hc.aam[l - 1] * 2 <= SPH);
+    return f;
+  }
   void copy_wide(Tile& t, const double* src, double* dst, int nplanes) {
     KLAUNCH(k_copy_frame, grid3(t.g.jde2 - t.g.jde1 + 1, t.g.ide2 - t.g.ide1 + 1, 1), BLK, 0, stream, t.g, t.gw,
             nplanes, src, (long)t.g.plane, dst, (long)t.gw.plane);
@@ -878,8 +893,9 @@ struct rcmdyn_engine {
     }
     if (bdy_dirty) {
       const int kz = cfg.kz;
-      xch({{FK::UB0, kz}, {FK::UBT, kz}, {FK::VB0, kz}, {FK::VBT, kz}}, 1, 0);
-      xch({{FK::TB0, kz}, {FK::TBT, kz}, {FK::QB0, kz}, {FK::QBT, kz}, {FK::PB0, 1}, {FK::PBT, 1}}, 1, 0);
+      // width 2: the ghost-ring kernels relax at ghost points (stencil radius 1)
+      xch({{FK::UB0, kz}, {FK::UBT, kz}, {FK::VB0, kz}, {FK::VBT, kz}}, 2, 0);
+      xch({{FK::TB0, kz}, {FK::TBT, kz}, {FK::QB0, kz}, {FK::QBT, kz}, {FK::PB0, 1}, {FK::PBT, 1}}, 2, 0);
       bdy_dirty = false;
       invalidate_graphs();
     }
@@ -1056,7 +1072,7 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0,
+      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
               stream, g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
               t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt,
               t.pb0, t.pbt, slices(t), slen, 0);
@@ -1081,9 +1097,13 @@ struct rcmdyn_engine {
     // Main/mod_slice.F90:102-300): the decoupled fields are recomputed where read, so their
     // exchanges become exchanges of atm1 (width 1) and atm2 (idif = 2); p* travels 3 wide so
     // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
-    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz},
-         {FK::A1QC, kz}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, 2},
-         {FK::A2QC, kz, 2}});
+    // atm1 travels 2 wide and atm2 3 wide: one more than the reference's widths, for the
+    // ghost rings the kernels below compute in place of the later exchanges
+    const bool fused = split_fused();
+    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2}, {FK::A1QV, kz, 2},
+         {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
+         {FK::A2QC, kz, 3}});
+    ghosts_stale = false;
     // surface_pressures + 2-D reciprocals, :815-834
     each([&](Tile& t) {
       KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
@@ -1098,32 +1118,31 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const Fields f = fields(t);
-      KLAUNCH(k_momentum, dim3((g.jdi2 - g.jdi1 + MBJ) / MBJ, (g.idi2 - g.idi1 + MBI) / MBI, kz), dim3(MBT), 0,
+      const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
+      KLAUNCH(k_momentum, dim3((mj2 - g.jdi1 + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, kz), dim3(MBT), 0,
               stream, g, dc, ds, f);
-      KLAUNCH(k_scalars, dim3((g.jce2 - g.jce1 + SBJ) / SBJ, (g.ice2 - g.ice1 + SBI) / SBI, kz), dim3(SBT), 0,
-              stream, g, dc, ds, f);
+      KLAUNCH(k_scalars, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, kz), dim3(SBT),
+              0, stream, g, dc, ds, f);
     });
-    xch({{FK::CQV, kz}, {FK::CQC, kz}});
+    if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     each([&](Tile& t) {
       KLAUNCH(k_qfilter, grid3((t.g.nj + 1) / 2, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
       t.cur = 1 - t.cur;
     });
     // splitf, Main/mod_split.F90:243-461
-    xch({{FK::PSA, 1}, {FK::A1U, kz, 1, 2}, {FK::A1V, kz, 1, 2}, {FK::A2U, kz, 1, 2}, {FK::A2V, kz, 1, 2}});
+    if (!fused) xch({{FK::PSA, 1}, {FK::A1U, kz, 1, 2}, {FK::A1V, kz, 1, 2}, {FK::A2U, kz, 1, 2}, {FK::A2V, kz, 1, 2}});
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
       QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
              t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.depplane};
-      const int nxp = (g.jde2 - g.jde1 + 64) / 64, nproj = nxp * (g.ide2 - g.ide1 + 1);
+      const int nxp = (g.jdx2() - g.jde1 + 64) / 64, nproj = nxp * (g.idx2() - g.ide1 + 1);
       KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
-    bool fused = wide_ok();
-    for (int l = 1; l <= ns; l++) fused = fused && ((int)hc.aam[l - 1] * 2 <= SPH);
     if (fused && ntiles > 1) {
       // one depth-SPX exchange of every split-step input instead of three per sub-step
       each([&](Tile& t) {
@@ -1137,8 +1156,7 @@ struct rcmdyn_engine {
     if (fused) {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        const int jlo = g.jce1 - (g.bl ? 0 : 1), ilo = g.ice1 - (g.bb ? 0 : 1);
-        dim3 gr((g.jce2 - jlo + SPB) / SPB, (g.ice2 - ilo + SPB) / SPB, ns);
+        dim3 gr((g.jcx2() - g.jcx1() + SPB) / SPB, (g.icx2() - g.icx1() + SPB) / SPB, ns);
         if (ntiles > 1)
           KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
                   t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
@@ -1169,7 +1187,7 @@ struct rcmdyn_engine {
       Tile& t = tiles[q];
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_split_correct, grid3((g.jde2 - g.jde1 + 2) / 2, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g,
+      KLAUNCH(k_split_correct, grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz), BLK, 0, stream, g,
                          dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
                          t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total);
     }
@@ -1204,13 +1222,14 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 64) / 64, 6, kz), dim3(64), 0,
+      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
               stream, g, ds,
                          t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
                          t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0,
                          t.qbt, t.pb0, t.pbt, slices(t), slen, (int)(cfg.idynamic == 1));
     });
-    xch_slices();
+    // the ghost-ring step wrote the slice entries past the tile itself (k_bdyval_set)
+    if (ghosts_stale || !split_fused()) xch_slices();
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),

@@ -46,6 +46,34 @@ struct Geom {
   __host__ __device__ __forceinline__ uint32_t o3(int j, int i, int k) const {
     return o2(j, i) + (uint32_t)(k - 1) * L8;
   }
+  // The owned dot (d) and cross (c) ranges extended by the ghost ring toward neighbours (depth
+  // 1).  The kernels of a decomposed hydrostatic step compute these rings exactly as their
+  // owners do, in place of the halo exchanges the reference performs there.
+  __host__ __device__ __forceinline__ int jdx1() const { return jde1 - (bl ? 0 : 1); }
+  __host__ __device__ __forceinline__ int jdx2() const { return jde2 + (br ? 0 : 1); }
+  __host__ __device__ __forceinline__ int idx1() const { return ide1 - (bb ? 0 : 1); }
+  __host__ __device__ __forceinline__ int idx2() const { return ide2 + (bt ? 0 : 1); }
+  __host__ __device__ __forceinline__ int jcx1() const { return jce1 - (bl ? 0 : 1); }
+  __host__ __device__ __forceinline__ int jcx2() const { return jce2 + (br ? 0 : 1); }
+  __host__ __device__ __forceinline__ int icx1() const { return ice1 - (bb ? 0 : 1); }
+  __host__ __device__ __forceinline__ int icx2() const { return ice2 + (bt ? 0 : 1); }
+  // Global index classes (Main/mod_atm_interface.F90:231-302 on one tile): equal to the tile
+  // ranges jce/jci/jcii/jdi/jdii on owned points, and defined on ghost points.
+  __host__ __device__ __forceinline__ bool gce(int j, int i) const {
+    return j >= 1 && j <= gjx - 1 && i >= 1 && i <= giy - 1;
+  }
+  __host__ __device__ __forceinline__ bool gci(int j, int i) const {
+    return j >= 2 && j <= gjx - 2 && i >= 2 && i <= giy - 2;
+  }
+  __host__ __device__ __forceinline__ bool gcii(int j, int i) const {
+    return j >= 3 && j <= gjx - 3 && i >= 3 && i <= giy - 3;
+  }
+  __host__ __device__ __forceinline__ bool gdi(int j, int i) const {
+    return j >= 2 && j <= gjx - 1 && i >= 2 && i <= giy - 1;
+  }
+  __host__ __device__ __forceinline__ bool gdii(int j, int i) const {
+    return j >= 3 && j <= gjx - 2 && i >= 3 && i <= giy - 2;
+  }
 };
 
 // Run constants (read-only on device, one copy per engine).

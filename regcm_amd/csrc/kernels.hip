@@ -27,18 +27,22 @@ namespace rcm {
 
 // K1. surface_pressures, Main/mod_tendency.F90:815-834, and the 2-D reciprocals of decouple
 // (rpsda, :868-875) and mkslice (1/psdotb, 1/psb, Main/mod_slice.F90:163-183), on the owned
-// points and the ghost ring the consumers read (ga for atm1-derived, gb for atm2-derived).
+// points and the ghost rings the consumers read: depth 2 for the atm1-derived ones and 3 for
+// the atm2-derived ones (the stencils of the ghost-ring kernels), inside the global domain.
 __global__ void k_surface_pressures(Geom g, Fields f) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
-  if (in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
-  if (in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
+  auto ring = [&](int d, int jhi, int ihi) {
+    return in(j, max(1, g.jde1 - d), min(jhi, g.jde2 + d)) && in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
+  };
+  if (ring(2, g.gjx - 1, g.giy - 1)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
+  if (ring(3, g.gjx - 1, g.giy - 1)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
+  if (ring(2, g.gjx, g.giy)) {
     const double v = psc2psd_global(g, f.psa, j, i);
     F2(f.psdota, j, i) = v;
     F2(f.rpsda, j, i) = d_one / v;
   }
-  if (in(j, g.jde1gb, g.jde2gb) && in(i, g.ide1gb, g.ide2gb)) {
+  if (ring(3, g.gjx, g.giy)) {
     const double v = psc2psd_global(g, f.psb, j, i);
     F2(f.psdotb, j, i) = v;
     F2(f.rpsdb, j, i) = d_one / v;
@@ -72,15 +76,14 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
   const int bb = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
-  // columns of the tile plus its ghost ring toward left/bottom neighbours: k_momentum reads
-  // qdot and phi there, and the ghost columns compute exactly what their owners do (no
-  // qdot/phi exchange)
-  const int jlo = g.jde1 - (g.bl ? 0 : 1), ilo = g.ide1 - (g.bb ? 0 : 1);
-  const int j = jlo + (bb % nxb) * 64 + tx, i = ilo + bb / nxb;
-  const bool valid = j <= g.jde2;
+  // columns of the tile plus its ghost ring toward neighbours: the ghost columns compute
+  // exactly what their owners do (qdot, phi, pten and the new p* there replace the
+  // reference's exchanges of them)
+  const int j = g.jdx1() + (bb % nxb) * 64 + tx, i = g.idx1() + bb / nxb;
+  const bool valid = j <= g.jdx2();
   const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
-  const bool ce = own || (valid && in(j, jlo, g.jce2) && in(i, ilo, g.ice2));
-  const bool ci = own && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+  const bool ce = valid && in(j, g.jcx1(), g.jcx2()) && in(i, g.icx1(), g.icx2());
+  const bool ci = ce && g.gci(j, i);
   const int kz = c->kz;
   double* sMD = lds;                                      // mass divergence, [k-1][tx]
   double* sTD = lds + kz * 64;                            // td
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       }
       ST(f.qdot, o2 + (uint32_t)kz * L8, d_zero);
     }
-    if (own) {
+    if (ce) {
       // new_pressure
       const double dt = s->dt;
       const double psbv = LD(f.psb, o2);
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       ST(f.ptenn, o2, pt);
       const double pc = psbv + pt * dt;
       ST(f.psc, o2, pc);
-      if (s->lcount > 0 && ci) {
+      if (s->lcount > 0 && ci && own) {
         na = fabs(pt);
         nb = fabs((pc + psbv - d_two * LD(f.psa, o2)) / (dt * dt * d_rfour));
       }
@@ -252,9 +255,11 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
   const double ep1 = c->ep1;
   // this thread's point and its point operands, loaded before the staging barrier so their
   // latency overlaps it (threads past the interior read a valid interior address)
+  // the tile's jdi x idi points and its right/top ghost ring (k_split_project's divergence and
+  // the bdyuv slices read the new u, v there); boundary branches test global indices
   const int tj = tid % MBJ, ti = tid / MBJ;
   const int j = J0 + tj, i = I0 + ti;
-  const bool valid = j <= g.jdi2 && i <= g.idi2;
+  const bool valid = j <= (g.br ? g.jdi2 : g.jde2 + 1) && i <= (g.bt ? g.idi2 : g.ide2 + 1);
   const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jdi1, g.idi1), o3 = o2 + kof;
   const double u1c = LD(f.a1u, o3), v1c = LD(f.a1v, o3), u2c = LD(f.a2u, o3), v2c = LD(f.a2v, o3);
   const double u1m = (k >= 2) ? LD(f.a1u, o3 - L8) : 0.0, v1m = (k >= 2) ? LD(f.a1v, o3 - L8) : 0.0;
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     const int t = tid + n * MBT, jj = t % TW0, ii = t / TW0, jg = J0 - 1 + jj, ig = I0 - 1 + ii;
     if (t < TW0 * TH0) {
       double xk = 0.0;
-      if (in(jg, g.jce1ga, g.jce2ga) && in(ig, g.ice1ga, g.ice2ga)) {
+      if (g.gce(jg, ig)) {
         const int y = ii + 1, x = jj + 1;            // (jg, ig) in the halo-2 tiles
         const double dudx = sUB[y][x + 1] + sUB[y + 1][x + 1] - sUB[y][x] - sUB[y + 1][x];
         const double dvdx = sVB[y][x + 1] + sVB[y + 1][x + 1] - sVB[y][x] - sVB[y + 1][x];
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
       vt = vt + xkd * (o4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +
                        o4_c2 * (UM(sVM, 1, 1) + UM(sVM, -1, -1) + UM(sVM, -1, 1) + UM(sVM, 1, -1)) +
                        o4_c3 * (UM(sVM, 0, 0)));
-    } else if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2)) {
+    } else if (g.gdii(j, i)) {
       ut = ut - xkd * (z4_c1 * (UM(sUM, 2, 0) + UM(sUM, -2, 0) + UM(sUM, 0, 2) + UM(sUM, 0, -2)) +
                        z4_c2 * (UM(sUM, 1, 0) + UM(sUM, -1, 0) + UM(sUM, 0, 1) + UM(sUM, 0, -1)) +
                        z4_c3 * (UM(sUM, 0, 0)));
@@ -473,10 +478,10 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
   vt = vt + xkd * (z4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +        \
                    z4_c2 * (UM(sVM, 0, 0)));
     if (c->idiffu == 1) {
-      if (g.bl && j == g.jdi1) { LAPD(); }
-      if (g.br && j == g.jdi2) { LAPD(); }
-      if (g.bb && i == g.idi1) { LAPD(); }
-      if (g.bt && i == g.idi2) { LAPD(); }
+      if (j == 2) { LAPD(); }
+      if (j == g.gjx - 1) { LAPD(); }
+      if (i == 2) { LAPD(); }
+      if (i == g.giy - 1) { LAPD(); }
     }
 #undef LAPD
 #undef UM
@@ -575,18 +580,18 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
            o4_c3 * H2T(S, 0, 0));                                                                 \
       break;                                                                                      \
     }                                                                                             \
-    if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))                                       \
+    if (g.gcii(j, i))                                                                             \
       ften = ften - d_one * xkcs *                                                                \
           (z4_c1 * (H2T(S, 2, 0) + H2T(S, -2, 0) + H2T(S, 0, 2) + H2T(S, 0, -2)) +                \
            z4_c2 * (H2T(S, 1, 0) + H2T(S, -1, 0) + H2T(S, 0, 1) + H2T(S, 0, -1)) +                \
            z4_c3 * H2T(S, 0, 0));                                                                 \
-    if (g.bl && j == g.jci1) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (j == 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
-    if (g.br && j == g.jci2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (j == g.gjx - 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
-    if (g.bb && i == g.ici1) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (i == 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
-    if (g.bt && i == g.ici2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (i == g.giy - 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
   } while (0)
 
@@ -599,7 +604,9 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
 #ifdef RCM_PHASE_TIMING
   const long long pt0 = wall_clock64();
 #endif
-  const int J0 = g.jce1 + (int)blockIdx.x * SBJ, I0 = g.ice1 + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
+  // the tile's cross points and its ghost ring (k_qfilter's moisture fix reads the forecasts
+  // there); boundary branches test global indices
+  const int J0 = g.jcx1() + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
   const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
@@ -608,7 +615,7 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
   // this thread's point and its point operands, loaded before the staging barrier
   const int tj = tid % SBJ, ti = tid / SBJ;
   const int j = J0 + tj, i = I0 + ti;
-  const bool valid = j <= g.jce2 && i <= g.ice2;
+  const bool valid = j <= g.jcx2() && i <= g.icx2();
   const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jce1, g.ice1), o3 = o2 + kof;
   const double t1 = LD(f.a1t, o3), t2 = LD(f.a2t, o3), qv2 = LD(f.a2qv, o3), qc2 = LD(f.a2qc, o3);
   const double qv1 = LD(f.a1qv, o3), qc1 = LD(f.a1qc, o3);
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
     const double duv = sqrt((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy));
     xkc = dmin(hgf + c->dydc * duv, c->xkhmax);
   }
-  if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
+  if (!g.gci(j, i)) {
     ST(f.cqv, o3, qv2);
     ST(f.cqc, o3, qc2);
     if (f.xkcs) ST(f.xkcs, o3, xkc);
@@ -904,15 +911,22 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
   const int k = (int)blockIdx.z + 1;
   if (jp >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
   const uint32_t o2 = g.o2(jp, i), o3 = o2 + (uint32_t)(k - 1) * g.L8;
-  const bool ici = in(i, g.ici1, g.ici2), idi = in(i, g.idi1, g.idi2);
+  // owned points (the moisture fix and filters)
+  const bool ici = in(i, g.ici1, g.ici2);
   const bool ci0 = ici && in(jp, g.jci1, g.jci2), ci1 = ici && in(jp + 1, g.jci1, g.jci2);
-  const bool di0 = idi && in(jp, g.jdi1, g.jdi2), di1 = idi && in(jp + 1, g.jdi1, g.jdi2);
+  // points k_scalars (cross ring) and k_momentum (dot, right/top ring) updated; p* is filtered
+  // on the cross ring too (k_split_project's psdota and the split corrections read it there)
+  const bool icx = in(i, g.icx1(), g.icx2()), idx = in(i, g.idi1, g.bt ? g.idi2 : g.ide2 + 1);
+  const int jd2 = g.br ? g.jdi2 : g.jde2 + 1;
+  const bool xi0 = icx && in(jp, g.jcx1(), g.jcx2()) && g.gci(jp, i);
+  const bool xi1 = icx && in(jp + 1, g.jcx1(), g.jcx2()) && g.gci(jp + 1, i);
+  const bool di0 = idx && in(jp, g.jdi1, jd2), di1 = idx && in(jp + 1, g.jdi1, jd2);
   // p* RA filter on the fly (k = 1 threads store it)
   double2 pa = LD2(f.psa, o2), pb = LD2(f.psb, o2);
-  if (ci0 || ci1) {
+  if (xi0 || xi1) {
     const double2 psc = LD2(f.psc, o2);
-    if (ci0) { const double d = c->gnu1 * (psc.x + pb.x - d_two * pa.x); pb.x = pa.x + d; pa.x = psc.x; }
-    if (ci1) { const double d = c->gnu1 * (psc.y + pb.y - d_two * pa.y); pb.y = pa.y + d; pa.y = psc.y; }
+    if (xi0) { const double d = c->gnu1 * (psc.x + pb.x - d_two * pa.x); pb.x = pa.x + d; pa.x = psc.x; }
+    if (xi1) { const double d = c->gnu1 * (psc.y + pb.y - d_two * pa.y); pb.y = pa.y + d; pa.y = psc.y; }
   }
   if (k == 1) { ST2(f.bpsa, o2, pa); ST2(f.bpsb, o2, pb); }
   // points k_momentum / k_scalars do not update keep their values in the next buffers
@@ -921,7 +935,7 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
 #define KEEP(dst, src, upd) x = LD2(dst, o3); { const double2 y = LD2(src, o3);              \
     if (!upd##0) x.x = y.x; if (!upd##1) x.y = y.y; } ST2(dst, o3, x);
     if (!(di0 && di1)) { KEEP(f.b1u, f.a1u, di) KEEP(f.b1v, f.a1v, di) KEEP(f.b2u, f.a2u, di) KEEP(f.b2v, f.a2v, di) }
-    if (!(ci0 && ci1)) { KEEP(f.b1t, f.a1t, ci) KEEP(f.b2t, f.a2t, ci) }
+    if (!(xi0 && xi1)) { KEEP(f.b1t, f.a1t, xi) KEEP(f.b2t, f.a2t, xi) }
 #undef KEEP
   }
   if (!ci0 && !ci1) {
@@ -1015,17 +1029,24 @@ __global__ __launch_bounds__(512) void k_split_project(
     return;
   }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  // owned dot points, plus psdota on the right/top ghost ring (the split corrections of the
+  // ghost-ring u, v read it there)
   const int j = g.jde1 + (b % nxp) * 64 + tx, i = g.ide1 + b / nxp;
-  const bool valid = j <= g.jde2;
+  const bool valid = j <= g.jde2 && i <= g.ide2;
+  const bool vpd = j <= g.jdx2() && i <= g.idx2();
   const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const int kz = c->kz;
   double* sD1 = lds;
   double* sD2 = lds + kz * 64;
   double* sT1 = lds + 2 * kz * 64;
   double* sT2 = lds + 3 * kz * 64;
-  if (valid && ty == 0) {
+  if (ty == 0) {
     double v;
-    if (psc2psd_at(g, psa, j, i, v)) F2(psdota, j, i) = v;
+    if (valid) {
+      if (psc2psd_at(g, psa, j, i, v)) F2(psdota, j, i) = v;
+    } else if (vpd) {
+      F2(psdota, j, i) = psc2psd_global(g, psa, j, i);
+    }
   }
   if (ce) {
     const double m00 = F2(msfd, j, i), m10 = F2(msfd, j + 1, i), m01 = F2(msfd, j, i + 1), m11 = F2(msfd, j + 1, i + 1);
@@ -1173,11 +1194,10 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
   __shared__ double Ds[2][SPR][SPP], Hs[2][SPR][SPP], U[SPR][SPP], V[SPR][SPP];
   const int l = blockIdx.z + 1;
-  // owned blocks tile the tile's cross points plus its ghost ring toward left/bottom
-  // neighbours (k_split_correct reads ddsum/dhsum there; no dhsum exchange).  The first block's
-  // region then starts SPH + 1 points below the tile, the depth of the wide exchange.
-  const int jlo = g.jce1 - (g.bl ? 0 : 1), ilo = g.ice1 - (g.bb ? 0 : 1);
-  const int J1 = jlo + blockIdx.x * SPB, I1 = ilo + blockIdx.y * SPB;
+  // owned blocks tile the tile's cross points plus its ghost ring (k_split_correct reads
+  // ddsum/dhsum there; no dhsum exchange).  The ring's regions reach SPH + 1 points beyond the
+  // tile, the depth of the wide exchange.
+  const int J1 = g.jcx1() + blockIdx.x * SPB, I1 = g.icx1() + blockIdx.y * SPB;
   const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
   const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 16
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
@@ -1274,7 +1294,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   }
   for (int r = 0; r < NR; r++) {
     const int j = jr0 + tx, i = ir0 + ty + 16 * r;
-    if (own[r] && in(j, g.jde1 - (g.bl ? 0 : 1), g.jde2) && in(i, g.ide1 - (g.bb ? 0 : 1), g.ide2)) {
+    if (own[r] && in(j, g.jdx1(), g.jdx2()) && in(i, g.idx1(), g.idx2())) {
       const long q = (long)(l - 1) * g.plane + g.ix(j, i);
       ddsum[q] = ce[r] ? sd[r] : d_zero;
       dhsum[q] = ce[r] ? sh[r] : d_zero;
@@ -1311,15 +1331,18 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
       if (s->lcount == 2) s->dt = d_two * c->dtsec;
     }
   }
-  // two adjacent points (jp, jp+1) per thread, 16-byte accesses (jp - j0 is even)
+  // two adjacent points (jp, jp+1) per thread, 16-byte accesses (jp - j0 is even); owned points
+  // and the right/top ghost ring (the bdyuv slices read the new u, v there)
   const int jp = g.jde1 + 2 * (j - g.jde1);
-  if (jp > g.jde2 || i > g.ide2) return;
+  if (jp > g.jdx2() || i > g.idx2()) return;
   const uint32_t o2 = g.o2(jp, i), o3 = o2 + (uint32_t)(k - 1) * g.L8;
   const double gnu1 = c->gnu1;
   const int ns = c->nsplit;
-  const bool ici = in(i, g.ici1, g.ici2), idi = in(i, g.idi1, g.idi2);
-  const bool ci0 = ici && in(jp, g.jci1, g.jci2), ci1 = ici && in(jp + 1, g.jci1, g.jci2);
-  const bool di0 = idi && in(jp, g.jdi1, g.jdi2), di1 = idi && in(jp + 1, g.jdi1, g.jdi2);
+  const int jd2 = g.br ? g.jdi2 : g.jde2 + 1, id2 = g.bt ? g.idi2 : g.ide2 + 1;
+  const bool ici = in(i, g.ice1, g.icx2()), idi = in(i, g.idi1, id2);
+  const bool ci0 = ici && in(jp, g.jce1, g.jcx2()) && g.gci(jp, i);
+  const bool ci1 = ici && in(jp + 1, g.jce1, g.jcx2()) && g.gci(jp + 1, i);
+  const bool di0 = idi && in(jp, g.jdi1, jd2), di1 = idi && in(jp + 1, g.jdi1, jd2);
   if (ci0 || ci1) {
     double dd[2][MAXSPLIT];
     for (int l = 1; l <= ns; l++) {
@@ -1388,19 +1411,25 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
   // thread -> one point of the boundary lines: blockIdx.y 0..2 = rows i = ide1 (bottom),
   // ide2 (top), ice2 (top cross row) over jde; 3..5 = columns j = jde1, jde2, jce2 over ide
   // minus the points a row owns.  Every point the body modifies lies on these lines.
+  // One point past the tile along each line (toward a neighbour) only writes the bdyuv slice
+  // entry there, from the ghost-ring u, v and the boundary data: k_bdyval_qc reads it (the
+  // reference exchanges the slices instead, exchange_bdy_lr/bt).
   const int line = blockIdx.y, k = (int)blockIdx.z + 1;
   const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);
   int j, i;
+  bool ghost = false;
   if (line < 3) {
     if (line == 0 ? !g.bb : !g.bt) return;
     i = (line == 0) ? g.ide1 : (line == 1) ? g.ide2 : g.ice2;
     j = g.jde1 + x;
-    if (j > g.jde2) return;
+    if (j > g.jdx2() || (j > g.jde2 && line == 2)) return;
+    ghost = j > g.jde2;
   } else {
     if (line == 3 ? !g.bl : !g.br) return;
     j = (line == 3) ? g.jde1 : (line == 4) ? g.jde2 : g.jce2;
     i = g.ide1 + x;
-    if (i > g.ide2) return;
+    if (i > g.idx2() || (i > g.ide2 && line == 5)) return;
+    ghost = i > g.ide2;
     if ((g.bb && i == g.ide1) || (g.bt && (i == g.ide2 || i == g.ice2))) return;
   }
   const long q = g.ix(j, i);
@@ -1412,7 +1441,7 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
   const bool dR = g.br && j == g.jde2 && in(i, g.idi1, g.idi2);
   const bool dB = g.bb && i == g.ide1;
   const bool dT = g.bt && i == g.ide2;
-  if (dL || dR || dB || dT) {
+  if (!ghost && (dL || dR || dB || dT)) {
     if (integ) { a2u[p] = a1u[p]; a2v[p] = a1v[p]; }
     a1u[p] = ub0[p] + xt * ubt[p];
     a1v[p] = vb0[p] + xt * vbt[p];
@@ -1422,7 +1451,7 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
   const bool cR = g.br && j == g.jce2 && in(i, g.ici1, g.ici2);
   const bool cB = g.bb && i == g.ice1 && in(j, g.jce1, g.jce2);
   const bool cT = g.bt && i == g.ice2 && in(j, g.jce1, g.jce2);
-  if (cL || cR || cB || cT) {
+  if (!ghost && (cL || cR || cB || cT)) {
     if (integ) {
       a2t[p] = a1t[p]; a2qv[p] = a1qv[p]; a2qc[p] = a1qc[p];
       if (set_ps && k == 1) psb[q] = psa[q];
@@ -1432,24 +1461,25 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
     a1qv[p] = qb0[p] + xt * qbt[p];
   }
   // bdyuv slices (interior slice values are interior points: not modified above)
-  if (g.bl && j == g.jde1 && in(i, g.idi1, g.idi2)) {
+  if (g.bl && j == g.jde1 && (in(i, g.idi1, g.idi2) || ghost)) {
     SLI(sl.s[1], i, k) = F3(a1u, g.jdi1, i, k); SLI(sl.s[5], i, k) = F3(a1v, g.jdi1, i, k);
     SLI(sl.s[0], i, k) = ub0[p] + xt * ubt[p]; SLI(sl.s[4], i, k) = vb0[p] + xt * vbt[p];
   }
-  if (g.br && j == g.jde2 && in(i, g.idi1, g.idi2)) {
+  if (g.br && j == g.jde2 && (in(i, g.idi1, g.idi2) || ghost)) {
     SLI(sl.s[3], i, k) = F3(a1u, g.jdi2, i, k); SLI(sl.s[7], i, k) = F3(a1v, g.jdi2, i, k);
     SLI(sl.s[2], i, k) = ub0[p] + xt * ubt[p]; SLI(sl.s[6], i, k) = vb0[p] + xt * vbt[p];
   }
   if (g.bb && i == g.ide1) {
-    if (in(j, g.jdi1, g.jdi2)) { SLJ(sl.s[9], j, k) = F3(a1u, j, g.idi1, k); SLJ(sl.s[13], j, k) = F3(a1v, j, g.idi1, k); }
+    if (in(j, g.jdi1, g.jdi2) || ghost) { SLJ(sl.s[9], j, k) = F3(a1u, j, g.idi1, k); SLJ(sl.s[13], j, k) = F3(a1v, j, g.idi1, k); }
     SLJ(sl.s[8], j, k) = ub0[p] + xt * ubt[p]; SLJ(sl.s[12], j, k) = vb0[p] + xt * vbt[p];
   }
   if (g.bt && i == g.ide2) {
-    if (in(j, g.jdi1, g.jdi2)) { SLJ(sl.s[11], j, k) = F3(a1u, j, g.idi2, k); SLJ(sl.s[15], j, k) = F3(a1v, j, g.idi2, k); }
+    if (in(j, g.jdi1, g.jdi2) || ghost) { SLJ(sl.s[11], j, k) = F3(a1u, j, g.idi2, k); SLJ(sl.s[15], j, k) = F3(a1v, j, g.idi2, k); }
     SLJ(sl.s[10], j, k) = ub0[p] + xt * ubt[p]; SLJ(sl.s[14], j, k) = vb0[p] + xt * vbt[p];
   }
   // bdyuv corner fills, Main/mod_bdycod.F90:1030-1061: every corner slice entry is the
   // boundary value b0 + xt*bt of a known point, written by the thread of that tile corner
+  if (ghost) return;
 #define UB(J, I) (F3(ub0, J, I, k) + xt * F3(ubt, J, I, k))
 #define VB(J, I) (F3(vb0, J, I, k) + xt * F3(vbt, J, I, k))
   if (g.bt && g.bl && j == g.jde1 && i == g.ide2) {
@@ -1551,7 +1581,9 @@ __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu
                                  double* mapf) {
   THREAD_POINT(g.j0, g.i0);
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
-  if (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2)) {
+  // dmsf/xmsf on the global dot interior of the tile and its 2-deep ghost ring (the map
+  // factors' exchange depth): the ghost-ring kernels read them there
+  if (g.gdi(j, i) && in(j, g.jde1 - 2, g.jde2 + 2) && in(i, g.ide1 - 2, g.ide2 + 2)) {
     F2(dmsf, j, i) = d_one / (F2(msfd, j, i) * F2(msfd, j, i) * c->dx16);
     F2(xmsf, j, i) = d_one / (F2(msfx, j, i) * F2(msfx, j, i) * c->dx4);
   }
