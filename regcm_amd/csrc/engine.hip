@@ -1132,6 +1132,7 @@ struct rcmdyn_engine {
     });
     // splitf, Main/mod_split.F90:243-461
     if (!fused) xch({{FK::PSA, 1}, {FK::A1U, kz, 1, 2}, {FK::A1V, kz, 1, 2}, {FK::A2U, kz, 1, 2}, {FK::A2V, kz, 1, 2}});
+    const bool wide = fused && ntiles > 1;     // k_split_project also fills the wide frames
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
@@ -1140,17 +1141,12 @@ struct rcmdyn_engine {
       const int nxp = (g.jdx2() - g.jde1 + 64) / 64, nproj = nxp * (g.idx2() - g.ide1 + 1);
       KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
-                         t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q);
+                         t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q, t.gw, wide ? t.wdeld : nullptr,
+                         t.wdelh, t.wpsdota, t.wpsa);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
-    if (fused && ntiles > 1) {
+    if (wide) {
       // one depth-SPX exchange of every split-step input instead of three per sub-step
-      each([&](Tile& t) {
-        copy_wide(t, t.deld, t.wdeld, 3 * ns);
-        copy_wide(t, t.delh, t.wdelh, 3 * ns);
-        copy_wide(t, t.psa_[t.cur], t.wpsa, 1);
-        copy_wide(t, t.psdota, t.wpsdota, 1);
-      });
       xch_wide({{&Tile::wdeld, 3 * ns}, {&Tile::wdelh, 3 * ns}, {&Tile::wpsa, 1}, {&Tile::wpsdota, 1}}, SPX);
     }
     if (fused) {

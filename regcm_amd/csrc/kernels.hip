@@ -1021,7 +1021,8 @@ __global__ __launch_bounds__(512) void k_split_project(
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
     const double* __restrict__ msfd, const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
-    double* delh, double* psdota, int nxp, int nproj, QFix qf) {
+    double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw, double* wdeld, double* wdelh,
+    double* wpsdota, double* wpsa) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   const int b = blockIdx.x;
   if (b >= nproj) {
@@ -1066,6 +1067,13 @@ __global__ __launch_bounds__(512) void k_split_project(
   const long q = g.ix(j, i);
   const double rdx2 = d_one / c->dx2;
   const int ns = c->nsplit;
+  // decomposed domain: the split step's inputs also go to the wide frame its exchange fills
+  const long qw = wdeld ? gw.ix(j, i) : 0;
+#define WSLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * gw.plane)
+  if (wdeld && ty == 0) {
+    wpsa[qw] = F2(psa, j, i);
+    wpsdota[qw] = F2(psdota, j, i);
+  }
   for (int w = ty; w < 2 * ns; w += 8) {
     const int l = w % ns + 1;
     if (w < ns) {
@@ -1082,6 +1090,7 @@ __global__ __launch_bounds__(512) void k_split_project(
       SLOT(deld, l, 1)[q] = ds - d2;
       SLOT(deld, l, 2)[q] = d2;
       SLOT(deld, l, 3)[q] = d3 - ds;
+      if (wdeld) { WSLOT(wdeld, l, 1)[qw] = ds - d2; WSLOT(wdeld, l, 2)[qw] = d2; WSLOT(wdeld, l, 3)[qw] = d3 - ds; }
       dstor[(long)(l - 1) * g.plane + q] = d2;
     } else {
       const double hs = hstor[(long)(l - 1) * g.plane + q];
@@ -1099,9 +1108,11 @@ __global__ __launch_bounds__(512) void k_split_project(
       SLOT(delh, l, 1)[q] = hs - h2;
       SLOT(delh, l, 2)[q] = h2;
       SLOT(delh, l, 3)[q] = h3 - hs;
+      if (wdeld) { WSLOT(wdelh, l, 1)[qw] = hs - h2; WSLOT(wdelh, l, 2)[qw] = h2; WSLOT(wdelh, l, 3)[qw] = h3 - hs; }
       hstor[(long)(l - 1) * g.plane + q] = h2;
     }
   }
+#undef WSLOT
 }
 
 // spstep init, Main/mod_split.F90:475-492

@@ -70,7 +70,8 @@ __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const doub
                                 const double* __restrict__ a2t, const double* __restrict__ psa,
                                 const double* __restrict__ psb, const double* __restrict__ msfd,
                                 const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
-                                double* delh, double* psdota, int nxp, int nproj, QFix qf);
+                                double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw,
+                                double* wdeld, double* wdelh, double* wpsdota, double* wpsa);
 __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
