@@ -380,9 +380,9 @@ struct rcmdyn_engine {
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     // column blocks of k_columns (one noise partial each)
-    // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
-    t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
-    t.nred = t.ncolx * (g.idx2() - g.idx1() + 1);
+    // k_columns blocks: 64 columns x one row, over the tile and a 3-deep ring
+    t.ncolx = (g.jde2 - g.jde1 + 6 + 64) / 64;
+    t.nred = t.ncolx * (g.ide2 - g.ide1 + 7);
     t.red_off = red_total;
     red_total += t.nred;
     if (cfg.idynamic == 2) setup_nh(t);
@@ -1073,9 +1073,7 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const int c = t.cur;
       KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
-              stream, g, ds, t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
-              t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0, t.qbt,
-              t.pb0, t.pbt, slices(t), slen, 0);
+              stream, g, ds, bdy_args(t, 0));
       const int nperim = 2 * (g.ici2 - g.ici1 + 1) + 2 * (g.jce2 - g.jce1 + 1);
       KLAUNCH(k_nh_bdyval, dim3((nperim + 63) / 64, kz + 1), dim3(64), 0, stream, g, kz, ds, nhfields(t));
       KLAUNCH(k_nh_bdyval_w1, dim3(1), dim3(256), 0, stream, g, nhfields(t));
@@ -1104,12 +1102,8 @@ struct rcmdyn_engine {
          {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
          {FK::A2QC, kz, 3}});
     ghosts_stale = false;
-    // surface_pressures + 2-D reciprocals, :815-834
-    each([&](Tile& t) {
-      KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
-    });
-    // compute_omega columns, new_pressure, geopotential (calc_coeff is formed where it is
-    // read, in k_momentum and k_scalars)
+    // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
+    // geopotential (calc_coeff is formed where it is read, in k_momentum and k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
       KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);
@@ -1207,29 +1201,34 @@ struct rcmdyn_engine {
     });
   }
 
+  BdyArgs bdy_args(Tile& t, int set_ps) {
+    const int c = t.cur;
+    BdyArgs a{};
+    a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a1t = t.a1t[c]; a.a1qv = t.a1qv[c]; a.a1qc = t.a1qc[c];
+    a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[c]; a.a2qv = t.a2qv[c]; a.a2qc = t.a2qc[c];
+    a.psa = t.psa_[c]; a.psb = t.psb_[c];
+    a.ub0 = t.ub0; a.ubt = t.ubt; a.vb0 = t.vb0; a.vbt = t.vbt; a.tb0 = t.tb0; a.tbt = t.tbt;
+    a.qb0 = t.qb0; a.qbt = t.qbt; a.pb0 = t.pb0; a.pbt = t.pbt;
+    for (int q = 0; q < 16; q++) a.sl.s[q] = t.sl[q];
+    a.slen = slen;
+    a.set_ps = set_ps;
+    return a;
+  }
+
   void bdyval() {
     if (cfg.idynamic == 2) { nh_bdyval(); return; }
     const int kz = cfg.kz;
-    auto slices = [&](Tile& t) {
-      Slices sl;
-      for (int s = 0; s < 16; s++) sl.s[s] = t.sl[s];
-      return sl;
-    };
     each([&](Tile& t) {
       const Geom& g = t.g;
-      const int c = t.cur;
       KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
-              stream, g, ds,
-                         t.a1u[c], t.a1v[c], t.a1t[c], t.a1qv[c], t.a1qc[c], t.a2u[c], t.a2v[c], t.a2t[c],
-                         t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.ub0, t.ubt, t.vb0, t.vbt, t.tb0, t.tbt, t.qb0,
-                         t.qbt, t.pb0, t.pbt, slices(t), slen, (int)(cfg.idynamic == 1));
+              stream, g, ds, bdy_args(t, 1));
     });
     // the ghost-ring step wrote the slice entries past the tile itself (k_bdyval_set)
     if (ghosts_stale || !split_fused()) xch_slices();
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
-              t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], slices(t), slen, ds, cfg.dtsec,
+              t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec,
               (int)(q + 1 == tiles.size()));
     }
     hs.xbctime = hs.xbctime + cfg.dtsec;

@@ -29,9 +29,7 @@ namespace rcm {
 // (rpsda, :868-875) and mkslice (1/psdotb, 1/psb, Main/mod_slice.F90:163-183), on the owned
 // points and the ghost rings the consumers read: depth 2 for the atm1-derived ones and 3 for
 // the atm2-derived ones (the stencils of the ghost-ring kernels), inside the global domain.
-__global__ void k_surface_pressures(Geom g, Fields f) {
-  THREAD_POINT(g.j0, g.i0);
-  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+__device__ __forceinline__ void surface_pressures_at(const Geom& g, const Fields& f, int j, int i) {
   auto ring = [&](int d, int jhi, int ihi) {
     return in(j, max(1, g.jde1 - d), min(jhi, g.jde2 + d)) && in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
   };
@@ -47,6 +45,11 @@ __global__ void k_surface_pressures(Geom g, Fields f) {
     F2(f.psdotb, j, i) = v;
     F2(f.rpsdb, j, i) = d_one / v;
   }
+}
+__global__ void k_surface_pressures(Geom g, Fields f) {
+  THREAD_POINT(g.j0, g.i0);
+  if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
+  surface_pressures_at(g, f, j, i);
 }
 
 // generic relaxation contribution (nudge*, Main/mod_bdycod.F90:4262-4263)
@@ -76,11 +79,13 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
   const int bb = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
-  // columns of the tile plus its ghost ring toward neighbours: the ghost columns compute
-  // exactly what their owners do (qdot, phi, pten and the new p* there replace the
-  // reference's exchanges of them)
-  const int j = g.jdx1() + (bb % nxb) * 64 + tx, i = g.idx1() + bb / nxb;
-  const bool valid = j <= g.jdx2();
+  // Blocks cover the tile and a 3-deep ring.  Columns of the tile plus its ghost ring toward
+  // neighbours run the column work: the ghost columns compute exactly what their owners do
+  // (qdot, phi, pten and the new p* there replace the reference's exchanges of them).  Every
+  // point of the 3-deep ring first forms the 2-D reciprocals of surface_pressures (K1).
+  const int j = g.jde1 - 3 + (bb % nxb) * 64 + tx, i = g.ide1 - 3 + bb / nxb;
+  if (ty == 0 && j <= g.jde2 + 3) surface_pressures_at(g, f, j, i);
+  const bool valid = in(j, g.jdx1(), g.jdx2()) && in(i, g.idx1(), g.idx2());
   const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const bool ce = valid && in(j, g.jcx1(), g.jcx2()) && in(i, g.icx1(), g.icx2());
   const bool ci = ce && g.gci(j, i);
@@ -98,8 +103,8 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     const double dummy = d_one / (c->dx2 * mx * mx);
     const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
     const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
-    rp = LD(f.rpsa, o2);
     const double psk = LD(f.psa, o2);
+    rp = d_one / psk;                                   // = rpsa (surface_pressures_at)
     for (int k = ty + 1; k <= kz; k += 8) {
       const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
       const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
@@ -976,7 +981,7 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
 }
 
 // serial sweep of one flagged (n,k) plane by one wavefront (see K6)
-__device__ void negfix_serial_plane(const Geom& g, const Consts* c, const QFix& q, int plane_id) {
+__device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFix q, int plane_id) {
   if (!q.depplane[plane_id]) return;
   const int kz = c->kz;
   const int n = plane_id / kz, k = plane_id % kz + 1;
@@ -1409,14 +1414,8 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
 // 12 sve 13 svi 14 nve 15 nvi (by j).
 
 
-__global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1u, double* a1v, double* a1t,
-                             double* a1qv, double* a1qc, double* a2u, double* a2v, double* a2t, double* a2qv,
-                             double* a2qc, double* psa, double* psb, const double* __restrict__ ub0,
-                             const double* __restrict__ ubt, const double* __restrict__ vb0,
-                             const double* __restrict__ vbt, const double* __restrict__ tb0,
-                             const double* __restrict__ tbt, const double* __restrict__ qb0,
-                             const double* __restrict__ qbt, const double* __restrict__ pb0,
-                             const double* __restrict__ pbt, Slices sl, long slen, int set_ps) {
+__device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyArgs a, int line, int x,
+                                             int k) {
   // set_ps = 0 for the non-hydrostatic core, whose p* is the constant reference p*
   // (Main/mod_bdycod.F90:1150-1165, 1430-1451 are hydrostatic-only).
   // thread -> one point of the boundary lines: blockIdx.y 0..2 = rows i = ide1 (bottom),
@@ -1425,8 +1424,13 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
   // One point past the tile along each line (toward a neighbour) only writes the bdyuv slice
   // entry there, from the ghost-ring u, v and the boundary data: k_bdyval_qc reads it (the
   // reference exchanges the slices instead, exchange_bdy_lr/bt).
-  const int line = blockIdx.y, k = (int)blockIdx.z + 1;
-  const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  double *a1u = a.a1u, *a1v = a.a1v, *a1t = a.a1t, *a1qv = a.a1qv, *a1qc = a.a1qc;
+  double *a2u = a.a2u, *a2v = a.a2v, *a2t = a.a2t, *a2qv = a.a2qv, *a2qc = a.a2qc, *psa = a.psa, *psb = a.psb;
+  const double *ub0 = a.ub0, *ubt = a.ubt, *vb0 = a.vb0, *vbt = a.vbt, *tb0 = a.tb0, *tbt = a.tbt;
+  const double *qb0 = a.qb0, *qbt = a.qbt, *pb0 = a.pb0, *pbt = a.pbt;
+  const Slices sl = a.sl;
+  const long slen = a.slen;
+  const int set_ps = a.set_ps;
   int j, i;
   bool ghost = false;
   if (line < 3) {
@@ -1445,8 +1449,6 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
   }
   const long q = g.ix(j, i);
   const long p = (long)(k - 1) * g.plane + q;
-  const double xt = s->xbctime + s->dt;
-  const bool integ = s->lcount > 0;
   // dot-point boundary rows: left/right on idi, bottom/top on the whole jde range
   const bool dL = g.bl && j == g.jde1 && in(i, g.idi1, g.idi2);
   const bool dR = g.br && j == g.jde2 && in(i, g.idi1, g.idi2);
@@ -1513,44 +1515,49 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1
 #undef VB
 }
 
+
+__global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a) {
+  const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  bdyval_point(g, s->xbctime + s->dt, s->lcount > 0, a, (int)blockIdx.y, x, (int)blockIdx.z + 1);
+}
+
 // qc inflow/outflow (present_qc = .false., bdyflow), Main/mod_bdycod.F90:2153-2220, one
 // block per level: west/east first (they read qc(jci1|jci2, ice1|ice2) before south/north
 // rewrite it), then south/north.  The last tile's launch also advances the boundary clock
 // xbctime += dtsec (Main/mod_bdycod.F90:2566): nothing here reads it.
-__global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa,
-                            Slices sl, long slen, StepState* s, double dtsec, int advance) {
-  const int k = (int)blockIdx.x + 1;
-  if (advance && k == 1 && threadIdx.x == 0) s->xbctime = s->xbctime + dtsec;
+template <class PS>
+__device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1qc, double* a1qv, PS ps, const Slices& sl,
+                                long slen, int k) {
   if (do_qv) {
     // qv inflow/outflow for iboudy = 3 or 4, Main/mod_bdycod.F90:1809-1950: west/east on ici,
     // then south/north on jce (reading the west/east results at the corners)
     for (int i = g.ici1 + (int)threadIdx.x; i <= g.ici2; i += (int)blockDim.x) {
       if (g.bl) {
-        const double qext = F3(a1qv, g.jce1, i, k) / F2(psa, g.jce1, i);
-        const double qint = F3(a1qv, g.jci1, i, k) / F2(psa, g.jci1, i);
+        const double qext = F3(a1qv, g.jce1, i, k) / ps(g.jce1, i);
+        const double qint = F3(a1qv, g.jci1, i, k) / ps(g.jci1, i);
         const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
-        F3(a1qv, g.jce1, i, k) = (w > d_zero) ? qext * F2(psa, g.jce1, i) : qint * F2(psa, g.jce1, i);
+        F3(a1qv, g.jce1, i, k) = (w > d_zero) ? qext * ps(g.jce1, i) : qint * ps(g.jce1, i);
       }
       if (g.br) {
-        const double qext = F3(a1qv, g.jce2, i, k) / F2(psa, g.jce2, i);
-        const double qint = F3(a1qv, g.jci2, i, k) / F2(psa, g.jci2, i);
+        const double qext = F3(a1qv, g.jce2, i, k) / ps(g.jce2, i);
+        const double qint = F3(a1qv, g.jci2, i, k) / ps(g.jci2, i);
         const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
-        F3(a1qv, g.jce2, i, k) = (w < d_zero) ? qext * F2(psa, g.jce2, i) : qint * F2(psa, g.jce2, i);
+        F3(a1qv, g.jce2, i, k) = (w < d_zero) ? qext * ps(g.jce2, i) : qint * ps(g.jce2, i);
       }
     }
     __syncthreads();
     for (int j = g.jce1 + (int)threadIdx.x; j <= g.jce2; j += (int)blockDim.x) {
       if (g.bb) {
-        const double qext = F3(a1qv, j, g.ice1, k) / F2(psa, j, g.ice1);
-        const double qint = F3(a1qv, j, g.ici1, k) / F2(psa, j, g.ici1);
+        const double qext = F3(a1qv, j, g.ice1, k) / ps(j, g.ice1);
+        const double qint = F3(a1qv, j, g.ici1, k) / ps(j, g.ici1);
         const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
-        F3(a1qv, j, g.ice1, k) = (w > d_zero) ? qext * F2(psa, j, g.ice1) : qint * F2(psa, j, g.ice1);
+        F3(a1qv, j, g.ice1, k) = (w > d_zero) ? qext * ps(j, g.ice1) : qint * ps(j, g.ice1);
       }
       if (g.bt) {
-        const double qext = F3(a1qv, j, g.ice2, k) / F2(psa, j, g.ice2);
-        const double qint = F3(a1qv, j, g.ici2, k) / F2(psa, j, g.ici2);
+        const double qext = F3(a1qv, j, g.ice2, k) / ps(j, g.ice2);
+        const double qint = F3(a1qv, j, g.ici2, k) / ps(j, g.ici2);
         const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
-        F3(a1qv, j, g.ice2, k) = (w < d_zero) ? qext * F2(psa, j, g.ice2) : qint * F2(psa, j, g.ice2);
+        F3(a1qv, j, g.ice2, k) = (w < d_zero) ? qext * ps(j, g.ice2) : qint * ps(j, g.ice2);
       }
     }
     __syncthreads();
@@ -1558,29 +1565,37 @@ __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* 
   if (!do_qc) return;
   for (int i = g.ice1 + (int)threadIdx.x; i <= g.ice2; i += (int)blockDim.x) {
     if (g.bl) {
-      const double qxint = F3(a1qc, g.jci1, i, k) / F2(psa, g.jci1, i);
+      const double qxint = F3(a1qc, g.jci1, i, k) / ps(g.jci1, i);
       const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
-      F3(a1qc, g.jce1, i, k) = (w > d_zero) ? d_zero : qxint * F2(psa, g.jce1, i);
+      F3(a1qc, g.jce1, i, k) = (w > d_zero) ? d_zero : qxint * ps(g.jce1, i);
     }
     if (g.br) {
-      const double qxint = F3(a1qc, g.jci2, i, k) / F2(psa, g.jci2, i);
+      const double qxint = F3(a1qc, g.jci2, i, k) / ps(g.jci2, i);
       const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
-      F3(a1qc, g.jce2, i, k) = (w < d_zero) ? d_zero : qxint * F2(psa, g.jce2, i);
+      F3(a1qc, g.jce2, i, k) = (w < d_zero) ? d_zero : qxint * ps(g.jce2, i);
     }
   }
   __syncthreads();
   for (int j = g.jci1 + (int)threadIdx.x; j <= g.jci2; j += (int)blockDim.x) {
     if (g.bb) {
-      const double qxint = F3(a1qc, j, g.ici1, k) / F2(psa, j, g.ici1);
+      const double qxint = F3(a1qc, j, g.ici1, k) / ps(j, g.ici1);
       const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
-      F3(a1qc, j, g.ice1, k) = (w > d_zero) ? d_zero : qxint * F2(psa, j, g.ice1);
+      F3(a1qc, j, g.ice1, k) = (w > d_zero) ? d_zero : qxint * ps(j, g.ice1);
     }
     if (g.bt) {
-      const double qxint = F3(a1qc, j, g.ici2, k) / F2(psa, j, g.ici2);
+      const double qxint = F3(a1qc, j, g.ici2, k) / ps(j, g.ici2);
       const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
-      F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * F2(psa, j, g.ice2);
+      F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * ps(j, g.ice2);
     }
   }
+}
+
+
+__global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa,
+                            Slices sl, long slen, StepState* s, double dtsec, int advance) {
+  const int k = (int)blockIdx.x + 1;
+  if (advance && k == 1 && threadIdx.x == 0) s->xbctime = s->xbctime + dtsec;
+  bdyval_qc_level(g, do_qc, do_qv, a1qc, a1qv, [&](int j, int i) { return F2(psa, j, i); }, sl, slen, k);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -77,7 +77,15 @@ __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int s
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_fused(Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
 __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total);
-__global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, double* a1u, double* a1v, double* a1t, double* a1qv, double* a1qc, double* a2u, double* a2v, double* a2t, double* a2qv, double* a2qc, double* psa, double* psb, const double* __restrict__ ub0, const double* __restrict__ ubt, const double* __restrict__ vb0, const double* __restrict__ vbt, const double* __restrict__ tb0, const double* __restrict__ tbt, const double* __restrict__ qb0, const double* __restrict__ qbt, const double* __restrict__ pb0, const double* __restrict__ pbt, Slices sl, long slen, int set_ps);
+// pointers of bdyval (k_bdyval_set)
+struct BdyArgs {
+  double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc, *psa, *psb;
+  const double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
+  Slices sl;
+  long slen;
+  int set_ps;
+};
+__global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a);
 __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance);
 __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu_hgtf, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ ht, double* xmsf, double* dmsf, double* hgfact, double* mapf);
 __global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack);

@@ -175,7 +175,7 @@ def test_kernel_times_hook(c1_data):
     for name in STATE_FIELDS:
         assert np.array_equal(e1.get(name), e2.get(name)), name
     for k in ("k_momentum", "k_scalars", "k_columns", "k_qfilter", "k_split_project",
-              "k_spstep_fused", "k_split_correct", "k_bdyval_set"):
+              "k_spstep_fused", "k_split_correct", "k_bdyval_set", "k_bdyval_qc"):
         assert k in kt and kt[k][0] == 3 and kt[k][1] > 0.0, k
 
 
