@@ -29,6 +29,34 @@ __device__ __forceinline__ double dmin(double a, double b) { return (a < b) ? a 
 
 __device__ __forceinline__ bool in(int v, int lo, int hi) { return v >= lo && v <= hi; }
 
+// Block phase timing (build with -DRCM_PHASE_TIMING): thread 0 of every block records
+// wall-clock marks (100 MHz) into a device buffer that rcm_phase_dump() (kernels.hip) writes
+// to a file; the measurement behind the kernel structure notes in DESIGN.md.
+#ifdef RCM_PHASE_TIMING
+struct PtRec { int kid, bx, by, bz, n, pad; long long t[8]; };
+constexpr int PT_CAP = 1 << 17;
+static __device__ PtRec rcm_pt_buf[PT_CAP];
+static __device__ int rcm_pt_count = 0;
+#define PT_DECL long long pt_[8]; int pt_n_ = 0; pt_[pt_n_++] = wall_clock64();
+#define PT_MARK() do { if (pt_n_ < 7) pt_[pt_n_++] = wall_clock64(); } while (0)
+#define PT_PRINT(KID_)                                                                          \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && threadIdx.y == 0) {                                                 \
+      pt_[pt_n_++] = wall_clock64();                                                            \
+      const int q_ = atomicAdd(&rcm_pt_count, 1);                                               \
+      if (q_ < PT_CAP) {                                                                        \
+        PtRec& r_ = rcm_pt_buf[q_];                                                             \
+        r_.kid = KID_; r_.bx = blockIdx.x; r_.by = blockIdx.y; r_.bz = blockIdx.z; r_.n = pt_n_;  \
+        for (int e_ = 0; e_ < pt_n_; e_++) r_.t[e_] = pt_[e_];                                  \
+      }                                                                                         \
+    }                                                                                           \
+  } while (0)
+#else
+#define PT_DECL
+#define PT_MARK() do { } while (0)
+#define PT_PRINT(KID_) do { } while (0)
+#endif
+
 // thread -> (j, i, k) over a box starting at (j1, i1); k = blockIdx.z + 1
 #define THREAD_POINT(j1, i1)                                   \
   const int j = (j1) + (int)(blockIdx.x * blockDim.x + threadIdx.x); \

@@ -380,9 +380,9 @@ struct rcmdyn_engine {
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     // column blocks of k_columns (one noise partial each)
-    // k_columns blocks: 64 columns x one row, over the tile and a 3-deep ring
-    t.ncolx = (g.jde2 - g.jde1 + 6 + 64) / 64;
-    t.nred = t.ncolx * (g.ide2 - g.ide1 + 7);
+    // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
+    t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
+    t.nred = t.ncolx * (g.idx2() - g.idx1() + 1);
     t.red_off = red_total;
     red_total += t.nred;
     if (cfg.idynamic == 2) setup_nh(t);
@@ -1102,8 +1102,12 @@ struct rcmdyn_engine {
          {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
          {FK::A2QC, kz, 3}});
     ghosts_stale = false;
-    // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
-    // geopotential (calc_coeff is formed where it is read, in k_momentum and k_scalars)
+    // surface_pressures + 2-D reciprocals, :815-834
+    each([&](Tile& t) {
+      KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
+    });
+    // compute_omega columns, new_pressure, geopotential (calc_coeff is formed where it is
+    // read, in k_momentum and k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
       KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);

@@ -20,12 +20,26 @@
 
 namespace rcm {
 
+// The device reads the polynomial coefficients from constant memory: scalar loads into SGPRs,
+// where the compiler would otherwise materialise each 64-bit literal in a VGPR pair, hoist it
+// out of the kernel's level loops and spill it (k_columns).
+#if defined(__HIP_DEVICE_COMPILE__)
+static __constant__ double rcm_fm_c[16] = {
+    6.666666666666735130e-01, 3.999999999940941908e-01, 2.857142874366239149e-01, 2.222219843214978396e-01,
+    1.818357216161805012e-01, 1.531383769920937332e-01, 1.479819860511658591e-01, 1.66666666666666019037e-01,
+    -2.77777777770155933842e-03, 6.61375632143793436117e-05, -1.65339022054652515390e-06,
+    4.13813679705723846039e-08, 0.0, 0.0, 0.0, 0.0};
+#define RCM_FMC(i, v) rcm_fm_c[i]
+#else
+#define RCM_FMC(i, v) (v)
+#endif
+
 RCM_HD double rcm_log(double x) {
   constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-  constexpr double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01;
-  constexpr double Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01;
-  constexpr double Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01;
-  constexpr double Lg7 = 1.479819860511658591e-01;
+  const double Lg1 = RCM_FMC(0, 6.666666666666735130e-01), Lg2 = RCM_FMC(1, 3.999999999940941908e-01);
+  const double Lg3 = RCM_FMC(2, 2.857142874366239149e-01), Lg4 = RCM_FMC(3, 2.222219843214978396e-01);
+  const double Lg5 = RCM_FMC(4, 1.818357216161805012e-01), Lg6 = RCM_FMC(5, 1.531383769920937332e-01);
+  const double Lg7 = RCM_FMC(6, 1.479819860511658591e-01);
   int e;
   double m = std::frexp(x, &e);                 // x = m * 2^e, m in [0.5, 1)
   if (m < 0.70710678118654752440) { m = m + m; e = e - 1; }   // m in [sqrt(1/2), sqrt(2))
@@ -43,9 +57,9 @@ RCM_HD double rcm_log(double x) {
 RCM_HD double rcm_exp(double x) {
   constexpr double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
   constexpr double invln2 = 1.44269504088896338700e+00;
-  constexpr double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03;
-  constexpr double P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06;
-  constexpr double P5 = 4.13813679705723846039e-08;
+  const double P1 = RCM_FMC(7, 1.66666666666666019037e-01), P2 = RCM_FMC(8, -2.77777777770155933842e-03);
+  const double P3 = RCM_FMC(9, 6.61375632143793436117e-05), P4 = RCM_FMC(10, -1.65339022054652515390e-06);
+  const double P5 = RCM_FMC(11, 4.13813679705723846039e-08);
   const double k = std::rint(x * invln2);      // x = k ln2 + r, |r| <= ln2/2
   const double hi = x - k * ln2HI;             // k * ln2HI exact for |k| < 2^11
   const double lo = k * ln2LO;

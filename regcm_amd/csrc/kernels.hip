@@ -19,6 +19,9 @@
 // Column recurrences (pten/qdot, phi, split projections) use one thread per (j,i) column.
 #include "engine.hpp"
 #include "kernels.hpp"
+
+#include <cstdio>
+#include <vector>
 #include "fastmath.hpp"
 #include "devcommon.hpp"
 
@@ -72,20 +75,19 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  terms (mass divergence, td, tvfac, the log ratios of the hypsometric equation) into LDS,
 //  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
 //  geopotential recurrence, each in the reference's sequential order.
-__global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+__global__ __launch_bounds__(512, 6) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxb) {
   extern __shared__ double lds[];                        // 4 x kz x 64
+  PT_DECL
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
-  // Blocks cover the tile and a 3-deep ring.  Columns of the tile plus its ghost ring toward
-  // neighbours run the column work: the ghost columns compute exactly what their owners do
-  // (qdot, phi, pten and the new p* there replace the reference's exchanges of them).  Every
-  // point of the 3-deep ring first forms the 2-D reciprocals of surface_pressures (K1).
-  const int j = g.jde1 - 3 + (bb % nxb) * 64 + tx, i = g.ide1 - 3 + bb / nxb;
-  if (ty == 0 && j <= g.jde2 + 3) surface_pressures_at(g, f, j, i);
-  const bool valid = in(j, g.jdx1(), g.jdx2()) && in(i, g.idx1(), g.idx2());
+  // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
+  // columns compute exactly what their owners do (qdot, phi, pten and the new p* there replace
+  // the reference's exchanges of them).
+  const int j = g.jdx1() + (bb % nxb) * 64 + tx, i = g.idx1() + bb / nxb;
+  const bool valid = j <= g.jdx2();
   const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const bool ce = valid && in(j, g.jcx1(), g.jcx2()) && in(i, g.icx1(), g.icx2());
   const bool ci = ce && g.gci(j, i);
@@ -104,26 +106,43 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
     const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
     const double psk = LD(f.psa, o2);
-    rp = d_one / psk;                                   // = rpsa (surface_pressures_at)
-    for (int k = ty + 1; k <= kz; k += 8) {
-      const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
-      const double a = LD(f.a1u, O3(1, 1)) * m11 + LD(f.a1u, O3(1, 0)) * m10 - LD(f.a1u, O3(0, 1)) * m01 -
-                       LD(f.a1u, o3) * m00;
-      const double bq = LD(f.a1v, O3(1, 1)) * m11 + LD(f.a1v, O3(0, 1)) * m01 - LD(f.a1v, O3(1, 0)) * m10 -
-                        LD(f.a1v, o3) * m00;
+    rp = LD(f.rpsa, o2);
+    // two levels per thread and pass: every load of the pass is issued before any use
+    constexpr int KU = 2;
+    for (int k0 = ty + 1; k0 <= kz; k0 += 8 * KU) {
+      double u00[KU], u10[KU], u01[KU], u11[KU], v00[KU], v10[KU], v01[KU], v11[KU], tt[KU], qq[KU], cc[KU];
+#pragma unroll
+      for (int n = 0; n < KU; n++) {
+        const int kk = k0 + 8 * n;
+        const uint32_t o3 = o2 + (uint32_t)((kk <= kz ? kk : kz) - 1) * L8;
+        u00[n] = LD(f.a1u, o3); u10[n] = LD(f.a1u, O3(1, 0)); u01[n] = LD(f.a1u, O3(0, 1)); u11[n] = LD(f.a1u, O3(1, 1));
+        v00[n] = LD(f.a1v, o3); v10[n] = LD(f.a1v, O3(1, 0)); v01[n] = LD(f.a1v, O3(0, 1)); v11[n] = LD(f.a1v, O3(1, 1));
+        tt[n] = LD(f.a1t, o3); qq[n] = LD(f.a1qv, o3); cc[n] = LD(f.a1qc, o3);
+      }
+#pragma unroll
+      for (int n = 0; n < KU; n++) {
+      const int k = k0 + 8 * n;
+      if (k > kz) break;
+      const double a = u11[n] * m11 + u10[n] * m10 - u01[n] * m01 - u00[n] * m00;
+      const double bq = v11[n] * m11 + v01[n] * m01 - v10[n] * m10 - v00[n] * m00;
       sMD[(k - 1) * 64 + tx] = (a + bq) * dummy;
-      const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
-      const double qc = dmax(LD(f.a1qc, o3) * rp, d_zero);
-      double tdk = LD(f.a1t, o3) * (d_one + ep1 * qv);
+      const double qv = dmax(qq[n] * rp, MINQQ);
+      const double qc = dmax(cc[n] * rp, d_zero);
+      double tdk = tt[n] * (d_one + ep1 * qv);
       // ipgf = 1: minus the reference-atmosphere temperature (ttld, :1893-1964)
-      if (c->ipgf == 1) tdk = tdk - psk * T00PG * pow((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
+      if (c->ipgf == 1) tdk = tdk - psk * T00PG * rcm_powpos((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
       sTD[(k - 1) * 64 + tx] = tdk;
       sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
+      }
+    }
+    // the hypsometric log ratios in a loop of their own (no loads in flight there: the log's
+    // polynomial constants stay in registers without spilling)
+    for (int k = ty + 1; k <= kz; k += 8)
       sLG[(k - 1) * 64 + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
                                         : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
-    }
   }
   __syncthreads();
+  PT_MARK();
   double na = 0.0, nb = 0.0;
   if (valid && ty == 0) {
     double pt = d_zero;
@@ -171,7 +190,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     double tdk1 = sTD[(kz - 1) * 64 + tx];
     const double tv = tdk1 * rp * sTV[(kz - 1) * 64 + tx];
     double top = LD(f.ht, o2);
-    if (c->ipgf == 1) top = top + rgas * T00PG / c->pgfaa1 * pow((ps + ptop) / P00PG, c->pgfaa1);  // :2045
+    if (c->ipgf == 1) top = top + rgas * T00PG / c->pgfaa1 * rcm_powpos((ps + ptop) / P00PG, c->pgfaa1);  // :2045
     double ph = top - rgas * tv * sLG[(kz - 1) * 64 + tx];
     ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
     for (int lev = kz - 1; lev >= 1; lev--) {
@@ -183,6 +202,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
       tdk1 = tdl;
     }
   }
+  PT_MARK();
   // per-block partial of the noise sums (fixed tree); k_split_correct sums the partials
   __shared__ double sa[512], sb[512];
   const int t = threadIdx.x;
@@ -196,6 +216,7 @@ __global__ __launch_bounds__(512) void k_columns(Geom g, const Consts* __restric
     f.red[2 * (f.red_off + bb)] = sa[0];
     f.red[2 * (f.red_off + bb) + 1] = sb[0];
   }
+  PT_PRINT(1);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -252,6 +273,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
 #define sVB sX.b.VB
   __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
   const int tid = threadIdx.x;
+  PT_DECL
   const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -345,6 +367,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     }
   }
   __syncthreads();
+  PT_MARK();
   // calc_coeff Smagorinsky xkc (Main/mod_diffusion.F90:194-210) at the low-halo tile points from
   // the staged ubd3d/vbd3d, over the cross points of the tile and its ghost ring toward
   // neighbouring tiles (the reference's exchanged xkc there is the same computation)
@@ -366,6 +389,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     }
   }
   __syncthreads();
+  PT_MARK();
 #undef sUB
 #undef sVB
   // PGF log terms (:1996-2025): the u term is LU(j,i) - LU(j-1,i), the v term LV(j,i) - LV(j,i-1),
@@ -383,6 +407,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     }
   }
   __syncthreads();
+  PT_MARK();
   if (!valid) return;
   const double dt = s->dt;
   // tile coordinates of (j,i): halo-1 tiles (b1,a1), halo-2 (b2,a2), low-halo (b0,a0)
@@ -495,7 +520,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
   {
     double rtbar = d_rfour * (sTV[a0 - 1][b0 - 1] + sTV[a0][b0 - 1] + sTV[a0 - 1][b0] + sTV[a0][b0]);
     if (c->ipgf == 1)                       // reference-atmosphere temperature, :1945-1946
-      rtbar = rtbar - T00PG * pow((c->hsigma[k] * pdota + c->ptop) / P00PG, c->pgfaa1);
+      rtbar = rtbar - T00PG * rcm_powpos((c->hsigma[k] * pdota + c->ptop) / P00PG, c->pgfaa1);
     rtbar = c->rgas * rtbar * pdota;
     const double den = c->dx * mfd;
     ut = ut - rtbar * (sX.l.LU[ti][tj + 1] - sX.l.LU[ti][tj]) / den;
@@ -519,6 +544,7 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
   d = g1 * (cv + v2 - d_two * v1c);
   ST(f.b2v, o3, v1c + d);
   ST(f.b1v, o3, cv);
+  PT_PRINT(2);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -533,9 +559,6 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
 // products formed once per staged point: umc/vmc/ud/vd at the dot points (j..j+1, i..i+1),
 // p*, t, qv, qc (atm1 * rpsa) with halo 1 and the mkslice fields atm2 * (1/psb) with halo 2.
 // The interior ring (jce \ jci) only passes atm2 moisture to the forecast buffers.
-#ifdef RCM_PHASE_TIMING
-__device__ int rcm_phase_count = 0;
-#endif
 constexpr int SDW = SBJ + 1, SDH = SBI + 1;    // dot points j..j+SBJ, i..i+SBI
 constexpr int SW1 = SBJ + 2, SH1 = SBI + 2;    // halo 1
 constexpr int SW2 = SBJ + 4, SH2 = SBI + 4;    // halo 2
@@ -606,9 +629,7 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
   __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
   __shared__ double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
   const int tid = threadIdx.x;
-#ifdef RCM_PHASE_TIMING
-  const long long pt0 = wall_clock64();
-#endif
+  PT_DECL
   // the tile's cross points and its ghost ring (k_qfilter's moisture fix reads the forecasts
   // there); boundary branches test global indices
   const int J0 = g.jcx1() + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
@@ -698,9 +719,7 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
     }
   }
   __syncthreads();
-#ifdef RCM_PHASE_TIMING
-  const long long pt1 = wall_clock64();
-#endif
+  PT_MARK();
   if (!valid) return;
 #define DT(S, dj, di) S[ti + (di)][tj + (dj)]
   // calc_coeff Smagorinsky xkc, Main/mod_diffusion.F90:194-210 (ubd3d/vbd3d = atm2 * (1/psdotb))
@@ -843,14 +862,7 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
   ST(f.cqv, o3, qv2 + dt * tq);
   ST(f.cqc, o3, qc2 + dt * tc);
-#ifdef RCM_PHASE_TIMING
-  if (tid == 0) {
-    const long long pt2 = wall_clock64();
-    const int n = atomicAdd(&rcm_phase_count, 1);
-    if (n < 400) printf("PT k_scalars blk %d %d %d t0 %lld stage %lld compute %lld\n", (int)blockIdx.x, (int)blockIdx.y,
-                        (int)blockIdx.z, pt0, pt1 - pt0, pt2 - pt1);
-  }
-#endif
+  PT_PRINT(3);
 }
 #undef DIFFU_X
 #undef H2T
@@ -911,6 +923,7 @@ __device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, do
 #define LD2(a, o) (*(const double2*)((const char*)(a) + (uint32_t)(o)))
 #define ST2(a, o, v) (*(double2*)((char*)(a) + (uint32_t)(o)) = (v))
 __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f) {
+  PT_DECL
   const int jp = g.j0 + 2 * (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int i = g.i0 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
   const int k = (int)blockIdx.z + 1;
@@ -978,6 +991,7 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
     ST2(n ? f.b1qc : f.b1qv, o3, n1);
     ST2(n ? f.b2qc : f.b2qv, o3, n2);
   }
+  PT_PRINT(4);
 }
 
 // serial sweep of one flagged (n,k) plane by one wavefront (see K6)
@@ -1021,7 +1035,7 @@ __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFi
 // reference's order.  Blocks [nproj, nproj + 2 kz) run the serial negative-moisture sweeps
 // (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
-__global__ __launch_bounds__(512) void k_split_project(
+__global__ __launch_bounds__(512, 6) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
@@ -1034,6 +1048,7 @@ __global__ __launch_bounds__(512) void k_split_project(
     if (threadIdx.x < 64) negfix_serial_plane(g, c, qf, b - nproj);
     return;
   }
+  PT_DECL
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   // owned dot points, plus psdota on the right/top ghost ring (the split corrections of the
   // ghost-ring u, v read it there)
@@ -1068,6 +1083,7 @@ __global__ __launch_bounds__(512) void k_split_project(
     }
   }
   __syncthreads();
+  PT_MARK();
   if (!valid) return;
   const long q = g.ix(j, i);
   const double rdx2 = d_one / c->dx2;
@@ -1118,6 +1134,7 @@ __global__ __launch_bounds__(512) void k_split_project(
     }
   }
 #undef WSLOT
+  PT_PRINT(5);
 }
 
 // spstep init, Main/mod_split.F90:475-492
@@ -1656,5 +1673,24 @@ __global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restri
   if (j > g.jde2 || i > g.ide2) return;
   for (int p = 0; p < nplanes; p++) dst[p * dstride + w.ix(j, i)] = src[p * sstride + g.ix(j, i)];
 }
+
+#ifdef RCM_PHASE_TIMING
+// phase records of the launches since the last dump (see PT_DECL in devcommon.hpp)
+extern "C" int rcm_phase_dump(const char* path) {
+  int n = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(rcm_pt_count), sizeof(int)) != hipSuccess) return -1;
+  n = n < PT_CAP ? n : PT_CAP;
+  std::vector<PtRec> v(n);
+  if (n && hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(rcm_pt_buf), sizeof(PtRec) * n) != hipSuccess) return -1;
+  FILE* fp = std::fopen(path, "wb");
+  if (!fp) return -1;
+  std::fwrite(v.data(), sizeof(PtRec), n, fp);
+  std::fclose(fp);
+  const int zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(rcm_pt_count), &zero, sizeof(int)) != hipSuccess) return -1;
+  return n;
+}
+#endif
 
 }  // namespace rcm
