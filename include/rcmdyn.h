@@ -9,7 +9,9 @@
  *   call bdyval      Main/mod_regcm_interface.F90:208 rcmdyn_bdyval()
  *   tend+bdyval loop Main/mod_regcm_interface.F90:172-228   rcmdyn_step()
  *   module state     Main/mod_atm_interface.F90:39-70 rcmdyn_put()/rcmdyn_get()
- *   bdyin (b0,bt)    Main/mod_bdycod.F90:654-889      rcmdyn_set_bdy_time() + put XxB_*
+ *   bdyin (b0,bt)    Main/mod_bdycod.F90:654-889      put XxB_B0/BT + rcmdyn_set_time(xbctime)
+ *   mkslice -> physics -> sums  Main/mod_tendency.F90:243,271,285-411
+ *                    rcmdyn_tend_pre_physics() + get ATMS_* / put *PHY + rcmdyn_tend_post_physics()
  *   rcmtimer/dt/xbctime Main/mpplib/mod_runparams.F90 rcmdyn_set_time()/get_time()
  *   exchange*        Main/mpplib/mod_mppparam.F90:6065-13190  internal (local copies / RCCL)
  *   fatal('CFL VIOLATION') Main/mod_tendency.F90:702  return code + rcmdyn_last_error()
@@ -34,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RCMDYN_ABI_VERSION 2
+#define RCMDYN_ABI_VERSION 3
 #define RCMDYN_MAXKZ 64
 #define RCMDYN_MAXSPLIT 4
 
@@ -103,6 +105,9 @@ typedef struct rcmdyn_config {
    * nh_dtsmax = dx / sqrt(gamma R max(t0)) / (1 + nhxkd), nh_xmsf = mean of msfx over the
    * interior cross points (the global sumall of :143-145) */
   double nh_dtsmax, nh_xmsf;
+  /* cldparam relative-humidity clamps of the mkslice export (Main/mod_params.F90:331-332,
+   * Main/mod_slice.F90:336-337) [rhmin 0.01, rhmax 1.01] */
+  double rhmin, rhmax;
 } rcmdyn_config;
 
 /* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */
@@ -136,6 +141,22 @@ enum rcmdyn_field {
   RCMDYN_ATM0_PF, RCMDYN_ATM0_RHOF, RCMDYN_ATM0_ZF,
   RCMDYN_DPSDXM, RCMDYN_DPSDYM, RCMDYN_DPRDDX, RCMDYN_DPRDDY,
   RCMDYN_EF, RCMDYN_DDX, RCMDYN_DDY, RCMDYN_DMDX, RCMDYN_DMDY, RCMDYN_EX, RCMDYN_CRX, RCMDYN_CRY,
+  /* physics coupling (put): the pc_physic component of aten that the
+   * host's physical_parametrizations produced (coupled with p*, like aten), added in tend's
+   * sums exactly where the reference adds them (Main/mod_tendency.F90:285-314, 332-341,
+   * 404-411).  Cross points for t, qv, qc, pp, w (w on kz+1 levels), dot points for u, v.
+   * The engine holds no physics buffers until the first put of one of these; they then
+   * persist (zero until put) and enter every later tend. */
+  RCMDYN_TPHY, RCMDYN_QVPHY, RCMDYN_QCPHY, RCMDYN_UPHY, RCMDYN_VPHY, RCMDYN_PPPHY, RCMDYN_WPHY,
+  /* atms slice fields (get, read-only) of mkslice, Main/mod_slice.F90:102-358, as the
+   * physics reads them: filled by rcmdyn_tend_pre_physics from the state at the start of the
+   * step; zero outside the index ranges the reference writes.  PF3D, WB3D, ZQ: kz+1 levels;
+   * PS2D, RHOX2D: 2-D.  ZQ, ZA, DZQ only for idynamic = 1 (constant in the NH core). */
+  RCMDYN_ATMS_UBX3D, RCMDYN_ATMS_VBX3D, RCMDYN_ATMS_UBD3D, RCMDYN_ATMS_VBD3D, RCMDYN_ATMS_TB3D,
+  RCMDYN_ATMS_QVB3D, RCMDYN_ATMS_QCB3D, RCMDYN_ATMS_TV3D, RCMDYN_ATMS_PB3D, RCMDYN_ATMS_PF3D,
+  RCMDYN_ATMS_PS2D, RCMDYN_ATMS_RHOX2D, RCMDYN_ATMS_TH3D, RCMDYN_ATMS_RHOB3D, RCMDYN_ATMS_TP3D,
+  RCMDYN_ATMS_WPX3D, RCMDYN_ATMS_WB3D, RCMDYN_ATMS_ZQ, RCMDYN_ATMS_ZA, RCMDYN_ATMS_DZQ,
+  RCMDYN_ATMS_QSB3D, RCMDYN_ATMS_RHB3D,
   RCMDYN_NFIELDS
 };
 
@@ -167,6 +188,13 @@ int rcmdyn_get_time(rcmdyn_t* h, int64_t* lcount, double* dt, double* xbctime);
 
 /* The hot path. */
 int rcmdyn_tend(rcmdyn_t* h);                  /* one mod_tendency::tend */
+/* tend split at the reference's call of physical_parametrizations (Main/mod_tendency.F90:
+ * 271): pre_physics runs surface_pressures, decouple, compute_omega, mkslice (device export
+ * of the ATMS_* fields) and new_pressure; the host then runs its physics on the ATMS_*
+ * fields, puts the *PHY tendencies, and post_physics runs the rest of tend.  pre + post is
+ * bit-identical to rcmdyn_tend with the same *PHY contents. */
+int rcmdyn_tend_pre_physics(rcmdyn_t* h);
+int rcmdyn_tend_post_physics(rcmdyn_t* h);
 int rcmdyn_bdyval(rcmdyn_t* h);                /* one mod_bdycod::bdyval */
 int rcmdyn_step(rcmdyn_t* h, int32_t nsteps);  /* nsteps x (tend + bdyval), graph-replayed */
 int rcmdyn_synchronize(rcmdyn_t* h);

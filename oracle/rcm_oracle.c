@@ -119,6 +119,10 @@ struct orc {
   double tmask[13][13];                     /* tmask(nsj, nsi), nsj/nsi = -6..6 */
   int tmask_valid, nh_istep;
   double nh_cfl;
+  /* physics coupling seam: pc_physic tendencies t, qv, qc, u, v, pp, w and the atms export
+   * (rcmdyn_field TPHY.. and ATMS_UBX3D.. order) */
+  double *phy[7], *atms[22];
+  double rhmin, rhmax;
   /* diagnostics */
   double ptntot, pt2tot;
   /* exchange */
@@ -215,6 +219,13 @@ static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
         A2(ib, j, i) = jgbr2 - j + 2; A2(rg, j, i) = 4;
       }
   }
+}
+
+static int atms_levels(int q, int kz) {
+  int f = RCMDYN_ATMS_UBX3D + q;
+  if (f == RCMDYN_ATMS_PF3D || f == RCMDYN_ATMS_WB3D || f == RCMDYN_ATMS_ZQ) return kz + 1;
+  if (f == RCMDYN_ATMS_PS2D || f == RCMDYN_ATMS_RHOX2D) return 1;
+  return kz;
 }
 
 orc_t* orc_create(const rcmdyn_config* cfg) {
@@ -377,6 +388,10 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
     for (size_t q = 0; q < sizeof(sc) / sizeof(sc[0]); q++) *sc[q] = alloc3(o, kp);
     o->estore = alloc3(o, 1); o->astore = alloc3(o, 1); o->wpval = alloc3(o, 1);
   }
+  for (int q = 0; q < 5; q++) o->phy[q] = alloc3(o, kz);
+  if (o->nh) { o->phy[5] = alloc3(o, kz); o->phy[6] = alloc3(o, kp); }
+  for (int q = 0; q < 22; q++) o->atms[q] = alloc3(o, atms_levels(q, kz));
+  o->rhmin = cfg->rhmin; o->rhmax = cfg->rhmax;
   size_t sjn = (size_t)o->nj * kz, sin_ = (size_t)o->ni * kz;
   o->sue = calloc(sjn, 8); o->sui = calloc(sjn, 8); o->nue = calloc(sjn, 8); o->nui = calloc(sjn, 8);
   o->sve = calloc(sjn, 8); o->svi = calloc(sjn, 8); o->nve = calloc(sjn, 8); o->nvi = calloc(sjn, 8);
@@ -411,6 +426,8 @@ void orc_destroy(orc_t* o) {
     &o->s_pxup, &o->s_pyvp, &o->s_tk, &o->s_cc, &o->s_cdd, &o->s_cj, &o->s_pi, &o->s_ucrs, &o->s_vcrs,
     &o->estore, &o->astore, &o->wpval};
   for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
+  for (int q = 0; q < 7; q++) free(o->phy[q]);
+  for (int q = 0; q < 22; q++) free(o->atms[q]);
   for (int n = 0; n < 2; n++) {
     free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
     free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
@@ -442,6 +459,14 @@ void orc_diagnostics(const orc_t* o, double out[4]) {
 
 static double* field_ptr(orc_t* o, int f, int* nk) {
   *nk = o->kz;
+  if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY) {
+    if (f == RCMDYN_WPHY) *nk = o->kz + 1;
+    return o->phy[f - RCMDYN_TPHY];
+  }
+  if (f >= RCMDYN_ATMS_UBX3D && f <= RCMDYN_ATMS_RHB3D) {
+    *nk = atms_levels(f - RCMDYN_ATMS_UBX3D, o->kz);
+    return o->atms[f - RCMDYN_ATMS_UBX3D];
+  }
   switch (f) {
     case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
     case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
@@ -774,6 +799,118 @@ static void mkslice(orc_t* o) {
     for (int i = o->ice1; i <= o->ice2; i++)
       for (int j = o->jce1; j <= o->jce2; j++)
         A3(o->pf3d, j, i, k) = (o->sigma[k] * A2(o->psb, j, i) + o->ptop) * d_1000;
+}
+
+/* pfesat / pfwsat, Share/pfesat.inc:21-49, Share/pfwsat.inc:1-17 */
+static double pfwsat(double t, double p) {
+  double tl = t - 273.15;
+  if (tl > 100.0) tl = 100.0;
+  if (tl < -75.0) tl = -75.0;
+  double td = tl, esat;
+  if (td >= 0.0)
+    esat = 6.11213476 + td * (0.444007856 + td * (0.143064234e-01 + td * (0.264461437e-03 + td * (0.305903558e-05 +
+           td * (0.196237241e-07 + td * (0.892344772e-10 + td * (-0.373208410e-12 + td * 0.209339997e-15)))))));
+  else
+    esat = 6.11123516 + td * (0.503109514 + td * (0.188369801e-01 + td * (0.420547422e-03 + td * (0.614396778e-05 +
+           td * (0.602780717e-07 + td * (0.387940929e-09 + td * (0.149436277e-11 + td * 0.262655803e-14)))))));
+  double es = esat * 100.0;
+  return (AMW / AMD) * (es / (p - es));
+}
+
+/* The rest of mkslice (Main/mod_slice.F90:163-338) as the physics reads it: the atms export
+ * of the physics coupling seam (rcmdyn ATMS_* fields), after mkslice / nh_mkslice, on the
+ * tile's owned points of each loop's range (zero elsewhere, as the reference's zero-filled
+ * allocations). */
+enum { S_UBX, S_VBX, S_UBD, S_VBD, S_TB, S_QVB, S_QCB, S_TV, S_PB, S_PF, S_PS2D, S_RHOX, S_TH, S_RHOB,
+       S_TP, S_WPX, S_WB, S_ZQ, S_ZA, S_DZQ, S_QSB, S_RHB };
+static void slice_export(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  double** s = o->atms;
+  const double rovcp = c_rgas * (d_one / c_cpd), rovg = c_rgas / EGRAV, p00 = 1.0e5;
+  for (int q = 0; q < 22; q++) memset(s[q], 0, sizeof(double) * o->plane * atms_levels(q, kz));
+  for (int k = 1; k <= kz; k++)                                    /* :171-174 */
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(s[S_UBD], j, i, k) = A3(o->ubd, j, i, k);
+        A3(s[S_VBD], j, i, k) = A3(o->vbd, j, i, k);
+      }
+  for (int k = 1; k <= kz; k++)                                    /* :176-183 */
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(s[S_UBX], j, i, k) = d_rfour * (A3(o->ubd, j, i, k) + A3(o->ubd, j, i + 1, k) +
+                                           A3(o->ubd, j + 1, i, k) + A3(o->ubd, j + 1, i + 1, k));
+        A3(s[S_VBX], j, i, k) = d_rfour * (A3(o->vbd, j, i, k) + A3(o->vbd, j, i + 1, k) +
+                                           A3(o->vbd, j + 1, i, k) + A3(o->vbd, j + 1, i + 1, k));
+      }
+  for (int k = 1; k <= kz; k++)                                    /* :185-202 */
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        double tb = A3(o->tb3d, j, i, k), qv = A3(o->qb3d[0], j, i, k), qc = A3(o->qb3d[1], j, i, k);
+        A3(s[S_TB], j, i, k) = tb;
+        A3(s[S_QVB], j, i, k) = qv;
+        A3(s[S_QCB], j, i, k) = qc;
+        A3(s[S_TV], j, i, k) = tb * (d_one + c_ep1 * qv - qc);
+        A3(s[S_PB], j, i, k) = A3(o->pb3d, j, i, k);
+      }
+  for (int k = 1; k <= kp; k++)                                    /* :215-234 */
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A3(s[S_PF], j, i, k) = A3(o->pf3d, j, i, k);
+  for (int i = o->ice1; i <= o->ice2; i++)
+    for (int j = o->jce1; j <= o->jce2; j++)
+      A2(s[S_PS2D], j, i) = o->nh ? A2(o->ps0, j, i) + o->ptop * d_1000 + A3(o->ppb3d, j, i, kz)
+                                  : (A2(o->psb, j, i) + o->ptop) * d_1000;
+  for (int i = o->ici1; i <= o->ici2; i++)                         /* :236-238 */
+    for (int j = o->jci1; j <= o->jci2; j++)
+      A2(s[S_RHOX], j, i) = A2(s[S_PS2D], j, i) / (c_rgas * A3(o->tb3d, j, i, kz));
+  for (int k = 1; k <= kz; k++)                                    /* :240-243 */
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++)
+        A3(s[S_TH], j, i, k) = A3(o->tb3d, j, i, k) * pow(p00 / A3(o->pb3d, j, i, k), rovcp);
+  for (int k = 1; k <= kz; k++)                                    /* :244-248 */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        A3(s[S_RHOB], j, i, k) = A3(o->pb3d, j, i, k) / (c_rgas * A3(o->tb3d, j, i, k));
+        A3(s[S_TP], j, i, k) = A3(o->tb3d, j, i, k) * pow(A2(s[S_PS2D], j, i) / A3(o->pb3d, j, i, k), rovcp);
+      }
+  if (o->nh) {                                                     /* :250-257 */
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) A3(s[S_WPX], j, i, k) = A3(o->omega, j, i, k);
+    for (int k = 1; k <= kp; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(s[S_WB], j, i, k) = A3(o->wb3d, j, i, k);
+  } else {                                                         /* :258-272 */
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) A3(s[S_WPX], j, i, k) = A3(o->omega, j, i, k) * d_1000;
+    for (int k = 2; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(s[S_WB], j, i, k) = -d_half * c_regrav *
+              (A3(s[S_WPX], j, i, k - 1) / A3(s[S_RHOB], j, i, k - 1) + A3(s[S_WPX], j, i, k) / A3(s[S_RHOB], j, i, k));
+    for (int k = kz; k >= 1; k--)                                  /* :273-293 */
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) {
+          double cell = o->ptop * A2(o->srpsb, j, i);
+          A3(s[S_ZQ], j, i, k) = A3(s[S_ZQ], j, i, k + 1) + rovg * A3(s[S_TV], j, i, k) *
+                                 log((o->sigma[k + 1] + cell) / (o->sigma[k] + cell));
+        }
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) {
+          A3(s[S_ZA], j, i, k) = d_half * (A3(s[S_ZQ], j, i, k) + A3(s[S_ZQ], j, i, k + 1));
+          A3(s[S_DZQ], j, i, k) = A3(s[S_ZQ], j, i, k) - A3(s[S_ZQ], j, i, k + 1);
+        }
+  }
+  for (int k = 1; k <= kz; k++)                                    /* :330-338 */
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(s[S_QSB], j, i, k) = pfwsat(A3(o->tb3d, j, i, k), A3(o->pb3d, j, i, k));
+        if (j >= o->jci1 && j <= o->jci2 && i >= o->ici1 && i <= o->ici2) {
+          double rh = A3(o->qb3d[0], j, i, k) / A3(s[S_QSB], j, i, k);
+          A3(s[S_RHB], j, i, k) = dmin(dmax(rh, o->rhmin), o->rhmax);
+        }
+      }
 }
 
 /* generic relaxation step shared by nudge2d/3d/4d3d/uv, Main/mod_bdycod.F90:4218-4766 */
@@ -2329,6 +2466,7 @@ static int nh_tend(orc_t* o) {
   nh_decouple(o);
   nh_compute_omega(o);
   nh_mkslice(o);
+  slice_export(o);
   nh_calc_coeff(o);
   memset(o->tten, 0, n3 * 8); memset(o->tdyn, 0, n3 * 8);
   memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
@@ -2356,22 +2494,22 @@ static int nh_tend(orc_t* o) {
   diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
   nh_diffu_xk(o, o->ppdyn, o->ppb3d, o->xkc, kz);
   nh_diffu_xk(o, o->wdyn, o->wb3d, o->xkcf, kp);
-  /* sums (:285-314, 332-335) */
+  /* sums (:285-314, 332-335) with the host's pc_physic tendencies (phy, 0 unless put) */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
-        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + 0.0;
-        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + 0.0;
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + A3(o->phy[0], j, i, k);
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + A3(o->phy[1], j, i, k);
       }
   for (int k = 1; k <= kp; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
-        A3(o->wten, j, i, k) = A3(o->wten, j, i, k) + A3(o->wdyn, j, i, k) + 0.0;
+        A3(o->wten, j, i, k) = A3(o->wten, j, i, k) + A3(o->wdyn, j, i, k) + A3(o->phy[6], j, i, k);
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
-        A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) + A3(o->ppdyn, j, i, k) + 0.0;
-        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + 0.0;
+        A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) + A3(o->ppdyn, j, i, k) + A3(o->phy[5], j, i, k);
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + A3(o->phy[2], j, i, k);
       }
   /* condtq (:336-350) is physics: stubbed, tphy = qxphy = 0 */
   for (int k = 1; k <= kz; k++)
@@ -2413,8 +2551,8 @@ static int nh_tend(orc_t* o) {
   for (int k = 1; k <= kz; k++)                                     /* :404-411 */
     for (int i = o->idi1; i <= o->idi2; i++)
       for (int j = o->jdi1; j <= o->jdi2; j++) {
-        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + 0.0;
-        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + 0.0;
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + A3(o->phy[3], j, i, k);
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + A3(o->phy[4], j, i, k);
       }
   /* time filters t, qx (:422-427) */
   double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;
@@ -2476,6 +2614,7 @@ int orc_tend(orc_t* o) {
   decouple(o);
   compute_omega(o);
   mkslice(o);
+  slice_export(o);
   new_pressure(o);
   calc_coeff(o);
   /* init_tendencies, :1227-1268 (total/dynamic/physic components all zero) */
@@ -2487,18 +2626,18 @@ int orc_tend(orc_t* o) {
   curvature(o);
   adiabatic(o);
   boundary(o);
-  /* physical_parametrizations: stubbed -> tphy = qxphy = uphy = vphy = 0 */
+  /* physical_parametrizations: the host's pc_physic tendencies (phy, 0 unless put) */
   diffu_d(o);
   diffu_x(o, o->tdyn, o->tb3d, d_one);
   diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
   diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
-  /* sums, :285-294 and :332-349 (tphy = qxphy = 0) */
+  /* sums, :285-294 and :332-349 (tphy, qxphy from the host; the SUBEX condtq terms = 0) */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
-        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + 0.0;
-        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + 0.0;
-        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + 0.0;
+        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + A3(o->phy[0], j, i, k);
+        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + A3(o->phy[1], j, i, k);
+        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + A3(o->phy[2], j, i, k);
         A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + 0.0;
         A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
         A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
@@ -2532,8 +2671,8 @@ int orc_tend(orc_t* o) {
   for (int k = 1; k <= kz; k++)                                     /* :404-411 */
     for (int i = o->idi1; i <= o->idi2; i++)
       for (int j = o->jdi1; j <= o->jdi2; j++) {
-        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + 0.0;
-        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + 0.0;
+        A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + A3(o->phy[3], j, i, k);
+        A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + A3(o->phy[4], j, i, k);
       }
   /* time filters, :419-427, Main/mod_timefilter.F90 */
   double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;

@@ -17,7 +17,7 @@ import numpy as np
 
 MAXKZ = 64
 MAXSPLIT = 4
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # Share/mod_sigma.F90:88-152 -- the hard-coded sigma tables (data, cited).
 SIGMA_TABLES = {
@@ -72,6 +72,7 @@ class RcmdynConfig(ctypes.Structure):
         ("nhbet", ctypes.c_double), ("nhxkd", ctypes.c_double),
         ("rayalpha0", ctypes.c_double), ("rayhd", ctypes.c_double),
         ("nh_dtsmax", ctypes.c_double), ("nh_xmsf", ctypes.c_double),
+        ("rhmin", ctypes.c_double), ("rhmax", ctypes.c_double),
     ]
 
 
@@ -88,13 +89,21 @@ FIELD_NAMES = [
     "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W", "XPPB_B0", "XPPB_BT", "XWWB_B0", "XWWB_BT",
     "ATM0_PS", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_Z", "ATM0_PF", "ATM0_RHOF", "ATM0_ZF",
     "DPSDXM", "DPSDYM", "DPRDDX", "DPRDDY", "EF", "DDX", "DDY", "DMDX", "DMDY", "EX", "CRX", "CRY",
+    "TPHY", "QVPHY", "QCPHY", "UPHY", "VPHY", "PPPHY", "WPHY",
+    "ATMS_UBX3D", "ATMS_VBX3D", "ATMS_UBD3D", "ATMS_VBD3D", "ATMS_TB3D", "ATMS_QVB3D", "ATMS_QCB3D",
+    "ATMS_TV3D", "ATMS_PB3D", "ATMS_PF3D", "ATMS_PS2D", "ATMS_RHOX2D", "ATMS_TH3D", "ATMS_RHOB3D",
+    "ATMS_TP3D", "ATMS_WPX3D", "ATMS_WB3D", "ATMS_ZQ", "ATMS_ZA", "ATMS_DZQ", "ATMS_QSB3D", "ATMS_RHB3D",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
          "PTEN", "PSDOTA", "ATM0_PS", "DPSDXM", "DPSDYM", "EF", "DDX", "DDY", "DMDX", "DMDY",
-         "EX", "CRX", "CRY"}
+         "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D"}
 FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM0_RHOF",
-               "ATM0_ZF"}
+               "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ"}
+# physics coupling seam: pc_physic tendencies (put) and the mkslice export (get)
+PHY_FIELDS = ["TPHY", "QVPHY", "QCPHY", "UPHY", "VPHY"]
+NH_PHY_FIELDS = ["PPPHY", "WPHY"]
+ATMS_FIELDS = [n for n in FIELD_NAMES if n.startswith("ATMS_")]
 NH_STATE_FIELDS = ["ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"]
 NH_BDY_FIELDS = ["XPPB_B0", "XPPB_BT", "XWWB_B0", "XWWB_BT"]
 NH_STATIC_FIELDS = ["ATM0_PS", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_Z", "ATM0_PF",
@@ -158,6 +167,8 @@ class RunConfig:
     rayndamp: int = 5
     rayalpha0: float = 0.0003
     rayhd: float = 10000.0
+    rhmin: float = 0.01              # cldparam, Main/mod_params.F90:331-332
+    rhmax: float = 1.01
     nhbet: float = 0.4
     nhxkd: float = 0.1
     base_state_pressure: float = 101325.0
@@ -251,6 +262,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
         ctypes.memmove(c.comm_unique_id, unique_id, 128)
     c.ifupr, c.ifrayd, c.rayndamp = rc.ifupr, rc.ifrayd, rc.rayndamp
     c.nhbet, c.nhxkd, c.rayalpha0, c.rayhd = rc.nhbet, rc.nhxkd, rc.rayalpha0, rc.rayhd
+    c.rhmin, c.rhmax = rc.rhmin, rc.rhmax
     if rc.idynamic == 2:
         c.nh_dtsmax = split["nh_dtsmax"]
         c.nh_xmsf = split["nh_xmsf"]

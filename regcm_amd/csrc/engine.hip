@@ -24,6 +24,7 @@
 #include "engine.hpp"
 #include "kernels.hpp"
 #include "kernels_nh.hpp"
+#include "slice.hpp"
 
 using namespace rcm;
 
@@ -445,6 +446,8 @@ struct rcmdyn_engine {
     f.psdotb = t.psdotb; f.qdot = t.qdot;
     f.tten = t.tten; f.qvten = t.qvten; f.qcten = t.qcten; f.uten = t.uten; f.vten = t.vten;
     f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc; f.depplane = t.depplane;
+    f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
+    f.ppphy = t.phy[5]; f.wphy = t.phy[6];
     return f;
   }
 
@@ -548,9 +551,23 @@ struct rcmdyn_engine {
   }
 
   // public field id -> (pointer, levels)
+  static int atms_levels(int q, int kz) {
+    const int f = RCMDYN_ATMS_UBX3D + q;
+    if (f == RCMDYN_ATMS_PF3D || f == RCMDYN_ATMS_WB3D || f == RCMDYN_ATMS_ZQ) return kz + 1;
+    if (f == RCMDYN_ATMS_PS2D || f == RCMDYN_ATMS_RHOX2D) return 1;
+    return kz;
+  }
   double* field_ptr(Tile& t, int f, int& nk) {
     nk = cfg.kz;
     const int c = t.cur;
+    if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY) {
+      if (f == RCMDYN_WPHY) nk = cfg.kz + 1;
+      return t.phy[f - RCMDYN_TPHY];
+    }
+    if (f >= RCMDYN_ATMS_UBX3D && f <= RCMDYN_ATMS_RHB3D) {
+      nk = atms_levels(f - RCMDYN_ATMS_UBX3D, cfg.kz);
+      return t.atms[f - RCMDYN_ATMS_UBX3D];
+    }
     if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
       if (cfg.idynamic != 2) return nullptr;
       NHFields& h = nhf[&t - tiles.data()];
@@ -613,10 +630,12 @@ struct rcmdyn_engine {
   }
 
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
-    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || f > RCMDYN_CRY)
+    const bool phyf = f >= RCMDYN_TPHY && f <= RCMDYN_WPHY;
+    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || (f > RCMDYN_CRY && !phyf))
       throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
-    if (f >= RCMDYN_ATM1_PP && cfg.idynamic != 2)
+    if (((f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) || f == RCMDYN_PPPHY || f == RCMDYN_WPHY) && cfg.idynamic != 2)
       throw std::runtime_error("rcmdyn_put: non-hydrostatic field on a hydrostatic engine");
+    if (phyf) enable_physics();
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -634,13 +653,61 @@ struct rcmdyn_engine {
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
     if ((f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) || (f >= RCMDYN_XPPB_B0 && f <= RCMDYN_XWWB_BT)) bdy_dirty = true;
     ghosts_stale = true;
-    if (f >= RCMDYN_ATM0_PS) invalidate_graphs();
+    if (f >= RCMDYN_ATM0_PS && f <= RCMDYN_CRY) invalidate_graphs();
+  }
+
+  // physics coupling seam: the pc_physic buffers exist from the first put of one of them on
+  // (zero-filled), and every later tend adds them; the captured graphs held null pointers
+  void enable_physics() {
+    if (tiles.empty() || tiles[0].phy[0]) return;
+    HIPCHK(hipStreamSynchronize(stream));
+    for (auto& t : tiles) {
+      const size_t P = t.g.plane;
+      for (int q = 0; q < 5; q++) t.phy[q] = dalloc(t, P * cfg.kz);
+      if (cfg.idynamic == 2) { t.phy[5] = dalloc(t, P * cfg.kz); t.phy[6] = dalloc(t, P * (cfg.kz + 1)); }
+    }
+    invalidate_graphs();
+  }
+
+  // mkslice export (slice.hip) for the host physics, run by rcmdyn_tend_pre_physics
+  void run_slice() {
+    for (auto& t : tiles) {
+      if (t.atms[0]) continue;
+      for (int q = 0; q < 22; q++) t.atms[q] = dalloc(t, t.g.plane * (size_t)atms_levels(q, cfg.kz));
+    }
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const int c = t.cur;
+      SliceArgs a{};
+      a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[c];
+      a.a2qv = t.a2qv[c]; a.a2qc = t.a2qc[c]; a.psa = t.psa_[c]; a.psb = t.psb_[c];
+      a.rpsb = t.rpsb; a.rpsdb = t.rpsdb; a.rpsda = t.rpsda; a.msfx = t.msfx; a.qdot = t.qdot; a.pten = t.pten;
+      if (cfg.idynamic == 2) {
+        const NHFields& h = nhf[&t - tiles.data()];
+        a.a2pp = h.a2pp; a.a2w = h.a2w; a.ps0 = h.ps0; a.pr0 = h.pr0; a.pf0 = h.pf0; a.rho0 = h.rho0;
+      }
+      double** o = t.atms;
+      a.ubx3d = o[0]; a.vbx3d = o[1]; a.ubd3d = o[2]; a.vbd3d = o[3]; a.tb3d = o[4]; a.qvb3d = o[5];
+      a.qcb3d = o[6]; a.tv3d = o[7]; a.pb3d = o[8]; a.pf3d = o[9]; a.ps2d = o[10]; a.rhox2d = o[11];
+      a.th3d = o[12]; a.rhob3d = o[13]; a.tp3d = o[14]; a.wpx3d = o[15]; a.wb3d = o[16]; a.zq = o[17];
+      a.za = o[18]; a.dzq = o[19]; a.qsb3d = o[20]; a.rhb3d = o[21];
+      a.ep2 = AMW / AMD;                                  // Share/mod_constants.F90:306
+      a.rhmin = cfg.rhmin; a.rhmax = cfg.rhmax;
+      KLAUNCH(k_slice, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc, a);
+    });
   }
 
   void get(int f, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
     if (!diag && (f == RCMDYN_TTEN || f == RCMDYN_UTEN || f == RCMDYN_VTEN || f == RCMDYN_QVTEN ||
                   f == RCMDYN_QCTEN || f == RCMDYN_OMEGA || f == RCMDYN_XKC))
       throw std::runtime_error("rcmdyn_get: tendency diagnostics are off (rcmdyn_set_diagnostics)");
+    if (f >= RCMDYN_ATMS_UBX3D && f <= RCMDYN_ATMS_RHB3D) {
+      if (!tiles[0].atms[0]) throw std::runtime_error("rcmdyn_get: no slice fields yet (rcmdyn_tend_pre_physics)");
+      if (cfg.idynamic == 2 && (f == RCMDYN_ATMS_ZQ || f == RCMDYN_ATMS_ZA || f == RCMDYN_ATMS_DZQ))
+        throw std::runtime_error("rcmdyn_get: zq/za/dzq are not computed by mkslice for idynamic=2");
+    }
+    if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY && !tiles[0].phy[0])
+      throw std::runtime_error("rcmdyn_get: no physics tendencies were put");
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -927,6 +994,7 @@ struct rcmdyn_engine {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
       f.omega = t.omega; f.xkcs = t.xkcs;
     }
+    f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.red = red; f.red_off = t.red_off;
     return f;
   }
@@ -952,7 +1020,7 @@ struct rcmdyn_engine {
   // compute_omega (cr, qdot), calc_coeff (xkc), the moisture forecast (atmc%qx), and per
   // acoustic sub-step dp'/dp0 with pp, then u and v (Main/mod_sound.F90:262-263, 294-295);
   // the upper radiative condition's estore gather (:496-497) becomes a 6-deep halo.
-  void nh_tend() {
+  void nh_tend(int phase, bool slice) {
     const int kz = cfg.kz, kp = kz + 1;
     const int istep = nh_istep();
     const bool alarm = nh_day_alarm();
@@ -965,6 +1033,7 @@ struct rcmdyn_engine {
                    grid3(nci_j, nci_i, 1), grid3(nci_j, nci_i, kz), grid3(nci_j, nci_i, kz - 1),
                    grid3(ndi_j, ndi_i, 1), grid3(ndi_j, ndi_i, kz)};
     };
+    if (phase & TEND_PRE) {
     xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz},
          {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2},
          {FK::A2QV, kz, 2}, {FK::A2QC, kz, 2}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}});
@@ -981,9 +1050,15 @@ struct rcmdyn_engine {
     xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
     each([&](Tile& t) {
       const Geom& g = t.g;
+      KLAUNCH(k_nh_coeff_scale, grids(g).fr, BLK, 0, stream, g, dc, nhfields(t));
+    });
+    if (slice) run_slice();
+    }
+    if (!(phase & TEND_POST)) return;
+    each([&](Tile& t) {
+      const Geom& g = t.g;
       const NHFields f = nhfields(t);
       const Grids q = grids(g);
-      KLAUNCH(k_nh_coeff_scale, q.fr, BLK, 0, stream, g, dc, f);
       // init_tendencies (:1227-1240)
       const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
       for (double* p : {f.tten, f.tdyn, f.qvten, f.qvdyn, f.qcten, f.qcdyn, f.uten, f.udyn, f.vten, f.vdyn,
@@ -1088,16 +1163,24 @@ struct rcmdyn_engine {
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }
 
-  void tend() {
-    if (cfg.idynamic == 2) { nh_tend(); return; }
-    const int kz = cfg.kz, ns = cfg.nsplit;
+  // tend in two phases split where the reference calls physical_parametrizations
+  // (Main/mod_tendency.F90:271): TEND_PRE runs surface_pressures .. new_pressure (and the
+  // mkslice export when `slice`), TEND_POST the rest; a step runs both.
+  static constexpr int TEND_PRE = 1, TEND_POST = 2, TEND_ALL = 3;
+  void tend(int phase = TEND_ALL, bool slice = false) {
+    if (cfg.idynamic == 2) { nh_tend(phase, slice); return; }
+    if (phase & TEND_PRE) tend_pre(slice);
+    if (phase & TEND_POST) tend_post();
+  }
+
+  void tend_pre(bool slice) {
+    const int kz = cfg.kz;
     // One exchange point for the whole prologue (Main/mod_tendency.F90:815-1116,
     // Main/mod_slice.F90:102-300): the decoupled fields are recomputed where read, so their
     // exchanges become exchanges of atm1 (width 1) and atm2 (idif = 2); p* travels 3 wide so
     // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
     // atm1 travels 2 wide and atm2 3 wide: one more than the reference's widths, for the
     // ghost rings the kernels below compute in place of the later exchanges
-    const bool fused = split_fused();
     xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2}, {FK::A1QV, kz, 2},
          {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
          {FK::A2QC, kz, 3}});
@@ -1112,6 +1195,12 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);
     });
+    if (slice) run_slice();
+  }
+
+  void tend_post() {
+    const int kz = cfg.kz, ns = cfg.nsplit;
+    const bool fused = split_fused();
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1436,6 +1525,25 @@ int rcmdyn_tend(rcmdyn_t* h) {
   return guard(h, [&] {
     h->prepare();
     h->tend();
+    HIPCHK(hipStreamSynchronize(h->stream));
+    StepState st;
+    HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
+    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+  });
+}
+
+int rcmdyn_tend_pre_physics(rcmdyn_t* h) {
+  return guard(h, [&] {
+    h->prepare();
+    h->tend(rcmdyn_engine::TEND_PRE, true);
+    HIPCHK(hipStreamSynchronize(h->stream));
+  });
+}
+
+int rcmdyn_tend_post_physics(rcmdyn_t* h) {
+  return guard(h, [&] {
+    h->prepare();
+    h->tend(rcmdyn_engine::TEND_POST);
     HIPCHK(hipStreamSynchronize(h->stream));
     StepState st;
     HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));

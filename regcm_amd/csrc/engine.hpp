@@ -141,6 +141,11 @@ struct Tile {
   double *wdeld = nullptr, *wdelh = nullptr, *wpsa = nullptr, *wpsdota = nullptr;
   double *wmsfx = nullptr, *wmsfd = nullptr, *wmapf = nullptr;
   double *westore = nullptr;       // NH: estore of sound on the wide frame (6-deep halo)
+  // physics coupling seam: pc_physic tendencies t, qv, qc, u, v, pp, w (allocated on the first
+  // put of one of them) and the exported atms slice fields (allocated on the first
+  // rcmdyn_tend_pre_physics), in rcmdyn_field order
+  double *phy[7] = {};
+  double *atms[22] = {};
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials

@@ -531,9 +531,10 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     ut = ut - pd * (f00 + f0m - fm0 - fmm) / den2;
     vt = vt - pd * (f00 + fm0 - f0m - fmm) / den2;
   }
-  // totals (uphy = 0), forecast, RA filter
-  ut = (spu + ut) + d_zero;
-  vt = (spv + vt) + d_zero;
+  // totals uten + udyn + uphy (Main/mod_tendency.F90:404-411), forecast, RA filter
+  // (pc_physic of the coupling seam, loaded here to keep registers free: absent = 0)
+  ut = (spu + ut) + (f.uphy ? LD(f.uphy, o3) : d_zero);
+  vt = (spv + vt) + (f.vphy ? LD(f.vphy, o3) : d_zero);
   if (f.uten) { ST(f.uten, o3, ut); ST(f.vten, o3, vt); }
   const double g1 = c->gnu1;
   const double u2 = u2c, v2 = v2c;
@@ -798,7 +799,9 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
 #undef FGT
     }
     DIFFU_X(td, sTB);
-    const double tt = ((spt + td) + d_zero) + d_zero;
+    // tten + tdyn + tphy (:285-288), then the SUBEX condensation term (:332-341, stubbed)
+    // (pc_physic of the coupling seam, loaded here to keep registers free: absent = 0)
+    const double tt = ((spt + td) + (f.tphy ? LD(f.tphy, o3) : d_zero)) + d_zero;
     if (f.tten) ST(f.tten, o3, tt);
     const double ct = t2 + dt * tt;
     const double d = c->gnu1 * (ct + t2 - d_two * t1);
@@ -857,8 +860,8 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
   DIFFU_X(tc, sQCB);
 #undef DT
 #undef H1T
-  tq = ((spq + tq) + d_zero) + d_zero;
-  tc = ((d_zero + tc) + d_zero) + d_zero;
+  tq = ((spq + tq) + (f.qvphy ? LD(f.qvphy, o3) : d_zero)) + d_zero;
+  tc = ((d_zero + tc) + (f.qcphy ? LD(f.qcphy, o3) : d_zero)) + d_zero;
   if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
   ST(f.cqv, o3, qv2 + dt * tq);
   ST(f.cqc, o3, qc2 + dt * tc);
@@ -939,13 +942,16 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
   const bool xi0 = icx && in(jp, g.jcx1(), g.jcx2()) && g.gci(jp, i);
   const bool xi1 = icx && in(jp + 1, g.jcx1(), g.jcx2()) && g.gci(jp + 1, i);
   const bool di0 = idx && in(jp, g.jdi1, jd2), di1 = idx && in(jp + 1, g.jdi1, jd2);
-  // p* RA filter on the fly (k = 1 threads store it)
+  // every operand is loaded before the first store (the buffers are not __restrict__, so a
+  // store would otherwise order the later loads behind it: one memory latency per field)
   double2 pa = LD2(f.psa, o2), pb = LD2(f.psb, o2);
-  if (xi0 || xi1) {
-    const double2 psc = LD2(f.psc, o2);
-    if (xi0) { const double d = c->gnu1 * (psc.x + pb.x - d_two * pa.x); pb.x = pa.x + d; pa.x = psc.x; }
-    if (xi1) { const double d = c->gnu1 * (psc.y + pb.y - d_two * pa.y); pb.y = pa.y + d; pa.y = psc.y; }
-  }
+  const double2 psc = LD2(f.psc, o2);
+  const double2 cvq[2] = {LD2(f.cqv, o3), LD2(f.cqc, o3)};
+  const double2 o1q[2] = {LD2(f.a1qv, o3), LD2(f.a1qc, o3)};
+  const double2 o2q[2] = {LD2(f.a2qv, o3), LD2(f.a2qc, o3)};
+  // p* RA filter on the fly (k = 1 threads store it)
+  if (xi0) { const double d = c->gnu1 * (psc.x + pb.x - d_two * pa.x); pb.x = pa.x + d; pa.x = psc.x; }
+  if (xi1) { const double d = c->gnu1 * (psc.y + pb.y - d_two * pa.y); pb.y = pa.y + d; pa.y = psc.y; }
   if (k == 1) { ST2(f.bpsa, o2, pa); ST2(f.bpsb, o2, pb); }
   // points k_momentum / k_scalars do not update keep their values in the next buffers
   {
@@ -957,16 +963,17 @@ __global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restric
 #undef KEEP
   }
   if (!ci0 && !ci1) {
-    ST2(f.b1qv, o3, LD2(f.a1qv, o3)); ST2(f.b1qc, o3, LD2(f.a1qc, o3));
-    ST2(f.b2qv, o3, LD2(f.a2qv, o3)); ST2(f.b2qc, o3, LD2(f.a2qc, o3));
+    ST2(f.b1qv, o3, o1q[0]); ST2(f.b1qc, o3, o1q[1]);
+    ST2(f.b2qv, o3, o2q[0]); ST2(f.b2qc, o3, o2q[1]);
     return;
   }
+#pragma unroll
   for (int n = 0; n < 2; n++) {
     const double* sv = n ? f.cqc : f.cqv;
     double* fx = n ? f.fqc : f.fqv;
-    const double2 cv = LD2(sv, o3);
-    const double2 o1 = LD2(n ? f.a1qc : f.a1qv, o3), o2v = LD2(n ? f.a2qc : f.a2qv, o3);
+    const double2 cv = cvq[n], o1 = o1q[n], o2v = o2q[n];
     double2 n1, n2;
+#pragma unroll
     for (int q = 0; q < 2; q++) {
       const int j = jp + q;
       const bool ci = q ? ci1 : ci0;
@@ -1376,14 +1383,37 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
   const bool ci0 = ici && in(jp, g.jce1, g.jcx2()) && g.gci(jp, i);
   const bool ci1 = ici && in(jp + 1, g.jce1, g.jcx2()) && g.gci(jp + 1, i);
   const bool di0 = idi && in(jp, g.jdi1, jd2), di1 = idi && in(jp + 1, g.jdi1, jd2);
-  if (ci0 || ci1) {
-    double dd[2][MAXSPLIT];
-    for (int l = 1; l <= ns; l++) {
+  // every operand is loaded before the first store (the state buffers are not __restrict__:
+  // a store would order the later loads behind it)
+  const bool cx = ci0 || ci1, dx = di0 || di1;
+  double dd[2][MAXSPLIT];
+  double2 pa{}, pb{}, t1{}, t2{}, u1{}, v1{}, u2{}, v2{}, pd{}, md{};
+  double2 h0[MAXSPLIT], hs[MAXSPLIT];
+  double hw[MAXSPLIT], hsw[MAXSPLIT];
+  if (cx) {
+#pragma unroll
+    for (int l = 1; l <= MAXSPLIT; l++) {
+      if (l > ns) break;
       const double2 d = LD2(ddsum, o2 + (uint32_t)(l - 1) * g.L8);
       dd[0][l - 1] = d.x; dd[1][l - 1] = d.y;
     }
+    if (k == 1) { pa = LD2(psa, o2); pb = LD2(psb, o2); }
+    t1 = LD2(a1t, o3); t2 = LD2(a2t, o3);
+  }
+  if (dx) {
+    u1 = LD2(a1u, o3); v1 = LD2(a1v, o3); u2 = LD2(a2u, o3); v2 = LD2(a2v, o3);
+    pd = LD2(psdota, o2); md = LD2(msfd, o2);
+#pragma unroll
+    for (int l = 1; l <= MAXSPLIT; l++) {
+      if (l > ns) break;
+      const uint32_t lo = o2 + (uint32_t)(l - 1) * g.L8;
+      // dhsum at (jp-1..jp+1, i-1..i)
+      h0[l - 1] = LD2(dhsum, lo); hs[l - 1] = LD2(dhsum, lo - g.P8);
+      hw[l - 1] = LD(dhsum, lo - 8u); hsw[l - 1] = LD(dhsum, lo - g.P8 - 8u);
+    }
+  }
+  if (cx) {
     if (k == 1) {
-      double2 pa = LD2(psa, o2), pb = LD2(psb, o2);
       for (int l = 1; l <= ns; l++) {
         const double an = c->an[l - 1];
         if (ci0) { pa.x = pa.x - an * dd[0][l - 1]; pb.x = pb.x - gnu1 * an * dd[0][l - 1]; }
@@ -1391,7 +1421,6 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
       }
       ST2(psa, o2, pa); ST2(psb, o2, pb);
     }
-    double2 t1 = LD2(a1t, o3), t2 = LD2(a2t, o3);
     for (int l = 1; l <= ns; l++) {
       const double am = c->am[l - 1][k - 1];
       if (ci0) { t1.x = t1.x + am * dd[0][l - 1]; t2.x = t2.x + gnu1 * am * dd[0][l - 1]; }
@@ -1399,24 +1428,20 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
     }
     ST2(a1t, o3, t1); ST2(a2t, o3, t2);
   }
-  if (di0 || di1) {
-    double2 u1 = LD2(a1u, o3), v1 = LD2(a1v, o3), u2 = LD2(a2u, o3), v2 = LD2(a2v, o3);
-    const double2 pd = LD2(psdota, o2), md = LD2(msfd, o2);
+  if (dx) {
     const double fac0 = pd.x / (c->dx2 * md.x), fac1 = pd.y / (c->dx2 * md.y);
-    for (int l = 1; l <= ns; l++) {
-      const uint32_t lo = o2 + (uint32_t)(l - 1) * g.L8;
-      // dhsum at (jp-1..jp+1, i-1..i)
-      const double2 h0 = LD2(dhsum, lo), hs = LD2(dhsum, lo - g.P8);
-      const double hw = LD(dhsum, lo - 8u), hsw = LD(dhsum, lo - g.P8 - 8u);
+#pragma unroll
+    for (int l = 1; l <= MAXSPLIT; l++) {
+      if (l > ns) break;
       const double zm = c->zmatx[l - 1][k - 1], gnuzm = gnu1 * zm;
       if (di0) {
-        const double x = fac0 * (h0.x + hs.x - hw - hsw);
-        const double y = fac0 * (h0.x - hs.x + hw - hsw);
+        const double x = fac0 * (h0[l - 1].x + hs[l - 1].x - hw[l - 1] - hsw[l - 1]);
+        const double y = fac0 * (h0[l - 1].x - hs[l - 1].x + hw[l - 1] - hsw[l - 1]);
         u1.x = u1.x - zm * x; v1.x = v1.x - zm * y; u2.x = u2.x - gnuzm * x; v2.x = v2.x - gnuzm * y;
       }
       if (di1) {
-        const double x = fac1 * (h0.y + hs.y - h0.x - hs.x);
-        const double y = fac1 * (h0.y - hs.y + h0.x - hs.x);
+        const double x = fac1 * (h0[l - 1].y + hs[l - 1].y - h0[l - 1].x - hs[l - 1].x);
+        const double y = fac1 * (h0[l - 1].y - hs[l - 1].y + h0[l - 1].x - hs[l - 1].x);
         u1.y = u1.y - zm * x; v1.y = v1.y - zm * y; u2.y = u2.y - gnuzm * x; v2.y = v2.y - gnuzm * y;
       }
     }

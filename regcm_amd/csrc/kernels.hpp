@@ -44,6 +44,8 @@ struct Fields {
   double *qdot, *phi, *cqv, *cqc, *fqv, *fqc;
   int* depplane;
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
+  // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
+  const double *tphy, *qvphy, *qcphy, *uphy, *vphy;
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
   int red_off;                 // this tile's first partial
 };

@@ -554,12 +554,13 @@ __global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepSt
   const int kz = c->kz;
   const double dt = s->dt;
   if (IN_CI(j, i)) {
-    F3(f.wten, j, i, k) = F3(f.wten, j, i, k) + F3(f.wdyn, j, i, k) + 0.0;
+#define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
+    F3(f.wten, j, i, k) = F3(f.wten, j, i, k) + F3(f.wdyn, j, i, k) + PHY(wphy);
     if (k <= kz) {
-      double tt = F3(f.tten, j, i, k) + F3(f.tdyn, j, i, k) + 0.0;
-      double qv = F3(f.qvten, j, i, k) + F3(f.qvdyn, j, i, k) + 0.0;
-      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) + F3(f.ppdyn, j, i, k) + 0.0;
-      double qc = F3(f.qcten, j, i, k) + F3(f.qcdyn, j, i, k) + 0.0;
+      double tt = F3(f.tten, j, i, k) + F3(f.tdyn, j, i, k) + PHY(tphy);
+      double qv = F3(f.qvten, j, i, k) + F3(f.qvdyn, j, i, k) + PHY(qvphy);
+      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) + F3(f.ppdyn, j, i, k) + PHY(ppphy);
+      double qc = F3(f.qcten, j, i, k) + F3(f.qcdyn, j, i, k) + PHY(qcphy);
       tt = tt + 0.0; qv = qv + 0.0; qc = qc + 0.0;
       if (c->ifrayd == 1 && k <= c->rayndamp) {
         const double xt = s->xbctime + dt;
@@ -582,9 +583,10 @@ __global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepSt
     F3(f.cqc, j, i, k) = qc;
   }
   if (IN_DI(j, i)) {
-    F3(f.uten, j, i, k) = F3(f.uten, j, i, k) + F3(f.udyn, j, i, k) + 0.0;
-    F3(f.vten, j, i, k) = F3(f.vten, j, i, k) + F3(f.vdyn, j, i, k) + 0.0;
+    F3(f.uten, j, i, k) = F3(f.uten, j, i, k) + F3(f.udyn, j, i, k) + PHY(uphy);
+    F3(f.vten, j, i, k) = F3(f.vten, j, i, k) + F3(f.vdyn, j, i, k) + PHY(vphy);
   }
+#undef PHY
 }
 
 // negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points

@@ -29,6 +29,8 @@ struct NHFields {
   // tendencies: total (pc_total) and dynamic (pc_dynamic)
   double *tten, *tdyn, *qvten, *qvdyn, *qcten, *qcdyn, *uten, *udyn, *vten, *vdyn;
   double *ppten, *ppdyn, *wten, *wdyn;
+  // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
+  const double *tphy, *qvphy, *qcphy, *uphy, *vphy, *ppphy, *wphy;
   // forecasts (atmc) and fixed moisture
   double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
   int* depplane;

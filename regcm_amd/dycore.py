@@ -20,7 +20,8 @@ import numpy as np
 from .config import FIELD, RcmdynConfig, build_config, field_levels
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librcmdyn.so")
+# RCMDYN_LIB selects an instrumented build (tools/phases.py); default: the in-tree engine
+LIB_PATH = os.environ.get("RCMDYN_LIB") or os.path.join(_HERE, "librcmdyn.so")
 _lib = None
 
 EXPORTED = [
@@ -28,6 +29,7 @@ EXPORTED = [
     "rcmdyn_tile_extent", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
+    "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics",
 ]
 
 
@@ -57,6 +59,8 @@ def lib():
     L.rcmdyn_set_time.argtypes = [P, ctypes.c_int64, ctypes.c_double, ctypes.c_double]
     L.rcmdyn_get_time.argtypes = [P, ctypes.POINTER(ctypes.c_int64), dp, dp]
     L.rcmdyn_tend.argtypes = [P]
+    L.rcmdyn_tend_pre_physics.argtypes = [P]
+    L.rcmdyn_tend_post_physics.argtypes = [P]
     L.rcmdyn_bdyval.argtypes = [P]
     L.rcmdyn_step.argtypes = [P, i32]
     L.rcmdyn_synchronize.argtypes = [P]
@@ -146,6 +150,14 @@ class DynCore:
 
     def tend(self):
         self._check(lib().rcmdyn_tend(self.h))
+
+    def tend_pre_physics(self):
+        """surface_pressures .. mkslice .. new_pressure: the ATMS_* fields become readable."""
+        self._check(lib().rcmdyn_tend_pre_physics(self.h))
+
+    def tend_post_physics(self):
+        """The rest of tend, with the *PHY tendencies put since (physics coupling seam)."""
+        self._check(lib().rcmdyn_tend_post_physics(self.h))
 
     def bdyval(self):
         self._check(lib().rcmdyn_bdyval(self.h))

@@ -11,7 +11,7 @@ module mod_gpu_dyn
   implicit none
   private
 
-  integer, parameter, public :: rcmdyn_abi_version = 2
+  integer, parameter, public :: rcmdyn_abi_version = 3
   integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
 
   ! field ids (enum rcmdyn_field)
@@ -29,7 +29,14 @@ module mod_gpu_dyn
     f_atm0_ps = 48, f_atm0_pr = 49, f_atm0_t = 50, f_atm0_rho = 51, f_atm0_z = 52, &
     f_atm0_pf = 53, f_atm0_rhof = 54, f_atm0_zf = 55, f_dpsdxm = 56, f_dpsdym = 57, &
     f_dprddx = 58, f_dprddy = 59, f_ef = 60, f_ddx = 61, f_ddy = 62, f_dmdx = 63, &
-    f_dmdy = 64, f_ex = 65, f_crx = 66, f_cry = 67
+    f_dmdy = 64, f_ex = 65, f_crx = 66, f_cry = 67, &
+    ! physics coupling seam: pc_physic tendencies (put) and the mkslice export (get)
+    f_tphy = 68, f_qvphy = 69, f_qcphy = 70, f_uphy = 71, f_vphy = 72, f_ppphy = 73, f_wphy = 74, &
+    f_atms_ubx3d = 75, f_atms_vbx3d = 76, f_atms_ubd3d = 77, f_atms_vbd3d = 78, f_atms_tb3d = 79, &
+    f_atms_qvb3d = 80, f_atms_qcb3d = 81, f_atms_tv3d = 82, f_atms_pb3d = 83, f_atms_pf3d = 84, &
+    f_atms_ps2d = 85, f_atms_rhox2d = 86, f_atms_th3d = 87, f_atms_rhob3d = 88, f_atms_tp3d = 89, &
+    f_atms_wpx3d = 90, f_atms_wb3d = 91, f_atms_zq = 92, f_atms_za = 93, f_atms_dzq = 94, &
+    f_atms_qsb3d = 95, f_atms_rhb3d = 96
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -56,6 +63,8 @@ module mod_gpu_dyn
     ! non-hydrostatic core (nonhydroparam, init_sound outputs)
     integer(c_int32_t) :: ifupr, ifrayd, rayndamp, nh_reserved
     real(c_double) :: nhbet, nhxkd, rayalpha0, rayhd, nh_dtsmax, nh_xmsf
+    ! cldparam rhmin, rhmax (mkslice rhb3d clamps)
+    real(c_double) :: rhmin, rhmax
   end type rcmdyn_config
 
   interface
@@ -100,6 +109,14 @@ module mod_gpu_dyn
       import :: c_int, c_ptr
       type(c_ptr), value :: h
     end function
+    integer(c_int) function rcmdyn_tend_pre_physics(h) bind(c, name='rcmdyn_tend_pre_physics')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
+    integer(c_int) function rcmdyn_tend_post_physics(h) bind(c, name='rcmdyn_tend_post_physics')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
     integer(c_int) function rcmdyn_bdyval(h) bind(c, name='rcmdyn_bdyval')
       import :: c_int, c_ptr
       type(c_ptr), value :: h
@@ -122,6 +139,7 @@ module mod_gpu_dyn
 
   public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
   public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics
+  public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics
   public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d
 
   contains

@@ -103,3 +103,16 @@ def test_create_without_gpu_fails_loudly():
     data = icbc.generate(rc)
     with pytest.raises(dycore.EngineError):
         dycore.DynCore(rc, data["split"])
+
+
+def test_field_enum_matches_header_python_fortran():
+    """rcmdyn_field order is one contract for C, the Python host and the Fortran shim."""
+    from regcm_amd.config import FIELD_NAMES
+    src = open(HEADER).read()
+    body = src[src.index("enum rcmdyn_field"):src.index("RCMDYN_NFIELDS")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"RCMDYN_(\w+)", body)
+    assert names == FIELD_NAMES
+    f90 = open(os.path.join(ROOT, "regcm_amd", "fortran", "mod_gpu_dyn.F90")).read()
+    ids = {m.group(1).upper(): int(m.group(2)) for m in re.finditer(r"\bf_(\w+)\s*=\s*(\d+)", f90)}
+    assert ids == {n: q for q, n in enumerate(FIELD_NAMES)}

@@ -240,3 +240,45 @@ def test_nh_oracle_stable_and_active():
     assert np.abs(pp - st["ATM1_PP"][:, :-1, :-1] / psn).max() < 2000.0
     for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_PP", "ATM1_W", "ATM2_W"):
         assert not np.array_equal(o.get(n), st[n]), n
+
+
+def test_oracle_physics_seam_sums_and_slices(c1_data):
+    """Physics coupling seam on the restatement: zero pc_physic tendencies leave the step
+    bit-identical, non-zero ones act linearly at first order, and the mkslice export obeys
+    the reference's own identities (za = mid-point of zq, dzq = zq difference, tv3d from
+    tb3d and the moistures, rhb3d inside [rhmin, rhmax])."""
+    from oracle.oracle import OracleCore
+    from regcm_amd.config import PHY_FIELDS, STATE_FIELDS
+    rc, data = c1_data
+    runs = []
+    for amp in (0.0, 1e-3, 2e-3):
+        o = OracleCore(rc, data["split"])
+        o.put_state(data["state"])
+        o.bdyval()
+        if amp or len(runs) == 0:
+            for name in PHY_FIELDS:
+                o.put(name, np.full((rc.kz, rc.iy, rc.jx), amp if name in ("TPHY", "UPHY") else 0.0))
+        o.tend()
+        runs.append(o)
+    base = OracleCore(rc, data["split"])
+    base.put_state(data["state"])
+    base.bdyval()
+    base.tend()
+    for name in STATE_FIELDS:
+        assert np.array_equal(runs[0].get(name), base.get(name)), name
+    # one tend: the forecast is linear in the tendency (t: dt * tphy exactly up to rounding)
+    t0, t1, t2 = (r.get("ATM1_T")[:, 1:rc.iy - 2, 1:rc.jx - 2] for r in runs)
+    d1, d2 = t1 - t0, t2 - t0
+    assert np.max(np.abs(d1)) > 0
+    assert np.allclose(d2, 2.0 * d1, rtol=1e-6, atol=1e-12)
+    o = runs[0]
+    zq, za, dzq = o.get("ATMS_ZQ"), o.get("ATMS_ZA"), o.get("ATMS_DZQ")
+    sl = (slice(None), slice(0, rc.iy - 1), slice(0, rc.jx - 1))
+    assert np.allclose(za[sl], 0.5 * (zq[:-1][sl] + zq[1:][sl]), rtol=1e-14, atol=0)
+    assert np.allclose(dzq[sl], zq[:-1][sl] - zq[1:][sl], rtol=1e-14, atol=0)
+    assert np.all(dzq[sl] > 0)
+    tb, qv, qc, tv = (o.get(n) for n in ("ATMS_TB3D", "ATMS_QVB3D", "ATMS_QCB3D", "ATMS_TV3D"))
+    from regcm_amd import constants as C
+    assert np.allclose(tv[sl], tb[sl] * (1.0 + C.ep1 * qv[sl] - qc[sl]), rtol=1e-15)
+    rh = o.get("ATMS_RHB3D")[:, 1:rc.iy - 2, 1:rc.jx - 2]
+    assert rh.min() >= rc.rhmin and rh.max() <= rc.rhmax
