@@ -157,6 +157,13 @@ enum rcmdyn_field {
   RCMDYN_ATMS_PS2D, RCMDYN_ATMS_RHOX2D, RCMDYN_ATMS_TH3D, RCMDYN_ATMS_RHOB3D, RCMDYN_ATMS_TP3D,
   RCMDYN_ATMS_WPX3D, RCMDYN_ATMS_WB3D, RCMDYN_ATMS_ZQ, RCMDYN_ATMS_ZA, RCMDYN_ATMS_DZQ,
   RCMDYN_ATMS_QSB3D, RCMDYN_ATMS_RHB3D,
+  /* device bdyin (put): the next ICBC record as read_icbc returns it
+   * (Main/mod_bdycod.F90:469-480): u, v (m/s, dot), t (K), qv (kg/kg), ps (2-D, hPa; not read
+   * for idynamic = 2), NH pp (Pa) and w (m/s, kz+1 levels), uncoupled; rcmdyn_bdyin converts
+   * and couples it.  ATM0_PSDOT: atm0%psdot (2-D, Pa, dot points), the NH coupling factor of
+   * u, v (:399). */
+  RCMDYN_XUB_B1, RCMDYN_XVB_B1, RCMDYN_XTB_B1, RCMDYN_XQB_B1, RCMDYN_XPSB_B1, RCMDYN_XPPB_B1,
+  RCMDYN_XWWB_B1, RCMDYN_ATM0_PSDOT,
   RCMDYN_NFIELDS
 };
 
@@ -196,6 +203,13 @@ int rcmdyn_tend(rcmdyn_t* h);                  /* one mod_tendency::tend */
 int rcmdyn_tend_pre_physics(rcmdyn_t* h);
 int rcmdyn_tend_post_physics(rcmdyn_t* h);
 int rcmdyn_bdyval(rcmdyn_t* h);                /* one mod_bdycod::bdyval */
+/* mod_bdycod::bdyin from read_icbc on (Main/mod_bdycod.F90:654-889), on the device:
+ * b0 <- b1; the record put into the XxB_B1 fields becomes the new b1 (p* = ps/10 - ptop,
+ * exchange, psc2psd, couple u, v with p* on dot points and t, qv (pp, w) with p*, exchange);
+ * bt = (b1 - b0)/dtbdys on the ga ranges (timeint); xbctime = 0.  The reference's init_bdy
+ * (:280-650) reads b0 and b1: call rcmdyn_bdyin twice, with the record at the start and the
+ * one dtbdys later. */
+int rcmdyn_bdyin(rcmdyn_t* h);
 int rcmdyn_step(rcmdyn_t* h, int32_t nsteps);  /* nsteps x (tend + bdyval), graph-replayed */
 int rcmdyn_synchronize(rcmdyn_t* h);
 

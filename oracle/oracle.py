@@ -50,6 +50,7 @@ def lib():
         L.orc_tend.restype = i
         L.orc_tend.argtypes = [P]
         L.orc_bdyval.argtypes = [P]
+        L.orc_bdyin.argtypes = [P]
         L.orc_step.restype = i
         L.orc_step.argtypes = [P, i]
         L.orc_diagnostics.argtypes = [P, dp]
@@ -121,6 +122,9 @@ class OracleCore:
 
     def bdyval(self):
         lib().orc_bdyval(self.h)
+
+    def bdyin(self):
+        lib().orc_bdyin(self.h)
 
     def step(self, n=1):
         if lib().orc_step(self.h, n):

@@ -122,6 +122,8 @@ struct orc {
   /* physics coupling seam: pc_physic tendencies t, qv, qc, u, v, pp, w and the atms export
    * (rcmdyn_field TPHY.. and ATMS_UBX3D.. order) */
   double *phy[7], *atms[22];
+  /* bdyin: raw record (u, v, t, qv, ps, pp, w), coupled b1 (same order), NH atm0%psdot */
+  double *bin[7], *bb1[7], *psdot0;
   double rhmin, rhmax;
   /* diagnostics */
   double ptntot, pt2tot;
@@ -391,6 +393,13 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   for (int q = 0; q < 5; q++) o->phy[q] = alloc3(o, kz);
   if (o->nh) { o->phy[5] = alloc3(o, kz); o->phy[6] = alloc3(o, kp); }
   for (int q = 0; q < 22; q++) o->atms[q] = alloc3(o, atms_levels(q, kz));
+  for (int q = 0; q < 4; q++) { o->bin[q] = alloc3(o, kz); o->bb1[q] = alloc3(o, kz); }
+  o->bin[4] = alloc3(o, 1); o->bb1[4] = alloc3(o, 1);
+  if (o->nh) {
+    o->bin[5] = alloc3(o, kz); o->bb1[5] = alloc3(o, kz);
+    o->bin[6] = alloc3(o, kp); o->bb1[6] = alloc3(o, kp);
+    o->psdot0 = alloc3(o, 1);
+  }
   o->rhmin = cfg->rhmin; o->rhmax = cfg->rhmax;
   size_t sjn = (size_t)o->nj * kz, sin_ = (size_t)o->ni * kz;
   o->sue = calloc(sjn, 8); o->sui = calloc(sjn, 8); o->nue = calloc(sjn, 8); o->nui = calloc(sjn, 8);
@@ -428,6 +437,8 @@ void orc_destroy(orc_t* o) {
   for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
   for (int q = 0; q < 7; q++) free(o->phy[q]);
   for (int q = 0; q < 22; q++) free(o->atms[q]);
+  for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
+  free(o->psdot0);
   for (int n = 0; n < 2; n++) {
     free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
     free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
@@ -467,6 +478,12 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     *nk = atms_levels(f - RCMDYN_ATMS_UBX3D, o->kz);
     return o->atms[f - RCMDYN_ATMS_UBX3D];
   }
+  if (f >= RCMDYN_XUB_B1 && f <= RCMDYN_XWWB_B1) {
+    if (f == RCMDYN_XPSB_B1) *nk = 1;
+    if (f == RCMDYN_XWWB_B1) *nk = o->kz + 1;
+    return o->bin[f - RCMDYN_XUB_B1];
+  }
+  if (f == RCMDYN_ATM0_PSDOT) { *nk = 1; return o->psdot0; }
   switch (f) {
     case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
     case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
@@ -2772,6 +2789,84 @@ static void bdyuv(orc_t* o, double xt) {
 }
 
 /* bdyval, Main/mod_bdycod.F90:1109-2571 (idynamic = 1, iboudy /= 0, bdyflow) */
+/* bdyin from read_icbc on, Main/mod_bdycod.F90:654-889: b0 <- b1 (:670-690), the record in
+ * bin converted and coupled into b1 (:757-799, couple :4938-4951), exchanges (:759, 800-815),
+ * timeint on the ga ranges (:801-825, :5087-5113), xbctime = 0 (:666).  NH: xpsb%b1 =
+ * atm0%ps*d_r1000, psdot = atm0%psdot*d_r1000 (:398-400). */
+void orc_bdyin(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  size_t n3 = o->plane * (size_t)kz;
+  double rdtbdy = d_one / o->cfg.dtbdys;
+  o->xbctime = d_zero;
+  memcpy(o->ub0, o->bb1[0], n3 * 8); memcpy(o->vb0, o->bb1[1], n3 * 8);
+  memcpy(o->tb0, o->bb1[2], n3 * 8); memcpy(o->qb0, o->bb1[3], n3 * 8);
+  if (o->nh) {
+    memcpy(o->ppb0, o->bb1[5], n3 * 8); memcpy(o->wwb0, o->bb1[6], o->plane * (size_t)kp * 8);
+  } else {
+    memcpy(o->pb0, o->bb1[4], o->plane * 8);
+  }
+  double* pb1 = o->bb1[4];
+  double* psdot = (double*)calloc(o->plane, sizeof(double));
+  if (o->nh) {
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A2(pb1, j, i) = A2(o->ps0, j, i) * 0.001;
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) A2(psdot, j, i) = A2(o->psdot0, j, i) * 0.001;
+  } else {
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A2(pb1, j, i) = (A2(o->bin[4], j, i) * 0.1) - o->ptop;
+    xch(o, pb1, 1, 1, 0);
+    psc2psd(o, pb1, psdot);
+  }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        A3(o->bb1[0], j, i, k) = A3(o->bin[0], j, i, k) * A2(psdot, j, i);
+        A3(o->bb1[1], j, i, k) = A3(o->bin[1], j, i, k) * A2(psdot, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(o->bb1[2], j, i, k) = A3(o->bin[2], j, i, k) * A2(pb1, j, i);
+        A3(o->bb1[3], j, i, k) = A3(o->bin[3], j, i, k) * A2(pb1, j, i);
+      }
+  for (int q = 0; q < 4; q++) xch(o, o->bb1[q], kz, 1, 0);
+  if (o->nh) {
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(o->bb1[5], j, i, k) = A3(o->bin[5], j, i, k) * A2(pb1, j, i);
+    for (int k = 1; k <= kp; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(o->bb1[6], j, i, k) = A3(o->bin[6], j, i, k) * A2(pb1, j, i);
+    xch(o, o->bb1[5], kz, 1, 0);
+    xch(o, o->bb1[6], kp, 1, 0);
+  }
+  free(psdot);
+  for (int k = 1; k <= kz; k++) {
+    for (int i = o->ide1ga; i <= o->ide2ga; i++)
+      for (int j = o->jde1ga; j <= o->jde2ga; j++) {
+        A3(o->ubt, j, i, k) = (A3(o->bb1[0], j, i, k) - A3(o->ub0, j, i, k)) * rdtbdy;
+        A3(o->vbt, j, i, k) = (A3(o->bb1[1], j, i, k) - A3(o->vb0, j, i, k)) * rdtbdy;
+      }
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++) {
+        A3(o->tbt, j, i, k) = (A3(o->bb1[2], j, i, k) - A3(o->tb0, j, i, k)) * rdtbdy;
+        A3(o->qbt, j, i, k) = (A3(o->bb1[3], j, i, k) - A3(o->qb0, j, i, k)) * rdtbdy;
+        if (o->nh) A3(o->ppbt, j, i, k) = (A3(o->bb1[5], j, i, k) - A3(o->ppb0, j, i, k)) * rdtbdy;
+      }
+  }
+  if (o->nh) {
+    for (int k = 1; k <= kp; k++)
+      for (int i = o->ice1ga; i <= o->ice2ga; i++)
+        for (int j = o->jce1ga; j <= o->jce2ga; j++)
+          A3(o->wwbt, j, i, k) = (A3(o->bb1[6], j, i, k) - A3(o->wwb0, j, i, k)) * rdtbdy;
+  } else {
+    for (int i = o->ice1ga; i <= o->ice2ga; i++)
+      for (int j = o->jce1ga; j <= o->jce2ga; j++)
+        A2(o->pbt, j, i) = (A2(pb1, j, i) - A2(o->pb0, j, i)) * rdtbdy;
+  }
+}
+
 void orc_bdyval(orc_t* o) {
   int kz = o->kz;
   double xt = o->xbctime + o->dt;

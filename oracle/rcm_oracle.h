@@ -49,6 +49,8 @@ void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
 void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);
 int orc_tend(orc_t* o);     /* returns 1 on CFL violation (NaN ptntot) */
 void orc_bdyval(orc_t* o);
+/* bdyin from read_icbc on: the record put into the XxB_B1 fields becomes b1 (see rcmdyn_bdyin) */
+void orc_bdyin(orc_t* o);
 void orc_diagnostics(const orc_t* o, double out[4]);
 /* OpenMP-free, single thread.  Runs nsteps x (tend + bdyval); returns first error. */
 int orc_step(orc_t* o, int nsteps);

@@ -93,13 +93,14 @@ FIELD_NAMES = [
     "ATMS_UBX3D", "ATMS_VBX3D", "ATMS_UBD3D", "ATMS_VBD3D", "ATMS_TB3D", "ATMS_QVB3D", "ATMS_QCB3D",
     "ATMS_TV3D", "ATMS_PB3D", "ATMS_PF3D", "ATMS_PS2D", "ATMS_RHOX2D", "ATMS_TH3D", "ATMS_RHOB3D",
     "ATMS_TP3D", "ATMS_WPX3D", "ATMS_WB3D", "ATMS_ZQ", "ATMS_ZA", "ATMS_DZQ", "ATMS_QSB3D", "ATMS_RHB3D",
+    "XUB_B1", "XVB_B1", "XTB_B1", "XQB_B1", "XPSB_B1", "XPPB_B1", "XWWB_B1", "ATM0_PSDOT",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
          "PTEN", "PSDOTA", "ATM0_PS", "DPSDXM", "DPSDYM", "EF", "DDX", "DDY", "DMDX", "DMDY",
-         "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D"}
+         "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D", "XPSB_B1", "ATM0_PSDOT"}
 FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM0_RHOF",
-               "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ"}
+               "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ", "XWWB_B1"}
 # physics coupling seam: pc_physic tendencies (put) and the mkslice export (get)
 PHY_FIELDS = ["TPHY", "QVPHY", "QCPHY", "UPHY", "VPHY"]
 NH_PHY_FIELDS = ["PPPHY", "WPHY"]

@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "kernels_nh.hpp"
 #include "slice.hpp"
+#include "bdyin.hpp"
 
 using namespace rcm;
 
@@ -197,7 +198,9 @@ enum class FK {
   RPSDA, RPSDB, QDOT, CQV, CQC, PHI, UU, VV, DHSUM, DELH, MSFX, MSFD, HT, CORIOL,
   UB0, UBT, VB0, VBT, TB0, TBT, QB0, QBT, PB0, PBT, DSTOR, HSTOR,
   // non-hydrostatic core
-  A1PP, A2PP, A1W, A2W, NCR, NXKCR, NCDT, NCPP, NCU, NCV
+  A1PP, A2PP, A1W, A2W, NCR, NXKCR, NCDT, NCPP, NCU, NCV,
+  // device bdyin: coupled boundary data at the interval end
+  UB1, VB1, TB1, QB1, PB1, PPB1, WWB1
 };
 
 struct rcmdyn_engine {
@@ -540,6 +543,12 @@ struct rcmdyn_engine {
       case FK::PBT: return t.pbt; case FK::DSTOR: return t.dstor; case FK::HSTOR: return t.hstor;
       default: break;
     }
+    switch (f) {
+      case FK::UB1: return t.bb1[0]; case FK::VB1: return t.bb1[1]; case FK::TB1: return t.bb1[2];
+      case FK::QB1: return t.bb1[3]; case FK::PB1: return t.bb1[4]; case FK::PPB1: return t.bb1[5];
+      case FK::WWB1: return t.bb1[6];
+      default: break;
+    }
     const NHFields& h = nhf[&t - tiles.data()];
     switch (f) {
       case FK::A1PP: return h.a1pp; case FK::A2PP: return h.a2pp; case FK::A1W: return h.a1w;
@@ -568,6 +577,12 @@ struct rcmdyn_engine {
       nk = atms_levels(f - RCMDYN_ATMS_UBX3D, cfg.kz);
       return t.atms[f - RCMDYN_ATMS_UBX3D];
     }
+    if (f >= RCMDYN_XUB_B1 && f <= RCMDYN_XWWB_B1) {
+      if (f == RCMDYN_XPSB_B1) nk = 1;
+      if (f == RCMDYN_XWWB_B1) nk = cfg.kz + 1;
+      return t.bin[f - RCMDYN_XUB_B1];
+    }
+    if (f == RCMDYN_ATM0_PSDOT) { nk = 1; return t.psdot0; }
     if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
       if (cfg.idynamic != 2) return nullptr;
       NHFields& h = nhf[&t - tiles.data()];
@@ -631,11 +646,16 @@ struct rcmdyn_engine {
 
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
     const bool phyf = f >= RCMDYN_TPHY && f <= RCMDYN_WPHY;
-    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || (f > RCMDYN_CRY && !phyf))
+    const bool binf = f >= RCMDYN_XUB_B1 && f <= RCMDYN_ATM0_PSDOT;
+    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || (f > RCMDYN_CRY && !phyf && !binf))
       throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
-    if (((f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) || f == RCMDYN_PPPHY || f == RCMDYN_WPHY) && cfg.idynamic != 2)
+    if (((f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) || f == RCMDYN_PPPHY || f == RCMDYN_WPHY ||
+         f == RCMDYN_XPPB_B1 || f == RCMDYN_XWWB_B1 || f == RCMDYN_ATM0_PSDOT) && cfg.idynamic != 2)
       throw std::runtime_error("rcmdyn_put: non-hydrostatic field on a hydrostatic engine");
+    if (f == RCMDYN_XPSB_B1 && cfg.idynamic == 2)
+      throw std::runtime_error("rcmdyn_put: the non-hydrostatic core reads no ps record (p* is atm0%ps)");
     if (phyf) enable_physics();
+    if (binf) enable_bdyin();
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -667,6 +687,63 @@ struct rcmdyn_engine {
       if (cfg.idynamic == 2) { t.phy[5] = dalloc(t, P * cfg.kz); t.phy[6] = dalloc(t, P * (cfg.kz + 1)); }
     }
     invalidate_graphs();
+  }
+
+  // device bdyin buffers (raw record, coupled b1; NH atm0%psdot), zero-filled
+  void enable_bdyin() {
+    if (tiles.empty() || tiles[0].bin[0]) return;
+    HIPCHK(hipStreamSynchronize(stream));
+    const bool nh = cfg.idynamic == 2;
+    for (auto& t : tiles) {
+      const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
+      for (int q = 0; q < 4; q++) { t.bin[q] = dalloc(t, P3); t.bb1[q] = dalloc(t, P3); }
+      t.bin[4] = dalloc(t, P); t.bb1[4] = dalloc(t, P);
+      if (nh) {
+        t.bin[5] = dalloc(t, P3); t.bb1[5] = dalloc(t, P3);
+        t.bin[6] = dalloc(t, P4); t.bb1[6] = dalloc(t, P4);
+        t.psdot0 = dalloc(t, P);
+      }
+    }
+  }
+
+  // mod_bdycod::bdyin from read_icbc on (bdyin.hip)
+  void bdyin() {
+    if (tiles.empty() || !tiles[0].bin[0]) throw std::runtime_error("rcmdyn_bdyin: no ICBC record was put (XUB_B1 ..)");
+    const int kz = cfg.kz;
+    const bool nh = cfg.idynamic == 2;
+    auto args = [&](Tile& t) {
+      BdyinArgs a{};
+      a.rub = t.bin[0]; a.rvb = t.bin[1]; a.rtb = t.bin[2]; a.rqb = t.bin[3]; a.rpb = t.bin[4];
+      a.rppb = t.bin[5]; a.rwwb = t.bin[6]; a.psdot0 = t.psdot0;
+      a.ub0 = t.ub0; a.ubt = t.ubt; a.ub1 = t.bb1[0]; a.vb0 = t.vb0; a.vbt = t.vbt; a.vb1 = t.bb1[1];
+      a.tb0 = t.tb0; a.tbt = t.tbt; a.tb1 = t.bb1[2]; a.qb0 = t.qb0; a.qbt = t.qbt; a.qb1 = t.bb1[3];
+      a.pb0 = t.pb0; a.pbt = t.pbt; a.pb1 = t.bb1[4];
+      if (nh) {
+        NHFields& h = nhf[&t - tiles.data()];
+        a.ps0 = h.ps0;
+        a.ppb0 = const_cast<double*>(h.ppb0); a.ppbt = const_cast<double*>(h.ppbt); a.ppb1 = t.bb1[5];
+        a.wwb0 = const_cast<double*>(h.wwb0); a.wwbt = const_cast<double*>(h.wwbt); a.wwb1 = t.bb1[6];
+      }
+      a.rdtbdy = 1.0 / cfg.dtbdys;                        // Main/mod_bdycod.F90:203
+      a.ptop = cfg.ptop; a.kz = kz; a.nh = nh ? 1 : 0;
+      return a;
+    };
+    each([&](Tile& t) {
+      KLAUNCH(k_bdyin_shift, grid3(t.g.nj, t.g.ni, kz + 1), BLK, 0, stream, t.g, args(t));
+      KLAUNCH(k_bdyin_ps, grid3(t.g.jce2 - t.g.jce1 + 1, t.g.ice2 - t.g.ice1 + 1, 1), BLK, 0, stream, t.g, args(t));
+    });
+    xch({{FK::PB1, 1}}, 1, 0);                              // :759
+    each([&](Tile& t) {
+      KLAUNCH(k_bdyin_couple, grid3(t.g.jde2 - t.g.jde1 + 1, t.g.ide2 - t.g.ide1 + 1, kz + 1), BLK, 0, stream,
+              t.g, args(t));
+    });
+    if (nh) xch({{FK::UB1, kz}, {FK::VB1, kz}, {FK::TB1, kz}, {FK::QB1, kz}, {FK::PPB1, kz}, {FK::WWB1, kz + 1}}, 1, 0);
+    else xch({{FK::UB1, kz}, {FK::VB1, kz}, {FK::TB1, kz}, {FK::QB1, kz}}, 1, 0);   // :800-815
+    each([&](Tile& t) {
+      KLAUNCH(k_bdyin_timeint, grid3(t.g.nj, t.g.ni, kz + 1), BLK, 0, stream, t.g, args(t));
+    });
+    set_time(hs.lcount, hs.dt, 0.0);                        // xbctime = d_zero, :666
+    bdy_dirty = true;                                       // b0/bt ghost rings (prepare)
   }
 
   // mkslice export (slice.hip) for the host physics, run by rcmdyn_tend_pre_physics
@@ -1548,6 +1625,13 @@ int rcmdyn_tend_post_physics(rcmdyn_t* h) {
     StepState st;
     HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
     if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+  });
+}
+
+int rcmdyn_bdyin(rcmdyn_t* h) {
+  return guard(h, [&] {
+    h->bdyin();
+    HIPCHK(hipStreamSynchronize(h->stream));
   });
 }
 

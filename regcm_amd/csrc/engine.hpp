@@ -146,6 +146,12 @@ struct Tile {
   // rcmdyn_tend_pre_physics), in rcmdyn_field order
   double *phy[7] = {};
   double *atms[22] = {};
+  // device bdyin: the raw record put by the host (u, v, t, qv, ps, pp, w) and the coupled
+  // boundary data at the interval end (b1, same order), allocated on the first put of a
+  // record field; NH: atm0%psdot (Pa) for the coupling of u, v
+  double *bin[7] = {};
+  double *bb1[7] = {};
+  double *psdot0 = nullptr;
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials

@@ -29,7 +29,7 @@ EXPORTED = [
     "rcmdyn_tile_extent", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
-    "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics",
+    "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin",
 ]
 
 
@@ -61,6 +61,7 @@ def lib():
     L.rcmdyn_tend.argtypes = [P]
     L.rcmdyn_tend_pre_physics.argtypes = [P]
     L.rcmdyn_tend_post_physics.argtypes = [P]
+    L.rcmdyn_bdyin.argtypes = [P]
     L.rcmdyn_bdyval.argtypes = [P]
     L.rcmdyn_step.argtypes = [P, i32]
     L.rcmdyn_synchronize.argtypes = [P]
@@ -161,6 +162,10 @@ class DynCore:
 
     def bdyval(self):
         self._check(lib().rcmdyn_bdyval(self.h))
+
+    def bdyin(self):
+        """bdyin from read_icbc on: the record put into the XxB_B1 fields becomes b1."""
+        self._check(lib().rcmdyn_bdyin(self.h))
 
     def step(self, n: int = 1):
         self._check(lib().rcmdyn_step(self.h, n))

@@ -36,7 +36,10 @@ module mod_gpu_dyn
     f_atms_qvb3d = 80, f_atms_qcb3d = 81, f_atms_tv3d = 82, f_atms_pb3d = 83, f_atms_pf3d = 84, &
     f_atms_ps2d = 85, f_atms_rhox2d = 86, f_atms_th3d = 87, f_atms_rhob3d = 88, f_atms_tp3d = 89, &
     f_atms_wpx3d = 90, f_atms_wb3d = 91, f_atms_zq = 92, f_atms_za = 93, f_atms_dzq = 94, &
-    f_atms_qsb3d = 95, f_atms_rhb3d = 96
+    f_atms_qsb3d = 95, f_atms_rhb3d = 96, &
+    ! device bdyin: the next ICBC record as read_icbc returns it; NH atm0%psdot
+    f_xub_b1 = 97, f_xvb_b1 = 98, f_xtb_b1 = 99, f_xqb_b1 = 100, f_xpsb_b1 = 101, &
+    f_xppb_b1 = 102, f_xwwb_b1 = 103, f_atm0_psdot = 104
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -117,6 +120,10 @@ module mod_gpu_dyn
       import :: c_int, c_ptr
       type(c_ptr), value :: h
     end function
+    integer(c_int) function rcmdyn_bdyin(h) bind(c, name='rcmdyn_bdyin')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
     integer(c_int) function rcmdyn_bdyval(h) bind(c, name='rcmdyn_bdyval')
       import :: c_int, c_ptr
       type(c_ptr), value :: h
@@ -139,7 +146,7 @@ module mod_gpu_dyn
 
   public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
   public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics
-  public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics
+  public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics, rcmdyn_bdyin
   public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d
 
   contains

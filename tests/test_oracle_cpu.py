@@ -282,3 +282,39 @@ def test_oracle_physics_seam_sums_and_slices(c1_data):
     assert np.allclose(tv[sl], tb[sl] * (1.0 + C.ep1 * qv[sl] - qc[sl]), rtol=1e-15)
     rh = o.get("ATMS_RHB3D")[:, 1:rc.iy - 2, 1:rc.jx - 2]
     assert rh.min() >= rc.rhmin and rh.max() <= rc.rhmax
+
+
+def test_oracle_bdyin_matches_numpy_restatement(c1_data):
+    """orc_bdyin against an independent NumPy restatement of bdyin (Main/mod_bdycod.F90:
+    654-889): p* = ps*d_r10 - ptop, psc2psd, couple, timeint -- bit for bit."""
+    from oracle.oracle import OracleCore
+    from regcm_amd import icbc
+    from test_bdyin_gpu import records
+    rc, data = c1_data
+    recs = records(rc, data, False)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    for rec in recs[:2]:
+        for name, a in rec.items():
+            o.put(name, a)
+        o.bdyin()
+    iy, jx = rc.iy, rc.jx
+    ce = (slice(None), slice(0, iy - 1), slice(0, jx - 1))
+
+    def coupled(rec):
+        ps = np.zeros((iy, jx))
+        ps[:iy - 1, :jx - 1] = rec["XPSB_B1"][0][:iy - 1, :jx - 1] * 0.1 - rc.ptop
+        pd = icbc.psc2psd_global(ps)
+        out = {"U": rec["XUB_B1"] * pd[None], "V": rec["XVB_B1"] * pd[None], "P": ps[None]}
+        for n, f in (("T", "XTB_B1"), ("Q", "XQB_B1")):
+            a = np.zeros_like(rec[f])
+            a[ce] = (rec[f] * ps[None])[ce]
+            out[n] = a
+        return out
+
+    b0, b1 = coupled(recs[0]), coupled(recs[1])
+    rdt = 1.0 / rc.dtbdys
+    for n, f in (("U", "XUB"), ("V", "XVB"), ("T", "XTB"), ("Q", "XQB"), ("P", "XPSB")):
+        assert np.array_equal(o.get(f + "_B0"), b0[n]), f
+        assert np.array_equal(o.get(f + "_BT"), (b1[n] - b0[n]) * rdt), f
+    assert o.get_time()[2] == 0.0
