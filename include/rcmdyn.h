@@ -108,6 +108,10 @@ typedef struct rcmdyn_config {
   /* cldparam relative-humidity clamps of the mkslice export (Main/mod_params.F90:331-332,
    * Main/mod_slice.F90:336-337) [rhmin 0.01, rhmax 1.01] */
   double rhmin, rhmax;
+  /* physicsparam isladvec [0] (1 = semi-Lagrangian horizontal advection of the moisture,
+   * Main/mod_sladvection.F90, hydrostatic core) and iqmsl [1] (its quasi-monotone limiter),
+   * Main/mod_params.F90:100, 243-244 */
+  int32_t isladvec, iqmsl;
 } rcmdyn_config;
 
 /* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */

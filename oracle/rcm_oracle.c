@@ -17,6 +17,7 @@
  * no golden vectors exist in the reference tree.
  */
 #include "rcm_oracle.h"
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -728,7 +729,10 @@ static void decouple(orc_t* o) {
             A3(o->vd, j, o->ide2, k) = A3(o->vd, j, o->idi2, k);
           }
   }
-  xch(o, o->ud, kz, 1, 0); xch(o, o->vd, kz, 1, 0);            /* :1003-1004 */
+  {                                                              /* :995-1004 */
+    int w = o->cfg.isladvec == 1 ? 2 : 1;
+    xch(o, o->ud, kz, w, 0); xch(o, o->vd, kz, w, 0);
+  }
   /* umd/vmd (:1005-1008) feed only non-hydrostatic terms: not needed for idynamic=1 */
   for (int k = 1; k <= kz; k++)                                   /* :1013-1025 */
     for (int i = o->ice1ga; i <= o->ice2ga; i++)
@@ -741,7 +745,10 @@ static void decouple(orc_t* o) {
       }
   /* atm1%pr/rho (:1037-1040) and atm2%pr (:1094-1096) feed only physics: skipped */
   xch(o, o->a2u, kz, 2, 0); xch(o, o->a2v, kz, 2, 0); xch(o, o->a2t, kz, 2, 0);
-  xch(o, o->a2q[0], kz, 2, 0); xch(o, o->a2q[1], kz, 2, 0);
+  {                                                              /* :1073-1077 */
+    int w = o->cfg.isladvec == 1 ? 4 : 2;
+    xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
+  }
 }
 
 /* compute_omega, Main/mod_tendency.F90:1118-1215 (hydrostatic) */
@@ -1179,16 +1186,114 @@ static void vadv4d_qc(orc_t* o) {                                  /* :859-961, 
 }
 
 /* advection driver, Main/mod_tendency.F90:1270-1392 (hydrostatic, isladvec = 0) */
-static void advection(orc_t* o) {
+/* Semi-Lagrangian horizontal advection of the moisture (isladvec = 1), Main/mod_sladvection.F90.
+ * trajcalc_x (:121-229, adv_velocity(.false.) :91-114) for every interior cross point and
+ * level, then slhadv_x4d (:401-479) of atm2 qx and hdvg_x4d (:596-664) of atm1 qx into qxdyn.
+ * ua/va = atmx%umd/vmd = ud*msfd (Main/mod_tendency.F90:998-1001), mapfx/mapfd = msfx/msfd. */
+#define UA(J, I) (A3(o->ud, J, I, k) * A2(o->msfd, J, I))
+#define VA(J, I) (A3(o->vd, J, I, k) * A2(o->msfd, J, I))
+static int sl_advection(orc_t* o) {
+  int kz = o->kz, bad = 0;
+  double ddx = o->dx, ddy = o->dx, dt = o->dt, dtsq = dt * dt, dtcb = dt * dt * dt;
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double uadvx = 0.25 * (UA(j, i) + UA(j, i + 1) + UA(j + 1, i + 1) + UA(j + 1, i)) / A2(o->msfx, j, i);
+        double uadxp1 = 0.25 * (UA(j + 1, i) + UA(j + 1, i + 1) + UA(j + 2, i + 1) + UA(j + 2, i)) / A2(o->msfx, j + 1, i);
+        double uadxm1 = 0.25 * (UA(j, i) + UA(j, i + 1) + UA(j - 1, i + 1) + UA(j - 1, i)) / A2(o->msfx, j - 1, i);
+        double vadvy = 0.25 * (VA(j, i) + VA(j, i + 1) + VA(j + 1, i + 1) + VA(j + 1, i)) / A2(o->msfx, j, i);
+        double vadyp1 = 0.25 * (VA(j, i + 1) + VA(j + 1, i + 1) + VA(j + 1, i + 2) + VA(j, i + 2)) / A2(o->msfx, j, i + 1);
+        /* as written at :109-111: va(j+1,i) twice */
+        double vadym1 = 0.25 * (VA(j, i) + VA(j, i - 1) + VA(j + 1, i) + VA(j + 1, i)) / A2(o->msfx, j, i - 1);
+        double ux = 0.5 * (uadxp1 - uadxm1) / ddx;
+        double uxx = (uadxp1 - 2.0 * uadvx + uadxm1) / (ddx * ddx);
+        double xdis = -(uadvx * dt) + 0.5 * (dtsq * uadvx * ux) - (dtcb * uadvx) * (ux * ux + uadvx * uxx) / 6.0;
+        double xn = xdis / ddx;
+        if (!(fabs(xn) < 2.0)) { bad = 1; continue; }
+        int xnp = (int)xn;
+        double alfax = fabs((xnp * ddx - xdis) / ddx);
+        int xsn = (int)copysign(1.0, xn);
+        int xnd = j + xnp, xm1 = xnd + xsn, xm2 = xm1 + xsn, xp1 = xnd - xsn;
+        if (o->bl) { if (xnd < o->jce1) xnd = o->jce1; if (xm1 < o->jce1) xm1 = o->jce1;
+                     if (xm2 < o->jce1) xm2 = o->jce1; if (xp1 < o->jce1) xp1 = o->jce1; }
+        if (o->br) { if (xnd > o->jce2) xnd = o->jce2; if (xm1 > o->jce2) xm1 = o->jce2;
+                     if (xm2 > o->jce2) xm2 = o->jce2; if (xp1 > o->jce2) xp1 = o->jce2; }
+        double vy = 0.5 * (vadyp1 - vadym1) / ddy;
+        double vyy = (vadyp1 - 2.0 * vadvy + vadym1) / (ddy * ddy);
+        double ydis = -(vadvy * dt) + 0.5 * (dtsq * vadvy * vy) - (dtcb * vadvy) * (vy * vy + vadvy * vyy) / 6.0;
+        double yn = ydis / ddy;
+        if (!(fabs(yn) < 2.0)) { bad = 1; continue; }
+        int ynp = (int)yn;
+        double betay = fabs((ynp * ddy - ydis) / ddy);
+        int ysn = (int)copysign(1.0, yn);
+        int ynd = i + ynp, ym1 = ynd + ysn, ym2 = ym1 + ysn, yp1 = ynd - ysn;
+        if (o->bb) { if (ynd < o->ice1) ynd = o->ice1; if (ym1 < o->ice1) ym1 = o->ice1;
+                     if (ym2 < o->ice1) ym2 = o->ice1; if (yp1 < o->ice1) yp1 = o->ice1; }
+        if (o->bt) { if (ynd > o->ice2) ynd = o->ice2; if (ym1 > o->ice2) ym1 = o->ice2;
+                     if (ym2 > o->ice2) ym2 = o->ice2; if (yp1 > o->ice2) yp1 = o->ice2; }
+        double alfm2 = -(alfax * (1.0 - alfax * alfax)) / 6.0;
+        double alfm1 = (alfax * (1.0 + alfax) * (2.0 - alfax)) / 2.0;
+        double alf0 = ((1.0 - alfax * alfax) * (2.0 - alfax)) / 2.0;
+        double alfp1 = -(alfax * (1.0 - alfax) * (2.0 - alfax)) / 6.0;
+        double betm2 = -(betay * (1.0 - betay * betay)) / 6.0;
+        double betm1 = (betay * (1.0 + betay) * (2.0 - betay)) / 2.0;
+        double bet0 = ((1.0 - betay * betay) * (2.0 - betay)) / 2.0;
+        double betp1 = -(betay * (1.0 - betay) * (2.0 - betay)) / 6.0;
+        /* hdvg_x4d divergence (:625-649) */
+        double ucapf = (UA(j + 1, i + 1) * A2(o->msfd, j + 1, i + 1) + UA(j + 1, i) * A2(o->msfd, j + 1, i)) * d_half;
+        double ucapi = (UA(j, i + 1) * A2(o->msfd, j, i + 1) + UA(j, i) * A2(o->msfd, j, i)) * d_half;
+        double vcapf = (VA(j + 1, i + 1) * A2(o->msfd, j + 1, i + 1) + VA(j, i + 1) * A2(o->msfd, j, i + 1)) * d_half;
+        double vcapi = (VA(j + 1, i) * A2(o->msfd, j + 1, i) + VA(j, i) * A2(o->msfd, j, i)) * d_half;
+        double ducapdx = (ucapf - ucapi) / o->dx;
+        double dvcapdy = (vcapf - vcapi) / o->dx;
+        double hdvg = (ducapdx + dvcapdy) / (A2(o->msfx, j, i) * A2(o->msfx, j, i));
+        for (int n = 0; n < 2; n++) {
+          const double* var = o->a2q[n];
+#define V(J, I) A3(var, J, I, k)
+          double bl1 = alfax * V(xm1, yp1) + (d_one - alfax) * V(xnd, yp1);
+          double bl2 = alfax * V(xm1, ym2) + (d_one - alfax) * V(xnd, ym2);
+          double cb1 = alfm2 * V(xm2, ynd) + alfm1 * V(xm1, ynd) + alf0 * V(xnd, ynd) + alfp1 * V(xp1, ynd);
+          double cb2 = alfm2 * V(xm2, ym1) + alfm1 * V(xm1, ym1) + alf0 * V(xnd, ym1) + alfp1 * V(xp1, ym1);
+          double tbadp = betm2 * bl2 + betm1 * cb2 + bet0 * cb1 + betp1 * bl1;
+          double tsla = tbadp;
+          if (o->cfg.iqmsl == 1) {
+            double tbmax = fmax(fmax(fmax(V(xnd, ynd), V(xnd, ym1)), V(xm1, ynd)), V(xm1, ym1));
+            double tbmin = fmin(fmin(fmin(V(xnd, ynd), V(xnd, ym1)), V(xm1, ynd)), V(xm1, ym1));
+            if (tbadp > tbmax) tsla = tbmax;
+            else if (tbadp < tbmin) tsla = tbmin;
+          }
+          if (fabs(tsla - V(j, i)) > DLOWVAL)
+            A3(o->qdyn[n], j, i, k) = A3(o->qdyn[n], j, i, k) + (tsla - V(j, i)) / dt;
+#undef V
+          double q1 = A3(o->a1q[n], j, i, k);
+          double tatot = (q1 > DBL_EPSILON) ? q1 * hdvg : d_zero;
+          A3(o->qdyn[n], j, i, k) = A3(o->qdyn[n], j, i, k) - tatot;
+        }
+      }
+  return bad;
+}
+#undef UA
+#undef VA
+
+static int advection(orc_t* o) {
+  int bad = 0;
   start_advect(o);
   hadvuv(o);
   vadvuv(o);
   hadv_scalar(o, o->xt, o->tdyn, 1);      /* hadvt */
   vadv3d_t(o);
-  hadv_scalar(o, o->xq[0], o->qdyn[0], 2); /* hadvqv */
-  vadvqv(o);                               /* all(icup /= 1) */
-  hadv_scalar(o, o->xq[1], o->qdyn[1], 0); /* hadvqx */
+  if (o->cfg.isladvec == 1) {
+    /* slhadv_x / hdvg_x of qv and qc (:1361-1363, 1378-1380); the reference runs the qv
+     * pass, then vadv of qv, then the qc pass: the passes touch disjoint qxdyn planes */
+    bad = sl_advection(o);
+    vadvqv(o);
+  } else {
+    hadv_scalar(o, o->xq[0], o->qdyn[0], 2); /* hadvqv */
+    vadvqv(o);                               /* all(icup /= 1) */
+    hadv_scalar(o, o->xq[1], o->qdyn[1], 0); /* hadvqx */
+  }
   vadv4d_qc(o);
+  return bad;
 }
 
 /* curvature, Main/mod_tendency.F90:1829-1838 */
@@ -2639,7 +2744,7 @@ int orc_tend(orc_t* o) {
   memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
   memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
   for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
-  advection(o);
+  int slbad = advection(o);
   curvature(o);
   adiabatic(o);
   boundary(o);
@@ -2742,8 +2847,9 @@ int orc_tend(orc_t* o) {
   /* rcmtimer%advance and dt switch, :608-616 */
   o->lcount += 1;
   if (o->lcount == 2) o->dt = d_two * o->dtsec;
-  /* NaN / CFL check, :624-703 */
+  /* NaN / CFL check, :624-703; departure point beyond one cell, Main/mod_sladvection.F90:149-154 */
   if (isnan(o->ptntot)) return 1;
+  if (slbad) return 2;
   return 0;
 }
 

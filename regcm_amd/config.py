@@ -73,6 +73,7 @@ class RcmdynConfig(ctypes.Structure):
         ("rayalpha0", ctypes.c_double), ("rayhd", ctypes.c_double),
         ("nh_dtsmax", ctypes.c_double), ("nh_xmsf", ctypes.c_double),
         ("rhmin", ctypes.c_double), ("rhmax", ctypes.c_double),
+        ("isladvec", ctypes.c_int32), ("iqmsl", ctypes.c_int32),
     ]
 
 
@@ -170,6 +171,8 @@ class RunConfig:
     rayhd: float = 10000.0
     rhmin: float = 0.01              # cldparam, Main/mod_params.F90:331-332
     rhmax: float = 1.01
+    isladvec: int = 0                # physicsparam, Main/mod_params.F90:243-244
+    iqmsl: int = 1
     nhbet: float = 0.4
     nhxkd: float = 0.1
     base_state_pressure: float = 101325.0
@@ -264,6 +267,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.ifupr, c.ifrayd, c.rayndamp = rc.ifupr, rc.ifrayd, rc.rayndamp
     c.nhbet, c.nhxkd, c.rayalpha0, c.rayhd = rc.nhbet, rc.nhxkd, rc.rayalpha0, rc.rayhd
     c.rhmin, c.rhmax = rc.rhmin, rc.rhmax
+    c.isladvec, c.iqmsl = rc.isladvec, rc.iqmsl
     if rc.idynamic == 2:
         c.nh_dtsmax = split["nh_dtsmax"]
         c.nh_xmsf = split["nh_xmsf"]

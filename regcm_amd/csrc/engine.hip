@@ -200,7 +200,9 @@ enum class FK {
   // non-hydrostatic core
   A1PP, A2PP, A1W, A2W, NCR, NXKCR, NCDT, NCPP, NCU, NCV,
   // device bdyin: coupled boundary data at the interval end
-  UB1, VB1, TB1, QB1, PB1, PPB1, WWB1
+  UB1, VB1, TB1, QB1, PB1, PPB1, WWB1,
+  // semi-Lagrangian moisture tendency starts
+  SLQV, SLQC
 };
 
 struct rcmdyn_engine {
@@ -246,6 +248,7 @@ struct rcmdyn_engine {
     c.c287 = rgasmol / AMD; c.rgas = c.c287 * 1000.0; c.cpd = 3.5 * c.rgas;
     c.ep1 = AMD / AMW - 1.0; c.regrav = 1.0 / EGRAV;
     c.ipgf = cfg.ipgf;
+    c.isladvec = cfg.isladvec; c.iqmsl = cfg.iqmsl;
     c.idiffu = cfg.idiffu;
     c.pgfaa1 = 6.5e-3 * c.rgas * c.regrav;                  // Share/mod_constants.F90:359-362
     c.dx = cfg.ds * 1000.0; c.dx2 = 2.0 * c.dx; c.dx4 = 4.0 * c.dx; c.dx8 = 8.0 * c.dx;
@@ -362,6 +365,7 @@ struct rcmdyn_engine {
     t.psc = dalloc(t, P); t.psdota = dalloc(t, P); t.psdotb = dalloc(t, P); t.pten = dalloc(t, 2 * P);
     t.qdot = dalloc(t, P * (kz + 1));
     t.phi = dalloc(t, P3);
+    if (cfg.isladvec == 1) { t.slqv = dalloc(t, P3); t.slqc = dalloc(t, P3); }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     t.depplane = talloc<int>(t, 2 * kz);
     t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
@@ -464,6 +468,9 @@ struct rcmdyn_engine {
     }
     if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
+    if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
+    if (cfg.isladvec == 1 && cfg.idynamic != 1)
+      throw std::runtime_error("rcmdyn: isladvec=1 is built for the hydrostatic core");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
@@ -547,6 +554,7 @@ struct rcmdyn_engine {
       case FK::UB1: return t.bb1[0]; case FK::VB1: return t.bb1[1]; case FK::TB1: return t.bb1[2];
       case FK::QB1: return t.bb1[3]; case FK::PB1: return t.bb1[4]; case FK::PPB1: return t.bb1[5];
       case FK::WWB1: return t.bb1[6];
+      case FK::SLQV: return t.slqv; case FK::SLQC: return t.slqc;
       default: break;
     }
     const NHFields& h = nhf[&t - tiles.data()];
@@ -1065,7 +1073,7 @@ struct rcmdyn_engine {
     f.qb0 = t.qb0; f.qbt = t.qbt; f.pb0 = t.pb0; f.pbt = t.pbt;
     f.rpsa = t.rpsa; f.rpsb = t.rpsb; f.rpsda = t.rpsda; f.rpsdb = t.rpsdb; f.psc = t.psc;
     f.psdota = t.psdota; f.psdotb = t.psdotb; f.pten = t.pten; f.ptenn = t.pten + t.g.plane;
-    f.qdot = t.qdot; f.phi = t.phi; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
+    f.qdot = t.qdot; f.phi = t.phi; f.slqv = t.slqv; f.slqc = t.slqc; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
     f.depplane = t.depplane;
     if (diag) {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
@@ -1278,6 +1286,15 @@ struct rcmdyn_engine {
   void tend_post() {
     const int kz = cfg.kz, ns = cfg.nsplit;
     const bool fused = split_fused();
+    // semi-Lagrangian moisture advection (isladvec = 1): owned points, then the ring k_scalars
+    // also computes comes from the neighbours
+    if (cfg.isladvec == 1) {
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
+      });
+      xch({{FK::SLQV, kz}, {FK::SLQC, kz}}, 1, 0);
+    }
     // fused tendencies + forecast + time filter
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1441,6 +1458,7 @@ struct rcmdyn_engine {
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
     if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
   }
 
   void capture(int par) {
@@ -1498,7 +1516,7 @@ struct rcmdyn_engine {
     HIPCHK(hipStreamSynchronize(stream));
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
-    st.lcount = lcount; st.dt = dt; st.xbctime = xbctime; st.nanflag = 0;
+    st.lcount = lcount; st.dt = dt; st.xbctime = xbctime; st.nanflag = 0; st.slflag = 0;
     HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
     hs.lcount = lcount; hs.dt = dt; hs.xbctime = xbctime;
   }
@@ -1606,6 +1624,7 @@ int rcmdyn_tend(rcmdyn_t* h) {
     StepState st;
     HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
     if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
   });
 }
 
@@ -1625,6 +1644,7 @@ int rcmdyn_tend_post_physics(rcmdyn_t* h) {
     StepState st;
     HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
     if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
+    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
   });
 }
 

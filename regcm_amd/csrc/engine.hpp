@@ -79,6 +79,7 @@ struct Geom {
 // Run constants (read-only on device, one copy per engine).
 struct Consts {
   int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc, ipgf, idiffu;
+  int isladvec, iqmsl;                 // semi-Lagrangian moisture advection (physicsparam)
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
   double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;
@@ -104,7 +105,7 @@ struct StepState {
   long long lcount;   // completed steps
   double ptntot, pt2tot;
   int nanflag;        // sticky: set when a step produced NaN ptntot
-  int pad;
+  int slflag;         // sticky: a semi-Lagrangian departure point beyond one cell
 };
 
 // Per-tile device buffers.
@@ -129,6 +130,7 @@ struct Tile {
   // 2-D reciprocals of the decoupling (decouple / mkslice, recomputed on the fly from them)
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten;
   double *qdot, *phi;
+  double *slqv = nullptr, *slqc = nullptr;   // isladvec = 1: k_sladv output
   double *cqv, *cqc, *fqv, *fqc;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;

@@ -18,6 +18,8 @@
 // shared neighbour offsets) addresses every field: loads are SGPR base + VGPR offset.
 // Column recurrences (pten/qdot, phi, split projections) use one thread per (j,i) column.
 #include "engine.hpp"
+#include <cfloat>
+
 #include "kernels.hpp"
 
 #include <cstdio>
@@ -255,6 +257,108 @@ __device__ double2 udvd_bdy(const Geom& g, const Fields& f, int j, int i, uint32
     if (i == g.giy && LD(f.a1v, g.o2(j, i) + kof) <= d_zero) return we(j, g.giy - 1);
   }
   return we(j, i);
+}
+
+// ---------------------------------------------------------------------------------------
+// K_SL. Semi-Lagrangian horizontal advection of qv and qc (isladvec = 1),
+// Main/mod_sladvection.F90: trajcalc_x (:121-229, adv_velocity(.false.) :91-114), slhadv_x4d
+// of atm2 qx (:401-479) and hdvg_x4d of atm1 qx (:596-664), one thread per owned interior cross
+// point and level.  The result is the start of qxdyn, (0 + sl) - hdvg, which k_scalars takes
+// in place of hadvqv/hadvqx (Main/mod_tendency.F90:1361-1380).  ua/va = atmx%umd/vmd = ud*msfd
+// (:998-1001); the departure points reach three points beyond (j, i), inside the exchanged
+// atm2 ring.  A departure point more than one cell away sets the step flag (fatal
+// 'SLADVECTION', :149-154, 184-189).
+__global__ __launch_bounds__(256) void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f) {
+  THREAD_POINT(g.jci1, g.ici1);
+  if (j > g.jci2 || i > g.ici2) return;
+  const uint32_t P8 = g.P8, L8 = g.L8, kof = (uint32_t)(k - 1) * L8;
+  (void)P8;
+  const bool ib4 = c->iboudy == 4;
+  auto ua = [&](int jj, int ii) {
+    const uint32_t q2 = g.o2(jj, ii);
+    double ud;
+    if (ib4 && (jj == 1 || jj == g.gjx || ii == 1 || ii == g.giy)) ud = udvd_bdy(g, f, jj, ii, kof).x;
+    else ud = LD(f.a1u, q2 + kof) * LD(f.rpsda, q2);
+    return ud * LD(f.msfd, q2);
+  };
+  auto va = [&](int jj, int ii) {
+    const uint32_t q2 = g.o2(jj, ii);
+    double vd;
+    if (ib4 && (jj == 1 || jj == g.gjx || ii == 1 || ii == g.giy)) vd = udvd_bdy(g, f, jj, ii, kof).y;
+    else vd = LD(f.a1v, q2 + kof) * LD(f.rpsda, q2);
+    return vd * LD(f.msfd, q2);
+  };
+  const double dt = s->dt, dtsq = dt * dt, dtcb = dt * dt * dt, ddx = c->dx, ddy = c->dx;
+  const double mx = F2(f.msfx, j, i);
+  const double u00 = ua(j, i), u01 = ua(j, i + 1), u11 = ua(j + 1, i + 1), u10 = ua(j + 1, i);
+  const double v00 = va(j, i), v01 = va(j, i + 1), v11 = va(j + 1, i + 1), v10 = va(j + 1, i);
+  const double uadvx = 0.25 * (u00 + u01 + u11 + u10) / mx;
+  const double uadxp1 = 0.25 * (u10 + u11 + ua(j + 2, i + 1) + ua(j + 2, i)) / F2(f.msfx, j + 1, i);
+  const double uadxm1 = 0.25 * (u00 + u01 + ua(j - 1, i + 1) + ua(j - 1, i)) / F2(f.msfx, j - 1, i);
+  const double vadvy = 0.25 * (v00 + v01 + v11 + v10) / mx;
+  const double vadyp1 = 0.25 * (v01 + v11 + va(j + 1, i + 2) + va(j, i + 2)) / F2(f.msfx, j, i + 1);
+  const double vadym1 = 0.25 * (v00 + va(j, i - 1) + v10 + v10) / F2(f.msfx, j, i - 1);   // as written, :109-111
+  const double ux = 0.5 * (uadxp1 - uadxm1) / ddx;
+  const double uxx = (uadxp1 - 2.0 * uadvx + uadxm1) / (ddx * ddx);
+  const double xdis = -(uadvx * dt) + 0.5 * (dtsq * uadvx * ux) - (dtcb * uadvx) * (ux * ux + uadvx * uxx) / 6.0;
+  const double vy = 0.5 * (vadyp1 - vadym1) / ddy;
+  const double vyy = (vadyp1 - 2.0 * vadvy + vadym1) / (ddy * ddy);
+  const double ydis = -(vadvy * dt) + 0.5 * (dtsq * vadvy * vy) - (dtcb * vadvy) * (vy * vy + vadvy * vyy) / 6.0;
+  const double xn = xdis / ddx, yn = ydis / ddy;
+  if (!(fabs(xn) < 2.0) || !(fabs(yn) < 2.0)) {          // |int(xn)| > 1, or not a number
+    s->slflag = 1;
+    return;
+  }
+  const int xnp = (int)xn, ynp = (int)yn;
+  const double alfax = fabs(((double)xnp * ddx - xdis) / ddx);
+  const double betay = fabs(((double)ynp * ddy - ydis) / ddy);
+  const int xsn = (int)copysign(1.0, xn), ysn = (int)copysign(1.0, yn);
+  int xnd = j + xnp, xm1 = xnd + xsn, xm2 = xm1 + xsn, xp1 = xnd - xsn;
+  int ynd = i + ynp, ym1 = ynd + ysn, ym2 = ym1 + ysn, yp1 = ynd - ysn;
+  if (g.bl) { xnd = max(xnd, g.jce1); xm1 = max(xm1, g.jce1); xm2 = max(xm2, g.jce1); xp1 = max(xp1, g.jce1); }
+  if (g.br) { xnd = min(xnd, g.jce2); xm1 = min(xm1, g.jce2); xm2 = min(xm2, g.jce2); xp1 = min(xp1, g.jce2); }
+  if (g.bb) { ynd = max(ynd, g.ice1); ym1 = max(ym1, g.ice1); ym2 = max(ym2, g.ice1); yp1 = max(yp1, g.ice1); }
+  if (g.bt) { ynd = min(ynd, g.ice2); ym1 = min(ym1, g.ice2); ym2 = min(ym2, g.ice2); yp1 = min(yp1, g.ice2); }
+  const double alfm2 = -(alfax * (1.0 - alfax * alfax)) / 6.0;
+  const double alfm1 = (alfax * (1.0 + alfax) * (2.0 - alfax)) / 2.0;
+  const double alf0 = ((1.0 - alfax * alfax) * (2.0 - alfax)) / 2.0;
+  const double alfp1 = -(alfax * (1.0 - alfax) * (2.0 - alfax)) / 6.0;
+  const double betm2 = -(betay * (1.0 - betay * betay)) / 6.0;
+  const double betm1 = (betay * (1.0 + betay) * (2.0 - betay)) / 2.0;
+  const double bet0 = ((1.0 - betay * betay) * (2.0 - betay)) / 2.0;
+  const double betp1 = -(betay * (1.0 - betay) * (2.0 - betay)) / 6.0;
+  // hdvg_x4d divergence (:625-649)
+  const double m11 = F2(f.msfd, j + 1, i + 1), m10 = F2(f.msfd, j + 1, i), m01 = F2(f.msfd, j, i + 1);
+  const double m00 = F2(f.msfd, j, i);
+  const double ucapf = (u11 * m11 + u10 * m10) * d_half;
+  const double ucapi = (u01 * m01 + u00 * m00) * d_half;
+  const double vcapf = (v11 * m11 + v01 * m01) * d_half;
+  const double vcapi = (v10 * m10 + v00 * m00) * d_half;
+  const double ducapdx = (ucapf - ucapi) / c->dx;
+  const double dvcapdy = (vcapf - vcapi) / c->dx;
+  const double hdvg = (ducapdx + dvcapdy) / (mx * mx);
+  for (int n = 0; n < 2; n++) {
+    const double* var = n ? f.a2qc : f.a2qv;
+#define V(J, I) F3(var, J, I, k)
+    const double bl1 = alfax * V(xm1, yp1) + (d_one - alfax) * V(xnd, yp1);
+    const double bl2 = alfax * V(xm1, ym2) + (d_one - alfax) * V(xnd, ym2);
+    const double cb1 = alfm2 * V(xm2, ynd) + alfm1 * V(xm1, ynd) + alf0 * V(xnd, ynd) + alfp1 * V(xp1, ynd);
+    const double cb2 = alfm2 * V(xm2, ym1) + alfm1 * V(xm1, ym1) + alf0 * V(xnd, ym1) + alfp1 * V(xp1, ym1);
+    const double tbadp = betm2 * bl2 + betm1 * cb2 + bet0 * cb1 + betp1 * bl1;
+    double tsla = tbadp;
+    if (c->iqmsl == 1) {
+      const double tbmax = fmax(fmax(fmax(V(xnd, ynd), V(xnd, ym1)), V(xm1, ynd)), V(xm1, ym1));
+      const double tbmin = fmin(fmin(fmin(V(xnd, ynd), V(xnd, ym1)), V(xm1, ynd)), V(xm1, ym1));
+      if (tbadp > tbmax) tsla = tbmax;
+      else if (tbadp < tbmin) tsla = tbmin;
+    }
+    double ften = d_zero;
+    if (fabs(tsla - V(j, i)) > DLOWVAL) ften = ften + (tsla - V(j, i)) / dt;
+#undef V
+    const double q1 = F3(n ? f.a1qc : f.a1qv, j, i, k);
+    const double tatot = (q1 > DBL_EPSILON) ? q1 * hdvg : d_zero;
+    F3(n ? f.slqc : f.slqv, j, i, k) = ften - tatot;
+  }
 }
 
 constexpr int TW1 = MBJ + 2, TH1 = MBI + 2;   // halo 1 on every side
@@ -809,8 +913,11 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
     ST(f.b1t, o3, ct);
   }
   // ================= qv
-  double tq = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQV, 0, 0), H1T(sXQV, -1, 0),
-                                 H1T(sXQV, 1, 0), H1T(sXQV, 0, -1), H1T(sXQV, 0, 1), 2);
+  // hadvqv, or the semi-Lagrangian start of qxdyn from k_sladv (isladvec = 1, :1361-1363)
+  double tq = c->isladvec ? LD(f.slqv, o3)
+                          : d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQV, 0, 0),
+                                               H1T(sXQV, -1, 0), H1T(sXQV, 1, 0), H1T(sXQV, 0, -1),
+                                               H1T(sXQV, 0, 1), 2);
   {
     const double thr = MINQQ * ps;
     const double qc0 = qv1;
@@ -839,8 +946,11 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
   }
   DIFFU_X(tq, sQVB);
   // ================= qc
-  double tc = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQC, 0, 0), H1T(sXQC, -1, 0),
-                                 H1T(sXQC, 1, 0), H1T(sXQC, 0, -1), H1T(sXQC, 0, 1), 0);
+  // hadvqx, or the semi-Lagrangian start of qxdyn (:1378-1380)
+  double tc = c->isladvec ? LD(f.slqc, o3)
+                          : d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQC, 0, 0),
+                                               H1T(sXQC, -1, 0), H1T(sXQC, 1, 0), H1T(sXQC, 0, -1),
+                                               H1T(sXQC, 0, 1), 0);
   {
     const double thr = MINQQ * MINQQ * ps;
     const double c0 = qc1;

@@ -42,6 +42,7 @@ struct Fields {
   double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten, *ptenn;
   double *qdot, *phi, *cqv, *cqc, *fqv, *fqc;
+  double *slqv, *slqc;         // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv)
   int* depplane;
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
@@ -63,6 +64,7 @@ struct QFix {
 
 __global__ void k_surface_pressures(Geom g, Fields f);
 __global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb);
+__global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);

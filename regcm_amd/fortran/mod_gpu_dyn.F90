@@ -68,6 +68,8 @@ module mod_gpu_dyn
     real(c_double) :: nhbet, nhxkd, rayalpha0, rayhd, nh_dtsmax, nh_xmsf
     ! cldparam rhmin, rhmax (mkslice rhb3d clamps)
     real(c_double) :: rhmin, rhmax
+    ! physicsparam isladvec, iqmsl (semi-Lagrangian moisture advection)
+    integer(c_int32_t) :: isladvec, iqmsl
   end type rcmdyn_config
 
   interface

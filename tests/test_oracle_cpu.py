@@ -162,15 +162,16 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     base.bdyval()
     base.step(10)
     ref = base.get("ATM1_T")
-    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}):
+    refq = base.get("ATM1_QV")
+    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"isladvec": 1}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])
         o.put_state(data["state"])
         o.bdyval()
         o.step(10)
-        t = o.get("ATM1_T")
-        assert np.isfinite(t).all(), variant
-        assert not np.array_equal(t, ref), variant
+        t, q = o.get("ATM1_T"), o.get("ATM1_QV")
+        assert np.isfinite(t).all() and np.isfinite(q).all(), variant
+        assert not (np.array_equal(t, ref) and np.array_equal(q, refq)), variant
 
 
 # ---- non-hydrostatic core (idynamic = 2) ---------------------------------------------------

@@ -222,7 +222,7 @@ def test_negative_moisture_serial_sweep(c1_data):
 
 
 # namelist options beyond the defaults, each against the oracle and under decomposition
-VARIANTS = [{"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}]
+VARIANTS = [{"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"isladvec": 1}, {"isladvec": 1, "iqmsl": 0}]
 
 
 def _variant_id(v):
@@ -274,3 +274,25 @@ def test_variant_decomposition(c1_data, variant):
         e.step(6)
     for name in STATE_FIELDS:
         assert np.array_equal(ref.get(name), til.get(name)), name
+
+
+def test_sladvection_departure_check(c1_data):
+    """A departure point more than one cell away stops the step like the reference's
+    fatal('SLADVECTION') (Main/mod_sladvection.F90:149-154), in the engine and the oracle."""
+    import dataclasses
+    from regcm_amd.dycore import EngineError
+    rc, data = c1_data
+    rcv = dataclasses.replace(rc, isladvec=1)
+    st = {k: v.copy() for k, v in data["state"].items()}
+    for name in ("ATM1_U", "ATM2_U"):
+        st[name] = st[name] * 60.0               # ~600 m/s: u dt > dx at 60 km, 150 s
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    o, e = OracleCore(rcv, data["split"]), DynCore(rcv, data["split"])
+    for c in (o, e):
+        c.put_state(st)
+        c.bdyval()
+    with pytest.raises(FloatingPointError):
+        o.tend()
+    with pytest.raises(EngineError, match="SLADVECTION"):
+        e.tend()
