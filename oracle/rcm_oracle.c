@@ -11,7 +11,7 @@
  *
  * Scope (defaults assumed): idynamic=1, upstream_mode and
  * stability_enhance on, idiffu=1, iboudy=5 (or 1), ipgf=0, nsplit from config,
- * nqx=2 (qv,qc), isladvec=0, ibltyp!=2, ichem=0, idiag=0, iboudy time-dependent.
+ * nqx=2 (qv,qc), isladvec=0/1, ibltyp!=2, ichem=0, idiag=0, iboudy time-dependent.
  *
  * Parity unpinned: no execution of the reference is available (netCDF-Fortran absent),
  * no golden vectors exist in the reference tree.
@@ -2038,7 +2038,8 @@ static void nh_vadv3d_t(orc_t* o) {
 }
 
 /* advection NH (Main/mod_tendency.F90:1270-1392) */
-static void nh_advection(orc_t* o) {
+static int nh_advection(orc_t* o) {
+  int bad = 0;
   start_advect(o);
   nh_hadvuv(o);
   vadvuv(o);
@@ -2048,10 +2049,16 @@ static void nh_advection(orc_t* o) {
   nh_vadv3d_lin(o, o->a1w, o->wdyn, 1);
   hadv_scalar(o, o->xt, o->tdyn, 1);          /* hadvt */
   nh_vadv3d_t(o);
-  hadv_scalar(o, o->xq[0], o->qdyn[0], 2);
-  vadvqv(o);
-  hadv_scalar(o, o->xq[1], o->qdyn[1], 0);
+  if (o->cfg.isladvec == 1) {                 /* :1361-1363, 1378-1380, as in advection() */
+    bad = sl_advection(o);
+    vadvqv(o);
+  } else {
+    hadv_scalar(o, o->xq[0], o->qdyn[0], 2);
+    vadvqv(o);
+    hadv_scalar(o, o->xq[1], o->qdyn[1], 0);
+  }
   vadv4d_qc(o);
+  return bad;
 }
 
 /* curvature NH (:1839-1879) */
@@ -2596,7 +2603,7 @@ static int nh_tend(orc_t* o) {
   for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
   memset(o->ppten, 0, n3 * 8); memset(o->ppdyn, 0, n3 * 8);
   memset(o->wten, 0, n3p * 8); memset(o->wdyn, 0, n3p * 8);
-  nh_advection(o);
+  int slbad = nh_advection(o);
   nh_curvature(o);
   nh_adiabatic(o);
   /* boundary (:1462-1501) */
@@ -2724,7 +2731,8 @@ static int nh_tend(orc_t* o) {
   o->lcount += 1;
   if (o->lcount == 2) o->dt = d_two * o->dtsec;
   o->ptntot = 0; o->pt2tot = 0;
-  return err;
+  if (err) return err;
+  return slbad ? 2 : 0;
 }
 
 /* tend, Main/mod_tendency.F90:212-726 (hydrostatic, physics stubbed) */

@@ -455,6 +455,7 @@ struct rcmdyn_engine {
     f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc; f.depplane = t.depplane;
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.ppphy = t.phy[5]; f.wphy = t.phy[6];
+    f.slqv = t.slqv; f.slqc = t.slqc;
     return f;
   }
 
@@ -469,8 +470,6 @@ struct rcmdyn_engine {
     if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
-    if (cfg.isladvec == 1 && cfg.idynamic != 1)
-      throw std::runtime_error("rcmdyn: isladvec=1 is built for the hydrostatic core");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
@@ -1119,9 +1118,12 @@ struct rcmdyn_engine {
                    grid3(ndi_j, ndi_i, 1), grid3(ndi_j, ndi_i, kz)};
     };
     if (phase & TEND_PRE) {
-    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz}, {FK::A1V, kz}, {FK::A1T, kz}, {FK::A1QV, kz},
+    // isladvec = 1: k_sladv forms ud*msfd two points out (the reference exchanges atmx%ud 2
+    // wide, :995-997) and interpolates atm2 qx up to three points out (max(idif, 4), :1073-1075)
+    const int wu = cfg.isladvec == 1 ? 2 : 1, wq = cfg.isladvec == 1 ? 3 : 2;
+    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz}, {FK::A1QV, kz},
          {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2},
-         {FK::A2QV, kz, 2}, {FK::A2QC, kz, 2}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}});
+         {FK::A2QV, kz, wq}, {FK::A2QC, kz, wq}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}});
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
@@ -1151,6 +1153,8 @@ struct rcmdyn_engine {
         HIPCHK(hipMemsetAsync(p, 0, b3, stream));
       for (double* p : {f.wten, f.wdyn}) HIPCHK(hipMemsetAsync(p, 0, b4, stream));
       KLAUNCH(k_nh_uv_adv, q.di1, BLK, 0, stream, g, dc, f);
+      if (cfg.isladvec == 1)
+        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
       KLAUNCH(k_nh_scalar_adv, q.ci1, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_curvature, q.dik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_adiabatic, q.ci1, BLK, 0, stream, g, dc, f);

@@ -77,7 +77,7 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  terms (mass divergence, td, tvfac, the log ratios of the hypsometric equation) into LDS,
 //  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
 //  geopotential recurrence, each in the reference's sequential order.
-__global__ __launch_bounds__(512, 6) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+__global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxb) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   PT_DECL
@@ -1152,7 +1152,7 @@ __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFi
 // reference's order.  Blocks [nproj, nproj + 2 kz) run the serial negative-moisture sweeps
 // (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
-__global__ __launch_bounds__(512, 6) void k_split_project(
+__global__ __launch_bounds__(512, 5) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,

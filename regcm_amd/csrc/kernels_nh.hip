@@ -281,8 +281,11 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
     avg(k, u1, u2, v1, v2);
     F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
     F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + hadv_fg(g, c, f.xt, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
-    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2);
-    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    // hadvqv/hadvqx, or the semi-Lagrangian start of qxdyn from k_sladv (isladvec = 1)
+    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + (c->isladvec ? F3(f.slqv, j, i, k)
+                                                   : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
+    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + (c->isladvec ? F3(f.slqc, j, i, k)
+                                                   : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
     if (k >= 2) {                                  // hadv3d ind = 1, :486-507
       const double t1 = c->twt1[k], t2 = c->twt2[k];
       const double uaz1 = (t1 * u1 + t2 * pu1), uaz2 = (t1 * u2 + t2 * pu2);

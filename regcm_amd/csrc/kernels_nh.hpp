@@ -31,6 +31,8 @@ struct NHFields {
   double *ppten, *ppdyn, *wten, *wdyn;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy, *ppphy, *wphy;
+  // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv; null otherwise)
+  const double *slqv, *slqc;
   // forecasts (atmc) and fixed moisture
   double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
   int* depplane;

@@ -117,7 +117,7 @@ def test_nh_rest_state():
         assert np.abs(e.get(n)[:, :-1, :-1] / ps).max() < lim, n
 
 
-NH_VARIANTS = [{"iboudy": 4}, {"idiffu": 2}, {"ifupr": 0}, {"ifrayd": 0}]
+NH_VARIANTS = [{"iboudy": 4}, {"idiffu": 2}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1}]
 
 
 @pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))

@@ -319,3 +319,22 @@ def test_oracle_bdyin_matches_numpy_restatement(c1_data):
         assert np.array_equal(o.get(f + "_B0"), b0[n]), f
         assert np.array_equal(o.get(f + "_BT"), (b1[n] - b0[n]) * rdt), f
     assert o.get_time()[2] == 0.0
+
+
+def test_nh_oracle_sladvection_changes_moisture():
+    """isladvec = 1 on the non-hydrostatic core: the semi-Lagrangian qv/qc advection replaces
+    the flux form (Main/mod_tendency.F90:1361-1380), stays finite, and changes only moisture
+    in the first step (temperature and winds see qv only through later steps)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    rc, data, base = _nh_oracle()
+    o = OracleCore(dataclasses.replace(rc, isladvec=1), data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    base.step(1)
+    o.step(1)
+    assert np.isfinite(o.get("ATM1_QV")).all()
+    assert not np.array_equal(o.get("ATM1_QV"), base.get("ATM1_QV"))
+    assert np.array_equal(o.get("ATM1_U"), base.get("ATM1_U"))
+    o.step(2)
+    assert np.isfinite(o.get("ATM1_T")).all() and np.isfinite(o.get("ATM1_PP")).all()
