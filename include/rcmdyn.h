@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RCMDYN_ABI_VERSION 3
+#define RCMDYN_ABI_VERSION 4
 #define RCMDYN_MAXKZ 64
 #define RCMDYN_MAXSPLIT 4
 
@@ -109,9 +109,16 @@ typedef struct rcmdyn_config {
    * Main/mod_slice.F90:336-337) [rhmin 0.01, rhmax 1.01] */
   double rhmin, rhmax;
   /* physicsparam isladvec [0] (1 = semi-Lagrangian horizontal advection of the moisture,
-   * Main/mod_sladvection.F90, hydrostatic core) and iqmsl [1] (its quasi-monotone limiter),
+   * Main/mod_sladvection.F90, both cores) and iqmsl [1] (its quasi-monotone limiter),
    * Main/mod_params.F90:100, 243-244 */
   int32_t isladvec, iqmsl;
+  /* physicsparam ibltyp [1]: 2 = UW PBL, whose TKE the dyn step advects, diffuses, forecasts
+   * and filters (Main/mod_tendency.F90:515-544, 1414-1425, 1545-1548) and bounds
+   * (Main/mod_bdycod.F90:1166-1306, 2415-2530); uwparam nuk [5] (its diffusion factor,
+   * Main/mod_params.F90:480); tkemin (uwtkemin = 1e-3, Main/pbllib/mod_pbl_uwtcm.F90:86,
+   * Main/mod_pbl_interface.F90:68) */
+  int32_t ibltyp, tke_reserved;
+  double nuk, tkemin;
 } rcmdyn_config;
 
 /* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */
@@ -168,6 +175,10 @@ enum rcmdyn_field {
    * u, v (:399). */
   RCMDYN_XUB_B1, RCMDYN_XVB_B1, RCMDYN_XTB_B1, RCMDYN_XQB_B1, RCMDYN_XPSB_B1, RCMDYN_XPPB_B1,
   RCMDYN_XWWB_B1, RCMDYN_ATM0_PSDOT,
+  /* UW PBL turbulent kinetic energy (ibltyp = 2): atm1/atm2 tke, decoupled (m2/s2), kz+1
+   * levels (Main/mod_atm_interface.F90), and the pc_physic tendency the UW scheme produces
+   * (put, like the *PHY fields; added to the advective tendency, :530-531) */
+  RCMDYN_ATM1_TKE, RCMDYN_ATM2_TKE, RCMDYN_TKEPHY,
   RCMDYN_NFIELDS
 };
 

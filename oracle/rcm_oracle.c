@@ -123,6 +123,8 @@ struct orc {
   /* physics coupling seam: pc_physic tendencies t, qv, qc, u, v, pp, w and the atms export
    * (rcmdyn_field TPHY.. and ATMS_UBX3D.. order) */
   double *phy[7], *atms[22];
+  /* UW PBL TKE (ibltyp = 2): atm1/atm2 tke, atmc%tke, tkedyn, tkeps, the pc_physic tendency */
+  double *a1tke, *a2tke, *ctke, *tkedyn, *tkeps, *tkephy;
   /* bdyin: raw record (u, v, t, qv, ps, pp, w), coupled b1 (same order), NH atm0%psdot */
   double *bin[7], *bb1[7], *psdot0;
   double rhmin, rhmax;
@@ -392,6 +394,11 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
     o->estore = alloc3(o, 1); o->astore = alloc3(o, 1); o->wpval = alloc3(o, 1);
   }
   for (int q = 0; q < 5; q++) o->phy[q] = alloc3(o, kz);
+  if (cfg->ibltyp == 2) {
+    o->a1tke = alloc3(o, kp); o->a2tke = alloc3(o, kp); o->ctke = alloc3(o, kp);
+    o->tkedyn = alloc3(o, kp); o->tkeps = alloc3(o, kp); o->tkephy = alloc3(o, kp);
+    if (!o->nh) o->xkcf = alloc3(o, kp);
+  }
   if (o->nh) { o->phy[5] = alloc3(o, kz); o->phy[6] = alloc3(o, kp); }
   for (int q = 0; q < 22; q++) o->atms[q] = alloc3(o, atms_levels(q, kz));
   for (int q = 0; q < 4; q++) { o->bin[q] = alloc3(o, kz); o->bb1[q] = alloc3(o, kz); }
@@ -437,6 +444,8 @@ void orc_destroy(orc_t* o) {
     &o->estore, &o->astore, &o->wpval};
   for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
   for (int q = 0; q < 7; q++) free(o->phy[q]);
+  free(o->a1tke); free(o->a2tke); free(o->ctke); free(o->tkedyn); free(o->tkeps); free(o->tkephy);
+  /* xkcf (also allocated for the hydrostatic core with ibltyp = 2) is in the list above */
   for (int q = 0; q < 22; q++) free(o->atms[q]);
   for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
   free(o->psdot0);
@@ -485,6 +494,10 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     return o->bin[f - RCMDYN_XUB_B1];
   }
   if (f == RCMDYN_ATM0_PSDOT) { *nk = 1; return o->psdot0; }
+  if (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) {
+    *nk = o->kz + 1;
+    return f == RCMDYN_ATM1_TKE ? o->a1tke : f == RCMDYN_ATM2_TKE ? o->a2tke : o->tkephy;
+  }
   switch (f) {
     case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
     case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
@@ -745,6 +758,9 @@ static void decouple(orc_t* o) {
       }
   /* atm1%pr/rho (:1037-1040) and atm2%pr (:1094-1096) feed only physics: skipped */
   xch(o, o->a2u, kz, 2, 0); xch(o, o->a2v, kz, 2, 0); xch(o, o->a2t, kz, 2, 0);
+  if (o->cfg.ibltyp == 2) {                                      /* :871, 1079 */
+    xch(o, o->a1tke, kz + 1, 1, 0); xch(o, o->a2tke, kz + 1, 2, 0);
+  }
   {                                                              /* :1073-1077 */
     int w = o->cfg.isladvec == 1 ? 4 : 2;
     xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
@@ -1010,6 +1026,17 @@ static void calc_coeff(orc_t* o) {
       for (int j = o->jdi1; j <= o->jdi2; j++)
         A3(o->xkd, j, i, k) = d_rfour * (A3(o->xkc, j, i, k) + A3(o->xkc, j - 1, i - 1, k) +
                                          A3(o->xkc, j - 1, i, k) + A3(o->xkc, j, i - 1, k));
+  if (o->cfg.ibltyp == 2) {                   /* xkcf, Main/mod_diffusion.F90:232-235, 245 */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->xkcf, j, i, 1) = A3(o->xkc, j, i, 1);
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) A3(o->xkcf, j, i, k + 1) = A3(o->xkc, j, i, k);
+    for (int k = 1; k <= kz + 1; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->xkcf, j, i, k) = A3(o->xkcf, j, i, k) * o->rdxsq * A2(o->psb, j, i);
+  }
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
@@ -2159,12 +2186,12 @@ static void nh_sponge3d(orc_t* o, const double* bt, double* ften, int nk) {
 }
 
 /* diffu_x3d / diffu_x3df on nk levels with coefficient xk (Main/mod_diffusion.F90:523-790) */
-static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* xk, int nk) {
+static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* xk, int nk, double fac) {
   if (o->cfg.idiffu == 2) {
     for (int k = 1; k <= nk; k++)
       for (int i = o->ici1; i <= o->ici2; i++)
         for (int j = o->jci1; j <= o->jci2; j++)
-          A3(ften, j, i, k) = A3(ften, j, i, k) + d_one * A3(xk, j, i, k) *
+          A3(ften, j, i, k) = A3(ften, j, i, k) + fac * A3(xk, j, i, k) *
               (o4_c1 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
                o4_c2 * (A3(f, j + 1, i + 1, k) + A3(f, j - 1, i - 1, k) + A3(f, j - 1, i + 1, k) + A3(f, j + 1, i - 1, k)) +
                o4_c3 * A3(f, j, i, k));
@@ -2173,12 +2200,12 @@ static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* x
   for (int k = 1; k <= nk; k++)
     for (int i = o->icii1; i <= o->icii2; i++)
       for (int j = o->jcii1; j <= o->jcii2; j++)
-        A3(ften, j, i, k) = A3(ften, j, i, k) - d_one * A3(xk, j, i, k) *
+        A3(ften, j, i, k) = A3(ften, j, i, k) - fac * A3(xk, j, i, k) *
             (z4_c1 * (A3(f, j + 2, i, k) + A3(f, j - 2, i, k) + A3(f, j, i + 2, k) + A3(f, j, i - 2, k)) +
              z4_c2 * (A3(f, j + 1, i, k) + A3(f, j - 1, i, k) + A3(f, j, i + 1, k) + A3(f, j, i - 1, k)) +
              z4_c3 * A3(f, j, i, k));
 #define LAP2(J, I) \
-  A3(ften, J, I, k) = A3(ften, J, I, k) + d_one * A3(xk, J, I, k) * \
+  A3(ften, J, I, k) = A3(ften, J, I, k) + fac * A3(xk, J, I, k) * \
       (z4_c1 * (A3(f, (J) + 1, I, k) + A3(f, (J) - 1, I, k) + A3(f, J, (I) + 1, k) + A3(f, J, (I) - 1, k)) + \
        z4_c2 * A3(f, J, I, k))
   if (o->bl) for (int k = 1; k <= nk; k++) for (int i = o->ici1; i <= o->ici2; i++) LAP2(o->jci1, i);
@@ -2588,6 +2615,36 @@ static int nh_sound(orc_t* o) {
 }
 
 /* tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2) */
+/* UW PBL TKE in tend (ibltyp = 2), both cores: hadv3d ind = 1 of atm1%tke and vadv3d of
+ * tke*p* (Main/mod_tendency.F90:1414-1425, at the end of advection, with its uavg and the
+ * start-of-step p*), diffu_x3df with nuk (:1545-1548), then tketen, the forecast with the
+ * tkemin floor and filter_ra_3d (:515-544).  Nothing else in tend reads or writes the TKE, and
+ * its inputs are unchanged between those points, so the three parts run here in sequence. */
+static void tke_tend(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  memset(o->tkedyn, 0, sizeof(double) * o->plane * kp);
+  nh_hadv3d_w(o, o->a1tke, o->tkedyn);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) A3(o->tkeps, j, i, k) = A3(o->a1tke, j, i, k) * A2(o->psa, j, i);
+  nh_vadv3d_lin(o, o->tkeps, o->tkedyn, 1);
+  nh_diffu_xk(o, o->tkedyn, o->a2tke, o->xkcf, kp, o->cfg.nuk);
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double ten = (d_zero + A3(o->tkedyn, j, i, k) * A2(o->rpsa, j, i)) + A3(o->tkephy, j, i, k);
+        double v = A3(o->a2tke, j, i, k) + o->dt * ten;
+        A3(o->ctke, j, i, k) = (v > o->cfg.tkemin) ? v : o->cfg.tkemin;
+      }
+  for (int k = 1; k <= kp; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double d = o->cfg.gnu2 * (A3(o->ctke, j, i, k) + A3(o->a2tke, j, i, k) - d_two * A3(o->a1tke, j, i, k));
+        A3(o->a2tke, j, i, k) = A3(o->a1tke, j, i, k) + d;
+        A3(o->a1tke, j, i, k) = A3(o->ctke, j, i, k);
+      }
+}
+
 static int nh_tend(orc_t* o) {
   int kz = o->kz, kp = kz + 1;
   size_t n3 = o->plane * (size_t)kz, n3p = o->plane * (size_t)kp;
@@ -2604,6 +2661,7 @@ static int nh_tend(orc_t* o) {
   memset(o->ppten, 0, n3 * 8); memset(o->ppdyn, 0, n3 * 8);
   memset(o->wten, 0, n3p * 8); memset(o->wdyn, 0, n3p * 8);
   int slbad = nh_advection(o);
+  if (o->cfg.ibltyp == 2) tke_tend(o);
   nh_curvature(o);
   nh_adiabatic(o);
   /* boundary (:1462-1501) */
@@ -2621,8 +2679,8 @@ static int nh_tend(orc_t* o) {
   diffu_x(o, o->tdyn, o->tb3d, d_one);
   diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
   diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
-  nh_diffu_xk(o, o->ppdyn, o->ppb3d, o->xkc, kz);
-  nh_diffu_xk(o, o->wdyn, o->wb3d, o->xkcf, kp);
+  nh_diffu_xk(o, o->ppdyn, o->ppb3d, o->xkc, kz, d_one);
+  nh_diffu_xk(o, o->wdyn, o->wb3d, o->xkcf, kp, d_one);
   /* sums (:285-314, 332-335) with the host's pc_physic tendencies (phy, 0 unless put) */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
@@ -2753,6 +2811,7 @@ int orc_tend(orc_t* o) {
   memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
   for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
   int slbad = advection(o);
+  if (o->cfg.ibltyp == 2) tke_tend(o);
   curvature(o);
   adiabatic(o);
   boundary(o);
@@ -2981,6 +3040,63 @@ void orc_bdyin(orc_t* o) {
   }
 }
 
+/* bdyval for the UW TKE (ibltyp = 2): atm2 = atm1 on the boundary lines while integrating
+ * (Main/mod_bdycod.F90:1166-1306, done first in bdyval), then tkemin on every line at the
+ * start, else (bdyflow) tkemin at k = 1 and, for k+1 = 3..kz+1, tkemin at inflow and the first
+ * interior value at outflow (:2415-2509; level 2 is left as it is, as written) */
+static void bdyval_tke(orc_t* o) {
+  int kz = o->kz, kp = kz + 1;
+  double tmin = o->cfg.tkemin;
+  double *t1 = o->a1tke, *t2 = o->a2tke;
+  if (o->lcount > 0) {
+    if (o->bl) for (int k = 1; k <= kp; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(t2, o->jce1, i, k) = A3(t1, o->jce1, i, k);
+    if (o->br) for (int k = 1; k <= kp; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(t2, o->jce2, i, k) = A3(t1, o->jce2, i, k);
+    if (o->bb) for (int k = 1; k <= kp; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(t2, j, o->ice1, k) = A3(t1, j, o->ice1, k);
+    if (o->bt) for (int k = 1; k <= kp; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(t2, j, o->ice2, k) = A3(t1, j, o->ice2, k);
+  }
+  if (o->lcount == 0) {
+    for (int k = 1; k <= kp; k++) {
+      if (o->bl) for (int i = o->ice1; i <= o->ice2; i++) { A3(t1, o->jce1, i, k) = tmin; A3(t2, o->jce1, i, k) = tmin; }
+      if (o->br) for (int i = o->ice1; i <= o->ice2; i++) { A3(t1, o->jce2, i, k) = tmin; A3(t2, o->jce2, i, k) = tmin; }
+      if (o->bt) for (int j = o->jce1; j <= o->jce2; j++) { A3(t1, j, o->ice2, k) = tmin; A3(t2, j, o->ice2, k) = tmin; }
+      if (o->bb) for (int j = o->jce1; j <= o->jce2; j++) { A3(t1, j, o->ice1, k) = tmin; A3(t2, j, o->ice1, k) = tmin; }
+    }
+    return;
+  }
+  if (o->bl) {
+    for (int i = o->ice1; i <= o->ice2; i++) { A3(t1, o->jce1, i, 1) = tmin; A3(t2, o->jce1, i, 1) = tmin; }
+    for (int k = 2; k <= kz; k++) for (int i = o->ice1; i <= o->ice2; i++) {
+      double tint = A3(t1, o->jci1, i, k + 1);
+      double w = SI(o->wue, i, k) + SI(o->wue, i + 1, k) + SI(o->wui, i, k) + SI(o->wui, i + 1, k) +
+                 SI(o->wue, i, k - 1) + SI(o->wue, i + 1, k - 1) + SI(o->wui, i, k - 1) + SI(o->wui, i + 1, k - 1);
+      A3(t1, o->jce1, i, k + 1) = (w > d_zero) ? tmin : tint; }
+  }
+  if (o->br) {
+    for (int i = o->ice1; i <= o->ice2; i++) { A3(t1, o->jce2, i, 1) = tmin; A3(t2, o->jce2, i, 1) = tmin; }
+    for (int k = 2; k <= kz; k++) for (int i = o->ice1; i <= o->ice2; i++) {
+      double tint = A3(t1, o->jci2, i, k + 1);
+      double w = SI(o->eue, i, k) + SI(o->eue, i + 1, k) + SI(o->eui, i, k) + SI(o->eui, i + 1, k) +
+                 SI(o->eue, i, k - 1) + SI(o->eue, i + 1, k - 1) + SI(o->eui, i, k - 1) + SI(o->eui, i + 1, k - 1);
+      A3(t1, o->jce2, i, k + 1) = (w < d_zero) ? tmin : tint; }
+  }
+  if (o->bb) {
+    for (int j = o->jce1; j <= o->jce2; j++) { A3(t1, j, o->ice1, 1) = tmin; A3(t2, j, o->ice1, 1) = tmin; }
+    for (int k = 2; k <= kz; k++) for (int j = o->jci1; j <= o->jci2; j++) {
+      double tint = A3(t1, j, o->ici1, k + 1);
+      double w = SJ(o->sve, j, k) + SJ(o->sve, j + 1, k) + SJ(o->svi, j, k) + SJ(o->svi, j + 1, k) +
+                 SJ(o->sve, j, k - 1) + SJ(o->sve, j + 1, k - 1) + SJ(o->svi, j, k - 1) + SJ(o->svi, j + 1, k - 1);
+      A3(t1, j, o->ice1, k + 1) = (w > d_zero) ? tmin : tint; }
+  }
+  if (o->bt) {
+    for (int j = o->jce1; j <= o->jce2; j++) { A3(t1, j, o->ice2, 1) = tmin; A3(t2, j, o->ice2, 1) = tmin; }
+    for (int k = 2; k <= kz; k++) for (int j = o->jci1; j <= o->jci2; j++) {
+      double tint = A3(t1, j, o->ici2, k + 1);
+      double w = SJ(o->nve, j, k) + SJ(o->nve, j + 1, k) + SJ(o->nvi, j, k) + SJ(o->nvi, j + 1, k) +
+                 SJ(o->nve, j, k - 1) + SJ(o->nve, j + 1, k - 1) + SJ(o->nvi, j, k - 1) + SJ(o->nvi, j + 1, k - 1);
+      A3(t1, j, o->ice2, k + 1) = (w < d_zero) ? tmin : tint; }
+  }
+}
+
 void orc_bdyval(orc_t* o) {
   int kz = o->kz;
   double xt = o->xbctime + o->dt;
@@ -3126,6 +3242,7 @@ void orc_bdyval(orc_t* o) {
       double w = SJ(o->nve, j, k) + SJ(o->nve, j + 1, k) + SJ(o->nvi, j, k) + SJ(o->nvi, j + 1, k);
       A3(q, j, o->ice2, k) = (w < d_zero) ? d_zero : qxint * A2(o->psa, j, o->ice2); }
   }
+  if (o->cfg.ibltyp == 2) bdyval_tke(o);
   o->xbctime = o->xbctime + o->dtsec;                               /* :2566 */
 }
 

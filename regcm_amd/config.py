@@ -17,7 +17,7 @@ import numpy as np
 
 MAXKZ = 64
 MAXSPLIT = 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # Share/mod_sigma.F90:88-152 -- the hard-coded sigma tables (data, cited).
 SIGMA_TABLES = {
@@ -74,6 +74,8 @@ class RcmdynConfig(ctypes.Structure):
         ("nh_dtsmax", ctypes.c_double), ("nh_xmsf", ctypes.c_double),
         ("rhmin", ctypes.c_double), ("rhmax", ctypes.c_double),
         ("isladvec", ctypes.c_int32), ("iqmsl", ctypes.c_int32),
+        ("ibltyp", ctypes.c_int32), ("tke_reserved", ctypes.c_int32),
+        ("nuk", ctypes.c_double), ("tkemin", ctypes.c_double),
     ]
 
 
@@ -95,13 +97,16 @@ FIELD_NAMES = [
     "ATMS_TV3D", "ATMS_PB3D", "ATMS_PF3D", "ATMS_PS2D", "ATMS_RHOX2D", "ATMS_TH3D", "ATMS_RHOB3D",
     "ATMS_TP3D", "ATMS_WPX3D", "ATMS_WB3D", "ATMS_ZQ", "ATMS_ZA", "ATMS_DZQ", "ATMS_QSB3D", "ATMS_RHB3D",
     "XUB_B1", "XVB_B1", "XTB_B1", "XQB_B1", "XPSB_B1", "XPPB_B1", "XWWB_B1", "ATM0_PSDOT",
+    "ATM1_TKE", "ATM2_TKE", "TKEPHY",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
          "PTEN", "PSDOTA", "ATM0_PS", "DPSDXM", "DPSDYM", "EF", "DDX", "DDY", "DMDX", "DMDY",
          "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D", "XPSB_B1", "ATM0_PSDOT"}
 FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM0_RHOF",
-               "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ", "XWWB_B1"}
+               "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ", "XWWB_B1",
+               "ATM1_TKE", "ATM2_TKE", "TKEPHY"}
+TKE_STATE_FIELDS = ["ATM1_TKE", "ATM2_TKE"]
 # physics coupling seam: pc_physic tendencies (put) and the mkslice export (get)
 PHY_FIELDS = ["TPHY", "QVPHY", "QCPHY", "UPHY", "VPHY"]
 NH_PHY_FIELDS = ["PPPHY", "WPHY"]
@@ -173,6 +178,9 @@ class RunConfig:
     rhmax: float = 1.01
     isladvec: int = 0                # physicsparam, Main/mod_params.F90:243-244
     iqmsl: int = 1
+    ibltyp: int = 1                  # physicsparam; 2 = UW PBL (TKE advected by the dyn step)
+    nuk: float = 5.0                 # uwparam, Main/mod_params.F90:480
+    tkemin: float = 1.0e-3           # uwtkemin, Main/pbllib/mod_pbl_uwtcm.F90:86
     nhbet: float = 0.4
     nhxkd: float = 0.1
     base_state_pressure: float = 101325.0
@@ -268,6 +276,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.nhbet, c.nhxkd, c.rayalpha0, c.rayhd = rc.nhbet, rc.nhxkd, rc.rayalpha0, rc.rayhd
     c.rhmin, c.rhmax = rc.rhmin, rc.rhmax
     c.isladvec, c.iqmsl = rc.isladvec, rc.iqmsl
+    c.ibltyp, c.nuk, c.tkemin = rc.ibltyp, rc.nuk, rc.tkemin
     if rc.idynamic == 2:
         c.nh_dtsmax = split["nh_dtsmax"]
         c.nh_xmsf = split["nh_xmsf"]

@@ -26,6 +26,7 @@
 #include "kernels_nh.hpp"
 #include "slice.hpp"
 #include "bdyin.hpp"
+#include "tke.hpp"
 
 using namespace rcm;
 
@@ -202,7 +203,9 @@ enum class FK {
   // device bdyin: coupled boundary data at the interval end
   UB1, VB1, TB1, QB1, PB1, PPB1, WWB1,
   // semi-Lagrangian moisture tendency starts
-  SLQV, SLQC
+  SLQV, SLQC,
+  // UW PBL TKE (ibltyp = 2)
+  A1TKE, A2TKE
 };
 
 struct rcmdyn_engine {
@@ -312,9 +315,10 @@ struct rcmdyn_engine {
       c.rayalpha0 = cfg.rayalpha0; c.rayhd = cfg.rayhd; c.nhbet = cfg.nhbet; c.nhxkd = cfg.nhxkd;
       c.nh_dtsmax = cfg.nh_dtsmax; c.nh_xmsf = cfg.nh_xmsf;
       c.xgamma = 1.0 / (1.0 - c.rgas * (1.0 / c.cpd));           // Main/mod_sound.F90:77
-      c.dds[1] = 0.0; c.dds[kz + 1] = 0.0;                          // Main/mod_advection.F90:101-105
-      for (int k = 2; k <= kz; k++) c.dds[k] = 1.0 / (c.dsigma[k] + c.dsigma[k - 1]);
     }
+    c.dds[1] = 0.0; c.dds[kz + 1] = 0.0;                            // Main/mod_advection.F90:101-105
+    for (int k = 2; k <= kz; k++) c.dds[k] = 1.0 / (c.dsigma[k] + c.dsigma[k - 1]);
+    c.ibltyp = cfg.ibltyp; c.nuk = cfg.nuk; c.tkemin = cfg.tkemin;
   }
 
   double* dalloc(Tile& t, size_t n) {
@@ -366,6 +370,9 @@ struct rcmdyn_engine {
     t.qdot = dalloc(t, P * (kz + 1));
     t.phi = dalloc(t, P3);
     if (cfg.isladvec == 1) { t.slqv = dalloc(t, P3); t.slqc = dalloc(t, P3); }
+    if (cfg.ibltyp == 2) {
+      t.a1tke = dalloc(t, P * (kz + 1)); t.a2tke = dalloc(t, P * (kz + 1)); t.ctke = dalloc(t, P * (kz + 1));
+    }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     t.depplane = talloc<int>(t, 2 * kz);
     t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
@@ -439,6 +446,36 @@ struct rcmdyn_engine {
     nhf.push_back(f);
   }
 
+  TkeArgs tke_args(Tile& t) {
+    const int c = t.cur;
+    TkeArgs a{};
+    a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.msfd = t.msfd; a.xmsf = t.xmsf; a.psa = t.psa_[c]; a.rpsa = t.rpsa;
+    a.qdot = t.qdot; a.tkephy = t.tkephy; a.a1tke = t.a1tke; a.a2tke = t.a2tke; a.ctke = t.ctke;
+    if (cfg.idynamic == 2) { a.xk = nhf[&t - tiles.data()].xkcf; a.xk_half = 0; }
+    else { a.xk = t.xkcs; a.xk_half = 1; }
+    return a;
+  }
+  // the TKE forecast and filter of tend (Main/mod_tendency.F90:515-544), after the kernels
+  // that produce qdot and the diffusion coefficients
+  void tke_step() {
+    if (cfg.ibltyp != 2) return;
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const dim3 grid = grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, cfg.kz + 1);
+      KLAUNCH(k_tke_tend, grid, BLK, 0, stream, g, dc, ds, tke_args(t));
+      KLAUNCH(k_tke_filter, grid, BLK, 0, stream, g, dc, tke_args(t));
+    });
+  }
+  // the TKE boundary lines of bdyval, once the boundary-wind slices are current
+  void tke_bdyval() {
+    if (cfg.ibltyp != 2) return;
+    each([&](Tile& t) {
+      Slices sl;
+      for (int q = 0; q < 16; q++) sl.s[q] = t.sl[q];
+      KLAUNCH(k_bdyval_tke, dim3(cfg.kz + 1), dim3(256), 0, stream, t.g, dc, ds, tke_args(t), sl, slen);
+    });
+  }
+
   NHFields nhfields(Tile& t) {
     NHFields f = nhf[&t - tiles.data()];
     const int c = t.cur;
@@ -470,6 +507,8 @@ struct rcmdyn_engine {
     if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
+    if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
+      throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
@@ -554,6 +593,7 @@ struct rcmdyn_engine {
       case FK::QB1: return t.bb1[3]; case FK::PB1: return t.bb1[4]; case FK::PPB1: return t.bb1[5];
       case FK::WWB1: return t.bb1[6];
       case FK::SLQV: return t.slqv; case FK::SLQC: return t.slqc;
+      case FK::A1TKE: return t.a1tke; case FK::A2TKE: return t.a2tke;
       default: break;
     }
     const NHFields& h = nhf[&t - tiles.data()];
@@ -590,6 +630,10 @@ struct rcmdyn_engine {
       return t.bin[f - RCMDYN_XUB_B1];
     }
     if (f == RCMDYN_ATM0_PSDOT) { nk = 1; return t.psdot0; }
+    if (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) {
+      nk = cfg.kz + 1;
+      return f == RCMDYN_ATM1_TKE ? t.a1tke : f == RCMDYN_ATM2_TKE ? t.a2tke : t.tkephy;
+    }
     if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
       if (cfg.idynamic != 2) return nullptr;
       NHFields& h = nhf[&t - tiles.data()];
@@ -654,8 +698,16 @@ struct rcmdyn_engine {
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
     const bool phyf = f >= RCMDYN_TPHY && f <= RCMDYN_WPHY;
     const bool binf = f >= RCMDYN_XUB_B1 && f <= RCMDYN_ATM0_PSDOT;
-    if (f < 0 || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) || (f > RCMDYN_CRY && !phyf && !binf))
+    const bool tkef = f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY;
+    if (f < 0 || f >= RCMDYN_NFIELDS || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) ||
+        (f > RCMDYN_CRY && !phyf && !binf && !tkef))
       throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
+    if (tkef && cfg.ibltyp != 2) throw std::runtime_error("rcmdyn_put: TKE fields need ibltyp=2 (UW PBL)");
+    if (f == RCMDYN_TKEPHY && !tiles.empty() && !tiles[0].tkephy) {
+      HIPCHK(hipStreamSynchronize(stream));
+      for (auto& t : tiles) t.tkephy = dalloc(t, t.g.plane * (cfg.kz + 1));
+      invalidate_graphs();
+    }
     if (((f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) || f == RCMDYN_PPPHY || f == RCMDYN_WPHY ||
          f == RCMDYN_XPPB_B1 || f == RCMDYN_XWWB_B1 || f == RCMDYN_ATM0_PSDOT) && cfg.idynamic != 2)
       throw std::runtime_error("rcmdyn_put: non-hydrostatic field on a hydrostatic engine");
@@ -792,6 +844,9 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY && !tiles[0].phy[0])
       throw std::runtime_error("rcmdyn_get: no physics tendencies were put");
+    if (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY && cfg.ibltyp != 2)
+      throw std::runtime_error("rcmdyn_get: TKE fields need ibltyp=2 (UW PBL)");
+    if (f == RCMDYN_TKEPHY && !tiles[0].tkephy) throw std::runtime_error("rcmdyn_get: no TKE tendency was put");
     HIPCHK(hipStreamSynchronize(stream));
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
@@ -926,8 +981,10 @@ struct rcmdyn_engine {
   // One exchange point: every field travels in the same per-neighbour message, each with its
   // own width and sides (0 exchange, 1 exchange_lb, 2 exchange_rt).
   void xch(std::initializer_list<XField> fields, int width = 1, int sides = 0) {
+    xchv(std::vector<XField>(fields), width, sides);
+  }
+  void xchv(std::vector<XField> fs, int width = 1, int sides = 0) {
     if (ntiles == 1) return;
-    std::vector<XField> fs(fields);
     for (XField& x : fs) {
       if (x.width == 0) x.width = width;
       if (x.sides < 0) x.sides = sides;
@@ -1078,6 +1135,7 @@ struct rcmdyn_engine {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
       f.omega = t.omega; f.xkcs = t.xkcs;
     }
+    if (cfg.ibltyp == 2) f.xkcs = t.xkcs;     // the TKE diffusion reads xkcf from it
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.red = red; f.red_off = t.red_off;
     return f;
@@ -1121,9 +1179,12 @@ struct rcmdyn_engine {
     // isladvec = 1: k_sladv forms ud*msfd two points out (the reference exchanges atmx%ud 2
     // wide, :995-997) and interpolates atm2 qx up to three points out (max(idif, 4), :1073-1075)
     const int wu = cfg.isladvec == 1 ? 2 : 1, wq = cfg.isladvec == 1 ? 3 : 2;
-    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz}, {FK::A1QV, kz},
-         {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2},
-         {FK::A2QV, kz, wq}, {FK::A2QC, kz, wq}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}});
+    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz},
+                            {FK::A1QV, kz}, {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2},
+                            {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, wq}, {FK::A2QC, kz, wq},
+                            {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}};
+    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro.push_back({FK::A2TKE, kp, 2}); }
+    xchv(pro);
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
@@ -1162,6 +1223,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_diffusion, q.fr, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_forecast, q.fr, BLK, 0, stream, g, dc, ds, f);
     });
+    tke_step();
     xch({{FK::CQV, kz}, {FK::CQC, kz}});
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1249,6 +1311,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
               t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()));
     }
+    tke_bdyval();
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }
 
@@ -1270,9 +1333,12 @@ struct rcmdyn_engine {
     // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
     // atm1 travels 2 wide and atm2 3 wide: one more than the reference's widths, for the
     // ghost rings the kernels below compute in place of the later exchanges
-    xch({{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2}, {FK::A1QV, kz, 2},
-         {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
-         {FK::A2QC, kz, 3}});
+    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2},
+                            {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3},
+                            {FK::A2T, kz, 3}, {FK::A2QV, kz, 3}, {FK::A2QC, kz, 3}};
+    // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
+    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro.push_back({FK::A2TKE, kz + 1, 2}); }
+    xchv(pro);
     ghosts_stale = false;
     // surface_pressures + 2-D reciprocals, :815-834
     each([&](Tile& t) {
@@ -1309,6 +1375,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_scalars, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, kz), dim3(SBT),
               0, stream, g, dc, ds, f);
     });
+    tke_step();
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     each([&](Tile& t) {
@@ -1422,6 +1489,7 @@ struct rcmdyn_engine {
               t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec,
               (int)(q + 1 == tiles.size()));
     }
+    tke_bdyval();
     hs.xbctime = hs.xbctime + cfg.dtsec;
   }
 

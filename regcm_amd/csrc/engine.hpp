@@ -80,6 +80,8 @@ struct Geom {
 struct Consts {
   int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc, ipgf, idiffu;
   int isladvec, iqmsl;                 // semi-Lagrangian moisture advection (physicsparam)
+  int ibltyp, tke_pad;                 // 2: UW PBL TKE advected/diffused/filtered (tke.hip)
+  double nuk, tkemin;
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
   double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;
@@ -131,6 +133,9 @@ struct Tile {
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten;
   double *qdot, *phi;
   double *slqv = nullptr, *slqc = nullptr;   // isladvec = 1: k_sladv output
+  // ibltyp = 2: atm1/atm2 tke (decoupled, kz+1 levels), the forecast atmc%tke, and the UW
+  // scheme's tendency (allocated on its first put)
+  double *a1tke = nullptr, *a2tke = nullptr, *ctke = nullptr, *tkephy = nullptr;
   double *cqv, *cqc, *fqv, *fqc;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;

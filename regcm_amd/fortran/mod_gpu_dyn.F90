@@ -11,7 +11,7 @@ module mod_gpu_dyn
   implicit none
   private
 
-  integer, parameter, public :: rcmdyn_abi_version = 3
+  integer, parameter, public :: rcmdyn_abi_version = 4
   integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
 
   ! field ids (enum rcmdyn_field)
@@ -39,7 +39,8 @@ module mod_gpu_dyn
     f_atms_qsb3d = 95, f_atms_rhb3d = 96, &
     ! device bdyin: the next ICBC record as read_icbc returns it; NH atm0%psdot
     f_xub_b1 = 97, f_xvb_b1 = 98, f_xtb_b1 = 99, f_xqb_b1 = 100, f_xpsb_b1 = 101, &
-    f_xppb_b1 = 102, f_xwwb_b1 = 103, f_atm0_psdot = 104
+    f_xppb_b1 = 102, f_xwwb_b1 = 103, f_atm0_psdot = 104, &
+    f_atm1_tke = 105, f_atm2_tke = 106, f_tkephy = 107
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -70,6 +71,9 @@ module mod_gpu_dyn
     real(c_double) :: rhmin, rhmax
     ! physicsparam isladvec, iqmsl (semi-Lagrangian moisture advection)
     integer(c_int32_t) :: isladvec, iqmsl
+    ! physicsparam ibltyp (2 = UW PBL TKE in the dyn step), uwparam nuk, tkemin (uwtkemin)
+    integer(c_int32_t) :: ibltyp, tke_reserved
+    real(c_double) :: nuk, tkemin
   end type rcmdyn_config
 
   interface

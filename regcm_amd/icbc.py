@@ -293,3 +293,22 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
     st["DSTOR"] = np.zeros((rc.nsplit, iy, jx))
     st["HSTOR"] = np.zeros((rc.nsplit, iy, jx))
     return dict(state=st, split=split)
+
+
+def tke_state(rc: RunConfig, seed: int = SEED) -> dict:
+    """Synthetic UW-PBL turbulent kinetic energy (ibltyp = 2): atm1/atm2 tke on the kz+1 full
+    sigma levels (decoupled, m2/s2), a boundary-layer profile of up to ~1.5 m2/s2 decaying
+    above sigma ~0.8, with cell-to-cell noise, floored at tkemin; zero on the dot row/column
+    jx, iy like every cross-point field."""
+    rng = np.random.Generator(np.random.PCG64(seed + 17))
+    jx, iy, kz = rc.jx, rc.iy, rc.kz
+    sig = np.asarray(rc.sigma, dtype=np.float64)[:, None, None]          # k = 1 (top) .. kz+1
+    prof = 1.5 * np.exp(-(1.0 - sig) / 0.08)
+    out = {}
+    for n, name in enumerate(("ATM1_TKE", "ATM2_TKE")):
+        t = prof * (1.0 + 0.3 * rng.standard_normal((kz + 1, iy, jx))) + 0.02 * n
+        t = np.maximum(t, rc.tkemin)
+        t[:, iy - 1, :] = 0.0
+        t[:, :, jx - 1] = 0.0
+        out[name] = t
+    return out

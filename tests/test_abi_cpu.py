@@ -46,7 +46,8 @@ int main(void) {
   printf("size %zu\n", sizeof(rcmdyn_config));
   O(jx); O(present_qc); O(ds); O(dtbdys); O(sigma); O(zmatx); O(zmatxr); O(am); O(tau);
   O(varpa1); O(an); O(hbar); O(aam); O(dtau); O(sigmah); O(pd); O(comm_rank); O(device);
-  O(comm_unique_id); O(nh_dtsmax); O(rhmin); O(rhmax); O(isladvec); O(iqmsl);
+  O(comm_unique_id); O(nh_dtsmax); O(rhmin); O(rhmax); O(isladvec); O(iqmsl); O(ibltyp); O(nuk);
+  O(tkemin);
   return 0;
 }
 """

@@ -338,3 +338,28 @@ def test_nh_oracle_sladvection_changes_moisture():
     assert np.array_equal(o.get("ATM1_U"), base.get("ATM1_U"))
     o.step(2)
     assert np.isfinite(o.get("ATM1_T")).all() and np.isfinite(o.get("ATM1_PP")).all()
+
+
+def test_oracle_tke_bounds_and_independence(c1_data):
+    """ibltyp = 2: the oracle's TKE stays finite and >= tkemin on every cross point it owns,
+    its boundary lines follow bdyval's inflow/outflow rule (tkemin at level 1), and the rest of
+    the state is bit-identical to the run without TKE (nothing in the dyn step reads it)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    rc0, data = c1_data
+    rc = dataclasses.replace(rc0, ibltyp=2)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    for name, a in icbc.tke_state(rc).items():
+        o.put(name, a)
+    o.bdyval()
+    b = OracleCore(rc0, data["split"])
+    b.put_state(data["state"])
+    b.bdyval()
+    o.step(4)
+    b.step(4)
+    t = o.get("ATM1_TKE")[:, : rc.iy - 1, : rc.jx - 1]
+    assert np.isfinite(t).all() and t.min() >= rc.tkemin
+    assert np.all(t[0, 0, :] == rc.tkemin) and np.all(t[0, :, 0] == rc.tkemin)
+    for name in ("ATM1_U", "ATM1_T", "ATM1_QV", "PSA"):
+        assert np.array_equal(o.get(name), b.get(name)), name
