@@ -1216,7 +1216,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_uv_adv, q.di1, BLK, 0, stream, g, dc, f);
       if (cfg.isladvec == 1)
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
-      KLAUNCH(k_nh_scalar_adv, q.ci1, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_scalar_adv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kp), BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_curvature, q.dik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_adiabatic, q.ci1, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_boundary, q.fr, BLK, 0, stream, g, dc, ds, f);

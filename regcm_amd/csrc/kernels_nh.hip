@@ -260,33 +260,32 @@ __device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const 
   return fg;
 }
 
-// scalar advection of the NH core, one thread per interior cross column (advection driver
-// Main/mod_tendency.F90:1308-1392): pp (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 +
-// vadv3d ind 0 on full levels), t (hadvt + vadv3d ind 1 NH form), qv (hadvqv + vadvqv),
-// qc (hadvqx + vadv4d ind 1)
+// scalar advection of the NH core (advection driver Main/mod_tendency.F90:1308-1392): pp
+// (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 + vadv3d ind 0 on full levels), t (hadvt +
+// vadv3d ind 1 NH form), qv (hadvqv + vadvqv), qc (hadvqx + vadv4d ind 1).  One thread per
+// interior cross point and level k = 1..kz+1 (w alone on kz+1): every element is written once,
+// with the reference's order of accumulation -- 0, the horizontal term, then the vertical flux
+// through its upper interface (the reference's loop iteration k, added) and through its lower
+// one (iteration k+1, subtracted).  An interface flux is formed by both levels it bounds, with
+// the same expression, so the values are those of the reference's k loops.
 __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
-  auto avg = [&](int k, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
-    u1 = F3(f.umc, j, i + 1, k) + F3(f.umc, j, i, k);
-    u2 = F3(f.umc, j + 1, i + 1, k) + F3(f.umc, j + 1, i, k);
-    v1 = F3(f.vmc, j + 1, i, k) + F3(f.vmc, j, i, k);
-    v2 = F3(f.vmc, j + 1, i + 1, k) + F3(f.vmc, j, i + 1, k);
+  auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
+    u1 = F3(f.umc, j, i + 1, kk) + F3(f.umc, j, i, kk);
+    u2 = F3(f.umc, j + 1, i + 1, kk) + F3(f.umc, j + 1, i, kk);
+    v1 = F3(f.vmc, j + 1, i, kk) + F3(f.vmc, j, i, kk);
+    v2 = F3(f.vmc, j + 1, i + 1, kk) + F3(f.vmc, j, i + 1, kk);
   };
-  double pu1 = 0, pu2 = 0, pv1 = 0, pv2 = 0;
-  for (int k = 1; k <= kz; k++) {
-    double u1, u2, v1, v2;
-    avg(k, u1, u2, v1, v2);
-    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
-    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + hadv_fg(g, c, f.xt, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
-    // hadvqv/hadvqx, or the semi-Lagrangian start of qxdyn from k_sladv (isladvec = 1)
-    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + (c->isladvec ? F3(f.slqv, j, i, k)
-                                                   : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
-    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + (c->isladvec ? F3(f.slqc, j, i, k)
-                                                   : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
-    if (k >= 2) {                                  // hadv3d ind = 1, :486-507
+  // ---- w on full levels k = 1..kz+1
+  {
+    double wd = F3(f.wdyn, j, i, k);
+    if (k >= 2 && k <= kz) {                       // hadv3d ind = 1, :486-507
+      double u1, u2, v1, v2, pu1, pu2, pv1, pv2;
+      avg(k, u1, u2, v1, v2);
+      avg(k - 1, pu1, pu2, pv1, pv2);
       const double t1 = c->twt1[k], t2 = c->twt2[k];
       const double uaz1 = (t1 * u1 + t2 * pu1), uaz2 = (t1 * u2 + t2 * pu2);
       const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
@@ -297,60 +296,71 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
       const double fx2 = (d_one + f1) * F3(w, j, i, k) + (d_one - f1) * F3(w, j + 1, i, k);
       const double fy1 = (d_one + f2) * F3(w, j, i - 1, k) + (d_one - f2) * F3(w, j, i, k);
       const double fy2 = (d_one + f2) * F3(w, j, i, k) + (d_one - f2) * F3(w, j, i + 1, k);
-      F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
+      wd = wd - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
     }
-    pu1 = u1; pu2 = u2; pv1 = v1; pv2 = v2;
+    // vadv3d ind = 0, nk = kz+1 (w), :756-765: flux through the interface below level kk
+    auto wflux = [&](int kk) {
+      const double qq = d_half * (F3(f.qdot, j, i, kk) + F3(f.qdot, j, i, kk + 1));
+      return qq * ((F3(f.a1w, j, i, kk) + F3(f.a1w, j, i, kk + 1)));
+    };
+    if (k >= 2) wd = wd + wflux(k - 1) * c->dds[k];
+    if (k <= kz) wd = wd - wflux(k) * c->dds[k];
+    F3(f.wdyn, j, i, k) = wd;
   }
-  // vadv3d ind = 0, nk = kz (pp), :746-754
-  for (int k = 2; k <= kz; k++) {
-    const double fx = F3(f.qdot, j, i, k) * (c->twt1[k] * F3(f.a1pp, j, i, k) + c->twt2[k] * F3(f.a1pp, j, i, k - 1));
-    F3(f.ppdyn, j, i, k - 1) = F3(f.ppdyn, j, i, k - 1) - fx * c->xds[k - 1];
-    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + fx * c->xds[k];
-  }
-  // vadv3d ind = 0, nk = kz+1 (w), :756-765
-  for (int k = 1; k <= kz; k++) {
-    const double qq = d_half * (F3(f.qdot, j, i, k) + F3(f.qdot, j, i, k + 1));
-    const double fx = qq * ((F3(f.a1w, j, i, k) + F3(f.a1w, j, i, k + 1)));
-    F3(f.wdyn, j, i, k + 1) = F3(f.wdyn, j, i, k + 1) + fx * c->dds[k + 1];
-    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - fx * c->dds[k];
-  }
-  // vadv3d ind = 1, non-hydrostatic form, :784-803
+  if (k > kz) return;
+  double u1, u2, v1, v2;
+  avg(k, u1, u2, v1, v2);
+  // ---- pp: hadv3d ind 0, then vadv3d ind = 0 (nk = kz), :746-754
   {
-    double dq = F3(f.a1t, j, i, 1) * exp(-c->c287 * log(F3(f.pb3d, j, i, 1)));
-    for (int k = 2; k <= kz; k++) {
-      const double rdphf = exp(-c->c287 * log(F3(f.pb3d, j, i, k)));
-      const double rdplf = exp(c->c287 * log(F3(f.pf3d, j, i, k)));
-      const double dk = F3(f.a1t, j, i, k) * rdphf;
-      const double fx = rdplf * F3(f.qdot, j, i, k) * (c->twt1[k] * dk + c->twt2[k] * dq);
-      F3(f.tdyn, j, i, k - 1) = F3(f.tdyn, j, i, k - 1) - fx * c->xds[k - 1];
-      F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + fx * c->xds[k];
-      dq = dk;
-    }
+    double pd = F3(f.ppdyn, j, i, k) + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    auto pflux = [&](int kk) {
+      return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
+    };
+    if (k >= 2) pd = pd + pflux(k) * c->xds[k];
+    if (k + 1 <= kz) pd = pd - pflux(k + 1) * c->xds[k];
+    F3(f.ppdyn, j, i, k) = pd;
   }
-  // vadvqv, :811-836
+  // ---- t: hadvt, then vadv3d ind = 1, non-hydrostatic form, :784-803
   {
+    double td = F3(f.tdyn, j, i, k) + hadv_fg(g, c, f.xt, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
+    auto dkt = [&](int kk) { return F3(f.a1t, j, i, kk) * exp(-c->c287 * log(F3(f.pb3d, j, i, kk))); };
+    auto tflux = [&](int kk) {
+      const double rdplf = exp(c->c287 * log(F3(f.pf3d, j, i, kk)));
+      return rdplf * F3(f.qdot, j, i, kk) * (c->twt1[kk] * dkt(kk) + c->twt2[kk] * dkt(kk - 1));
+    };
+    if (k >= 2) td = td + tflux(k) * c->xds[k];
+    if (k + 1 <= kz) td = td - tflux(k + 1) * c->xds[k];
+    F3(f.tdyn, j, i, k) = td;
+  }
+  // ---- qv: hadvqv (or the semi-Lagrangian start, isladvec = 1), then vadvqv, :811-836
+  {
+    double qd = F3(f.qvdyn, j, i, k) + (c->isladvec ? F3(f.slqv, j, i, k)
+                                                    : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
     const double thr = MINQQ * ps;
-    for (int k = 2; k <= kz; k++) {
-      const double fk = F3(f.a1qv, j, i, k), fkm = F3(f.a1qv, j, i, k - 1);
+    auto qflux = [&](int kk) {
+      const double fk = F3(f.a1qv, j, i, kk), fkm = F3(f.a1qv, j, i, kk - 1);
       double fg = d_zero;
-      if (fk > thr && fkm > thr) fg = fk * rcm_powpos(fkm / fk, c->qcon[k]);
-      const double q = F3(f.qdot, j, i, k);
-      F3(f.qvdyn, j, i, k - 1) = F3(f.qvdyn, j, i, k - 1) - q * fg * c->xds[k - 1];
-      F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + q * fg * c->xds[k];
-    }
+      if (fk > thr && fkm > thr) fg = fk * rcm_powpos(fkm / fk, c->qcon[kk]);
+      return F3(f.qdot, j, i, kk) * fg;
+    };
+    if (k >= 2) qd = qd + qflux(k) * c->xds[k];
+    if (k + 1 <= kz) qd = qd - qflux(k + 1) * c->xds[k];
+    F3(f.qvdyn, j, i, k) = qd;
   }
-  // vadv4d ind = 1 (qc), :873-894, 958-961
+  // ---- qc: hadvqx (or the semi-Lagrangian start), then vadv4d ind = 1, :873-894, 958-961
   {
+    double cd = F3(f.qcdyn, j, i, k) + (c->isladvec ? F3(f.slqc, j, i, k)
+                                                    : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
     const double thr = MINQQ * MINQQ * ps;
-    for (int k = 2; k <= kz; k++) {
-      const double svv = F3(f.qdot, j, i, k);
-      const double fk = F3(f.a1qc, j, i, k), fkm = F3(f.a1qc, j, i, k - 1);
-      double fg;
-      if (svv > d_zero) fg = (fkm > thr) ? svv * (c->twt1[k] * fk + c->twt2[k] * fkm) : d_zero;
-      else fg = (fk > thr) ? svv * (c->twt1[k] * fk + c->twt2[k] * fkm) : d_zero;
-      F3(f.qcdyn, j, i, k - 1) = F3(f.qcdyn, j, i, k - 1) - fg * c->xds[k - 1];
-      F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + fg * c->xds[k];
-    }
+    auto cflux = [&](int kk) {
+      const double svv = F3(f.qdot, j, i, kk);
+      const double fk = F3(f.a1qc, j, i, kk), fkm = F3(f.a1qc, j, i, kk - 1);
+      if (svv > d_zero) return (fkm > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+      return (fk > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+    };
+    if (k >= 2) cd = cd + cflux(k) * c->xds[k];
+    if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
+    F3(f.qcdyn, j, i, k) = cd;
   }
 }
 
