@@ -927,17 +927,33 @@ __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields
   gbuf[n + q] = F3(f.rho1, j, i, 1) * sqrt(ensq);
 }
 
-__global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask) {
+// The two sums stay sequential in the reference's order (one thread adds); the block stages
+// the next TMC terms of both into LDS in parallel, so the adding thread reads LDS instead of
+// waiting on one global load per term.
+constexpr int TMC = 2048;
+__global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restrict__ c,
+                                                  const double* __restrict__ gbuf, double* tmask) {
   __shared__ double sh[2];
+  __shared__ double sA[TMC], sR[TMC];
+  const long n = (long)g.gjx * g.giy;
+  const int nj = g.gjx - 3, ni = g.giy - 3;       // j = 2..gjx-2, i = 2..giy-2
+  const long total = (long)nj * ni;
+  double atot = d_zero, rhontot = d_zero;
+  for (long base = 0; base < total; base += TMC) {
+    const int cnt = (int)((total - base) < TMC ? (total - base) : TMC);
+    for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
+      const long p = base + t;                    // i-major, j-minor: the reference's loop order
+      const int i = 2 + (int)(p / nj), j = 2 + (int)(p % nj);
+      const long q = (long)(i - 1) * g.gjx + (j - 1);
+      sA[t] = gbuf[q];
+      sR[t] = gbuf[n + q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < cnt; t++) { atot = atot + sA[t]; rhontot = rhontot + sR[t]; }
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
-    const long n = (long)g.gjx * g.giy;
-    double atot = d_zero, rhontot = d_zero;
-    for (int i = 2; i <= g.giy - 2; i++)
-      for (int j = 2; j <= g.gjx - 2; j++) {
-        const long q = (long)(i - 1) * g.gjx + (j - 1);
-        atot = atot + gbuf[q];
-        rhontot = rhontot + gbuf[n + q];
-      }
     const double rnpts = d_one / (double)((g.giy - 3) * (g.gjx - 3));
     sh[0] = atot * rnpts;
     sh[1] = rhontot * rnpts;
