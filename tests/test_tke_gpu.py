@@ -149,3 +149,26 @@ def test_tke_errors(c1_data, tke_c1):
     e2 = DynCore(rc2, data["split"])
     with pytest.raises(EngineError, match="no TKE tendency"):
         e2.get("TKEPHY")
+
+
+def test_tke_restart_bit_identical(tke_c1):
+    """SAV restart with the UW TKE (mod_savefile writes atm1/atm2 tke for ibltyp = 2): the
+    continued run equals the uninterrupted one bit for bit, also on another decomposition."""
+    from regcm_amd.dycore import DynCore
+    rc, data = tke_c1
+    ref = start(DynCore(rc, data["split"]), rc, data)
+    ref.step(6)
+    run = start(DynCore(rc, data["split"]), rc, data)
+    run.step(3)
+    names = STATE_FIELDS + TKE_STATE_FIELDS
+    sav = {n: run.get(n) for n in names}
+    clock = run.get_time()
+    run.close()
+    rst = DynCore(rc, data["split"], nproc_j=2, nproc_i=2)
+    rst.put_state(data["state"])                  # statics and boundary data
+    for n, a in sav.items():
+        rst.put(n, a)
+    rst.set_time(*clock)
+    rst.step(3)
+    for n in names:
+        assert np.array_equal(rst.get(n), ref.get(n)), n
