@@ -762,7 +762,9 @@ static void decouple(orc_t* o) {
     xch(o, o->a1tke, kz + 1, 1, 0); xch(o, o->a2tke, kz + 1, 2, 0);
   }
   {                                                              /* :1073-1077 */
-    int w = o->cfg.isladvec == 1 ? 4 : 2;
+    /* the reference exchanges max(idif, 4) for isladvec = 1; the departure stencil reads at
+     * most 3 points out (|xn| < 2, then two more cells), the frame's ghost width */
+    int w = o->cfg.isladvec == 1 ? 3 : 2;
     xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
   }
 }

@@ -38,7 +38,21 @@ def recv_dir(sides, d):
     return d in (1, 3, 7)
 
 
-def _worker(rank, world, cj, ci, port, q):
+def _fields(variant):
+    from regcm_amd.config import TKE_STATE_FIELDS
+    return STATE_FIELDS + (TKE_STATE_FIELDS if variant.get("ibltyp") == 2 else [])
+
+
+def _setup(o, rc, data, variant):
+    from regcm_amd import icbc
+    o.put_state(data["state"])
+    if variant.get("ibltyp") == 2:
+        for name, a in icbc.tke_state(rc).items():
+            o.put(name, a)
+    o.bdyval()
+
+
+def _worker(rank, world, cj, ci, port, q, variant):
     import ctypes
     import torch
     import torch.distributed as dist
@@ -47,7 +61,8 @@ def _worker(rank, world, cj, ci, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from regcm_amd import icbc
     from oracle.oracle import OracleCore
-    rc = CONFIGS["C1"]
+    import dataclasses
+    rc = dataclasses.replace(CONFIGS["C1"], **variant)
     data = icbc.generate(rc)
     o = OracleCore(rc, data["split"], nproc_j=cj, nproc_i=ci, tile=rank)
     j0, i0, nj, ni = o.info[:4]
@@ -112,36 +127,39 @@ def _worker(rank, world, cj, ci, port, q):
             a[:, dst] = buf.numpy()
 
     o.set_exchange(exch, exchb)
-    o.put_state(data["state"])
-    o.bdyval()
+    _setup(o, rc, data, variant)
     o.step(NSTEPS)
-    res = {name: o.get(name) for name in STATE_FIELDS}
+    res = {name: o.get(name) for name in _fields(variant)}
     res["_ext"] = (jde1, jde2, ide1, ide2)
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("cj,ci", [(2, 1), (2, 2)])
-def test_oracle_tiles_over_gloo_match_single_tile(cj, ci, c1_data):
+@pytest.mark.parametrize("cj,ci,variant", [(2, 1, {}), (2, 2, {}), (2, 2, {"ibltyp": 2, "isladvec": 1})],
+                         ids=["2x1", "2x2", "2x2-tke-sl"])
+def test_oracle_tiles_over_gloo_match_single_tile(cj, ci, variant, c1_data):
+    """Also with the UW TKE and semi-Lagrangian moisture advection: their wider exchanges
+    (atm1 ud 2, atm2 qx 4, tke 1/2) travel in the same schedule."""
+    import dataclasses
     from oracle.oracle import OracleCore
-    rc, data = c1_data
+    rc0, data = c1_data
+    rc = dataclasses.replace(rc0, **variant)
     ref = OracleCore(rc, data["split"])
-    ref.put_state(data["state"])
-    ref.bdyval()
+    _setup(ref, rc, data, variant)
     ref.step(NSTEPS)
     world = cj * ci
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, cj, ci, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, cj, ci, port, q, variant)) for r in range(world)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=300) for _ in range(world))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for name in STATE_FIELDS:
+    for name in _fields(variant):
         full = ref.get(name)
         for r, res in results.items():
             jde1, jde2, ide1, ide2 = res["_ext"]
