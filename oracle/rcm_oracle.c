@@ -34,7 +34,7 @@ static const double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
 #define MINQQ   1.0e-8                       /* :57  */
 #define DLOWVAL 1.0e-20                      /* :68  */
 #define VONKAR  0.4                          /* :296 */
-static double c_rgas, c_cpd, c_c287, c_ep1, c_regrav;
+static double c_rgas, c_cpd, c_c287, c_ep1, c_regrav, c_rovcp;
 static const double alpha_hyd = 0.0;         /* :319 */
 static const double beta_hyd = 1.0 - 2.0 * 0.0; /* :320 */
 /* mod_diffusion.F90:69-71 */
@@ -53,6 +53,7 @@ static void init_constants(void) {
   c_cpd = 3.5 * c_rgas;                      /* :144 */
   c_ep1 = AMD / AMW - d_one;                 /* :303 */
   c_regrav = d_one / EGRAV;                  /* :182 */
+  c_rovcp = c_rgas * (d_one / c_cpd);        /* :183-184, rovcp = rgas*rcpd */
   c_pgfaa1 = ALAM * c_rgas * c_regrav;       /* :362 */
 }
 
@@ -113,6 +114,7 @@ struct orc {
   double *ps0, *pr0, *t0, *rho0, *z0, *pf0, *rhof0, *zf0, *dpsdxm, *dpsdym, *dprddx, *dprddy;
   double *ef, *ddx, *ddy, *dmdx, *dmdy, *ex, *crx, *cry;
   double *umd, *vmd, *xpp, *xw, *pr1, *rho1, *xpr, *ucc, *vcc, *ppb3d, *wb3d, *xkcf;
+  double *th, *tha, *thten;                 /* potential temperature advection, ithadv = 1 */
   double *ppten, *ppdyn, *wten, *wdyn, *cpp, *cw, *cdt;
   double *s_wo, *s_e, *s_f, *s_aa, *s_b, *s_c, *s_rhs, *s_ca, *s_g1, *s_g2, *s_ptend, *s_pxup,
          *s_pyvp, *s_tk, *s_cc, *s_cdd, *s_cj, *s_pi, *s_ucrs, *s_vcrs;
@@ -385,6 +387,7 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
     o->pr1 = alloc3(o, kz); o->rho1 = alloc3(o, kz); o->xpr = alloc3(o, kz);
     o->ucc = alloc3(o, kz); o->vcc = alloc3(o, kz); o->ppb3d = alloc3(o, kz); o->wb3d = alloc3(o, kp);
     o->xkcf = alloc3(o, kp);
+    o->th = alloc3(o, kz); o->tha = alloc3(o, kz); o->thten = alloc3(o, kz);
     o->ppten = alloc3(o, kz); o->ppdyn = alloc3(o, kz); o->wten = alloc3(o, kp); o->wdyn = alloc3(o, kp);
     o->cpp = alloc3(o, kz); o->cw = alloc3(o, kp); o->cdt = alloc3(o, kz);
     double** sc[] = {&o->s_wo, &o->s_e, &o->s_f, &o->s_aa, &o->s_b, &o->s_c, &o->s_rhs, &o->s_ca,
@@ -441,7 +444,7 @@ void orc_destroy(orc_t* o) {
     &o->xkcf, &o->ppten, &o->ppdyn, &o->wten, &o->wdyn, &o->cpp, &o->cw, &o->cdt, &o->s_wo, &o->s_e,
     &o->s_f, &o->s_aa, &o->s_b, &o->s_c, &o->s_rhs, &o->s_ca, &o->s_g1, &o->s_g2, &o->s_ptend,
     &o->s_pxup, &o->s_pyvp, &o->s_tk, &o->s_cc, &o->s_cdd, &o->s_cj, &o->s_pi, &o->s_ucrs, &o->s_vcrs,
-    &o->estore, &o->astore, &o->wpval};
+    &o->estore, &o->astore, &o->wpval, &o->th, &o->tha, &o->thten};
   for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
   for (int q = 0; q < 7; q++) free(o->phy[q]);
   free(o->a1tke); free(o->a2tke); free(o->ctke); free(o->tkedyn); free(o->tkeps); free(o->tkephy);
@@ -1808,7 +1811,7 @@ static void splitf(orc_t* o) {
 
 /* ======================================================================================
  * Non-hydrostatic core (idynamic = 2): Main/mod_tendency.F90 NH branches, Main/mod_sound.F90,
- * raydamp (Main/mod_bdycod.F90:4953-5123).  ithadv = 0, ipptls = 1 (qcd aliases atmx%qx(iqc),
+ * raydamp (Main/mod_bdycod.F90:4953-5123).  ithadv = 1, ipptls = 1 (qcd aliases atmx%qx(iqc),
  * Main/mod_tendency.F90:117-121), i_crm = 0, physics stubbed.
  * ====================================================================================== */
 #define NH_REARTHRAD (d_one / 6.371229e6)            /* Share/mod_constants.F90:282-284 */
@@ -2045,25 +2048,23 @@ static void nh_vadv3d_lin(orc_t* o, const double* f, double* ften, int full) {
     }
 }
 
-/* vadv3d ind = 1, non-hydrostatic form (Main/mod_advection.F90:784-803) */
-static void nh_vadv3d_t(orc_t* o) {
-  const double* f = o->a1t;
-  for (int i = o->ici1; i <= o->ici2; i++)
-    for (int j = o->jci1; j <= o->jci2; j++) {
-      double rdphf = exp(-c_c287 * log(A3(o->pb3d, j, i, 1)));
-      A3(o->dotqdot, j, i, 1) = A3(f, j, i, 1) * rdphf;
-    }
-  for (int k = 2; k <= o->kz; k++)
-    for (int i = o->ici1; i <= o->ici2; i++)
-      for (int j = o->jci1; j <= o->jci2; j++) {
-        double rdphf = exp(-c_c287 * log(A3(o->pb3d, j, i, k)));
-        double rdplf = exp(c_c287 * log(A3(o->pf3d, j, i, k)));
-        A3(o->dotqdot, j, i, k) = A3(f, j, i, k) * rdphf;
-        double fx = rdplf * A3(o->qdot, j, i, k) *
-                    (o->twt1[k] * A3(o->dotqdot, j, i, k) + o->twt2[k] * A3(o->dotqdot, j, i, k - 1));
-        A3(o->tdyn, j, i, k - 1) = A3(o->tdyn, j, i, k - 1) - fx * o->xds[k - 1];
-        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + fx * o->xds[k];
+/* potential temperature advection of the NH core, ithadv = 1 (Main/mod_tendency.F90:98,128-129:
+ * ithadv is reset to 0 only for idynamic = 1, so every idynamic = 2 run takes this branch,
+ * :1347-1356): th = atmx%t*(p00/atm1%pr)**rovcp, tha = th*p*, exchange(th,1), hadvt of th and
+ * vadv3d ind = 0 of tha into thten */
+#define NH_P00 1.000000e5                              /* Share/mod_constants.F90:229 */
+static void nh_theta_advection(orc_t* o) {
+  int kz = o->kz;
+  memset(o->thten, 0, sizeof(double) * o->plane * kz);
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->ice1; i <= o->ice2; i++)
+      for (int j = o->jce1; j <= o->jce2; j++) {
+        A3(o->th, j, i, k) = A3(o->xt, j, i, k) * pow(NH_P00 / A3(o->pr1, j, i, k), c_rovcp);
+        A3(o->tha, j, i, k) = A3(o->th, j, i, k) * A2(o->psa, j, i);
       }
+  xch(o, o->th, kz, 1, 0);
+  hadv_scalar(o, o->th, o->thten, 1);          /* hadv(thten,th) -> hadvt */
+  nh_vadv3d_lin(o, o->tha, o->thten, 0);       /* vadv(thten,tha,kz,0) */
 }
 
 /* advection NH (Main/mod_tendency.F90:1270-1392) */
@@ -2076,8 +2077,7 @@ static int nh_advection(orc_t* o) {
   nh_vadv3d_lin(o, o->a1pp, o->ppdyn, 0);
   nh_hadv3d_w(o, o->xw, o->wdyn);
   nh_vadv3d_lin(o, o->a1w, o->wdyn, 1);
-  hadv_scalar(o, o->xt, o->tdyn, 1);          /* hadvt */
-  nh_vadv3d_t(o);
+  nh_theta_advection(o);                      /* ithadv = 1, :1347-1356 */
   if (o->cfg.isladvec == 1) {                 /* :1361-1363, 1378-1380, as in advection() */
     bad = sl_advection(o);
     vadvqv(o);
@@ -2110,17 +2110,14 @@ static void nh_curvature(orc_t* o) {
       }
 }
 
-/* adiabatic NH (:1581-1593, 1612-1671), ithadv = 0, ipptls > 0 */
+/* adiabatic NH (:1594-1600, 1606-1671), ithadv = 1, ipptls > 0 */
 static void nh_adiabatic(orc_t* o) {
   int kz = o->kz;
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
-        double cpm = c_cpd * (d_one + 0.80 * A3(o->xq[0], j, i, k));
-        double scr1 = d_half * EGRAV * A3(o->rho0, j, i, k) * (A3(o->a1w, j, i, k) + A3(o->a1w, j, i, k + 1));
-        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + A3(o->xt, j, i, k) * A3(o->cr, j, i, k) -
-            (scr1 + A3(o->ppdyn, j, i, k) + A3(o->ppten, j, i, k) + A3(o->xpp, j, i, k) * A3(o->cr, j, i, k)) /
-            (A3(o->rho1, j, i, k) * cpm);
+        A3(o->thten, j, i, k) = A3(o->thten, j, i, k) + A3(o->th, j, i, k) * A3(o->cr, j, i, k);
+        A3(o->tdyn, j, i, k) = A3(o->tdyn, j, i, k) + A3(o->a1t, j, i, k) * A3(o->thten, j, i, k) / A3(o->tha, j, i, k);
       }
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)

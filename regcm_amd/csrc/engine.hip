@@ -250,6 +250,7 @@ struct rcmdyn_engine {
     const double rgasmol = NAVGDR * BOLTZK;
     c.c287 = rgasmol / AMD; c.rgas = c.c287 * 1000.0; c.cpd = 3.5 * c.rgas;
     c.ep1 = AMD / AMW - 1.0; c.regrav = 1.0 / EGRAV;
+    c.rovcp = c.rgas * (1.0 / c.cpd);                        // Share/mod_constants.F90:183-184
     c.ipgf = cfg.ipgf;
     c.isladvec = cfg.isladvec; c.iqmsl = cfg.iqmsl;
     c.idiffu = cfg.idiffu;
@@ -422,7 +423,7 @@ struct rcmdyn_engine {
                        &f.ppb3d, &f.pb3d, &f.xkcr, &f.xkc, &f.xkd, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
                        &f.ppten, &f.ppdyn, &f.ct, &f.cu, &f.cv, &f.cpp, &f.cdt, &f.se, &f.sf, &f.saa, &f.sb,
                        &f.sc, &f.rhs, &f.sca, &f.sg1, &f.sg2, &f.ptend, &f.pxup, &f.pyvp, &f.tk, &f.scc, &f.scdd,
-                       &f.scj, &f.spi})
+                       &f.scj, &f.spi, &f.th})
       *p = dalloc(t, P3);
     for (double** p : {&f.a1w, &f.a2w, &f.xw, &f.wb3d, &f.pf3d, &f.xkcf, &f.wten, &f.wdyn, &f.cw, &f.wo})
       *p = dalloc(t, P4);

@@ -85,7 +85,7 @@ struct Consts {
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
   double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;
-  double rgas, cpd, c287, ep1, regrav;
+  double rgas, cpd, c287, ep1, regrav, rovcp;
   double sigma[MAXKZ + 2], hsigma[MAXKZ + 1], dsigma[MAXKZ + 1];
   double twt1[MAXKZ + 1], twt2[MAXKZ + 1], qcon[MAXKZ + 1], xds[MAXKZ + 1];
   double hefc[MAXNSP][MAXKZ + 1], hegc[MAXNSP][MAXKZ + 1];

@@ -1,7 +1,8 @@
 // kernels_nh.hip -- HIP/CDNA4 kernels of the non-hydrostatic (MM5-type) dynamical-core step
 // (idynamic = 2): the NH branches of tend (Main/mod_tendency.F90), the acoustic sub-stepping
 // of sound (Main/mod_sound.F90:163-718), Rayleigh damping (Main/mod_bdycod.F90:4953-5123)
-// and the NH boundary values.  ithadv = 0, ipptls = 1, i_crm = 0, physics stubbed.
+// and the NH boundary values.  ithadv = 1 (the only NH temperature path of the reference,
+// Main/mod_tendency.F90:98,128-129), ipptls = 1, i_crm = 0, physics stubbed.
 //
 // Each kernel restates one reference loop nest (or the whole vertical recurrence of a column,
 // one thread per column) with the same floating-point operation order as oracle/rcm_oracle.c
@@ -20,6 +21,7 @@ namespace rcm {
 static constexpr double EGRAV_NH = 9.80665;                 // Share/mod_constants.F90:85
 static constexpr double REARTHRAD = 1.0 / 6.371229e6;       // :282-284
 static constexpr double MATHPI = 3.1415926535897932384626433832795029;
+static constexpr double P00 = 1.000000e5;                  // Share/mod_constants.F90:229
 
 #define IN_CE(j, i) (in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2))
 #define IN_CI(j, i) (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))
@@ -57,7 +59,9 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 // ---------------------------------------------------------------------------------------
 // decouple NH (Main/mod_tendency.F90:852-1066): coupled/decoupled winds on the dot frame
 // (umc, vmc, ud, vd, umd, vmd), decoupled t, q, tv, pp, w, atm1 pr/rho and the buoyancy
-// helper atmx%pr on the cross frame.  k = 1..kz+1 (w only on kz+1).
+// helper atmx%pr on the cross frame, and the potential temperature th of ithadv = 1
+// (:1349-1353) on the cross frame with its ghost ring, the points exchange(th,1) fills: th is
+// pointwise in atmx%t and atm1%pr, which are defined there.  k = 1..kz+1 (w only on kz+1).
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
@@ -84,6 +88,7 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   F3(f.xt, j, i, k) = xt; F3(f.xqv, j, i, k) = xqv; F3(f.xqc, j, i, k) = xqc; F3(f.xtv, j, i, k) = xtv;
   F3(f.xpp, j, i, k) = xpp; F3(f.pr1, j, i, k) = pr1;
   F3(f.rho1, j, i, k) = pr1 / (c->rgas * xtv);
+  F3(f.th, j, i, k) = xt * rcm_powpos(P00 / pr1, c->rovcp);
   if (IN_CI(j, i))
     F3(f.xpr, j, i, k) = (xtv - F3(f.t0, j, i, k) - xpp / (c->cpd * F3(f.rho0, j, i, k))) / xt;
 }
@@ -261,8 +266,8 @@ __device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const 
 }
 
 // scalar advection of the NH core (advection driver Main/mod_tendency.F90:1308-1392): pp
-// (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 + vadv3d ind 0 on full levels), t (hadvt +
-// vadv3d ind 1 NH form), qv (hadvqv + vadvqv), qc (hadvqx + vadv4d ind 1).  One thread per
+// (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 + vadv3d ind 0 on full levels), potential
+// temperature (hadvt + vadv3d ind 0, and its adiabatic term), qv (hadvqv + vadvqv), qc (hadvqx + vadv4d ind 1).  One thread per
 // interior cross point and level k = 1..kz+1 (w alone on kz+1): every element is written once,
 // with the reference's order of accumulation -- 0, the horizontal term, then the vertical flux
 // through its upper interface (the reference's loop iteration k, added) and through its lower
@@ -320,17 +325,20 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
     if (k + 1 <= kz) pd = pd - pflux(k + 1) * c->xds[k];
     F3(f.ppdyn, j, i, k) = pd;
   }
-  // ---- t: hadvt, then vadv3d ind = 1, non-hydrostatic form, :784-803
+  // ---- t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d ind = 0
+  // (nk = kz) of tha = th*p*, plus th*cr; the adiabatic term adds atm1%t*thten/tha to tdyn
+  // (zero until then: advection and curvature do not touch it)
   {
-    double td = F3(f.tdyn, j, i, k) + hadv_fg(g, c, f.xt, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
-    auto dkt = [&](int kk) { return F3(f.a1t, j, i, kk) * exp(-c->c287 * log(F3(f.pb3d, j, i, kk))); };
-    auto tflux = [&](int kk) {
-      const double rdplf = exp(c->c287 * log(F3(f.pf3d, j, i, kk)));
-      return rdplf * F3(f.qdot, j, i, kk) * (c->twt1[kk] * dkt(kk) + c->twt2[kk] * dkt(kk - 1));
+    double thd = d_zero + hadv_fg(g, c, f.th, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
+    auto thflux = [&](int kk) {
+      return F3(f.qdot, j, i, kk) *
+             (c->twt1[kk] * (F3(f.th, j, i, kk) * ps) + c->twt2[kk] * (F3(f.th, j, i, kk - 1) * ps));
     };
-    if (k >= 2) td = td + tflux(k) * c->xds[k];
-    if (k + 1 <= kz) td = td - tflux(k + 1) * c->xds[k];
-    F3(f.tdyn, j, i, k) = td;
+    if (k >= 2) thd = thd + thflux(k) * c->xds[k];
+    if (k + 1 <= kz) thd = thd - thflux(k + 1) * c->xds[k];
+    const double th = F3(f.th, j, i, k);
+    thd = thd + th * F3(f.cr, j, i, k);
+    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + F3(f.a1t, j, i, k) * thd / (th * ps);
   }
   // ---- qv: hadvqv (or the semi-Lagrangian start, isladvec = 1), then vadvqv, :811-836
   {
@@ -384,19 +392,15 @@ __global__ void k_nh_curvature(Geom g, const Consts* __restrict__ c, NHFields f)
                         vc * amfac;
 }
 
-// adiabatic NH (:1581-1593, 1612-1671), one thread per interior cross column
+// adiabatic NH (:1601-1671), one thread per interior cross column; the ithadv = 1 temperature
+// term (:1594-1600) is formed in k_nh_scalar_adv with thten
 __global__ void k_nh_adiabatic(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   for (int k = 1; k <= kz; k++) {
-    const double cpm = c->cpd * (d_one + 0.80 * F3(f.xqv, j, i, k));
-    const double scr1 = d_half * EGRAV_NH * F3(f.rho0, j, i, k) * (F3(f.a1w, j, i, k) + F3(f.a1w, j, i, k + 1));
-    const double cr = F3(f.cr, j, i, k), xpp = F3(f.xpp, j, i, k);
-    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + F3(f.xt, j, i, k) * cr -
-                          (scr1 + F3(f.ppdyn, j, i, k) + F3(f.ppten, j, i, k) + xpp * cr) /
-                              (F3(f.rho1, j, i, k) * cpm);
-    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + xpp * cr;
+    const double cr = F3(f.cr, j, i, k);
+    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + F3(f.xpp, j, i, k) * cr;
     F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + F3(f.xqv, j, i, k) * cr;
     F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + F3(f.xqc, j, i, k) * cr;
   }

@@ -24,6 +24,7 @@ struct NHFields {
   const double *rpsa, *rpsb, *rpsda, *rpsdb, *psdota, *psdotb;
   // decoupled / derived fields of the step
   double *umc, *vmc, *ud, *vd, *umd, *vmd, *xt, *xqv, *xqc, *xtv, *xpp, *xw, *pr1, *rho1, *xpr;
+  double *th;                    // potential temperature atmx%t*(p00/atm1%pr)**rovcp (ithadv = 1)
   double *cr, *qdot, *ubd, *vbd, *tb3d, *qvb3d, *qcb3d, *ppb3d, *wb3d, *pb3d, *pf3d;
   double *xkcr, *xkc, *xkd, *xkcf, *uavg1, *uavg2, *vavg1, *vavg2;
   // tendencies: total (pc_total) and dynamic (pc_dynamic)

@@ -363,3 +363,106 @@ def test_oracle_tke_bounds_and_independence(c1_data):
     assert np.all(t[0, 0, :] == rc.tkemin) and np.all(t[0, :, 0] == rc.tkemin)
     for name in ("ATM1_U", "ATM1_T", "ATM1_QV", "PSA"):
         assert np.array_equal(o.get(name), b.get(name)), name
+
+
+def test_nh_theta_advection_matches_numpy_restatement():
+    """The NH temperature tendency of the restatement against an independent NumPy
+    restatement of the reference's ithadv = 1 path (Main/mod_tendency.F90:98,128-129: ithadv
+    stays 1 for idynamic = 2; :1347-1356, 1594-1600): th = atmx%t*(p00/atm1%pr)**rovcp,
+    tha = th*p*, thten = hadvt(th) + vadv3d ind 0 (tha) + th*cr, tdyn = atm1%t*thten/tha.
+    Also restates qdot of compute_omega NH (:1157-1191).  With ckh = adyndif = 0 (xkc = 0,
+    no diffusion) and ifrayd = 0, tten at points outside the relaxation band is exactly that
+    tdyn.  The comparison is at 1e-13 relative (numpy and the C restatement both call libm
+    pow/division in the same order, so it is usually bit-exact)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    rc = dataclasses.replace(CONFIGS["N1"], ckh=0.0, adyndif=0.0, ifrayd=0)
+    data = icbc.generate_nh(rc)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_PP", "ATM1_W", "PSA", "MSFX", "MSFD",
+                                "ATM0_PR", "ATM0_PS", "ATM0_RHOF", "DPSDXM", "DPSDYM")}
+    o.tend()
+    tten, qdot_o = o.get("TTEN"), o.get("QDOT")
+
+    kz, nsp = rc.kz, rc.nspgx
+    sig = rc.sigma
+    hsig = (sig[1:] + sig[:-1]) * 0.5
+    dsig = sig[1:] - sig[:-1]
+    twt1 = np.zeros(kz + 1); twt2 = np.zeros(kz + 1)
+    for k in range(2, kz + 1):                                   # Main/mod_params.F90:2212-2213
+        twt1[k] = (sig[k - 1] - hsig[k - 2]) / (hsig[k - 1] - hsig[k - 2])
+        twt2[k] = 1.0 - twt1[k]
+    dx = rc.ds * 1000.0
+    ul = rc.uoffc * 0.5 * rc.dt / dx                             # Main/mod_advection.F90:106
+    from regcm_amd import constants as C
+    rgas = C.rgas
+    cpd = 3.5 * rgas
+    rovcp = rgas * (1.0 / cpd)                                   # Share/mod_constants.F90:183-184
+    egrav = 9.80665
+    # interior cross points outside the relaxation band (1-based global j, i)
+    J = np.arange(nsp + 1, rc.jx - nsp)
+    I = np.arange(nsp + 1, rc.iy - nsp)
+
+    def at(a, dj=0, di=0):                                      # a[k][i][j] at (J+dj, I+di)
+        return a[:, (I + di - 1)[:, None], (J + dj - 1)[None, :]]
+
+    ps = at(g["PSA"])[0]
+    msfx, msfd = at(g["MSFX"])[0], g["MSFD"]
+    umc = g["ATM1_U"] * msfd[0][None]
+    vmc = g["ATM1_V"] * msfd[0][None]
+    # compute_omega NH: qdot from w and the reference-p* slopes (decoupled dot winds umd)
+    pa = g["PSA"][0]
+    psd = np.zeros_like(pa)
+    psd[1:, 1:] = (pa[1:, 1:] + pa[:-1, 1:] + pa[1:, :-1] + pa[:-1, :-1]) * 0.25
+    rpsd = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0)
+    umd = g["ATM1_U"] * rpsd[None] * msfd[0][None]
+    vmd = g["ATM1_V"] * rpsd[None] * msfd[0][None]
+    ucc = at(umd) + at(umd, 0, 1) + at(umd, 1, 0) + at(umd, 1, 1)
+    vcc = at(vmd) + at(vmd, 0, 1) + at(vmd, 1, 0) + at(vmd, 1, 1)
+    pinv = np.divide(1.0, g["PSA"][0], out=np.zeros_like(g["PSA"][0]), where=g["PSA"][0] > 0)
+    xw = g["ATM1_W"] * pinv[None]
+    qdot = np.zeros((kz + 1,) + ps.shape)
+    for k in range(2, kz + 1):
+        qdot[k - 1] = (-at(g["ATM0_RHOF"])[k - 1] * egrav * at(xw)[k - 1] / at(g["ATM0_PS"])[0] -
+                       sig[k - 1] * (at(g["DPSDXM"])[0] * (twt1[k] * ucc[k - 1] + twt2[k] * ucc[k - 2]) +
+                                     at(g["DPSDYM"])[0] * (twt1[k] * vcc[k - 1] + twt2[k] * vcc[k - 2])))
+    np.testing.assert_allclose(qdot, at(qdot_o), rtol=1e-13, atol=1e-13 * np.abs(qdot).max())
+    # mass divergence cr
+    a = at(umc, 1, 1) + at(umc, 1, 0) - at(umc, 0, 1) - at(umc)
+    b = at(vmc, 1, 1) + at(vmc, 0, 1) - at(vmc, 1, 0) - at(vmc)
+    dummy = 1.0 / (2.0 * dx * msfx * msfx)
+    cr = (a + b) * dummy[None] + (qdot[1:] - qdot[:-1]) * ps[None] / dsig[:, None, None]
+    # th on the interior and its four neighbours
+    rps = pinv
+    with np.errstate(divide="ignore", invalid="ignore"):
+        thf = (g["ATM1_T"] * rps[None]) * (1.0e5 / (g["ATM0_PR"] + g["ATM1_PP"] * rps[None])) ** rovcp
+    th, thw, the, ths, thn = at(thf), at(thf, -1), at(thf, 1), at(thf, 0, -1), at(thf, 0, 1)
+    u1 = at(umc, 0, 1) + at(umc)
+    u2 = at(umc, 1, 1) + at(umc, 1, 0)
+    v1 = at(vmc, 1, 0) + at(vmc)
+    v2 = at(vmc, 1, 1) + at(vmc, 0, 1)
+    f1 = 0.5 * ul * (u2 + u1) / ps[None]
+    f2 = 0.5 * ul * (v2 + v1) / ps[None]
+    fx1 = (1.0 + f1) * thw + (1.0 - f1) * th
+    fx2 = (1.0 + f1) * th + (1.0 - f1) * the
+    fy1 = (1.0 + f2) * ths + (1.0 - f2) * th
+    fy2 = (1.0 + f2) * th + (1.0 - f2) * thn
+    xmsf = 1.0 / (msfx * msfx * (4.0 * dx))                      # Main/mod_params.F90:1993-2001
+    fg = -xmsf[None] * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1)
+    for (p, m) in ((thn, ths), (the, thw)):                      # hadvt limiter :359-386
+        big = np.abs(p + m - 2.0 * th) / ps[None] > rc.t_extrema
+        fg = np.where(big & (th > p) & (th > m), np.minimum(fg, 0.0), fg)
+        fg = np.where(big & (th < p) & (th < m), np.maximum(fg, 0.0), fg)
+    tha = th * ps[None]
+    thten = 0.0 + fg
+    for k in range(2, kz + 1):                                   # vadv3d ind = 0, nk = kz
+        fx = qdot[k - 1] * (twt1[k] * tha[k - 1] + twt2[k] * tha[k - 2])
+        thten[k - 2] = thten[k - 2] - fx * (1.0 / dsig[k - 2])
+        thten[k - 1] = thten[k - 1] + fx * (1.0 / dsig[k - 1])
+    thten = thten + th * cr
+    tdyn = at(g["ATM1_T"]) * thten / tha
+    got = at(tten)
+    assert np.abs(tdyn).max() > 1e-6
+    np.testing.assert_allclose(got, tdyn, rtol=1e-12, atol=1e-13 * np.abs(tdyn).max())
