@@ -53,25 +53,64 @@ def pmc_traffic(kernel: str, config: str):
     return k["hbm_bytes_per_launch"], d.get("source")
 
 
-def cpu_baseline(rc, data, budget_s: float = 15.0):
-    """Time the CPU restatement (oracle, 1 thread) on a bounded sample of the same workload."""
-    from oracle.oracle import OracleCore
-    o = OracleCore(rc, data["split"])
-    o.put_state(data["state"])
-    o.bdyval()
-    o.step(1)
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _time_steps(o, budget_s):
+    o.step(1)                                   # warm-up (the leapfrog dt switch)
     n, t0 = 0, time.perf_counter()
     while True:
         o.step(1)
         n += 1
         el = time.perf_counter() - t0
         if el > budget_s or n >= 200:
-            break
-    t = el / n
-    return {"value": rc.dt / (365.0 * t), "unit": "simulated-years/wall-day", "cores": 1,
-            "kind": "port", "ms_per_step": t * 1e3,
-            "sample": f"{rc.name}: {n} steps of tend+bdyval after 1 warm-up step, 1 host thread "
-                      f"(oracle/rcm_oracle.c, gcc -O2)"}
+            return el / n, n
+
+
+def cpu_baseline(rc, data, budget_s: float = 15.0):
+    """Time the CPU restatement on a bounded sample of the same workload: on all the host
+    threads this job may use (set_nproc tiles on OpenMP threads, oracle/orc_par.c,
+    bit-identical to one tile), and on one thread as a secondary figure."""
+    from oracle.oracle import OracleCore, OracleParallel
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, affinity))
+    threads = max(1, min(threads, affinity))
+
+    def setup(o):
+        o.put_state(data["state"])
+        o.bdyval()
+        return o
+
+    res = {"unit": "simulated-years/wall-day", "kind": "port", "nproc": nproc, "affinity_cpus": affinity,
+           "cpu_model": _cpu_model()}
+    if rc.idynamic == 1 and threads > 1:
+        o = setup(OracleParallel(rc, data["split"], threads))
+        t, n = _time_steps(o, budget_s * 0.65)
+        o.close()
+        t1, n1 = _time_steps(setup(OracleCore(rc, data["split"])), budget_s * 0.35)
+        res.update({"value": rc.dt / (365.0 * t), "cores": o.nthreads, "ms_per_step": t * 1e3,
+                    "single_thread": {"value": rc.dt / (365.0 * t1), "ms_per_step": t1 * 1e3, "steps": n1},
+                    "sample": f"{rc.name}: {n} steps of tend+bdyval after 1 warm-up step, "
+                              f"{o.nthreads} set_nproc tiles on {o.nthreads} OpenMP threads (oracle/orc_par.c over "
+                              f"oracle/rcm_oracle.c, gcc -O2); single_thread: {n1} steps on 1 thread"})
+    else:
+        t, n = _time_steps(setup(OracleCore(rc, data["split"])), budget_s)
+        res.update({"value": rc.dt / (365.0 * t), "cores": 1, "ms_per_step": t * 1e3,
+                    "sample": f"{rc.name}: {n} steps of tend+bdyval after 1 warm-up step, 1 host thread "
+                              "(oracle/rcm_oracle.c, gcc -O2; the NH restatement is single-tile)"})
+    return res
 
 
 def main():

@@ -54,6 +54,18 @@ def lib():
         L.orc_step.restype = i
         L.orc_step.argtypes = [P, i]
         L.orc_diagnostics.argtypes = [P, dp]
+        L.orc_par_create.restype = P
+        L.orc_par_create.argtypes = [ctypes.POINTER(RcmdynConfig)]
+        L.orc_par_destroy.argtypes = [P]
+        L.orc_par_put.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_par_get.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_par_set_time.argtypes = [P, ctypes.c_longlong, ctypes.c_double, ctypes.c_double]
+        L.orc_par_get_time.argtypes = [P, ctypes.POINTER(ctypes.c_longlong),
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        L.orc_par_bdyval.restype = i
+        L.orc_par_bdyval.argtypes = [P]
+        L.orc_par_step.restype = i
+        L.orc_par_step.argtypes = [P, i]
         _lib = L
     return _lib
 
@@ -134,3 +146,68 @@ class OracleCore:
         out = (ctypes.c_double * 4)()
         lib().orc_diagnostics(self.h, out)
         return list(out)
+
+
+class OracleParallel:
+    """The hydrostatic restatement as set_nproc tiles on OpenMP threads (oracle/orc_par.c):
+    the reference's MPI decomposition on host cores, bit-identical to one tile.  Same host
+    API as OracleCore for put/get/bdyval/step/set_time/get_time."""
+
+    def __init__(self, rc, split, nthreads=1):
+        from regcm_amd.config import set_nproc
+        cj, ci = set_nproc(int(nthreads), rc.jx, rc.iy)
+        self.rc = rc
+        self.nthreads = cj * ci
+        self.cfg = build_config(rc, split, cj, ci, tile_first=0, tile_count=1)
+        self.h = lib().orc_par_create(ctypes.byref(self.cfg))
+        if not self.h:
+            raise RuntimeError("orc_par_create failed")
+
+    def close(self):
+        if self.h:
+            lib().orc_par_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def put(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        nk, ni, nj = a.shape
+        if lib().orc_par_put(self.h, FIELD[name], a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             1, nj, 1, ni, 1, nk):
+            raise KeyError(name)
+
+    def get(self, name):
+        nk = field_levels(name, self.rc.kz, self.rc.nsplit)
+        out = np.zeros((nk, self.rc.iy, self.rc.jx))
+        if lib().orc_par_get(self.h, FIELD[name], out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             1, self.rc.jx, 1, self.rc.iy, 1, nk):
+            raise KeyError(name)
+        return out
+
+    def put_state(self, st):
+        for name, arr in st.items():
+            self.put(name, arr)
+
+    def set_time(self, lcount, dt, xbctime):
+        lib().orc_par_set_time(self.h, lcount, dt, xbctime)
+
+    def get_time(self):
+        a, b, c = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+        lib().orc_par_get_time(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def bdyval(self):
+        if lib().orc_par_bdyval(self.h):
+            raise RuntimeError("orc_par_bdyval: could not get one OpenMP thread per tile")
+
+    def step(self, n=1):
+        rc = lib().orc_par_step(self.h, n)
+        if rc < 0:
+            raise RuntimeError("orc_par_step: could not get one OpenMP thread per tile")
+        if rc:
+            raise FloatingPointError("CFL VIOLATION")

@@ -466,3 +466,22 @@ def test_nh_theta_advection_matches_numpy_restatement():
     got = at(tten)
     assert np.abs(tdyn).max() > 1e-6
     np.testing.assert_allclose(got, tdyn, rtol=1e-12, atol=1e-13 * np.abs(tdyn).max())
+
+
+@pytest.mark.parametrize("nthreads", [2, 4, 6])
+def test_oracle_threads_match_single_tile(c1_data, nthreads):
+    """The all-cores CPU baseline (oracle/orc_par.c: set_nproc tiles on OpenMP threads with
+    neighbour-to-neighbour exchanges in shared memory) reproduces the single-tile restatement
+    bit for bit, as the reference does across MPI rank counts."""
+    from oracle.oracle import OracleCore, OracleParallel
+    rc, data = c1_data
+    ref = OracleCore(rc, data["split"])
+    par = OracleParallel(rc, data["split"], nthreads)
+    assert par.nthreads == nthreads
+    for o in (ref, par):
+        o.put_state(data["state"])
+        o.bdyval()
+        o.step(3)
+    assert par.get_time() == ref.get_time()
+    for name in STATE_FIELDS:
+        assert np.array_equal(par.get(name), ref.get(name)), name
