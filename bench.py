@@ -172,6 +172,20 @@ def main():
         wall = float(tt.item())
     t_step = wall / args.steps
     sypd = rc.dt / (365.0 * t_step)
+    # the drop-in call sequence of INTEGRATION.md section 4 (RCM_run: rcmdyn_tend then
+    # rcmdyn_bdyval per step through the C-ABI, each replaying its own graph), same K steps
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.tend()
+        eng.bdyval()
+    barrier()
+    wall_d = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([wall_d], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall_d = float(tt.item())
     # per-kernel device time (HIP events around each launch on the engine's stream), on
     # every rank (the eager steps exchange halos), after the timed region
     kt = eng.kernel_times(args.prof_steps) if args.prof_steps > 0 else {}
@@ -240,6 +254,8 @@ def main():
                           "note": "SURVEY 8(d) " + ("B_nh" if nh else "B_h") + " per step / wall time per step"},
         "kernel_us": {k: round(v[1] * 1e3, 2) for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0] * kv[1][1])},
         "device_ms_per_step": dev_ms,
+        "dropin_ms_per_step": wall_d / args.steps * 1e3,
+        "dropin_note": "rcmdyn_tend + rcmdyn_bdyval per step (INTEGRATION.md section 4), timed like value",
     }
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(rc, data, args.cpu_budget)

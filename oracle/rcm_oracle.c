@@ -57,7 +57,7 @@ static void init_constants(void) {
   c_pgfaa1 = ALAM * c_rgas * c_regrav;       /* :362 */
 }
 
-#define GO 3   /* frame ghost width (covers ga/gb/gc halos) */
+#define GO 4   /* frame ghost width (covers ga/gb/gc halos and the isladvec = 1 exchange, 4 wide) */
 
 struct orc {
   rcmdyn_config cfg;
@@ -765,9 +765,7 @@ static void decouple(orc_t* o) {
     xch(o, o->a1tke, kz + 1, 1, 0); xch(o, o->a2tke, kz + 1, 2, 0);
   }
   {                                                              /* :1073-1077 */
-    /* the reference exchanges max(idif, 4) for isladvec = 1; the departure stencil reads at
-     * most 3 points out (|xn| < 2, then two more cells), the frame's ghost width */
-    int w = o->cfg.isladvec == 1 ? 3 : 2;
+    int w = o->cfg.isladvec == 1 ? 4 : 2;                         /* max(idif, 4) */
     xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
   }
 }

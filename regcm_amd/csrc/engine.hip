@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <string>
@@ -218,7 +219,17 @@ struct rcmdyn_engine {
   std::vector<Geom> all;     // every tile of the decomposition
   std::vector<Tile> tiles;   // tiles owned here
   hipStream_t stream = nullptr;
-  hipGraphExec_t gexec[2] = {nullptr, nullptr};
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};   // tend + bdyval, per ping-pong parity
+  hipGraphExec_t gtend[2] = {nullptr, nullptr};   // tend alone (the drop-in rcmdyn_tend)
+  hipGraphExec_t gbdy[2] = {nullptr, nullptr};    // bdyval alone (rcmdyn_bdyval)
+  // step error flags: host-mapped snapshot ring written by the last launch of every tend,
+  // one event per slot; the host checks a step's flags once its event completed and keeps
+  // at most FLAG_LAG steps unchecked, so no entry point synchronises the stream per step
+  FlagSnap* hflags = nullptr;
+  FlagSnap* dflags = nullptr;
+  hipEvent_t fev[NFLAGSLOT] = {};
+  std::deque<long long> pending;
+  static constexpr int FLAG_LAG = 2;
   bool statics_dirty = true;
   bool bdy_dirty = true;
   bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
@@ -545,12 +556,19 @@ struct rcmdyn_engine {
       setup_tile(tiles[t], cfg.tile_first + t);
     }
     HIPCHK(hipMalloc(&red, sizeof(double) * 2 * (size_t)(red_total + 1)));
+    HIPCHK(hipHostMalloc((void**)&hflags, sizeof(FlagSnap) * NFLAGSLOT, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(hflags, 0, sizeof(FlagSnap) * NFLAGSLOT);
+    HIPCHK(hipHostGetDevicePointer((void**)&dflags, hflags, 0));
+    for (auto& e : fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg, stream));
   }
 
   void destroy() {
-    for (int p = 0; p < 2; p++)
-      if (gexec[p]) hipGraphExecDestroy(gexec[p]);
+    if (stream) (void)hipStreamSynchronize(stream);
+    invalidate_graphs();
+    for (auto& e : fev)
+      if (e) hipEventDestroy(e);
+    if (hflags) hipHostFree(hflags);
     for (auto& t : tiles)
       for (void* p : t.allocs) hipFree(p);
     tiles.clear();
@@ -563,8 +581,41 @@ struct rcmdyn_engine {
   }
 
   void invalidate_graphs() {
-    for (int p = 0; p < 2; p++)
-      if (gexec[p]) { hipGraphExecDestroy(gexec[p]); gexec[p] = nullptr; }
+    for (hipGraphExec_t* g : {gexec, gtend, gbdy})
+      for (int p = 0; p < 2; p++)
+        if (g[p]) { hipGraphExecDestroy(g[p]); g[p] = nullptr; }
+  }
+
+  // ------------------------------------------------------------------ step error flags
+  // a tend was issued whose clock is lc once it ran: remember its snapshot slot
+  void note_step(long long lc) {
+    if ((int)pending.size() >= NFLAGSLOT - 1) check(0);
+    HIPCHK(hipEventRecord(fev[(lc - 1 + NFLAGSLOT) % NFLAGSLOT], stream));
+    pending.push_back(lc);
+  }
+  // check the flags of the oldest steps until at most `keep` stay unchecked; on a failure
+  // the stream drains, the sticky device flags are cleared (reported once) and the error
+  // is raised -- the reference's fatal (Main/mod_tendency.F90:702, Main/mod_sound.F90:679-681,
+  // Main/mod_sladvection.F90:149-154)
+  void check(size_t keep) {
+    while (pending.size() > keep) {
+      const long long lc = pending.front();
+      const int slot = (int)((lc - 1 + NFLAGSLOT) % NFLAGSLOT);
+      HIPCHK(hipEventSynchronize(fev[slot]));
+      pending.pop_front();
+      const volatile FlagSnap* f = hflags + slot;
+      const int sl = f->slflag, nan = f->nanflag;
+      if (!sl && !nan) continue;
+      HIPCHK(hipStreamSynchronize(stream));
+      pending.clear();
+      StepState st;
+      HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+      st.nanflag = 0; st.slflag = 0;
+      HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
+      const std::string at = " (step " + std::to_string(lc) + ")";
+      if (sl) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell" + at);
+      throw std::runtime_error("CFL VIOLATION" + at);
+    }
   }
 
   // ------------------------------------------------------------------ field access
@@ -1321,9 +1372,12 @@ struct rcmdyn_engine {
   // mkslice export when `slice`), TEND_POST the rest; a step runs both.
   static constexpr int TEND_PRE = 1, TEND_POST = 2, TEND_ALL = 3;
   void tend(int phase = TEND_ALL, bool slice = false) {
-    if (cfg.idynamic == 2) { nh_tend(phase, slice); return; }
-    if (phase & TEND_PRE) tend_pre(slice);
-    if (phase & TEND_POST) tend_post();
+    if (cfg.idynamic == 2) nh_tend(phase, slice);
+    else {
+      if (phase & TEND_PRE) tend_pre(slice);
+      if (phase & TEND_POST) tend_post();
+    }
+    if (phase & TEND_POST) KLAUNCH(k_flag_snapshot, dim3(1), dim3(64), 0, stream, ds, dflags);
   }
 
   void tend_pre(bool slice) {
@@ -1495,31 +1549,40 @@ struct rcmdyn_engine {
   }
 
   // ------------------------------------------------------------------ graph replay
+  // graph replay applies: not profiling, not an RCCL transport that cannot be captured, and
+  // for NH not a step of another shape (istep on the first two steps, the day alarm's
+  // radiative coefficients)
+  bool graph_ok() const {
+    if (no_graph || prof || (comm && !comm->graph_safe())) return false;
+    return !(cfg.idynamic == 2 && (hs.lcount < 2 || nh_day_alarm()));
+  }
+  // host bookkeeping of a replayed tend / bdyval (what tend() and bdyval() do on the host)
+  void replayed_tend() {
+    if (cfg.idynamic != 2) for (auto& t : tiles) t.cur = 1 - t.cur;
+    hs.lcount += 1;
+    if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+  void replayed_bdyval() { hs.xbctime = hs.xbctime + cfg.dtsec; }
+
   void step(int n) {
     prepare();
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
-    const bool use_graph = !no_graph && !(comm && !comm->graph_safe());
     HIPCHK(hipEventRecord(e0, stream));
     for (int s = 0; s < n; s++) {
+      check(FLAG_LAG);
       const int par = tiles[0].cur;
-      const bool nh = cfg.idynamic == 2;
-      // the NH step changes shape on the first two steps (istep) and on the day alarm (upper
-      // radiative coefficients): those run eagerly, the steady step is graph-replayed
-      const bool eager_nh = nh && (hs.lcount < 2 || nh_day_alarm());
-      if (use_graph && !eager_nh) {
-        if (!gexec[par]) capture(par);
+      if (graph_ok()) {
+        if (!gexec[par]) capture(par, 3);
         HIPCHK(hipGraphLaunch(gexec[par], stream));
-        // replay the host-side bookkeeping of one tend + bdyval
-        if (!nh) for (auto& t : tiles) t.cur = 1 - t.cur;
-        hs.lcount += 1;
-        if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
-        hs.xbctime = hs.xbctime + cfg.dtsec;
+        replayed_tend();
+        replayed_bdyval();
       } else {
         tend();
         bdyval();
       }
+      note_step(hs.lcount);
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
@@ -1528,24 +1591,51 @@ struct rcmdyn_engine {
     last_ms = n > 0 ? (double)ms / n : 0.0;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
-    StepState st;
-    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
-    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
-    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
+    check(0);
   }
 
-  void capture(int par) {
-    // capture one tend + bdyval for the current ping-pong parity; host bookkeeping done in
-    // tend()/bdyval() is rolled back because step() replays it per launch.
+  // the drop-in call sequence of RCM_run (Main/mod_regcm_interface.F90:189,208): each call
+  // replays its own captured graph and returns without synchronising the stream
+  void tend_call() {
+    prepare();
+    check(FLAG_LAG);
+    const int par = tiles[0].cur;
+    if (graph_ok()) {
+      if (!gtend[par]) capture(par, 1);
+      HIPCHK(hipGraphLaunch(gtend[par], stream));
+      replayed_tend();
+    } else {
+      tend();
+    }
+    note_step(hs.lcount);
+  }
+  void bdyval_call() {
+    prepare();
+    const int par = tiles[0].cur;
+    // after a put the ghost rings are not step results: bdyval runs eagerly (its slice
+    // exchange depends on that, bdyval())
+    if (graph_ok() && !ghosts_stale) {
+      if (!gbdy[par]) capture(par, 2);
+      HIPCHK(hipGraphLaunch(gbdy[par], stream));
+      replayed_bdyval();
+    } else {
+      bdyval();
+    }
+  }
+
+  // capture tend (what & 1) and/or bdyval (what & 2) for the current ping-pong parity; the
+  // host bookkeeping done in tend()/bdyval() is rolled back, the replay redoes it per launch
+  void capture(int par, int what) {
     const StepState save = hs;
     std::vector<int> curs;
     for (auto& t : tiles) curs.push_back(t.cur);
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    tend();
-    bdyval();
+    if (what & 1) tend();
+    if (what & 2) bdyval();
     HIPCHK(hipStreamEndCapture(stream, &graph));
-    HIPCHK(hipGraphInstantiate(&gexec[par], graph, nullptr, nullptr, 0));
+    hipGraphExec_t& x = what == 3 ? gexec[par] : what == 1 ? gtend[par] : gbdy[par];
+    HIPCHK(hipGraphInstantiate(&x, graph, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(graph));
     hs = save;
     for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
@@ -1587,6 +1677,7 @@ struct rcmdyn_engine {
 
   void set_time(long long lcount, double dt, double xbctime) {
     HIPCHK(hipStreamSynchronize(stream));
+    pending.clear();
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
     st.lcount = lcount; st.dt = dt; st.xbctime = xbctime; st.nanflag = 0; st.slflag = 0;
@@ -1689,35 +1780,22 @@ int rcmdyn_get_time(rcmdyn_t* h, int64_t* lcount, double* dt, double* xbctime) {
   });
 }
 
-int rcmdyn_tend(rcmdyn_t* h) {
-  return guard(h, [&] {
-    h->prepare();
-    h->tend();
-    HIPCHK(hipStreamSynchronize(h->stream));
-    StepState st;
-    HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
-    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
-    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
-  });
-}
+int rcmdyn_tend(rcmdyn_t* h) { return guard(h, [&] { h->tend_call(); }); }
 
 int rcmdyn_tend_pre_physics(rcmdyn_t* h) {
   return guard(h, [&] {
     h->prepare();
+    h->check(rcmdyn_engine::FLAG_LAG);
     h->tend(rcmdyn_engine::TEND_PRE, true);
-    HIPCHK(hipStreamSynchronize(h->stream));
   });
 }
 
 int rcmdyn_tend_post_physics(rcmdyn_t* h) {
   return guard(h, [&] {
     h->prepare();
+    h->check(rcmdyn_engine::FLAG_LAG);
     h->tend(rcmdyn_engine::TEND_POST);
-    HIPCHK(hipStreamSynchronize(h->stream));
-    StepState st;
-    HIPCHK(hipMemcpy(&st, h->ds, sizeof(st), hipMemcpyDeviceToHost));
-    if (st.nanflag) throw std::runtime_error("CFL VIOLATION");
-    if (st.slflag) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell");
+    h->note_step(h->hs.lcount);
   });
 }
 
@@ -1728,17 +1806,16 @@ int rcmdyn_bdyin(rcmdyn_t* h) {
   });
 }
 
-int rcmdyn_bdyval(rcmdyn_t* h) {
-  return guard(h, [&] {
-    h->prepare();
-    h->bdyval();
-    HIPCHK(hipStreamSynchronize(h->stream));
-  });
-}
+int rcmdyn_bdyval(rcmdyn_t* h) { return guard(h, [&] { h->bdyval_call(); }); }
 
 int rcmdyn_step(rcmdyn_t* h, int32_t nsteps) { return guard(h, [&] { h->step(nsteps); }); }
 
-int rcmdyn_synchronize(rcmdyn_t* h) { return guard(h, [&] { HIPCHK(hipStreamSynchronize(h->stream)); }); }
+int rcmdyn_synchronize(rcmdyn_t* h) {
+  return guard(h, [&] {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->check(0);
+  });
+}
 
 int rcmdyn_diagnostics(rcmdyn_t* h, double out[4]) { return guard(h, [&] { h->diagnostics(out); }); }
 

@@ -110,6 +110,15 @@ struct StepState {
   int slflag;         // sticky: a semi-Lagrangian departure point beyond one cell
 };
 
+// Per-step copy of the step's error flags in host-mapped memory (k_flag_snapshot, the last
+// launch of every tend): the host checks a step's flags once that step's event completed,
+// without synchronising the stream.
+struct FlagSnap {
+  long long lcount;   // the clock after the step
+  int nanflag, slflag;
+};
+constexpr int NFLAGSLOT = 16;       // ring of snapshots, slot (lcount - 1) % NFLAGSLOT
+
 // Per-tile device buffers.
 struct Tile {
   int index = 0;                   // tile number in the decomposition

@@ -1750,6 +1750,16 @@ __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* 
   bdyval_qc_level(g, do_qc, do_qv, a1qc, a1qv, [&](int j, int i) { return F2(psa, j, i); }, sl, slen, k);
 }
 
+// the step's error flags into the host-mapped ring (one lane), after the clock advanced
+__global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring) {
+  if (threadIdx.x != 0) return;
+  const long long lc = s->lcount;
+  FlagSnap& r = ring[(lc - 1 + NFLAGSLOT) % NFLAGSLOT];
+  r.nanflag = s->nanflag;
+  r.slflag = s->slflag;
+  r.lcount = lc;
+}
+
 // ---------------------------------------------------------------------------------------
 // static derived fields: Main/mod_params.F90:1993-2001 (xmsf, dmsf), Main/mod_diffusion.F90:
 // 124-140 (hgfact), Main/mod_split.F90:99-101 (map)

@@ -91,12 +91,46 @@ def test_tend_bdyval_equals_step(c1_data):
     for e in (e1, e2):
         e.put_state(data["state"])
         e.bdyval()
-    for _ in range(3):
+    for _ in range(6):                  # the drop-in sequence: graph per call, both parities
         e1.tend()
         e1.bdyval()
-    e2.step(3)
+    e2.step(6)
+    assert e1.get_time() == e2.get_time()
     for name in STATE_FIELDS:
         assert np.array_equal(e1.get(name), e2.get(name)), name
+
+
+def test_cfl_violation_stops_within_lag(c1_data):
+    """A state that goes NaN stops rcmdyn_step within FLAG_LAG steps of the failing step
+    (checked on the host from per-step flag snapshots, no per-step stream sync), reports the
+    step the oracle fails at, and clears the flag once reported (Main/mod_tendency.F90:702)."""
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore, EngineError
+    rc, data = c1_data
+    st = {k: v.copy() for k, v in data["state"].items()}
+    for name in ("ATM1_T", "ATM2_T"):
+        st[name][5, 20:24, 20:24] = np.nan
+    o = OracleCore(rc, data["split"])
+    o.put_state(st)
+    o.bdyval()
+    fail = None
+    for n in range(1, 20):
+        try:
+            o.step(1)
+        except FloatingPointError:
+            fail = n
+            break
+    assert fail is not None
+    e = DynCore(rc, data["split"])
+    e.put_state(st)
+    e.bdyval()
+    with pytest.raises(EngineError, match=rf"CFL VIOLATION \(step {fail}\)"):
+        e.step(100)
+    assert e.get_time()[0] <= fail + 3             # FLAG_LAG = 2 steps in flight at most
+    e.set_time(0, rc.dt, 0.0)
+    e.put_state(data["state"])
+    e.bdyval()
+    e.step(2)                                       # the flag was cleared
 
 
 @pytest.mark.parametrize("nproc", [(2, 1), (2, 2), (1, 3), (1, 7)])
@@ -295,4 +329,5 @@ def test_sladvection_departure_check(c1_data):
     with pytest.raises(FloatingPointError):
         o.tend()
     with pytest.raises(EngineError, match="SLADVECTION"):
-        e.tend()
+        e.tend()            # reported by the call, at the latest by the next synchronize
+        e.synchronize()
