@@ -1,0 +1,172 @@
+"""GPU parity at every BASELINE.json configuration (C2-C5) and SURVEY 8(c)'s whole-step
+contract: the HIP engine through the C-ABI against the CPU restatement.
+
+Tolerances (written per test):
+* rel-L2 per prognostic field: <= 1e-13 after one step, <= 1e-9 after 100
+  steps (C2); plus the relative max-norm of the other parity tests (1e-12 after one step).
+* Decomposed runs (the set_nproc tiles of C4 and C5 held on one GPU, exchanging through the
+  same staging layout RCCL moves) are bit-identical to one tile, as the reference is across
+  rank counts.
+* NH (C5 / N2): relative max-norm 1e-11 after one step, 1e-10 after two (see test_nh_gpu.py).
+
+The large oracles run on host threads (oracle/orc_par.c, bit-identical to one tile); the
+tests print progress so a long one is visibly alive.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from regcm_amd.config import CONFIGS, NH_STATE_FIELDS, STATE_FIELDS
+from regcm_amd import icbc
+
+pytestmark = pytest.mark.gpu
+
+CROSS = {"ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_T", "ATM2_QV", "ATM2_QC", "PSA", "PSB",
+         "DSTOR", "HSTOR", "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"}
+NH_FIELDS = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_U", "ATM2_V", "ATM2_T",
+             "ATM2_QV", "ATM2_QC", "PSA", "PSB"] + NH_STATE_FIELDS
+
+
+def _crop(a, rc, name):
+    return a[:, : rc.iy - 1, : rc.jx - 1] if name in CROSS else a
+
+
+def rel_l2(a, b, rc, name):
+    a, b = _crop(a, rc, name), _crop(b, rc, name)
+    den = float(np.sqrt(np.sum(b * b)))
+    return float(np.sqrt(np.sum((a - b) ** 2))) / max(den, 1e-300)
+
+
+def rel_max(a, b, rc, name):
+    a, b = _crop(a, rc, name), _crop(b, rc, name)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _threads():
+    n = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(16, len(os.sched_getaffinity(0)))
+    return max(1, min(n, 16))
+
+
+def say(*a):
+    print("[configs]", *a, flush=True)
+
+
+def oracle(rc, data):
+    from oracle.oracle import OracleCore, OracleParallel
+    o = OracleParallel(rc, data["split"], _threads()) if rc.idynamic == 1 else OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    return o
+
+
+def engine(rc, data, nproc_j=1, nproc_i=1):
+    from regcm_amd.dycore import DynCore
+    e = DynCore(rc, data["split"], nproc_j=nproc_j, nproc_i=nproc_i)
+    e.put_state(data["state"])
+    e.bdyval()
+    return e
+
+
+def check_close(e, o, rc, fields, l2tol, maxtol, what):
+    worst = (0.0, 0.0, "")
+    for name in fields:
+        a, b = e.get(name), o.get(name)
+        l2, mx = rel_l2(a, b, rc, name), rel_max(a, b, rc, name)
+        assert l2 <= l2tol and mx <= maxtol, (what, name, l2, mx)
+        worst = max(worst, (l2, mx, name))
+    say(what, "worst rel-L2 %.2e rel-max %.2e (%s)" % worst)
+
+
+def test_c3_five_steps_vs_oracle():
+    """C3 (the headline grid): 1 step at rel-L2 1e-13 / rel-max 1e-12, 5 steps at rel-L2
+    1e-12 / rel-max 1e-11."""
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    o, e = oracle(rc, data), engine(rc, data)
+    o.step(1)
+    e.step(1)
+    assert e.get_time() == o.get_time()
+    check_close(e, o, rc, STATE_FIELDS, 1e-13, 1e-12, "C3 1 step")
+    o.step(4)
+    e.step(4)
+    check_close(e, o, rc, STATE_FIELDS, 1e-12, 1e-11, "C3 5 steps")
+
+
+def test_c2_hundred_steps_rel_l2():
+    """rel-L2 <= 1e-9 after 100 steps (C2, dycore only)."""
+    rc = CONFIGS["C2"]
+    data = icbc.generate(rc)
+    o, e = oracle(rc, data), engine(rc, data)
+    for n in range(4):
+        o.step(25)
+        e.step(25)
+        say("C2 step", 25 * (n + 1))
+    assert e.get_time() == o.get_time()
+    check_close(e, o, rc, STATE_FIELDS, 1e-9, 1e-7, "C2 100 steps")
+
+
+def test_c4_two_by_two_tiles():
+    """C4 (384x384x23 on 2x2 tiles): the decomposed engine is bit-identical to one tile over
+    3 steps, and both match the oracle after 2 steps."""
+    rc = CONFIGS["C4"]
+    data = icbc.generate(rc)
+    one, dec = engine(rc, data), engine(rc, data, 2, 2)
+    o = oracle(rc, data)
+    for x in (one, dec, o):
+        x.step(2)
+    check_close(dec, o, rc, STATE_FIELDS, 1e-13, 1e-11, "C4 2x2 vs oracle, 2 steps")
+    one.step(1)
+    dec.step(1)
+    for name in STATE_FIELDS:
+        assert np.array_equal(one.get(name), dec.get(name)), name
+    say("C4 2x2 tiles bit-identical to one tile after 3 steps")
+
+
+@pytest.fixture(scope="module")
+def c5_data():
+    rc = CONFIGS["C5"]
+    say("generating C5 ICBC")
+    return rc, icbc.generate_nh(rc)
+
+
+def test_c5_two_by_four_tiles(c5_data):
+    """C5 (768x768x41 NH, 2x4 tiles as on 8 GPUs): bit-identical to one tile over 3 steps
+    (the first two change shape: istep and the day-alarm radiative mask)."""
+    rc, data = c5_data
+    one = engine(rc, data)
+    say("C5 one tile ready")
+    dec = engine(rc, data, 2, 4)
+    say("C5 2x4 tiles ready")
+    one.step(3)
+    dec.step(3)
+    for name in NH_FIELDS:
+        assert np.array_equal(one.get(name), dec.get(name)), name
+    say("C5 2x4 tiles bit-identical to one tile after 3 steps")
+
+
+def test_c5_vs_oracle(c5_data):
+    """C5 against the NH restatement: 1 step at rel-max 1e-11, 2 steps at 1e-10."""
+    rc, data = c5_data
+    e = engine(rc, data)
+    o = oracle(rc, data)
+    say("C5 oracle ready")
+    for n, tol in ((1, 1e-11), (1, 1e-10)):
+        o.step(n)
+        say("C5 oracle stepped")
+        e.step(n)
+        assert e.get_time() == o.get_time()
+        check_close(e, o, rc, NH_FIELDS, tol, tol, f"C5 {e.get_time()[0]} steps")
+
+
+def test_n2_vs_oracle():
+    """N2 (96x96x41 NH): 1 step at rel-max 1e-11, 3 steps at 1e-10."""
+    rc = CONFIGS["N2"]
+    data = icbc.generate_nh(rc)
+    o, e = oracle(rc, data), engine(rc, data)
+    o.step(1)
+    e.step(1)
+    check_close(e, o, rc, NH_FIELDS, 1e-11, 1e-11, "N2 1 step")
+    o.step(2)
+    e.step(2)
+    check_close(e, o, rc, NH_FIELDS, 1e-10, 1e-10, "N2 3 steps")
