@@ -232,6 +232,21 @@ int rcmdyn_synchronize(rcmdyn_t* h);
  * owned tiles, Main/mod_tendency.F90:1449-1459), out[2]=1 if ptntot is NaN. */
 int rcmdyn_diagnostics(rcmdyn_t* h, double out[4]);
 
+/* The 3-hourly report of tend and sound (syncro_rep, Main/mod_tendency.F90:705-725,
+ * Main/mod_sound.F90:634-646), reduced over every tile of the job (sumall / maxall: the
+ * engine's own tiles, then RCCL across ranks; collective in RCCL mode -- every rank calls
+ * it): out[0] = sum of |pten| (ptntot), out[1] = sum of the 2nd time derivative of p*
+ * (pt2tot) over the interior points of the last step (the host multiplies both by its
+ * rptn = 1/npoints, :715-716); out[2] = NH: the maximum sigma-velocity CFL of the last
+ * acoustic sub-step (maxall(cfl), :637), 0 for the hydrostatic core. */
+int rcmdyn_reductions(rcmdyn_t* h, double out[3]);
+
+/* Which runtime libraries the engine's calls are bound to: "hip=<path>; rccl=<path>
+ * (<version>)" into buf (NUL-terminated, at most len bytes).  In a PyTorch process the
+ * already-loaded libamdhip64.so.7 / librccl.so.1 (torch's copies, same sonames) are the
+ * ones bound when torch was imported first; otherwise ROCm's (/opt/rocm/lib). */
+int rcmdyn_runtime_info(char* buf, int32_t len);
+
 /* Multi-process: rank 0 creates the id, the host broadcasts it (MPI / torch.distributed),
  * every rank passes it in rcmdyn_config.comm_unique_id. */
 int rcmdyn_comm_unique_id(uint8_t out[128]);

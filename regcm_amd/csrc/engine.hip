@@ -9,6 +9,7 @@
 // device exchange through a ghost-fill kernel, tiles on other ranks through RCCL
 // (comm.hip).
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 
 #include <algorithm>
 #include <cmath>
@@ -245,7 +246,16 @@ struct rcmdyn_engine {
   const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
   std::string err;
   std::unique_ptr<Comm> comm;
+  // RCMDYN_FORCE_RCCL=1: the halo messages between tiles held by this engine travel as RCCL
+  // sends/receives to itself (one-rank communicator), not as device copies
+  const bool force_rccl = std::getenv("RCMDYN_FORCE_RCCL") != nullptr;
   int device = 0;
+  // halo/compute overlap: the second stream carries the atm2 part of the prologue exchange
+  // while the first computes what needs only atm1 and p* (xch_begin / xch_join)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t evfork = nullptr, evjoin = nullptr;
+  bool join_pending = false;
+  bool on2 = false;           // an exchange is being issued on stream2 (its staging buffers)
 
   std::vector<NHFields> nhf;   // non-hydrostatic buffers of each owned tile (idynamic = 2)
   double* nh_gbuf = nullptr;   // global-indexed day-alarm terms of the radiative condition
@@ -406,6 +416,10 @@ struct rcmdyn_engine {
     staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 32 * (kz + 1));
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
+    if (cfg.nproc_j * cfg.nproc_i > 1) {
+      t.sbuf2 = dalloc(t, staging_cap);
+      t.rbuf2 = dalloc(t, staging_cap);
+    }
     // column blocks of k_columns (one noise partial each)
     // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
     t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
@@ -449,10 +463,12 @@ struct rcmdyn_engine {
     if (nhf.empty()) {                 // engine-wide: mask, CFL slots, day-alarm gather buffer
       f.tmask = dalloc(t, 169);
       f.cfl = talloc<unsigned long long>(t, NH_CFL_SLOTS);
+      f.cfll = talloc<unsigned long long>(t, NH_CFL_SLOTS);
       nh_gbuf = dalloc(t, 2 * (size_t)cfg.jx * cfg.iy);
     } else {
       f.tmask = nhf[0].tmask;
       f.cfl = nhf[0].cfl;
+      f.cfll = nhf[0].cfll;
     }
     if (ntiles > 1) t.westore = dalloc(t, t.gw.plane);
     nhf.push_back(f);
@@ -560,7 +576,13 @@ struct rcmdyn_engine {
     std::memset(hflags, 0, sizeof(FlagSnap) * NFLAGSLOT);
     HIPCHK(hipHostGetDevicePointer((void**)&dflags, hflags, 0));
     for (auto& e : fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg, stream));
+    if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg));
+    else if (force_rccl && ntiles > 1) comm.reset(make_rccl_self_comm());
+    if (ntiles > 1) {
+      HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&evfork, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&evjoin, hipEventDisableTiming));
+    }
   }
 
   void destroy() {
@@ -577,6 +599,9 @@ struct rcmdyn_engine {
     if (ds) hipFree(ds);
     if (red) hipFree(red);
 
+    if (evfork) (void)hipEventDestroy(evfork);
+    if (evjoin) (void)hipEventDestroy(evjoin);
+    if (stream2) (void)hipStreamDestroy(stream2);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -987,12 +1012,15 @@ struct rcmdyn_engine {
   void exchange_generic(const SegFn& fn, const std::function<bool(int)>& send_on,
                         const std::function<bool(int)>& recv_on) {
     if (ntiles == 1) return;
+    // staging of the stream this exchange is issued on (the two streams' exchanges overlap)
+    auto SB = [&](Tile& x) { return on2 ? x.sbuf2 : x.sbuf; };
+    auto RB = [&](Tile& x) { return on2 ? x.rbuf2 : x.rbuf; };
     std::vector<Layout> S, R;
     for (auto& t : tiles) {
       S.push_back(layout(t, fn, true, send_on));
       R.push_back(layout(t, fn, false, recv_on));
     }
-    for (size_t q = 0; q < tiles.size(); q++) launch_segs(S[q].segs, tiles[q].sbuf, 0);
+    for (size_t q = 0; q < tiles.size(); q++) launch_segs(S[q].segs, SB(tiles[q]), 0);
     std::vector<Xfer> sends, recvs;
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
@@ -1000,24 +1028,32 @@ struct rcmdyn_engine {
         const int p = peer_of(t, d);
         if (p < 0) continue;
         Tile* pt = local_tile(p);
+        if (S[q].count[d] && pt && force_rccl && comm) {
+          // one-rank communicator: the n-th send to self matches the n-th receive
+          const size_t pq = pt - tiles.data();
+          if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
+          sends.push_back({comm->rank(), SB(t) + S[q].start[d], (size_t)S[q].count[d]});
+          recvs.push_back({comm->rank(), RB(*pt) + R[pq].start[OPP[d]], (size_t)S[q].count[d]});
+          continue;
+        }
         if (S[q].count[d]) {
           if (pt) {
             const size_t pq = pt - tiles.data();
             if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
-            HIPCHK(hipMemcpyAsync(pt->rbuf + R[pq].start[OPP[d]], t.sbuf + S[q].start[d],
+            HIPCHK(hipMemcpyAsync(RB(*pt) + R[pq].start[OPP[d]], SB(t) + S[q].start[d],
                                   S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
           } else {
-            sends.push_back({p, t.sbuf + S[q].start[d], (size_t)S[q].count[d]});
+            sends.push_back({p, SB(t) + S[q].start[d], (size_t)S[q].count[d]});
           }
         }
-        if (R[q].count[d] && !pt) recvs.push_back({p, t.rbuf + R[q].start[d], (size_t)R[q].count[d]});
+        if (R[q].count[d] && !pt) recvs.push_back({p, RB(t) + R[q].start[d], (size_t)R[q].count[d]});
       }
     }
     if (!sends.empty() || !recvs.empty()) {
       if (!comm) throw std::runtime_error("rcmdyn: remote neighbour without a communicator");
-      comm->sendrecv(sends, recvs);
+      comm->sendrecv(sends, recvs, stream);
     }
-    for (size_t q = 0; q < tiles.size(); q++) launch_segs(R[q].segs, tiles[q].rbuf, 1);
+    for (size_t q = 0; q < tiles.size(); q++) launch_segs(R[q].segs, RB(tiles[q]), 1);
   }
 
   Seg field_seg(Tile& t, double* p, int nk, int d, int w, bool send) {
@@ -1047,6 +1083,38 @@ struct rcmdyn_engine {
     };
     auto all = [](int) { return true; };
     exchange_generic(fn, all, all);
+  }
+
+  // Halo/compute overlap (north star): issue an exchange point on the second
+  // stream, forked from the first at this point of the step; the first stream goes on with
+  // kernels that do not read these fields' ghost rings and waits for it in xch_join.  Both
+  // streams' RCCL calls go to one communicator in the same order on every rank; captured
+  // into the step graph as a fork/join.
+  void fork_point() {
+    if (ntiles == 1) return;
+    HIPCHK(hipEventRecord(evfork, stream));
+  }
+  void xch_begin(std::vector<XField> fs) {
+    if (ntiles == 1) return;
+    HIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
+    std::swap(stream, stream2);
+    on2 = true;
+    try {
+      xchv(std::move(fs));
+    } catch (...) {
+      on2 = false;
+      std::swap(stream, stream2);
+      throw;
+    }
+    on2 = false;
+    std::swap(stream, stream2);
+    HIPCHK(hipEventRecord(evjoin, stream2));
+    join_pending = true;
+  }
+  void xch_join() {
+    if (!join_pending) return;
+    HIPCHK(hipStreamWaitEvent(stream, evjoin, 0));
+    join_pending = false;
   }
 
   // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
@@ -1231,12 +1299,15 @@ struct rcmdyn_engine {
     // isladvec = 1: k_sladv forms ud*msfd two points out (the reference exchanges atmx%ud 2
     // wide, :995-997) and interpolates atm2 qx up to three points out (max(idif, 4), :1073-1075)
     const int wu = cfg.isladvec == 1 ? 2 : 1, wq = cfg.isladvec == 1 ? 3 : 2;
+    // atm2 on the second stream, overlapped with decouple and compute_omega (atm1 only)
     std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz},
-                            {FK::A1QV, kz}, {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}, {FK::A2U, kz, 2},
-                            {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, wq}, {FK::A2QC, kz, wq},
-                            {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}};
-    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro.push_back({FK::A2TKE, kp, 2}); }
+                            {FK::A1QV, kz}, {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}};
+    std::vector<XField> pro2{{FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, wq},
+                             {FK::A2QC, kz, wq}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}};
+    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro2.push_back({FK::A2TKE, kp, 2}); }
+    fork_point();
     xchv(pro);
+    xch_begin(pro2);
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
@@ -1244,6 +1315,12 @@ struct rcmdyn_engine {
       KLAUNCH(k_surface_pressures, grid3(g.nj, g.ni, 1), BLK, 0, stream, g, fields(t));
       KLAUNCH(k_nh_decouple, q.fr, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_omega, q.ce1, BLK, 0, stream, g, dc, f);
+    });
+    xch_join();
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      const NHFields f = nhfields(t);
+      const Grids q = grids(g);
       KLAUNCH(k_nh_mkslice, q.fr, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
     });
@@ -1310,7 +1387,7 @@ struct rcmdyn_engine {
           each([&](Tile& t) {
             KLAUNCH(k_nh_tmask_gather, grids(t.g).ci1, BLK, 0, stream, t.g, dc, nhfields(t), nh_gbuf);
           });
-          if (comm) comm->allreduce_sum(nh_gbuf, 2 * (size_t)cfg.jx * cfg.iy);
+          if (comm) comm->allreduce_sum(nh_gbuf, 2 * (size_t)cfg.jx * cfg.iy, stream);
           KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, tiles[0].g, dc, nh_gbuf, nhf[0].tmask);
           nh_tmask_valid = true;
         }
@@ -1327,7 +1404,7 @@ struct rcmdyn_engine {
           KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, f);
         else
           KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, g, f.estore, dc, f);
-        KLAUNCH(k_nh_sound_c2, q.cik, BLK, 0, stream, g, dc, ds, f, istep);
+        KLAUNCH(k_nh_sound_c2, q.cik, BLK, 0, stream, g, dc, ds, f, istep, (int)(it == istep));
       });
     }
     each([&](Tile& t) {
@@ -1388,12 +1465,17 @@ struct rcmdyn_engine {
     // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
     // atm1 travels 2 wide and atm2 3 wide: one more than the reference's widths, for the
     // ghost rings the kernels below compute in place of the later exchanges
+    // The atm2 part travels on the second stream while k_surface_pressures and k_columns,
+    // which read only atm1 and p*, run (halo/compute overlap); joined before k_momentum.
     std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2},
-                            {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}, {FK::A2U, kz, 3}, {FK::A2V, kz, 3},
-                            {FK::A2T, kz, 3}, {FK::A2QV, kz, 3}, {FK::A2QC, kz, 3}};
+                            {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}};
+    std::vector<XField> pro2{{FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
+                             {FK::A2QC, kz, 3}};
     // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
-    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro.push_back({FK::A2TKE, kz + 1, 2}); }
+    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro2.push_back({FK::A2TKE, kz + 1, 2}); }
+    fork_point();
     xchv(pro);
+    xch_begin(pro2);
     ghosts_stale = false;
     // surface_pressures + 2-D reciprocals, :815-834
     each([&](Tile& t) {
@@ -1405,6 +1487,7 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);
     });
+    xch_join();
     if (slice) run_slice();
   }
 
@@ -1685,6 +1768,26 @@ struct rcmdyn_engine {
     hs.lcount = lcount; hs.dt = dt; hs.xbctime = xbctime;
   }
 
+  void reductions(double out[3]) {
+    check(0);
+    HIPCHK(hipStreamSynchronize(stream));
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    out[0] = st.ptntot; out[1] = st.pt2tot; out[2] = cfg.idynamic == 2 ? st.cflmax : 0.0;
+    if (comm && cfg.tile_count < ntiles) {        // sumall / maxall over the ranks
+      double* d = nullptr;
+      HIPCHK(hipMalloc(&d, 3 * sizeof(double)));
+      double hv[3] = {out[0], out[1], out[2]};
+      HIPCHK(hipMemcpy(d, hv, sizeof(hv), hipMemcpyHostToDevice));
+      comm->allreduce_sum(d, 2, stream);
+      comm->allreduce_max_d(d + 2, 1, stream);
+      HIPCHK(hipStreamSynchronize(stream));
+      HIPCHK(hipMemcpy(hv, d, sizeof(hv), hipMemcpyDeviceToHost));
+      (void)hipFree(d);
+      out[0] = hv[0]; out[1] = hv[1]; out[2] = hv[2];
+    }
+  }
+
   void diagnostics(double out[4]) {
     HIPCHK(hipStreamSynchronize(stream));
     StepState st;
@@ -1818,6 +1921,24 @@ int rcmdyn_synchronize(rcmdyn_t* h) {
 }
 
 int rcmdyn_diagnostics(rcmdyn_t* h, double out[4]) { return guard(h, [&] { h->diagnostics(out); }); }
+
+int rcmdyn_reductions(rcmdyn_t* h, double out[3]) { return guard(h, [&] { h->reductions(out); }); }
+
+int rcmdyn_runtime_info(char* buf, int32_t len) {
+  try {
+    Dl_info info{};
+    std::string hip = dladdr((void*)&hipGetDeviceCount, &info) && info.dli_fname ? info.dli_fname : "?";
+    std::string s = "hip=" + hip + "; rccl=" + rccl_describe();
+    if (buf && len > 0) {
+      std::strncpy(buf, s.c_str(), (size_t)len - 1);
+      buf[len - 1] = 0;
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return 1;
+  }
+}
 
 int rcmdyn_comm_unique_id(uint8_t out[128]) {
   try {

@@ -106,6 +106,8 @@ struct StepState {
   double xbctime;     // s since boundary interval start
   long long lcount;   // completed steps
   double ptntot, pt2tot;
+  double cflmax;      // NH: max sigma-velocity CFL of the last acoustic sub-step
+                      // (Main/mod_sound.F90:619-646); 0 for the hydrostatic core
   int nanflag;        // sticky: set when a step produced NaN ptntot
   int slflag;         // sticky: a semi-Lagrangian departure point beyond one cell
 };
@@ -170,6 +172,7 @@ struct Tile {
   double *psdot0 = nullptr;
   // halo staging buffers
   double *sbuf = nullptr, *rbuf = nullptr;
+  double *sbuf2 = nullptr, *rbuf2 = nullptr;   // of the exchange on the engine's second stream
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials
   int ncolx = 0;                   // k_columns blocks per row
   std::vector<void*> allocs;

@@ -1034,7 +1034,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, Geom ge, const doub
 // D2, one thread per interior cross point and level: CFL of the sigma velocity (:624-640),
 // the new pp (:661-674) and its temperature correction (:675-681)
 __global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep) {
+                              int istep, int last) {
   THREAD_POINT(g.jci1, g.ici1);
   const bool active = IN_CI(j, i);
   const double dt = s->dt, dts = dt / (double)istep;
@@ -1065,7 +1065,10 @@ __global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepSt
     unsigned long long b = sred[0];
     for (int q = 1; q < 4; q++) b = (sred[q] > b) ? sred[q] : b;
     const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * 7919u) & (NH_CFL_SLOTS - 1);
-    if (b != 0ull) atomicMax(&f.cfl[slot], b);
+    if (b != 0ull) {
+      atomicMax(&f.cfl[slot], b);
+      if (last) atomicMax(&f.cfll[slot], b);
+    }
   }
   if (!active) return;
   const double ppold = F3(f.spi, j, i, k);
@@ -1118,22 +1121,29 @@ __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields 
 // rcmtimer advance and the sound CFL stop (Main/mod_sound.F90:661-682,
 // Main/mod_tendency.F90:608-616)
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f) {
-  __shared__ unsigned long long sm[256];
-  unsigned long long b = 0ull;
+  __shared__ unsigned long long sm[256], sl[256];
+  unsigned long long b = 0ull, bl = 0ull;
   for (int q = threadIdx.x; q < NH_CFL_SLOTS; q += blockDim.x) {
-    const unsigned long long v = f.cfl[q];
+    const unsigned long long v = f.cfl[q], vl = f.cfll[q];
     b = (v > b) ? v : b;
+    bl = (vl > bl) ? vl : bl;
     f.cfl[q] = 0ull;
+    f.cfll[q] = 0ull;
   }
   sm[threadIdx.x] = b;
+  sl[threadIdx.x] = bl;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) sm[threadIdx.x] = (sm[threadIdx.x + w] > sm[threadIdx.x]) ? sm[threadIdx.x + w] : sm[threadIdx.x];
+    if ((int)threadIdx.x < w) {
+      sm[threadIdx.x] = (sm[threadIdx.x + w] > sm[threadIdx.x]) ? sm[threadIdx.x + w] : sm[threadIdx.x];
+      sl[threadIdx.x] = (sl[threadIdx.x + w] > sl[threadIdx.x]) ? sl[threadIdx.x + w] : sl[threadIdx.x];
+    }
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
   const double cfl = __longlong_as_double((long long)sm[0]);
   if (cfl > d_one || cfl != cfl) s->nanflag = 1;
+  s->cflmax = __longlong_as_double((long long)sl[0]);
   s->lcount += 1;
   if (s->lcount == 2) s->dt = d_two * c->dtsec;
   s->ptntot = 0.0;

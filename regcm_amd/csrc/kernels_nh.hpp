@@ -42,6 +42,8 @@ struct NHFields {
   double *scc, *scdd, *scj, *spi, *estore, *astore, *tmask;
   unsigned long long* cfl;       // NH_CFL_SLOTS partial maxima of the step's CFL (non-negative
                                  // doubles as ordered bits), reduced by k_nh_advance
+  unsigned long long* cfll;      // the same for the last acoustic sub-step alone (the value
+                                 // the reference reports, Main/mod_sound.F90:634-646)
 };
 constexpr int NH_CFL_SLOTS = 1024;
 
@@ -70,7 +72,7 @@ __global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
 __global__ void k_nh_sound_c1(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
 __global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);

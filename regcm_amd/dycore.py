@@ -29,7 +29,7 @@ EXPORTED = [
     "rcmdyn_tile_extent", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
-    "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin",
+    "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin", "rcmdyn_reductions", "rcmdyn_runtime_info",
 ]
 
 
@@ -69,6 +69,8 @@ def lib():
     L.rcmdyn_comm_unique_id.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
     L.rcmdyn_last_step_ms.argtypes = [P, dp]
     L.rcmdyn_set_diagnostics.argtypes = [P, i32]
+    L.rcmdyn_reductions.argtypes = [P, dp]
+    L.rcmdyn_runtime_info.argtypes = [ctypes.c_char_p, i32]
     L.rcmdyn_kernel_times.argtypes = [P, i32, i32, ctypes.c_char_p, ctypes.POINTER(i32), dp, ctypes.POINTER(i32)]
     _lib = L
     return L
@@ -87,6 +89,14 @@ def tile_extent(jx: int, iy: int, nproc_j: int, nproc_i: int, tile: int):
     if lib().rcmdyn_tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy):
         raise EngineError("rcmdyn_tile_extent failed")
     return list(ext), list(bdy)
+
+
+def runtime_info() -> str:
+    """Paths (and RCCL version) of the HIP runtime and librccl the engine is bound to."""
+    buf = ctypes.create_string_buffer(1024)
+    if lib().rcmdyn_runtime_info(buf, 1024):
+        raise EngineError(lib().rcmdyn_last_error(None).decode())
+    return buf.value.decode()
 
 
 def comm_unique_id() -> bytes:
@@ -177,6 +187,13 @@ class DynCore:
         out = (ctypes.c_double * 4)()
         self._check(lib().rcmdyn_diagnostics(self.h, out))
         return list(out)
+
+    def reductions(self):
+        """(ptntot, pt2tot, cflmax) of the last step over the whole job (the 3-hourly report,
+        Main/mod_tendency.F90:705-725, Main/mod_sound.F90:634-646); collective over ranks."""
+        out = (ctypes.c_double * 3)()
+        self._check(lib().rcmdyn_reductions(self.h, out))
+        return tuple(out)
 
     def last_step_ms(self) -> float:
         v = ctypes.c_double()

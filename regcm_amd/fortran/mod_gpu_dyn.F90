@@ -139,6 +139,12 @@ module mod_gpu_dyn
       type(c_ptr), value :: h
       integer(c_int32_t), value :: n
     end function
+    ! the 3-hourly report sums (sumall/maxall over the job): ptntot, pt2tot, NH max CFL
+    integer(c_int) function rcmdyn_reductions(h, out) bind(c, name='rcmdyn_reductions')
+      import :: c_int, c_ptr, c_double
+      type(c_ptr), value :: h
+      real(c_double), intent(out) :: out(3)
+    end function
     integer(c_int) function rcmdyn_diagnostics(h, out) bind(c, name='rcmdyn_diagnostics')
       import :: c_int, c_ptr, c_double
       type(c_ptr), value :: h
@@ -151,7 +157,7 @@ module mod_gpu_dyn
   end interface
 
   public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
-  public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics
+  public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics, rcmdyn_reductions
   public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics, rcmdyn_bdyin
   public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d
 
