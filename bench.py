@@ -135,7 +135,7 @@ def main():
     data = icbc.generate_nh(rc) if nh else icbc.generate(rc)
     cj, ci = set_nproc(world, rc.jx, rc.iy)
 
-    from regcm_amd.dycore import DynCore, comm_unique_id
+    from regcm_amd.dycore import DynCore, comm_unique_id, runtime_info
     dist = None
     if world > 1:
         import torch
@@ -256,6 +256,7 @@ def main():
         "device_ms_per_step": dev_ms,
         "dropin_ms_per_step": wall_d / args.steps * 1e3,
         "dropin_note": "rcmdyn_tend + rcmdyn_bdyval per step (INTEGRATION.md section 4), timed like value",
+        "runtime": runtime_info(),
     }
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(rc, data, args.cpu_budget)

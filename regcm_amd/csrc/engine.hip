@@ -231,6 +231,17 @@ struct rcmdyn_engine {
   hipEvent_t fev[NFLAGSLOT] = {};
   std::deque<long long> pending;
   static constexpr int FLAG_LAG = 2;
+  // with a communicator the flags are max-reduced over the ranks every GLOBAL_EVERY steps
+  // (and at the end of every rcmdyn_step) and only the reduced word raises the error, so
+  // every rank stops at the same step -- the reference's fatal aborts the whole job
+  // (Main/abort.F90:20-36); a rank stopping alone would leave its neighbours waiting
+  static constexpr int GLOBAL_EVERY = 8;
+  int32_t* derr = nullptr;
+  int32_t* hgerr = nullptr;
+  int32_t* dgerr = nullptr;
+  hipEvent_t gev[NFLAGSLOT] = {};
+  std::deque<std::pair<long long, int>> gpending;   // (step, slot)
+  int gslot = 0;
   bool statics_dirty = true;
   bool bdy_dirty = true;
   bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
@@ -578,6 +589,13 @@ struct rcmdyn_engine {
     for (auto& e : fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg));
     else if (force_rccl && ntiles > 1) comm.reset(make_rccl_self_comm());
+    if (comm) {
+      HIPCHK(hipMalloc(&derr, sizeof(int32_t)));
+      HIPCHK(hipHostMalloc((void**)&hgerr, sizeof(int32_t) * NFLAGSLOT, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(hgerr, 0, sizeof(int32_t) * NFLAGSLOT);
+      HIPCHK(hipHostGetDevicePointer((void**)&dgerr, hgerr, 0));
+      for (auto& e : gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
     if (ntiles > 1) {
       HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&evfork, hipEventDisableTiming));
@@ -589,8 +607,12 @@ struct rcmdyn_engine {
     if (stream) (void)hipStreamSynchronize(stream);
     invalidate_graphs();
     for (auto& e : fev)
-      if (e) hipEventDestroy(e);
-    if (hflags) hipHostFree(hflags);
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : gev)
+      if (e) (void)hipEventDestroy(e);
+    if (hflags) (void)hipHostFree(hflags);
+    if (hgerr) (void)hipHostFree(hgerr);
+    if (derr) (void)hipFree(derr);
     for (auto& t : tiles)
       for (void* p : t.allocs) hipFree(p);
     tiles.clear();
@@ -612,17 +634,54 @@ struct rcmdyn_engine {
   }
 
   // ------------------------------------------------------------------ step error flags
-  // a tend was issued whose clock is lc once it ran: remember its snapshot slot
-  void note_step(long long lc) {
+  // a tend was issued whose clock is lc once it ran: remember its snapshot slot; with a
+  // communicator, every GLOBAL_EVERY steps (or when `global`) issue the job-wide reduction
+  void note_step(long long lc, bool global = false) {
+    if (comm) {
+      if (global || lc % GLOBAL_EVERY == 0) {
+        if ((int)gpending.size() >= NFLAGSLOT - 1) check(0);
+        const int slot = gslot++ % NFLAGSLOT;
+        hipLaunchKernelGGL(k_err_gather, dim3(1), dim3(64), 0, stream, ds, derr);
+        comm->allreduce_max(derr, 1, stream);
+        hipLaunchKernelGGL(k_err_publish, dim3(1), dim3(64), 0, stream, derr, dgerr + slot);
+        HIPCHK(hipEventRecord(gev[slot], stream));
+        gpending.push_back({lc, slot});
+      }
+      return;
+    }
     if ((int)pending.size() >= NFLAGSLOT - 1) check(0);
     HIPCHK(hipEventRecord(fev[(lc - 1 + NFLAGSLOT) % NFLAGSLOT], stream));
     pending.push_back(lc);
   }
-  // check the flags of the oldest steps until at most `keep` stay unchecked; on a failure
-  // the stream drains, the sticky device flags are cleared (reported once) and the error
-  // is raised -- the reference's fatal (Main/mod_tendency.F90:702, Main/mod_sound.F90:679-681,
-  // Main/mod_sladvection.F90:149-154)
+  // a failure: the stream drains, the sticky device flags are cleared (reported once) and
+  // the error is raised -- the reference's fatal (Main/mod_tendency.F90:702,
+  // Main/mod_sound.F90:679-681, Main/mod_sladvection.F90:149-154)
+  [[noreturn]] void fail(int sl, long long lc, const std::string& scope) {
+    HIPCHK(hipStreamSynchronize(stream));
+    pending.clear();
+    gpending.clear();
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    st.nanflag = 0; st.slflag = 0;
+    HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
+    const std::string at = " (" + scope + std::to_string(lc) + ")";
+    if (sl) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell" + at);
+    throw std::runtime_error("CFL VIOLATION" + at);
+  }
+  // check the flags of the oldest steps until at most `keep` stay unchecked (with a
+  // communicator: the reduced words, one reduction interval behind unless keep = 0)
   void check(size_t keep) {
+    if (comm) {
+      const size_t gkeep = keep == 0 ? 0 : 1;
+      while (gpending.size() > gkeep) {
+        const auto [lc, slot] = gpending.front();
+        HIPCHK(hipEventSynchronize(gev[slot]));
+        gpending.pop_front();
+        const int w = ((volatile int32_t*)hgerr)[slot];
+        if (w) fail(w & 2, lc, "job, by step ");
+      }
+      return;
+    }
     while (pending.size() > keep) {
       const long long lc = pending.front();
       const int slot = (int)((lc - 1 + NFLAGSLOT) % NFLAGSLOT);
@@ -630,18 +689,10 @@ struct rcmdyn_engine {
       pending.pop_front();
       const volatile FlagSnap* f = hflags + slot;
       const int sl = f->slflag, nan = f->nanflag;
-      if (!sl && !nan) continue;
-      HIPCHK(hipStreamSynchronize(stream));
-      pending.clear();
-      StepState st;
-      HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
-      st.nanflag = 0; st.slflag = 0;
-      HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
-      const std::string at = " (step " + std::to_string(lc) + ")";
-      if (sl) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell" + at);
-      throw std::runtime_error("CFL VIOLATION" + at);
+      if (sl || nan) fail(sl, lc, "step ");
     }
   }
+
 
   // ------------------------------------------------------------------ field access
   double* fptr(Tile& t, FK f) {
@@ -1665,7 +1716,7 @@ struct rcmdyn_engine {
         tend();
         bdyval();
       }
-      note_step(hs.lcount);
+      note_step(hs.lcount, s == n - 1);
     }
     HIPCHK(hipEventRecord(e1, stream));
     HIPCHK(hipEventSynchronize(e1));
@@ -1761,6 +1812,7 @@ struct rcmdyn_engine {
   void set_time(long long lcount, double dt, double xbctime) {
     HIPCHK(hipStreamSynchronize(stream));
     pending.clear();
+    gpending.clear();
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
     st.lcount = lcount; st.dt = dt; st.xbctime = xbctime; st.nanflag = 0; st.slflag = 0;
@@ -1915,6 +1967,7 @@ int rcmdyn_step(rcmdyn_t* h, int32_t nsteps) { return guard(h, [&] { h->step(nst
 
 int rcmdyn_synchronize(rcmdyn_t* h) {
   return guard(h, [&] {
+    if (h->comm) h->note_step(h->hs.lcount, true);   // collective: every rank synchronizes
     HIPCHK(hipStreamSynchronize(h->stream));
     h->check(0);
   });

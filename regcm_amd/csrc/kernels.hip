@@ -1760,6 +1760,15 @@ __global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring)
   r.lcount = lc;
 }
 
+// the sticky error flags as one word for the RCCL max-reduction of a multi-rank job, and the
+// reduced word into the host-mapped slot the host checks
+__global__ void k_err_gather(const StepState* __restrict__ s, int32_t* derr) {
+  if (threadIdx.x == 0) derr[0] = s->nanflag | (s->slflag << 1);
+}
+__global__ void k_err_publish(const int32_t* __restrict__ derr, int32_t* hslot) {
+  if (threadIdx.x == 0) hslot[0] = derr[0];
+}
+
 // ---------------------------------------------------------------------------------------
 // static derived fields: Main/mod_params.F90:1993-2001 (xmsf, dmsf), Main/mod_diffusion.F90:
 // 124-140 (hgfact), Main/mod_split.F90:99-101 (map)

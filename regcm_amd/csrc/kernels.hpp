@@ -92,6 +92,8 @@ struct BdyArgs {
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a);
 __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance);
 __global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring);
+__global__ void k_err_gather(const StepState* __restrict__ s, int32_t* derr);
+__global__ void k_err_publish(const int32_t* __restrict__ derr, int32_t* hslot);
 __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu_hgtf, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ ht, double* xmsf, double* dmsf, double* hgfact, double* mapf);
 __global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack);
 __global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restrict__ src, long sstride, double* dst, long dstride);

@@ -88,3 +88,22 @@ def test_reductions_report(c1_data):
     d = o.diagnostics()
     assert np.allclose(r[:2], d[:2], rtol=1e-10, atol=0), (r, d)
     assert r[0] > 0.0 and r[1] > 0.0
+
+
+def test_rccl_job_wide_cfl_stop(c1_data, monkeypatch):
+    """With a communicator the error flags are max-reduced over the ranks every 8 steps
+    (GLOBAL_EVERY) and only the reduced word stops the run, so every rank fails at the same
+    call, as the reference's fatal aborts the whole job (Main/abort.F90:20-36)."""
+    from regcm_amd.dycore import EngineError
+    rc, data = c1_data
+    st = {k: v.copy() for k, v in data["state"].items()}
+    for name in ("ATM1_T", "ATM2_T"):
+        st[name][5, 20:24, 20:24] = np.nan
+    monkeypatch.setenv("RCMDYN_FORCE_RCCL", "1")
+    from regcm_amd.dycore import DynCore
+    e = DynCore(rc, data["split"], nproc_j=2, nproc_i=2)
+    e.put_state(st)
+    e.bdyval()
+    with pytest.raises(EngineError, match=r"CFL VIOLATION \(job, by step (8|16)\)"):
+        e.step(100)
+    assert e.get_time()[0] <= 24
