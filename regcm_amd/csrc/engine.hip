@@ -1505,7 +1505,8 @@ struct rcmdyn_engine {
       if (phase & TEND_PRE) tend_pre(slice);
       if (phase & TEND_POST) tend_post();
     }
-    if (phase & TEND_POST) KLAUNCH(k_flag_snapshot, dim3(1), dim3(64), 0, stream, ds, dflags);
+    // the hydrostatic step's snapshot is written by k_split_correct's clock lane
+    if ((phase & TEND_POST) && cfg.idynamic == 2) KLAUNCH(k_flag_snapshot, dim3(1), dim3(64), 0, stream, ds, dflags);
   }
 
   void tend_pre(bool slice) {
@@ -1626,7 +1627,7 @@ struct rcmdyn_engine {
       const int c = t.cur;
       KLAUNCH(k_split_correct, grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz), BLK, 0, stream, g,
                          dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
-                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total);
+                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total, dflags);
     }
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;

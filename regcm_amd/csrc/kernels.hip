@@ -1457,11 +1457,12 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                 const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
                                 double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
-                                int advance, const double* __restrict__ red, int red_total) {
+                                int advance, const double* __restrict__ red, int red_total, FlagSnap* ring) {
   THREAD_POINT(g.jde1, g.ide1);
   // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
   // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch
-  // (:608-616); nothing else here reads the clock
+  // (:608-616); nothing else here reads the clock.  The same lane then copies the step's error
+  // flags into the host-mapped ring (k_flag_snapshot's work; this is the step's last flag writer)
   if (advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
     __shared__ double sa[256], sb[256];
     const int t = threadIdx.y * blockDim.x + threadIdx.x;
@@ -1479,6 +1480,11 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
       if (sa[0] != sa[0]) s->nanflag = 1;
       s->lcount = s->lcount + 1;
       if (s->lcount == 2) s->dt = d_two * c->dtsec;
+      const long long lc = s->lcount;
+      FlagSnap& r = ring[(lc - 1 + NFLAGSLOT) % NFLAGSLOT];
+      r.nanflag = s->nanflag;
+      r.slflag = s->slflag;
+      r.lcount = lc;
     }
   }
   // two adjacent points (jp, jp+1) per thread, 16-byte accesses (jp - j0 is even); owned points

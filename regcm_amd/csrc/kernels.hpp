@@ -80,7 +80,7 @@ __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_fused(Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
-__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total);
+__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring);
 // pointers of bdyval (k_bdyval_set)
 struct BdyArgs {
   double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc, *psa, *psb;

@@ -5,8 +5,10 @@ SURVEY.md section 8(e), and of the NH core).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 tools/rccl_check.py --config C1 --steps 6
 
-Ranks use device local_rank modulo the visible device count, so the check also runs with
-several ranks on one GPU (the RCCL transport then moves the halos within the device).
+Each rank needs a device of its own: RCCL refuses two ranks of one communicator on the same
+GPU (ncclCommInitRank: invalid usage), so the check exits early, with a message, when fewer
+devices than ranks are visible.  On a one-GPU box the RCCL transport is exercised instead by
+the one-rank self communicator (RCMDYN_FORCE_RCCL, tests/test_rccl_gpu.py).
 Rank 0 prints one JSON line and exits non-zero on a mismatch.
 """
 import argparse
@@ -35,8 +37,12 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = max(torch.cuda.device_count(), 1)
-    dev = local_rank % ndev
+    ndev = torch.cuda.device_count()
+    if ndev < world:
+        print(f"rccl_check: {world} ranks need {world} GPUs, {ndev} visible (RCCL allows one rank per "
+              "device); use tests/test_rccl_gpu.py on a one-GPU box", file=sys.stderr, flush=True)
+        sys.exit(2)
+    dev = local_rank
     dist.init_process_group(backend="gloo", init_method="env://")
     rc = CONFIGS[args.config]
     nh = rc.idynamic == 2
