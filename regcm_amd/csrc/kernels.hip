@@ -1612,65 +1612,77 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
   const bool dR = g.br && j == g.jde2 && in(i, g.idi1, g.idi2);
   const bool dB = g.bb && i == g.ide1;
   const bool dT = g.bt && i == g.ide2;
-  if (!ghost && (dL || dR || dB || dT)) {
-    if (integ) { a2u[p] = a1u[p]; a2v[p] = a1v[p]; }
-    a1u[p] = ub0[p] + xt * ubt[p];
-    a1v[p] = vb0[p] + xt * vbt[p];
-  }
+  const bool dset = !ghost && (dL || dR || dB || dT);
   // cross-point boundary rows: left/right on ici, bottom/top on the jce range
   const bool cL = g.bl && j == g.jce1 && in(i, g.ici1, g.ici2);
   const bool cR = g.br && j == g.jce2 && in(i, g.ici1, g.ici2);
   const bool cB = g.bb && i == g.ice1 && in(j, g.jce1, g.jce2);
   const bool cT = g.bt && i == g.ice2 && in(j, g.jce1, g.jce2);
-  if (!ghost && (cL || cR || cB || cT)) {
-    if (integ) {
-      a2t[p] = a1t[p]; a2qv[p] = a1qv[p]; a2qc[p] = a1qc[p];
-      if (set_ps && k == 1) psb[q] = psa[q];
-    }
-    if (set_ps && k == 1) psa[q] = pb0[q] + xt * pbt[q];
-    a1t[p] = tb0[p] + xt * tbt[p];
-    a1qv[p] = qb0[p] + xt * qbt[p];
+  const bool cset = !ghost && (cL || cR || cB || cT);
+  const bool ps1 = cset && set_ps && k == 1;
+  // bdyuv slices (the interior slice values are interior points, which nothing here modifies)
+  const bool sW = g.bl && j == g.jde1 && (in(i, g.idi1, g.idi2) || ghost);
+  const bool sE = g.br && j == g.jde2 && (in(i, g.idi1, g.idi2) || ghost);
+  const bool sS = g.bb && i == g.ide1, sSi = sS && (in(j, g.jdi1, g.jdi2) || ghost);
+  const bool sN = g.bt && i == g.ide2, sNi = sN && (in(j, g.jdi1, g.jdi2) || ghost);
+  // ---- every operand first (no load waits behind a store of the same thread), then the stores
+  double ubv = 0.0, vbv = 0.0, u1o = 0.0, v1o = 0.0, t1o = 0.0, qv1o = 0.0, qc1o = 0.0, pso = 0.0;
+  double tbv = 0.0, qbv = 0.0, pbv = 0.0, su = 0.0, sv = 0.0;
+  if (dset || sW || sE || sS || sN) { ubv = ub0[p] + xt * ubt[p]; vbv = vb0[p] + xt * vbt[p]; }
+  if (dset && integ) { u1o = a1u[p]; v1o = a1v[p]; }
+  if (cset) {
+    if (integ) { t1o = a1t[p]; qv1o = a1qv[p]; qc1o = a1qc[p]; }
+    if (ps1) { if (integ) pso = psa[q]; pbv = pb0[q] + xt * pbt[q]; }
+    tbv = tb0[p] + xt * tbt[p];
+    qbv = qb0[p] + xt * qbt[p];
   }
-  // bdyuv slices (interior slice values are interior points: not modified above)
-  if (g.bl && j == g.jde1 && (in(i, g.idi1, g.idi2) || ghost)) {
-    SLI(sl.s[1], i, k) = F3(a1u, g.jdi1, i, k); SLI(sl.s[5], i, k) = F3(a1v, g.jdi1, i, k);
-    SLI(sl.s[0], i, k) = ub0[p] + xt * ubt[p]; SLI(sl.s[4], i, k) = vb0[p] + xt * vbt[p];
-  }
-  if (g.br && j == g.jde2 && (in(i, g.idi1, g.idi2) || ghost)) {
-    SLI(sl.s[3], i, k) = F3(a1u, g.jdi2, i, k); SLI(sl.s[7], i, k) = F3(a1v, g.jdi2, i, k);
-    SLI(sl.s[2], i, k) = ub0[p] + xt * ubt[p]; SLI(sl.s[6], i, k) = vb0[p] + xt * vbt[p];
-  }
-  if (g.bb && i == g.ide1) {
-    if (in(j, g.jdi1, g.jdi2) || ghost) { SLJ(sl.s[9], j, k) = F3(a1u, j, g.idi1, k); SLJ(sl.s[13], j, k) = F3(a1v, j, g.idi1, k); }
-    SLJ(sl.s[8], j, k) = ub0[p] + xt * ubt[p]; SLJ(sl.s[12], j, k) = vb0[p] + xt * vbt[p];
-  }
-  if (g.bt && i == g.ide2) {
-    if (in(j, g.jdi1, g.jdi2) || ghost) { SLJ(sl.s[11], j, k) = F3(a1u, j, g.idi2, k); SLJ(sl.s[15], j, k) = F3(a1v, j, g.idi2, k); }
-    SLJ(sl.s[10], j, k) = ub0[p] + xt * ubt[p]; SLJ(sl.s[14], j, k) = vb0[p] + xt * vbt[p];
-  }
+  if (sW) { su = F3(a1u, g.jdi1, i, k); sv = F3(a1v, g.jdi1, i, k); }
+  else if (sE) { su = F3(a1u, g.jdi2, i, k); sv = F3(a1v, g.jdi2, i, k); }
+  else if (sSi) { su = F3(a1u, j, g.idi1, k); sv = F3(a1v, j, g.idi1, k); }
+  else if (sNi) { su = F3(a1u, j, g.idi2, k); sv = F3(a1v, j, g.idi2, k); }
   // bdyuv corner fills, Main/mod_bdycod.F90:1030-1061: every corner slice entry is the
   // boundary value b0 + xt*bt of a known point, written by the thread of that tile corner
-  if (ghost) return;
+  const bool kTL = !ghost && g.bt && g.bl && j == g.jde1 && i == g.ide2;
+  const bool kBL = !ghost && g.bb && g.bl && j == g.jde1 && i == g.ide1;
+  const bool kTR = !ghost && g.bt && g.br && j == g.jde2 && i == g.ide2;
+  const bool kBR = !ghost && g.bb && g.br && j == g.jde2 && i == g.ide1;
+  double cu1 = 0.0, cv1 = 0.0, cu2 = 0.0, cv2 = 0.0;
 #define UB(J, I) (F3(ub0, J, I, k) + xt * F3(ubt, J, I, k))
 #define VB(J, I) (F3(vb0, J, I, k) + xt * F3(vbt, J, I, k))
-  if (g.bt && g.bl && j == g.jde1 && i == g.ide2) {
-    SLI(sl.s[1], g.ide2, k) = UB(g.jdi1, g.ide2); SLI(sl.s[5], g.ide2, k) = VB(g.jdi1, g.ide2);
-    SLJ(sl.s[11], g.jde1, k) = UB(g.jde1, g.idi2); SLJ(sl.s[15], g.jde1, k) = VB(g.jde1, g.idi2);
-  }
-  if (g.bb && g.bl && j == g.jde1 && i == g.ide1) {
-    SLI(sl.s[1], g.ide1, k) = UB(g.jdi1, g.ide1); SLI(sl.s[5], g.ide1, k) = VB(g.jdi1, g.ide1);
-    SLJ(sl.s[9], g.jde1, k) = UB(g.jde1, g.idi1); SLJ(sl.s[13], g.jde1, k) = VB(g.jde1, g.idi1);
-  }
-  if (g.bt && g.br && j == g.jde2 && i == g.ide2) {
-    SLI(sl.s[3], g.ide2, k) = UB(g.jdi2, g.ide2); SLI(sl.s[7], g.ide2, k) = VB(g.jdi2, g.ide2);
-    SLJ(sl.s[11], g.jde2, k) = UB(g.jde2, g.idi2); SLJ(sl.s[15], g.jde2, k) = VB(g.jde2, g.idi2);
-  }
-  if (g.bb && g.br && j == g.jde2 && i == g.ide1) {
-    SLI(sl.s[3], g.ide1, k) = UB(g.jdi2, g.ide1); SLI(sl.s[7], g.ide1, k) = VB(g.jdi2, g.ide1);
-    SLJ(sl.s[9], g.jde2, k) = UB(g.jde2, g.idi1); SLJ(sl.s[13], g.jde2, k) = VB(g.jde2, g.idi1);
-  }
+  if (kTL) { cu1 = UB(g.jdi1, g.ide2); cv1 = VB(g.jdi1, g.ide2); cu2 = UB(g.jde1, g.idi2); cv2 = VB(g.jde1, g.idi2); }
+  if (kBL) { cu1 = UB(g.jdi1, g.ide1); cv1 = VB(g.jdi1, g.ide1); cu2 = UB(g.jde1, g.idi1); cv2 = VB(g.jde1, g.idi1); }
+  if (kTR) { cu1 = UB(g.jdi2, g.ide2); cv1 = VB(g.jdi2, g.ide2); cu2 = UB(g.jde2, g.idi2); cv2 = VB(g.jde2, g.idi2); }
+  if (kBR) { cu1 = UB(g.jdi2, g.ide1); cv1 = VB(g.jdi2, g.ide1); cu2 = UB(g.jde2, g.idi1); cv2 = VB(g.jde2, g.idi1); }
 #undef UB
 #undef VB
+  if (dset) {
+    if (integ) { a2u[p] = u1o; a2v[p] = v1o; }
+    a1u[p] = ubv;
+    a1v[p] = vbv;
+  }
+  if (cset) {
+    if (integ) {
+      a2t[p] = t1o; a2qv[p] = qv1o; a2qc[p] = qc1o;
+      if (ps1) psb[q] = pso;
+    }
+    if (ps1) psa[q] = pbv;
+    a1t[p] = tbv;
+    a1qv[p] = qbv;
+  }
+  if (sW) { SLI(sl.s[1], i, k) = su; SLI(sl.s[5], i, k) = sv; SLI(sl.s[0], i, k) = ubv; SLI(sl.s[4], i, k) = vbv; }
+  if (sE) { SLI(sl.s[3], i, k) = su; SLI(sl.s[7], i, k) = sv; SLI(sl.s[2], i, k) = ubv; SLI(sl.s[6], i, k) = vbv; }
+  if (sS) {
+    if (sSi) { SLJ(sl.s[9], j, k) = su; SLJ(sl.s[13], j, k) = sv; }
+    SLJ(sl.s[8], j, k) = ubv; SLJ(sl.s[12], j, k) = vbv;
+  }
+  if (sN) {
+    if (sNi) { SLJ(sl.s[11], j, k) = su; SLJ(sl.s[15], j, k) = sv; }
+    SLJ(sl.s[10], j, k) = ubv; SLJ(sl.s[14], j, k) = vbv;
+  }
+  if (kTL) { SLI(sl.s[1], g.ide2, k) = cu1; SLI(sl.s[5], g.ide2, k) = cv1; SLJ(sl.s[11], g.jde1, k) = cu2; SLJ(sl.s[15], g.jde1, k) = cv2; }
+  if (kBL) { SLI(sl.s[1], g.ide1, k) = cu1; SLI(sl.s[5], g.ide1, k) = cv1; SLJ(sl.s[9], g.jde1, k) = cu2; SLJ(sl.s[13], g.jde1, k) = cv2; }
+  if (kTR) { SLI(sl.s[3], g.ide2, k) = cu1; SLI(sl.s[7], g.ide2, k) = cv1; SLJ(sl.s[11], g.jde2, k) = cu2; SLJ(sl.s[15], g.jde2, k) = cv2; }
+  if (kBR) { SLI(sl.s[3], g.ide1, k) = cu1; SLI(sl.s[7], g.ide1, k) = cv1; SLJ(sl.s[9], g.jde2, k) = cu2; SLJ(sl.s[13], g.jde2, k) = cv2; }
 }
 
 
@@ -1721,30 +1733,46 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
     __syncthreads();
   }
   if (!do_qc) return;
-  for (int i = g.ice1 + (int)threadIdx.x; i <= g.ice2; i += (int)blockDim.x) {
-    if (g.bl) {
+  // the west/east pass reads interior columns jci1/jci2 (including the rows ice1/ice2 the
+  // south/north pass rewrites) before that pass; the south/north pass reads the interior rows
+  // ici1/ici2, which the west/east pass never writes: every read of both passes is issued first,
+  // then (after the block barrier) every write
+  const int ni = g.ice2 - g.ice1 + 1, nj = g.jci2 - g.jci1 + 1, nx = max(ni, nj);
+  for (int base = 0; base < nx; base += (int)blockDim.x) {
+    const int x = base + (int)threadIdx.x;
+    const int i = g.ice1 + x, j = g.jci1 + x;
+    const bool wi = x < ni, sj = x < nj;
+    double vw = 0.0, ve = 0.0, vs = 0.0, vn = 0.0;
+    bool ow = false, oe = false, os = false, on = false;
+    if (wi && g.bl) {
       const double qxint = F3(a1qc, g.jci1, i, k) / ps(g.jci1, i);
       const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
-      F3(a1qc, g.jce1, i, k) = (w > d_zero) ? d_zero : qxint * ps(g.jce1, i);
+      vw = (w > d_zero) ? d_zero : qxint * ps(g.jce1, i);
+      ow = true;
     }
-    if (g.br) {
+    if (wi && g.br) {
       const double qxint = F3(a1qc, g.jci2, i, k) / ps(g.jci2, i);
       const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
-      F3(a1qc, g.jce2, i, k) = (w < d_zero) ? d_zero : qxint * ps(g.jce2, i);
+      ve = (w < d_zero) ? d_zero : qxint * ps(g.jce2, i);
+      oe = true;
     }
-  }
-  __syncthreads();
-  for (int j = g.jci1 + (int)threadIdx.x; j <= g.jci2; j += (int)blockDim.x) {
-    if (g.bb) {
+    if (sj && g.bb) {
       const double qxint = F3(a1qc, j, g.ici1, k) / ps(j, g.ici1);
       const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
-      F3(a1qc, j, g.ice1, k) = (w > d_zero) ? d_zero : qxint * ps(j, g.ice1);
+      vs = (w > d_zero) ? d_zero : qxint * ps(j, g.ice1);
+      os = true;
     }
-    if (g.bt) {
+    if (sj && g.bt) {
       const double qxint = F3(a1qc, j, g.ici2, k) / ps(j, g.ici2);
       const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
-      F3(a1qc, j, g.ice2, k) = (w < d_zero) ? d_zero : qxint * ps(j, g.ice2);
+      vn = (w < d_zero) ? d_zero : qxint * ps(j, g.ice2);
+      on = true;
     }
+    __syncthreads();
+    if (ow) F3(a1qc, g.jce1, i, k) = vw;
+    if (oe) F3(a1qc, g.jce2, i, k) = ve;
+    if (os) F3(a1qc, j, g.ice1, k) = vs;
+    if (on) F3(a1qc, j, g.ice2, k) = vn;
   }
 }
 
