@@ -36,9 +36,19 @@ KERNEL_FIELDS = {
 }
 
 
+# level-marching forms of a kernel move the same fields (template arguments are stripped)
+ALIASES = {"k_scalars_km": "k_scalars", "k_momentum_km": "k_momentum"}
+
+
+def base_name(name: str) -> str:
+    n = name.split("<")[0]
+    return ALIASES.get(n, n)
+
+
 def kernel_bytes(name: str, jx: int, iy: int, kz: int, nspgx: int) -> float | None:
     """Algorithmic bytes of one launch of `name` over a jx x iy x kz domain (None if the
     kernel has no entry)."""
+    name = base_name(name)
     if name not in KERNEL_FIELDS:
         return None
     f3, fband, f2 = KERNEL_FIELDS[name]
