@@ -1429,9 +1429,7 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
-        KLAUNCH(k_nh_sound_b1, q.cik, BLK, 0, stream, g, dc, ds, f, istep, it);
-        KLAUNCH(k_nh_sound_b2, q.cik1, BLK, 0, stream, g, dc, ds, f, istep);
-        KLAUNCH(k_nh_sound_b3, q.ci1, BLK, 0, stream, g, dc, f);
+        KLAUNCH(k_nh_sound_bc, q.ci1, BLK, 0, stream, g, dc, ds, f, istep, it);
       });
       if (cfg.ifupr == 1) {
         if (it == 1 && alarm) {
@@ -1452,10 +1450,9 @@ struct rcmdyn_engine {
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
         if (ntiles > 1)
-          KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, f);
+          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep));
         else
-          KLAUNCH(k_nh_sound_c1, q.ci1, BLK, 0, stream, g, g, f.estore, dc, f);
-        KLAUNCH(k_nh_sound_c2, q.cik, BLK, 0, stream, g, dc, ds, f, istep, (int)(it == istep));
+          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep));
       });
     }
     each([&](Tile& t) {

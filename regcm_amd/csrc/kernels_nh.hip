@@ -790,38 +790,32 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
   F3(f.cv, j, i, k) = v + F3(f.vten, j, i, k);
 }
 
-// substep part C (:297-483) in three launches: level-parallel coefficients (C1, C2), then
-// the column work (C3).
-// C1, one thread per interior cross point and level: undo the divergence damping of pp,
-// lower-boundary w (k = 1 threads: it seeds the sweep), Ikawa coefficients cc/cdd/cj, the
-// temperature factor tk, the horizontal pressure-advection terms and ptend
-__global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep, int it) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (!IN_CI(j, i)) return;
-  const int kz = c->kz;
-  const double dts = s->dt / (double)istep;
+// substep part C (:297-483) as one column kernel, one thread per interior cross column
+// walking k = kz..1: the level-parallel coefficients of a level (undo of the divergence
+// damping of pp, Ikawa cc/cdd/cj, the temperature factor tk, the horizontal pressure-advection
+// terms and ptend, :297-399) are formed once, in registers, when the walk reaches the level,
+// and feed the tridiagonal coefficients and right-hand side of the implicit w equation at the
+// level below them (:400-457), the pp predictor (:458-464) and the sweep of the tridiagonal
+// system (:468-476) in the same pass; the inputs of the upper radiative condition (:488-494)
+// close the column.  Every value is the reference's expression; only se and sf (read by the
+// downward sweep after the radiative condition's domain convolution) and the new pp, pi leave
+// the column.
+struct NhB1 { double p, cc, cdd, cj, tk, ptend; };
+__device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
+                                               int k, int kz, int it, double dts, double msfx, double ps0,
+                                               double rpb) {
+  NhB1 r;
   const double xg = c->xgamma;
   const double* cu = f.cu;
   const double* cv = f.cv;
   const double* pr0 = f.pr0;
-  if (it > 1) F3(f.cpp, j, i, k) = F3(f.cpp, j, i, k) - c->nhxkd * F3(f.spi, j, i, k);
-  const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
-  if (k == 1) {
-    F3(f.se, j, i, kz) = d_zero;
-    F3(f.sf, j, i, kz) = d_half * d_rfour * c->regrav *
-        ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
-             (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
-         (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
-             (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
-        (c->dx * msfx);
-  }
+  r.p = F3(f.cpp, j, i, k);
+  if (it > 1) r.p = r.p - c->nhxkd * F3(f.spi, j, i, k);
   const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
-  const double cc = xg * pr1 * dts / (c->dx * msfx);
-  F3(f.scc, j, i, k) = cc;
-  F3(f.scdd, j, i, k) = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
-  F3(f.scj, j, i, k) = d_half * rho0 * EGRAV_NH * dts;
-  F3(f.tk, j, i, k) = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
+  r.cc = xg * pr1 * dts / (c->dx * msfx);
+  r.cdd = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+  r.cj = d_half * rho0 * EGRAV_NH * dts;
+  r.tk = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
   double pxup, pyvp;
   if (k == 1) {
     pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
@@ -849,72 +843,81 @@ __global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepSt
                       F3(cv, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cv, j + 1, i, k) * F2(m, j + 1, i) +
                       F3(cu, j + 1, i, k) * F2(m, j + 1, i) - F3(cu, j, i, k) * F2(m, j, i) +
                       F3(cu, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cu, j, i + 1, k) * F2(m, j, i + 1)) / msfx;
-  F3(f.ptend, j, i, k) = F3(f.ppten, j, i, k) - d_half * cc * (div - d_two * (pyvp + pxup));
+  r.ptend = F3(f.ppten, j, i, k) - d_half * r.cc * (div - d_two * (pyvp + pxup));
+  return r;
 }
 
-// C2, one thread per interior cross point and level k = 2..kz: tridiagonal coefficients and
-// right-hand side of the implicit w equation (Ikawa), Main/mod_sound.F90:400-457
-__global__ void k_nh_sound_b2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep) {
-  const int j = g.jci1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int i = g.ici1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-  const int k = (int)blockIdx.z + 2;
-  if (!IN_CI(j, i) || k > c->kz) return;
-  const double dts = s->dt / (double)istep;
-  const double bet = c->nhbet;
-  const double bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
-  const double bpxbp = bp * bp, bpxbm = bp * bm;
-  const int km1 = k - 1;
-  const double rofac = (c->dsigma[km1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, km1)) /
-                       (c->dsigma[km1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, km1));
-  const double ca = EGRAV_NH * dts / (F3(f.pr0, j, i, k) - F3(f.pr0, j, i, km1)) * rofac;
-  const double g1 = d_one - c->dsigma[km1] * F3(f.tk, j, i, k);
-  const double g2 = d_one + c->dsigma[k] * F3(f.tk, j, i, km1);
-  const double cdm = F3(f.scdd, j, i, km1), cjm = F3(f.scj, j, i, km1);
-  const double cdk = F3(f.scdd, j, i, k), cjk = F3(f.scj, j, i, k);
-  F3(f.sc, j, i, k) = -ca * (cdm - cjm) * g2 * bpxbp;
-  F3(f.sb, j, i, k) = d_one + ca * (g1 * (cdk - cjk) + g2 * (cdm + cjm)) * bpxbp;
-  F3(f.saa, j, i, k) = -ca * (cdk + cjk) * g1 * bpxbp;
-  const double* w = f.cw;                       // still the old w (wo) on levels 1..kz+1
-  F3(f.rhs, j, i, k) = F3(w, j, i, k) + F3(f.wten, j, i, k) + ca *
-      (bpxbm * ((cdm - cjm) * g2 * F3(w, j, i, k - 1) - ((cdm + cjm) * g2 + (cdk - cjk) * g1) * F3(w, j, i, k) +
-                (cdk + cjk) * g1 * F3(w, j, i, k + 1)) +
-       (F3(f.cpp, j, i, k) * g1 - F3(f.cpp, j, i, k - 1) * g2) +
-       (g1 * F3(f.ptend, j, i, k) - g2 * F3(f.ptend, j, i, k - 1)) * bp);
-  (void)bm;
-}
-
-// C3, one thread per interior cross column: pp predictor (:458-464), upward sweep of the
-// tridiagonal system (:468-476), inputs of the upper radiative condition (:488-494)
-__global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f) {
+__global__ __launch_bounds__(256) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep, int it) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
+  const double dts = s->dt / (double)istep;
+  const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
   const double bet = c->nhbet, bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
-  const double* w = f.cw;
-  double wk = F3(w, j, i, 1);
-  for (int k = 1; k <= kz; k++) {
-    const double wk1 = F3(w, j, i, k + 1);
-    const double p = F3(f.cpp, j, i, k);
-    F3(f.spi, j, i, k) = p;
-    F3(f.cpp, j, i, k) = p + F3(f.ptend, j, i, k) +
-        (F3(f.scj, j, i, k) * (wk1 + wk) + F3(f.scdd, j, i, k) * (wk1 - wk)) * bm;
-    wk = wk1;
+  const double bpxbp = bp * bp, bpxbm = bp * bm;
+  const double* cu = f.cu;
+  const double* cv = f.cv;
+  const double* w = f.cw;                       // still the old w (wo) on levels 1..kz+1
+  // the sweep's start at the model top (:340-345)
+  double e = d_zero;
+  double ff = d_half * d_rfour * c->regrav *
+      ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
+           (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
+       (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
+           (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
+      (c->dx * msfx);
+  F3(f.se, j, i, kz) = e;
+  F3(f.sf, j, i, kz) = ff;
+  NhB1 cur = nh_sound_b1_at(g, c, f, j, i, kz, kz, it, dts, msfx, ps0, rpb);
+  double rho0k = F3(f.rho0, j, i, kz), rho1k = F3(f.rho1, j, i, kz), pr0k = F3(f.pr0, j, i, kz);
+  double wk1 = F3(w, j, i, kz + 1), wk = F3(w, j, i, kz);
+  double pnew = d_zero;
+  for (int k = kz; k >= 1; k--) {
+    const double wkm = (k >= 2) ? F3(w, j, i, k - 1) : d_zero;
+    NhB1 prv;
+    double rho0m = d_zero, rho1m = d_zero, pr0m = d_zero;
+    if (k >= 2) {
+      prv = nh_sound_b1_at(g, c, f, j, i, k - 1, kz, it, dts, msfx, ps0, rpb);
+      rho0m = F3(f.rho0, j, i, k - 1); rho1m = F3(f.rho1, j, i, k - 1); pr0m = F3(f.pr0, j, i, k - 1);
+      // tridiagonal coefficients and right-hand side at k (:400-457)
+      const int km1 = k - 1;
+      const double rofac = (c->dsigma[km1] * rho0k + c->dsigma[k] * rho0m) /
+                           (c->dsigma[km1] * rho1k + c->dsigma[k] * rho1m);
+      const double ca = EGRAV_NH * dts / (pr0k - pr0m) * rofac;
+      const double g1 = d_one - c->dsigma[km1] * cur.tk;
+      const double g2 = d_one + c->dsigma[k] * prv.tk;
+      const double cdm = prv.cdd, cjm = prv.cj;
+      const double cdk = cur.cdd, cjk = cur.cj;
+      const double sc = -ca * (cdm - cjm) * g2 * bpxbp;
+      const double sb = d_one + ca * (g1 * (cdk - cjk) + g2 * (cdm + cjm)) * bpxbp;
+      const double saa = -ca * (cdk + cjk) * g1 * bpxbp;
+      const double rhs = wk + F3(f.wten, j, i, k) + ca *
+          (bpxbm * ((cdm - cjm) * g2 * wkm - ((cdm + cjm) * g2 + (cdk - cjk) * g1) * wk +
+                    (cdk + cjk) * g1 * wk1) +
+           (cur.p * g1 - prv.p * g2) +
+           (g1 * cur.ptend - g2 * prv.ptend) * bp);
+      // upward sweep (:468-476)
+      const double denom = saa * e + sb;
+      e = -sc / denom;
+      ff = (rhs - ff * saa) / denom;
+      F3(f.se, j, i, k - 1) = e;
+      F3(f.sf, j, i, k - 1) = ff;
+    }
+    // pp predictor (:458-464)
+    F3(f.spi, j, i, k) = cur.p;
+    pnew = cur.p + cur.ptend + (cur.cj * (wk1 + wk) + cur.cdd * (wk1 - wk)) * bm;
+    F3(f.cpp, j, i, k) = pnew;
+    if (k >= 2) {
+      cur = prv;
+      rho0k = rho0m; rho1k = rho1m; pr0k = pr0m;
+      wk1 = wk; wk = wkm;
+    }
   }
-  double e = F3(f.se, j, i, kz), ff = F3(f.sf, j, i, kz);
-  for (int k = kz; k >= 2; k--) {
-    const double aa = F3(f.saa, j, i, k);
-    const double denom = aa * e + F3(f.sb, j, i, k);
-    e = -F3(f.sc, j, i, k) / denom;
-    ff = (F3(f.rhs, j, i, k) - ff * aa) / denom;
-    F3(f.se, j, i, k - 1) = e;
-    F3(f.sf, j, i, k - 1) = ff;
-  }
-  if (c->ifupr == 1) {
-    const double cdd1 = F3(f.scdd, j, i, 1), cj1 = F3(f.scj, j, i, 1);
-    const double denom = (cdd1 + cj1) * bp;
-    F2(f.estore, j, i) = F3(f.cpp, j, i, 1) + ff * denom;
-    F2(f.astore, j, i) = denom * e + (cj1 - cdd1) * bp;
+  if (c->ifupr == 1) {          // cur: level 1; pnew: its predicted pp
+    const double denom = (cur.cdd + cur.cj) * bp;
+    F2(f.estore, j, i) = pnew + ff * denom;
+    F2(f.astore, j, i) = denom * e + (cur.cj - cur.cdd) * bp;
   }
 }
 
@@ -985,15 +988,21 @@ __global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restri
   tmask[t] = acc;
 }
 
-// substep part D (:488-685) in two launches.
-// D1, 64 x 4 interior columns per block: upper boundary value from the 13 x 13 convolution
-// of estore (staged in LDS, clamped to the interior) and the downward sweep of w
+// substep part D (:488-685) as one kernel, 64 x 4 interior columns per block: the upper
+// boundary value from the 13 x 13 convolution of estore (staged in LDS, clamped to the
+// interior), then per column the downward sweep of w (:544-560) and, as each level's w(k+1)
+// becomes known, the level's sigma-velocity CFL (:624-640), new pp (:661-674) and its
+// temperature correction (:675-681).  The CFL maximum is reduced over the block (wavefront
+// shuffles, one atomic per block; non-negative doubles order like their bit patterns and a NaN
+// sorts above every finite value, raising the stop).
 // estore is read from the frame ge (the tile frame, or on a decomposed domain the wide frame
 // filled by a 6-deep exchange: the convolution reaches 6 points, clamped to the interior).
-__global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, Geom ge, const double* __restrict__ est,
-                                                     const Consts* __restrict__ c, NHFields f) {
+__global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est,
+                                                     const Consts* __restrict__ c, const StepState* __restrict__ s,
+                                                     NHFields f, int istep, int last) {
   __shared__ double sE[4 + 12][64 + 12];
   __shared__ double sM[169];
+  __shared__ unsigned long long sred[4];
   const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
   const int J0 = g.jci1 + (int)blockIdx.x * 64, I0 = g.ici1 + (int)blockIdx.y * 4;
   const int tid = threadIdx.y * 64 + threadIdx.x;
@@ -1010,79 +1019,75 @@ __global__ __launch_bounds__(256) void k_nh_sound_c1(Geom g, Geom ge, const doub
     __syncthreads();
   }
   const int j = J0 + (int)threadIdx.x, i = I0 + (int)threadIdx.y;
-  if (!IN_CI(j, i)) return;
-  const int kz = c->kz;
-  double wpval = d_zero;
-  if (upr) {
-    for (int nsi = -6; nsi <= 6; nsi++) {
-      int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
-      for (int nsj = -6; nsj <= 6; nsj++) {
-        int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
-        wpval = wpval + sE[inn - I0 + 6][jnn - J0 + 6] * sM[(nsj + 6) * 13 + (nsi + 6)];
+  const bool active = IN_CI(j, i);
+  unsigned long long cfl = 0ull;                       // bits of the column's CFL maximum
+  if (active) {
+    const int kz = c->kz;
+    const double dt = s->dt, dts = dt / (double)istep;
+    const double bp = (d_one + c->nhbet) * d_half;
+    double wpval = d_zero;
+    if (upr) {
+      for (int nsi = -6; nsi <= 6; nsi++) {
+        int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
+        for (int nsj = -6; nsj <= 6; nsj++) {
+          int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
+          wpval = wpval + sE[inn - I0 + 6][jnn - J0 + 6] * sM[(nsj + 6) * 13 + (nsi + 6)];
+        }
       }
     }
-  }
-  double* w = f.cw;
-  F3(w, j, i, 1) = wpval;
-  double wk = wpval;
-  for (int k = 1; k <= kz; k++) {
-    wk = F3(f.se, j, i, k) * wk + F3(f.sf, j, i, k);
-    F3(w, j, i, k + 1) = wk;
-  }
-}
-
-// D2, one thread per interior cross point and level: CFL of the sigma velocity (:624-640),
-// the new pp (:661-674) and its temperature correction (:675-681)
-__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep, int last) {
-  THREAD_POINT(g.jci1, g.ici1);
-  const bool active = IN_CI(j, i);
-  const double dt = s->dt, dts = dt / (double)istep;
-  const double bet = c->nhbet, bp = (d_one + bet) * d_half;
-  const double* w = f.cw;
-  // CFL maximum: wavefront reduction, one atomic per wavefront (non-negative doubles order
-  // like their bit patterns; a NaN sorts above every finite value and raises the stop)
-  double cfl = d_zero;
-  if (active && k >= 2) {
+    double* w = f.cw;
+    F3(w, j, i, 1) = wpval;
+    const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i);
+    const double dpx = F2(f.dpsdxm, j, i), dpy = F2(f.dpsdym, j, i);
     auto crs = [&](const double* a, int kk) {
       return F3(a, j, i, kk) + F3(a, j, i + 1, kk) + F3(a, j + 1, i, kk) + F3(a, j + 1, i + 1, kk);
     };
-    const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(w, j, i, k) / F2(f.ps0, j, i) -
-        c->sigma[k] * (F2(f.dpsdxm, j, i) * (c->twt1[k] * crs(f.cu, k) + c->twt2[k] * crs(f.cu, k - 1)) +
-                       F2(f.dpsdym, j, i) * (c->twt1[k] * crs(f.cv, k) + c->twt2[k] * crs(f.cv, k - 1)));
-    cfl = dmax(fabs(sigdot) * dt / (c->dsigma[k] + c->dsigma[k - 1]), d_zero);
+    double wm = wpval;
+    double cum = d_zero, cvm = d_zero;          // crs(cu/cv, k-1)
+    for (int k = 1; k <= kz; k++) {
+      const double wp = F3(f.se, j, i, k) * wm + F3(f.sf, j, i, k);
+      F3(w, j, i, k + 1) = wp;
+      const double cuk = crs(f.cu, k), cvk = crs(f.cv, k);
+      if (k >= 2) {
+        const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * wm / ps0 -
+            c->sigma[k] * (dpx * (c->twt1[k] * cuk + c->twt2[k] * cum) +
+                           dpy * (c->twt1[k] * cvk + c->twt2[k] * cvm));
+        const unsigned long long b =
+            (unsigned long long)__double_as_longlong(dmax(fabs(sigdot) * dt / (c->dsigma[k] + c->dsigma[k - 1]), d_zero));
+        cfl = (b > cfl) ? b : cfl;
+      }
+      cum = cuk; cvm = cvk;
+      const double ppold = F3(f.spi, j, i, k);
+      const double rho0 = F3(f.rho0, j, i, k);
+      const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+      const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
+      const double p = F3(f.cpp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
+      F3(f.cpp, j, i, k) = p;
+      F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
+      const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
+      const double dpterm = psb * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
+      F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
+      F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
+      wm = wp;
+    }
   }
-  unsigned long long bits = (unsigned long long)__double_as_longlong(cfl);
+  unsigned long long bits = cfl;
   for (int off = 32; off > 0; off >>= 1) {
     const unsigned long long o = __shfl_xor(bits, off);
     bits = (o > bits) ? o : bits;
   }
-  __shared__ unsigned long long sred[4];
   const int wv = threadIdx.y;                          // blockDim = 64 x 4: one wavefront per row
   if (threadIdx.x == 0) sred[wv] = bits;
   __syncthreads();
   if (threadIdx.x == 0 && wv == 0) {
     unsigned long long b = sred[0];
     for (int q = 1; q < 4; q++) b = (sred[q] > b) ? sred[q] : b;
-    const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x + blockIdx.z * 7919u) & (NH_CFL_SLOTS - 1);
+    const unsigned slot = (blockIdx.x + blockIdx.y * gridDim.x) & (NH_CFL_SLOTS - 1);
     if (b != 0ull) {
       atomicMax(&f.cfl[slot], b);
       if (last) atomicMax(&f.cfll[slot], b);
     }
   }
-  if (!active) return;
-  const double ppold = F3(f.spi, j, i, k);
-  const double rho0 = F3(f.rho0, j, i, k);
-  const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (F2(f.ps0, j, i) * c->dsigma[k]);
-  const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
-  const double wp = F3(w, j, i, k + 1), wm = F3(w, j, i, k);
-  const double p = F3(f.cpp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
-  F3(f.cpp, j, i, k) = p;
-  F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
-  const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
-  const double dpterm = F2(f.psb, j, i) * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
-  F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
-  F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
 }
 
 // time filters after the acoustic loop (:686-702).  k = 1..kz+1.

@@ -66,13 +66,10 @@ __global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepSta
 __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it);
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
-__global__ void k_nh_sound_b1(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
-__global__ void k_nh_sound_b2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
-__global__ void k_nh_sound_b3(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
-__global__ void k_nh_sound_c1(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_sound_c2(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last);
+__global__ void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
 __global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);
