@@ -1387,12 +1387,15 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
       const Grids q = grids(g);
-      // init_tendencies (:1227-1240)
-      const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
-      for (double* p : {f.tten, f.tdyn, f.qvten, f.qvdyn, f.qcten, f.qcdyn, f.uten, f.udyn, f.vten, f.vdyn,
-                        f.ppten, f.ppdyn})
-        HIPCHK(hipMemsetAsync(p, 0, b3, stream));
-      for (double* p : {f.wten, f.wdyn}) HIPCHK(hipMemsetAsync(p, 0, b4, stream));
+      // init_tendencies (:1227-1240): the zero is the leading summand of each tendency's first
+      // writer (k_nh_uv_adv, k_nh_scalar_adv, the iboudy = 4 sponges, k_nh_forecast), which
+      // covers every point a later kernel reads.  With diagnostics on, the total tendencies
+      // are also zeroed, so a get shows 0 at the points no kernel writes.
+      if (diag) {
+        const size_t b3 = sizeof(double) * g.plane * kz, b4 = sizeof(double) * g.plane * kp;
+        for (double* p : {f.tten, f.qvten, f.qcten, f.uten, f.vten, f.ppten}) HIPCHK(hipMemsetAsync(p, 0, b3, stream));
+        HIPCHK(hipMemsetAsync(f.wten, 0, b4, stream));
+      }
       KLAUNCH(k_nh_uv_adv, q.di1, BLK, 0, stream, g, dc, f);
       if (cfg.isladvec == 1)
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
@@ -1417,9 +1420,11 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_sound_init, q.fr, BLK, 0, stream, g, dc, ds, f, istep);
     });
     for (int it = 1; it <= istep; it++) {
-      each([&](Tile& t) {
-        KLAUNCH(k_nh_sound_a, grids(t.g).ce1, BLK, 0, stream, t.g, dc, nhfields(t), it);
-      });
+      if (it == 1) {             // later sub-steps: part A ran in the previous k_nh_sound_cd
+        each([&](Tile& t) {
+          KLAUNCH(k_nh_sound_a, grids(t.g).ce1, BLK, 0, stream, t.g, dc, nhfields(t), it);
+        });
+      }
       xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
       each([&](Tile& t) {
         KLAUNCH(k_nh_sound_uv, grids(t.g).dik, BLK, 0, stream, t.g, dc, ds, nhfields(t), istep);
@@ -1450,9 +1455,11 @@ struct rcmdyn_engine {
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
         if (ntiles > 1)
-          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep));
+          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
+                  (int)(it < istep));
         else
-          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep));
+          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep),
+                  (int)(it < istep));
       });
     }
     each([&](Tile& t) {

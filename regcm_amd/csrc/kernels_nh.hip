@@ -220,8 +220,9 @@ __global__ void k_nh_uv_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
     ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
     vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
     vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
-    F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + u0 * diag - dm * (ue * ucmonb - uw * ucmonc + un * vcmonb - us * vcmonc);
-    F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) + v0 * diag - dm * (ve * ucmonb - vw * ucmonc + vn * vcmonb - vs * vcmonc);
+    // first writer of udyn/vdyn (init_tendencies' zero, :1227-1240, as the leading summand)
+    F3(f.udyn, j, i, k) = d_zero + u0 * diag - dm * (ue * ucmonb - uw * ucmonc + un * vcmonb - us * vcmonc);
+    F3(f.vdyn, j, i, k) = d_zero + v0 * diag - dm * (ve * ucmonb - vw * ucmonc + vn * vcmonb - vs * vcmonc);
   }
   for (int k = 2; k <= kz; k++) {
     const double qq = d_rfour * (F3(f.qdot, j, i, k) + F3(f.qdot, j, i - 1, k) + F3(f.qdot, j - 1, i, k) +
@@ -284,9 +285,11 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
     v1 = F3(f.vmc, j + 1, i, kk) + F3(f.vmc, j, i, kk);
     v2 = F3(f.vmc, j + 1, i + 1, kk) + F3(f.vmc, j, i + 1, kk);
   };
+  // first writer of wdyn, ppdyn, tdyn, qvdyn, qcdyn: init_tendencies' zero (:1227-1240) is the
+  // leading summand of each
   // ---- w on full levels k = 1..kz+1
   {
-    double wd = F3(f.wdyn, j, i, k);
+    double wd = d_zero;
     if (k >= 2 && k <= kz) {                       // hadv3d ind = 1, :486-507
       double u1, u2, v1, v2, pu1, pu2, pv1, pv2;
       avg(k, u1, u2, v1, v2);
@@ -317,7 +320,7 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
   avg(k, u1, u2, v1, v2);
   // ---- pp: hadv3d ind 0, then vadv3d ind = 0 (nk = kz), :746-754
   {
-    double pd = F3(f.ppdyn, j, i, k) + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    double pd = d_zero + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
     auto pflux = [&](int kk) {
       return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
     };
@@ -338,11 +341,11 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
     if (k + 1 <= kz) thd = thd - thflux(k + 1) * c->xds[k];
     const double th = F3(f.th, j, i, k);
     thd = thd + th * F3(f.cr, j, i, k);
-    F3(f.tdyn, j, i, k) = F3(f.tdyn, j, i, k) + F3(f.a1t, j, i, k) * thd / (th * ps);
+    F3(f.tdyn, j, i, k) = d_zero + F3(f.a1t, j, i, k) * thd / (th * ps);
   }
   // ---- qv: hadvqv (or the semi-Lagrangian start, isladvec = 1), then vadvqv, :811-836
   {
-    double qd = F3(f.qvdyn, j, i, k) + (c->isladvec ? F3(f.slqv, j, i, k)
+    double qd = d_zero + (c->isladvec ? F3(f.slqv, j, i, k)
                                                     : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
     const double thr = MINQQ * ps;
     auto qflux = [&](int kk) {
@@ -357,7 +360,7 @@ __global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f
   }
   // ---- qc: hadvqx (or the semi-Lagrangian start), then vadv4d ind = 1, :873-894, 958-961
   {
-    double cd = F3(f.qcdyn, j, i, k) + (c->isladvec ? F3(f.slqc, j, i, k)
+    double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
                                                     : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
     const double thr = MINQQ * MINQQ * ps;
     auto cflux = [&](int kk) {
@@ -447,12 +450,13 @@ __global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepSt
     const int ib = f.ibcr[g.ix(j, i)];
     if (c->iboudy == 4) {
       const double w = c->wgtx[ib];
+      // the total tendencies are still init_tendencies' zero here
       if (k <= kz) {
-        F3(f.tten, j, i, k) = w * F3(f.tten, j, i, k) + (d_one - w) * F3(f.tbt, j, i, k);
-        F3(f.qvten, j, i, k) = w * F3(f.qvten, j, i, k) + (d_one - w) * F3(f.qbt, j, i, k);
-        F3(f.ppten, j, i, k) = w * F3(f.ppten, j, i, k) + (d_one - w) * F3(f.ppbt, j, i, k);
+        F3(f.tten, j, i, k) = w * d_zero + (d_one - w) * F3(f.tbt, j, i, k);
+        F3(f.qvten, j, i, k) = w * d_zero + (d_one - w) * F3(f.qbt, j, i, k);
+        F3(f.ppten, j, i, k) = w * d_zero + (d_one - w) * F3(f.ppbt, j, i, k);
       }
-      F3(f.wten, j, i, k) = w * F3(f.wten, j, i, k) + (d_one - w) * F3(f.wwbt, j, i, k);
+      F3(f.wten, j, i, k) = w * d_zero + (d_one - w) * F3(f.wwbt, j, i, k);
     } else {
       double xf, xg;
       if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
@@ -477,8 +481,8 @@ __global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepSt
     const int ib = f.ibdt[g.ix(j, i)];
     if (c->iboudy == 4) {
       const double w = c->wgtd[ib];
-      F3(f.uten, j, i, k) = w * F3(f.uten, j, i, k) + (d_one - w) * F3(f.ubt, j, i, k);
-      F3(f.vten, j, i, k) = w * F3(f.vten, j, i, k) + (d_one - w) * F3(f.vbt, j, i, k);
+      F3(f.uten, j, i, k) = w * d_zero + (d_one - w) * F3(f.ubt, j, i, k);
+      F3(f.vten, j, i, k) = w * d_zero + (d_one - w) * F3(f.vbt, j, i, k);
     } else {
       double xf, xg;
       if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
@@ -570,14 +574,19 @@ __global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepSt
   FRAME_POINT();
   const int kz = c->kz;
   const double dt = s->dt;
+  // the total tendencies are init_tendencies' zero except where the iboudy = 4 sponges of
+  // k_nh_boundary wrote them (band points), so they are read only there
+  const bool spc = c->iboudy == 4 && IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0;
+  const bool spd = c->iboudy == 4 && IN_DI(j, i) && f.rgdt[g.ix(j, i)] > 0;
+#define TEN0(p, sp) ((sp) ? F3(f.p, j, i, k) : d_zero)
   if (IN_CI(j, i)) {
 #define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
-    F3(f.wten, j, i, k) = F3(f.wten, j, i, k) + F3(f.wdyn, j, i, k) + PHY(wphy);
+    F3(f.wten, j, i, k) = TEN0(wten, spc) + F3(f.wdyn, j, i, k) + PHY(wphy);
     if (k <= kz) {
-      double tt = F3(f.tten, j, i, k) + F3(f.tdyn, j, i, k) + PHY(tphy);
-      double qv = F3(f.qvten, j, i, k) + F3(f.qvdyn, j, i, k) + PHY(qvphy);
-      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) + F3(f.ppdyn, j, i, k) + PHY(ppphy);
-      double qc = F3(f.qcten, j, i, k) + F3(f.qcdyn, j, i, k) + PHY(qcphy);
+      double tt = TEN0(tten, spc) + F3(f.tdyn, j, i, k) + PHY(tphy);
+      double qv = TEN0(qvten, spc) + F3(f.qvdyn, j, i, k) + PHY(qvphy);
+      F3(f.ppten, j, i, k) = TEN0(ppten, spc) + F3(f.ppdyn, j, i, k) + PHY(ppphy);
+      double qc = d_zero + F3(f.qcdyn, j, i, k) + PHY(qcphy);
       tt = tt + 0.0; qv = qv + 0.0; qc = qc + 0.0;
       if (c->ifrayd == 1 && k <= c->rayndamp) {
         const double xt = s->xbctime + dt;
@@ -600,10 +609,11 @@ __global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepSt
     F3(f.cqc, j, i, k) = qc;
   }
   if (IN_DI(j, i)) {
-    F3(f.uten, j, i, k) = F3(f.uten, j, i, k) + F3(f.udyn, j, i, k) + PHY(uphy);
-    F3(f.vten, j, i, k) = F3(f.vten, j, i, k) + F3(f.vdyn, j, i, k) + PHY(vphy);
+    F3(f.uten, j, i, k) = TEN0(uten, spd) + F3(f.udyn, j, i, k) + PHY(uphy);
+    F3(f.vten, j, i, k) = TEN0(vten, spd) + F3(f.vdyn, j, i, k) + PHY(vphy);
   }
 #undef PHY
+#undef TEN0
 }
 
 // negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points
@@ -847,7 +857,10 @@ __device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, c
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+#ifndef NHBC_W
+#define NHBC_W 2
+#endif
+__global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
                               int istep, int it) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
@@ -992,14 +1005,17 @@ __global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restri
 // boundary value from the 13 x 13 convolution of estore (staged in LDS, clamped to the
 // interior), then per column the downward sweep of w (:544-560) and, as each level's w(k+1)
 // becomes known, the level's sigma-velocity CFL (:624-640), new pp (:661-674) and its
-// temperature correction (:675-681).  The CFL maximum is reduced over the block (wavefront
+// temperature correction (:675-681); unless this is the last sub-step, part A of the next one
+// (pp += xkd*pi and dp'/dp0, :250-262) follows on the column: the boundary ring's dp'/dp0 that
+// part A also forms reads pp the sub-steps never change there, so it keeps its first-sub-step
+// value.  The CFL maximum is reduced over the block (wavefront
 // shuffles, one atomic per block; non-negative doubles order like their bit patterns and a NaN
 // sorts above every finite value, raising the stop).
 // estore is read from the frame ge (the tile frame, or on a decomposed domain the wide frame
 // filled by a 6-deep exchange: the convolution reaches 6 points, clamped to the interior).
 __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est,
                                                      const Consts* __restrict__ c, const StepState* __restrict__ s,
-                                                     NHFields f, int istep, int last) {
+                                                     NHFields f, int istep, int last, int nexta) {
   __shared__ double sE[4 + 12][64 + 12];
   __shared__ double sM[169];
   __shared__ unsigned long long sred[4];
@@ -1044,6 +1060,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
     };
     double wm = wpval;
     double cum = d_zero, cvm = d_zero;          // crs(cu/cv, k-1)
+    double pam = d_zero, pamm = d_zero, prm = d_zero, prmm = d_zero;   // next part A: pp, pr0 at k-1, k-2
     for (int k = 1; k <= kz; k++) {
       const double wp = F3(f.se, j, i, k) * wm + F3(f.sf, j, i, k);
       F3(w, j, i, k + 1) = wp;
@@ -1062,13 +1079,28 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
       const double cddtmp = c->xgamma * F3(f.pr1, j, i, k) * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
       const double cjtmp = rho0 * EGRAV_NH * dts * d_half;
       const double p = F3(f.cpp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
-      F3(f.cpp, j, i, k) = p;
-      F3(f.spi, j, i, k) = p - ppold - F3(f.ppten, j, i, k);
+      const double spn = p - ppold - F3(f.ppten, j, i, k);
+      F3(f.spi, j, i, k) = spn;
       const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
       const double dpterm = psb * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
       F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
       F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
       wm = wp;
+      if (!nexta) {
+        F3(f.cpp, j, i, k) = p;
+        continue;
+      }
+      // part A of the next sub-step on this column (:250-262): pp += xkd*pi, then dp'/dp0 at
+      // the level above, whose neighbours k-2 (clamped to 1) and k are now known
+      const double pa = p + c->nhxkd * spn;
+      const double pr = F3(f.pr0, j, i, k);
+      F3(f.cpp, j, i, k) = pa;
+      if (k >= 2) {
+        const double pk1 = (k >= 3) ? pamm : pam, rk1 = (k >= 3) ? prmm : prm;
+        F3(f.cdt, j, i, k - 1) = (pk1 - pa) / (rk1 - pr);
+      }
+      if (k == kz) F3(f.cdt, j, i, kz) = (pam - pa) / (prm - pr);
+      pamm = pam; prmm = prm; pam = pa; prm = pr;
     }
   }
   unsigned long long bits = cfl;

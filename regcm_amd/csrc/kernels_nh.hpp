@@ -69,7 +69,7 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
 __global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
-__global__ void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last);
+__global__ void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last, int nexta);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
 __global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);
