@@ -1396,15 +1396,11 @@ struct rcmdyn_engine {
         for (double* p : {f.tten, f.qvten, f.qcten, f.uten, f.vten, f.ppten}) HIPCHK(hipMemsetAsync(p, 0, b3, stream));
         HIPCHK(hipMemsetAsync(f.wten, 0, b4, stream));
       }
-      KLAUNCH(k_nh_uv_adv, q.di1, BLK, 0, stream, g, dc, f);
       if (cfg.isladvec == 1)
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
-      KLAUNCH(k_nh_scalar_adv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kp), BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_curvature, q.dik, BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_adiabatic, q.ci1, BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_boundary, q.fr, BLK, 0, stream, g, dc, ds, f);
-      KLAUNCH(k_nh_diffusion, q.fr, BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_forecast, q.fr, BLK, 0, stream, g, dc, ds, f);
+      // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
+      KLAUNCH(k_nh_tend_d, q.dik, BLK, 0, stream, g, dc, ds, f);
+      KLAUNCH(k_nh_tend_c, q.fr, BLK, 0, stream, g, dc, ds, f, (int)diag);
     });
     tke_step();
     xch({{FK::CQV, kz}, {FK::CQC, kz}});

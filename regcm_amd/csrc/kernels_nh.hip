@@ -192,50 +192,6 @@ __global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields 
   }
 }
 
-// hadvuv NH upstream branch (Main/mod_advection.F90:235-264) + vadvuv (:286-299), one thread
-// per dot column
-__global__ void k_nh_uv_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jdi1, g.idi1);
-  if (!IN_DI(j, i)) return;
-  const int kz = c->kz;
-  const double ul = c->ul, dm = F2(f.dmsf, j, i);
-  const double* ua = f.umc; const double* va = f.vmc; const double* u = f.ud; const double* v = f.vd;
-  for (int k = 1; k <= kz; k++) {
-    const double divd = d_rfour * (F3(f.cr, j, i, k) + F3(f.cr, j, i - 1, k) + F3(f.cr, j - 1, i, k) +
-                                   F3(f.cr, j - 1, i - 1, k));
-    const double ucmona = F3(ua, j, i + 1, k) + d_two * F3(ua, j, i, k) + F3(ua, j, i - 1, k);
-    double ucmonb = F3(ua, j + 1, i + 1, k) + d_two * F3(ua, j + 1, i, k) + F3(ua, j + 1, i - 1, k);
-    double ucmonc = F3(ua, j - 1, i + 1, k) + d_two * F3(ua, j - 1, i, k) + F3(ua, j - 1, i - 1, k);
-    const double vcmona = F3(va, j + 1, i, k) + d_two * F3(va, j, i, k) + F3(va, j - 1, i, k);
-    double vcmonb = F3(va, j + 1, i + 1, k) + d_two * F3(va, j, i + 1, k) + F3(va, j - 1, i + 1, k);
-    double vcmonc = F3(va, j + 1, i - 1, k) + d_two * F3(va, j, i - 1, k) + F3(va, j - 1, i - 1, k);
-    const double diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc));
-    const double u0 = F3(u, j, i, k), ue = F3(u, j + 1, i, k), uw = F3(u, j - 1, i, k);
-    const double un = F3(u, j, i + 1, k), us = F3(u, j, i - 1, k);
-    const double v0 = F3(v, j, i, k), ve = F3(v, j + 1, i, k), vw = F3(v, j - 1, i, k);
-    const double vn = F3(v, j, i + 1, k), vs = F3(v, j, i - 1, k);
-    const double ff1 = ul * (ue + u0), ff2 = ul * (uw + u0);
-    const double ff3 = ul * (vn + v0), ff4 = ul * (vs + v0);
-    ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
-    ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
-    vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
-    vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
-    // first writer of udyn/vdyn (init_tendencies' zero, :1227-1240, as the leading summand)
-    F3(f.udyn, j, i, k) = d_zero + u0 * diag - dm * (ue * ucmonb - uw * ucmonc + un * vcmonb - us * vcmonc);
-    F3(f.vdyn, j, i, k) = d_zero + v0 * diag - dm * (ve * ucmonb - vw * ucmonc + vn * vcmonb - vs * vcmonc);
-  }
-  for (int k = 2; k <= kz; k++) {
-    const double qq = d_rfour * (F3(f.qdot, j, i, k) + F3(f.qdot, j, i - 1, k) + F3(f.qdot, j - 1, i, k) +
-                                 F3(f.qdot, j - 1, i - 1, k));
-    const double uu = qq * (c->twt1[k] * F3(f.a1u, j, i, k) + c->twt2[k] * F3(f.a1u, j, i, k - 1));
-    const double vv = qq * (c->twt1[k] * F3(f.a1v, j, i, k) + c->twt2[k] * F3(f.a1v, j, i, k - 1));
-    F3(f.udyn, j, i, k - 1) = F3(f.udyn, j, i, k - 1) - uu * c->xds[k - 1];
-    F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + uu * c->xds[k];
-    F3(f.vdyn, j, i, k - 1) = F3(f.vdyn, j, i, k - 1) - vv * c->xds[k - 1];
-    F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) + vv * c->xds[k];
-  }
-}
-
 // upstream flux form of hadvt/hadvqv/hadvqx/hadv3d ind 0 at one cross point
 // (Main/mod_advection.F90:337-386, 547-596, 639-653, 466-480); limiter 0 none, 1 t, 2 q
 __device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const double* fa, int j, int i, int k,
@@ -266,233 +222,9 @@ __device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const 
   return fg;
 }
 
-// scalar advection of the NH core (advection driver Main/mod_tendency.F90:1308-1392): pp
-// (hadv3d ind 0 + vadv3d ind 0), w (hadv3d ind 1 + vadv3d ind 0 on full levels), potential
-// temperature (hadvt + vadv3d ind 0, and its adiabatic term), qv (hadvqv + vadvqv), qc (hadvqx + vadv4d ind 1).  One thread per
-// interior cross point and level k = 1..kz+1 (w alone on kz+1): every element is written once,
-// with the reference's order of accumulation -- 0, the horizontal term, then the vertical flux
-// through its upper interface (the reference's loop iteration k, added) and through its lower
-// one (iteration k+1, subtracted).  An interface flux is formed by both levels it bounds, with
-// the same expression, so the values are those of the reference's k loops.
-__global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (!IN_CI(j, i)) return;
-  const int kz = c->kz;
-  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
-  auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
-    u1 = F3(f.umc, j, i + 1, kk) + F3(f.umc, j, i, kk);
-    u2 = F3(f.umc, j + 1, i + 1, kk) + F3(f.umc, j + 1, i, kk);
-    v1 = F3(f.vmc, j + 1, i, kk) + F3(f.vmc, j, i, kk);
-    v2 = F3(f.vmc, j + 1, i + 1, kk) + F3(f.vmc, j, i + 1, kk);
-  };
-  // first writer of wdyn, ppdyn, tdyn, qvdyn, qcdyn: init_tendencies' zero (:1227-1240) is the
-  // leading summand of each
-  // ---- w on full levels k = 1..kz+1
-  {
-    double wd = d_zero;
-    if (k >= 2 && k <= kz) {                       // hadv3d ind = 1, :486-507
-      double u1, u2, v1, v2, pu1, pu2, pv1, pv2;
-      avg(k, u1, u2, v1, v2);
-      avg(k - 1, pu1, pu2, pv1, pv2);
-      const double t1 = c->twt1[k], t2 = c->twt2[k];
-      const double uaz1 = (t1 * u1 + t2 * pu1), uaz2 = (t1 * u2 + t2 * pu2);
-      const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
-      const double f1 = d_half * ul * (u2 + u1) / ps;
-      const double f2 = d_half * ul * (v2 + v1) / ps;
-      const double* w = f.xw;
-      const double fx1 = (d_one + f1) * F3(w, j - 1, i, k) + (d_one - f1) * F3(w, j, i, k);
-      const double fx2 = (d_one + f1) * F3(w, j, i, k) + (d_one - f1) * F3(w, j + 1, i, k);
-      const double fy1 = (d_one + f2) * F3(w, j, i - 1, k) + (d_one - f2) * F3(w, j, i, k);
-      const double fy2 = (d_one + f2) * F3(w, j, i, k) + (d_one - f2) * F3(w, j, i + 1, k);
-      wd = wd - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
-    }
-    // vadv3d ind = 0, nk = kz+1 (w), :756-765: flux through the interface below level kk
-    auto wflux = [&](int kk) {
-      const double qq = d_half * (F3(f.qdot, j, i, kk) + F3(f.qdot, j, i, kk + 1));
-      return qq * ((F3(f.a1w, j, i, kk) + F3(f.a1w, j, i, kk + 1)));
-    };
-    if (k >= 2) wd = wd + wflux(k - 1) * c->dds[k];
-    if (k <= kz) wd = wd - wflux(k) * c->dds[k];
-    F3(f.wdyn, j, i, k) = wd;
-  }
-  if (k > kz) return;
-  double u1, u2, v1, v2;
-  avg(k, u1, u2, v1, v2);
-  // ---- pp: hadv3d ind 0, then vadv3d ind = 0 (nk = kz), :746-754
-  {
-    double pd = d_zero + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
-    auto pflux = [&](int kk) {
-      return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
-    };
-    if (k >= 2) pd = pd + pflux(k) * c->xds[k];
-    if (k + 1 <= kz) pd = pd - pflux(k + 1) * c->xds[k];
-    F3(f.ppdyn, j, i, k) = pd;
-  }
-  // ---- t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d ind = 0
-  // (nk = kz) of tha = th*p*, plus th*cr; the adiabatic term adds atm1%t*thten/tha to tdyn
-  // (zero until then: advection and curvature do not touch it)
-  {
-    double thd = d_zero + hadv_fg(g, c, f.th, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
-    auto thflux = [&](int kk) {
-      return F3(f.qdot, j, i, kk) *
-             (c->twt1[kk] * (F3(f.th, j, i, kk) * ps) + c->twt2[kk] * (F3(f.th, j, i, kk - 1) * ps));
-    };
-    if (k >= 2) thd = thd + thflux(k) * c->xds[k];
-    if (k + 1 <= kz) thd = thd - thflux(k + 1) * c->xds[k];
-    const double th = F3(f.th, j, i, k);
-    thd = thd + th * F3(f.cr, j, i, k);
-    F3(f.tdyn, j, i, k) = d_zero + F3(f.a1t, j, i, k) * thd / (th * ps);
-  }
-  // ---- qv: hadvqv (or the semi-Lagrangian start, isladvec = 1), then vadvqv, :811-836
-  {
-    double qd = d_zero + (c->isladvec ? F3(f.slqv, j, i, k)
-                                                    : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
-    const double thr = MINQQ * ps;
-    auto qflux = [&](int kk) {
-      const double fk = F3(f.a1qv, j, i, kk), fkm = F3(f.a1qv, j, i, kk - 1);
-      double fg = d_zero;
-      if (fk > thr && fkm > thr) fg = fk * rcm_powpos(fkm / fk, c->qcon[kk]);
-      return F3(f.qdot, j, i, kk) * fg;
-    };
-    if (k >= 2) qd = qd + qflux(k) * c->xds[k];
-    if (k + 1 <= kz) qd = qd - qflux(k + 1) * c->xds[k];
-    F3(f.qvdyn, j, i, k) = qd;
-  }
-  // ---- qc: hadvqx (or the semi-Lagrangian start), then vadv4d ind = 1, :873-894, 958-961
-  {
-    double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
-                                                    : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
-    const double thr = MINQQ * MINQQ * ps;
-    auto cflux = [&](int kk) {
-      const double svv = F3(f.qdot, j, i, kk);
-      const double fk = F3(f.a1qc, j, i, kk), fkm = F3(f.a1qc, j, i, kk - 1);
-      if (svv > d_zero) return (fkm > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
-      return (fk > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
-    };
-    if (k >= 2) cd = cd + cflux(k) * c->xds[k];
-    if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
-    F3(f.qcdyn, j, i, k) = cd;
-  }
-}
-
-// curvature NH (Main/mod_tendency.F90:1839-1879): horizontal and vertical Coriolis,
-// horizontal and vertical curvature
-__global__ void k_nh_curvature(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jdi1, g.idi1);
-  if (!IN_DI(j, i)) return;
-  const double* w = f.a1w;
-  const double wadot = 0.125 * (F3(w, j - 1, i - 1, k) + F3(w, j - 1, i, k) + F3(w, j, i - 1, k) + F3(w, j, i, k));
-  const double wadotp1 = 0.125 * (F3(w, j - 1, i - 1, k + 1) + F3(w, j - 1, i, k + 1) + F3(w, j, i - 1, k + 1) +
-                                  F3(w, j, i, k + 1));
-  const double wabar = wadot + wadotp1;
-  const double amfac = wabar * F2(f.rpsda, j, i) * REARTHRAD;
-  const double uc = F3(f.a1u, j, i, k), vc = F3(f.a1v, j, i, k);
-  const double duv = uc * F2(f.dmdy, j, i) - vc * F2(f.dmdx, j, i);
-  const double cor = F2(f.coriol, j, i), ef = F2(f.ef, j, i);
-  F3(f.udyn, j, i, k) = F3(f.udyn, j, i, k) + cor * vc - ef * F2(f.ddx, j, i) * wabar + F3(f.vmd, j, i, k) * duv -
-                        uc * amfac;
-  F3(f.vdyn, j, i, k) = F3(f.vdyn, j, i, k) - cor * uc + ef * F2(f.ddy, j, i) * wabar - F3(f.umd, j, i, k) * duv -
-                        vc * amfac;
-}
-
-// adiabatic NH (:1601-1671), one thread per interior cross column; the ithadv = 1 temperature
-// term (:1594-1600) is formed in k_nh_scalar_adv with thten
-__global__ void k_nh_adiabatic(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (!IN_CI(j, i)) return;
-  const int kz = c->kz;
-  for (int k = 1; k <= kz; k++) {
-    const double cr = F3(f.cr, j, i, k);
-    F3(f.ppdyn, j, i, k) = F3(f.ppdyn, j, i, k) + F3(f.xpp, j, i, k) * cr;
-    F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + F3(f.xqv, j, i, k) * cr;
-    F3(f.qcdyn, j, i, k) = F3(f.qcdyn, j, i, k) + F3(f.xqc, j, i, k) * cr;
-  }
-  auto ucc = [&](int k) {
-    return F3(f.a1u, j, i, k) + F3(f.a1u, j, i + 1, k) + F3(f.a1u, j + 1, i, k) + F3(f.a1u, j + 1, i + 1, k);
-  };
-  auto vcc = [&](int k) {
-    return F3(f.a1v, j, i, k) + F3(f.a1v, j, i + 1, k) + F3(f.a1v, j + 1, i, k) + F3(f.a1v, j + 1, i + 1, k);
-  };
-  const double ps = F2(f.psa, j, i), rps = F2(f.rpsa, j, i);
-  const double ex = F2(f.ex, j, i), crx = F2(f.crx, j, i), cry = F2(f.cry, j, i);
-  double um = ucc(1), vm = vcc(1);
-  for (int k = 2; k <= kz; k++) {
-    const double uk = ucc(k), vk = vcc(k);
-    const double rofac = (c->dsigma[k - 1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, k - 1)) /
-                         (c->dsigma[k - 1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, k - 1));
-    const double uaq = d_rfour * (c->twt1[k] * uk + c->twt2[k] * um);
-    const double vaq = d_rfour * (c->twt1[k] * vk + c->twt2[k] * vm);
-    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) +
-        (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
-        ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
-        F3(f.xw, j, i, k) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
-    um = uk; vm = vk;
-  }
-  for (int k = 2; k <= kz; k++)                 // water loading, qcd = atmx%qx(iqc)
-    F3(f.wdyn, j, i, k) = F3(f.wdyn, j, i, k) - EGRAV_NH * ps *
-                          (c->twt2[k] * F3(f.xqc, j, i, k - 1) + c->twt1[k] * F3(f.xqc, j, i, k));
-}
-
 __device__ __forceinline__ double nh_relax(double ften, double xf, double xg, double f0, double f1, double f2,
                                            double f3, double f4) {
   return ften + xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0);
-}
-
-// boundary (Main/mod_tendency.F90:1462-1501): nudge3d/nudge4d3d/nudgeuv of t, qv, u, v, pp
-// and w (hefc(ib, min(k,kz)) on the w top level, Main/mod_bdycod.F90:4332-4333), or the
-// sponges of iboudy = 4 on the total tendencies.  k = 1..kz+1.
-__global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  const double xt = s->xbctime + s->dt;
-  const int kc = (k < kz) ? k : kz;
-  if (IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0) {
-    const int ib = f.ibcr[g.ix(j, i)];
-    if (c->iboudy == 4) {
-      const double w = c->wgtx[ib];
-      // the total tendencies are still init_tendencies' zero here
-      if (k <= kz) {
-        F3(f.tten, j, i, k) = w * d_zero + (d_one - w) * F3(f.tbt, j, i, k);
-        F3(f.qvten, j, i, k) = w * d_zero + (d_one - w) * F3(f.qbt, j, i, k);
-        F3(f.ppten, j, i, k) = w * d_zero + (d_one - w) * F3(f.ppbt, j, i, k);
-      }
-      F3(f.wten, j, i, k) = w * d_zero + (d_one - w) * F3(f.wwbt, j, i, k);
-    } else {
-      double xf, xg;
-      if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
-      else { xf = c->hefc[ib][kc]; xg = c->hegc[ib][kc]; }
-#define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
-#define RELAX5(ten, b0, bt, a)                                                                    \
-  F3(ten, j, i, k) = nh_relax(F3(ten, j, i, k), xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), \
-                              FG(b0, bt, a, j + 1, i), FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
-      if (k <= kz) {
-        RELAX5(f.tdyn, f.tb0, f.tbt, f.a2t);
-        const double nfac = 1.0e3, rfac = d_one / nfac;
-#define FQ(J, I) (nfac * (F3(f.qb0, J, I, k) + xt * F3(f.qbt, J, I, k)) - nfac * F3(f.a2qv, J, I, k))
-        const double q0 = FQ(j, i), q1 = FQ(j - 1, i), q2 = FQ(j + 1, i), q3 = FQ(j, i - 1), q4 = FQ(j, i + 1);
-#undef FQ
-        F3(f.qvdyn, j, i, k) = F3(f.qvdyn, j, i, k) + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
-        RELAX5(f.ppdyn, f.ppb0, f.ppbt, f.a2pp);
-      }
-      RELAX5(f.wdyn, f.wwb0, f.wwbt, f.a2w);
-    }
-  }
-  if (k <= kz && IN_DI(j, i) && f.rgdt[g.ix(j, i)] > 0) {
-    const int ib = f.ibdt[g.ix(j, i)];
-    if (c->iboudy == 4) {
-      const double w = c->wgtd[ib];
-      F3(f.uten, j, i, k) = w * d_zero + (d_one - w) * F3(f.ubt, j, i, k);
-      F3(f.vten, j, i, k) = w * d_zero + (d_one - w) * F3(f.vbt, j, i, k);
-    } else {
-      double xf, xg;
-      if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
-      else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
-      RELAX5(f.udyn, f.ub0, f.ubt, f.a2u);
-      RELAX5(f.vdyn, f.vb0, f.vbt, f.a2v);
-    }
-  }
-#undef RELAX5
-#undef FG
 }
 
 // 4th-order (idiffu = 1) / 9-point (idiffu = 2) diffusion of one cross field at (j,i,k)
@@ -517,48 +249,6 @@ __device__ __forceinline__ double diffx_at(const Geom& g, const Consts* c, doubl
   return ften;
 }
 
-// diffusion (Main/mod_tendency.F90:1515-1538): diffu_d for u, v; diffu_x for t, qv, qc, pp
-// (xkc) and w (xkcf, full levels)
-__global__ void k_nh_diffusion(Geom g, const Consts* __restrict__ c, NHFields f) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  if (IN_CI(j, i)) {
-    if (k <= kz) {
-      F3(f.tdyn, j, i, k) = diffx_at(g, c, F3(f.tdyn, j, i, k), f.tb3d, f.xkc, j, i, k);
-      F3(f.qvdyn, j, i, k) = diffx_at(g, c, F3(f.qvdyn, j, i, k), f.qvb3d, f.xkc, j, i, k);
-      F3(f.qcdyn, j, i, k) = diffx_at(g, c, F3(f.qcdyn, j, i, k), f.qcb3d, f.xkc, j, i, k);
-      F3(f.ppdyn, j, i, k) = diffx_at(g, c, F3(f.ppdyn, j, i, k), f.ppb3d, f.xkc, j, i, k);
-    }
-    F3(f.wdyn, j, i, k) = diffx_at(g, c, F3(f.wdyn, j, i, k), f.wb3d, f.xkcf, j, i, k);
-  }
-  if (k > kz || !IN_DI(j, i)) return;
-  // diffu_d, Main/mod_diffusion.F90:281-411
-  const double* m = f.msfd;
-#define UM(a, J, I) (F3(a, J, I, k) / F2(m, J, I))
-  for (int pass = 0; pass < 2; pass++) {
-    const double* b = pass ? f.vbd : f.ubd;
-    double* ten = pass ? f.vdyn : f.udyn;
-    double t = F3(ten, j, i, k);
-    const double xkd = F3(f.xkd, j, i, k);
-    if (c->idiffu == 2) {
-      t = t + xkd * (o4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
-                     o4_c2 * (UM(b, j + 1, i + 1) + UM(b, j - 1, i - 1) + UM(b, j - 1, i + 1) + UM(b, j + 1, i - 1)) +
-                     o4_c3 * (UM(b, j, i)));
-    } else {
-      if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2))
-        t = t - xkd * (z4_c1 * (UM(b, j + 2, i) + UM(b, j - 2, i) + UM(b, j, i + 2) + UM(b, j, i - 2)) +
-                       z4_c2 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
-                       z4_c3 * (UM(b, j, i)));
-      const int nb = (g.bl && j == g.jdi1) + (g.br && j == g.jdi2) + (g.bb && i == g.idi1) + (g.bt && i == g.idi2);
-      for (int q = 0; q < nb; q++)
-        t = t + xkd * (z4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
-                       z4_c2 * (UM(b, j, i)));
-    }
-    F3(ten, j, i, k) = t;
-  }
-#undef UM
-}
-
 // tau, Main/mod_bdycod.F90:5115-5123
 __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax) {
   if (z > zmax - c->rayhd) {
@@ -568,53 +258,325 @@ __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax)
   return d_zero;
 }
 
-// tendency sums (:285-314, 332-349), Rayleigh damping of t and qv (:356-364), forecast of t
-// and moisture (:368-380) and the momentum sums (:404-411).  k = 1..kz+1.
-__global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
+// ---------------------------------------------------------------------------------------
+// The tendency chain of the NH core as two point kernels.  For each variable the reference
+// accumulates pc_dynamic over several loop nests -- advection (hadv/vadv), curvature or the
+// adiabatic terms, the boundary relaxation, the diffusion -- and then sums pc_total + pc_dynamic
+// + pc_physic in the forecast (Main/mod_tendency.F90:1227-1680, 285-411).  Every one of those
+// nests updates the element of its own point only, and reads fields the chain never writes,
+// so one thread can run the whole chain for its point and level in the reference's order,
+// holding the running tendency in a register: the values are those of the separate nests,
+// and pc_dynamic never reaches memory.
+//   k_nh_tend_c, cross points, k = 1..kz+1: w, pp, t (ithadv = 1), qv, qc and the forecast of
+//     t and moisture (atmc), with the t/qv Rayleigh damping; the ring of the cross frame
+//     passes atm2 moisture to the forecasts;
+//   k_nh_tend_d, dot points, k = 1..kz: u, v.
+// The total tendencies (pc_total) are init_tendencies' zero except where the iboudy = 4
+// sponges set them (band points).  tten/qvten/qcten are stored only with diagnostics on
+// (wdiag): the step itself reads the forecasts.
+__global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
+                                                   const StepState* __restrict__ s, NHFields f, int wdiag) {
   FRAME_POINT();
   const int kz = c->kz;
   const double dt = s->dt;
-  // the total tendencies are init_tendencies' zero except where the iboudy = 4 sponges of
-  // k_nh_boundary wrote them (band points), so they are read only there
-  const bool spc = c->iboudy == 4 && IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0;
-  const bool spd = c->iboudy == 4 && IN_DI(j, i) && f.rgdt[g.ix(j, i)] > 0;
-#define TEN0(p, sp) ((sp) ? F3(f.p, j, i, k) : d_zero)
-  if (IN_CI(j, i)) {
-#define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
-    F3(f.wten, j, i, k) = TEN0(wten, spc) + F3(f.wdyn, j, i, k) + PHY(wphy);
-    if (k <= kz) {
-      double tt = TEN0(tten, spc) + F3(f.tdyn, j, i, k) + PHY(tphy);
-      double qv = TEN0(qvten, spc) + F3(f.qvdyn, j, i, k) + PHY(qvphy);
-      F3(f.ppten, j, i, k) = TEN0(ppten, spc) + F3(f.ppdyn, j, i, k) + PHY(ppphy);
-      double qc = d_zero + F3(f.qcdyn, j, i, k) + PHY(qcphy);
-      tt = tt + 0.0; qv = qv + 0.0; qc = qc + 0.0;
-      if (c->ifrayd == 1 && k <= c->rayndamp) {
-        const double xt = s->xbctime + dt;
-        const double tau = nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1));
-        tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
-        qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
-      }
-      F3(f.tten, j, i, k) = tt; F3(f.qvten, j, i, k) = qv; F3(f.qcten, j, i, k) = qc;
-      F3(f.ct, j, i, k) = F3(f.a2t, j, i, k) + dt * tt;
+  if (!IN_CI(j, i)) {
+    if (k <= kz && IN_CE(j, i)) {
+      F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k);
+      F3(f.cqc, j, i, k) = F3(f.a2qc, j, i, k);
     }
+    return;
+  }
+  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
+  auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
+    u1 = F3(f.umc, j, i + 1, kk) + F3(f.umc, j, i, kk);
+    u2 = F3(f.umc, j + 1, i + 1, kk) + F3(f.umc, j + 1, i, kk);
+    v1 = F3(f.vmc, j + 1, i, kk) + F3(f.vmc, j, i, kk);
+    v2 = F3(f.vmc, j + 1, i + 1, kk) + F3(f.vmc, j, i + 1, kk);
+  };
+  // boundary relaxation (:1462-1501, Main/mod_bdycod.F90): nudging coefficients of the band
+  const bool band = f.rgcr[g.ix(j, i)] > 0;
+  const bool sponge = band && c->iboudy == 4;
+  const bool nudge = band && c->iboudy != 4;
+  const double xt = s->xbctime + s->dt;
+  const int kc = (k < kz) ? k : kz;
+  double xf = d_zero, xg = d_zero, wsp = d_zero;
+  if (band) {
+    const int ib = f.ibcr[g.ix(j, i)];
+    if (c->iboudy == 4) wsp = c->wgtx[ib];
+    else if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
+    else { xf = c->hefc[ib][kc]; xg = c->hegc[ib][kc]; }
+  }
+#define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
+#define RELAX5(x, b0, bt, a) \
+  x = nh_relax(x, xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), FG(b0, bt, a, j + 1, i), \
+               FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
+#define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
+  // ================= w on full levels k = 1..kz+1
+  {
+    double wd = d_zero;
+    if (k >= 2 && k <= kz) {                       // hadv3d ind = 1, Main/mod_advection.F90:486-507
+      double u1, u2, v1, v2, pu1, pu2, pv1, pv2;
+      avg(k, u1, u2, v1, v2);
+      avg(k - 1, pu1, pu2, pv1, pv2);
+      const double t1 = c->twt1[k], t2 = c->twt2[k];
+      const double uaz1 = (t1 * u1 + t2 * pu1), uaz2 = (t1 * u2 + t2 * pu2);
+      const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
+      const double f1 = d_half * ul * (u2 + u1) / ps;
+      const double f2 = d_half * ul * (v2 + v1) / ps;
+      const double* w = f.xw;
+      const double fx1 = (d_one + f1) * F3(w, j - 1, i, k) + (d_one - f1) * F3(w, j, i, k);
+      const double fx2 = (d_one + f1) * F3(w, j, i, k) + (d_one - f1) * F3(w, j + 1, i, k);
+      const double fy1 = (d_one + f2) * F3(w, j, i - 1, k) + (d_one - f2) * F3(w, j, i, k);
+      const double fy2 = (d_one + f2) * F3(w, j, i, k) + (d_one - f2) * F3(w, j, i + 1, k);
+      wd = wd - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
+    }
+    // vadv3d ind = 0, nk = kz+1 (w), :756-765: flux through the interface below level kk
+    auto wflux = [&](int kk) {
+      const double qq = d_half * (F3(f.qdot, j, i, kk) + F3(f.qdot, j, i, kk + 1));
+      return qq * ((F3(f.a1w, j, i, kk) + F3(f.a1w, j, i, kk + 1)));
+    };
+    if (k >= 2) wd = wd + wflux(k - 1) * c->dds[k];
+    if (k <= kz) wd = wd - wflux(k) * c->dds[k];
+    if (k >= 2 && k <= kz) {                       // adiabatic NH, Main/mod_tendency.F90:1601-1671
+      auto ucc = [&](int kk) {
+        return F3(f.a1u, j, i, kk) + F3(f.a1u, j, i + 1, kk) + F3(f.a1u, j + 1, i, kk) + F3(f.a1u, j + 1, i + 1, kk);
+      };
+      auto vcc = [&](int kk) {
+        return F3(f.a1v, j, i, kk) + F3(f.a1v, j, i + 1, kk) + F3(f.a1v, j + 1, i, kk) + F3(f.a1v, j + 1, i + 1, kk);
+      };
+      const double uk = ucc(k), vk = vcc(k), um = ucc(k - 1), vm = vcc(k - 1);
+      const double rps = F2(f.rpsa, j, i);
+      const double ex = F2(f.ex, j, i), crx = F2(f.crx, j, i), cry = F2(f.cry, j, i);
+      const double rofac = (c->dsigma[k - 1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, k - 1)) /
+                           (c->dsigma[k - 1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, k - 1));
+      const double uaq = d_rfour * (c->twt1[k] * uk + c->twt2[k] * um);
+      const double vaq = d_rfour * (c->twt1[k] * vk + c->twt2[k] * vm);
+      wd = wd +
+          (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
+          ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
+          F3(f.xw, j, i, k) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
+      wd = wd - EGRAV_NH * ps * (c->twt2[k] * F3(f.xqc, j, i, k - 1) + c->twt1[k] * F3(f.xqc, j, i, k));
+    }
+    double wt0 = d_zero;
+    if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
+    if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
+    wd = diffx_at(g, c, wd, f.wb3d, f.xkcf, j, i, k);
+    F3(f.wten, j, i, k) = wt0 + wd + PHY(wphy);
   }
   if (k > kz) return;
-  if (IN_CE(j, i)) {
-    double qv = F3(f.a2qv, j, i, k), qc = F3(f.a2qc, j, i, k);
-    if (IN_CI(j, i)) {
-      qv = qv + dt * F3(f.qvten, j, i, k);
-      qc = qc + dt * F3(f.qcten, j, i, k);
+  double u1, u2, v1, v2;
+  avg(k, u1, u2, v1, v2);
+  const double cr = F3(f.cr, j, i, k);
+  // ================= pp: hadv3d ind 0, vadv3d ind = 0 (nk = kz), adiabatic, boundary, diffusion
+  {
+    double pd = d_zero + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    auto pflux = [&](int kk) {
+      return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
+    };
+    if (k >= 2) pd = pd + pflux(k) * c->xds[k];
+    if (k + 1 <= kz) pd = pd - pflux(k + 1) * c->xds[k];
+    pd = pd + F3(f.xpp, j, i, k) * cr;
+    double pt0 = d_zero;
+    if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
+    if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
+    pd = diffx_at(g, c, pd, f.ppb3d, f.xkc, j, i, k);
+    F3(f.ppten, j, i, k) = pt0 + pd + PHY(ppphy);
+  }
+  const bool ray = c->ifrayd == 1 && k <= c->rayndamp;
+  const double tau = ray ? nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) : d_zero;
+  // ================= t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d
+  // ind = 0 (nk = kz) of tha = th*p*, plus th*cr; tdyn = atm1%t*thten/tha
+  {
+    double thd = d_zero + hadv_fg(g, c, f.th, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
+    auto thflux = [&](int kk) {
+      return F3(f.qdot, j, i, kk) *
+             (c->twt1[kk] * (F3(f.th, j, i, kk) * ps) + c->twt2[kk] * (F3(f.th, j, i, kk - 1) * ps));
+    };
+    if (k >= 2) thd = thd + thflux(k) * c->xds[k];
+    if (k + 1 <= kz) thd = thd - thflux(k + 1) * c->xds[k];
+    const double th = F3(f.th, j, i, k);
+    thd = thd + th * cr;
+    double td = d_zero + F3(f.a1t, j, i, k) * thd / (th * ps);
+    double tt0 = d_zero;
+    if (sponge) tt0 = wsp * d_zero + (d_one - wsp) * F3(f.tbt, j, i, k);
+    if (nudge) RELAX5(td, f.tb0, f.tbt, f.a2t);
+    td = diffx_at(g, c, td, f.tb3d, f.xkc, j, i, k);
+    double tt = tt0 + td + PHY(tphy);
+    tt = tt + 0.0;
+    if (ray) tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
+    if (wdiag) F3(f.tten, j, i, k) = tt;
+    F3(f.ct, j, i, k) = F3(f.a2t, j, i, k) + dt * tt;
+  }
+  // ================= qv: hadvqv (or the semi-Lagrangian start), vadvqv, adiabatic, boundary,
+  // diffusion, forecast
+  {
+    double qd = d_zero + (c->isladvec ? F3(f.slqv, j, i, k)
+                                      : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
+    const double thr = MINQQ * ps;
+    auto qflux = [&](int kk) {
+      const double fk = F3(f.a1qv, j, i, kk), fkm = F3(f.a1qv, j, i, kk - 1);
+      double fg = d_zero;
+      if (fk > thr && fkm > thr) fg = fk * rcm_powpos(fkm / fk, c->qcon[kk]);
+      return F3(f.qdot, j, i, kk) * fg;
+    };
+    if (k >= 2) qd = qd + qflux(k) * c->xds[k];
+    if (k + 1 <= kz) qd = qd - qflux(k + 1) * c->xds[k];
+    qd = qd + F3(f.xqv, j, i, k) * cr;
+    double qt0 = d_zero;
+    if (sponge) qt0 = wsp * d_zero + (d_one - wsp) * F3(f.qbt, j, i, k);
+    if (nudge) {
+      const double nfac = 1.0e3, rfac = d_one / nfac;
+#define FQ(J, I) (nfac * (F3(f.qb0, J, I, k) + xt * F3(f.qbt, J, I, k)) - nfac * F3(f.a2qv, J, I, k))
+      const double q0 = FQ(j, i), q1 = FQ(j - 1, i), q2 = FQ(j + 1, i), q3 = FQ(j, i - 1), q4 = FQ(j, i + 1);
+#undef FQ
+      qd = qd + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
     }
-    F3(f.cqv, j, i, k) = qv;
-    F3(f.cqc, j, i, k) = qc;
+    qd = diffx_at(g, c, qd, f.qvb3d, f.xkc, j, i, k);
+    double qv = qt0 + qd + PHY(qvphy);
+    qv = qv + 0.0;
+    if (ray) qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
+    if (wdiag) F3(f.qvten, j, i, k) = qv;
+    F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) + dt * qv;
   }
-  if (IN_DI(j, i)) {
-    F3(f.uten, j, i, k) = TEN0(uten, spd) + F3(f.udyn, j, i, k) + PHY(uphy);
-    F3(f.vten, j, i, k) = TEN0(vten, spd) + F3(f.vdyn, j, i, k) + PHY(vphy);
+  // ================= qc: hadvqx (or the semi-Lagrangian start), vadv4d ind = 1, adiabatic,
+  // diffusion, forecast
+  {
+    double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
+                                      : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
+    const double thr = MINQQ * MINQQ * ps;
+    auto cflux = [&](int kk) {
+      const double svv = F3(f.qdot, j, i, kk);
+      const double fk = F3(f.a1qc, j, i, kk), fkm = F3(f.a1qc, j, i, kk - 1);
+      if (svv > d_zero) return (fkm > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+      return (fk > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+    };
+    if (k >= 2) cd = cd + cflux(k) * c->xds[k];
+    if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
+    cd = cd + F3(f.xqc, j, i, k) * cr;
+    cd = diffx_at(g, c, cd, f.qcb3d, f.xkc, j, i, k);
+    double qc = d_zero + cd + PHY(qcphy);
+    qc = qc + 0.0;
+    if (wdiag) F3(f.qcten, j, i, k) = qc;
+    F3(f.cqc, j, i, k) = F3(f.a2qc, j, i, k) + dt * qc;
   }
-#undef PHY
-#undef TEN0
 }
+
+__global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restrict__ c,
+                                                   const StepState* __restrict__ s, NHFields f) {
+  THREAD_POINT(g.jdi1, g.idi1);
+  if (!IN_DI(j, i)) return;
+  const int kz = c->kz;
+  double ud, vd;
+  // hadvuv NH upstream branch, Main/mod_advection.F90:235-264
+  {
+    const double ul = c->ul, dm = F2(f.dmsf, j, i);
+    const double* ua = f.umc; const double* va = f.vmc; const double* u = f.ud; const double* v = f.vd;
+    const double divd = d_rfour * (F3(f.cr, j, i, k) + F3(f.cr, j, i - 1, k) + F3(f.cr, j - 1, i, k) +
+                                   F3(f.cr, j - 1, i - 1, k));
+    const double ucmona = F3(ua, j, i + 1, k) + d_two * F3(ua, j, i, k) + F3(ua, j, i - 1, k);
+    double ucmonb = F3(ua, j + 1, i + 1, k) + d_two * F3(ua, j + 1, i, k) + F3(ua, j + 1, i - 1, k);
+    double ucmonc = F3(ua, j - 1, i + 1, k) + d_two * F3(ua, j - 1, i, k) + F3(ua, j - 1, i - 1, k);
+    const double vcmona = F3(va, j + 1, i, k) + d_two * F3(va, j, i, k) + F3(va, j - 1, i, k);
+    double vcmonb = F3(va, j + 1, i + 1, k) + d_two * F3(va, j, i + 1, k) + F3(va, j - 1, i + 1, k);
+    double vcmonc = F3(va, j + 1, i - 1, k) + d_two * F3(va, j, i - 1, k) + F3(va, j - 1, i - 1, k);
+    const double diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc));
+    const double u0 = F3(u, j, i, k), ue = F3(u, j + 1, i, k), uw = F3(u, j - 1, i, k);
+    const double un = F3(u, j, i + 1, k), us = F3(u, j, i - 1, k);
+    const double v0 = F3(v, j, i, k), ve = F3(v, j + 1, i, k), vw = F3(v, j - 1, i, k);
+    const double vn = F3(v, j, i + 1, k), vs = F3(v, j, i - 1, k);
+    const double ff1 = ul * (ue + u0), ff2 = ul * (uw + u0);
+    const double ff3 = ul * (vn + v0), ff4 = ul * (vs + v0);
+    ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+    ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+    vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+    vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+    ud = d_zero + u0 * diag - dm * (ue * ucmonb - uw * ucmonc + un * vcmonb - us * vcmonc);
+    vd = d_zero + v0 * diag - dm * (ve * ucmonb - vw * ucmonc + vn * vcmonb - vs * vcmonc);
+  }
+  // vadvuv (:286-299): the flux through interface kk reaches level kk (added) and kk-1
+  // (subtracted), in the reference's loop order
+  {
+    auto flux = [&](int kk, double& uu, double& vv) {
+      const double qq = d_rfour * (F3(f.qdot, j, i, kk) + F3(f.qdot, j, i - 1, kk) + F3(f.qdot, j - 1, i, kk) +
+                                   F3(f.qdot, j - 1, i - 1, kk));
+      uu = qq * (c->twt1[kk] * F3(f.a1u, j, i, kk) + c->twt2[kk] * F3(f.a1u, j, i, kk - 1));
+      vv = qq * (c->twt1[kk] * F3(f.a1v, j, i, kk) + c->twt2[kk] * F3(f.a1v, j, i, kk - 1));
+    };
+    double uu, vv;
+    if (k >= 2) {
+      flux(k, uu, vv);
+      ud = ud + uu * c->xds[k];
+      vd = vd + vv * c->xds[k];
+    }
+    if (k + 1 <= kz) {
+      flux(k + 1, uu, vv);
+      ud = ud - uu * c->xds[k];
+      vd = vd - vv * c->xds[k];
+    }
+  }
+  // curvature NH (:1839-1879): horizontal and vertical Coriolis, horizontal and vertical curvature
+  {
+    const double* w = f.a1w;
+    const double wadot = 0.125 * (F3(w, j - 1, i - 1, k) + F3(w, j - 1, i, k) + F3(w, j, i - 1, k) + F3(w, j, i, k));
+    const double wadotp1 = 0.125 * (F3(w, j - 1, i - 1, k + 1) + F3(w, j - 1, i, k + 1) + F3(w, j, i - 1, k + 1) +
+                                    F3(w, j, i, k + 1));
+    const double wabar = wadot + wadotp1;
+    const double amfac = wabar * F2(f.rpsda, j, i) * REARTHRAD;
+    const double uc = F3(f.a1u, j, i, k), vc = F3(f.a1v, j, i, k);
+    const double duv = uc * F2(f.dmdy, j, i) - vc * F2(f.dmdx, j, i);
+    const double cor = F2(f.coriol, j, i), ef = F2(f.ef, j, i);
+    ud = ud + cor * vc - ef * F2(f.ddx, j, i) * wabar + F3(f.vmd, j, i, k) * duv - uc * amfac;
+    vd = vd - cor * uc + ef * F2(f.ddy, j, i) * wabar - F3(f.umd, j, i, k) * duv - vc * amfac;
+  }
+  // boundary relaxation of u, v (nudgeuv) or the iboudy = 4 sponge of their total tendencies
+  double ut0 = d_zero, vt0 = d_zero;
+  if (f.rgdt[g.ix(j, i)] > 0) {
+    const int ib = f.ibdt[g.ix(j, i)];
+    if (c->iboudy == 4) {
+      const double w = c->wgtd[ib];
+      ut0 = w * d_zero + (d_one - w) * F3(f.ubt, j, i, k);
+      vt0 = w * d_zero + (d_one - w) * F3(f.vbt, j, i, k);
+    } else {
+      const double xt = s->xbctime + s->dt;
+      double xf, xg;
+      if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
+      else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
+      RELAX5(ud, f.ub0, f.ubt, f.a2u);
+      RELAX5(vd, f.vb0, f.vbt, f.a2v);
+    }
+  }
+  // diffu_d, Main/mod_diffusion.F90:281-411
+  {
+    const double* m = f.msfd;
+#define UM(a, J, I) (F3(a, J, I, k) / F2(m, J, I))
+    const double xkd = F3(f.xkd, j, i, k);
+    for (int pass = 0; pass < 2; pass++) {
+      const double* b = pass ? f.vbd : f.ubd;
+      double t = pass ? vd : ud;
+      if (c->idiffu == 2) {
+        t = t + xkd * (o4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                       o4_c2 * (UM(b, j + 1, i + 1) + UM(b, j - 1, i - 1) + UM(b, j - 1, i + 1) + UM(b, j + 1, i - 1)) +
+                       o4_c3 * (UM(b, j, i)));
+      } else {
+        if (in(j, g.jdii1, g.jdii2) && in(i, g.idii1, g.idii2))
+          t = t - xkd * (z4_c1 * (UM(b, j + 2, i) + UM(b, j - 2, i) + UM(b, j, i + 2) + UM(b, j, i - 2)) +
+                         z4_c2 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                         z4_c3 * (UM(b, j, i)));
+        const int nb = (g.bl && j == g.jdi1) + (g.br && j == g.jdi2) + (g.bb && i == g.idi1) + (g.bt && i == g.idi2);
+        for (int q = 0; q < nb; q++)
+          t = t + xkd * (z4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
+                         z4_c2 * (UM(b, j, i)));
+      }
+      if (pass) vd = t; else ud = t;
+    }
+#undef UM
+  }
+  F3(f.uten, j, i, k) = ut0 + ud + PHY(uphy);
+  F3(f.vten, j, i, k) = vt0 + vd + PHY(vphy);
+}
+#undef PHY
+#undef RELAX5
+#undef FG
 
 // negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points
 // whose sweep predecessors are non-negative, serial sweep of the flagged planes after it.

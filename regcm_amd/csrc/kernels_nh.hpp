@@ -52,13 +52,8 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_uv_adv(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_scalar_adv(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_curvature(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_adiabatic(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_boundary(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
-__global__ void k_nh_diffusion(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_forecast(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_tend_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int wdiag);
+__global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f);
