@@ -1399,8 +1399,8 @@ struct rcmdyn_engine {
       if (cfg.isladvec == 1)
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
       // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
-      KLAUNCH(k_nh_tend_d, q.dik, BLK, 0, stream, g, dc, ds, f);
-      KLAUNCH(k_nh_tend_c, q.fr, BLK, 0, stream, g, dc, ds, f, (int)diag);
+      KLAUNCH(k_nh_tend_d, q.dik, BLK, 0, stream, g, dc, ds, f, istep);
+      KLAUNCH(k_nh_tend_c, q.fr, BLK, 0, stream, g, dc, ds, f, (int)diag, istep);
     });
     tke_step();
     xch({{FK::CQV, kz}, {FK::CQC, kz}});
@@ -1411,7 +1411,6 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
       KLAUNCH(k_nh_tfilter, q.cik, BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_raydamp, q.fr, BLK, 0, stream, g, dc, ds, f);
       // sound, Main/mod_sound.F90:163-718
       KLAUNCH(k_nh_sound_init, q.fr, BLK, 0, stream, g, dc, ds, f, istep);
     });

@@ -273,9 +273,13 @@ __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax)
 //   k_nh_tend_d, dot points, k = 1..kz: u, v.
 // The total tendencies (pc_total) are init_tendencies' zero except where the iboudy = 4
 // sponges set them (band points).  tten/qvten/qcten are stored only with diagnostics on
-// (wdiag): the step itself reads the forecasts.
+// (wdiag): the step itself reads the forecasts.  The chains of u, v, pp and w end with the
+// Rayleigh damping and decoupling of raydamp (:466-499; they read atm2 u, v, pp, w, which the
+// time filters in between do not change) and with sound's scaling by the acoustic step
+// (Main/mod_sound.F90:229-245): those are the tendencies sound reads.
 __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
-                                                   const StepState* __restrict__ s, NHFields f, int wdiag) {
+                                                   const StepState* __restrict__ s, NHFields f, int wdiag,
+                                                   int istep) {
   FRAME_POINT();
   const int kz = c->kz;
   const double dt = s->dt;
@@ -298,6 +302,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   const bool sponge = band && c->iboudy == 4;
   const bool nudge = band && c->iboudy != 4;
   const double xt = s->xbctime + s->dt;
+  const double dts = s->dt / (double)istep;
   const int kc = (k < kz) ? k : kz;
   double xf = d_zero, xg = d_zero, wsp = d_zero;
   if (band) {
@@ -361,7 +366,11 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
     if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
     wd = diffx_at(g, c, wd, f.wb3d, f.xkcf, j, i, k);
-    F3(f.wten, j, i, k) = wt0 + wd + PHY(wphy);
+    double wt = wt0 + wd + PHY(wphy);
+    // raydamp3f and decoupling before sound (:466-499), sound's acoustic-step scaling (:229-245)
+    if (c->ifrayd == 1 && k <= c->rayndamp)
+      wt = wt + nh_tau(c, F3(f.zf0, j, i, k), F3(f.zf0, j, i, 1)) * (d_zero - F3(f.a2w, j, i, k));
+    F3(f.wten, j, i, k) = (wt * F2(f.rpsa, j, i)) * dts;
   }
   if (k > kz) return;
   double u1, u2, v1, v2;
@@ -380,7 +389,11 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
     if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
     pd = diffx_at(g, c, pd, f.ppb3d, f.xkc, j, i, k);
-    F3(f.ppten, j, i, k) = pt0 + pd + PHY(ppphy);
+    double pt = pt0 + pd + PHY(ppphy);
+    if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3, decoupling, acoustic-step scaling
+      pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
+                    ((F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k)) - F3(f.a2pp, j, i, k));
+    F3(f.ppten, j, i, k) = (pt * F2(f.rpsa, j, i)) * dts;
   }
   const bool ray = c->ifrayd == 1 && k <= c->rayndamp;
   const double tau = ray ? nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) : d_zero;
@@ -462,7 +475,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
 }
 
 __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restrict__ c,
-                                                   const StepState* __restrict__ s, NHFields f) {
+                                                   const StepState* __restrict__ s, NHFields f, int istep) {
   THREAD_POINT(g.jdi1, g.idi1);
   if (!IN_DI(j, i)) return;
   const int kz = c->kz;
@@ -571,8 +584,22 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
     }
 #undef UM
   }
-  F3(f.uten, j, i, k) = ut0 + ud + PHY(uphy);
-  F3(f.vten, j, i, k) = vt0 + vd + PHY(vphy);
+  double ut = ut0 + ud + PHY(uphy);
+  double vt = vt0 + vd + PHY(vphy);
+  // Rayleigh damping and decoupling before sound (raydampuv, :466-499), then sound's scaling
+  // by the acoustic step (Main/mod_sound.F90:229-236)
+  if (c->ifrayd == 1 && k <= c->rayndamp) {
+    const double xt = s->xbctime + s->dt;
+    const double* z = f.z0;
+    const double zz = d_rfour * (F3(z, j, i, k) + F3(z, j - 1, i, k) + F3(z, j, i - 1, k) + F3(z, j - 1, i - 1, k));
+    const double zm = d_rfour * (F3(z, j, i, 1) + F3(z, j - 1, i, 1) + F3(z, j, i - 1, 1) + F3(z, j - 1, i - 1, 1));
+    const double tau = nh_tau(c, zz, zm);
+    ut = ut + tau * ((F3(f.ub0, j, i, k) + xt * F3(f.ubt, j, i, k)) - F3(f.a2u, j, i, k));
+    vt = vt + tau * ((F3(f.vb0, j, i, k) + xt * F3(f.vbt, j, i, k)) - F3(f.a2v, j, i, k));
+  }
+  const double dts = s->dt / (double)istep;
+  F3(f.uten, j, i, k) = (ut * F2(f.rpsda, j, i)) * dts;
+  F3(f.vten, j, i, k) = (vt * F2(f.rpsda, j, i)) * dts;
 }
 #undef PHY
 #undef RELAX5
@@ -669,64 +696,24 @@ __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f) {
   }
 }
 
-// Rayleigh damping of u, v, pp, w and decoupling of the tendencies before sound
-// (:466-499; raydampuv/raydamp3/raydamp3f, Main/mod_bdycod.F90:4953-5045).  k = 1..kz+1.
-__global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  const bool ray = c->ifrayd == 1 && k <= c->rayndamp;
-  const double xt = s->xbctime + s->dt;
-  if (k <= kz && IN_DI(j, i)) {
-    double ut = F3(f.uten, j, i, k), vt = F3(f.vten, j, i, k);
-    if (ray) {
-      const double* z = f.z0;
-      const double zz = d_rfour * (F3(z, j, i, k) + F3(z, j - 1, i, k) + F3(z, j, i - 1, k) + F3(z, j - 1, i - 1, k));
-      const double zm = d_rfour * (F3(z, j, i, 1) + F3(z, j - 1, i, 1) + F3(z, j, i - 1, 1) + F3(z, j - 1, i - 1, 1));
-      const double tau = nh_tau(c, zz, zm);
-      ut = ut + tau * ((F3(f.ub0, j, i, k) + xt * F3(f.ubt, j, i, k)) - F3(f.a2u, j, i, k));
-      vt = vt + tau * ((F3(f.vb0, j, i, k) + xt * F3(f.vbt, j, i, k)) - F3(f.a2v, j, i, k));
-    }
-    F3(f.uten, j, i, k) = ut * F2(f.rpsda, j, i);
-    F3(f.vten, j, i, k) = vt * F2(f.rpsda, j, i);
-  }
-  if (!IN_CI(j, i)) return;
-  if (k <= kz) {
-    double pt = F3(f.ppten, j, i, k);
-    if (ray)
-      pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
-                    ((F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k)) - F3(f.a2pp, j, i, k));
-    F3(f.ppten, j, i, k) = pt * F2(f.rpsa, j, i);
-  }
-  double wt = F3(f.wten, j, i, k);
-  if (ray) wt = wt + nh_tau(c, F3(f.zf0, j, i, k), F3(f.zf0, j, i, 1)) * (d_zero - F3(f.a2w, j, i, k));
-  F3(f.wten, j, i, k) = wt * F2(f.rpsa, j, i);
-}
-
 // ======================================================================= sound
-// initial arrays of the acoustic loop (Main/mod_sound.F90:217-245).  k = 1..kz+1.
+// initial arrays of the acoustic loop (Main/mod_sound.F90:217-245; the tendencies' scaling by
+// the acoustic step ends the tendency kernels).  k = 1..kz+1.
 __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
                                 int istep) {
   FRAME_POINT();
   const int kz = c->kz;
-  const double dts = s->dt / (double)istep;
+  (void)s; (void)istep;
   const double rpb = IN_CE(j, i) ? F2(f.rpsb, j, i) : 0.0;
   if (k <= kz) {
     if (IN_DE(j, i)) {
       F3(f.cu, j, i, k) = F3(f.a2u, j, i, k) / F2(f.psdotb, j, i);
       F3(f.cv, j, i, k) = F3(f.a2v, j, i, k) / F2(f.psdotb, j, i);
     }
-    if (IN_DI(j, i)) {
-      F3(f.uten, j, i, k) = F3(f.uten, j, i, k) * dts;
-      F3(f.vten, j, i, k) = F3(f.vten, j, i, k) * dts;
-    }
     if (IN_CE(j, i)) F3(f.cpp, j, i, k) = F3(f.a2pp, j, i, k) * rpb;
-    if (IN_CI(j, i)) {
-      F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) * rpb;
-      F3(f.ppten, j, i, k) = F3(f.ppten, j, i, k) * dts;
-    }
+    if (IN_CI(j, i)) F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) * rpb;
   }
   if (IN_CE(j, i)) F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
-  if (IN_CI(j, i)) F3(f.wten, j, i, k) = F3(f.wten, j, i, k) * dts;
 }
 
 // substep part A (:250-262), one thread per cross column: pp += xkd*pi, then dp'/dp0
@@ -762,6 +749,52 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
   F3(f.cv, j, i, k) = v + F3(f.vten, j, i, k);
 }
 
+// cu, cv at the dot points (j,i), (j+1,i), (j,i+1), (j+1,i+1) around a cross point, one level
+struct NhQ { double u[4], v[4]; };
+__device__ __forceinline__ NhQ nh_q_at(const Geom& g, const NHFields& f, int j, int i, int k) {
+  NhQ q;
+  q.u[0] = F3(f.cu, j, i, k); q.u[1] = F3(f.cu, j + 1, i, k); q.u[2] = F3(f.cu, j, i + 1, k); q.u[3] = F3(f.cu, j + 1, i + 1, k);
+  q.v[0] = F3(f.cv, j, i, k); q.v[1] = F3(f.cv, j + 1, i, k); q.v[2] = F3(f.cv, j, i + 1, k); q.v[3] = F3(f.cv, j + 1, i + 1, k);
+  return q;
+}
+struct NhB1 { double p, cc, cdd, cj, tk, ptend, rho0; };
+// the level-parallel coefficients of level k (:297-399) from the column's rings: qm, q0, qp are
+// cu/cv at km1 = k-1, k and kp1 = min(k+1, kz) (k = 1: levels 1 and 2 in q0, qp), pcm/pc/pcp
+// pr0 of the column there; m[] msfd at the four dot points
+__device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
+                                               int k, int kz, int it, double dts, double msfx, double ps0,
+                                               double rpb, const NhQ& qm, const NhQ& q0, const NhQ& qp,
+                                               double pcm, double pc, double pcp, const double* m) {
+  NhB1 r;
+  const double xg = c->xgamma;
+  const double* pr0 = f.pr0;
+  r.p = F3(f.cpp, j, i, k);
+  if (it > 1) r.p = r.p - c->nhxkd * F3(f.spi, j, i, k);
+  const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
+  r.rho0 = rho0;
+  r.cc = xg * pr1 * dts / (c->dx * msfx);
+  r.cdd = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
+  r.cj = d_half * rho0 * EGRAV_NH * dts;
+  r.tk = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * pc * F3(f.a2t, j, i, k) * rpb);
+  double pxup, pyvp;
+  if (k == 1) {
+    pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
+        (q0.u[0] + q0.u[1] + q0.u[2] + q0.u[3] - qp.u[0] - qp.u[1] - qp.u[2] - qp.u[3]) / (pc - pcp);
+    pyvp = 0.0625 * (F3(pr0, j, i + 1, 1) - F3(pr0, j, i - 1, 1)) *
+        (q0.v[0] + q0.v[1] + q0.v[2] + q0.v[3] - qp.v[0] - qp.v[1] - qp.v[2] - qp.v[3]) / (pc - pcp);
+  } else {
+    pyvp = 0.125 * (F3(pr0, j, i + 1, k) - F3(pr0, j, i - 1, k)) *
+        (qm.v[0] + qm.v[1] + qm.v[2] + qm.v[3] - qp.v[0] - qp.v[1] - qp.v[2] - qp.v[3]) / (pcm - pcp);
+    pxup = 0.125 * (F3(pr0, j + 1, i, k) - F3(pr0, j - 1, i, k)) *
+        (qm.u[0] + qm.u[1] + qm.u[2] + qm.u[3] - qp.u[0] - qp.u[1] - qp.u[2] - qp.u[3]) / (pcm - pcp);
+    if (k == kz) { pyvp = pyvp * d_half; pxup = pxup * d_half; }
+  }
+  const double div = (q0.v[2] * m[2] - q0.v[0] * m[0] + q0.v[3] * m[3] - q0.v[1] * m[1] +
+                      q0.u[1] * m[1] - q0.u[0] * m[0] + q0.u[3] * m[3] - q0.u[2] * m[2]) / msfx;
+  r.ptend = F3(f.ppten, j, i, k) - d_half * r.cc * (div - d_two * (pyvp + pxup));
+  return r;
+}
+
 // substep part C (:297-483) as one column kernel, one thread per interior cross column
 // walking k = kz..1: the level-parallel coefficients of a level (undo of the divergence
 // damping of pp, Ikawa cc/cdd/cj, the temperature factor tk, the horizontal pressure-advection
@@ -769,97 +802,57 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
 // and feed the tridiagonal coefficients and right-hand side of the implicit w equation at the
 // level below them (:400-457), the pp predictor (:458-464) and the sweep of the tridiagonal
 // system (:468-476) in the same pass; the inputs of the upper radiative condition (:488-494)
-// close the column.  Every value is the reference's expression; only se and sf (read by the
-// downward sweep after the radiative condition's domain convolution) and the new pp, pi leave
-// the column.
-struct NhB1 { double p, cc, cdd, cj, tk, ptend; };
-__device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
-                                               int k, int kz, int it, double dts, double msfx, double ps0,
-                                               double rpb) {
-  NhB1 r;
-  const double xg = c->xgamma;
-  const double* cu = f.cu;
-  const double* cv = f.cv;
-  const double* pr0 = f.pr0;
-  r.p = F3(f.cpp, j, i, k);
-  if (it > 1) r.p = r.p - c->nhxkd * F3(f.spi, j, i, k);
-  const double pr1 = F3(f.pr1, j, i, k), rho0 = F3(f.rho0, j, i, k);
-  r.cc = xg * pr1 * dts / (c->dx * msfx);
-  r.cdd = xg * pr1 * rho0 * EGRAV_NH * dts / (ps0 * c->dsigma[k]);
-  r.cj = d_half * rho0 * EGRAV_NH * dts;
-  r.tk = (d_half * ps0 * F3(f.t0, j, i, k)) / (xg * F3(pr0, j, i, k) * F3(f.a2t, j, i, k) * rpb);
-  double pxup, pyvp;
-  if (k == 1) {
-    pxup = 0.0625 * (F3(pr0, j + 1, i, 1) - F3(pr0, j - 1, i, 1)) *
-        (F3(cu, j, i, 1) + F3(cu, j + 1, i, 1) + F3(cu, j, i + 1, 1) + F3(cu, j + 1, i + 1, 1) -
-         F3(cu, j, i, 2) - F3(cu, j + 1, i, 2) - F3(cu, j, i + 1, 2) - F3(cu, j + 1, i + 1, 2)) /
-        (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
-    pyvp = 0.0625 * (F3(pr0, j, i + 1, 1) - F3(pr0, j, i - 1, 1)) *
-        (F3(cv, j, i, 1) + F3(cv, j + 1, i, 1) + F3(cv, j, i + 1, 1) + F3(cv, j + 1, i + 1, 1) -
-         F3(cv, j, i, 2) - F3(cv, j + 1, i, 2) - F3(cv, j, i + 1, 2) - F3(cv, j + 1, i + 1, 2)) /
-        (F3(pr0, j, i, 1) - F3(pr0, j, i, 2));
-  } else {
-    const int kp1 = (k + 1 < kz) ? k + 1 : kz, km1 = k - 1;
-    pyvp = 0.125 * (F3(pr0, j, i + 1, k) - F3(pr0, j, i - 1, k)) *
-        (F3(cv, j, i, km1) + F3(cv, j + 1, i, km1) + F3(cv, j, i + 1, km1) + F3(cv, j + 1, i + 1, km1) -
-         F3(cv, j, i, kp1) - F3(cv, j + 1, i, kp1) - F3(cv, j, i + 1, kp1) - F3(cv, j + 1, i + 1, kp1)) /
-        (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
-    pxup = 0.125 * (F3(pr0, j + 1, i, k) - F3(pr0, j - 1, i, k)) *
-        (F3(cu, j, i, km1) + F3(cu, j + 1, i, km1) + F3(cu, j, i + 1, km1) + F3(cu, j + 1, i + 1, km1) -
-         F3(cu, j, i, kp1) - F3(cu, j + 1, i, kp1) - F3(cu, j, i + 1, kp1) - F3(cu, j + 1, i + 1, kp1)) /
-        (F3(pr0, j, i, km1) - F3(pr0, j, i, kp1));
-    if (k == kz) { pyvp = pyvp * d_half; pxup = pxup * d_half; }
-  }
-  const double* m = f.msfd;
-  const double div = (F3(cv, j, i + 1, k) * F2(m, j, i + 1) - F3(cv, j, i, k) * F2(m, j, i) +
-                      F3(cv, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cv, j + 1, i, k) * F2(m, j + 1, i) +
-                      F3(cu, j + 1, i, k) * F2(m, j + 1, i) - F3(cu, j, i, k) * F2(m, j, i) +
-                      F3(cu, j + 1, i + 1, k) * F2(m, j + 1, i + 1) - F3(cu, j, i + 1, k) * F2(m, j, i + 1)) / msfx;
-  r.ptend = F3(f.ppten, j, i, k) - d_half * r.cc * (div - d_two * (pyvp + pxup));
-  return r;
-}
-
+// close the column.  cu/cv around the column and its pr0 are loaded once per level and kept
+// in three-level rings.  Every value is the reference's expression; only se and sf (read by
+// the downward sweep after the radiative condition's domain convolution) and the new pp, pi
+// leave the column.
 #ifndef NHBC_W
 #define NHBC_W 2
 #endif
-__global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep, int it) {
+__global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c,
+                                                             const StepState* __restrict__ s, NHFields f,
+                                                             int istep, int it) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double dts = s->dt / (double)istep;
   const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
+  const double m[4] = {F2(f.msfd, j, i), F2(f.msfd, j + 1, i), F2(f.msfd, j, i + 1), F2(f.msfd, j + 1, i + 1)};
   const double bet = c->nhbet, bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
   const double bpxbp = bp * bp, bpxbm = bp * bm;
-  const double* cu = f.cu;
-  const double* cv = f.cv;
   const double* w = f.cw;                       // still the old w (wo) on levels 1..kz+1
+  NhQ qb = nh_q_at(g, f, j, i, kz), qa = nh_q_at(g, f, j, i, kz - 1);   // levels kz, kz-1
+  double pcb = F3(f.pr0, j, i, kz), pca = F3(f.pr0, j, i, kz - 1);
   // the sweep's start at the model top (:340-345)
   double e = d_zero;
   double ff = d_half * d_rfour * c->regrav *
-      ((F3(cv, j, i + 1, kz) + F3(cv, j, i, kz) + F3(cv, j + 1, i + 1, kz) + F3(cv, j + 1, i, kz)) *
-           (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
-       (F3(cu, j, i + 1, kz) + F3(cu, j, i, kz) + F3(cu, j + 1, i + 1, kz) + F3(cu, j + 1, i, kz)) *
-           (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
+      ((qb.v[2] + qb.v[0] + qb.v[3] + qb.v[1]) * (F2(f.ht, j, i + 1) - F2(f.ht, j, i - 1)) +
+       (qb.u[2] + qb.u[0] + qb.u[3] + qb.u[1]) * (F2(f.ht, j + 1, i) - F2(f.ht, j - 1, i))) /
       (c->dx * msfx);
   F3(f.se, j, i, kz) = e;
   F3(f.sf, j, i, kz) = ff;
-  NhB1 cur = nh_sound_b1_at(g, c, f, j, i, kz, kz, it, dts, msfx, ps0, rpb);
-  double rho0k = F3(f.rho0, j, i, kz), rho1k = F3(f.rho1, j, i, kz), pr0k = F3(f.pr0, j, i, kz);
+  NhB1 cur = nh_sound_b1_at(g, c, f, j, i, kz, kz, it, dts, msfx, ps0, rpb, qa, qb, qb, pca, pcb, pcb, m);
+  double rho1k = F3(f.rho1, j, i, kz);
   double wk1 = F3(w, j, i, kz + 1), wk = F3(w, j, i, kz);
   double pnew = d_zero;
   for (int k = kz; k >= 1; k--) {
+    // rings: qb/pcb at k, qa/pca at k-1
     const double wkm = (k >= 2) ? F3(w, j, i, k - 1) : d_zero;
     NhB1 prv;
-    double rho0m = d_zero, rho1m = d_zero, pr0m = d_zero;
+    double rho1m = d_zero;
+    NhQ qc;
+    double pcc = d_zero;
     if (k >= 2) {
-      prv = nh_sound_b1_at(g, c, f, j, i, k - 1, kz, it, dts, msfx, ps0, rpb);
-      rho0m = F3(f.rho0, j, i, k - 1); rho1m = F3(f.rho1, j, i, k - 1); pr0m = F3(f.pr0, j, i, k - 1);
+      if (k >= 3) { qc = nh_q_at(g, f, j, i, k - 2); pcc = F3(f.pr0, j, i, k - 2); }
+      else { qc = qa; pcc = pca; }                // unused by level 1's special form
+      if (k - 1 == 1) prv = nh_sound_b1_at(g, c, f, j, i, 1, kz, it, dts, msfx, ps0, rpb, qa, qa, qb, pca, pca, pcb, m);
+      else prv = nh_sound_b1_at(g, c, f, j, i, k - 1, kz, it, dts, msfx, ps0, rpb, qc, qa, qb, pcc, pca, pcb, m);
+      rho1m = F3(f.rho1, j, i, k - 1);
       // tridiagonal coefficients and right-hand side at k (:400-457)
       const int km1 = k - 1;
-      const double rofac = (c->dsigma[km1] * rho0k + c->dsigma[k] * rho0m) /
+      const double rofac = (c->dsigma[km1] * cur.rho0 + c->dsigma[k] * prv.rho0) /
                            (c->dsigma[km1] * rho1k + c->dsigma[k] * rho1m);
-      const double ca = EGRAV_NH * dts / (pr0k - pr0m) * rofac;
+      const double ca = EGRAV_NH * dts / (pcb - pca) * rofac;
       const double g1 = d_one - c->dsigma[km1] * cur.tk;
       const double g2 = d_one + c->dsigma[k] * prv.tk;
       const double cdm = prv.cdd, cjm = prv.cj;
@@ -885,8 +878,9 @@ __global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Const
     F3(f.cpp, j, i, k) = pnew;
     if (k >= 2) {
       cur = prv;
-      rho0k = rho0m; rho1k = rho1m; pr0k = pr0m;
+      rho1k = rho1m;
       wk1 = wk; wk = wkm;
+      qb = qa; qa = qc; pcb = pca; pca = pcc;
     }
   }
   if (c->ifupr == 1) {          // cur: level 1; pnew: its predicted pp

@@ -52,12 +52,11 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_tend_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int wdiag);
-__global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
+__global__ void k_nh_tend_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int wdiag, int istep);
+__global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_raydamp(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f);
 __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it);
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
