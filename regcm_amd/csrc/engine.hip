@@ -1400,7 +1400,8 @@ struct rcmdyn_engine {
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
       // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
       KLAUNCH(k_nh_tend_d, q.dik, BLK, 0, stream, g, dc, ds, f, istep);
-      KLAUNCH(k_nh_tend_c, q.fr, BLK, 0, stream, g, dc, ds, f, (int)diag, istep);
+      KLAUNCH(k_nh_tend_c, dim3((g.nj + 31) / 32, (g.ni + 7) / 8, kp), dim3(32, 8), 0, stream, g, dc, ds, f,
+              (int)diag, istep);
     });
     tke_step();
     xch({{FK::CQV, kz}, {FK::CQC, kz}});

@@ -27,6 +27,8 @@ static constexpr double P00 = 1.000000e5;                  // Share/mod_constant
 #define IN_CI(j, i) (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))
 #define IN_DI(j, i) (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))
 #define IN_DE(j, i) (in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2))
+__device__ __forceinline__ int j0c(const Geom& g) { return g.j0; }
+__device__ __forceinline__ int i0c(const Geom& g) { return g.i0; }
 #define FRAME_POINT()                                                  \
   THREAD_POINT(g.j0, g.i0);                                             \
   if (j >= g.j0 + g.nj || i >= g.i0 + g.ni) return;
@@ -258,6 +260,56 @@ __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax)
   return d_zero;
 }
 
+// hadv_fg / diffx_at on a field staged in LDS: S[ti][tj] is the thread's point
+template <int W>
+__device__ __forceinline__ double hadv_fgl(const Consts* c, const double (*S)[W], int ti, int tj, double u1,
+                                           double u2, double v1, double v2, double xmf, double ps, int limiter) {
+  const double f1 = d_half * c->ul * (u2 + u1) / ps;
+  const double f2 = d_half * c->ul * (v2 + v1) / ps;
+  const double fc = S[ti][tj], fw = S[ti][tj - 1], fe = S[ti][tj + 1];
+  const double fs = S[ti - 1][tj], fn = S[ti + 1][tj];
+  const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
+  const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
+  const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
+  const double fy2 = (d_one + f2) * fc + (d_one - f2) * fn;
+  double fg = -xmf * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1);
+  if (limiter && c->stability_enhance) {
+    double den, thr;
+    if (limiter == 1) { den = ps; thr = c->t_extrema; }
+    else { den = dmax(fc, DLOWVAL); thr = c->q_rel_extrema; }
+    if (fabs(fn + fs - d_two * fc) / den > thr) {
+      if (fc > fn && fc > fs) fg = dmin(fg, d_zero);
+      else if (fc < fn && fc < fs) fg = dmax(fg, d_zero);
+    }
+    if (fabs(fe + fw - d_two * fc) / den > thr) {
+      if (fc > fe && fc > fw) fg = dmin(fg, d_zero);
+      else if (fc < fe && fc < fw) fg = dmax(fg, d_zero);
+    }
+  }
+  return fg;
+}
+template <int W>
+__device__ __forceinline__ double diffx_l(const Geom& g, const Consts* c, double ften, const double (*S)[W],
+                                          double xk, int j, int i, int ti, int tj) {
+#define SA(dj, di) S[ti + (di)][tj + (dj)]
+  if (c->idiffu == 2) {
+    return ften + d_one * xk *
+        (o4_c1 * (SA(1, 0) + SA(-1, 0) + SA(0, 1) + SA(0, -1)) +
+         o4_c2 * (SA(1, 1) + SA(-1, -1) + SA(-1, 1) + SA(1, -1)) +
+         o4_c3 * SA(0, 0));
+  }
+  if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))
+    ften = ften - d_one * xk *
+        (z4_c1 * (SA(2, 0) + SA(-2, 0) + SA(0, 2) + SA(0, -2)) +
+         z4_c2 * (SA(1, 0) + SA(-1, 0) + SA(0, 1) + SA(0, -1)) +
+         z4_c3 * SA(0, 0));
+  const double lap = z4_c1 * (SA(1, 0) + SA(-1, 0) + SA(0, 1) + SA(0, -1)) + z4_c2 * SA(0, 0);
+  const int nb = (g.bl && j == g.jci1) + (g.br && j == g.jci2) + (g.bb && i == g.ici1) + (g.bt && i == g.ici2);
+  for (int q = 0; q < nb; q++) ften = ften + d_one * xk * lap;
+  return ften;
+#undef SA
+}
+
 // ---------------------------------------------------------------------------------------
 // The tendency chain of the NH core as two point kernels.  For each variable the reference
 // accumulates pc_dynamic over several loop nests -- advection (hadv/vadv), curvature or the
@@ -277,11 +329,70 @@ __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax)
 // Rayleigh damping and decoupling of raydamp (:466-499; they read atm2 u, v, pp, w, which the
 // time filters in between do not change) and with sound's scaling by the acoustic step
 // (Main/mod_sound.F90:229-245): those are the tendencies sound reads.
+constexpr int TCJ = 32, TCI = 8, TCW = TCJ + 4, TCH = TCI + 4;   // k_nh_tend_c block and staged tile
+#ifndef TC_HADV            // stage the advected fields (else read from L1/L2)
+#define TC_HADV 0
+#endif
+#ifndef TC_FG              // stage the relaxation differences (else read from L1/L2)
+#define TC_FG 0
+#endif
+constexpr int TC_NF = 5 + (TC_HADV ? 5 : 0) + (TC_FG ? 4 : 0);
+constexpr int TC_IH = 5, TC_IF = TC_HADV ? 10 : 5;   // first hadv / FG slot
 __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
                                                    int istep) {
-  FRAME_POINT();
+  // the horizontal stencil operands of this level for the 32 x 8 block and a 2-point halo,
+  // staged in LDS once: the diffusion fields (13-point); optionally (TC_HADV, TC_FG) the
+  // advected fields (5-point) and, in blocks holding band points under nudging, the 5-point
+  // relaxation differences FG/FQ -- measured slower at C5 (3.36 ms diffusion only, 3.66 ms
+  // with the advected fields, 4.27 ms with both: LDS occupancy costs more than the L1 loads)
+  __shared__ double sT[TC_NF][TCH][TCW];
+  THREAD_POINT(g.j0, g.i0);
   const int kz = c->kz;
+  const double xt = s->xbctime + s->dt;
+  const bool inframe = j < g.j0 + g.nj && i < g.i0 + g.ni;
+  const int anyband = __syncthreads_or(inframe && IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0);
+  {
+    const int J0 = g.j0 + (int)(blockIdx.x * blockDim.x) - 2, I0 = g.i0 + (int)(blockIdx.y * blockDim.y) - 2;
+    const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+    const bool nb = TC_FG && anyband && c->iboudy != 4;
+    constexpr int NS = (TCW * TCH + 255) / 256;
+    double va[NS][TC_NF];
+    bool ok[NS];
+#pragma unroll
+    for (int n = 0; n < NS; n++) {
+      const int q = tid + n * 256, jg = J0 + q % TCW, ig = I0 + q / TCW;
+      ok[n] = q < TCW * TCH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
+      const int jr = ok[n] ? jg : g.j0, ir = ok[n] ? ig : g.i0;
+      for (int m = 0; m < TC_NF; m++) va[n][m] = 0.0;
+      va[n][4] = F3(f.wb3d, jr, ir, k);
+      if (nb) va[n][TC_IF + 3] = (F3(f.wwb0, jr, ir, k) + xt * F3(f.wwbt, jr, ir, k)) - F3(f.a2w, jr, ir, k);
+      if (k <= kz) {
+        va[n][0] = F3(f.tb3d, jr, ir, k); va[n][1] = F3(f.qvb3d, jr, ir, k);
+        va[n][2] = F3(f.qcb3d, jr, ir, k); va[n][3] = F3(f.ppb3d, jr, ir, k);
+        if (TC_HADV) {
+          va[n][TC_IH] = F3(f.xpp, jr, ir, k); va[n][TC_IH + 1] = F3(f.th, jr, ir, k);
+          va[n][TC_IH + 2] = F3(f.xqv, jr, ir, k); va[n][TC_IH + 3] = F3(f.xqc, jr, ir, k);
+          if (k >= 2) va[n][TC_IH + 4] = F3(f.xw, jr, ir, k);
+        }
+        if (nb) {
+          const double nfac = 1.0e3;
+          va[n][TC_IF] = (F3(f.tb0, jr, ir, k) + xt * F3(f.tbt, jr, ir, k)) - F3(f.a2t, jr, ir, k);
+          va[n][TC_IF + 1] = nfac * (F3(f.qb0, jr, ir, k) + xt * F3(f.qbt, jr, ir, k)) - nfac * F3(f.a2qv, jr, ir, k);
+          va[n][TC_IF + 2] = (F3(f.ppb0, jr, ir, k) + xt * F3(f.ppbt, jr, ir, k)) - F3(f.a2pp, jr, ir, k);
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NS; n++) {
+      const int q = tid + n * 256, jj = q % TCW, ii = q / TCW;
+      if (q < TCW * TCH)
+        for (int m = 0; m < TC_NF; m++) sT[m][ii][jj] = ok[n] ? va[n][m] : 0.0;
+    }
+    __syncthreads();
+  }
+  if (!inframe) return;
+  const int tj = (int)threadIdx.x + 2, ti = (int)threadIdx.y + 2;
   const double dt = s->dt;
   if (!IN_CI(j, i)) {
     if (k <= kz && IN_CE(j, i)) {
@@ -301,7 +412,6 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   const bool band = f.rgcr[g.ix(j, i)] > 0;
   const bool sponge = band && c->iboudy == 4;
   const bool nudge = band && c->iboudy != 4;
-  const double xt = s->xbctime + s->dt;
   const double dts = s->dt / (double)istep;
   const int kc = (k < kz) ? k : kz;
   double xf = d_zero, xg = d_zero, wsp = d_zero;
@@ -315,6 +425,17 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
 #define RELAX5(x, b0, bt, a) \
   x = nh_relax(x, xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), FG(b0, bt, a, j + 1, i), \
                FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
+#if TC_FG
+#define RELAXL(x, m, b0, bt, a) \
+  x = nh_relax(x, xf, xg, sT[m][ti][tj], sT[m][ti][tj - 1], sT[m][ti][tj + 1], sT[m][ti - 1][tj], sT[m][ti + 1][tj])
+#else
+#define RELAXL(x, m, b0, bt, a) RELAX5(x, b0, bt, a)
+#endif
+#if TC_HADV
+#define HADVL(m, fa, lim) hadv_fgl(c, sT[m], ti, tj, u1, u2, v1, v2, xmf, ps, lim)
+#else
+#define HADVL(m, fa, lim) hadv_fg(g, c, fa, j, i, k, u1, u2, v1, v2, xmf, ps, lim)
+#endif
 #define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
   // ================= w on full levels k = 1..kz+1
   {
@@ -328,11 +449,17 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
       const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
       const double f1 = d_half * ul * (u2 + u1) / ps;
       const double f2 = d_half * ul * (v2 + v1) / ps;
-      const double* w = f.xw;
-      const double fx1 = (d_one + f1) * F3(w, j - 1, i, k) + (d_one - f1) * F3(w, j, i, k);
-      const double fx2 = (d_one + f1) * F3(w, j, i, k) + (d_one - f1) * F3(w, j + 1, i, k);
-      const double fy1 = (d_one + f2) * F3(w, j, i - 1, k) + (d_one - f2) * F3(w, j, i, k);
-      const double fy2 = (d_one + f2) * F3(w, j, i, k) + (d_one - f2) * F3(w, j, i + 1, k);
+#if TC_HADV
+      const double (*w)[TCW] = sT[TC_IH + 4];
+#define XW(dj, di) w[ti + (di)][tj + (dj)]
+#else
+#define XW(dj, di) F3(f.xw, j + (dj), i + (di), k)
+#endif
+      const double fx1 = (d_one + f1) * XW(-1, 0) + (d_one - f1) * XW(0, 0);
+      const double fx2 = (d_one + f1) * XW(0, 0) + (d_one - f1) * XW(1, 0);
+      const double fy1 = (d_one + f2) * XW(0, -1) + (d_one - f2) * XW(0, 0);
+      const double fy2 = (d_one + f2) * XW(0, 0) + (d_one - f2) * XW(0, 1);
+#undef XW
       wd = wd - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
     }
     // vadv3d ind = 0, nk = kz+1 (w), :756-765: flux through the interface below level kk
@@ -364,8 +491,8 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     }
     double wt0 = d_zero;
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
-    if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
-    wd = diffx_at(g, c, wd, f.wb3d, f.xkcf, j, i, k);
+    if (nudge) RELAXL(wd, TC_IF + 3, f.wwb0, f.wwbt, f.a2w);
+    wd = diffx_l(g, c, wd, sT[4], F3(f.xkcf, j, i, k), j, i, ti, tj);
     double wt = wt0 + wd + PHY(wphy);
     // raydamp3f and decoupling before sound (:466-499), sound's acoustic-step scaling (:229-245)
     if (c->ifrayd == 1 && k <= c->rayndamp)
@@ -378,7 +505,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   const double cr = F3(f.cr, j, i, k);
   // ================= pp: hadv3d ind 0, vadv3d ind = 0 (nk = kz), adiabatic, boundary, diffusion
   {
-    double pd = d_zero + hadv_fg(g, c, f.xpp, j, i, k, u1, u2, v1, v2, xmf, ps, 0);
+    double pd = d_zero + HADVL(TC_IH, f.xpp, 0);
     auto pflux = [&](int kk) {
       return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
     };
@@ -387,8 +514,9 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     pd = pd + F3(f.xpp, j, i, k) * cr;
     double pt0 = d_zero;
     if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
-    if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
-    pd = diffx_at(g, c, pd, f.ppb3d, f.xkc, j, i, k);
+    if (nudge) RELAXL(pd, TC_IF + 2, f.ppb0, f.ppbt, f.a2pp);
+    const double xkc = F3(f.xkc, j, i, k);
+    pd = diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
     double pt = pt0 + pd + PHY(ppphy);
     if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3, decoupling, acoustic-step scaling
       pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
@@ -400,7 +528,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   // ================= t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d
   // ind = 0 (nk = kz) of tha = th*p*, plus th*cr; tdyn = atm1%t*thten/tha
   {
-    double thd = d_zero + hadv_fg(g, c, f.th, j, i, k, u1, u2, v1, v2, xmf, ps, 1);
+    double thd = d_zero + HADVL(TC_IH + 1, f.th, 1);
     auto thflux = [&](int kk) {
       return F3(f.qdot, j, i, kk) *
              (c->twt1[kk] * (F3(f.th, j, i, kk) * ps) + c->twt2[kk] * (F3(f.th, j, i, kk - 1) * ps));
@@ -412,8 +540,8 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     double td = d_zero + F3(f.a1t, j, i, k) * thd / (th * ps);
     double tt0 = d_zero;
     if (sponge) tt0 = wsp * d_zero + (d_one - wsp) * F3(f.tbt, j, i, k);
-    if (nudge) RELAX5(td, f.tb0, f.tbt, f.a2t);
-    td = diffx_at(g, c, td, f.tb3d, f.xkc, j, i, k);
+    if (nudge) RELAXL(td, TC_IF, f.tb0, f.tbt, f.a2t);
+    td = diffx_l(g, c, td, sT[0], F3(f.xkc, j, i, k), j, i, ti, tj);
     double tt = tt0 + td + PHY(tphy);
     tt = tt + 0.0;
     if (ray) tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
@@ -424,7 +552,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   // diffusion, forecast
   {
     double qd = d_zero + (c->isladvec ? F3(f.slqv, j, i, k)
-                                      : hadv_fg(g, c, f.xqv, j, i, k, u1, u2, v1, v2, xmf, ps, 2));
+                                      : HADVL(TC_IH + 2, f.xqv, 2));
     const double thr = MINQQ * ps;
     auto qflux = [&](int kk) {
       const double fk = F3(f.a1qv, j, i, kk), fkm = F3(f.a1qv, j, i, kk - 1);
@@ -439,12 +567,17 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     if (sponge) qt0 = wsp * d_zero + (d_one - wsp) * F3(f.qbt, j, i, k);
     if (nudge) {
       const double nfac = 1.0e3, rfac = d_one / nfac;
+#if TC_FG
+      const double (*Q)[TCW] = sT[TC_IF + 1];
+      const double q0 = Q[ti][tj], q1 = Q[ti][tj - 1], q2 = Q[ti][tj + 1], q3 = Q[ti - 1][tj], q4 = Q[ti + 1][tj];
+#else
 #define FQ(J, I) (nfac * (F3(f.qb0, J, I, k) + xt * F3(f.qbt, J, I, k)) - nfac * F3(f.a2qv, J, I, k))
       const double q0 = FQ(j, i), q1 = FQ(j - 1, i), q2 = FQ(j + 1, i), q3 = FQ(j, i - 1), q4 = FQ(j, i + 1);
 #undef FQ
+#endif
       qd = qd + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
     }
-    qd = diffx_at(g, c, qd, f.qvb3d, f.xkc, j, i, k);
+    qd = diffx_l(g, c, qd, sT[1], F3(f.xkc, j, i, k), j, i, ti, tj);
     double qv = qt0 + qd + PHY(qvphy);
     qv = qv + 0.0;
     if (ray) qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
@@ -455,7 +588,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   // diffusion, forecast
   {
     double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
-                                      : hadv_fg(g, c, f.xqc, j, i, k, u1, u2, v1, v2, xmf, ps, 0));
+                                      : HADVL(TC_IH + 3, f.xqc, 0));
     const double thr = MINQQ * MINQQ * ps;
     auto cflux = [&](int kk) {
       const double svv = F3(f.qdot, j, i, kk);
@@ -466,7 +599,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
     if (k >= 2) cd = cd + cflux(k) * c->xds[k];
     if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
     cd = cd + F3(f.xqc, j, i, k) * cr;
-    cd = diffx_at(g, c, cd, f.qcb3d, f.xkc, j, i, k);
+    cd = diffx_l(g, c, cd, sT[2], F3(f.xkc, j, i, k), j, i, ti, tj);
     double qc = d_zero + cd + PHY(qcphy);
     qc = qc + 0.0;
     if (wdiag) F3(f.qcten, j, i, k) = qc;
@@ -474,29 +607,64 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   }
 }
 
+// k_nh_tend_d stages its horizontal stencil operands of one level for a 64 x 4 block plus a
+// 2-point halo in LDS, one load (and for ubd/msfd, vbd/msfd one division) per staged point:
+// umc, vmc, ud, vd, cr (hadvuv) and the diffu_d operands; lanes outside the frame stage zero
+constexpr int TDW = 64 + 4, TDH = 4 + 4;
 __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int istep) {
+  __shared__ double sUA[TDH][TDW], sVA[TDH][TDW], sU[TDH][TDW], sV[TDH][TDW], sCR[TDH][TDW];
+  __shared__ double sBU[TDH][TDW], sBV[TDH][TDW];
   THREAD_POINT(g.jdi1, g.idi1);
+  {
+    const int J0 = g.jdi1 + (int)(blockIdx.x * blockDim.x) - 2, I0 = g.idi1 + (int)(blockIdx.y * blockDim.y) - 2;
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    constexpr int NS = (TDW * TDH + 255) / 256;
+    double va[NS][7];
+    bool ok[NS];
+#pragma unroll
+    for (int n = 0; n < NS; n++) {
+      const int q = tid + n * 256, jg = J0 + q % TDW, ig = I0 + q / TDW;
+      ok[n] = q < TDW * TDH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
+      const int jr = ok[n] ? jg : j0c(g), ir = ok[n] ? ig : i0c(g);
+      va[n][0] = F3(f.umc, jr, ir, k); va[n][1] = F3(f.vmc, jr, ir, k);
+      va[n][2] = F3(f.ud, jr, ir, k); va[n][3] = F3(f.vd, jr, ir, k); va[n][4] = F3(f.cr, jr, ir, k);
+      va[n][5] = F3(f.ubd, jr, ir, k); va[n][6] = F3(f.vbd, jr, ir, k);
+      const double m = F2(f.msfd, jr, ir);
+      va[n][5] = va[n][5] / m; va[n][6] = va[n][6] / m;     // UM of diffu_d, Main/mod_diffusion.F90:281-411
+    }
+#pragma unroll
+    for (int n = 0; n < NS; n++) {
+      const int q = tid + n * 256, jj = q % TDW, ii = q / TDW;
+      if (q < TDW * TDH) {
+        const bool o = ok[n];
+        sUA[ii][jj] = o ? va[n][0] : 0.0; sVA[ii][jj] = o ? va[n][1] : 0.0;
+        sU[ii][jj] = o ? va[n][2] : 0.0; sV[ii][jj] = o ? va[n][3] : 0.0; sCR[ii][jj] = o ? va[n][4] : 0.0;
+        sBU[ii][jj] = o ? va[n][5] : 0.0; sBV[ii][jj] = o ? va[n][6] : 0.0;
+      }
+    }
+    __syncthreads();
+  }
   if (!IN_DI(j, i)) return;
   const int kz = c->kz;
+  const int tj = (int)threadIdx.x + 2, ti = (int)threadIdx.y + 2;
+#define L2(S, dj, di) S[ti + (di)][tj + (dj)]
   double ud, vd;
   // hadvuv NH upstream branch, Main/mod_advection.F90:235-264
   {
     const double ul = c->ul, dm = F2(f.dmsf, j, i);
-    const double* ua = f.umc; const double* va = f.vmc; const double* u = f.ud; const double* v = f.vd;
-    const double divd = d_rfour * (F3(f.cr, j, i, k) + F3(f.cr, j, i - 1, k) + F3(f.cr, j - 1, i, k) +
-                                   F3(f.cr, j - 1, i - 1, k));
-    const double ucmona = F3(ua, j, i + 1, k) + d_two * F3(ua, j, i, k) + F3(ua, j, i - 1, k);
-    double ucmonb = F3(ua, j + 1, i + 1, k) + d_two * F3(ua, j + 1, i, k) + F3(ua, j + 1, i - 1, k);
-    double ucmonc = F3(ua, j - 1, i + 1, k) + d_two * F3(ua, j - 1, i, k) + F3(ua, j - 1, i - 1, k);
-    const double vcmona = F3(va, j + 1, i, k) + d_two * F3(va, j, i, k) + F3(va, j - 1, i, k);
-    double vcmonb = F3(va, j + 1, i + 1, k) + d_two * F3(va, j, i + 1, k) + F3(va, j - 1, i + 1, k);
-    double vcmonc = F3(va, j + 1, i - 1, k) + d_two * F3(va, j, i - 1, k) + F3(va, j - 1, i - 1, k);
+    const double divd = d_rfour * (L2(sCR, 0, 0) + L2(sCR, 0, -1) + L2(sCR, -1, 0) + L2(sCR, -1, -1));
+    const double ucmona = L2(sUA, 0, 1) + d_two * L2(sUA, 0, 0) + L2(sUA, 0, -1);
+    double ucmonb = L2(sUA, 1, 1) + d_two * L2(sUA, 1, 0) + L2(sUA, 1, -1);
+    double ucmonc = L2(sUA, -1, 1) + d_two * L2(sUA, -1, 0) + L2(sUA, -1, -1);
+    const double vcmona = L2(sVA, 1, 0) + d_two * L2(sVA, 0, 0) + L2(sVA, -1, 0);
+    double vcmonb = L2(sVA, 1, 1) + d_two * L2(sVA, 0, 1) + L2(sVA, -1, 1);
+    double vcmonc = L2(sVA, 1, -1) + d_two * L2(sVA, 0, -1) + L2(sVA, -1, -1);
     const double diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc));
-    const double u0 = F3(u, j, i, k), ue = F3(u, j + 1, i, k), uw = F3(u, j - 1, i, k);
-    const double un = F3(u, j, i + 1, k), us = F3(u, j, i - 1, k);
-    const double v0 = F3(v, j, i, k), ve = F3(v, j + 1, i, k), vw = F3(v, j - 1, i, k);
-    const double vn = F3(v, j, i + 1, k), vs = F3(v, j, i - 1, k);
+    const double u0 = L2(sU, 0, 0), ue = L2(sU, 1, 0), uw = L2(sU, -1, 0);
+    const double un = L2(sU, 0, 1), us = L2(sU, 0, -1);
+    const double v0 = L2(sV, 0, 0), ve = L2(sV, 1, 0), vw = L2(sV, -1, 0);
+    const double vn = L2(sV, 0, 1), vs = L2(sV, 0, -1);
     const double ff1 = ul * (ue + u0), ff2 = ul * (uw + u0);
     const double ff3 = ul * (vn + v0), ff4 = ul * (vs + v0);
     ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
@@ -558,13 +726,13 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
       RELAX5(vd, f.vb0, f.vbt, f.a2v);
     }
   }
-  // diffu_d, Main/mod_diffusion.F90:281-411
+  // diffu_d, Main/mod_diffusion.F90:281-411 (UM = ubd/msfd, vbd/msfd staged)
   {
-    const double* m = f.msfd;
-#define UM(a, J, I) (F3(a, J, I, k) / F2(m, J, I))
+#define UM(S, J, I) L2(S, (J) - j, (I) - i)
     const double xkd = F3(f.xkd, j, i, k);
+#pragma unroll
     for (int pass = 0; pass < 2; pass++) {
-      const double* b = pass ? f.vbd : f.ubd;
+      double (*b)[TDW] = pass ? sBV : sBU;
       double t = pass ? vd : ud;
       if (c->idiffu == 2) {
         t = t + xkd * (o4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
@@ -584,6 +752,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
     }
 #undef UM
   }
+#undef L2
   double ut = ut0 + ud + PHY(uphy);
   double vt = vt0 + vd + PHY(vphy);
   // Rayleigh damping and decoupling before sound (raydampuv, :466-499), then sound's scaling
@@ -603,6 +772,8 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
 }
 #undef PHY
 #undef RELAX5
+#undef RELAXL
+#undef HADVL
 #undef FG
 
 // negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points
