@@ -1423,7 +1423,7 @@ struct rcmdyn_engine {
       }
       xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
       each([&](Tile& t) {
-        KLAUNCH(k_nh_sound_uv, grids(t.g).dik, BLK, 0, stream, t.g, dc, ds, nhfields(t), istep);
+        KLAUNCH(k_nh_sound_uv, grids(t.g).dik, BLK, 0, stream, t.g, dc, ds, nhfields(t), istep, (int)(it == istep));
       });
       xch({{FK::NCU, kz}, {FK::NCV, kz}});
       each([&](Tile& t) {

@@ -902,7 +902,7 @@ __global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, i
 
 // substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep) {
+                              int istep, int fin) {
   THREAD_POINT(g.jdi1, g.idi1);
   if (!IN_DI(j, i)) return;
   const double dts = s->dt / (double)istep;
@@ -916,8 +916,19 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
                                         F3(pp, j - 1, i - 1, k) - F3(f.dprddx, j, i, k) * dppdp0);
   double v = F3(f.cv, j, i, k) - chh * (F3(pp, j, i, k) - F3(pp, j, i - 1, k) + F3(pp, j - 1, i, k) -
                                         F3(pp, j - 1, i - 1, k) - F3(f.dprddy, j, i, k) * dppdp0);
-  F3(f.cu, j, i, k) = u + F3(f.uten, j, i, k);
-  F3(f.cv, j, i, k) = v + F3(f.vten, j, i, k);
+  const double cu = u + F3(f.uten, j, i, k), cv = v + F3(f.vten, j, i, k);
+  F3(f.cu, j, i, k) = cu;
+  F3(f.cv, j, i, k) = cv;
+  if (fin) {       // the last sub-step's u, v are final: the RA filters after the loop (:686-693)
+    const double pd = F2(f.psdotb, j, i);
+    const double uu = pd * cu, vv = pd * cv;
+    double d = c->gnu1 * (uu + F3(f.a2u, j, i, k) - d_two * F3(f.a1u, j, i, k));
+    F3(f.a2u, j, i, k) = F3(f.a1u, j, i, k) + d;
+    F3(f.a1u, j, i, k) = uu;
+    d = c->gnu1 * (vv + F3(f.a2v, j, i, k) - d_two * F3(f.a1v, j, i, k));
+    F3(f.a2v, j, i, k) = F3(f.a1v, j, i, k) + d;
+    F3(f.a1v, j, i, k) = vv;
+  }
 }
 
 // cu, cv at the dot points (j,i), (j+1,i), (j,i+1), (j+1,i+1) around a cross point, one level
@@ -1179,8 +1190,21 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
       }
     }
     double* w = f.cw;
-    F3(w, j, i, 1) = wpval;
     const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i);
+    // last sub-step: the RA filters of pp and w after the loop (:694-702) follow on the column
+    auto wfilt = [&](int kk, double wv) {
+      if (!last) { F3(w, j, i, kk) = wv; return; }
+      if (fabs(wv) < DLOWVAL) wv = d_zero;
+      wv = psb * wv;
+      const double d = c->gnu2 * (wv + F3(f.a2w, j, i, kk) - d_two * F3(f.a1w, j, i, kk));
+      double a2 = F3(f.a1w, j, i, kk) + d, a1 = wv;
+      F3(w, j, i, kk) = wv;
+      if (fabs(a2) < DLOWVAL) a2 = d_zero;
+      if (fabs(a1) < DLOWVAL) a1 = d_zero;
+      F3(f.a2w, j, i, kk) = a2;
+      F3(f.a1w, j, i, kk) = a1;
+    };
+    wfilt(1, wpval);
     const double dpx = F2(f.dpsdxm, j, i), dpy = F2(f.dpsdym, j, i);
     auto crs = [&](const double* a, int kk) {
       return F3(a, j, i, kk) + F3(a, j, i + 1, kk) + F3(a, j + 1, i, kk) + F3(a, j + 1, i + 1, kk);
@@ -1190,7 +1214,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
     double pam = d_zero, pamm = d_zero, prm = d_zero, prmm = d_zero;   // next part A: pp, pr0 at k-1, k-2
     for (int k = 1; k <= kz; k++) {
       const double wp = F3(f.se, j, i, k) * wm + F3(f.sf, j, i, k);
-      F3(w, j, i, k + 1) = wp;
+      wfilt(k + 1, wp);
       const double cuk = crs(f.cu, k), cvk = crs(f.cv, k);
       if (k >= 2) {
         const double sigdot = -F3(f.rhof0, j, i, k) * EGRAV_NH * wm / ps0 -
@@ -1215,6 +1239,12 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
       wm = wp;
       if (!nexta) {
         F3(f.cpp, j, i, k) = p;
+        if (last) {
+          const double pf = psb * p;
+          const double d = c->gnu1 * (pf + F3(f.a2pp, j, i, k) - d_two * F3(f.a1pp, j, i, k));
+          F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k) + d;
+          F3(f.a1pp, j, i, k) = pf;
+        }
         continue;
       }
       // part A of the next sub-step on this column (:250-262): pp += xkd*pi, then dp'/dp0 at
@@ -1249,34 +1279,16 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
   }
 }
 
-// time filters after the acoustic loop (:686-702).  k = 1..kz+1.
+// time filters after the acoustic loop (:686-702) off the interior cross columns: the last
+// sub-step's k_nh_sound_uv filters u, v and its k_nh_sound_cd pp and w on the interior; what
+// remains is the small-value clamp of w (the acoustic w, atm1/atm2 w) on the other frame
+// points.  k = 1..kz+1.
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
-  const int kz = c->kz;
-  if (k <= kz && IN_DI(j, i)) {
-    const double pd = F2(f.psdotb, j, i);
-    const double u = pd * F3(f.cu, j, i, k), v = pd * F3(f.cv, j, i, k);
-    double d = c->gnu1 * (u + F3(f.a2u, j, i, k) - d_two * F3(f.a1u, j, i, k));
-    F3(f.a2u, j, i, k) = F3(f.a1u, j, i, k) + d;
-    F3(f.a1u, j, i, k) = u;
-    d = c->gnu1 * (v + F3(f.a2v, j, i, k) - d_two * F3(f.a1v, j, i, k));
-    F3(f.a2v, j, i, k) = F3(f.a1v, j, i, k) + d;
-    F3(f.a1v, j, i, k) = v;
-  }
-  if (k <= kz && IN_CI(j, i)) {
-    const double p = F2(f.psb, j, i) * F3(f.cpp, j, i, k);
-    const double d = c->gnu1 * (p + F3(f.a2pp, j, i, k) - d_two * F3(f.a1pp, j, i, k));
-    F3(f.a2pp, j, i, k) = F3(f.a1pp, j, i, k) + d;
-    F3(f.a1pp, j, i, k) = p;
-  }
+  (void)c;
+  if (IN_CI(j, i)) return;
   double w = F3(f.cw, j, i, k);
   if (fabs(w) < DLOWVAL) w = d_zero;
-  if (IN_CI(j, i)) {
-    w = F2(f.psb, j, i) * w;
-    const double d = c->gnu2 * (w + F3(f.a2w, j, i, k) - d_two * F3(f.a1w, j, i, k));
-    F3(f.a2w, j, i, k) = F3(f.a1w, j, i, k) + d;
-    F3(f.a1w, j, i, k) = w;
-  }
   F3(f.cw, j, i, k) = w;
   if (fabs(F3(f.a2w, j, i, k)) < DLOWVAL) F3(f.a2w, j, i, k) = d_zero;
   if (fabs(F3(f.a1w, j, i, k)) < DLOWVAL) F3(f.a1w, j, i, k) = d_zero;

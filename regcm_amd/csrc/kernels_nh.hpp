@@ -59,7 +59,7 @@ __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHField
 __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it);
-__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
+__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int fin);
 __global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
