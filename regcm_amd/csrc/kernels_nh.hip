@@ -87,7 +87,7 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   const double xtv = xt * (d_one + c->ep1 * xqv);
   const double xpp = F3(f.a1pp, j, i, k) * rp;
   const double pr1 = F3(f.pr0, j, i, k) + xpp;
-  F3(f.xt, j, i, k) = xt; F3(f.xqv, j, i, k) = xqv; F3(f.xqc, j, i, k) = xqc; F3(f.xtv, j, i, k) = xtv;
+  F3(f.xqv, j, i, k) = xqv; F3(f.xqc, j, i, k) = xqc;      // atmx%t, tv: read only here
   F3(f.xpp, j, i, k) = xpp; F3(f.pr1, j, i, k) = pr1;
   F3(f.rho1, j, i, k) = pr1 / (c->rgas * xtv);
   F3(f.th, j, i, k) = xt * rcm_powpos(P00 / pr1, c->rovcp);
@@ -127,8 +127,9 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   }
 }
 
-// mkslice NH subset (Main/mod_slice.F90:163-183, 215-238, 278-281): b-level decoupled winds,
-// t, q, pp, w and the NH half/full level pressures
+// mkslice NH subset (Main/mod_slice.F90:163-183, 278-281): the b-level decoupled winds, t, q,
+// pp and w the step reads (the NH level pressures of :207-225 are formed by the physics-seam
+// export, slice.hip, which is their only reader)
 __global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
@@ -140,26 +141,11 @@ __global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f) {
   if (!(in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb))) return;
   const double rp = F2(f.rpsb, j, i);
   F3(f.wb3d, j, i, k) = F3(f.a2w, j, i, k) * rp;
-  const double ptoppa = c->ptop * d_1000;
   if (k <= kz) {
     F3(f.tb3d, j, i, k) = F3(f.a2t, j, i, k) * rp;
     F3(f.qvb3d, j, i, k) = dmax(F3(f.a2qv, j, i, k) * rp, MINQQ);
     F3(f.qcb3d, j, i, k) = dmax(F3(f.a2qc, j, i, k) * rp, d_zero);
-    const double ppb = F3(f.a2pp, j, i, k) * rp;
-    F3(f.ppb3d, j, i, k) = ppb;
-    if (IN_CE(j, i)) {
-      if (k >= 2) {
-        F3(f.pb3d, j, i, k) = F3(f.pr0, j, i, k) + ppb;
-        const double ppm = F3(f.a2pp, j, i, k - 1) * rp;
-        F3(f.pf3d, j, i, k) = F3(f.pf0, j, i, k) + d_half * (ppm + ppb);
-      } else {
-        F3(f.pb3d, j, i, 1) = dmax(F3(f.pr0, j, i, 1) + ppb, ptoppa + 1.0);
-        F3(f.pf3d, j, i, 1) = ptoppa;
-      }
-    }
-  } else if (IN_CE(j, i)) {
-    const double ppkz = F3(f.a2pp, j, i, kz) * rp;
-    F3(f.pf3d, j, i, kz + 1) = F2(f.ps0, j, i) + ptoppa + ppkz;
+    F3(f.ppb3d, j, i, k) = F3(f.a2pp, j, i, k) * rp;
   }
 }
 
@@ -882,7 +868,6 @@ __global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const Step
       F3(f.cv, j, i, k) = F3(f.a2v, j, i, k) / F2(f.psdotb, j, i);
     }
     if (IN_CE(j, i)) F3(f.cpp, j, i, k) = F3(f.a2pp, j, i, k) * rpb;
-    if (IN_CI(j, i)) F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) * rpb;
   }
   if (IN_CE(j, i)) F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
 }
@@ -1190,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
       }
     }
     double* w = f.cw;
-    const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i);
+    const double ps0 = F2(f.ps0, j, i), psb = F2(f.psb, j, i), rpsb = F2(f.rpsb, j, i);
     // last sub-step: the RA filters of pp and w after the loop (:694-702) follow on the column
     auto wfilt = [&](int kk, double wv) {
       if (!last) { F3(w, j, i, kk) = wv; return; }
@@ -1232,7 +1217,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
       const double p = F3(f.cpp, j, i, k) + (cjtmp * (wp + wm) + cddtmp * (wp - wm)) * bp;
       const double spn = p - ppold - F3(f.ppten, j, i, k);
       F3(f.spi, j, i, k) = spn;
-      const double cpm = c->cpd * (d_one + 0.80 * F3(f.cqv, j, i, k));
+      const double cpm = c->cpd * (d_one + 0.80 * (F3(f.a2qv, j, i, k) * rpsb));   // qv = atm2 qv / p*b
       const double dpterm = psb * (p - ppold) / (cpm * F3(f.rho1, j, i, k));
       F3(f.a2t, j, i, k) = F3(f.a2t, j, i, k) + c->gnu1 * dpterm;
       F3(f.a1t, j, i, k) = F3(f.a1t, j, i, k) + dpterm;
