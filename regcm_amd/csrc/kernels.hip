@@ -412,23 +412,35 @@ __global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __res
     const int t = tid + n * MBT, jg = J0 - 1 + t % TW1, ig = I0 - 1 + t / TW1;
     aok[n] = t < TW1 * TH1 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
     const uint32_t q2 = aok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
+    if (t < TW1 * TH1) {          // waves wholly past the staged tile skip the loads
+      au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
+    } else {
+      au[n] = av[n] = am[n] = ar[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < N2; n++) {
     const int t = tid + n * MBT, jg = J0 - 2 + t % TW2, ig = I0 - 2 + t / TW2;
     bok[n] = t < TW2 * TH2 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
     const uint32_t q2 = bok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    br[n] = LD(f.rpsdb, q2); bm[n] = LD(f.msfd, q2); bu[n] = LD(f.a2u, q3); bv[n] = LD(f.a2v, q3);
+    if (t < TW2 * TH2) {          // waves wholly past the staged tile skip the loads
+      br[n] = LD(f.rpsdb, q2); bm[n] = LD(f.msfd, q2); bu[n] = LD(f.a2u, q3); bv[n] = LD(f.a2v, q3);
+    } else {
+      br[n] = bm[n] = bu[n] = bv[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < N0; n++) {
     const int t = tid + n * MBT, jg = J0 - 1 + t % TW0, ig = I0 - 1 + t / TW0;
     cok[n] = t < TW0 * TH0 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
     const uint32_t q2 = cok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    crp[n] = LD(f.rpsa, q2); ct[n] = LD(f.a1t, q3); cqv[n] = LD(f.a1qv, q3);
-    cq0[n] = LD(f.qdot, q3); cq1[n] = LD(f.qdot, q3 + L8); cph[n] = LD(f.phi, q3); cps[n] = LD(f.psa, q2);
-    chg[n] = LD(f.hgfact, q2);
+    if (t < TW0 * TH0) {          // waves wholly past the staged tile skip the loads
+      crp[n] = LD(f.rpsa, q2); ct[n] = LD(f.a1t, q3); cqv[n] = LD(f.a1qv, q3);
+      cq0[n] = LD(f.qdot, q3); cq1[n] = LD(f.qdot, q3 + L8); cph[n] = LD(f.phi, q3); cps[n] = LD(f.psa, q2);
+      chg[n] = LD(f.hgfact, q2);
+    } else {
+      crp[n] = ct[n] = cqv[n] = cq0[n] = cq1[n] = cph[n] = cps[n] = chg[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < N1; n++) {
@@ -772,23 +784,35 @@ __global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __rest
     const int t = tid + n * SBT, jg = J0 + t % SDW, ig = I0 + t / SDW;
     aok[n] = t < SDW * SDH && jg <= jhi && ig <= ihi;
     const uint32_t q2 = aok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
-    arb[n] = LD(f.rpsdb, q2); au2[n] = LD(f.a2u, q3); av2[n] = LD(f.a2v, q3);
+    if (t < SDW * SDH) {          // waves wholly past the staged tile skip the loads
+      au[n] = LD(f.a1u, q3); av[n] = LD(f.a1v, q3); am[n] = LD(f.msfd, q2); ar[n] = LD(f.rpsda, q2);
+      arb[n] = LD(f.rpsdb, q2); au2[n] = LD(f.a2u, q3); av2[n] = LD(f.a2v, q3);
+    } else {
+      au[n] = av[n] = am[n] = ar[n] = arb[n] = au2[n] = av2[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < NB; n++) {
     const int t = tid + n * SBT, jg = J0 - 1 + t % SW1, ig = I0 - 1 + t / SW1;
     bok[n] = t < SW1 * SH1 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
     const uint32_t q2 = bok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    bps[n] = LD(f.psa, q2); brp[n] = LD(f.rpsa, q2);
-    bt[n] = LD(f.a1t, q3); bqv[n] = LD(f.a1qv, q3); bqc[n] = LD(f.a1qc, q3);
+    if (t < SW1 * SH1) {          // waves wholly past the staged tile skip the loads
+      bps[n] = LD(f.psa, q2); brp[n] = LD(f.rpsa, q2);
+      bt[n] = LD(f.a1t, q3); bqv[n] = LD(f.a1qv, q3); bqc[n] = LD(f.a1qc, q3);
+    } else {
+      bps[n] = brp[n] = bt[n] = bqv[n] = bqc[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < NC; n++) {
     const int t = tid + n * SBT, jg = J0 - 2 + t % SW2, ig = I0 - 2 + t / SW2;
     cok[n] = t < SW2 * SH2 && jg >= jlo && jg <= jhi && ig >= ilo && ig <= ihi;
     const uint32_t q2 = cok[n] ? g.o2(jg, ig) : o2, q3 = q2 + kof;
-    crb[n] = LD(f.rpsb, q2); ct2[n] = LD(f.a2t, q3); cqv[n] = LD(f.a2qv, q3); cqc[n] = LD(f.a2qc, q3);
+    if (t < SW2 * SH2) {          // waves wholly past the staged tile skip the loads
+      crb[n] = LD(f.rpsb, q2); ct2[n] = LD(f.a2t, q3); cqv[n] = LD(f.a2qv, q3); cqc[n] = LD(f.a2qc, q3);
+    } else {
+      crb[n] = ct2[n] = cqv[n] = cqc[n] = 0.0;
+    }
   }
 #pragma unroll
   for (int n = 0; n < NA; n++) {
