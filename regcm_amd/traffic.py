@@ -33,6 +33,18 @@ KERNEL_FIELDS = {
     "k_qfilter": (10, 0, 5),
     "k_split_project": (6, 0, 20),
     "k_split_correct": (12, 0, 8),
+    # non-hydrostatic core (kernels_nh.hip); 3-D fields of kz or kz+1 levels counted alike
+    #   k_nh_sound_cd  reads se, sf, rhof0, cu, cv, pi, rho0, pr1, pp, ppten, atm2 qv, rho1,
+    #                  atm2/atm1 t, pr0 (15); writes w, pp, pi, atm2/atm1 t, dp'/dp0 (6)
+    #   k_nh_sound_bc  reads pp, pi, pr1, rho0, t0, pr0, atm2 t, ppten, cu, cv, rho1, w, wten (13);
+    #                  writes se, sf, pi, pp (4)
+    #   k_nh_tend_c    reads the decoupled/derived fields of the tendency chains (30) + t, qv, pp,
+    #                  w b0/bt in the band (8 f_b); writes wten, ppten, atmc t, qv, qc (5)
+    #   k_nh_tend_d    reads 16 + u, v b0/bt in the band (4 f_b); writes uten, vten (2)
+    "k_nh_sound_cd": (21, 0, 5),
+    "k_nh_sound_bc": (17, 0, 6),
+    "k_nh_tend_c": (35, 8, 6),
+    "k_nh_tend_d": (18, 4, 10),
 }
 
 
