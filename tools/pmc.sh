@@ -1,13 +1,13 @@
 #!/bin/bash
-# PMC passes over the C3 bench (graph replay, no eager profiling) and the FETCH/WRITE
+# PMC passes over the bench of config CFG (default C3) (graph replay, no eager profiling) and the FETCH/WRITE
 # calibration kernel.  Counter passes run with counter collection only (no tracing domains),
 # each under its own time limit; any failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=gpurun_out/pmc_${CFG:-C3}
 mkdir -p $OUT
-BENCH="python3 bench.py --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --prof-steps 0"
+BENCH="python3 bench.py --config ${CFG:-C3} --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --prof-steps 0"
 pass() {  # pass <name> <counters...>
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT/$name -o $name --output-format csv -- $BENCH \

@@ -37,7 +37,7 @@ def load(pass_dir):
 
 
 def main():
-    base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
+    base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_C3")
     known = 64 * 2**20 * 8
     cf = load(os.path.join(base, "cal_fetch")).get("k_calib_copy", {}).get("FETCH_SIZE")
     cw = load(os.path.join(base, "cal_write")).get("k_calib_copy", {}).get("WRITE_SIZE")
