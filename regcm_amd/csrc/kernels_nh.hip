@@ -27,6 +27,15 @@ static constexpr double P00 = 1.000000e5;                  // Share/mod_constant
 #define IN_CI(j, i) (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))
 #define IN_DI(j, i) (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))
 #define IN_DE(j, i) (in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2))
+#if NH_ZFIRST
+#define TBX ((int)blockIdx.y)
+#define TBY ((int)blockIdx.z)
+#define TBZ ((int)blockIdx.x)
+#else
+#define TBX ((int)blockIdx.x)
+#define TBY ((int)blockIdx.y)
+#define TBZ ((int)blockIdx.z)
+#endif
 __device__ __forceinline__ int j0c(const Geom& g) { return g.j0; }
 __device__ __forceinline__ int i0c(const Geom& g) { return g.i0; }
 #define FRAME_POINT()                                                  \
@@ -333,13 +342,13 @@ __global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restr
   // relaxation differences FG/FQ -- measured slower at C5 (3.36 ms diffusion only, 3.66 ms
   // with the advected fields, 4.27 ms with both: LDS occupancy costs more than the L1 loads)
   __shared__ double sT[TC_NF][TCH][TCW];
-  THREAD_POINT(g.j0, g.i0);
+  const int j = g.j0 + TBX * TCJ + (int)threadIdx.x, i = g.i0 + TBY * TCI + (int)threadIdx.y, k = TBZ + 1;
   const int kz = c->kz;
   const double xt = s->xbctime + s->dt;
   const bool inframe = j < g.j0 + g.nj && i < g.i0 + g.ni;
   const int anyband = __syncthreads_or(inframe && IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0);
   {
-    const int J0 = g.j0 + (int)(blockIdx.x * blockDim.x) - 2, I0 = g.i0 + (int)(blockIdx.y * blockDim.y) - 2;
+    const int J0 = g.j0 + TBX * TCJ - 2, I0 = g.i0 + TBY * TCI - 2;
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
     const bool nb = TC_FG && anyband && c->iboudy != 4;
     constexpr int NS = (TCW * TCH + 255) / 256;
@@ -601,9 +610,9 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
                                                    const StepState* __restrict__ s, NHFields f, int istep) {
   __shared__ double sUA[TDH][TDW], sVA[TDH][TDW], sU[TDH][TDW], sV[TDH][TDW], sCR[TDH][TDW];
   __shared__ double sBU[TDH][TDW], sBV[TDH][TDW];
-  THREAD_POINT(g.jdi1, g.idi1);
+  const int j = g.jdi1 + TBX * 64 + (int)threadIdx.x, i = g.idi1 + TBY * 4 + (int)threadIdx.y, k = TBZ + 1;
   {
-    const int J0 = g.jdi1 + (int)(blockIdx.x * blockDim.x) - 2, I0 = g.idi1 + (int)(blockIdx.y * blockDim.y) - 2;
+    const int J0 = g.jdi1 + TBX * 64 - 2, I0 = g.idi1 + TBY * 4 - 2;
     const int tid = threadIdx.y * 64 + threadIdx.x;
     constexpr int NS = (TDW * TDH + 255) / 256;
     double va[NS][7];

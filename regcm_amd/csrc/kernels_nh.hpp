@@ -46,6 +46,11 @@ struct NHFields {
                                  // the reference reports, Main/mod_sound.F90:634-646)
 };
 constexpr int NH_CFL_SLOTS = 1024;
+// block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,
+// tiles_i) grids, consecutive blocks on consecutive levels of one tile
+#ifndef NH_ZFIRST
+#define NH_ZFIRST 1
+#endif
 
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
