@@ -1480,7 +1480,6 @@ struct rcmdyn_engine {
     };
     each([&](Tile& t) {
       const Geom& g = t.g;
-      const int c = t.cur;
       KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
               stream, g, ds, bdy_args(t, 0));
       const int nperim = 2 * (g.ici2 - g.ici1 + 1) + 2 * (g.jce2 - g.jce1 + 1);
