@@ -333,7 +333,10 @@ constexpr int TCJ = 32, TCI = 8, TCW = TCJ + 4, TCH = TCI + 4;   // k_nh_tend_c 
 #endif
 constexpr int TC_NF = 5 + (TC_HADV ? 5 : 0) + (TC_FG ? 4 : 0);
 constexpr int TC_IH = 5, TC_IF = TC_HADV ? 10 : 5;   // first hadv / FG slot
-__global__ __launch_bounds__(256) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
+#ifndef TC_W
+#define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
+#endif
+__global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
                                                    int istep) {
   // the horizontal stencil operands of this level for the 32 x 8 block and a 2-point halo,
