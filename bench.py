@@ -31,17 +31,20 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 def kernels_digest() -> str:
     import hashlib
     h = hashlib.sha256()
-    for f in ("kernels.hip", "kernels.hpp", "engine.hip", "engine.hpp"):
-        with open(os.path.join(ROOT, "regcm_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
+    src = os.path.join(ROOT, "regcm_amd", "csrc")
+    for f in sorted(os.listdir(src)):
+        if f.endswith((".hip", ".hpp")):
+            with open(os.path.join(src, f), "rb") as fh:
+                h.update(fh.read())
     return h.hexdigest()[:16]
 
 
 def pmc_traffic(kernel: str, config: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (tools/pmc_summary.py), only if it was measured on this exact kernel source."""
+    pmc_file = PMC_FILE if config == "C3" else os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
     try:
-        with open(PMC_FILE) as fh:
+        with open(pmc_file) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None, None

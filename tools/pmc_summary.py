@@ -37,7 +37,8 @@ def load(pass_dir):
 
 
 def main():
-    base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_C3")
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "C3"
+    base = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc_" + cfg)
     known = 64 * 2**20 * 8
     cf = load(os.path.join(base, "cal_fetch")).get("k_calib_copy", {}).get("FETCH_SIZE")
     cw = load(os.path.join(base, "cal_write")).get("k_calib_copy", {}).get("WRITE_SIZE")
@@ -51,8 +52,8 @@ def main():
             for k, d in load(os.path.join(base, p)).items():
                 extra.setdefault(k, {}).update(d)
     from bench import kernels_digest
-    res = {"digest": kernels_digest(), "config": "C3",
-           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py C3 graph replay; "
+    res = {"digest": kernels_digest(), "config": cfg,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), bench.py {cfg} graph replay; "
                      "read scale from tools/calib/calib_fetch.hip",
            "calibration": {"fetch_kib_reported": cf, "write_kib_reported": cw, "bytes_known": known,
                            "read_scale": rf, "write_scale": rw},
@@ -66,7 +67,7 @@ def main():
         wb = w * 1024.0 * (rw or 1.0)
         res["kernels"][k] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
                              "hbm_bytes_per_launch": rb + wb, "counters": extra.get(k, {})}
-    out = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    out = os.path.join(ROOT, "profiles", "pmc_traffic.json" if cfg == "C3" else f"pmc_traffic_{cfg}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
     print(json.dumps(res["calibration"]))
