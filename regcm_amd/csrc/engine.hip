@@ -455,13 +455,12 @@ struct rcmdyn_engine {
     const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
     NHFields f{};
     for (double** p : {&f.a1pp, &f.a2pp, &f.umc, &f.vmc, &f.ud, &f.vd, &f.umd, &f.vmd, &f.xt, &f.xqv, &f.xqc,
-                       &f.xtv, &f.xpp, &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.ubd, &f.vbd, &f.tb3d, &f.qvb3d, &f.qcb3d,
-                       &f.ppb3d, &f.pb3d, &f.xkcr, &f.xkc, &f.xkd, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
+                       &f.xtv, &f.xpp, &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.xkc, &f.xkd, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
                        &f.ppten, &f.ppdyn, &f.ct, &f.cu, &f.cv, &f.cpp, &f.cdt, &f.se, &f.sf, &f.saa, &f.sb,
                        &f.sc, &f.rhs, &f.sca, &f.sg1, &f.sg2, &f.ptend, &f.pxup, &f.pyvp, &f.tk, &f.scc, &f.scdd,
                        &f.scj, &f.spi, &f.th})
       *p = dalloc(t, P3);
-    for (double** p : {&f.a1w, &f.a2w, &f.xw, &f.wb3d, &f.pf3d, &f.xkcf, &f.wten, &f.wdyn, &f.cw, &f.wo})
+    for (double** p : {&f.a1w, &f.a2w, &f.xw, &f.xkcf, &f.wten, &f.wdyn, &f.cw, &f.wo})
       *p = dalloc(t, P4);
     f.ppb0 = dalloc(t, P3); f.ppbt = dalloc(t, P3); f.wwb0 = dalloc(t, P4); f.wwbt = dalloc(t, P4);
     f.pr0 = dalloc(t, P3); f.t0 = dalloc(t, P3); f.rho0 = dalloc(t, P3); f.z0 = dalloc(t, P3);
@@ -1372,7 +1371,6 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
       const Grids q = grids(g);
-      KLAUNCH(k_nh_mkslice, q.fr, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
     });
     xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});

@@ -137,38 +137,26 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
 }
 
 // mkslice NH subset (Main/mod_slice.F90:163-183, 278-281): the b-level decoupled winds, t, q,
-// pp and w the step reads (the NH level pressures of :207-225 are formed by the physics-seam
-// export, slice.hip, which is their only reader)
-__global__ void k_nh_mkslice(Geom g, const Consts* __restrict__ c, NHFields f) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  if (k <= kz && in(j, g.jde1gb, g.jde2gb) && in(i, g.ide1gb, g.ide2gb)) {
-    const double r = F2(f.rpsdb, j, i);
-    F3(f.ubd, j, i, k) = F3(f.a2u, j, i, k) * r;
-    F3(f.vbd, j, i, k) = F3(f.a2v, j, i, k) * r;
-  }
-  if (!(in(j, g.jce1gb, g.jce2gb) && in(i, g.ice1gb, g.ice2gb))) return;
-  const double rp = F2(f.rpsb, j, i);
-  F3(f.wb3d, j, i, k) = F3(f.a2w, j, i, k) * rp;
-  if (k <= kz) {
-    F3(f.tb3d, j, i, k) = F3(f.a2t, j, i, k) * rp;
-    F3(f.qvb3d, j, i, k) = dmax(F3(f.a2qv, j, i, k) * rp, MINQQ);
-    F3(f.qcb3d, j, i, k) = dmax(F3(f.a2qc, j, i, k) * rp, d_zero);
-    F3(f.ppb3d, j, i, k) = F3(f.a2pp, j, i, k) * rp;
-  }
-}
+// pp and w (atm2 times 1/psdotb or 1/psb, q clipped at minqq / 0) are formed by their readers
+// as they load them -- k_nh_coeff_raw and the LDS staging of k_nh_tend_c / k_nh_tend_d --
+// so they never reach memory (the NH level pressures of :207-225 are formed by the
+// physics-seam export, slice.hip, which is their only reader)
+#define UBD(J, I, K) (F3(f.a2u, J, I, K) * F2(f.rpsdb, J, I))
+#define VBD(J, I, K) (F3(f.a2v, J, I, K) * F2(f.rpsdb, J, I))
 
 // calc_coeff NH (Main/mod_diffusion.F90:215-250): Smagorinsky coefficient with the
 // vertical-velocity term, unscaled (xkcr) ...
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
-  const double* ud = f.ubd; const double* vd = f.vbd;
-  const double dudx = F3(ud, j + 1, i, k) + F3(ud, j + 1, i + 1, k) - F3(ud, j, i, k) - F3(ud, j, i + 1, k);
-  const double dvdx = F3(vd, j + 1, i, k) + F3(vd, j + 1, i + 1, k) - F3(vd, j, i, k) - F3(vd, j, i + 1, k);
-  const double dudy = F3(ud, j, i + 1, k) + F3(ud, j + 1, i + 1, k) - F3(ud, j, i, k) - F3(ud, j + 1, i, k);
-  const double dvdy = F3(vd, j, i + 1, k) + F3(vd, j + 1, i + 1, k) - F3(vd, j, i, k) - F3(vd, j + 1, i, k);
-  const double dwdz = F3(f.wb3d, j, i, k) - F3(f.wb3d, j, i, k + 1);
+  const double u00 = UBD(j, i, k), u10 = UBD(j + 1, i, k), u01 = UBD(j, i + 1, k), u11 = UBD(j + 1, i + 1, k);
+  const double v00 = VBD(j, i, k), v10 = VBD(j + 1, i, k), v01 = VBD(j, i + 1, k), v11 = VBD(j + 1, i + 1, k);
+  const double dudx = u10 + u11 - u00 - u01;
+  const double dvdx = v10 + v11 - v00 - v01;
+  const double dudy = u01 + u11 - u00 - u10;
+  const double dvdy = v01 + v11 - v00 - v10;
+  const double rpb = F2(f.rpsb, j, i);
+  const double dwdz = F3(f.a2w, j, i, k) * rpb - F3(f.a2w, j, i, k + 1) * rpb;
   const double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
   F3(f.xkcr, j, i, k) = dmin(F2(f.hgfact, j, i) + c->dydc * duv, c->xkhmax);
 }
@@ -363,11 +351,12 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
       ok[n] = q < TCW * TCH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
       const int jr = ok[n] ? jg : g.j0, ir = ok[n] ? ig : g.i0;
       for (int m = 0; m < TC_NF; m++) va[n][m] = 0.0;
-      va[n][4] = F3(f.wb3d, jr, ir, k);
+      const double rpb = F2(f.rpsb, jr, ir);             // mkslice's products (:163-183)
+      va[n][4] = F3(f.a2w, jr, ir, k) * rpb;
       if (nb) va[n][TC_IF + 3] = (F3(f.wwb0, jr, ir, k) + xt * F3(f.wwbt, jr, ir, k)) - F3(f.a2w, jr, ir, k);
       if (k <= kz) {
-        va[n][0] = F3(f.tb3d, jr, ir, k); va[n][1] = F3(f.qvb3d, jr, ir, k);
-        va[n][2] = F3(f.qcb3d, jr, ir, k); va[n][3] = F3(f.ppb3d, jr, ir, k);
+        va[n][0] = F3(f.a2t, jr, ir, k) * rpb; va[n][1] = dmax(F3(f.a2qv, jr, ir, k) * rpb, MINQQ);
+        va[n][2] = dmax(F3(f.a2qc, jr, ir, k) * rpb, d_zero); va[n][3] = F3(f.a2pp, jr, ir, k) * rpb;
         if (TC_HADV) {
           va[n][TC_IH] = F3(f.xpp, jr, ir, k); va[n][TC_IH + 1] = F3(f.th, jr, ir, k);
           va[n][TC_IH + 2] = F3(f.xqv, jr, ir, k); va[n][TC_IH + 3] = F3(f.xqc, jr, ir, k);
@@ -627,7 +616,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
       const int jr = ok[n] ? jg : j0c(g), ir = ok[n] ? ig : i0c(g);
       va[n][0] = F3(f.umc, jr, ir, k); va[n][1] = F3(f.vmc, jr, ir, k);
       va[n][2] = F3(f.ud, jr, ir, k); va[n][3] = F3(f.vd, jr, ir, k); va[n][4] = F3(f.cr, jr, ir, k);
-      va[n][5] = F3(f.ubd, jr, ir, k); va[n][6] = F3(f.vbd, jr, ir, k);
+      va[n][5] = UBD(jr, ir, k); va[n][6] = VBD(jr, ir, k);
       const double m = F2(f.msfd, jr, ir);
       va[n][5] = va[n][5] / m; va[n][6] = va[n][6] / m;     // UM of diffu_d, Main/mod_diffusion.F90:281-411
     }
