@@ -69,22 +69,17 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 
 // ---------------------------------------------------------------------------------------
 // decouple NH (Main/mod_tendency.F90:852-1066): coupled/decoupled winds on the dot frame
-// (umc, vmc, ud, vd, umd, vmd), decoupled t, q, tv, pp, w, atm1 pr/rho and the buoyancy
-// helper atmx%pr on the cross frame, and the potential temperature th of ithadv = 1
+// (ud, vd; umc/vmc and umd/vmd are formed by their readers), decoupled q, pp, w, atm1 pr/rho
+// and the buoyancy helper atmx%pr on the cross frame, and the potential temperature th of ithadv = 1
 // (:1349-1353) on the cross frame with its ghost ring, the points exchange(th,1) fills: th is
 // pointwise in atmx%t and atm1%pr, which are defined there.  k = 1..kz+1 (w only on kz+1).
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
   if (k <= kz && in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
-    const double m = F2(f.msfd, j, i);
-    F3(f.umc, j, i, k) = F3(f.a1u, j, i, k) * m;
-    F3(f.vmc, j, i, k) = F3(f.a1v, j, i, k) * m;
     const double2 d = udvd_nh(g, c->iboudy, f.a1u, f.a1v, f.rpsda, j, i, k);
-    F3(f.ud, j, i, k) = d.x;
+    F3(f.ud, j, i, k) = d.x;                           // umd = ud*msfd: formed by omega, tend_d
     F3(f.vd, j, i, k) = d.y;
-    F3(f.umd, j, i, k) = d.x * m;
-    F3(f.vmd, j, i, k) = d.y * m;
   }
   if (!(in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga))) return;
   const double rp = F2(f.rpsa, j, i);
@@ -111,11 +106,16 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   if (!IN_CE(j, i)) return;
   const int kz = c->kz;
   const double dummy = d_one / (c->dx2 * F2(f.msfx, j, i) * F2(f.msfx, j, i));
+  // umd, vmd = ud, vd * msfd (decouple :893-994) at the four dot points of the column
+  const double m00 = F2(f.msfd, j, i), m01 = F2(f.msfd, j, i + 1), m10 = F2(f.msfd, j + 1, i),
+               m11 = F2(f.msfd, j + 1, i + 1);
   auto ucc = [&](int kk) {
-    return F3(f.umd, j, i, kk) + F3(f.umd, j, i + 1, kk) + F3(f.umd, j + 1, i, kk) + F3(f.umd, j + 1, i + 1, kk);
+    return F3(f.ud, j, i, kk) * m00 + F3(f.ud, j, i + 1, kk) * m01 + F3(f.ud, j + 1, i, kk) * m10 +
+           F3(f.ud, j + 1, i + 1, kk) * m11;
   };
   auto vcc = [&](int kk) {
-    return F3(f.vmd, j, i, kk) + F3(f.vmd, j, i + 1, kk) + F3(f.vmd, j + 1, i, kk) + F3(f.vmd, j + 1, i + 1, kk);
+    return F3(f.vd, j, i, kk) * m00 + F3(f.vd, j, i + 1, kk) * m01 + F3(f.vd, j + 1, i, kk) * m10 +
+           F3(f.vd, j + 1, i + 1, kk) * m11;
   };
   const double ps0 = F2(f.ps0, j, i), dx = F2(f.dpsdxm, j, i), dy = F2(f.dpsdym, j, i);
   F3(f.qdot, j, i, 1) = d_zero;
@@ -130,8 +130,11 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   }
   const double ps = F2(f.psa, j, i);
   for (int k = 1; k <= kz; k++) {
-    const double a = F3(f.umc, j + 1, i + 1, k) + F3(f.umc, j + 1, i, k) - F3(f.umc, j, i + 1, k) - F3(f.umc, j, i, k);
-    const double b = F3(f.vmc, j + 1, i + 1, k) + F3(f.vmc, j, i + 1, k) - F3(f.vmc, j + 1, i, k) - F3(f.vmc, j, i, k);
+    // umc, vmc = atm1 u, v * msfd (decouple)
+    const double a = F3(f.a1u, j + 1, i + 1, k) * m11 + F3(f.a1u, j + 1, i, k) * m10 -
+                     F3(f.a1u, j, i + 1, k) * m01 - F3(f.a1u, j, i, k) * m00;
+    const double b = F3(f.a1v, j + 1, i + 1, k) * m11 + F3(f.a1v, j, i + 1, k) * m01 -
+                     F3(f.a1v, j + 1, i, k) * m10 - F3(f.a1v, j, i, k) * m00;
     F3(f.cr, j, i, k) = (a + b) * dummy + (F3(f.qdot, j, i, k + 1) - F3(f.qdot, j, i, k)) * ps / c->dsigma[k];
   }
 }
@@ -389,11 +392,13 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     return;
   }
   const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
+  const double m00 = F2(f.msfd, j, i), m01 = F2(f.msfd, j, i + 1), m10 = F2(f.msfd, j + 1, i),
+               m11 = F2(f.msfd, j + 1, i + 1);
   auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
-    u1 = F3(f.umc, j, i + 1, kk) + F3(f.umc, j, i, kk);
-    u2 = F3(f.umc, j + 1, i + 1, kk) + F3(f.umc, j + 1, i, kk);
-    v1 = F3(f.vmc, j + 1, i, kk) + F3(f.vmc, j, i, kk);
-    v2 = F3(f.vmc, j + 1, i + 1, kk) + F3(f.vmc, j, i + 1, kk);
+    u1 = F3(f.a1u, j, i + 1, kk) * m01 + F3(f.a1u, j, i, kk) * m00;          // umc = atm1 u * msfd
+    u2 = F3(f.a1u, j + 1, i + 1, kk) * m11 + F3(f.a1u, j + 1, i, kk) * m10;
+    v1 = F3(f.a1v, j + 1, i, kk) * m10 + F3(f.a1v, j, i, kk) * m00;
+    v2 = F3(f.a1v, j + 1, i + 1, kk) * m11 + F3(f.a1v, j, i + 1, kk) * m01;
   };
   // boundary relaxation (:1462-1501, Main/mod_bdycod.F90): nudging coefficients of the band
   const bool band = f.rgcr[g.ix(j, i)] > 0;
@@ -614,10 +619,10 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
       const int q = tid + n * 256, jg = J0 + q % TDW, ig = I0 + q / TDW;
       ok[n] = q < TDW * TDH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
       const int jr = ok[n] ? jg : j0c(g), ir = ok[n] ? ig : i0c(g);
-      va[n][0] = F3(f.umc, jr, ir, k); va[n][1] = F3(f.vmc, jr, ir, k);
+      const double m = F2(f.msfd, jr, ir);
+      va[n][0] = F3(f.a1u, jr, ir, k) * m; va[n][1] = F3(f.a1v, jr, ir, k) * m;   // umc, vmc
       va[n][2] = F3(f.ud, jr, ir, k); va[n][3] = F3(f.vd, jr, ir, k); va[n][4] = F3(f.cr, jr, ir, k);
       va[n][5] = UBD(jr, ir, k); va[n][6] = VBD(jr, ir, k);
-      const double m = F2(f.msfd, jr, ir);
       va[n][5] = va[n][5] / m; va[n][6] = va[n][6] / m;     // UM of diffu_d, Main/mod_diffusion.F90:281-411
     }
 #pragma unroll
@@ -693,8 +698,9 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
     const double uc = F3(f.a1u, j, i, k), vc = F3(f.a1v, j, i, k);
     const double duv = uc * F2(f.dmdy, j, i) - vc * F2(f.dmdx, j, i);
     const double cor = F2(f.coriol, j, i), ef = F2(f.ef, j, i);
-    ud = ud + cor * vc - ef * F2(f.ddx, j, i) * wabar + F3(f.vmd, j, i, k) * duv - uc * amfac;
-    vd = vd - cor * uc + ef * F2(f.ddy, j, i) * wabar - F3(f.umd, j, i, k) * duv - vc * amfac;
+    const double msd = F2(f.msfd, j, i);              // umd, vmd = ud, vd * msfd (decouple)
+    ud = ud + cor * vc - ef * F2(f.ddx, j, i) * wabar + (L2(sV, 0, 0) * msd) * duv - uc * amfac;
+    vd = vd - cor * uc + ef * F2(f.ddy, j, i) * wabar - (L2(sU, 0, 0) * msd) * duv - vc * amfac;
   }
   // boundary relaxation of u, v (nudgeuv) or the iboudy = 4 sponge of their total tendencies
   double ut0 = d_zero, vt0 = d_zero;
