@@ -68,11 +68,12 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 }
 
 // ---------------------------------------------------------------------------------------
-// decouple NH (Main/mod_tendency.F90:852-1066): coupled/decoupled winds on the dot frame
-// (ud, vd; umc/vmc and umd/vmd are formed by their readers), decoupled q, pp, w, atm1 pr/rho
-// and the buoyancy helper atmx%pr on the cross frame, and the potential temperature th of ithadv = 1
-// (:1349-1353) on the cross frame with its ghost ring, the points exchange(th,1) fills: th is
-// pointwise in atmx%t and atm1%pr, which are defined there.  k = 1..kz+1 (w only on kz+1).
+// decouple NH (Main/mod_tendency.F90:852-1066): the decoupled winds ud, vd (with the iboudy
+// inflow/outflow rule) on the dot frame; atm1 pr/rho, the buoyancy helper atmx%pr and the
+// potential temperature th of ithadv = 1 (:1349-1353) on the cross frame with its ghost ring,
+// the points exchange(th,1) fills: th is pointwise in atmx%t and atm1%pr, which are defined
+// there.  The other decoupled fields -- umc, vmc, umd, vmd and atmx w, pp, qv, qc -- are one
+// product (and clip) of a state field each and are formed by their readers.
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
@@ -83,16 +84,13 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   }
   if (!(in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga))) return;
   const double rp = F2(f.rpsa, j, i);
-  F3(f.xw, j, i, k) = F3(f.a1w, j, i, k) * rp;
   if (k > kz) return;
   const double xt = F3(f.a1t, j, i, k) * rp;
   const double xqv = dmax(F3(f.a1qv, j, i, k) * rp, MINQQ);
-  const double xqc = dmax(F3(f.a1qc, j, i, k) * rp, d_zero);
   const double xtv = xt * (d_one + c->ep1 * xqv);
   const double xpp = F3(f.a1pp, j, i, k) * rp;
   const double pr1 = F3(f.pr0, j, i, k) + xpp;
-  F3(f.xqv, j, i, k) = xqv; F3(f.xqc, j, i, k) = xqc;      // atmx%t, tv: read only here
-  F3(f.xpp, j, i, k) = xpp; F3(f.pr1, j, i, k) = pr1;
+  F3(f.pr1, j, i, k) = pr1;      // atmx t, tv, qv, qc, pp, w: formed by their readers
   F3(f.rho1, j, i, k) = pr1 / (c->rgas * xtv);
   F3(f.th, j, i, k) = xt * rcm_powpos(P00 / pr1, c->rovcp);
   if (IN_CI(j, i))
@@ -123,7 +121,7 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   double um = ucc(1), vm = vcc(1);
   for (int k = 2; k <= kz; k++) {
     const double uk = ucc(k), vk = vcc(k);
-    F3(f.qdot, j, i, k) = -F3(f.rhof0, j, i, k) * EGRAV_NH * F3(f.xw, j, i, k) / ps0 -
+    F3(f.qdot, j, i, k) = -F3(f.rhof0, j, i, k) * EGRAV_NH * (F3(f.a1w, j, i, k) * F2(f.rpsa, j, i)) / ps0 -
                           c->sigma[k] * (dx * (c->twt1[k] * uk + c->twt2[k] * um) +
                                          dy * (c->twt1[k] * vk + c->twt2[k] * vm));
     um = uk; vm = vk;
@@ -181,14 +179,13 @@ __global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields 
 }
 
 // upstream flux form of hadvt/hadvqv/hadvqx/hadv3d ind 0 at one cross point
-// (Main/mod_advection.F90:337-386, 547-596, 639-653, 466-480); limiter 0 none, 1 t, 2 q
-__device__ __forceinline__ double hadv_fg(const Geom& g, const Consts* c, const double* fa, int j, int i, int k,
-                                          double u1, double u2, double v1, double v2, double xmf, double ps,
-                                          int limiter) {
+// (Main/mod_advection.F90:337-386, 547-596, 639-653, 466-480) on the values of the advected
+// field at the point and its west/east/south/north neighbours; limiter 0 none, 1 t, 2 q
+__device__ __forceinline__ double hadv_v(const Consts* c, double fc, double fw, double fe, double fs, double fn,
+                                         double u1, double u2, double v1, double v2, double xmf, double ps,
+                                         int limiter) {
   const double f1 = d_half * c->ul * (u2 + u1) / ps;
   const double f2 = d_half * c->ul * (v2 + v1) / ps;
-  const double fc = F3(fa, j, i, k), fw = F3(fa, j - 1, i, k), fe = F3(fa, j + 1, i, k);
-  const double fs = F3(fa, j, i - 1, k), fn = F3(fa, j, i + 1, k);
   const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
   const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
   const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
@@ -246,34 +243,7 @@ __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax)
   return d_zero;
 }
 
-// hadv_fg / diffx_at on a field staged in LDS: S[ti][tj] is the thread's point
-template <int W>
-__device__ __forceinline__ double hadv_fgl(const Consts* c, const double (*S)[W], int ti, int tj, double u1,
-                                           double u2, double v1, double v2, double xmf, double ps, int limiter) {
-  const double f1 = d_half * c->ul * (u2 + u1) / ps;
-  const double f2 = d_half * c->ul * (v2 + v1) / ps;
-  const double fc = S[ti][tj], fw = S[ti][tj - 1], fe = S[ti][tj + 1];
-  const double fs = S[ti - 1][tj], fn = S[ti + 1][tj];
-  const double fx1 = (d_one + f1) * fw + (d_one - f1) * fc;
-  const double fx2 = (d_one + f1) * fc + (d_one - f1) * fe;
-  const double fy1 = (d_one + f2) * fs + (d_one - f2) * fc;
-  const double fy2 = (d_one + f2) * fc + (d_one - f2) * fn;
-  double fg = -xmf * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1);
-  if (limiter && c->stability_enhance) {
-    double den, thr;
-    if (limiter == 1) { den = ps; thr = c->t_extrema; }
-    else { den = dmax(fc, DLOWVAL); thr = c->q_rel_extrema; }
-    if (fabs(fn + fs - d_two * fc) / den > thr) {
-      if (fc > fn && fc > fs) fg = dmin(fg, d_zero);
-      else if (fc < fn && fc < fs) fg = dmax(fg, d_zero);
-    }
-    if (fabs(fe + fw - d_two * fc) / den > thr) {
-      if (fc > fe && fc > fw) fg = dmin(fg, d_zero);
-      else if (fc < fe && fc < fw) fg = dmax(fg, d_zero);
-    }
-  }
-  return fg;
-}
+// diffx_at on a field staged in LDS: S[ti][tj] is the thread's point
 template <int W>
 __device__ __forceinline__ double diffx_l(const Geom& g, const Consts* c, double ften, const double (*S)[W],
                                           double xk, int j, int i, int ti, int tj) {
@@ -316,14 +286,7 @@ __device__ __forceinline__ double diffx_l(const Geom& g, const Consts* c, double
 // time filters in between do not change) and with sound's scaling by the acoustic step
 // (Main/mod_sound.F90:229-245): those are the tendencies sound reads.
 constexpr int TCJ = 32, TCI = 8, TCW = TCJ + 4, TCH = TCI + 4;   // k_nh_tend_c block and staged tile
-#ifndef TC_HADV            // stage the advected fields (else read from L1/L2)
-#define TC_HADV 0
-#endif
-#ifndef TC_FG              // stage the relaxation differences (else read from L1/L2)
-#define TC_FG 0
-#endif
-constexpr int TC_NF = 5 + (TC_HADV ? 5 : 0) + (TC_FG ? 4 : 0);
-constexpr int TC_IH = 5, TC_IF = TC_HADV ? 10 : 5;   // first hadv / FG slot
+constexpr int TC_NF = 5;
 #ifndef TC_W
 #define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
 #endif
@@ -331,20 +294,17 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
                                                    int istep) {
   // the horizontal stencil operands of this level for the 32 x 8 block and a 2-point halo,
-  // staged in LDS once: the diffusion fields (13-point); optionally (TC_HADV, TC_FG) the
-  // advected fields (5-point) and, in blocks holding band points under nudging, the 5-point
-  // relaxation differences FG/FQ -- measured slower at C5 (3.36 ms diffusion only, 3.66 ms
+  // staged in LDS once: the diffusion fields (13-point).  Staging the advected fields or the
+  // relaxation differences as well measured slower at C5 (3.36 ms diffusion only, 3.66 ms
   // with the advected fields, 4.27 ms with both: LDS occupancy costs more than the L1 loads)
   __shared__ double sT[TC_NF][TCH][TCW];
   const int j = g.j0 + TBX * TCJ + (int)threadIdx.x, i = g.i0 + TBY * TCI + (int)threadIdx.y, k = TBZ + 1;
   const int kz = c->kz;
   const double xt = s->xbctime + s->dt;
   const bool inframe = j < g.j0 + g.nj && i < g.i0 + g.ni;
-  const int anyband = __syncthreads_or(inframe && IN_CI(j, i) && f.rgcr[g.ix(j, i)] > 0);
   {
     const int J0 = g.j0 + TBX * TCJ - 2, I0 = g.i0 + TBY * TCI - 2;
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
-    const bool nb = TC_FG && anyband && c->iboudy != 4;
     constexpr int NS = (TCW * TCH + 255) / 256;
     double va[NS][TC_NF];
     bool ok[NS];
@@ -356,21 +316,9 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
       for (int m = 0; m < TC_NF; m++) va[n][m] = 0.0;
       const double rpb = F2(f.rpsb, jr, ir);             // mkslice's products (:163-183)
       va[n][4] = F3(f.a2w, jr, ir, k) * rpb;
-      if (nb) va[n][TC_IF + 3] = (F3(f.wwb0, jr, ir, k) + xt * F3(f.wwbt, jr, ir, k)) - F3(f.a2w, jr, ir, k);
       if (k <= kz) {
         va[n][0] = F3(f.a2t, jr, ir, k) * rpb; va[n][1] = dmax(F3(f.a2qv, jr, ir, k) * rpb, MINQQ);
         va[n][2] = dmax(F3(f.a2qc, jr, ir, k) * rpb, d_zero); va[n][3] = F3(f.a2pp, jr, ir, k) * rpb;
-        if (TC_HADV) {
-          va[n][TC_IH] = F3(f.xpp, jr, ir, k); va[n][TC_IH + 1] = F3(f.th, jr, ir, k);
-          va[n][TC_IH + 2] = F3(f.xqv, jr, ir, k); va[n][TC_IH + 3] = F3(f.xqc, jr, ir, k);
-          if (k >= 2) va[n][TC_IH + 4] = F3(f.xw, jr, ir, k);
-        }
-        if (nb) {
-          const double nfac = 1.0e3;
-          va[n][TC_IF] = (F3(f.tb0, jr, ir, k) + xt * F3(f.tbt, jr, ir, k)) - F3(f.a2t, jr, ir, k);
-          va[n][TC_IF + 1] = nfac * (F3(f.qb0, jr, ir, k) + xt * F3(f.qbt, jr, ir, k)) - nfac * F3(f.a2qv, jr, ir, k);
-          va[n][TC_IF + 2] = (F3(f.ppb0, jr, ir, k) + xt * F3(f.ppbt, jr, ir, k)) - F3(f.a2pp, jr, ir, k);
-        }
       }
     }
 #pragma unroll
@@ -394,6 +342,18 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
   const double m00 = F2(f.msfd, j, i), m01 = F2(f.msfd, j, i + 1), m10 = F2(f.msfd, j + 1, i),
                m11 = F2(f.msfd, j + 1, i + 1);
+  // atmx of decouple (:852-1066) formed here: xw, xpp = atm1 w, pp * (1/p*), xqv, xqc the same
+  // clipped at minqq / 0, at the point and its four neighbours (the 1/p* values of the five)
+  const double r0 = F2(f.rpsa, j, i), rw = F2(f.rpsa, j - 1, i), re = F2(f.rpsa, j + 1, i),
+               rs = F2(f.rpsa, j, i - 1), rn = F2(f.rpsa, j, i + 1);
+  auto hadx = [&](const double* a, int clip, double u1, double u2, double v1, double v2, int lim) {
+    double x[5] = {F3(a, j, i, k) * r0, F3(a, j - 1, i, k) * rw, F3(a, j + 1, i, k) * re, F3(a, j, i - 1, k) * rs,
+                   F3(a, j, i + 1, k) * rn};
+    if (clip)
+      for (int q = 0; q < 5; q++) x[q] = dmax(x[q], clip == 1 ? MINQQ : d_zero);
+    return hadv_v(c, x[0], x[1], x[2], x[3], x[4], u1, u2, v1, v2, xmf, ps, lim);
+  };
+  auto xqcat = [&](int kk) { return dmax(F3(f.a1qc, j, i, kk) * r0, d_zero); };
   auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
     u1 = F3(f.a1u, j, i + 1, kk) * m01 + F3(f.a1u, j, i, kk) * m00;          // umc = atm1 u * msfd
     u2 = F3(f.a1u, j + 1, i + 1, kk) * m11 + F3(f.a1u, j + 1, i, kk) * m10;
@@ -417,17 +377,6 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
 #define RELAX5(x, b0, bt, a) \
   x = nh_relax(x, xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), FG(b0, bt, a, j + 1, i), \
                FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
-#if TC_FG
-#define RELAXL(x, m, b0, bt, a) \
-  x = nh_relax(x, xf, xg, sT[m][ti][tj], sT[m][ti][tj - 1], sT[m][ti][tj + 1], sT[m][ti - 1][tj], sT[m][ti + 1][tj])
-#else
-#define RELAXL(x, m, b0, bt, a) RELAX5(x, b0, bt, a)
-#endif
-#if TC_HADV
-#define HADVL(m, fa, lim) hadv_fgl(c, sT[m], ti, tj, u1, u2, v1, v2, xmf, ps, lim)
-#else
-#define HADVL(m, fa, lim) hadv_fg(g, c, fa, j, i, k, u1, u2, v1, v2, xmf, ps, lim)
-#endif
 #define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
   // ================= w on full levels k = 1..kz+1
   {
@@ -441,17 +390,12 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
       const double vaz1 = (t1 * v1 + t2 * pv1), vaz2 = (t1 * v2 + t2 * pv2);
       const double f1 = d_half * ul * (u2 + u1) / ps;
       const double f2 = d_half * ul * (v2 + v1) / ps;
-#if TC_HADV
-      const double (*w)[TCW] = sT[TC_IH + 4];
-#define XW(dj, di) w[ti + (di)][tj + (dj)]
-#else
-#define XW(dj, di) F3(f.xw, j + (dj), i + (di), k)
-#endif
-      const double fx1 = (d_one + f1) * XW(-1, 0) + (d_one - f1) * XW(0, 0);
-      const double fx2 = (d_one + f1) * XW(0, 0) + (d_one - f1) * XW(1, 0);
-      const double fy1 = (d_one + f2) * XW(0, -1) + (d_one - f2) * XW(0, 0);
-      const double fy2 = (d_one + f2) * XW(0, 0) + (d_one - f2) * XW(0, 1);
-#undef XW
+      const double wc = F3(f.a1w, j, i, k) * r0, ww = F3(f.a1w, j - 1, i, k) * rw, we = F3(f.a1w, j + 1, i, k) * re;
+      const double ws = F3(f.a1w, j, i - 1, k) * rs, wn = F3(f.a1w, j, i + 1, k) * rn;     // xw
+      const double fx1 = (d_one + f1) * ww + (d_one - f1) * wc;
+      const double fx2 = (d_one + f1) * wc + (d_one - f1) * we;
+      const double fy1 = (d_one + f2) * ws + (d_one - f2) * wc;
+      const double fy2 = (d_one + f2) * wc + (d_one - f2) * wn;
       wd = wd - xmf * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
     }
     // vadv3d ind = 0, nk = kz+1 (w), :756-765: flux through the interface below level kk
@@ -469,7 +413,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
         return F3(f.a1v, j, i, kk) + F3(f.a1v, j, i + 1, kk) + F3(f.a1v, j + 1, i, kk) + F3(f.a1v, j + 1, i + 1, kk);
       };
       const double uk = ucc(k), vk = vcc(k), um = ucc(k - 1), vm = vcc(k - 1);
-      const double rps = F2(f.rpsa, j, i);
+      const double rps = r0;
       const double ex = F2(f.ex, j, i), crx = F2(f.crx, j, i), cry = F2(f.cry, j, i);
       const double rofac = (c->dsigma[k - 1] * F3(f.rho0, j, i, k) + c->dsigma[k] * F3(f.rho0, j, i, k - 1)) /
                            (c->dsigma[k - 1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, k - 1));
@@ -478,12 +422,12 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
       wd = wd +
           (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
           ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
-          F3(f.xw, j, i, k) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
-      wd = wd - EGRAV_NH * ps * (c->twt2[k] * F3(f.xqc, j, i, k - 1) + c->twt1[k] * F3(f.xqc, j, i, k));
+          (F3(f.a1w, j, i, k) * r0) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
+      wd = wd - EGRAV_NH * ps * (c->twt2[k] * xqcat(k - 1) + c->twt1[k] * xqcat(k));
     }
     double wt0 = d_zero;
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
-    if (nudge) RELAXL(wd, TC_IF + 3, f.wwb0, f.wwbt, f.a2w);
+    if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
     wd = diffx_l(g, c, wd, sT[4], F3(f.xkcf, j, i, k), j, i, ti, tj);
     double wt = wt0 + wd + PHY(wphy);
     // raydamp3f and decoupling before sound (:466-499), sound's acoustic-step scaling (:229-245)
@@ -497,16 +441,16 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   const double cr = F3(f.cr, j, i, k);
   // ================= pp: hadv3d ind 0, vadv3d ind = 0 (nk = kz), adiabatic, boundary, diffusion
   {
-    double pd = d_zero + HADVL(TC_IH, f.xpp, 0);
+    double pd = d_zero + hadx(f.a1pp, 0, u1, u2, v1, v2, 0);
     auto pflux = [&](int kk) {
       return F3(f.qdot, j, i, kk) * (c->twt1[kk] * F3(f.a1pp, j, i, kk) + c->twt2[kk] * F3(f.a1pp, j, i, kk - 1));
     };
     if (k >= 2) pd = pd + pflux(k) * c->xds[k];
     if (k + 1 <= kz) pd = pd - pflux(k + 1) * c->xds[k];
-    pd = pd + F3(f.xpp, j, i, k) * cr;
+    pd = pd + (F3(f.a1pp, j, i, k) * r0) * cr;
     double pt0 = d_zero;
     if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
-    if (nudge) RELAXL(pd, TC_IF + 2, f.ppb0, f.ppbt, f.a2pp);
+    if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
     const double xkc = F3(f.xkc, j, i, k);
     pd = diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
     double pt = pt0 + pd + PHY(ppphy);
@@ -520,7 +464,8 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   // ================= t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d
   // ind = 0 (nk = kz) of tha = th*p*, plus th*cr; tdyn = atm1%t*thten/tha
   {
-    double thd = d_zero + HADVL(TC_IH + 1, f.th, 1);
+    double thd = d_zero + hadv_v(c, F3(f.th, j, i, k), F3(f.th, j - 1, i, k), F3(f.th, j + 1, i, k),
+                                 F3(f.th, j, i - 1, k), F3(f.th, j, i + 1, k), u1, u2, v1, v2, xmf, ps, 1);
     auto thflux = [&](int kk) {
       return F3(f.qdot, j, i, kk) *
              (c->twt1[kk] * (F3(f.th, j, i, kk) * ps) + c->twt2[kk] * (F3(f.th, j, i, kk - 1) * ps));
@@ -532,7 +477,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double td = d_zero + F3(f.a1t, j, i, k) * thd / (th * ps);
     double tt0 = d_zero;
     if (sponge) tt0 = wsp * d_zero + (d_one - wsp) * F3(f.tbt, j, i, k);
-    if (nudge) RELAXL(td, TC_IF, f.tb0, f.tbt, f.a2t);
+    if (nudge) RELAX5(td, f.tb0, f.tbt, f.a2t);
     td = diffx_l(g, c, td, sT[0], F3(f.xkc, j, i, k), j, i, ti, tj);
     double tt = tt0 + td + PHY(tphy);
     tt = tt + 0.0;
@@ -544,7 +489,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   // diffusion, forecast
   {
     double qd = d_zero + (c->isladvec ? F3(f.slqv, j, i, k)
-                                      : HADVL(TC_IH + 2, f.xqv, 2));
+                                      : hadx(f.a1qv, 1, u1, u2, v1, v2, 2));
     const double thr = MINQQ * ps;
     auto qflux = [&](int kk) {
       const double fk = F3(f.a1qv, j, i, kk), fkm = F3(f.a1qv, j, i, kk - 1);
@@ -554,19 +499,14 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     };
     if (k >= 2) qd = qd + qflux(k) * c->xds[k];
     if (k + 1 <= kz) qd = qd - qflux(k + 1) * c->xds[k];
-    qd = qd + F3(f.xqv, j, i, k) * cr;
+    qd = qd + dmax(F3(f.a1qv, j, i, k) * r0, MINQQ) * cr;
     double qt0 = d_zero;
     if (sponge) qt0 = wsp * d_zero + (d_one - wsp) * F3(f.qbt, j, i, k);
     if (nudge) {
       const double nfac = 1.0e3, rfac = d_one / nfac;
-#if TC_FG
-      const double (*Q)[TCW] = sT[TC_IF + 1];
-      const double q0 = Q[ti][tj], q1 = Q[ti][tj - 1], q2 = Q[ti][tj + 1], q3 = Q[ti - 1][tj], q4 = Q[ti + 1][tj];
-#else
 #define FQ(J, I) (nfac * (F3(f.qb0, J, I, k) + xt * F3(f.qbt, J, I, k)) - nfac * F3(f.a2qv, J, I, k))
       const double q0 = FQ(j, i), q1 = FQ(j - 1, i), q2 = FQ(j + 1, i), q3 = FQ(j, i - 1), q4 = FQ(j, i + 1);
 #undef FQ
-#endif
       qd = qd + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
     }
     qd = diffx_l(g, c, qd, sT[1], F3(f.xkc, j, i, k), j, i, ti, tj);
@@ -580,7 +520,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   // diffusion, forecast
   {
     double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
-                                      : HADVL(TC_IH + 3, f.xqc, 0));
+                                      : hadx(f.a1qc, 2, u1, u2, v1, v2, 0));
     const double thr = MINQQ * MINQQ * ps;
     auto cflux = [&](int kk) {
       const double svv = F3(f.qdot, j, i, kk);
@@ -590,7 +530,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     };
     if (k >= 2) cd = cd + cflux(k) * c->xds[k];
     if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
-    cd = cd + F3(f.xqc, j, i, k) * cr;
+    cd = cd + xqcat(k) * cr;
     cd = diffx_l(g, c, cd, sT[2], F3(f.xkc, j, i, k), j, i, ti, tj);
     double qc = d_zero + cd + PHY(qcphy);
     qc = qc + 0.0;
@@ -765,8 +705,6 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
 }
 #undef PHY
 #undef RELAX5
-#undef RELAXL
-#undef HADVL
 #undef FG
 
 // negative-moisture fix (:382-393): see K6 in kernels.hip.  Parallel pass for the points

@@ -23,7 +23,7 @@ struct NHFields {
   // 2-D reciprocals (k_surface_pressures)
   const double *rpsa, *rpsb, *rpsda, *rpsdb, *psdota, *psdotb;
   // decoupled / derived fields of the step
-  double *ud, *vd, *xqv, *xqc, *xpp, *xw, *pr1, *rho1, *xpr;
+  double *ud, *vd, *pr1, *rho1, *xpr;
   double *th;                    // potential temperature atmx%t*(p00/atm1%pr)**rovcp (ithadv = 1)
   double *cr, *qdot;
   double *xkcr, *xkc, *xkd, *xkcf, *uavg1, *uavg2, *vavg1, *vavg2;
