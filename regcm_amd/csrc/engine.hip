@@ -455,12 +455,12 @@ struct rcmdyn_engine {
     const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
     NHFields f{};
     for (double** p : {&f.a1pp, &f.a2pp, &f.ud, &f.vd,
-                       &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.xkc, &f.xkd, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
+                       &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
                        &f.ppten, &f.ppdyn, &f.ct, &f.cu, &f.cv, &f.cpp, &f.cdt, &f.se, &f.sf, &f.saa, &f.sb,
                        &f.sc, &f.rhs, &f.sca, &f.sg1, &f.sg2, &f.ptend, &f.pxup, &f.pyvp, &f.tk, &f.scc, &f.scdd,
                        &f.scj, &f.spi, &f.th})
       *p = dalloc(t, P3);
-    for (double** p : {&f.a1w, &f.a2w, &f.xkcf, &f.wten, &f.wdyn, &f.cw, &f.wo})
+    for (double** p : {&f.a1w, &f.a2w, &f.wten, &f.wdyn, &f.cw, &f.wo})
       *p = dalloc(t, P4);
     f.ppb0 = dalloc(t, P3); f.ppbt = dalloc(t, P3); f.wwb0 = dalloc(t, P4); f.wwbt = dalloc(t, P4);
     f.pr0 = dalloc(t, P3); f.t0 = dalloc(t, P3); f.rho0 = dalloc(t, P3); f.z0 = dalloc(t, P3);
@@ -489,7 +489,7 @@ struct rcmdyn_engine {
     TkeArgs a{};
     a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.msfd = t.msfd; a.xmsf = t.xmsf; a.psa = t.psa_[c]; a.rpsa = t.rpsa;
     a.qdot = t.qdot; a.tkephy = t.tkephy; a.a1tke = t.a1tke; a.a2tke = t.a2tke; a.ctke = t.ctke;
-    if (cfg.idynamic == 2) { a.xk = nhf[&t - tiles.data()].xkcf; a.xk_half = 0; }
+    if (cfg.idynamic == 2) { a.xk = nhf[&t - tiles.data()].xkcr; a.xkpb = t.psb_[t.cur]; a.xk_half = 0; }
     else { a.xk = t.xkcs; a.xk_half = 1; }
     return a;
   }
@@ -1374,10 +1374,6 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
     });
     xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      KLAUNCH(k_nh_coeff_scale, grids(g).fr, BLK, 0, stream, g, dc, nhfields(t));
-    });
     if (slice) run_slice();
     }
     if (!(phase & TEND_POST)) return;

@@ -162,21 +162,9 @@ __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f)
   F3(f.xkcr, j, i, k) = dmin(F2(f.hgfact, j, i) + c->dydc * duv, c->xkhmax);
 }
 
-// ... then xkc, xkcf (cross interior, full levels) and xkd (dot interior), scaled
-__global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  if (IN_CI(j, i)) {
-    const double pb = F2(f.psb, j, i);
-    if (k <= kz) F3(f.xkc, j, i, k) = F3(f.xkcr, j, i, k) * c->rdxsq * pb;
-    F3(f.xkcf, j, i, k) = F3(f.xkcr, j, i, (k == 1) ? 1 : k - 1) * c->rdxsq * pb;
-  }
-  if (k <= kz && IN_DI(j, i)) {
-    const double x = d_rfour * (F3(f.xkcr, j, i, k) + F3(f.xkcr, j - 1, i - 1, k) + F3(f.xkcr, j - 1, i, k) +
-                                F3(f.xkcr, j, i - 1, k));
-    F3(f.xkd, j, i, k) = x * c->rdxsq * F2(f.psdotb, j, i);
-  }
-}
+// ... then scaled by rdxsq and p* (b) by their readers: xkc, xkcf (cross interior, full
+// levels: xkcr of level k-1) in k_nh_tend_c, xkd (dot interior, the four-point mean) in
+// k_nh_tend_d (Main/mod_diffusion.F90:236-250)
 
 // upstream flux form of hadvt/hadvqv/hadvqx/hadv3d ind 0 at one cross point
 // (Main/mod_advection.F90:337-386, 547-596, 639-653, 466-480) on the values of the advected
@@ -339,7 +327,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     }
     return;
   }
-  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul;
+  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), ul = c->ul, pbs = F2(f.psb, j, i);
   const double m00 = F2(f.msfd, j, i), m01 = F2(f.msfd, j, i + 1), m10 = F2(f.msfd, j + 1, i),
                m11 = F2(f.msfd, j + 1, i + 1);
   // atmx of decouple (:852-1066) formed here: xw, xpp = atm1 w, pp * (1/p*), xqv, xqc the same
@@ -428,7 +416,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double wt0 = d_zero;
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
     if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
-    wd = diffx_l(g, c, wd, sT[4], F3(f.xkcf, j, i, k), j, i, ti, tj);
+    wd = diffx_l(g, c, wd, sT[4], F3(f.xkcr, j, i, (k == 1) ? 1 : k - 1) * c->rdxsq * pbs, j, i, ti, tj);   // xkcf
     double wt = wt0 + wd + PHY(wphy);
     // raydamp3f and decoupling before sound (:466-499), sound's acoustic-step scaling (:229-245)
     if (c->ifrayd == 1 && k <= c->rayndamp)
@@ -436,6 +424,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     F3(f.wten, j, i, k) = (wt * F2(f.rpsa, j, i)) * dts;
   }
   if (k > kz) return;
+  const double xkc = F3(f.xkcr, j, i, k) * c->rdxsq * pbs;      // calc_coeff's xkc
   double u1, u2, v1, v2;
   avg(k, u1, u2, v1, v2);
   const double cr = F3(f.cr, j, i, k);
@@ -451,7 +440,6 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double pt0 = d_zero;
     if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
     if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
-    const double xkc = F3(f.xkc, j, i, k);
     pd = diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
     double pt = pt0 + pd + PHY(ppphy);
     if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3, decoupling, acoustic-step scaling
@@ -478,7 +466,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double tt0 = d_zero;
     if (sponge) tt0 = wsp * d_zero + (d_one - wsp) * F3(f.tbt, j, i, k);
     if (nudge) RELAX5(td, f.tb0, f.tbt, f.a2t);
-    td = diffx_l(g, c, td, sT[0], F3(f.xkc, j, i, k), j, i, ti, tj);
+    td = diffx_l(g, c, td, sT[0], xkc, j, i, ti, tj);
     double tt = tt0 + td + PHY(tphy);
     tt = tt + 0.0;
     if (ray) tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
@@ -509,7 +497,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
 #undef FQ
       qd = qd + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
     }
-    qd = diffx_l(g, c, qd, sT[1], F3(f.xkc, j, i, k), j, i, ti, tj);
+    qd = diffx_l(g, c, qd, sT[1], xkc, j, i, ti, tj);
     double qv = qt0 + qd + PHY(qvphy);
     qv = qv + 0.0;
     if (ray) qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
@@ -531,7 +519,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     if (k >= 2) cd = cd + cflux(k) * c->xds[k];
     if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
     cd = cd + xqcat(k) * cr;
-    cd = diffx_l(g, c, cd, sT[2], F3(f.xkc, j, i, k), j, i, ti, tj);
+    cd = diffx_l(g, c, cd, sT[2], xkc, j, i, ti, tj);
     double qc = d_zero + cd + PHY(qcphy);
     qc = qc + 0.0;
     if (wdiag) F3(f.qcten, j, i, k) = qc;
@@ -662,7 +650,8 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
   // diffu_d, Main/mod_diffusion.F90:281-411 (UM = ubd/msfd, vbd/msfd staged)
   {
 #define UM(S, J, I) L2(S, (J) - j, (I) - i)
-    const double xkd = F3(f.xkd, j, i, k);
+    const double xkd = d_rfour * (F3(f.xkcr, j, i, k) + F3(f.xkcr, j - 1, i - 1, k) + F3(f.xkcr, j - 1, i, k) +
+                                  F3(f.xkcr, j, i - 1, k)) * c->rdxsq * F2(f.psdotb, j, i);   // calc_coeff
 #pragma unroll
     for (int pass = 0; pass < 2; pass++) {
       double (*b)[TDW] = pass ? sBV : sBU;

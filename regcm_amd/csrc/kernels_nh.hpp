@@ -26,7 +26,7 @@ struct NHFields {
   double *ud, *vd, *pr1, *rho1, *xpr;
   double *th;                    // potential temperature atmx%t*(p00/atm1%pr)**rovcp (ithadv = 1)
   double *cr, *qdot;
-  double *xkcr, *xkc, *xkd, *xkcf, *uavg1, *uavg2, *vavg1, *vavg2;
+  double *xkcr, *uavg1, *uavg2, *vavg1, *vavg2;
   // tendencies: total (pc_total) and dynamic (pc_dynamic)
   double *tten, *tdyn, *qvten, *qvdyn, *qcten, *qcdyn, *uten, *udyn, *vten, *vdyn;
   double *ppten, *ppdyn, *wten, *wdyn;
@@ -55,7 +55,6 @@ constexpr int NH_CFL_SLOTS = 1024;
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_coeff_scale(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tend_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int wdiag, int istep);
 __global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);

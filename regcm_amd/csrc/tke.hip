@@ -54,7 +54,8 @@ __global__ void k_tke_tend(Geom g, const Consts* __restrict__ c, const StepState
   }
   {                                         // diffu_x3df(tkedyn, atm2%tke, nuk), :523-598
     const double* x = a.a2tke;
-    const double xk = a.xk_half ? F3(a.xk, j, i, k > 1 ? k - 1 : 1) : F3(a.xk, j, i, k);
+    const double xk = a.xkpb ? F3(a.xk, j, i, k > 1 ? k - 1 : 1) * c->rdxsq * F2(a.xkpb, j, i)
+                    : a.xk_half ? F3(a.xk, j, i, k > 1 ? k - 1 : 1) : F3(a.xk, j, i, k);
     const double fac = c->nuk;
 #define X(dj, di) F3(x, j + (dj), i + (di), k)
     if (c->idiffu == 2) {

@@ -10,6 +10,7 @@ namespace rcm {
 // level down (Main/mod_diffusion.F90:232-235, 245): xkcf(1) = xkcs(1), xkcf(k+1) = xkcs(k).
 struct TkeArgs {
   const double *a1u, *a1v, *msfd, *xmsf, *psa, *rpsa, *qdot, *xk, *tkephy;
+  const double* xkpb;   // NH: xk is the unscaled xkcr, scaled here by rdxsq * p*(b) (xkcf)
   double *a1tke, *a2tke, *ctke;
   int xk_half;
 };
