@@ -1409,18 +1409,21 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
       KLAUNCH(k_nh_tfilter, q.cik, BLK, 0, stream, g, dc, f);
-      // sound, Main/mod_sound.F90:163-718
-      KLAUNCH(k_nh_sound_init, q.fr, BLK, 0, stream, g, dc, ds, f, istep);
     });
+    // sound, Main/mod_sound.F90:163-718
     for (int it = 1; it <= istep; it++) {
       if (it == 1) {             // later sub-steps: part A ran in the previous k_nh_sound_cd
         each([&](Tile& t) {
-          KLAUNCH(k_nh_sound_a, grids(t.g).ce1, BLK, 0, stream, t.g, dc, nhfields(t), it);
+          const Geom& g = t.g;
+          KLAUNCH(k_nh_sound_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc,
+                  nhfields(t));
         });
       }
       xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
       each([&](Tile& t) {
-        KLAUNCH(k_nh_sound_uv, grids(t.g).dik, BLK, 0, stream, t.g, dc, ds, nhfields(t), istep, (int)(it == istep));
+        const Geom& g = t.g;
+        KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, dc, ds,
+                nhfields(t), istep, (int)(it == istep), (int)(it == 1));
       });
       xch({{FK::NCU, kz}, {FK::NCV, kz}});
       each([&](Tile& t) {

@@ -788,42 +788,41 @@ __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f) {
 }
 
 // ======================================================================= sound
-// initial arrays of the acoustic loop (Main/mod_sound.F90:217-245; the tendencies' scaling by
-// the acoustic step ends the tendency kernels).  k = 1..kz+1.
-__global__ void k_nh_sound_init(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                                int istep) {
-  FRAME_POINT();
-  const int kz = c->kz;
-  (void)s; (void)istep;
-  const double rpb = IN_CE(j, i) ? F2(f.rpsb, j, i) : 0.0;
-  if (k <= kz) {
-    if (IN_DE(j, i)) {
-      F3(f.cu, j, i, k) = F3(f.a2u, j, i, k) / F2(f.psdotb, j, i);
-      F3(f.cv, j, i, k) = F3(f.a2v, j, i, k) / F2(f.psdotb, j, i);
-    }
-    if (IN_CE(j, i)) F3(f.cpp, j, i, k) = F3(f.a2pp, j, i, k) * rpb;
-  }
-  if (IN_CE(j, i)) F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
-}
+// The initial arrays of the acoustic loop (Main/mod_sound.F90:217-228: atmc pp, w = atm2 *
+// 1/psb on the cross frame, u, v = atm2 / psdotb on the dot frame) are formed by their first
+// readers: part A of sub-step 1 (pp, w) and part B of sub-step 1 (u, v); the tendencies'
+// scaling by the acoustic step (:229-245) ends the tendency kernels.
 
-// substep part A (:250-262), one thread per cross column: pp += xkd*pi, then dp'/dp0
-__global__ void k_nh_sound_a(Geom g, const Consts* __restrict__ c, NHFields f, int it) {
+// part A of sub-step 1, one thread per cross point and level k = 1..kz+1: the loop's initial
+// pp and w (:217-228, atm2 * 1/psb) and dp'/dp0 from that pp (:258-262)
+__global__ void k_nh_sound_a1(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
   const int kz = c->kz;
-  if (it > 1 && IN_CI(j, i))
-    for (int k = 1; k <= kz; k++) F3(f.cpp, j, i, k) = F3(f.cpp, j, i, k) + c->nhxkd * F3(f.spi, j, i, k);
-  for (int k = 1; k <= kz; k++) {
-    const int kp1 = (kz < k + 1) ? kz : k + 1, km1 = (1 > k - 1) ? 1 : k - 1;
-    F3(f.cdt, j, i, k) = (F3(f.cpp, j, i, km1) - F3(f.cpp, j, i, kp1)) / (F3(f.pr0, j, i, km1) - F3(f.pr0, j, i, kp1));
-  }
+  const double rpb = F2(f.rpsb, j, i);
+  F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
+  if (k > kz) return;
+  F3(f.cpp, j, i, k) = F3(f.a2pp, j, i, k) * rpb;
+  const int kp1 = (kz < k + 1) ? kz : k + 1, km1 = (1 > k - 1) ? 1 : k - 1;
+  F3(f.cdt, j, i, k) = (F3(f.a2pp, j, i, km1) * rpb - F3(f.a2pp, j, i, kp1) * rpb) /
+                       (F3(f.pr0, j, i, km1) - F3(f.pr0, j, i, kp1));
 }
 
 // substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep, int fin) {
-  THREAD_POINT(g.jdi1, g.idi1);
-  if (!IN_DI(j, i)) return;
+                              int istep, int fin, int first) {
+  THREAD_POINT(g.jde1, g.ide1);
+  // sub-step 1: the loop's initial u, v = atm2 / psdotb (:217-228), formed here; on the dot
+  // frame's boundary ring they stay so for the whole loop
+  auto init_u = [&](int jj, int ii) { return F3(f.a2u, jj, ii, k) / F2(f.psdotb, jj, ii); };
+  auto init_v = [&](int jj, int ii) { return F3(f.a2v, jj, ii, k) / F2(f.psdotb, jj, ii); };
+  if (!IN_DI(j, i)) {
+    if (first && IN_DE(j, i)) {
+      F3(f.cu, j, i, k) = init_u(j, i);
+      F3(f.cv, j, i, k) = init_v(j, i);
+    }
+    return;
+  }
   const double dts = s->dt / (double)istep;
   const double rho = d_rfour * (F3(f.rho1, j, i, k) + F3(f.rho1, j - 1, i, k) + F3(f.rho1, j, i - 1, k) +
                                 F3(f.rho1, j - 1, i - 1, k));
@@ -831,9 +830,9 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
                                    F3(f.cdt, j - 1, i - 1, k));
   const double chh = d_half * dts / (rho * c->dx) / F2(f.msfd, j, i);
   const double* pp = f.cpp;
-  double u = F3(f.cu, j, i, k) - chh * (F3(pp, j, i, k) - F3(pp, j - 1, i, k) + F3(pp, j, i - 1, k) -
+  double u = (first ? init_u(j, i) : F3(f.cu, j, i, k)) - chh * (F3(pp, j, i, k) - F3(pp, j - 1, i, k) + F3(pp, j, i - 1, k) -
                                         F3(pp, j - 1, i - 1, k) - F3(f.dprddx, j, i, k) * dppdp0);
-  double v = F3(f.cv, j, i, k) - chh * (F3(pp, j, i, k) - F3(pp, j, i - 1, k) + F3(pp, j - 1, i, k) -
+  double v = (first ? init_v(j, i) : F3(f.cv, j, i, k)) - chh * (F3(pp, j, i, k) - F3(pp, j, i - 1, k) + F3(pp, j - 1, i, k) -
                                         F3(pp, j - 1, i - 1, k) - F3(f.dprddy, j, i, k) * dppdp0);
   const double cu = u + F3(f.uten, j, i, k), cv = v + F3(f.vten, j, i, k);
   F3(f.cu, j, i, k) = cu;
