@@ -38,13 +38,17 @@ KERNEL_FIELDS = {
     #                  atm2/atm1 t, pr0 (15); writes w, pp, pi, atm2/atm1 t, dp'/dp0 (6)
     #   k_nh_sound_bc  reads pp, pi, pr1, rho0, t0, pr0, atm2 t, ppten, cu, cv, rho1, w, wten (13);
     #                  writes se, sf, pi, pp (4)
-    #   k_nh_tend_c    reads the decoupled/derived fields of the tendency chains (30) + t, qv, pp,
-    #                  w b0/bt in the band (8 f_b); writes wten, ppten, atmc t, qv, qc (5)
-    #   k_nh_tend_d    reads 16 + u, v b0/bt in the band (4 f_b); writes uten, vten (2)
+    #   k_nh_tend_c    reads atm1 u, v, t, qv, qc, pp, w, atm2 t, qv, qc, pp, w, th, qdot, cr,
+    #                  rho0, rho1, xpr, xkcr, z0, zf0 (21) + t, qv, pp, w b0/bt in the band
+    #                  (8 f_b); writes wten, ppten, atmc t, qv, qc (5); the decoupled products
+    #                  (xw, xpp, xqv, xqc, umc, vmc, the b-level fields, xkc, xkcf) are formed
+    #                  from these as they are read
+    #   k_nh_tend_d    reads atm1 u, v, w, atm2 u, v, ud, vd, cr, qdot, xkcr, z0 (11) + u, v b0/bt
+    #                  in the band (4 f_b); writes uten, vten (2)
     "k_nh_sound_cd": (21, 0, 5),
     "k_nh_sound_bc": (17, 0, 6),
-    "k_nh_tend_c": (35, 8, 6),
-    "k_nh_tend_d": (18, 4, 10),
+    "k_nh_tend_c": (26, 8, 9),
+    "k_nh_tend_d": (13, 4, 10),
 }
 
 
