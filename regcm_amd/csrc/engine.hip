@@ -1408,17 +1408,12 @@ struct rcmdyn_engine {
       const Grids q = grids(g);
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
-      KLAUNCH(k_nh_tfilter, q.cik, BLK, 0, stream, g, dc, f);
+      // tend's time filters with part A of the first acoustic sub-step (sound, :163-718)
+      KLAUNCH(k_nh_tfilter_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc, f);
     });
     // sound, Main/mod_sound.F90:163-718
     for (int it = 1; it <= istep; it++) {
-      if (it == 1) {             // later sub-steps: part A ran in the previous k_nh_sound_cd
-        each([&](Tile& t) {
-          const Geom& g = t.g;
-          KLAUNCH(k_nh_sound_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc,
-                  nhfields(t));
-        });
-      }
+      // part A: sub-step 1 in k_nh_tfilter_a1, the later ones in the previous k_nh_sound_cd
       xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
       each([&](Tile& t) {
         const Geom& g = t.g;

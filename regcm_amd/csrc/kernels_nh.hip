@@ -755,10 +755,10 @@ __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHField
   if (lane == 0) f.depplane[plane] = 0;
 }
 
-// time filters of t (RA), qv and qc (RAW), Main/mod_tendency.F90:422-427; p* is constant
-__global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jci1, g.ici1);
-  if (!IN_CI(j, i)) return;
+// time filters of t (RA), qv and qc (RAW), Main/mod_tendency.F90:422-427 (p* is constant),
+// at one interior cross point and level
+__device__ __forceinline__ void nh_tfilter_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
+                                              int k) {
   {
     const double o1 = F3(f.a1t, j, i, k), o2 = F3(f.a2t, j, i, k), nw = F3(f.ct, j, i, k);
     const double d = c->gnu1 * (nw + o2 - d_two * o1);
@@ -795,9 +795,8 @@ __global__ void k_nh_tfilter(Geom g, const Consts* __restrict__ c, NHFields f) {
 
 // part A of sub-step 1, one thread per cross point and level k = 1..kz+1: the loop's initial
 // pp and w (:217-228, atm2 * 1/psb) and dp'/dp0 from that pp (:258-262)
-__global__ void k_nh_sound_a1(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jce1, g.ice1);
-  if (!IN_CE(j, i)) return;
+__device__ __forceinline__ void nh_sound_a1_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
+                                               int k) {
   const int kz = c->kz;
   const double rpb = F2(f.rpsb, j, i);
   F3(f.cw, j, i, k) = F3(f.a2w, j, i, k) * rpb;
@@ -806,6 +805,15 @@ __global__ void k_nh_sound_a1(Geom g, const Consts* __restrict__ c, NHFields f) 
   const int kp1 = (kz < k + 1) ? kz : k + 1, km1 = (1 > k - 1) ? 1 : k - 1;
   F3(f.cdt, j, i, k) = (F3(f.a2pp, j, i, km1) * rpb - F3(f.a2pp, j, i, kp1) * rpb) /
                        (F3(f.pr0, j, i, km1) - F3(f.pr0, j, i, kp1));
+}
+
+// the filters of tend's end and part A of the first acoustic sub-step in one
+// launch: independent point work over the cross frame, k = 1..kz+1
+__global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  if (k <= c->kz && IN_CI(j, i)) nh_tfilter_at(g, c, f, j, i, k);
+  nh_sound_a1_at(g, c, f, j, i, k);
 }
 
 // substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
