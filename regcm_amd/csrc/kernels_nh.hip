@@ -4,13 +4,15 @@
 // and the NH boundary values.  ithadv = 1 (the only NH temperature path of the reference,
 // Main/mod_tendency.F90:98,128-129), ipptls = 1, i_crm = 0, physics stubbed.
 //
-// Each kernel restates one reference loop nest (or the whole vertical recurrence of a column,
-// one thread per column) with the same floating-point operation order as oracle/rcm_oracle.c
+// Every value is formed with the same floating-point operation order as oracle/rcm_oracle.c
 // (compiled with -ffp-contract=off), so transcendental-free results are bit-identical.  The
-// state is updated in place (the reference's own in-place semantics); intermediates the
-// reference keeps in module arrays live in HBM (NHFields).  This first NH path favours a
-// literal, verifiable structure over fusion: see DESIGN.md section 4 for its kernels and the
-// fusion plan.
+// kernels fuse the reference's loop nests where that keeps each element's operation sequence:
+// a chain of nests that each update only their own element becomes one thread's register
+// accumulation (k_nh_tend_c / k_nh_tend_d), a column recurrence absorbs the level-parallel work
+// that feeds it (k_nh_sound_bc / k_nh_sound_cd), and a decoupled product of a state field is
+// formed where it is read instead of being stored.  The state is updated in place (the
+// reference's own semantics); the intermediates that remain live in HBM (NHFields).  DESIGN.md
+// section 4.2 lists the kernels with their roofline position.
 #include "engine.hpp"
 #include "kernels_nh.hpp"
 #include "fastmath.hpp"
