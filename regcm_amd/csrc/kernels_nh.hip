@@ -532,21 +532,21 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
 // k_nh_tend_d stages its horizontal stencil operands of one level for a 64 x 4 block plus a
 // 2-point halo in LDS, one load (and for ubd/msfd, vbd/msfd one division) per staged point:
 // umc, vmc, ud, vd, cr (hadvuv) and the diffu_d operands; lanes outside the frame stage zero
-constexpr int TDW = 64 + 4, TDH = 4 + 4;
-__global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restrict__ c,
+constexpr int TDW = 64 + 4, TDH = TD_I + 4, TDT = 64 * TD_I;
+__global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int istep) {
   __shared__ double sUA[TDH][TDW], sVA[TDH][TDW], sU[TDH][TDW], sV[TDH][TDW], sCR[TDH][TDW];
   __shared__ double sBU[TDH][TDW], sBV[TDH][TDW];
-  const int j = g.jdi1 + TBX * 64 + (int)threadIdx.x, i = g.idi1 + TBY * 4 + (int)threadIdx.y, k = TBZ + 1;
+  const int j = g.jdi1 + TBX * 64 + (int)threadIdx.x, i = g.idi1 + TBY * TD_I + (int)threadIdx.y, k = TBZ + 1;
   {
-    const int J0 = g.jdi1 + TBX * 64 - 2, I0 = g.idi1 + TBY * 4 - 2;
+    const int J0 = g.jdi1 + TBX * 64 - 2, I0 = g.idi1 + TBY * TD_I - 2;
     const int tid = threadIdx.y * 64 + threadIdx.x;
-    constexpr int NS = (TDW * TDH + 255) / 256;
+    constexpr int NS = (TDW * TDH + TDT - 1) / TDT;
     double va[NS][7];
     bool ok[NS];
 #pragma unroll
     for (int n = 0; n < NS; n++) {
-      const int q = tid + n * 256, jg = J0 + q % TDW, ig = I0 + q / TDW;
+      const int q = tid + n * TDT, jg = J0 + q % TDW, ig = I0 + q / TDW;
       ok[n] = q < TDW * TDH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
       const int jr = ok[n] ? jg : j0c(g), ir = ok[n] ? ig : i0c(g);
       const double m = F2(f.msfd, jr, ir);
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(256) void k_nh_tend_d(Geom g, const Consts* __restr
     }
 #pragma unroll
     for (int n = 0; n < NS; n++) {
-      const int q = tid + n * 256, jj = q % TDW, ii = q / TDW;
+      const int q = tid + n * TDT, jj = q % TDW, ii = q / TDW;
       if (q < TDW * TDH) {
         const bool o = ok[n];
         sUA[ii][jj] = o ? va[n][0] : 0.0; sVA[ii][jj] = o ? va[n][1] : 0.0;

@@ -48,6 +48,10 @@ struct NHFields {
 constexpr int NH_CFL_SLOTS = 1024;
 // block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,
 // tiles_i) grids, consecutive blocks on consecutive levels of one tile
+// rows of dot points per k_nh_tend_d block (64 x TD_I threads)
+#ifndef TD_I
+#define TD_I 8
+#endif
 #ifndef NH_ZFIRST
 #define NH_ZFIRST 1
 #endif
