@@ -1395,9 +1395,9 @@ struct rcmdyn_engine {
       // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
       {
         const dim3 gd((g.jdi2 - g.jdi1 + 64) / 64, (g.idi2 - g.idi1 + TD_I) / TD_I, kz),
-            gc((g.nj + 31) / 32, (g.ni + 7) / 8, kp);
+            gc((g.nj + TC_J - 1) / TC_J, (g.ni + TC_I - 1) / TC_I, kp);
         KLAUNCH(k_nh_tend_d, NH_ZFIRST ? dim3(gd.z, gd.x, gd.y) : gd, dim3(64, TD_I), 0, stream, g, dc, ds, f, istep);
-        KLAUNCH(k_nh_tend_c, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(32, 8), 0, stream, g, dc, ds, f,
+        KLAUNCH(k_nh_tend_c, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
                 (int)diag, istep);
       }
     });

@@ -275,12 +275,12 @@ __device__ __forceinline__ double diffx_l(const Geom& g, const Consts* c, double
 // Rayleigh damping and decoupling of raydamp (:466-499; they read atm2 u, v, pp, w, which the
 // time filters in between do not change) and with sound's scaling by the acoustic step
 // (Main/mod_sound.F90:229-245): those are the tendencies sound reads.
-constexpr int TCJ = 32, TCI = 8, TCW = TCJ + 4, TCH = TCI + 4;   // k_nh_tend_c block and staged tile
+constexpr int TCJ = TC_J, TCI = TC_I, TCW = TCJ + 4, TCH = TCI + 4, TCT = TCJ * TCI;   // block, staged tile
 constexpr int TC_NF = 5;
 #ifndef TC_W
 #define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
 #endif
-__global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
+__global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
                                                    int istep) {
   // the horizontal stencil operands of this level for the 32 x 8 block and a 2-point halo,
@@ -295,12 +295,12 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   {
     const int J0 = g.j0 + TBX * TCJ - 2, I0 = g.i0 + TBY * TCI - 2;
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
-    constexpr int NS = (TCW * TCH + 255) / 256;
+    constexpr int NS = (TCW * TCH + TCT - 1) / TCT;
     double va[NS][TC_NF];
     bool ok[NS];
 #pragma unroll
     for (int n = 0; n < NS; n++) {
-      const int q = tid + n * 256, jg = J0 + q % TCW, ig = I0 + q / TCW;
+      const int q = tid + n * TCT, jg = J0 + q % TCW, ig = I0 + q / TCW;
       ok[n] = q < TCW * TCH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
       const int jr = ok[n] ? jg : g.j0, ir = ok[n] ? ig : g.i0;
       for (int m = 0; m < TC_NF; m++) va[n][m] = 0.0;
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     }
 #pragma unroll
     for (int n = 0; n < NS; n++) {
-      const int q = tid + n * 256, jj = q % TCW, ii = q / TCW;
+      const int q = tid + n * TCT, jj = q % TCW, ii = q / TCW;
       if (q < TCW * TCH)
         for (int m = 0; m < TC_NF; m++) sT[m][ii][jj] = ok[n] ? va[n][m] : 0.0;
     }

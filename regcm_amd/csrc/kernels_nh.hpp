@@ -48,6 +48,13 @@ struct NHFields {
 constexpr int NH_CFL_SLOTS = 1024;
 // block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,
 // tiles_i) grids, consecutive blocks on consecutive levels of one tile
+// k_nh_tend_c block: TC_J x TC_I cross points of one level
+#ifndef TC_J
+#define TC_J 32
+#endif
+#ifndef TC_I
+#define TC_I 8
+#endif
 // rows of dot points per k_nh_tend_d block (64 x TD_I threads)
 #ifndef TD_I
 #define TD_I 8
