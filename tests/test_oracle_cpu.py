@@ -365,27 +365,29 @@ def test_oracle_tke_bounds_and_independence(c1_data):
         assert np.array_equal(o.get(name), b.get(name)), name
 
 
-def test_nh_theta_advection_matches_numpy_restatement():
-    """The NH temperature tendency of the restatement against an independent NumPy
-    restatement of the reference's ithadv = 1 path (Main/mod_tendency.F90:98,128-129: ithadv
-    stays 1 for idynamic = 2; :1347-1356, 1594-1600): th = atmx%t*(p00/atm1%pr)**rovcp,
-    tha = th*p*, thten = hadvt(th) + vadv3d ind 0 (tha) + th*cr, tdyn = atm1%t*thten/tha.
-    Also restates qdot of compute_omega NH (:1157-1191).  With ckh = adyndif = 0 (xkc = 0,
-    no diffusion) and ifrayd = 0, tten at points outside the relaxation band is exactly that
-    tdyn.  The comparison is at 1e-13 relative (numpy and the C restatement both call libm
-    pow/division in the same order, so it is usually bit-exact)."""
+def _nh_tend_restatement(extra=(), cloud=False):
+    """One oracle tend of the N1 NH case with no diffusion (ckh = adyndif = 0, so xkc = 0) and
+    no Rayleigh damping, plus the NumPy restatement's shared pieces: the interior points
+    outside the relaxation band, the horizontal wind averages of start_advect, qdot of
+    compute_omega NH (Main/mod_tendency.F90:1157-1191) and the mass divergence cr."""
     import dataclasses
     from oracle.oracle import OracleCore
     rc = dataclasses.replace(CONFIGS["N1"], ckh=0.0, adyndif=0.0, ifrayd=0)
     data = icbc.generate_nh(rc)
     o = OracleCore(rc, data["split"])
-    o.put_state(data["state"])
+    state = dict(data["state"])
+    if cloud:       # a cloud layer: qc = 1 % of qv on levels 4..12, none elsewhere (both vadv4d branches)
+        for a1, a2 in (("ATM1_QC", "ATM1_QV"), ("ATM2_QC", "ATM2_QV")):
+            qc = np.zeros_like(state[a2])
+            qc[3:12] = 0.01 * state[a2][3:12]
+            state[a1] = qc
+    o.put_state(state)
     o.bdyval()
     g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_PP", "ATM1_W", "PSA", "MSFX", "MSFD",
-                                "ATM0_PR", "ATM0_PS", "ATM0_RHOF", "DPSDXM", "DPSDYM")}
+                                "ATM0_PR", "ATM0_PS", "ATM0_RHOF", "DPSDXM", "DPSDYM") + tuple(extra)}
     o.tend()
-    tten, qdot_o = o.get("TTEN"), o.get("QDOT")
-
+    r = {"rc": rc, "g": g, "out": {n: o.get(n) for n in ("TTEN", "QVTEN", "QCTEN", "QDOT")}}
+    o.close()
     kz, nsp = rc.kz, rc.nspgx
     sig = rc.sigma
     hsig = (sig[1:] + sig[:-1]) * 0.5
@@ -395,12 +397,6 @@ def test_nh_theta_advection_matches_numpy_restatement():
         twt1[k] = (sig[k - 1] - hsig[k - 2]) / (hsig[k - 1] - hsig[k - 2])
         twt2[k] = 1.0 - twt1[k]
     dx = rc.ds * 1000.0
-    ul = rc.uoffc * 0.5 * rc.dt / dx                             # Main/mod_advection.F90:106
-    from regcm_amd import constants as C
-    rgas = C.rgas
-    cpd = 3.5 * rgas
-    rovcp = rgas * (1.0 / cpd)                                   # Share/mod_constants.F90:183-184
-    egrav = 9.80665
     # interior cross points outside the relaxation band (1-based global j, i)
     J = np.arange(nsp + 1, rc.jx - nsp)
     I = np.arange(nsp + 1, rc.iy - nsp)
@@ -423,34 +419,60 @@ def test_nh_theta_advection_matches_numpy_restatement():
     vcc = at(vmd) + at(vmd, 0, 1) + at(vmd, 1, 0) + at(vmd, 1, 1)
     pinv = np.divide(1.0, g["PSA"][0], out=np.zeros_like(g["PSA"][0]), where=g["PSA"][0] > 0)
     xw = g["ATM1_W"] * pinv[None]
+    egrav = 9.80665
     qdot = np.zeros((kz + 1,) + ps.shape)
     for k in range(2, kz + 1):
         qdot[k - 1] = (-at(g["ATM0_RHOF"])[k - 1] * egrav * at(xw)[k - 1] / at(g["ATM0_PS"])[0] -
                        sig[k - 1] * (at(g["DPSDXM"])[0] * (twt1[k] * ucc[k - 1] + twt2[k] * ucc[k - 2]) +
                                      at(g["DPSDYM"])[0] * (twt1[k] * vcc[k - 1] + twt2[k] * vcc[k - 2])))
-    np.testing.assert_allclose(qdot, at(qdot_o), rtol=1e-13, atol=1e-13 * np.abs(qdot).max())
-    # mass divergence cr
     a = at(umc, 1, 1) + at(umc, 1, 0) - at(umc, 0, 1) - at(umc)
     b = at(vmc, 1, 1) + at(vmc, 0, 1) - at(vmc, 1, 0) - at(vmc)
     dummy = 1.0 / (2.0 * dx * msfx * msfx)
     cr = (a + b) * dummy[None] + (qdot[1:] - qdot[:-1]) * ps[None] / dsig[:, None, None]
-    # th on the interior and its four neighbours
-    rps = pinv
-    with np.errstate(divide="ignore", invalid="ignore"):
-        thf = (g["ATM1_T"] * rps[None]) * (1.0e5 / (g["ATM0_PR"] + g["ATM1_PP"] * rps[None])) ** rovcp
-    th, thw, the, ths, thn = at(thf), at(thf, -1), at(thf, 1), at(thf, 0, -1), at(thf, 0, 1)
+    # start_advect's wind averages (Main/mod_advection.F90:114-119) and hadv's f1, f2, xmapf
     u1 = at(umc, 0, 1) + at(umc)
     u2 = at(umc, 1, 1) + at(umc, 1, 0)
     v1 = at(vmc, 1, 0) + at(vmc)
     v2 = at(vmc, 1, 1) + at(vmc, 0, 1)
+    ul = rc.uoffc * 0.5 * rc.dt / dx                             # Main/mod_advection.F90:106
     f1 = 0.5 * ul * (u2 + u1) / ps[None]
     f2 = 0.5 * ul * (v2 + v1) / ps[None]
-    fx1 = (1.0 + f1) * thw + (1.0 - f1) * th
-    fx2 = (1.0 + f1) * th + (1.0 - f1) * the
-    fy1 = (1.0 + f2) * ths + (1.0 - f2) * th
-    fy2 = (1.0 + f2) * th + (1.0 - f2) * thn
     xmsf = 1.0 / (msfx * msfx * (4.0 * dx))                      # Main/mod_params.F90:1993-2001
-    fg = -xmsf[None] * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1)
+
+    def hadv(c, w, e, s_, n):                                    # the upstream flux form
+        fx1 = (1.0 + f1) * w + (1.0 - f1) * c
+        fx2 = (1.0 + f1) * c + (1.0 - f1) * e
+        fy1 = (1.0 + f2) * s_ + (1.0 - f2) * c
+        fy2 = (1.0 + f2) * c + (1.0 - f2) * n
+        return -xmsf[None] * (u2 * fx2 - u1 * fx1 + v2 * fy2 - v1 * fy1)
+
+    r.update(kz=kz, sig=sig, hsig=hsig, dsig=dsig, twt1=twt1, twt2=twt2, at=at, ps=ps, pinv=pinv,
+             qdot=qdot, cr=cr, hadv=hadv)
+    return r
+
+
+def test_nh_theta_advection_matches_numpy_restatement():
+    """The NH temperature tendency of the restatement against an independent NumPy
+    restatement of the reference's ithadv = 1 path (Main/mod_tendency.F90:98,128-129: ithadv
+    stays 1 for idynamic = 2; :1347-1356, 1594-1600): th = atmx%t*(p00/atm1%pr)**rovcp,
+    tha = th*p*, thten = hadvt(th) + vadv3d ind 0 (tha) + th*cr, tdyn = atm1%t*thten/tha.
+    Also restates qdot of compute_omega NH (:1157-1191).  With ckh = adyndif = 0 (xkc = 0,
+    no diffusion) and ifrayd = 0, tten at points outside the relaxation band is exactly that
+    tdyn.  The comparison is at 1e-13 relative (numpy and the C restatement both call libm
+    pow/division in the same order, so it is usually bit-exact)."""
+    r = _nh_tend_restatement()
+    rc, g, at, ps, kz = r["rc"], r["g"], r["at"], r["ps"], r["kz"]
+    qdot, cr, dsig, twt1, twt2 = r["qdot"], r["cr"], r["dsig"], r["twt1"], r["twt2"]
+    np.testing.assert_allclose(qdot, at(r["out"]["QDOT"]), rtol=1e-13, atol=1e-13 * np.abs(qdot).max())
+    from regcm_amd import constants as C
+    rgas = C.rgas
+    cpd = 3.5 * rgas
+    rovcp = rgas * (1.0 / cpd)                                   # Share/mod_constants.F90:183-184
+    rps = r["pinv"]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        thf = (g["ATM1_T"] * rps[None]) * (1.0e5 / (g["ATM0_PR"] + g["ATM1_PP"] * rps[None])) ** rovcp
+    th, thw, the, ths, thn = at(thf), at(thf, -1), at(thf, 1), at(thf, 0, -1), at(thf, 0, 1)
+    fg = r["hadv"](th, thw, the, ths, thn)
     for (p, m) in ((thn, ths), (the, thw)):                      # hadvt limiter :359-386
         big = np.abs(p + m - 2.0 * th) / ps[None] > rc.t_extrema
         fg = np.where(big & (th > p) & (th > m), np.minimum(fg, 0.0), fg)
@@ -463,9 +485,59 @@ def test_nh_theta_advection_matches_numpy_restatement():
         thten[k - 1] = thten[k - 1] + fx * (1.0 / dsig[k - 1])
     thten = thten + th * cr
     tdyn = at(g["ATM1_T"]) * thten / tha
-    got = at(tten)
+    got = at(r["out"]["TTEN"])
     assert np.abs(tdyn).max() > 1e-6
     np.testing.assert_allclose(got, tdyn, rtol=1e-12, atol=1e-13 * np.abs(tdyn).max())
+
+
+def test_nh_moisture_advection_matches_numpy_restatement():
+    """The NH qv and qc tendencies against an independent NumPy restatement of the reference
+    (no diffusion, no Rayleigh damping, points outside the band, as above): qv = hadvqv of
+    atmx%qx (upstream form with the q_rel_extrema limiter, Main/mod_advection.F90:517-603) +
+    vadvqv of atm1%qx (the qcon power form, :811-836) + atmx%qx*cr (Main/mod_tendency.F90:1616);
+    qc = hadvqx (:607-662) + vadv4d ind 1 (the upwind-thresholded twt form, :873-894) +
+    atmx%qx*cr, with atmx%qx = max(atm1%qx/p*, minqq) for qv and max(atm1%qx/p*, 0) for qc
+    (decouple).  minqq = 1e-8, dlowval = 1e-20 (Share/mod_constants.F90:57, 68)."""
+    r = _nh_tend_restatement(extra=("ATM1_QV", "ATM1_QC"), cloud=True)
+    rc, g, at, ps, kz = r["rc"], r["g"], r["at"], r["ps"], r["kz"]
+    qdot, cr, dsig, sig, hsig = r["qdot"], r["cr"], r["dsig"], r["sig"], r["hsig"]
+    twt1, twt2 = r["twt1"], r["twt2"]
+    minqq, dlowval = 1.0e-8, 1.0e-20
+    xds = 1.0 / dsig
+    qcon = np.zeros(kz + 1)
+    for k in range(2, kz + 1):                                   # Main/mod_params.F90:2214
+        qcon[k] = (sig[k - 1] - hsig[k - 1]) / (hsig[k - 2] - hsig[k - 1])
+    rps = r["pinv"]
+    for name, clip in (("ATM1_QV", minqq), ("ATM1_QC", 0.0)):
+        q1 = g[name]
+        xq = np.maximum(q1 * rps[None], clip)
+        c, w, e, s_, n = at(xq), at(xq, -1), at(xq, 1), at(xq, 0, -1), at(xq, 0, 1)
+        fg = r["hadv"](c, w, e, s_, n)
+        if name == "ATM1_QV":                   # hadvqv limiter :569-596 (stability_enhance on)
+            den = np.maximum(c, dlowval)
+            for (p, m) in ((n, s_), (e, w)):
+                big = np.abs(p + m - 2.0 * c) / den > rc.q_rel_extrema
+                fg = np.where(big & (c > p) & (c > m), np.minimum(fg, 0.0), fg)
+                fg = np.where(big & (c < p) & (c < m), np.maximum(fg, 0.0), fg)
+        ten = 0.0 + fg
+        f = at(q1)
+        for k in range(2, kz + 1):
+            fk, fkm, svv = f[k - 1], f[k - 2], qdot[k - 1]
+            if name == "ATM1_QV":                                # vadvqv
+                ok = (fk > minqq * ps) & (fkm > minqq * ps)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    fgk = np.where(ok, fk * (fkm / fk) ** qcon[k], 0.0)
+                flux = svv * fgk
+            else:                                                # vadv4d ind = 1
+                thr = minqq * minqq * ps
+                ok = np.where(svv > 0.0, fkm > thr, fk > thr)
+                flux = np.where(ok, svv * (twt1[k] * fk + twt2[k] * fkm), 0.0)
+            ten[k - 2] = ten[k - 2] - flux * xds[k - 2]
+            ten[k - 1] = ten[k - 1] + flux * xds[k - 1]
+        ten = ten + c * cr
+        got = at(r["out"]["QVTEN" if name == "ATM1_QV" else "QCTEN"])
+        assert np.abs(ten).max() > 0.0
+        np.testing.assert_allclose(got, ten, rtol=1e-11, atol=1e-12 * np.abs(ten).max(), err_msg=name)
 
 
 @pytest.mark.parametrize("nthreads", [2, 4, 6])
