@@ -386,7 +386,8 @@ def _nh_tend_restatement(extra=(), cloud=False):
     g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_PP", "ATM1_W", "PSA", "MSFX", "MSFD",
                                 "ATM0_PR", "ATM0_PS", "ATM0_RHOF", "DPSDXM", "DPSDYM") + tuple(extra)}
     o.tend()
-    r = {"rc": rc, "g": g, "out": {n: o.get(n) for n in ("TTEN", "QVTEN", "QCTEN", "QDOT")}}
+    r = {"rc": rc, "g": g, "out": {n: o.get(n) for n in ("TTEN", "QVTEN", "QCTEN", "QDOT", "UTEN", "VTEN")},
+         "dtsmax": data["split"]["nh_dtsmax"]}
     o.close()
     kz, nsp = rc.kz, rc.nspgx
     sig = rc.sigma
@@ -538,6 +539,95 @@ def test_nh_moisture_advection_matches_numpy_restatement():
         got = at(r["out"]["QVTEN" if name == "ATM1_QV" else "QCTEN"])
         assert np.abs(ten).max() > 0.0
         np.testing.assert_allclose(got, ten, rtol=1e-11, atol=1e-12 * np.abs(ten).max(), err_msg=name)
+
+
+def test_nh_wind_tendency_matches_numpy_restatement():
+    """The NH u, v tendencies of the first step against an independent NumPy restatement of
+    the reference (no diffusion, no Rayleigh damping, dot points outside the band): hadvuv's
+    NH upstream branch of atmx%ud, vd with the divergence term (Main/mod_advection.F90:235-264;
+    dmapf = 1/(msfd^2 16 dx), Main/mod_params.F90:1996), vadvuv of atmx%uc, vc (:271-303), the NH curvature and
+    Coriolis terms (Main/mod_tendency.F90:1839-1879), the decoupling by 1/psdota (:466-499)
+    and sound's scaling by the acoustic step dts = dt/istep (Main/mod_sound.F90:229-245;
+    istep = max(int(dt/dtsmax), 2) on the first step).  Shifted whole-domain arrays; only
+    the interior is compared."""
+    r = _nh_tend_restatement(extra=("CORIOL", "EF", "DDX", "DDY", "DMDX", "DMDY"))
+    rc, g, kz = r["rc"], r["g"], r["kz"]
+    sig, dsig, twt1, twt2 = r["sig"], r["dsig"], r["twt1"], r["twt2"]
+    dx = rc.ds * 1000.0
+    ul = rc.uoffc * 0.5 * rc.dt / dx
+    xds = 1.0 / dsig
+
+    def sh(a, dj, di):                                           # sh(a)[k, i, j] = a[k, i+di, j+dj]
+        return np.roll(a, shift=(-di, -dj), axis=(-2, -1))
+
+    u1, v1, w1 = g["ATM1_U"], g["ATM1_V"], g["ATM1_W"]
+    msfd, msfx = g["MSFD"][0], g["MSFX"][0]
+    pa = g["PSA"][0]
+    psd = np.zeros_like(pa)
+    psd[1:, 1:] = (pa[1:, 1:] + pa[:-1, 1:] + pa[1:, :-1] + pa[:-1, :-1]) * 0.25
+    rpsd = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0)
+    pinv = np.divide(1.0, pa, out=np.zeros_like(pa), where=pa > 0)
+    umc, vmc = u1 * msfd, v1 * msfd
+    ud, vd = u1 * rpsd, v1 * rpsd
+    umd, vmd = ud * msfd, vd * msfd
+    # compute_omega NH over the whole domain (cross point (j, i): dots j..j+1, i..i+1)
+    ucc = umd + sh(umd, 0, 1) + sh(umd, 1, 0) + sh(umd, 1, 1)
+    vcc = vmd + sh(vmd, 0, 1) + sh(vmd, 1, 0) + sh(vmd, 1, 1)
+    qdot = np.zeros_like(w1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for k in range(2, kz + 1):
+            qdot[k - 1] = (-g["ATM0_RHOF"][k - 1] * 9.80665 * (w1[k - 1] * pinv) / g["ATM0_PS"][0] -
+                           sig[k - 1] * (g["DPSDXM"][0] * (twt1[k] * ucc[k - 1] + twt2[k] * ucc[k - 2]) +
+                                         g["DPSDYM"][0] * (twt1[k] * vcc[k - 1] + twt2[k] * vcc[k - 2])))
+        a = sh(umc, 1, 1) + sh(umc, 1, 0) - sh(umc, 0, 1) - umc
+        b = sh(vmc, 1, 1) + sh(vmc, 0, 1) - sh(vmc, 1, 0) - vmc
+        cr = (a + b) / (2.0 * dx * msfx * msfx) + (qdot[1:] - qdot[:-1]) * pa / dsig[:, None, None]
+        dm = 1.0 / (msfd * msfd * 16.0 * dx)
+    # hadvuv, NH upstream branch
+    divd = 0.25 * (cr + sh(cr, 0, -1) + sh(cr, -1, 0) + sh(cr, -1, -1))
+    ucmona = sh(umc, 0, 1) + 2.0 * umc + sh(umc, 0, -1)
+    ucmonb = sh(umc, 1, 1) + 2.0 * sh(umc, 1, 0) + sh(umc, 1, -1)
+    ucmonc = sh(umc, -1, 1) + 2.0 * sh(umc, -1, 0) + sh(umc, -1, -1)
+    vcmona = sh(vmc, 1, 0) + 2.0 * vmc + sh(vmc, -1, 0)
+    vcmonb = sh(vmc, 1, 1) + 2.0 * sh(vmc, 0, 1) + sh(vmc, -1, 1)
+    vcmonc = sh(vmc, 1, -1) + 2.0 * sh(vmc, 0, -1) + sh(vmc, -1, -1)
+    diag = divd - dm * ((ucmonb - ucmonc) + (vcmonb - vcmonc))
+    ff1, ff2 = ul * (sh(ud, 1, 0) + ud), ul * (sh(ud, -1, 0) + ud)
+    ff3, ff4 = ul * (sh(vd, 0, 1) + vd), ul * (sh(vd, 0, -1) + vd)
+    ucb = (1.0 + ff1) * ucmona + (1.0 - ff1) * ucmonb
+    ucc_ = (1.0 + ff2) * ucmonc + (1.0 - ff2) * ucmona
+    vcb = (1.0 + ff3) * vcmona + (1.0 - ff3) * vcmonb
+    vcc_ = (1.0 + ff4) * vcmonc + (1.0 - ff4) * vcmona
+    udyn = ud * diag - dm * (sh(ud, 1, 0) * ucb - sh(ud, -1, 0) * ucc_ + sh(ud, 0, 1) * vcb - sh(ud, 0, -1) * vcc_)
+    vdyn = vd * diag - dm * (sh(vd, 1, 0) * ucb - sh(vd, -1, 0) * ucc_ + sh(vd, 0, 1) * vcb - sh(vd, 0, -1) * vcc_)
+    # vadvuv of the coupled winds atmx%uc, vc = atm1 u, v (Main/mod_tendency.F90:1304)
+    for k in range(2, kz + 1):
+        qq = 0.25 * (qdot[k - 1] + sh(qdot, 0, -1)[k - 1] + sh(qdot, -1, 0)[k - 1] + sh(qdot, -1, -1)[k - 1])
+        uu = qq * (twt1[k] * u1[k - 1] + twt2[k] * u1[k - 2])
+        vv = qq * (twt1[k] * v1[k - 1] + twt2[k] * v1[k - 2])
+        udyn[k - 2] = udyn[k - 2] - uu * xds[k - 2]
+        udyn[k - 1] = udyn[k - 1] + uu * xds[k - 1]
+        vdyn[k - 2] = vdyn[k - 2] - vv * xds[k - 2]
+        vdyn[k - 1] = vdyn[k - 1] + vv * xds[k - 1]
+    # curvature NH
+    wad = 0.125 * (sh(w1, -1, -1) + sh(w1, -1, 0) + sh(w1, 0, -1) + w1)
+    wabar = wad[:-1] + wad[1:]
+    amfac = wabar * rpsd * (1.0 / 6.371229e6)
+    duv = u1 * g["DMDY"][0] - v1 * g["DMDX"][0]
+    cor, ef = g["CORIOL"][0], g["EF"][0]
+    udyn = udyn + cor * v1 - ef * g["DDX"][0] * wabar + vmd * duv - u1 * amfac
+    vdyn = vdyn - cor * u1 + ef * g["DDY"][0] * wabar - umd * duv - v1 * amfac
+    istep = max(int(rc.dt / r["dtsmax"]), 2)
+    dts = rc.dt / istep
+    nsp = rc.nspgx
+    J = np.arange(nsp + 2, rc.jx - nsp)                          # dot points off the band
+    I = np.arange(nsp + 2, rc.iy - nsp)
+    sl = (slice(None), (I - 1)[:, None], (J - 1)[None, :])
+    for name, dyn in (("UTEN", udyn), ("VTEN", vdyn)):
+        want = (dyn * rpsd * dts)[sl]
+        got = r["out"][name][sl]
+        assert np.abs(want).max() > 0.0
+        np.testing.assert_allclose(got, want, rtol=1e-11, atol=1e-12 * np.abs(want).max(), err_msg=name)
 
 
 @pytest.mark.parametrize("nthreads", [2, 4, 6])
