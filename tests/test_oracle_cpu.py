@@ -630,6 +630,118 @@ def test_nh_wind_tendency_matches_numpy_restatement():
         np.testing.assert_allclose(got, want, rtol=1e-11, atol=1e-12 * np.abs(want).max(), err_msg=name)
 
 
+def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
+    """The hydrostatic t tendency of the first step against an independent NumPy restatement
+    of the reference (C1 with no diffusion, points off the relaxation band): compute_omega's
+    cr, pten and the qdot scan and omega (Main/mod_tendency.F90:1118-1215), hadvt of atmx%t in
+    the upstream form with the t_extrema limiter (Main/mod_advection.F90:311-393; upstream_mode
+    and stability_enhance are on for idynamic < 3, Main/mod_params.F90:645-647), vadv3d ind 1
+    of atm1%t with the (pf/pb)**c287 interpolation on mkslice's b-level pressures
+    (:767-779, Main/mod_slice.F90:233-239) and the adiabatic term
+    omega*rgas/cpmf(qv)*tv/(ptop/p* + hsigma) (Main/mod_tendency.F90:1565-1575; cpmf =
+    cpd*(1 + 0.8 qv), Share/cpmf.inc)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    from regcm_amd import constants as C
+    rc = dataclasses.replace(CONFIGS["C1"], ckh=0.0, adyndif=0.0)
+    data = icbc.generate(rc)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "PSB", "MSFX", "MSFD")}
+    o.tend()
+    tten = o.get("TTEN")
+    o.close()
+    kz = rc.kz
+    sig = rc.sigma
+    hsig = (sig[1:] + sig[:-1]) * 0.5
+    dsig = sig[1:] - sig[:-1]
+    twt1 = np.zeros(kz + 1); twt2 = np.zeros(kz + 1)
+    for k in range(2, kz + 1):
+        twt1[k] = (sig[k - 1] - hsig[k - 2]) / (hsig[k - 1] - hsig[k - 2])
+        twt2[k] = 1.0 - twt1[k]
+    dx = rc.ds * 1000.0
+    ul = rc.uoffc * 0.5 * rc.dt / dx
+    rgas = C.rgas
+    cpd = 3.5 * rgas
+    c287 = rgas / 1000.0                                         # Share/mod_constants.F90:132-134
+    ep1 = 28.96454 / 18.01528 - 1.0                              # amd/amw - 1 (:303)
+    minqq = 1.0e-8
+
+    def sh(a, dj, di):                                           # sh(a)[k, i, j] = a[k, i+di, j+dj]
+        return np.roll(a, shift=(-di, -dj), axis=(-2, -1))
+
+    u1, v1, t1, q1 = g["ATM1_U"], g["ATM1_V"], g["ATM1_T"], g["ATM1_QV"]
+    pa, pb = g["PSA"][0], g["PSB"][0]
+    msfx, msfd = g["MSFX"][0], g["MSFD"][0]
+    psd = np.zeros_like(pa)
+    psd[1:, 1:] = (pa[1:, 1:] + pa[:-1, 1:] + pa[1:, :-1] + pa[:-1, :-1]) * 0.25
+    rpsd = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0)
+    rpsa = np.divide(1.0, pa, out=np.zeros_like(pa), where=pa > 0)
+    umc, vmc = u1 * msfd, v1 * msfd
+    ud, vd = u1 * rpsd, v1 * rpsd
+    with np.errstate(divide="ignore", invalid="ignore"):
+        cr = ((sh(umc, 1, 1) + sh(umc, 1, 0) - sh(umc, 0, 1) - umc) +
+              (sh(vmc, 1, 1) + sh(vmc, 0, 1) - sh(vmc, 1, 0) - vmc)) / (2.0 * dx * msfx * msfx)
+        pten = np.zeros_like(pa)
+        for k in range(kz):
+            pten = pten - cr[k] * dsig[k]
+        qdot = np.zeros((kz + 1,) + pa.shape)
+        for k in range(2, kz + 1):
+            qdot[k - 1] = qdot[k - 2] - (pten + cr[k - 2]) * dsig[k - 2] * rpsa
+    xt = t1 * rpsa
+    xq = np.maximum(q1 * rpsa, minqq)
+    tv = xt * (1.0 + ep1 * xq)
+    # upstream hadvt of atmx%t with the t_extrema limiter (frame-edge values, never compared,
+    # may be inf/nan: p* is zero outside the frame)
+    old_err = np.seterr(divide="ignore", invalid="ignore")
+    u1a = sh(umc, 0, 1) + umc
+    u2a = sh(umc, 1, 1) + sh(umc, 1, 0)
+    v1a = sh(vmc, 1, 0) + vmc
+    v2a = sh(vmc, 1, 1) + sh(vmc, 0, 1)
+    f1 = 0.5 * ul * (u2a + u1a) / pa
+    f2 = 0.5 * ul * (v2a + v1a) / pa
+    c, w, e, s_, n = xt, sh(xt, -1, 0), sh(xt, 1, 0), sh(xt, 0, -1), sh(xt, 0, 1)
+    fx1 = (1.0 + f1) * w + (1.0 - f1) * c
+    fx2 = (1.0 + f1) * c + (1.0 - f1) * e
+    fy1 = (1.0 + f2) * s_ + (1.0 - f2) * c
+    fy2 = (1.0 + f2) * c + (1.0 - f2) * n
+    xmsf = 1.0 / (msfx * msfx * (4.0 * dx))
+    fg = -xmsf * (u2a * fx2 - u1a * fx1 + v2a * fy2 - v1a * fy1)
+    for (p_, m_) in ((n, s_), (e, w)):
+        big = np.abs(p_ + m_ - 2.0 * c) / pa > rc.t_extrema
+        fg = np.where(big & (c > p_) & (c > m_), np.minimum(fg, 0.0), fg)
+        fg = np.where(big & (c < p_) & (c < m_), np.maximum(fg, 0.0), fg)
+    tdyn = 0.0 + fg
+    # vadv3d ind 1 (idynamic = 1) on mkslice's b-level pressures
+    pbh = (hsig[:, None, None] * pb + rc.ptop) * 1000.0
+    pbf = (sig[:, None, None] * pb + rc.ptop) * 1000.0
+    for k in range(2, kz + 1):
+        dq = qdot[k - 1] * (twt1[k] * t1[k - 1] * (pbf[k - 1] / pbh[k - 1]) ** c287 +
+                            twt2[k] * t1[k - 2] * (pbf[k - 1] / pbh[k - 2]) ** c287)
+        tdyn[k - 2] = tdyn[k - 2] - dq * (1.0 / dsig[k - 2])
+        tdyn[k - 1] = tdyn[k - 1] + dq * (1.0 / dsig[k - 1])
+    nsp = rc.nspgx
+    J = np.arange(nsp + 1, rc.jx - nsp)
+    I = np.arange(nsp + 1, rc.iy - nsp)
+    sl = (slice(None), (I - 1)[:, None], (J - 1)[None, :])
+    # omega (dummy = 1/(dx8 msfx), dx8 = 8 dx, Main/mod_params.F90:1766) and the adiabatic term
+    dummy = 1.0 / (8.0 * dx * msfx)
+    om = np.zeros_like(t1)
+    for k in range(kz):
+        om[k] = (0.5 * (qdot[k + 1] + qdot[k]) * pa + hsig[k] * (
+            pten + ((ud[k] + sh(ud, 0, 1)[k] + sh(ud, 1, 1)[k] + sh(ud, 1, 0)[k]) * (sh(pa, 1, 0) - sh(pa, -1, 0)) +
+                    (vd[k] + sh(vd, 0, 1)[k] + sh(vd, 1, 1)[k] + sh(vd, 1, 0)[k]) * (sh(pa, 0, 1) - sh(pa, 0, -1))) *
+            dummy))
+    rovcpm = rgas / (cpd * (1.0 + 0.80 * xq))
+    tdyn = tdyn + (om * rovcpm * tv) / (rc.ptop * rpsa + hsig[:, None, None])
+    np.seterr(**old_err)
+    want = tdyn[sl]
+    got = tten[sl]
+    assert np.abs(want).max() > 1e-8
+    np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max())
+
+
 @pytest.mark.parametrize("nthreads", [2, 4, 6])
 def test_oracle_threads_match_single_tile(c1_data, nthreads):
     """The all-cores CPU baseline (oracle/orc_par.c: set_nproc tiles on OpenMP threads with
