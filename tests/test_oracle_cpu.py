@@ -631,7 +631,7 @@ def test_nh_wind_tendency_matches_numpy_restatement():
 
 
 def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
-    """The hydrostatic t tendency of the first step against an independent NumPy restatement
+    """The hydrostatic t and qv tendencies of the first step against an independent NumPy restatement
     of the reference (C1 with no diffusion, points off the relaxation band): compute_omega's
     cr, pten and the qdot scan and omega (Main/mod_tendency.F90:1118-1215), hadvt of atmx%t in
     the upstream form with the t_extrema limiter (Main/mod_advection.F90:311-393; upstream_mode
@@ -639,7 +639,7 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     of atm1%t with the (pf/pb)**c287 interpolation on mkslice's b-level pressures
     (:767-779, Main/mod_slice.F90:233-239) and the adiabatic term
     omega*rgas/cpmf(qv)*tv/(ptop/p* + hsigma) (Main/mod_tendency.F90:1565-1575; cpmf =
-    cpd*(1 + 0.8 qv), Share/cpmf.inc)."""
+    cpd*(1 + 0.8 qv), Share/cpmf.inc); qv = hadvqv + vadvqv as in the NH check."""
     import dataclasses
     from oracle.oracle import OracleCore
     from regcm_amd import constants as C
@@ -650,7 +650,7 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     o.bdyval()
     g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "PSB", "MSFX", "MSFD")}
     o.tend()
-    tten = o.get("TTEN")
+    tten, qvten = o.get("TTEN"), o.get("QVTEN")
     o.close()
     kz = rc.kz
     sig = rc.sigma
@@ -735,11 +735,30 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
             dummy))
     rovcpm = rgas / (cpd * (1.0 + 0.80 * xq))
     tdyn = tdyn + (om * rovcpm * tv) / (rc.ptop * rpsa + hsig[:, None, None])
+    # qv: hadvqv of atmx%qx (q_rel_extrema limiter) + vadvqv of atm1%qx (qcon power form)
+    c, w, e, s_, n = xq, sh(xq, -1, 0), sh(xq, 1, 0), sh(xq, 0, -1), sh(xq, 0, 1)
+    fx1 = (1.0 + f1) * w + (1.0 - f1) * c
+    fx2 = (1.0 + f1) * c + (1.0 - f1) * e
+    fy1 = (1.0 + f2) * s_ + (1.0 - f2) * c
+    fy2 = (1.0 + f2) * c + (1.0 - f2) * n
+    fq = -xmsf * (u2a * fx2 - u1a * fx1 + v2a * fy2 - v1a * fy1)
+    den = np.maximum(c, 1.0e-20)
+    for (p_, m_) in ((n, s_), (e, w)):
+        big = np.abs(p_ + m_ - 2.0 * c) / den > rc.q_rel_extrema
+        fq = np.where(big & (c > p_) & (c > m_), np.minimum(fq, 0.0), fq)
+        fq = np.where(big & (c < p_) & (c < m_), np.maximum(fq, 0.0), fq)
+    qdyn = 0.0 + fq
+    for k in range(2, kz + 1):
+        qcon = (sig[k - 1] - hsig[k - 1]) / (hsig[k - 2] - hsig[k - 1])   # Main/mod_params.F90:2214
+        fk, fkm = q1[k - 1], q1[k - 2]
+        ok = (fk > minqq * pa) & (fkm > minqq * pa)
+        flux = qdot[k - 1] * np.where(ok, fk * (fkm / fk) ** qcon, 0.0)
+        qdyn[k - 2] = qdyn[k - 2] - flux * (1.0 / dsig[k - 2])
+        qdyn[k - 1] = qdyn[k - 1] + flux * (1.0 / dsig[k - 1])
     np.seterr(**old_err)
-    want = tdyn[sl]
-    got = tten[sl]
-    assert np.abs(want).max() > 1e-8
-    np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max())
+    for name, want, got in (("t", tdyn[sl], tten[sl]), ("qv", qdyn[sl], qvten[sl])):
+        assert np.abs(want).max() > 0.0
+        np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
 
 
 @pytest.mark.parametrize("nthreads", [2, 4, 6])
