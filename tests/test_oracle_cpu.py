@@ -630,6 +630,58 @@ def test_nh_wind_tendency_matches_numpy_restatement():
         np.testing.assert_allclose(got, want, rtol=1e-11, atol=1e-12 * np.abs(want).max(), err_msg=name)
 
 
+def _cross_band(rc):
+    """{(j, i): ibnd} of the cross-point relaxation band, restating setup_boundaries
+    (Main/mod_atm_interface.F90:383-512) for a domain that is neither a channel (bandflag) nor
+    a CRM: the south/north rows, then the west/east columns, with the corner rules."""
+    jx, iy, nsp = rc.jx, rc.iy, rc.nspgx
+    icx = icy = 1
+    igbb1, igbb2, jgbl1, jgbl2 = 2, nsp - 1, 2, nsp - 1
+    igbt1, igbt2 = iy - icy - nsp + 2, iy - icy - 1
+    jgbr1, jgbr2 = jx - icx - nsp + 2, jx - icx - 1
+    ib = {}
+    for i in range(1, iy + 1):                                   # south
+        if igbb1 <= i <= igbb2:
+            for j in range(1, jx + 1):
+                if jgbl1 <= j <= jgbr2:
+                    if j <= jgbl2 and i >= j:
+                        continue
+                    if j >= jgbr1 and i >= (jgbr2 - j + 2):
+                        continue
+                    ib[(j, i)] = i - igbb1 + 2
+    for i in range(1, iy + 1):                                   # north
+        if igbt1 <= i <= igbt2:
+            for j in range(1, jx + 1):
+                if jgbl1 <= j <= jgbr2:
+                    if j <= jgbl2 and (igbt2 - i + 2) >= j:
+                        continue
+                    if j >= jgbr1 and (igbt2 - i) >= (jgbr2 - j):
+                        continue
+                    ib[(j, i)] = igbt2 - i + 2
+    for i in range(1, iy + 1):                                   # west
+        if i < igbb1 or i > igbt2:
+            continue
+        for j in range(1, jx + 1):
+            if jgbl1 <= j <= jgbl2:
+                if i < igbb2 and j > i:
+                    continue
+                if i > igbt1 and j > (igbt2 - i + 2):
+                    continue
+                ib[(j, i)] = j - jgbl1 + 2
+    for i in range(1, iy + 1):                                   # east
+        if i < igbb1 or i > igbt2:
+            continue
+        for j in range(1, jx + 1):
+            if jgbr1 <= j <= jgbr2:
+                if i < igbb2 and (jgbr2 - j + 2) > i:
+                    continue
+                if i > igbt1 and (jgbr2 - j) > (igbt2 - i):
+                    continue
+                ib[(j, i)] = jgbr2 - j + 2
+    # the nudging loops run over the interior cross points only (jci, ici)
+    return {(j, i): n for (j, i), n in ib.items() if 2 <= j <= jx - 2 and 2 <= i <= iy - 2}
+
+
 def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     """The hydrostatic t and qv tendencies of the first step against an independent NumPy restatement
     of the reference (C1 with no diffusion, points off the relaxation band): compute_omega's
@@ -648,7 +700,9 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     o = OracleCore(rc, data["split"])
     o.put_state(data["state"])
     o.bdyval()
-    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "PSB", "MSFX", "MSFD")}
+    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "PSB", "MSFX", "MSFD",
+                                "ATM2_T", "XTB_B0", "XTB_BT")}
+    _, dt0, xbc = o.get_time()
     o.tend()
     tten, qvten = o.get("TTEN"), o.get("QVTEN")
     o.close()
@@ -756,6 +810,23 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
         qdyn[k - 2] = qdyn[k - 2] - flux * (1.0 / dsig[k - 2])
         qdyn[k - 1] = qdyn[k - 1] + flux * (1.0 / dsig[k - 1])
     np.seterr(**old_err)
+    # the band: relaxation of t toward the boundary data (iboudy = 5), at every interior point
+    band = _cross_band(rc)
+    fnudge, gnudge = 0.1 / rc.dt, 1.0 / (rc.dt * 50.0)           # Main/mod_bdycod.F90:204-215
+    anudge = np.where(hsig < 0.4, rc.high_nudge, np.where(hsig < 0.8, rc.medium_nudge, rc.low_nudge))
+    fg = (g["XTB_B0"] + (xbc + dt0) * g["XTB_BT"]) - g["ATM2_T"]  # nudge3d, :4242-4245
+    relax = np.zeros_like(tdyn)
+    lap = sh(fg, -1, 0) + sh(fg, 1, 0) + sh(fg, 0, -1) + sh(fg, 0, 1) - 4.0 * fg
+    for (jj, ii), ib in band.items():
+        xfun = np.exp(-((ib - 2) / anudge))                      # hefc, hegc (:258-267)
+        relax[:, ii - 1, jj - 1] = (fnudge * xfun) * fg[:, ii - 1, jj - 1] - (gnudge * xfun) * lap[:, ii - 1, jj - 1]
+    tall = tdyn + relax
+    Jc = np.arange(2, rc.jx - 1)
+    Ic = np.arange(2, rc.iy - 1)
+    sc = (slice(None), (Ic - 1)[:, None], (Jc - 1)[None, :])
+    assert len(band) > 0
+    np.testing.assert_allclose(tten[sc], tall[sc], rtol=1e-10, atol=1e-11 * np.abs(tall[sc]).max(),
+                               err_msg="t with the band")
     for name, want, got in (("t", tdyn[sl], tten[sl]), ("qv", qdyn[sl], qvten[sl])):
         assert np.abs(want).max() > 0.0
         np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
