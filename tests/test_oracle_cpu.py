@@ -683,7 +683,7 @@ def _cross_band(rc):
 
 
 def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
-    """The hydrostatic t and qv tendencies of the first step against an independent NumPy restatement
+    """The hydrostatic t, qv and qc tendencies of the first step against an independent NumPy restatement
     of the reference (C1 with no diffusion, points off the relaxation band): compute_omega's
     cr, pten and the qdot scan and omega (Main/mod_tendency.F90:1118-1215), hadvt of atmx%t in
     the upstream form with the t_extrema limiter (Main/mod_advection.F90:311-393; upstream_mode
@@ -691,20 +691,26 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     of atm1%t with the (pf/pb)**c287 interpolation on mkslice's b-level pressures
     (:767-779, Main/mod_slice.F90:233-239) and the adiabatic term
     omega*rgas/cpmf(qv)*tv/(ptop/p* + hsigma) (Main/mod_tendency.F90:1565-1575; cpmf =
-    cpd*(1 + 0.8 qv), Share/cpmf.inc); qv = hadvqv + vadvqv as in the NH check."""
+    cpd*(1 + 0.8 qv), Share/cpmf.inc); qv = hadvqv + vadvqv and qc = hadvqx + vadv4d ind 1
+    (on a cloud layer) as in the NH check."""
     import dataclasses
     from oracle.oracle import OracleCore
     from regcm_amd import constants as C
     rc = dataclasses.replace(CONFIGS["C1"], ckh=0.0, adyndif=0.0)
     data = icbc.generate(rc)
     o = OracleCore(rc, data["split"])
-    o.put_state(data["state"])
+    state = dict(data["state"])
+    for a1, a2 in (("ATM1_QC", "ATM1_QV"), ("ATM2_QC", "ATM2_QV")):   # a cloud layer for the qc check
+        qc = np.zeros_like(state[a2])
+        qc[3:12] = 0.01 * state[a2][3:12]
+        state[a1] = qc
+    o.put_state(state)
     o.bdyval()
-    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "PSB", "MSFX", "MSFD",
-                                "ATM2_T", "XTB_B0", "XTB_BT")}
+    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "PSA", "PSB", "MSFX",
+                                "MSFD", "ATM2_T", "XTB_B0", "XTB_BT")}
     _, dt0, xbc = o.get_time()
     o.tend()
-    tten, qvten = o.get("TTEN"), o.get("QVTEN")
+    tten, qvten, qcten = o.get("TTEN"), o.get("QVTEN"), o.get("QCTEN")
     o.close()
     kz = rc.kz
     sig = rc.sigma
@@ -809,6 +815,22 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
         flux = qdot[k - 1] * np.where(ok, fk * (fkm / fk) ** qcon, 0.0)
         qdyn[k - 2] = qdyn[k - 2] - flux * (1.0 / dsig[k - 2])
         qdyn[k - 1] = qdyn[k - 1] + flux * (1.0 / dsig[k - 1])
+    # qc: hadvqx of atmx%qc + vadv4d ind 1 of atm1%qc (no relaxation of qc: every interior point)
+    qc1 = g["ATM1_QC"]
+    xc = np.maximum(qc1 * rpsa, 0.0)
+    c, w, e, s_, n = xc, sh(xc, -1, 0), sh(xc, 1, 0), sh(xc, 0, -1), sh(xc, 0, 1)
+    fx1 = (1.0 + f1) * w + (1.0 - f1) * c
+    fx2 = (1.0 + f1) * c + (1.0 - f1) * e
+    fy1 = (1.0 + f2) * s_ + (1.0 - f2) * c
+    fy2 = (1.0 + f2) * c + (1.0 - f2) * n
+    cdyn = 0.0 - xmsf * (u2a * fx2 - u1a * fx1 + v2a * fy2 - v1a * fy1)
+    for k in range(2, kz + 1):
+        fk, fkm, svv = qc1[k - 1], qc1[k - 2], qdot[k - 1]
+        thr = minqq * minqq * pa
+        ok = np.where(svv > 0.0, fkm > thr, fk > thr)
+        flux = np.where(ok, svv * (twt1[k] * fk + twt2[k] * fkm), 0.0)
+        cdyn[k - 2] = cdyn[k - 2] - flux * (1.0 / dsig[k - 2])
+        cdyn[k - 1] = cdyn[k - 1] + flux * (1.0 / dsig[k - 1])
     np.seterr(**old_err)
     # the band: relaxation of t toward the boundary data (iboudy = 5), at every interior point
     band = _cross_band(rc)
@@ -827,6 +849,9 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
     assert len(band) > 0
     np.testing.assert_allclose(tten[sc], tall[sc], rtol=1e-10, atol=1e-11 * np.abs(tall[sc]).max(),
                                err_msg="t with the band")
+    assert np.abs(cdyn[sc]).max() > 0.0
+    np.testing.assert_allclose(qcten[sc], cdyn[sc], rtol=1e-10, atol=1e-11 * np.abs(cdyn[sc]).max(),
+                               err_msg="qc")
     for name, want, got in (("t", tdyn[sl], tten[sl]), ("qv", qdyn[sl], qvten[sl])):
         assert np.abs(want).max() > 0.0
         np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
