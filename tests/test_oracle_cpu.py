@@ -857,6 +857,126 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
         np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
 
 
+def test_hydrostatic_wind_tendency_matches_numpy_restatement():
+    """The hydrostatic u, v tendencies of the first step against an independent NumPy
+    restatement of the reference (C1, no diffusion, dot points off the band): hadvuv's
+    hydrostatic upstream branch (Main/mod_advection.F90:203-233), vadvuv of atmx%uc, vc
+    (:271-303), the Coriolis term (Main/mod_tendency.F90:1830-1838) and the pressure-gradient
+    force with ipgf = 0 (:1886-2119): the log-p* term with rtbar from atmx%tv, the geopotential
+    of the hydrostatic column integral (td = atm1%t (1 + ep1 qv) since alpha_hyd = 0,
+    Share/mod_constants.F90:319-320; tvfac = 1/(1 + qc/(1 + qv))) and its gradient."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    from regcm_amd import constants as C
+    rc = dataclasses.replace(CONFIGS["C1"], ckh=0.0, adyndif=0.0)
+    assert rc.ipgf == 0
+    data = icbc.generate(rc)
+    o = OracleCore(rc, data["split"])
+    o.put_state(data["state"])
+    o.bdyval()
+    g = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "PSA", "MSFX", "MSFD",
+                                "CORIOL", "HT")}
+    o.tend()
+    uten, vten = o.get("UTEN"), o.get("VTEN")
+    o.close()
+    kz = rc.kz
+    sig = rc.sigma
+    hsig = (sig[1:] + sig[:-1]) * 0.5
+    dsig = sig[1:] - sig[:-1]
+    twt1 = np.zeros(kz + 1); twt2 = np.zeros(kz + 1)
+    for k in range(2, kz + 1):
+        twt1[k] = (sig[k - 1] - hsig[k - 2]) / (hsig[k - 1] - hsig[k - 2])
+        twt2[k] = 1.0 - twt1[k]
+    dx = rc.ds * 1000.0
+    ul = rc.uoffc * 0.5 * rc.dt / dx
+    rgas = C.rgas
+    ep1 = 28.96454 / 18.01528 - 1.0
+    minqq = 1.0e-8
+    ptop = rc.ptop
+
+    def sh(a, dj, di):                                           # sh(a)[k, i, j] = a[k, i+di, j+dj]
+        return np.roll(a, shift=(-di, -dj), axis=(-2, -1))
+
+    old_err = np.seterr(divide="ignore", invalid="ignore")      # frame edges: never compared
+    u1, v1, t1 = g["ATM1_U"], g["ATM1_V"], g["ATM1_T"]
+    pa, msfx, msfd = g["PSA"][0], g["MSFX"][0], g["MSFD"][0]
+    psd = np.zeros_like(pa)
+    psd[1:, 1:] = (pa[1:, 1:] + pa[:-1, 1:] + pa[1:, :-1] + pa[:-1, :-1]) * 0.25
+    rpsd = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0)
+    rpsa = np.divide(1.0, pa, out=np.zeros_like(pa), where=pa > 0)
+    umc, vmc = u1 * msfd, v1 * msfd
+    ud, vd = u1 * rpsd, v1 * rpsd
+    # compute_omega's qdot (hydrostatic scan) for vadvuv
+    cr = ((sh(umc, 1, 1) + sh(umc, 1, 0) - sh(umc, 0, 1) - umc) +
+          (sh(vmc, 1, 1) + sh(vmc, 0, 1) - sh(vmc, 1, 0) - vmc)) / (2.0 * dx * msfx * msfx)
+    pten = np.zeros_like(pa)
+    for k in range(kz):
+        pten = pten - cr[k] * dsig[k]
+    qdot = np.zeros((kz + 1,) + pa.shape)
+    for k in range(2, kz + 1):
+        qdot[k - 1] = qdot[k - 2] - (pten + cr[k - 2]) * dsig[k - 2] * rpsa
+    # hadvuv, hydrostatic upstream branch
+    ucmona = sh(umc, 0, 1) + 2.0 * umc + sh(umc, 0, -1)
+    ucmonb = sh(umc, 1, 1) + 2.0 * sh(umc, 1, 0) + sh(umc, 1, -1)
+    ucmonc = sh(umc, -1, 1) + 2.0 * sh(umc, -1, 0) + sh(umc, -1, -1)
+    vcmona = sh(vmc, 1, 0) + 2.0 * vmc + sh(vmc, -1, 0)
+    vcmonb = sh(vmc, 1, 1) + 2.0 * sh(vmc, 0, 1) + sh(vmc, -1, 1)
+    vcmonc = sh(vmc, 1, -1) + 2.0 * sh(vmc, 0, -1) + sh(vmc, -1, -1)
+    ff1, ff2 = ul * (sh(ud, 1, 0) + ud), ul * (sh(ud, -1, 0) + ud)
+    ff3, ff4 = ul * (sh(vd, 0, 1) + vd), ul * (sh(vd, 0, -1) + vd)
+    ucb = (1.0 + ff1) * ucmona + (1.0 - ff1) * ucmonb
+    ucc_ = (1.0 + ff2) * ucmonc + (1.0 - ff2) * ucmona
+    vcb = (1.0 + ff3) * vcmona + (1.0 - ff3) * vcmonb
+    vcc_ = (1.0 + ff4) * vcmonc + (1.0 - ff4) * vcmona
+    dm = 1.0 / (msfd * msfd * 16.0 * dx)
+    udyn = -dm * ((sh(ud, 1, 0) + ud) * ucb - (ud + sh(ud, -1, 0)) * ucc_ +
+                  (sh(ud, 0, 1) + ud) * vcb - (ud + sh(ud, 0, -1)) * vcc_)
+    vdyn = -dm * ((sh(vd, 1, 0) + vd) * ucb - (vd + sh(vd, -1, 0)) * ucc_ +
+                  (sh(vd, 0, 1) + vd) * vcb - (vd + sh(vd, 0, -1)) * vcc_)
+    for k in range(2, kz + 1):                                   # vadvuv of atm1 u, v
+        qq = 0.25 * (qdot[k - 1] + sh(qdot, 0, -1)[k - 1] + sh(qdot, -1, 0)[k - 1] + sh(qdot, -1, -1)[k - 1])
+        uu = qq * (twt1[k] * u1[k - 1] + twt2[k] * u1[k - 2])
+        vv = qq * (twt1[k] * v1[k - 1] + twt2[k] * v1[k - 2])
+        udyn[k - 2] = udyn[k - 2] - uu / dsig[k - 2]
+        udyn[k - 1] = udyn[k - 1] + uu / dsig[k - 1]
+        vdyn[k - 2] = vdyn[k - 2] - vv / dsig[k - 2]
+        vdyn[k - 1] = vdyn[k - 1] + vv / dsig[k - 1]
+    cor = g["CORIOL"][0]                                         # Coriolis
+    udyn = udyn + cor * v1
+    vdyn = vdyn - cor * u1
+    # pressure-gradient force, ipgf = 0: the log-p* part
+    xq = np.maximum(g["ATM1_QV"] * rpsa, minqq)
+    xc = np.maximum(g["ATM1_QC"] * rpsa, 0.0)
+    tv = (t1 * rpsa) * (1.0 + ep1 * xq)
+    rtbar = 0.25 * (sh(tv, -1, -1) + sh(tv, -1, 0) + sh(tv, 0, -1) + tv)
+    rtbar = rgas * rtbar * psd
+    h = hsig[:, None, None]
+    udyn = udyn - rtbar * (np.log(0.5 * (pa + sh(pa, 0, -1)) * h + ptop) -
+                           np.log(0.5 * (sh(pa, -1, 0) + sh(pa, -1, -1)) * h + ptop)) / (dx * msfd)
+    vdyn = vdyn - rtbar * (np.log(0.5 * (pa + sh(pa, -1, 0)) * h + ptop) -
+                           np.log(0.5 * (sh(pa, -1, -1) + sh(pa, 0, -1)) * h + ptop)) / (dx * msfd)
+    # geopotential (half levels, cross points) and its gradient
+    td = t1 * (1.0 + ep1 * xq)
+    tvfac = 1.0 / (1.0 + xc / (1.0 + xq))
+    phi = np.zeros_like(t1)
+    phi[kz - 1] = g["HT"][0] - rgas * (td[kz - 1] * rpsa * tvfac[kz - 1]) * np.log(
+        (hsig[kz - 1] + ptop * rpsa) / (1.0 + ptop * rpsa))
+    for lev in range(kz - 1, 0, -1):                             # 1-based lev = kz-1 .. 1
+        tvavg = ((td[lev - 1] * dsig[lev - 1] + td[lev] * dsig[lev]) /
+                 (pa * (dsig[lev - 1] + dsig[lev]))) * tvfac[lev - 1]
+        phi[lev - 1] = phi[lev] - rgas * tvavg * np.log((hsig[lev - 1] + ptop * rpsa) / (hsig[lev] + ptop * rpsa))
+    udyn = udyn - psd * (phi + sh(phi, 0, -1) - sh(phi, -1, 0) - sh(phi, -1, -1)) / (2.0 * dx * msfd)
+    vdyn = vdyn - psd * (phi + sh(phi, -1, 0) - sh(phi, 0, -1) - sh(phi, -1, -1)) / (2.0 * dx * msfd)
+    np.seterr(**old_err)
+    nsp = rc.nspgx
+    J = np.arange(nsp + 2, rc.jx - nsp)                          # dot points off the band
+    I = np.arange(nsp + 2, rc.iy - nsp)
+    sl = (slice(None), (I - 1)[:, None], (J - 1)[None, :])
+    for name, want, got in (("u", udyn[sl], uten[sl]), ("v", vdyn[sl], vten[sl])):
+        assert np.abs(want).max() > 0.0
+        np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
+
+
 @pytest.mark.parametrize("nthreads", [2, 4, 6])
 def test_oracle_threads_match_single_tile(c1_data, nthreads):
     """The all-cores CPU baseline (oracle/orc_par.c: set_nproc tiles on OpenMP threads with
