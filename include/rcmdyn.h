@@ -202,6 +202,12 @@ int rcmdyn_put(rcmdyn_t* h, int32_t field, const double* src,
                int32_t j1, int32_t j2, int32_t i1, int32_t i2, int32_t k1, int32_t k2);
 int rcmdyn_get(rcmdyn_t* h, int32_t field, double* dst,
                int32_t j1, int32_t j2, int32_t i1, int32_t i2, int32_t k1, int32_t k2);
+/* Step failures (CFL VIOLATION, SLADVECTION) are detected on the device.  rcmdyn_step and
+ * rcmdyn_tend report a failed step at most 2 steps late (one-rank jobs) or one reduction
+ * interval (8 steps) late (RCCL jobs), so they never wait for the stream per step;
+ * rcmdyn_get and rcmdyn_diagnostics wait for the stream and report any failure of the steps
+ * issued so far before copying anything (with RCCL: the job-wide words already reduced and
+ * this rank's own flags; no collective is issued, so a rank may call them alone). */
 
 /* rcm_timer state: lcount (steps done), dt (current leapfrog dt, s), xbctime (s since
  * the current boundary interval started). */
@@ -226,6 +232,10 @@ int rcmdyn_bdyval(rcmdyn_t* h);                /* one mod_bdycod::bdyval */
  * one dtbdys later. */
 int rcmdyn_bdyin(rcmdyn_t* h);
 int rcmdyn_step(rcmdyn_t* h, int32_t nsteps);  /* nsteps x (tend + bdyval), graph-replayed */
+/* Waits for the device and reports a failure of any step issued so far.  In RCCL mode it is
+ * COLLECTIVE (it max-reduces the step error flags over the job so that every rank stops at
+ * the same call): every rank must call it, as every rank calls rcmdyn_step and
+ * rcmdyn_reductions. */
 int rcmdyn_synchronize(rcmdyn_t* h);
 
 /* Diagnostics of the last tend: out[0]=ptntot, out[1]=pt2tot (Bleck noise sums of the

@@ -153,6 +153,7 @@ class RunConfig:
     nspgx: Optional[int] = None
     nspgd: Optional[int] = None
     diffu_hgtf: int = 1
+    upstream_mode: int = 1           # dynparam; .false. (centred advection) is refused
     gnu1: float = 0.0625
     gnu2: float = 0.0625
     uoffc: float = 0.25
@@ -241,7 +242,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.iboudy, c.idiffu, c.ipgf, c.nsplit = rc.iboudy, rc.idiffu, rc.ipgf, rc.nsplit
     c.nspgx, c.nspgd = rc.nspgx, rc.nspgd
     c.diffu_hgtf = rc.diffu_hgtf
-    c.upstream_mode = 1
+    c.upstream_mode = rc.upstream_mode
     c.stability_enhance = 1
     c.present_qc = rc.present_qc
     c.ds, c.dtsec, c.ptop = rc.ds, rc.dt, rc.ptop

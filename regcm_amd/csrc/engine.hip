@@ -177,16 +177,16 @@ struct KernelProf {
   }
   hipEvent_t begin(hipStream_t s) {
     hipEvent_t e = get();
-    hipEventRecord(e, s);
+    (void)hipEventRecord(e, s);
     return e;
   }
   void end(hipStream_t s, const char* name, hipEvent_t e0) {
     hipEvent_t e1 = get();
-    hipEventRecord(e1, s);
+    (void)hipEventRecord(e1, s);
     rec.push_back({name, {e0, e1}});
   }
   ~KernelProf() {
-    for (hipEvent_t e : pool) hipEventDestroy(e);
+    for (hipEvent_t e : pool) (void)hipEventDestroy(e);
   }
 };
 
@@ -549,6 +549,12 @@ struct rcmdyn_engine {
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
+    // dynparam's upstream_mode (default .true., Main/mod_params.F90:646): the centred
+    // advection branches (Main/mod_advection.F90:141,322,409,532,624,682) are not built
+    if (cfg.upstream_mode != 1)
+      throw std::runtime_error("rcmdyn: upstream_mode = .false. (centred advection) is not supported");
+    if (cfg.stability_enhance != 0 && cfg.stability_enhance != 1)
+      throw std::runtime_error("rcmdyn: stability_enhance must be 0 or 1");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");
     if (cfg.nsplit < 1 || cfg.nsplit > MAXSPLIT) throw std::runtime_error("rcmdyn: nsplit out of range");
     if (cfg.nspgx >= MAXNSP || cfg.nspgd != cfg.nspgx) throw std::runtime_error("rcmdyn: nspgx/nspgd unsupported");
@@ -613,23 +619,23 @@ struct rcmdyn_engine {
     if (hgerr) (void)hipHostFree(hgerr);
     if (derr) (void)hipFree(derr);
     for (auto& t : tiles)
-      for (void* p : t.allocs) hipFree(p);
+      for (void* p : t.allocs) (void)hipFree(p);
     tiles.clear();
     comm.reset();
-    if (dc) hipFree(dc);
-    if (ds) hipFree(ds);
-    if (red) hipFree(red);
+    if (dc) (void)hipFree(dc);
+    if (ds) (void)hipFree(ds);
+    if (red) (void)hipFree(red);
 
     if (evfork) (void)hipEventDestroy(evfork);
     if (evjoin) (void)hipEventDestroy(evjoin);
     if (stream2) (void)hipStreamDestroy(stream2);
-    if (stream) hipStreamDestroy(stream);
+    if (stream) (void)hipStreamDestroy(stream);
   }
 
   void invalidate_graphs() {
     for (hipGraphExec_t* g : {gexec, gtend, gbdy})
       for (int p = 0; p < 2; p++)
-        if (g[p]) { hipGraphExecDestroy(g[p]); g[p] = nullptr; }
+        if (g[p]) { (void)hipGraphExecDestroy(g[p]); g[p] = nullptr; }
   }
 
   // ------------------------------------------------------------------ step error flags
@@ -690,6 +696,19 @@ struct rcmdyn_engine {
       const int sl = f->slflag, nan = f->nanflag;
       if (sl || nan) fail(sl, lc, "step ");
     }
+  }
+  // at a host read point (get, diagnostics) with the stream idle: every step issued so far is
+  // checked, so no field of a failed run leaves the engine (the reference's fatal stops before
+  // any output).  With a communicator the reductions already issued are drained (no new
+  // collective: a get need not be called by every rank) and this rank's own sticky flags are
+  // read as well; a rank-local failure is reported to its host, which aborts the job as the
+  // reference's fatal does (Main/abort.F90:20-36).
+  void check_now() {
+    check(0);
+    if (!comm) return;
+    StepState st;
+    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+    if (st.nanflag || st.slflag) fail(st.slflag, hs.lcount, "this rank, by step ");
   }
 
 
@@ -975,6 +994,7 @@ struct rcmdyn_engine {
       throw std::runtime_error("rcmdyn_get: TKE fields need ibltyp=2 (UW PBL)");
     if (f == RCMDYN_TKEPHY && !tiles[0].tkephy) throw std::runtime_error("rcmdyn_get: no TKE tendency was put");
     HIPCHK(hipStreamSynchronize(stream));
+    check_now();
     const long nj = j2 - j1 + 1, ni = i2 - i1 + 1;
     for (auto& t : tiles) {
       int nk;
@@ -1380,7 +1400,6 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
-      const Grids q = grids(g);
       // init_tendencies (:1227-1240): the zero is the leading summand of each tendency's first
       // writer (k_nh_uv_adv, k_nh_scalar_adv, the iboudy = 4 sponges, k_nh_forecast), which
       // covers every point a later kernel reads.  With diagnostics on, the total tendencies
@@ -1719,8 +1738,8 @@ struct rcmdyn_engine {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     last_ms = n > 0 ? (double)ms / n : 0.0;
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
     check(0);
   }
 
@@ -1838,6 +1857,7 @@ struct rcmdyn_engine {
 
   void diagnostics(double out[4]) {
     HIPCHK(hipStreamSynchronize(stream));
+    check_now();
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
     out[0] = st.ptntot; out[1] = st.pt2tot; out[2] = std::isnan(st.ptntot) ? 1.0 : 0.0; out[3] = st.nanflag;

@@ -1757,10 +1757,20 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
     __syncthreads();
   }
   if (!do_qc) return;
-  // the west/east pass reads interior columns jci1/jci2 (including the rows ice1/ice2 the
-  // south/north pass rewrites) before that pass; the south/north pass reads the interior rows
-  // ici1/ici2, which the west/east pass never writes: every read of both passes is issued first,
-  // then (after the block barrier) every write
+  // The west/east pass reads the interior columns jci1/jci2 on rows ice1..ice2 before the
+  // south/north pass rewrites rows ice1/ice2 on jci1..jci2: the two passes share exactly the
+  // four points (jci1|jci2, ice1|ice2), which are read here before any write.  Otherwise the
+  // passes are independent (west/east writes columns jce1/jce2, which south/north never reads;
+  // south/north reads rows ici1/ici2, which nothing writes), so every chunk of the loop below
+  // may write as soon as it has read, whatever the tile's extent.
+  const double c11 = F3(a1qc, g.jci1, g.ice1, k), c12 = F3(a1qc, g.jci1, g.ice2, k);
+  const double c21 = F3(a1qc, g.jci2, g.ice1, k), c22 = F3(a1qc, g.jci2, g.ice2, k);
+  __syncthreads();
+  auto qcw = [&](int jc, int i) {
+    if (i == g.ice1) return jc == g.jci1 ? c11 : c21;
+    if (i == g.ice2) return jc == g.jci1 ? c12 : c22;
+    return F3(a1qc, jc, i, k);
+  };
   const int ni = g.ice2 - g.ice1 + 1, nj = g.jci2 - g.jci1 + 1, nx = max(ni, nj);
   for (int base = 0; base < nx; base += (int)blockDim.x) {
     const int x = base + (int)threadIdx.x;
@@ -1769,13 +1779,13 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
     double vw = 0.0, ve = 0.0, vs = 0.0, vn = 0.0;
     bool ow = false, oe = false, os = false, on = false;
     if (wi && g.bl) {
-      const double qxint = F3(a1qc, g.jci1, i, k) / ps(g.jci1, i);
+      const double qxint = qcw(g.jci1, i) / ps(g.jci1, i);
       const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
       vw = (w > d_zero) ? d_zero : qxint * ps(g.jce1, i);
       ow = true;
     }
     if (wi && g.br) {
-      const double qxint = F3(a1qc, g.jci2, i, k) / ps(g.jci2, i);
+      const double qxint = qcw(g.jci2, i) / ps(g.jci2, i);
       const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
       ve = (w < d_zero) ? d_zero : qxint * ps(g.jce2, i);
       oe = true;
@@ -1792,7 +1802,6 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
       vn = (w < d_zero) ? d_zero : qxint * ps(j, g.ice2);
       on = true;
     }
-    __syncthreads();
     if (ow) F3(a1qc, g.jce1, i, k) = vw;
     if (oe) F3(a1qc, g.jce2, i, k) = ve;
     if (os) F3(a1qc, j, g.ice1, k) = vs;

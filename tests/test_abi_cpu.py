@@ -106,6 +106,20 @@ def test_create_without_gpu_fails_loudly():
         dycore.DynCore(rc, data["split"])
 
 
+@pytest.mark.parametrize("opt,msg", [({"upstream_mode": 0}, "upstream_mode"),
+                                     ({"idiffu": 3}, "idiffu"), ({"iboudy": 3}, "iboudy")])
+def test_create_refuses_unbuilt_options(opt, msg):
+    """A drop-in refuses what it does not compute: option values whose reference branches are
+    not built fail rcmdyn_create with the option's name, before any device call (so here too)."""
+    import dataclasses
+    from regcm_amd.config import CONFIGS
+    from regcm_amd import icbc
+    rc = dataclasses.replace(CONFIGS["C1"], **opt)
+    data = icbc.generate(CONFIGS["C1"])
+    with pytest.raises(dycore.EngineError, match=msg):
+        dycore.DynCore(rc, data["split"])
+
+
 def test_field_enum_matches_header_python_fortran():
     """rcmdyn_field order is one contract for C, the Python host and the Fortran shim."""
     from regcm_amd.config import FIELD_NAMES

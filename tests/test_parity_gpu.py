@@ -133,6 +133,25 @@ def test_cfl_violation_stops_within_lag(c1_data):
     e.step(2)                                       # the flag was cleared
 
 
+def test_get_reports_failed_step(c1_data):
+    """rcmdyn_get never hands out fields of a failed run: a step that went NaN inside the
+    2-step report lag of rcmdyn_tend is reported by the next get (the reference's fatal stops
+    before any output, Main/mod_tendency.F90:702)."""
+    from regcm_amd.dycore import DynCore, EngineError
+    rc, data = c1_data
+    st = {k: v.copy() for k, v in data["state"].items()}
+    for name in ("ATM1_T", "ATM2_T"):
+        st[name][5, 20:24, 20:24] = np.nan
+    e = DynCore(rc, data["split"])
+    e.put_state(st)
+    e.bdyval()
+    with pytest.raises(EngineError, match="CFL VIOLATION"):
+        for _ in range(6):
+            e.tend()
+            e.bdyval()
+        e.get("ATM1_T")
+
+
 @pytest.mark.parametrize("nproc", [(2, 1), (2, 2), (1, 3), (1, 7)])
 def test_decomposition_invariance(c1_data, nproc):
     """Tiles exchanging halos reproduce the single-tile result bit-for-bit; tiles
@@ -312,6 +331,35 @@ def test_variant_decomposition(c1_data, variant):
         e.step(6)
     for name in STATE_FIELDS:
         assert np.array_equal(ref.get(name), til.get(name)), name
+
+
+@pytest.mark.parametrize("iy", [300, 560])
+def test_bdyval_qc_tall_tile(iy):
+    """bdyval's qc inflow/outflow on a tile taller than one 256-thread block: the west/east
+    pass must read qc(jci1|jci2, ice1|ice2) before the south/north pass rewrites them
+    (Main/mod_bdycod.F90:2153-2220), whichever chunk of the block loop each lands in.  Random
+    positive qc everywhere, so the corners carry distinct values; bit-exact after bdyval."""
+    import dataclasses
+    rc = dataclasses.replace(CONFIGS["C1"], jx=24, iy=iy, nspgx=None, nspgd=None)
+    data = icbc.generate(rc)
+    st = {k: v.copy() for k, v in data["state"].items()}
+    rng = np.random.default_rng(11)
+    for name in ("ATM1_QC", "ATM2_QC"):
+        st[name] = rng.uniform(1e-6, 1e-4, size=st[name].shape) * st["PSA"][0][None]
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    o, e = OracleCore(rc, data["split"]), DynCore(rc, data["split"])
+    for c in (o, e):
+        c.put_state(st)
+        c.bdyval()
+    for name in STATE_FIELDS:
+        assert np.array_equal(e.get(name)[..., : rc.iy - 1, : rc.jx - 1],
+                              o.get(name)[..., : rc.iy - 1, : rc.jx - 1]), name
+    for c in (o, e):
+        c.step(2)
+    for name in STATE_FIELDS:
+        err = relerr(e.get(name), o.get(name), rc, name)
+        assert err < 1e-11, (name, err)
 
 
 def test_sladvection_departure_check(c1_data):
