@@ -221,6 +221,10 @@ struct rcmdyn_engine {
   std::vector<Tile> tiles;   // tiles owned here
   hipStream_t stream = nullptr;
   hipGraphExec_t gexec[2] = {nullptr, nullptr};   // tend + bdyval, per ping-pong parity
+  hipGraphExec_t gexec2[2] = {nullptr, nullptr};  // two steps (tend + bdyval) x 2, per parity
+  // steps per replayed graph in rcmdyn_step (RCMDYN_GRAPH_STEPS, 1 or 2): two steps per launch
+  // return to the same ping-pong parity and halve the graph launches
+  const int graph_steps = std::getenv("RCMDYN_GRAPH_STEPS") ? std::max(1, std::min(2, std::atoi(std::getenv("RCMDYN_GRAPH_STEPS")))) : 2;
   hipGraphExec_t gtend[2] = {nullptr, nullptr};   // tend alone (the drop-in rcmdyn_tend)
   hipGraphExec_t gbdy[2] = {nullptr, nullptr};    // bdyval alone (rcmdyn_bdyval)
   // step error flags: host-mapped snapshot ring written by the last launch of every tend,
@@ -633,7 +637,7 @@ struct rcmdyn_engine {
   }
 
   void invalidate_graphs() {
-    for (hipGraphExec_t* g : {gexec, gtend, gbdy})
+    for (hipGraphExec_t* g : {gexec, gexec2, gtend, gbdy})
       for (int p = 0; p < 2; p++)
         if (g[p]) { (void)hipGraphExecDestroy(g[p]); g[p] = nullptr; }
   }
@@ -1340,9 +1344,10 @@ struct rcmdyn_engine {
   }
   // alarm_day (Main/mpplib/mod_timer.F90:277-337): active at the start and at the first step
   // whose start time reaches the next multiple of a day
-  bool nh_day_alarm() const {
-    const double tnow = (double)hs.lcount * cfg.dtsec;
-    return hs.lcount == 0 || !nh_tmask_valid ||
+  bool nh_day_alarm() const { return nh_day_alarm_at(hs.lcount); }
+  bool nh_day_alarm_at(long long lc) const {
+    const double tnow = (double)lc * cfg.dtsec;
+    return lc == 0 || !nh_tmask_valid ||
            std::floor(tnow / 86400.0) != std::floor((tnow - cfg.dtsec) / 86400.0);
   }
   bool nh_tmask_valid = false;
@@ -1543,15 +1548,13 @@ struct rcmdyn_engine {
     xchv(pro);
     xch_begin(pro2);
     ghosts_stale = false;
-    // surface_pressures + 2-D reciprocals, :815-834
-    each([&](Tile& t) {
-      KLAUNCH(k_surface_pressures, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, fields(t));
-    });
-    // compute_omega columns, new_pressure, geopotential (calc_coeff is formed where it is
-    // read, in k_momentum and k_scalars)
+    // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
+    // geopotential in one launch (calc_coeff is formed where it is read, in k_momentum and
+    // k_scalars)
     each([&](Tile& t) {
       const Geom& g = t.g;
-      KLAUNCH(k_columns, dim3(t.nred), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx);
+      const int nsp = (int)((g.nj * (long)g.ni + 511) / 512);
+      KLAUNCH(k_columns, dim3(t.nred + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx, t.nred);
     });
     xch_join();
     if (slice) run_slice();
@@ -1701,9 +1704,12 @@ struct rcmdyn_engine {
   // graph replay applies: not profiling, not an RCCL transport that cannot be captured, and
   // for NH not a step of another shape (istep on the first two steps, the day alarm's
   // radiative coefficients)
-  bool graph_ok() const {
+  bool graph_ok(int nsteps = 1) const {
     if (no_graph || prof || (comm && !comm->graph_safe())) return false;
-    return !(cfg.idynamic == 2 && (hs.lcount < 2 || nh_day_alarm()));
+    if (cfg.idynamic != 2) return true;
+    for (int q = 0; q < nsteps; q++)
+      if (hs.lcount + q < 2 || nh_day_alarm_at(hs.lcount + q)) return false;
+    return true;
   }
   // host bookkeeping of a replayed tend / bdyval (what tend() and bdyval() do on the host)
   void replayed_tend() {
@@ -1722,7 +1728,16 @@ struct rcmdyn_engine {
     for (int s = 0; s < n; s++) {
       check(FLAG_LAG);
       const int par = tiles[0].cur;
-      if (graph_ok()) {
+      if (graph_steps == 2 && s + 1 < n && graph_ok(2)) {
+        if (!gexec2[par]) capture(par, 3, 2);
+        HIPCHK(hipGraphLaunch(gexec2[par], stream));
+        replayed_tend();
+        replayed_bdyval();
+        note_step(hs.lcount);
+        replayed_tend();
+        replayed_bdyval();
+        s++;
+      } else if (graph_ok()) {
         if (!gexec[par]) capture(par, 3);
         HIPCHK(hipGraphLaunch(gexec[par], stream));
         replayed_tend();
@@ -1774,16 +1789,18 @@ struct rcmdyn_engine {
 
   // capture tend (what & 1) and/or bdyval (what & 2) for the current ping-pong parity; the
   // host bookkeeping done in tend()/bdyval() is rolled back, the replay redoes it per launch
-  void capture(int par, int what) {
+  void capture(int par, int what, int nsteps = 1) {
     const StepState save = hs;
     std::vector<int> curs;
     for (auto& t : tiles) curs.push_back(t.cur);
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    if (what & 1) tend();
-    if (what & 2) bdyval();
+    for (int q = 0; q < nsteps; q++) {
+      if (what & 1) tend();
+      if (what & 2) bdyval();
+    }
     HIPCHK(hipStreamEndCapture(stream, &graph));
-    hipGraphExec_t& x = what == 3 ? gexec[par] : what == 1 ? gtend[par] : gbdy[par];
+    hipGraphExec_t& x = nsteps == 2 ? gexec2[par] : what == 3 ? gexec[par] : what == 1 ? gtend[par] : gbdy[par];
     HIPCHK(hipGraphInstantiate(&x, graph, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(graph));
     hs = save;

@@ -77,12 +77,23 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  terms (mass divergence, td, tvfac, the log ratios of the hypsometric equation) into LDS,
 //  then wavefront 0 runs the pten sum / qdot scan / new_pressure and wavefront 1 the
 //  geopotential recurrence, each in the reference's sequential order.
+//  The same launch runs K1 (surface_pressures and the 2-D reciprocals): the column blocks on
+//  their own columns, and `nsp` trailing blocks on the frame points outside the column box
+//  (the deeper ghost rings of the reciprocals).  Nothing here reads those outputs elsewhere
+//  than at the thread's own point, where rpsa = 1/psa is formed again (the same bits).
 __global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
-                                                 int nxb) {
+                                                 int nxb, int ncol) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   PT_DECL
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
+  if (bb >= ncol) {                                      // surface pressures outside the box
+    const int q = (bb - ncol) * 512 + (int)threadIdx.x;
+    const int jj = g.j0 + q % g.nj, ii = g.i0 + q / g.nj;
+    if (ii < g.i0 + g.ni && !(in(jj, g.jdx1(), g.jdx2()) && in(ii, g.idx1(), g.idx2())))
+      surface_pressures_at(g, f, jj, ii);
+    return;
+  }
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
@@ -100,6 +111,7 @@ __global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __rest
   double* sLG = lds + 3 * kz * 64;                        // log ratio of the layer below level k
   const uint32_t o2 = valid ? g.o2(j, i) : 0u;
   const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
+  if (valid && ty == 7) surface_pressures_at(g, f, j, i);
   double rp = 0.0;
   if (ce) {
     // phase 1: umc/vmc = atm1 * msfd (decouple :880-890); xqv/xqc decoupled moisture (:1000-1016)
@@ -108,7 +120,7 @@ __global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __rest
     const double m00 = LD(f.msfd, o2), m10 = LD(f.msfd, O2(1, 0));
     const double m01 = LD(f.msfd, O2(0, 1)), m11 = LD(f.msfd, O2(1, 1));
     const double psk = LD(f.psa, o2);
-    rp = LD(f.rpsa, o2);
+    rp = d_one / psk;                                    // rpsa (K1), the same division
     // two levels per thread and pass: every load of the pass is issued before any use
     constexpr int KU = 2;
     for (int k0 = ty + 1; k0 <= kz; k0 += 8 * KU) {

@@ -63,7 +63,7 @@ struct QFix {
 };
 
 __global__ void k_surface_pressures(Geom g, Fields f);
-__global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb);
+__global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb, int ncol);
 __global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
