@@ -78,18 +78,42 @@ def _time_steps(o, budget_s):
             return el / n, n
 
 
-def cpu_baseline(rc, data, budget_s: float = 15.0):
-    """Time the CPU restatement on a bounded sample of the same workload: on all the host
-    threads this job may use (set_nproc tiles on OpenMP threads, oracle/orc_par.c,
-    bit-identical to one tile), and on one thread as a secondary figure."""
+def cpu_quota() -> int:
+    """CPUs' worth of time the cgroup grants this process (cgroup v2 cpu.max, v1 cfs quota);
+    0 if unlimited or unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return 0 if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        return 0 if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return 0
+
+
+def cpu_baseline(rc, data, budget_s: float = 15.0, threads: int = 0):
+    """Time the CPU restatement on a bounded sample of the same workload: on every host CPU this
+    process is granted (SURVEY 8(d) / BASELINE.md: set_nproc tiles on OpenMP threads,
+    oracle/orc_par.c, bit-identical to one tile, both cores) -- the CPUs it may run on, capped
+    by the cgroup's CPU quota: the sweep of profiles/r03/cpu_sweep_c3.jsonl on the GPU box (256
+    CPUs visible, a 16-CPU quota) peaks at 16 threads and collapses beyond (28 ms/step at 32,
+    1.7 s at 256) -- unless `threads` names a count; the hydrostatic core also on one thread as
+    a secondary figure."""
     from oracle.oracle import OracleCore, OracleParallel
     nproc = os.cpu_count() or 1
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = nproc
-    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, affinity))
-    threads = max(1, min(threads, affinity))
+    quota = cpu_quota()
+    granted = min(affinity, quota) if quota else affinity
+    threads = max(1, min(threads or granted, affinity))
 
     def setup(o):
         o.put_state(data["state"])
@@ -97,22 +121,24 @@ def cpu_baseline(rc, data, budget_s: float = 15.0):
         return o
 
     res = {"unit": "simulated-years/wall-day", "kind": "port", "nproc": nproc, "affinity_cpus": affinity,
-           "cpu_model": _cpu_model()}
-    if rc.idynamic == 1 and threads > 1:
+           "cgroup_cpu_quota": quota or None, "cpu_model": _cpu_model()}
+    if threads > 1:
         o = setup(OracleParallel(rc, data["split"], threads))
-        t, n = _time_steps(o, budget_s * 0.65)
+        t, n = _time_steps(o, budget_s * (0.65 if rc.idynamic == 1 else 1.0))
         o.close()
-        t1, n1 = _time_steps(setup(OracleCore(rc, data["split"])), budget_s * 0.35)
         res.update({"value": rc.dt / (365.0 * t), "cores": o.nthreads, "ms_per_step": t * 1e3,
-                    "single_thread": {"value": rc.dt / (365.0 * t1), "ms_per_step": t1 * 1e3, "steps": n1},
                     "sample": f"{rc.name}: {n} steps of tend+bdyval after 1 warm-up step, "
                               f"{o.nthreads} set_nproc tiles on {o.nthreads} OpenMP threads (oracle/orc_par.c over "
-                              f"oracle/rcm_oracle.c, gcc -O2); single_thread: {n1} steps on 1 thread"})
+                              f"oracle/rcm_oracle.c, gcc -O2)"})
+        if rc.idynamic == 1:
+            t1, n1 = _time_steps(setup(OracleCore(rc, data["split"])), budget_s * 0.35)
+            res["single_thread"] = {"value": rc.dt / (365.0 * t1), "ms_per_step": t1 * 1e3, "steps": n1}
+            res["sample"] += f"; single_thread: {n1} steps on 1 thread"
     else:
         t, n = _time_steps(setup(OracleCore(rc, data["split"])), budget_s)
         res.update({"value": rc.dt / (365.0 * t), "cores": 1, "ms_per_step": t * 1e3,
                     "sample": f"{rc.name}: {n} steps of tend+bdyval after 1 warm-up step, 1 host thread "
-                              "(oracle/rcm_oracle.c, gcc -O2; the NH restatement is single-tile)"})
+                              "(oracle/rcm_oracle.c, gcc -O2)"})
     return res
 
 
@@ -124,6 +150,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0: every CPU this process is granted)")
     ap.add_argument("--prof-steps", type=int, default=5,
                     help="eager steps timed per kernel with HIP events (dominant-kernel roofline)")
     args = ap.parse_args()
@@ -262,7 +290,7 @@ def main():
         "runtime": runtime_info(),
     }
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(rc, data, args.cpu_budget)
+        line["cpu_baseline"] = cpu_baseline(rc, data, args.cpu_budget, args.cpu_threads)
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

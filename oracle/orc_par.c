@@ -28,7 +28,8 @@
 #define MAXT 256
 
 struct orc_par {
-  int ntiles, cj, ci, kz;
+  int ntiles, cj, ci, kz, jx, iy;
+  double* glob[3];                   /* whole-domain gathers of the NH radiative condition */
   orc_t* t[MAXT];
   int info[MAXT][16];
   /* mailbox of the message tile s sends toward direction d */
@@ -137,11 +138,30 @@ static void bfn(void* ctx, double* s, int nk, int along) {
   drain(p, me, out);
 }
 
+/* whole-domain gather (the NH upper radiative condition, Main/mod_sound.F90:496-497): a
+ * barrier (nobody still reads the slot's previous contents), every tile copies its owned cross
+ * points into the shared global array, a barrier, and every tile reads the whole array */
+static const double* gfn(void* ctx, const double* a, int slot) {
+  orc_par_t* p = (orc_par_t*)ctx;
+  const int me = omp_get_thread_num();
+  const int* f = p->info[me];
+  double* gl = p->glob[slot];
+#pragma omp barrier
+  for (int i = f[10]; i <= f[11]; i++)
+    for (int j = f[8]; j <= f[9]; j++)
+      gl[(size_t)(i - 1) * p->jx + (j - 1)] = a[(size_t)(i - f[1]) * f[2] + (j - f[0])];
+#pragma omp barrier
+  return gl;
+}
+
 orc_par_t* orc_par_create(const rcmdyn_config* cfg) {
   const int nt = cfg->nproc_j * cfg->nproc_i;
-  if (nt < 1 || nt > MAXT || cfg->idynamic != 1) return NULL;
+  if (nt < 1 || nt > MAXT || (cfg->idynamic != 1 && cfg->idynamic != 2)) return NULL;
   orc_par_t* p = (orc_par_t*)calloc(1, sizeof(orc_par_t));
   p->ntiles = nt; p->cj = cfg->nproc_j; p->ci = cfg->nproc_i; p->kz = cfg->kz;
+  p->jx = cfg->jx; p->iy = cfg->iy;
+  if (cfg->idynamic == 2 && nt > 1)
+    for (int q = 0; q < 3; q++) p->glob[q] = (double*)calloc((size_t)cfg->jx * cfg->iy, sizeof(double));
   for (int t = 0; t < nt; t++) {
     rcmdyn_config c = *cfg;
     c.tile_first = t; c.tile_count = 1;
@@ -153,6 +173,7 @@ orc_par_t* orc_par_create(const rcmdyn_config* cfg) {
     }
     orc_frame_info(p->t[t], p->info[t]);
     if (nt > 1) orc_set_exchange(p->t[t], xfn, bfn, p);
+    if (nt > 1 && cfg->idynamic == 2) orc_set_gather(p->t[t], gfn);
   }
   return p;
 }
@@ -160,6 +181,7 @@ orc_par_t* orc_par_create(const rcmdyn_config* cfg) {
 void orc_par_destroy(orc_par_t* p) {
   if (!p) return;
   for (int t = 0; t < p->ntiles; t++) orc_destroy(p->t[t]);
+  for (int q = 0; q < 3; q++) free(p->glob[q]);
   free(p);
 }
 

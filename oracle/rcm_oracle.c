@@ -135,7 +135,9 @@ struct orc {
   /* exchange */
   orc_exchange_fn xfn;
   orc_exchange_bdy_fn bfn;
+  orc_gather_fn gfn;
   void* xctx;
+  double* s_tr;                             /* gather scratch of the day-alarm rho*N terms */
 };
 
 /* ---- indexing: frame [k][i][j], global Fortran indices ---- */
@@ -239,9 +241,8 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   init_constants();
   if (cfg->tile_count != 1 || cfg->kz > RCMDYN_MAXKZ || cfg->nsplit > RCMDYN_MAXSPLIT)
     return NULL;
-  /* the non-hydrostatic restatement covers one tile (the upper radiative condition of sound
-   * gathers estore over the whole domain, Main/mod_sound.F90:496-497) */
-  if (cfg->idynamic == 2 && cfg->nproc_j * cfg->nproc_i != 1) return NULL;
+  /* a non-hydrostatic tile of a decomposition needs the whole-domain gather of sound's upper
+   * radiative condition (Main/mod_sound.F90:496-497): orc_set_gather, before the first step */
   if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
   o->cfg = *cfg;
@@ -452,12 +453,18 @@ void orc_destroy(orc_t* o) {
   for (int q = 0; q < 22; q++) free(o->atms[q]);
   for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
   free(o->psdot0);
+  free(o->s_tr);
   for (int n = 0; n < 2; n++) {
     free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
     free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
   }
   free(o->rg_cr); free(o->rg_dt); free(o->ib_cr); free(o->ib_dt);
   free(o);
+}
+
+void orc_set_gather(orc_t* o, orc_gather_fn fn) {
+  o->gfn = fn;
+  if (fn && !o->s_tr) o->s_tr = alloc3(o, 1);
 }
 
 void orc_set_exchange(orc_t* o, orc_exchange_fn fn, orc_exchange_bdy_fn bfn, void* ctx) {
@@ -1819,8 +1826,12 @@ static double nh_xgamma(void) { return d_one / (d_one - c_rgas * (d_one / c_cpd)
 /* surface_pressures NH (:836-848): p* is the constant reference p*; psdota/psdotb as
  * mod_init leaves them (Main/mod_init.F90:174-178) */
 static void nh_surface_pressures(orc_t* o) {
+  /* the constant p* on dot points as mod_init leaves it, ghosts included
+   * (Main/mod_init.F90:174-178) */
   psc2psd(o, o->psa, o->psdota);
+  xch(o, o->psdota, 1, 1, 0);
   psc2psd(o, o->psb, o->psdotb);
+  xch(o, o->psdotb, 1, 2, 0);
   for (int i = o->ice1ga; i <= o->ice2ga; i++)
     for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->rpsa, j, i) = d_one / A2(o->psa, j, i);
   for (int i = o->ice1; i <= o->ice2; i++)
@@ -2263,12 +2274,29 @@ static void nh_tmask(orc_t* o, const double* rpsb) {
   for (int n = 1; n <= 5; n++) fk[n] = d_two;
   fk[0] = d_one; fk[6] = d_one;
   double atot = d_zero, rhontot = d_zero;
-  for (int i = o->ici1; i <= o->ici2; i++)
-    for (int j = o->jci1; j <= o->jci2; j++) {
-      atot = atot + A2(o->astore, j, i);
-      double ensq = EGRAV * EGRAV / c_cpd / (A3(o->a2t, j, i, 1) * A2(rpsb, j, i));
-      rhontot = rhontot + A3(o->rho1, j, i, 1) * sqrt(ensq);
-    }
+  if (o->gfn) {
+    /* decomposed: the per-point terms of every tile, summed over the global interior in the
+     * single-tile order (i-major), so every tile gets the one-tile sums bit for bit */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        double ensq = EGRAV * EGRAV / c_cpd / (A3(o->a2t, j, i, 1) * A2(rpsb, j, i));
+        A2(o->s_tr, j, i) = A3(o->rho1, j, i, 1) * sqrt(ensq);
+      }
+    const double* ga = o->gfn(o->xctx, o->astore, 1);
+    const double* gr = o->gfn(o->xctx, o->s_tr, 2);
+    for (int i = 2; i <= o->iy - 2; i++)
+      for (int j = 2; j <= o->jx - 2; j++) {
+        atot = atot + ga[(size_t)(i - 1) * o->jx + (j - 1)];
+        rhontot = rhontot + gr[(size_t)(i - 1) * o->jx + (j - 1)];
+      }
+  } else {
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        atot = atot + A2(o->astore, j, i);
+        double ensq = EGRAV * EGRAV / c_cpd / (A3(o->a2t, j, i, 1) * A2(rpsb, j, i));
+        rhontot = rhontot + A3(o->rho1, j, i, 1) * sqrt(ensq);
+      }
+  }
   double rnpts = d_one / (double)((o->iy - 3) * (o->jx - 3));
   double abar = atot * rnpts, rhon = rhontot * rnpts;
   double dxmsfb = d_two / o->dxsq / o->cfg.nh_xmsf;
@@ -2499,6 +2527,8 @@ static int nh_sound(orc_t* o) {
         }
       if (day_alarm && it == 1) nh_tmask(o, rpsb);
       int ilo = 2, ihi = o->iy - 2, jlo = 2, jhi = o->jx - 2;  /* icross1+1 .. icross2-1 */
+      /* decomposed: the whole-domain estore (Main/mod_sound.F90:496-497) */
+      const double* ge = o->gfn ? o->gfn(o->xctx, o->estore, 0) : NULL;
       for (int i = o->ici1; i <= o->ici2; i++)
         for (int j = o->jci1; j <= o->jci2; j++) {
           double acc = A2(o->wpval, j, i);
@@ -2506,7 +2536,8 @@ static int nh_sound(orc_t* o) {
             int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
             for (int nsj = -6; nsj <= 6; nsj++) {
               int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
-              acc = acc + A2(o->estore, jnn, inn) * o->tmask[nsj + 6][nsi + 6];
+              const double ev = ge ? ge[(size_t)(inn - 1) * o->jx + (jnn - 1)] : A2(o->estore, jnn, inn);
+              acc = acc + ev * o->tmask[nsj + 6][nsi + 6];
             }
           }
           A2(o->wpval, j, i) = acc;

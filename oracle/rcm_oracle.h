@@ -36,6 +36,14 @@ typedef void (*orc_exchange_fn)(void* ctx, double* field, int nk, int nex, int s
  * along = 1: slice indexed by i (west/east slices), exchanged with bottom/top tiles. */
 typedef void (*orc_exchange_bdy_fn)(void* ctx, double* slice, int nk, int along);
 
+/* whole-domain gather of a 2-D cross field (the NH upper radiative condition gathers estore
+ * over the domain, Main/mod_sound.F90:496-497, and sums the day-alarm means over it): every
+ * tile passes its frame array and gets back the global [iy][jx] array (i-major, 1-based indices
+ * at [(i-1)*jx + (j-1)]) holding every tile's owned cross points.  Called by every tile at the
+ * same point; slot selects one of the run's global buffers. */
+typedef const double* (*orc_gather_fn)(void* ctx, const double* field, int slot);
+void orc_set_gather(orc_t* o, orc_gather_fn fn);
+
 /* config->tile_first selects the tile; tile_count must be 1. */
 orc_t* orc_create(const rcmdyn_config* cfg);
 void orc_destroy(orc_t* o);

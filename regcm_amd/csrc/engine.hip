@@ -10,6 +10,9 @@
 // (comm.hip).
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -157,9 +160,15 @@ void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::ve
 // Launch with an optional HIP event pair around the kernel (rcmdyn_kernel_times).
 #define KLAUNCH(kern, ...)                                  \
   do {                                                      \
+    if (dry) break;                                         \
     hipEvent_t e0_ = prof ? prof->begin(stream) : nullptr;  \
     hipLaunchKernelGGL(kern, __VA_ARGS__);                  \
     if (prof) prof->end(stream, #kern, e0_);                \
+  } while (0)
+// a stream-path HIP call that a plan-only engine (rcmdyn_exchange_plan) skips
+#define DHIPCHK(x)           \
+  do {                       \
+    if (!dry) HIPCHK(x);     \
   } while (0)
 
 // per-launch event pairs, aggregated by kernel name after the run
@@ -271,6 +280,9 @@ struct rcmdyn_engine {
   hipEvent_t evfork = nullptr, evjoin = nullptr;
   bool join_pending = false;
   bool on2 = false;           // an exchange is being issued on stream2 (its staging buffers)
+  // plan-only engine (rcmdyn_exchange_plan): host logic only, no device call; the exchanges and
+  // collectives a rank would issue are logged by a PlanComm
+  bool dry = false;
 
   std::vector<NHFields> nhf;   // non-hydrostatic buffers of each owned tile (idynamic = 2)
   double* nh_gbuf = nullptr;   // global-indexed day-alarm terms of the radiative condition
@@ -359,6 +371,7 @@ struct rcmdyn_engine {
   }
 
   double* dalloc(Tile& t, size_t n) {
+    if (dry) return nullptr;
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, n * sizeof(double)));
     HIPCHK(hipMemset(p, 0, n * sizeof(double)));
@@ -367,6 +380,7 @@ struct rcmdyn_engine {
   }
   template <class T>
   T* talloc(Tile& t, size_t n) {
+    if (dry) return nullptr;
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, n * sizeof(T)));
     HIPCHK(hipMemset(p, 0, n * sizeof(T)));
@@ -445,6 +459,7 @@ struct rcmdyn_engine {
     // boundary masks
     std::vector<int8_t> rg;
     std::vector<int16_t> ib;
+    if (dry) return;
     setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgx, false, rg, ib);
     HIPCHK(hipMemcpy(t.rgcr, rg.data(), P, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(t.ibcr, ib.data(), P * 2, hipMemcpyHostToDevice));
@@ -538,8 +553,9 @@ struct rcmdyn_engine {
     return f;
   }
 
-  void create(const rcmdyn_config* c) {
+  void create(const rcmdyn_config* c, std::vector<PlanOp>* plan = nullptr) {
     cfg = *c;
+    dry = plan != nullptr;
     if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
     if (cfg.idynamic != 1 && cfg.idynamic != 2) throw std::runtime_error("rcmdyn: idynamic must be 1 or 2");
     if (cfg.idynamic == 2) {
@@ -565,8 +581,10 @@ struct rcmdyn_engine {
     ntiles = cfg.nproc_j * cfg.nproc_i;
     if (ntiles < 1 || cfg.tile_first < 0 || cfg.tile_count < 1 || cfg.tile_first + cfg.tile_count > ntiles)
       throw std::runtime_error("rcmdyn: bad tile range");
-    if (cfg.device >= 0) HIPCHK(hipSetDevice(cfg.device));
-    HIPCHK(hipGetDevice(&device));
+    if (!dry) {
+      if (cfg.device >= 0) HIPCHK(hipSetDevice(cfg.device));
+      HIPCHK(hipGetDevice(&device));
+    }
     for (int t = 0; t < ntiles; t++) {
       all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t));
       const Geom& g = all.back();
@@ -577,6 +595,16 @@ struct rcmdyn_engine {
         throw std::runtime_error("rcmdyn: non-hydrostatic tiles must be at least 6x6 points");
     }
     compute_constants();
+    if (dry) {
+      if (cfg.tile_count != 1 || cfg.comm_size != ntiles || cfg.tile_first != cfg.comm_rank)
+        throw std::runtime_error("rcmdyn_exchange_plan: one tile per rank (tile_first == comm_rank, comm_size = tiles)");
+      hs = StepState{};
+      hs.dt = cfg.dtsec;
+      tiles.resize(1);
+      setup_tile(tiles[0], cfg.tile_first);
+      comm.reset(make_plan_comm(cfg.comm_rank, plan));
+      return;
+    }
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&dc, sizeof(Consts)));
     HIPCHK(hipMemcpy(dc, &hc, sizeof(Consts), hipMemcpyHostToDevice));
@@ -596,7 +624,17 @@ struct rcmdyn_engine {
     std::memset(hflags, 0, sizeof(FlagSnap) * NFLAGSLOT);
     HIPCHK(hipHostGetDevicePointer((void**)&dflags, hflags, 0));
     for (auto& e : fev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (cfg.tile_count < ntiles) comm.reset(make_rccl_comm(cfg));
+    if (cfg.tile_count < ntiles) {
+      // RCMDYN_LOCAL_COMM=<group>: the in-process loopback transport of the multi-rank tests
+      const char* lg = std::getenv("RCMDYN_LOCAL_COMM");
+      if (lg && *lg) {
+        if (cfg.comm_size != ntiles || cfg.tile_count != 1 || cfg.tile_first != cfg.comm_rank)
+          throw std::runtime_error("rcmdyn: local communicator mode needs one tile per rank (tile_first == comm_rank)");
+        comm.reset(make_local_comm(lg, cfg.comm_rank, cfg.comm_size));
+      } else {
+        comm.reset(make_rccl_comm(cfg));
+      }
+    }
     else if (force_rccl && ntiles > 1) comm.reset(make_rccl_self_comm());
     if (comm) {
       HIPCHK(hipMalloc(&derr, sizeof(int32_t)));
@@ -646,6 +684,10 @@ struct rcmdyn_engine {
   // a tend was issued whose clock is lc once it ran: remember its snapshot slot; with a
   // communicator, every GLOBAL_EVERY steps (or when `global`) issue the job-wide reduction
   void note_step(long long lc, bool global = false) {
+    if (dry) {
+      if (global || lc % GLOBAL_EVERY == 0) comm->allreduce_max(nullptr, 1, stream);
+      return;
+    }
     if (comm) {
       if (global || lc % GLOBAL_EVERY == 0) {
         if ((int)gpending.size() >= NFLAGSLOT - 1) check(0);
@@ -1056,21 +1098,26 @@ struct rcmdyn_engine {
   struct Layout {
     std::vector<Seg> segs;
     long start[8], count[8];
+    uint64_t sig[8];       // shape signature of each direction's message (FNV-1a of nk, nj, ni)
   };
   Layout layout(Tile& t, const SegFn& fn, bool send, const std::function<bool(int)>& dir_on) {
     Layout L;
     long off = 0;
     for (int d = 0; d < 8; d++) {
       L.start[d] = off; L.count[d] = 0;
-      if (peer_of(t, d) < 0 || !dir_on(d)) continue;
+      uint64_t h = 1469598103934665603ull;
+      auto mix = [&h](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+      if (peer_of(t, d) < 0 || !dir_on(d)) { L.sig[d] = 0; continue; }
       std::vector<Seg> v;
       fn(t, d, send, v);
       for (Seg& s : v) {
         s.off = off;
         off += (long)(s.j2 - s.j1 + 1) * (s.i2 - s.i1 + 1) * s.nk;
+        mix((uint64_t)s.nk); mix((uint64_t)(s.j2 - s.j1 + 1)); mix((uint64_t)(s.i2 - s.i1 + 1));
         L.segs.push_back(s);
       }
       L.count[d] = off - L.start[d];
+      L.sig[d] = h & 0x7fffffffffffffffull;
     }
     if (off > staging_cap) throw std::runtime_error("rcmdyn: halo staging buffer too small");
     return L;
@@ -1106,26 +1153,26 @@ struct rcmdyn_engine {
           // one-rank communicator: the n-th send to self matches the n-th receive
           const size_t pq = pt - tiles.data();
           if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
-          sends.push_back({comm->rank(), SB(t) + S[q].start[d], (size_t)S[q].count[d]});
-          recvs.push_back({comm->rank(), RB(*pt) + R[pq].start[OPP[d]], (size_t)S[q].count[d]});
+          sends.push_back({comm->rank(), SB(t) + S[q].start[d], (size_t)S[q].count[d], S[q].sig[d]});
+          recvs.push_back({comm->rank(), RB(*pt) + R[pq].start[OPP[d]], (size_t)S[q].count[d], R[pq].sig[OPP[d]]});
           continue;
         }
         if (S[q].count[d]) {
           if (pt) {
             const size_t pq = pt - tiles.data();
             if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
-            HIPCHK(hipMemcpyAsync(RB(*pt) + R[pq].start[OPP[d]], SB(t) + S[q].start[d],
-                                  S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
+            DHIPCHK(hipMemcpyAsync(RB(*pt) + R[pq].start[OPP[d]], SB(t) + S[q].start[d],
+                                   S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
           } else {
-            sends.push_back({p, SB(t) + S[q].start[d], (size_t)S[q].count[d]});
+            sends.push_back({p, SB(t) + S[q].start[d], (size_t)S[q].count[d], S[q].sig[d]});
           }
         }
-        if (R[q].count[d] && !pt) recvs.push_back({p, RB(t) + R[q].start[d], (size_t)R[q].count[d]});
+        if (R[q].count[d] && !pt) recvs.push_back({p, RB(t) + R[q].start[d], (size_t)R[q].count[d], R[q].sig[d]});
       }
     }
     if (!sends.empty() || !recvs.empty()) {
       if (!comm) throw std::runtime_error("rcmdyn: remote neighbour without a communicator");
-      comm->sendrecv(sends, recvs, stream);
+      comm->sendrecv(sends, recvs, stream, on2 ? 1 : 0);
     }
     for (size_t q = 0; q < tiles.size(); q++) launch_segs(R[q].segs, RB(tiles[q]), 1);
   }
@@ -1166,11 +1213,11 @@ struct rcmdyn_engine {
   // into the step graph as a fork/join.
   void fork_point() {
     if (ntiles == 1) return;
-    HIPCHK(hipEventRecord(evfork, stream));
+    DHIPCHK(hipEventRecord(evfork, stream));
   }
   void xch_begin(std::vector<XField> fs) {
     if (ntiles == 1) return;
-    HIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
+    DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
     std::swap(stream, stream2);
     on2 = true;
     try {
@@ -1182,12 +1229,12 @@ struct rcmdyn_engine {
     }
     on2 = false;
     std::swap(stream, stream2);
-    HIPCHK(hipEventRecord(evjoin, stream2));
+    DHIPCHK(hipEventRecord(evjoin, stream2));
     join_pending = true;
   }
   void xch_join() {
     if (!join_pending) return;
-    HIPCHK(hipStreamWaitEvent(stream, evjoin, 0));
+    DHIPCHK(hipStreamWaitEvent(stream, evjoin, 0));
     join_pending = false;
   }
 
@@ -1279,8 +1326,8 @@ struct rcmdyn_engine {
     if (statics_dirty) {
       xch({{FK::MSFX, 1}, {FK::MSFD, 1}, {FK::HT, 1}, {FK::CORIOL, 1}}, 2, 0);
       each([&](Tile& t) {
-        hipLaunchKernelGGL(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
-                           t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
+        KLAUNCH(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
+                t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
       });
       if (ntiles > 1) {
         each([&](Tile& t) {
@@ -1807,6 +1854,17 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
   }
 
+  // rcmdyn_exchange_plan: the communication calls of prepare + nsteps x (tend + bdyval), the
+  // eager step sequence every rank runs (graph replay issues the same calls in the same order)
+  void plan_run(int nsteps) {
+    prepare();
+    for (int s = 0; s < nsteps; s++) {
+      tend();
+      bdyval();
+      note_step(hs.lcount, s == nsteps - 1);
+    }
+  }
+
   void kernel_times(int nsteps, int cap, char* names, int32_t* launches, double* avg, int32_t* count) {
     prepare();
     KernelProf kp;
@@ -1898,8 +1956,20 @@ int guard(rcmdyn_t* h, F fn) {
 
 extern "C" {
 
+// RCMDYN_SEGV_TRACE=1: print the native backtrace of a segmentation fault (host debugging aid)
+static void segv_trace(int sig) {
+  void* bt[64];
+  const int n = backtrace(bt, 64);
+  const char msg[] = "rcmdyn: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(bt, n, 2);
+  std::signal(sig, SIG_DFL);
+  std::raise(sig);
+}
+
 int rcmdyn_create(const rcmdyn_config* cfg, rcmdyn_t** out) {
   if (!cfg || !out) { g_last_error = "rcmdyn_create: null argument"; return 1; }
+  if (std::getenv("RCMDYN_SEGV_TRACE")) std::signal(SIGSEGV, segv_trace);
   auto* h = new rcmdyn_engine();
   int rc = guard(h, [&] { h->create(cfg); });
   if (rc) {
@@ -1910,6 +1980,30 @@ int rcmdyn_create(const rcmdyn_config* cfg, rcmdyn_t** out) {
     return rc;
   }
   *out = h;
+  return 0;
+}
+
+int rcmdyn_exchange_plan(const rcmdyn_config* cfg, int32_t nsteps, int64_t* ops, int64_t cap, int64_t* count) {
+  if (!cfg || !count || nsteps < 0 || cap < 0 || (cap > 0 && !ops)) {
+    g_last_error = "rcmdyn_exchange_plan: bad argument";
+    return 1;
+  }
+  std::vector<PlanOp> log;
+  auto* h = new rcmdyn_engine();
+  int rc = guard(h, [&] {
+    h->create(cfg, &log);
+    h->plan_run(nsteps);
+  });
+  if (rc) g_last_error = h->err;
+  h->destroy();
+  delete h;
+  if (rc) return rc;
+  *count = (int64_t)log.size();
+  for (int64_t q = 0; q < std::min<int64_t>(cap, (int64_t)log.size()); q++) {
+    const PlanOp& o = log[q];
+    const int64_t v[7] = {o.seq, o.kind, o.chan, o.dir, o.peer, o.count, o.sig};
+    std::memcpy(ops + 7 * q, v, sizeof(v));
+  }
   return 0;
 }
 

@@ -376,7 +376,14 @@ __global__ __launch_bounds__(256) void k_sladv(Geom g, const Consts* __restrict_
 constexpr int TW1 = MBJ + 2, TH1 = MBI + 2;   // halo 1 on every side
 constexpr int TW2 = MBJ + 4, TH2 = MBI + 4;   // halo 2 on every side
 constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i-1)
-__global__ __launch_bounds__(MBT, 4) void k_momentum(Geom g, const Consts* __restrict__ c,
+// blocks per CU the register budget is sized for (LDS admits 2 of these blocks per CU)
+#ifndef MO_LB
+#define MO_LB 4
+#endif
+#ifndef SC_LB
+#define SC_LB 4
+#endif
+__global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* __restrict__ c,
                                                      const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
   __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
@@ -752,7 +759,7 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
   } while (0)
 
-__global__ __launch_bounds__(SBT, 4) void k_scalars(Geom g, const Consts* __restrict__ c,
+__global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __restrict__ c,
                                                     const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
   __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];

@@ -30,6 +30,7 @@ EXPORTED = [
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
     "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin", "rcmdyn_reductions", "rcmdyn_runtime_info",
+    "rcmdyn_exchange_plan",
 ]
 
 
@@ -71,6 +72,8 @@ def lib():
     L.rcmdyn_set_diagnostics.argtypes = [P, i32]
     L.rcmdyn_reductions.argtypes = [P, dp]
     L.rcmdyn_runtime_info.argtypes = [ctypes.c_char_p, i32]
+    L.rcmdyn_exchange_plan.argtypes = [ctypes.POINTER(RcmdynConfig), i32, ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
     L.rcmdyn_kernel_times.argtypes = [P, i32, i32, ctypes.c_char_p, ctypes.POINTER(i32), dp, ctypes.POINTER(i32)]
     _lib = L
     return L
@@ -89,6 +92,24 @@ def tile_extent(jx: int, iy: int, nproc_j: int, nproc_i: int, tile: int):
     if lib().rcmdyn_tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy):
         raise EngineError("rcmdyn_tile_extent failed")
     return list(ext), list(bdy)
+
+
+PLAN_COLUMNS = ("call", "kind", "chan", "dir", "peer", "count", "sig")
+
+
+def exchange_plan(rc, split, nproc_j: int, nproc_i: int, rank: int, nsteps: int) -> np.ndarray:
+    """Host-only communication plan of one rank (rcmdyn_exchange_plan): an (n, 7) int64 array
+    with the columns PLAN_COLUMNS, in issue order.  No GPU is touched."""
+    cfg = build_config(rc, split, nproc_j, nproc_i, tile_first=rank, tile_count=1, comm_rank=rank,
+                       comm_size=nproc_j * nproc_i)
+    n = ctypes.c_int64()
+    if lib().rcmdyn_exchange_plan(ctypes.byref(cfg), nsteps, None, 0, ctypes.byref(n)):
+        raise EngineError(lib().rcmdyn_last_error(None).decode())
+    out = np.zeros((n.value, 7), dtype=np.int64)
+    if lib().rcmdyn_exchange_plan(ctypes.byref(cfg), nsteps, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                  n.value, ctypes.byref(n)):
+        raise EngineError(lib().rcmdyn_last_error(None).decode())
+    return out
 
 
 def runtime_info() -> str:

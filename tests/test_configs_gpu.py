@@ -9,8 +9,8 @@ Tolerances (written per test):
   rank counts.
 * NH (C5 / N2): relative max-norm 1e-11 after one step, 1e-10 after two (see test_nh_gpu.py).
 
-The large oracles run on host threads (oracle/orc_par.c, bit-identical to one tile); the
-tests print progress so a long one is visibly alive.
+The large oracles run as set_nproc tiles on host threads (oracle/orc_par.c, both cores,
+bit-identical to one tile); the tests print progress so a long one is visibly alive.
 """
 import os
 
@@ -53,8 +53,8 @@ def say(*a):
 
 
 def oracle(rc, data):
-    from oracle.oracle import OracleCore, OracleParallel
-    o = OracleParallel(rc, data["split"], _threads()) if rc.idynamic == 1 else OracleCore(rc, data["split"])
+    from oracle.oracle import OracleParallel
+    o = OracleParallel(rc, data["split"], _threads())
     o.put_state(data["state"])
     o.bdyval()
     return o

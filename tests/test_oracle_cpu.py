@@ -994,3 +994,36 @@ def test_oracle_threads_match_single_tile(c1_data, nthreads):
     assert par.get_time() == ref.get_time()
     for name in STATE_FIELDS:
         assert np.array_equal(par.get(name), ref.get(name)), name
+
+
+NH_VARIANTS = [{}, {"isladvec": 1}, {"ibltyp": 2}, {"iboudy": 4}, {"idiffu": 2}]
+
+
+@pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()) or "default")
+@pytest.mark.parametrize("nthreads", [2, 4])
+def test_nh_oracle_threads_match_single_tile(nthreads, variant):
+    """The NH restatement as set_nproc tiles on OpenMP threads (the all-cores NH CPU baseline):
+    the reference's exchanges, plus the whole-domain gather of sound's upper radiative
+    condition (estore, Main/mod_sound.F90:496-497) and of its day-alarm means, summed in the
+    single-tile order -- bit-identical to one tile over 3 steps (istep changes on the first
+    two, the radiative mask is built on the first)."""
+    import dataclasses
+    from oracle.oracle import OracleCore, OracleParallel
+    from regcm_amd.config import CONFIGS, NH_STATE_FIELDS
+    from regcm_amd import icbc
+    rc = dataclasses.replace(CONFIGS["N1"], **variant)
+    data = icbc.generate_nh(CONFIGS["N1"])
+    st = dict(data["state"])
+    if rc.ibltyp == 2:
+        st.update(icbc.tke_state(rc))
+    ref = OracleCore(rc, data["split"])
+    par = OracleParallel(rc, data["split"], nthreads)
+    assert par.nthreads == nthreads
+    for o in (ref, par):
+        o.put_state(st)
+        o.bdyval()
+        o.step(3)
+    assert par.get_time() == ref.get_time()
+    names = STATE_FIELDS[:12] + NH_STATE_FIELDS + (["ATM1_TKE", "ATM2_TKE"] if rc.ibltyp == 2 else [])
+    for name in names:
+        assert np.array_equal(par.get(name), ref.get(name)), name

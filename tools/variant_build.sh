@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds an experimental engine variant: tools/variant_build.sh <name> <hipcc flags...>
-# into build/var_<name>.so (select it with RCMDYN_LIB=build/var_<name>.so, e.g. in
+# into varlib/var_<name>.so (select it with RCMDYN_LIB=varlib/var_<name>.so, e.g. in
 # tools/ab_bench.sh or bench.py).  The sources are copied to a scratch tree first so the
 # in-tree objects are untouched.
 set -eu
@@ -10,7 +10,7 @@ W=/tmp/rcm_var_$name
 rm -rf $W && mkdir -p $W/regcm_amd/csrc $W/include
 cp regcm_amd/csrc/*.hip regcm_amd/csrc/*.hpp regcm_amd/csrc/Makefile $W/regcm_amd/csrc/
 cp include/*.h $W/include/
-mkdir -p build
+mkdir -p varlib
 make -s -C $W/regcm_amd/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function $*"
-cp $W/regcm_amd/librcmdyn.so build/var_$name.so
-echo "built build/var_$name.so"
+cp $W/regcm_amd/librcmdyn.so varlib/var_$name.so
+echo "built varlib/var_$name.so"
