@@ -43,18 +43,18 @@ class RcclComm final : public Comm {
     ncclUniqueId id;
     std::memcpy(id.internal, cfg.comm_unique_id, NCCL_UNIQUE_ID_BYTES);
     NCCLCHK(ncclCommInitRank(&comm_[0], cfg.comm_size, id, cfg.comm_rank));
-    split();
     rank_ = cfg.comm_rank;
+    second(cfg.comm_size);
   }
   RcclComm() {                       // one rank: sends to itself
     ncclUniqueId id;
     NCCLCHK(ncclGetUniqueId(&id));
     NCCLCHK(ncclCommInitRank(&comm_[0], 1, id, 0));
-    split();
+    second(1);
   }
   ~RcclComm() override {            // the split communicator before its parent
     for (int q = NCHAN - 1; q >= 0; q--)
-      if (comm_[q]) ncclCommDestroy(comm_[q]);
+      if (comm_[q] && (q == 0 || comm_[q] != comm_[0])) ncclCommDestroy(comm_[q]);
   }
   void sendrecv(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s, int chan) override {
     if (sends.empty() && recvs.empty()) return;
@@ -77,10 +77,51 @@ class RcclComm final : public Comm {
   // decomposed steps eagerly instead
   bool graph_safe() const override { return std::getenv("RCMDYN_RCCL_EAGER") == nullptr; }
   int rank() const override { return rank_; }
+  bool shared_channels() const override { return comm_[1] == comm_[0]; }
 
  private:
-  // the second channel's communicator: every rank, same color, same key order
-  void split() { NCCLCHK(ncclCommSplit(comm_[0], 0, rank_of(comm_[0]), &comm_[1], nullptr)); }
+  // The second channel's communicator.  "one" (default): the first communicator, with the
+  // engine ordering the second stream's exchange after the first stream's (shared_channels).
+  // "init": rank 0 draws a second unique id and broadcasts it over the first communicator,
+  // every rank joins it with ncclCommInitRank; "split": ncclCommSplit.  Both second-
+  // communicator forms crash the first graph-captured step under the RCCL 2.26 that torch
+  // bundles (a process that imported torch before loading the engine binds torch's
+  // librccl.so.1, same soname as /opt/rocm's 2.27), measured with the one-rank communicator
+  // (tools/rccl_dbg.py --torch-first); one communicator runs under both.
+  void second(int size) {
+    const char* m = std::getenv("RCMDYN_RCCL_CHAN2");
+    const std::string mode = m ? m : "one";
+    if (mode == "one") { comm_[1] = comm_[0]; return; }
+    if (mode == "split") {
+      NCCLCHK(ncclCommSplit(comm_[0], 0, rank_of(comm_[0]), &comm_[1], nullptr));
+      return;
+    }
+    if (mode != "init") throw std::runtime_error("rcmdyn: RCMDYN_RCCL_CHAN2 must be init, split or one");
+    ncclUniqueId id2;
+    std::memset(&id2, 0, sizeof(id2));
+    if (size > 1) {
+      if (rank_ == 0) NCCLCHK(ncclGetUniqueId(&id2));
+      void* d = nullptr;
+      hipStream_t st = nullptr;
+      HIPCHK_C(hipMalloc(&d, sizeof(id2)));
+      try {
+        HIPCHK_C(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHK_C(hipMemcpy(d, &id2, sizeof(id2), hipMemcpyHostToDevice));
+        NCCLCHK(ncclBroadcast(d, d, sizeof(id2), ncclUint8, 0, comm_[0], st));
+        HIPCHK_C(hipStreamSynchronize(st));
+        HIPCHK_C(hipMemcpy(&id2, d, sizeof(id2), hipMemcpyDeviceToHost));
+      } catch (...) {
+        if (st) (void)hipStreamDestroy(st);
+        (void)hipFree(d);
+        throw;
+      }
+      (void)hipStreamDestroy(st);
+      (void)hipFree(d);
+    } else {
+      NCCLCHK(ncclGetUniqueId(&id2));
+    }
+    NCCLCHK(ncclCommInitRank(&comm_[1], size, id2, rank_));
+  }
   static int rank_of(ncclComm_t c) {
     int r = 0;
     NCCLCHK(ncclCommUserRank(c, &r));

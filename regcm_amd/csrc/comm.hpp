@@ -49,10 +49,15 @@ class Comm {
   virtual void allreduce_max_d(double* p, size_t count, hipStream_t s) = 0;
   virtual bool graph_safe() const = 0;
   virtual int rank() const = 0;
+  // both channels go through one communicator: the engine then orders the second stream's
+  // exchange after the first stream's preceding one (no two grouped calls in flight at once)
+  virtual bool shared_channels() const { return false; }
 };
 
-// one rank per tile: the communicator of the job (cfg.comm_rank / comm_size / unique id),
-// split once more for the second channel
+// one rank per tile: the communicator of the job (cfg.comm_rank / comm_size / unique id);
+// the second channel (RCMDYN_RCCL_CHAN2) shares it ("one", default; the engine orders the two
+// streams' exchanges), or gets a second communicator ("init": ncclCommInitRank on a unique id
+// rank 0 broadcasts over the first; "split": ncclCommSplit)
 Comm* make_rccl_comm(const rcmdyn_config& cfg);
 // a communicator of one rank that carries the halo messages between the tiles one engine
 // holds, as RCCL sends and receives to itself (RCMDYN_FORCE_RCCL=1: exercises the RCCL

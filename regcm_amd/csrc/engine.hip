@@ -268,6 +268,10 @@ struct rcmdyn_engine {
   double last_ms = 0.0;
   // RCMDYN_NO_GRAPH=1 runs rcmdyn_step eagerly (the path of RCCL-decomposed runs), for timing
   const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
+  // rcmdyn_step's hydrostatic bdyval runs inside k_split_correct_bdy (RCMDYN_NO_FUSE_BDY: two
+  // launches of its own, as after rcmdyn_tend)
+  const bool no_fuse_bdy = std::getenv("RCMDYN_NO_FUSE_BDY") != nullptr;
+  bool fuse_bdy = false;      // set by step_once for the tend + bdyval pair it runs
   std::string err;
   std::unique_ptr<Comm> comm;
   // RCMDYN_FORCE_RCCL=1: the halo messages between tiles held by this engine travel as RCCL
@@ -1215,6 +1219,12 @@ struct rcmdyn_engine {
     if (ntiles == 1) return;
     DHIPCHK(hipEventRecord(evfork, stream));
   }
+  // one communicator for both streams (RCMDYN_RCCL_CHAN2=one): the second stream's exchange
+  // forks after the first stream's preceding exchange instead, so the two grouped calls are
+  // never in flight together; the overlap with the kernels that follow stays
+  void fork_after_exchange() {
+    if (comm && comm->shared_channels()) fork_point();
+  }
   void xch_begin(std::vector<XField> fs) {
     if (ntiles == 1) return;
     DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
@@ -1429,6 +1439,7 @@ struct rcmdyn_engine {
     if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro2.push_back({FK::A2TKE, kp, 2}); }
     fork_point();
     xchv(pro);
+    fork_after_exchange();
     xch_begin(pro2);
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1555,7 +1566,7 @@ struct rcmdyn_engine {
       Tile& t = tiles[q];
       const int c = t.cur;
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
-              t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()));
+              t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()), dflags);
     }
     tke_bdyval();
     hs.xbctime = hs.xbctime + cfg.dtsec;
@@ -1593,6 +1604,7 @@ struct rcmdyn_engine {
     if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro2.push_back({FK::A2TKE, kz + 1, 2}); }
     fork_point();
     xchv(pro);
+    fork_after_exchange();
     xch_begin(pro2);
     ghosts_stale = false;
     // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
@@ -1689,9 +1701,18 @@ struct rcmdyn_engine {
       Tile& t = tiles[q];
       const Geom& g = t.g;
       const int c = t.cur;
-      KLAUNCH(k_split_correct, grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz), BLK, 0, stream, g,
-                         dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c],
-                         t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red, red_total, dflags);
+      dim3 gr = grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
+      if (fuse_bdy) {
+        // the bdyval blocks past the correction grid: 6 lines x bdy_chunks 64-point chunks, 4
+        // per block
+        gr.y += (6 * bdy_chunks(g) + 4 * gr.x - 1) / (4 * gr.x);
+        KLAUNCH(k_split_correct_bdy, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, ds,
+                (int)(q + 1 == tiles.size()), red, red_total, bdy_args(t, 1));
+      }
+      else
+        KLAUNCH(k_split_correct, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c],
+                t.a1t[c], t.a2t[c], t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red,
+                red_total, dflags);
     }
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
@@ -1730,21 +1751,41 @@ struct rcmdyn_engine {
   void bdyval() {
     if (cfg.idynamic == 2) { nh_bdyval(); return; }
     const int kz = cfg.kz;
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
-              stream, g, ds, bdy_args(t, 1));
-    });
-    // the ghost-ring step wrote the slice entries past the tile itself (k_bdyval_set)
-    if (ghosts_stale || !split_fused()) xch_slices();
+    // fused (step_once): the boundary lines and slices were set by k_split_correct_bdy, and
+    // the clock advance of the step moves here (last tile's launch)
+    if (!fuse_bdy) {
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        KLAUNCH(k_bdyval_set, dim3((std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64, 6, kz), dim3(64), 0,
+                stream, g, ds, bdy_args(t, 1));
+      });
+      // the ghost-ring step wrote the slice entries past the tile itself (k_bdyval_set)
+      if (ghosts_stale || !split_fused()) xch_slices();
+    }
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
+      const int adv = q + 1 == tiles.size() ? (fuse_bdy ? 2 : 1) : 0;
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
-              t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec,
-              (int)(q + 1 == tiles.size()));
+              t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec, adv, dflags);
     }
     tke_bdyval();
     hs.xbctime = hs.xbctime + cfg.dtsec;
+  }
+
+  // one tend + bdyval of rcmdyn_step (no host work between them): the hydrostatic bdyval's
+  // boundary lines and slices then run in k_split_correct_bdy, only its moisture
+  // inflow/outflow pass in a launch of its own.  A decomposed domain needs no slice exchange
+  // then (split_fused: every tile computes its ghost ring).
+  void step_once() {
+    fuse_bdy = cfg.idynamic != 2 && !no_fuse_bdy && (ntiles == 1 || split_fused());
+    try {
+      tend();
+      bdyval();
+    } catch (...) {
+      fuse_bdy = false;
+      throw;
+    }
+    fuse_bdy = false;
   }
 
   // ------------------------------------------------------------------ graph replay
@@ -1790,8 +1831,7 @@ struct rcmdyn_engine {
         replayed_tend();
         replayed_bdyval();
       } else {
-        tend();
-        bdyval();
+        step_once();
       }
       note_step(hs.lcount, s == n - 1);
     }
@@ -1843,8 +1883,9 @@ struct rcmdyn_engine {
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (int q = 0; q < nsteps; q++) {
-      if (what & 1) tend();
-      if (what & 2) bdyval();
+      if (what == 3) step_once();
+      else if (what & 1) tend();
+      else bdyval();
     }
     HIPCHK(hipStreamEndCapture(stream, &graph));
     hipGraphExec_t& x = nsteps == 2 ? gexec2[par] : what == 3 ? gexec[par] : what == 1 ? gtend[par] : gbdy[par];
@@ -1859,8 +1900,7 @@ struct rcmdyn_engine {
   void plan_run(int nsteps) {
     prepare();
     for (int s = 0; s < nsteps; s++) {
-      tend();
-      bdyval();
+      step_once();
       note_step(hs.lcount, s == nsteps - 1);
     }
   }
@@ -1871,7 +1911,7 @@ struct rcmdyn_engine {
     HIPCHK(hipStreamSynchronize(stream));
     prof = &kp;
     try {
-      for (int s = 0; s < nsteps; s++) { tend(); bdyval(); }
+      for (int s = 0; s < nsteps; s++) step_once();
     } catch (...) {
       prof = nullptr;
       throw;

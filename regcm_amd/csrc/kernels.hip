@@ -1495,13 +1495,36 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   }
 }
 
-// splitf corrections, Main/mod_split.F90:417-457 (ps and t on ci, u and v on di)
-__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
-                                const double* __restrict__ dhsum, const double* __restrict__ psdota,
-                                const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
-                                double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
-                                int advance, const double* __restrict__ red, int red_total, FlagSnap* ring) {
+__device__ __forceinline__ void bdyval_point(const Geom& g, double xt, bool integ, const BdyArgs& a, int line, int x,
+                                             int k, bool interior);
+__device__ __forceinline__ int bdy_chunks_d(const Geom& g) { return (max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64; }
+
+// splitf corrections, Main/mod_split.F90:417-457 (ps and t on ci, u and v on di).
+// BDY (k_split_correct_bdy, rcmdyn_step): the step's bdyval (Main/mod_bdycod.F90:1109-1529 +
+// bdyuv :896-1061, hydrostatic, after a tend: the integration branch) runs in the same launch.
+// The corrections never touch a boundary-line point (ci and di exclude them), and with BDY the
+// correcting threads store only the lanes they corrected, so extra blocks past the correction
+// grid run bdyval's line loop (bdyval_point) concurrently: each bdyval write reads only its own
+// point and the boundary data, except the slices' interior entries (u, v of the first interior
+// row/column), which the thread correcting that interior point writes from its registers.
+// The clock is advanced by k_bdyval_qc (advance = 2 here: noise sums only), so the bdyval time
+// level is formed from the clock before the step's advance.
+template <bool BDY>
+__device__ __forceinline__ void split_correct_body(
+    const Geom& g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum,
+    const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
+    double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance,
+    const double* __restrict__ red, int red_total, FlagSnap* ring, const BdyArgs& ba) {
   THREAD_POINT(g.jde1, g.ide1);
+  // bdyval blocks: 4 (line, chunk) items of 64 points per block, over every level
+  const int ycorr = (g.idx2() - g.ide1 + 4) / 4;
+  if (BDY && (int)blockIdx.y >= ycorr) {
+    const int item = (((int)blockIdx.y - ycorr) * (int)gridDim.x + (int)blockIdx.x) * 4 + (int)threadIdx.y;
+    if (item >= 6 * bdy_chunks_d(g)) return;
+    const double xt = s->xbctime + ((s->lcount + 1 == 2) ? d_two * c->dtsec : s->dt);
+    bdyval_point(g, xt, true, ba, item % 6, (item / 6) * 64 + (int)threadIdx.x, k, false);
+    return;
+  }
   // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
   // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch
   // (:608-616); nothing else here reads the clock.  The same lane then copies the step's error
@@ -1521,6 +1544,8 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
       s->ptntot = sa[0];
       s->pt2tot = sb[0];
       if (sa[0] != sa[0]) s->nanflag = 1;
+    }
+    if (t == 0 && advance == 1) {
       s->lcount = s->lcount + 1;
       if (s->lcount == 2) s->dt = d_two * c->dtsec;
       const long long lc = s->lcount;
@@ -1578,14 +1603,18 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
         if (ci0) { pa.x = pa.x - an * dd[0][l - 1]; pb.x = pb.x - gnu1 * an * dd[0][l - 1]; }
         if (ci1) { pa.y = pa.y - an * dd[1][l - 1]; pb.y = pb.y - gnu1 * an * dd[1][l - 1]; }
       }
-      ST2(psa, o2, pa); ST2(psb, o2, pb);
+      if (!BDY || (ci0 && ci1)) { ST2(psa, o2, pa); ST2(psb, o2, pb); }
+      else if (ci0) { ST(psa, o2, pa.x); ST(psb, o2, pb.x); }
+      else { ST(psa, o2 + 8u, pa.y); ST(psb, o2 + 8u, pb.y); }
     }
     for (int l = 1; l <= ns; l++) {
       const double am = c->am[l - 1][k - 1];
       if (ci0) { t1.x = t1.x + am * dd[0][l - 1]; t2.x = t2.x + gnu1 * am * dd[0][l - 1]; }
       if (ci1) { t1.y = t1.y + am * dd[1][l - 1]; t2.y = t2.y + gnu1 * am * dd[1][l - 1]; }
     }
-    ST2(a1t, o3, t1); ST2(a2t, o3, t2);
+    if (!BDY || (ci0 && ci1)) { ST2(a1t, o3, t1); ST2(a2t, o3, t2); }
+    else if (ci0) { ST(a1t, o3, t1.x); ST(a2t, o3, t2.x); }
+    else { ST(a1t, o3 + 8u, t1.y); ST(a2t, o3 + 8u, t2.y); }
   }
   if (dx) {
     const double fac0 = pd.x / (c->dx2 * md.x), fac1 = pd.y / (c->dx2 * md.y);
@@ -1604,10 +1633,36 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
         u1.y = u1.y - zm * x; v1.y = v1.y - zm * y; u2.y = u2.y - gnuzm * x; v2.y = v2.y - gnuzm * y;
       }
     }
-    ST2(a1u, o3, u1); ST2(a1v, o3, v1); ST2(a2u, o3, u2); ST2(a2v, o3, v2);
+    if (!BDY || (di0 && di1)) { ST2(a1u, o3, u1); ST2(a1v, o3, v1); ST2(a2u, o3, u2); ST2(a2v, o3, v2); }
+    else if (di0) { ST(a1u, o3, u1.x); ST(a1v, o3, v1.x); ST(a2u, o3, u2.x); ST(a2v, o3, v2.x); }
+    else { ST(a1u, o3 + 8u, u1.y); ST(a1v, o3 + 8u, v1.y); ST(a2u, o3 + 8u, u2.y); ST(a2v, o3 + 8u, v2.y); }
+  }
+  if (!BDY) return;
+  const Slices& sl = ba.sl;
+  const long slen = ba.slen;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int jj = jp + r;
+    // the slices' interior entries: this point's corrected u, v
+    if (r ? di1 : di0) {
+      const double uu = r ? u1.y : u1.x, vv = r ? v1.y : v1.x;
+      if (g.bl && jj == g.jdi1) { SLI(sl.s[1], i, k) = uu; SLI(sl.s[5], i, k) = vv; }
+      if (g.br && jj == g.jdi2) { SLI(sl.s[3], i, k) = uu; SLI(sl.s[7], i, k) = vv; }
+      if (g.bb && i == g.idi1) { SLJ(sl.s[9], jj, k) = uu; SLJ(sl.s[13], jj, k) = vv; }
+      if (g.bt && i == g.idi2) { SLJ(sl.s[11], jj, k) = uu; SLJ(sl.s[15], jj, k) = vv; }
+    }
   }
 }
 #undef SLOT
+
+__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
+                                const double* __restrict__ dhsum, const double* __restrict__ psdota,
+                                const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
+                                double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
+                                int advance, const double* __restrict__ red, int red_total, FlagSnap* ring) {
+  split_correct_body<false>(g, c, ddsum, dhsum, psdota, msfd, psa, psb, a1t, a2t, a1u, a1v, a2u, a2v, s, advance,
+                            red, red_total, ring, BdyArgs{});
+}
 
 // ---------------------------------------------------------------------------------------
 // bdyval, Main/mod_bdycod.F90:1109-1529 (+ bdyuv :896-1061).  Slice order:
@@ -1615,8 +1670,15 @@ __global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const doub
 // 12 sve 13 svi 14 nve 15 nvi (by j).
 
 
-__device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyArgs a, int line, int x,
-                                             int k) {
+// One boundary point (j, i) at level k: ghost = a point of the right/top ghost ring (only its
+// slice entries are written).  interior: also write the slices' interior entries (u, v of the
+// first interior row/column) from memory; the split-correct fusion writes them from the
+// thread that corrects that point instead (k_split_correct_bdy).
+__device__ __forceinline__ void bdyval_body(const Geom& g, double xt, bool integ, const BdyArgs& a, int j, int i,
+                                            int k, bool ghost, bool interior);
+
+__device__ __forceinline__ void bdyval_point(const Geom& g, double xt, bool integ, const BdyArgs& a, int line, int x,
+                                             int k, bool interior) {
   // set_ps = 0 for the non-hydrostatic core, whose p* is the constant reference p*
   // (Main/mod_bdycod.F90:1150-1165, 1430-1451 are hydrostatic-only).
   // thread -> one point of the boundary lines: blockIdx.y 0..2 = rows i = ide1 (bottom),
@@ -1625,13 +1687,6 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
   // One point past the tile along each line (toward a neighbour) only writes the bdyuv slice
   // entry there, from the ghost-ring u, v and the boundary data: k_bdyval_qc reads it (the
   // reference exchanges the slices instead, exchange_bdy_lr/bt).
-  double *a1u = a.a1u, *a1v = a.a1v, *a1t = a.a1t, *a1qv = a.a1qv, *a1qc = a.a1qc;
-  double *a2u = a.a2u, *a2v = a.a2v, *a2t = a.a2t, *a2qv = a.a2qv, *a2qc = a.a2qc, *psa = a.psa, *psb = a.psb;
-  const double *ub0 = a.ub0, *ubt = a.ubt, *vb0 = a.vb0, *vbt = a.vbt, *tb0 = a.tb0, *tbt = a.tbt;
-  const double *qb0 = a.qb0, *qbt = a.qbt, *pb0 = a.pb0, *pbt = a.pbt;
-  const Slices sl = a.sl;
-  const long slen = a.slen;
-  const int set_ps = a.set_ps;
   int j, i;
   bool ghost = false;
   if (line < 3) {
@@ -1648,6 +1703,18 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
     ghost = i > g.ide2;
     if ((g.bb && i == g.ide1) || (g.bt && (i == g.ide2 || i == g.ice2))) return;
   }
+  bdyval_body(g, xt, integ, a, j, i, k, ghost, interior);
+}
+
+__device__ __forceinline__ void bdyval_body(const Geom& g, double xt, bool integ, const BdyArgs& a, int j, int i,
+                                            int k, bool ghost, bool interior) {
+  double *a1u = a.a1u, *a1v = a.a1v, *a1t = a.a1t, *a1qv = a.a1qv, *a1qc = a.a1qc;
+  double *a2u = a.a2u, *a2v = a.a2v, *a2t = a.a2t, *a2qv = a.a2qv, *a2qc = a.a2qc, *psa = a.psa, *psb = a.psb;
+  const double *ub0 = a.ub0, *ubt = a.ubt, *vb0 = a.vb0, *vbt = a.vbt, *tb0 = a.tb0, *tbt = a.tbt;
+  const double *qb0 = a.qb0, *qbt = a.qbt, *pb0 = a.pb0, *pbt = a.pbt;
+  const Slices& sl = a.sl;
+  const long slen = a.slen;
+  const int set_ps = a.set_ps;
   const long q = g.ix(j, i);
   const long p = (long)(k - 1) * g.plane + q;
   // dot-point boundary rows: left/right on idi, bottom/top on the whole jde range
@@ -1679,7 +1746,8 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
     tbv = tb0[p] + xt * tbt[p];
     qbv = qb0[p] + xt * qbt[p];
   }
-  if (sW) { su = F3(a1u, g.jdi1, i, k); sv = F3(a1v, g.jdi1, i, k); }
+  if (!interior) { }
+  else if (sW) { su = F3(a1u, g.jdi1, i, k); sv = F3(a1v, g.jdi1, i, k); }
   else if (sE) { su = F3(a1u, g.jdi2, i, k); sv = F3(a1v, g.jdi2, i, k); }
   else if (sSi) { su = F3(a1u, j, g.idi1, k); sv = F3(a1v, j, g.idi1, k); }
   else if (sNi) { su = F3(a1u, j, g.idi2, k); sv = F3(a1v, j, g.idi2, k); }
@@ -1712,14 +1780,14 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
     a1t[p] = tbv;
     a1qv[p] = qbv;
   }
-  if (sW) { SLI(sl.s[1], i, k) = su; SLI(sl.s[5], i, k) = sv; SLI(sl.s[0], i, k) = ubv; SLI(sl.s[4], i, k) = vbv; }
-  if (sE) { SLI(sl.s[3], i, k) = su; SLI(sl.s[7], i, k) = sv; SLI(sl.s[2], i, k) = ubv; SLI(sl.s[6], i, k) = vbv; }
+  if (sW) { if (interior) { SLI(sl.s[1], i, k) = su; SLI(sl.s[5], i, k) = sv; } SLI(sl.s[0], i, k) = ubv; SLI(sl.s[4], i, k) = vbv; }
+  if (sE) { if (interior) { SLI(sl.s[3], i, k) = su; SLI(sl.s[7], i, k) = sv; } SLI(sl.s[2], i, k) = ubv; SLI(sl.s[6], i, k) = vbv; }
   if (sS) {
-    if (sSi) { SLJ(sl.s[9], j, k) = su; SLJ(sl.s[13], j, k) = sv; }
+    if (sSi && interior) { SLJ(sl.s[9], j, k) = su; SLJ(sl.s[13], j, k) = sv; }
     SLJ(sl.s[8], j, k) = ubv; SLJ(sl.s[12], j, k) = vbv;
   }
   if (sN) {
-    if (sNi) { SLJ(sl.s[11], j, k) = su; SLJ(sl.s[15], j, k) = sv; }
+    if (sNi && interior) { SLJ(sl.s[11], j, k) = su; SLJ(sl.s[15], j, k) = sv; }
     SLJ(sl.s[10], j, k) = ubv; SLJ(sl.s[14], j, k) = vbv;
   }
   if (kTL) { SLI(sl.s[1], g.ide2, k) = cu1; SLI(sl.s[5], g.ide2, k) = cv1; SLJ(sl.s[11], g.jde1, k) = cu2; SLJ(sl.s[15], g.jde1, k) = cv2; }
@@ -1729,9 +1797,17 @@ __device__ __forceinline__ void bdyval_point(Geom g, double xt, bool integ, BdyA
 }
 
 
+__global__ void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
+                                    const double* __restrict__ dhsum, const double* __restrict__ psdota,
+                                    const double* __restrict__ msfd, StepState* s, int advance,
+                                    const double* __restrict__ red, int red_total, BdyArgs a) {
+  split_correct_body<true>(g, c, ddsum, dhsum, psdota, msfd, a.psa, a.psb, a.a1t, a.a2t, a.a1u, a.a1v, a.a2u, a.a2v,
+                           s, advance ? 2 : 0, red, red_total, nullptr, a);
+}
+
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a) {
   const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  bdyval_point(g, s->xbctime + s->dt, s->lcount > 0, a, (int)blockIdx.y, x, (int)blockIdx.z + 1);
+  bdyval_point(g, s->xbctime + s->dt, s->lcount > 0, a, (int)blockIdx.y, x, (int)blockIdx.z + 1, true);
 }
 
 // qc inflow/outflow (present_qc = .false., bdyflow), Main/mod_bdycod.F90:2153-2220, one
@@ -1830,9 +1906,22 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
 
 
 __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa,
-                            Slices sl, long slen, StepState* s, double dtsec, int advance) {
+                            Slices sl, long slen, StepState* s, double dtsec, int advance, FlagSnap* ring) {
   const int k = (int)blockIdx.x + 1;
-  if (advance && k == 1 && threadIdx.x == 0) s->xbctime = s->xbctime + dtsec;
+  if (advance && k == 1 && threadIdx.x == 0) {
+    s->xbctime = s->xbctime + dtsec;
+    if (advance == 2) {
+      // the step clock of a fused step (k_split_correct_bdy): rcmtimer%advance + dt switch
+      // (Main/mod_tendency.F90:608-616) and the step's flag snapshot
+      s->lcount = s->lcount + 1;
+      if (s->lcount == 2) s->dt = d_two * dtsec;
+      const long long lc = s->lcount;
+      FlagSnap& r = ring[(lc - 1 + NFLAGSLOT) % NFLAGSLOT];
+      r.nanflag = s->nanflag;
+      r.slflag = s->slflag;
+      r.lcount = lc;
+    }
+  }
   bdyval_qc_level(g, do_qc, do_qv, a1qc, a1qv, [&](int j, int i) { return F2(psa, j, i); }, sl, slen, k);
 }
 

@@ -90,7 +90,10 @@ struct BdyArgs {
   int set_ps;
 };
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a);
-__global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance);
+// 64-point chunks of the longest boundary line, one point past the tile included
+inline int bdy_chunks(const Geom& g) { return (std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64; }
+__global__ void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, StepState* s, int advance, const double* __restrict__ red, int red_total, BdyArgs a);
+__global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance, FlagSnap* ring);
 __global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring);
 __global__ void k_err_gather(const StepState* __restrict__ s, int32_t* derr);
 __global__ void k_err_publish(const int32_t* __restrict__ derr, int32_t* hslot);

@@ -231,9 +231,41 @@ def test_kernel_times_hook(c1_data):
     for name, v in kt.items():          # level-marching forms: k_scalars_km<opt> -> k_scalars
         b = name.split("<")[0]
         base[b[:-3] if b.endswith("_km") else b] = v
+    # rcmdyn_step's step: bdyval's boundary lines run inside k_split_correct_bdy
     for k in ("k_momentum", "k_scalars", "k_columns", "k_qfilter", "k_split_project",
-              "k_spstep_fused", "k_split_correct", "k_bdyval_set", "k_bdyval_qc"):
+              "k_spstep_fused", "k_split_correct_bdy", "k_bdyval_qc"):
         assert k in base and base[k][0] == 3 and base[k][1] > 0.0, k
+    assert "k_bdyval_set" not in base and "k_split_correct" not in base, sorted(base)
+
+
+FUSE_CASES = [({}, (1, 1)), ({}, (2, 2)), ({}, (1, 3)), ({"iboudy": 4}, (1, 1)), ({"iboudy": 4}, (2, 2)),
+              ({"isladvec": 1}, (2, 1)), ({"ibltyp": 2}, (1, 1)), ({"ibltyp": 2}, (2, 2))]
+
+
+@pytest.mark.parametrize("variant,nproc", FUSE_CASES, ids=lambda x: str(x))
+def test_fused_bdyval_equals_separate(c1_data, monkeypatch, variant, nproc):
+    """rcmdyn_step runs bdyval's boundary lines inside the split-correct launch
+    (k_split_correct_bdy): bit-identical to the separate k_bdyval_set launch of the drop-in
+    call sequence (RCMDYN_NO_FUSE_BDY), for eager and graph-replayed steps, with the iboudy = 4
+    qv inflow/outflow, semi-Lagrangian and TKE options, on one tile and decomposed."""
+    import dataclasses
+    from regcm_amd.dycore import DynCore
+    rc, data = c1_data
+    rcv = dataclasses.replace(rc, **variant)
+    st = {k: v.copy() for k, v in data["state"].items()}
+    if rcv.ibltyp == 2:
+        st.update(icbc.tke_state(rcv))
+    fused = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    monkeypatch.setenv("RCMDYN_NO_FUSE_BDY", "1")
+    sep = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    for e in (fused, sep):
+        e.put_state(st)
+        e.bdyval()
+        e.step(5)
+    assert fused.get_time() == sep.get_time()
+    for name in list(STATE_FIELDS) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
+        assert np.array_equal(fused.get(name), sep.get(name)), name
+    assert np.array_equal(fused.reductions(), sep.reductions())
 
 
 def _dependent_negatives(cq, rc):

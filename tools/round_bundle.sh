@@ -17,7 +17,7 @@ run() {  # run <name> <timeout> <cmd...>
 STAGES=${STAGES:-"pytest smoke bench prof c5bench c5prof"}
 for s in $STAGES; do
   case $s in
-    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider ;;
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --durations=0 --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py --steps 200 --warmup 20 ;;
     prof)   run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline ;;
