@@ -270,7 +270,10 @@ struct rcmdyn_engine {
   const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
   // rcmdyn_step's hydrostatic bdyval runs inside k_split_correct_bdy (RCMDYN_NO_FUSE_BDY: two
   // launches of its own, as after rcmdyn_tend)
-  const bool no_fuse_bdy = std::getenv("RCMDYN_NO_FUSE_BDY") != nullptr;
+  const bool no_fuse_bdy = [] {
+    const char* v = std::getenv("RCMDYN_NO_FUSE_BDY");
+    return v && *v && std::strcmp(v, "0") != 0;
+  }();
   bool fuse_bdy = false;      // set by step_once for the tend + bdyval pair it runs
   std::string err;
   std::unique_ptr<Comm> comm;
@@ -1703,9 +1706,10 @@ struct rcmdyn_engine {
       const int c = t.cur;
       dim3 gr = grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
       if (fuse_bdy) {
-        // the bdyval blocks past the correction grid: 6 lines x bdy_chunks 64-point chunks, 4
-        // per block
-        gr.y += (6 * bdy_chunks(g) + 4 * gr.x - 1) / (4 * gr.x);
+        // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
+        // levels, 4 per block
+        const unsigned per = 4 * gr.x * gr.y;
+        gr.z += (6 * bdy_chunks(g) * kz + per - 1) / per;
         KLAUNCH(k_split_correct_bdy, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, ds,
                 (int)(q + 1 == tiles.size()), red, red_total, bdy_args(t, 1));
       }

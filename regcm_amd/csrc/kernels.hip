@@ -1515,21 +1515,29 @@ __device__ __forceinline__ void split_correct_body(
     const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
     double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance,
     const double* __restrict__ red, int red_total, FlagSnap* ring, const BdyArgs& ba) {
-  THREAD_POINT(g.jde1, g.ide1);
-  // bdyval blocks: 4 (line, chunk) items of 64 points per block, over every level
-  const int ycorr = (g.idx2() - g.ide1 + 4) / 4;
-  if (BDY && (int)blockIdx.y >= ycorr) {
-    const int item = (((int)blockIdx.y - ycorr) * (int)gridDim.x + (int)blockIdx.x) * 4 + (int)threadIdx.y;
-    if (item >= 6 * bdy_chunks_d(g)) return;
+  // bdyval blocks first: the leading z slices (blockIdx.z < zbdy) are dispatched before any
+  // correction block, so their latency chain overlaps the corrections instead of trailing
+  // them; 4 (line, chunk, level) items of 64 points per block
+  const int kz = c->kz;
+  const int zbdy = BDY ? (int)gridDim.z - kz : 0;
+  if (BDY && (int)blockIdx.z < zbdy) {
+    const int nchunk = bdy_chunks_d(g);
+    const int item = (((int)blockIdx.z * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x) * 4 +
+                     (int)threadIdx.y;
+    if (item >= 6 * nchunk * kz) return;
+    const int line = item % 6, chunk = (item / 6) % nchunk, k = item / (6 * nchunk) + 1;
     const double xt = s->xbctime + ((s->lcount + 1 == 2) ? d_two * c->dtsec : s->dt);
-    bdyval_point(g, xt, true, ba, item % 6, (item / 6) * 64 + (int)threadIdx.x, k, false);
+    bdyval_point(g, xt, true, ba, line, chunk * 64 + (int)threadIdx.x, k, false);
     return;
   }
+  const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int i = g.ide1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int k = (int)blockIdx.z - zbdy + 1;
   // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
   // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch
   // (:608-616); nothing else here reads the clock.  The same lane then copies the step's error
   // flags into the host-mapped ring (k_flag_snapshot's work; this is the step's last flag writer)
-  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && (int)blockIdx.z == zbdy) {
     __shared__ double sa[256], sb[256];
     const int t = threadIdx.y * blockDim.x + threadIdx.x;
     double a = 0.0, b = 0.0;
@@ -1909,16 +1917,19 @@ __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* 
                             Slices sl, long slen, StepState* s, double dtsec, int advance, FlagSnap* ring) {
   const int k = (int)blockIdx.x + 1;
   if (advance && k == 1 && threadIdx.x == 0) {
-    s->xbctime = s->xbctime + dtsec;
+    // every clock word is loaded before the first store (one memory latency, not one per word)
+    const double xb = s->xbctime;
+    const long long lc = s->lcount + 1;
+    const int nanf = s->nanflag, slf = s->slflag;
+    s->xbctime = xb + dtsec;
     if (advance == 2) {
       // the step clock of a fused step (k_split_correct_bdy): rcmtimer%advance + dt switch
       // (Main/mod_tendency.F90:608-616) and the step's flag snapshot
-      s->lcount = s->lcount + 1;
-      if (s->lcount == 2) s->dt = d_two * dtsec;
-      const long long lc = s->lcount;
+      s->lcount = lc;
+      if (lc == 2) s->dt = d_two * dtsec;
       FlagSnap& r = ring[(lc - 1 + NFLAGSLOT) % NFLAGSLOT];
-      r.nanflag = s->nanflag;
-      r.slflag = s->slflag;
+      r.nanflag = nanf;
+      r.slflag = slf;
       r.lcount = lc;
     }
   }
