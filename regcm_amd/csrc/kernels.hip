@@ -81,7 +81,13 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
 //  their own columns, and `nsp` trailing blocks on the frame points outside the column box
 //  (the deeper ghost rings of the reciprocals).  Nothing here reads those outputs elsewhere
 //  than at the thread's own point, where rpsa = 1/psa is formed again (the same bits).
-__global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+#ifndef COL_LB
+#define COL_LB 6
+#endif
+#ifndef COL_KU
+#define COL_KU 1
+#endif
+__global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxb, int ncol) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   PT_DECL
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __rest
     const double psk = LD(f.psa, o2);
     rp = d_one / psk;                                    // rpsa (K1), the same division
     // two levels per thread and pass: every load of the pass is issued before any use
-    constexpr int KU = 2;
+    constexpr int KU = COL_KU;
     for (int k0 = ty + 1; k0 <= kz; k0 += 8 * KU) {
       double u00[KU], u10[KU], u01[KU], u11[KU], v00[KU], v10[KU], v01[KU], v11[KU], tt[KU], qq[KU], cc[KU];
 #pragma unroll
@@ -217,18 +223,20 @@ __global__ __launch_bounds__(512, 5) void k_columns(Geom g, const Consts* __rest
     }
   }
   PT_MARK();
-  // per-block partial of the noise sums (fixed tree); k_split_correct sums the partials
-  __shared__ double sa[512], sb[512];
-  const int t = threadIdx.x;
-  sa[t] = na; sb[t] = nb;
-  __syncthreads();
-  for (int w = 256; w > 0; w >>= 1) {
-    if (t < w) { sa[t] += sa[t + w]; sb[t] += sb[t + w]; }
-    __syncthreads();
-  }
-  if (t == 0) {
-    f.red[2 * (f.red_off + bb)] = sa[0];
-    f.red[2 * (f.red_off + bb) + 1] = sb[0];
+  // per-block partial of the noise sums (fixed tree); k_split_correct sums the partials.  Only
+  // wavefront 0 holds non-zero terms, so the block's halving tree (a[t] += a[t + w], w = 256 ..
+  // 1) reduces to wavefront 0's halving tree from w = 32 (adding the +0.0 terms of the other
+  // wavefronts changes no bit): a shuffle reduction in registers, and no LDS for it (3 blocks
+  // per CU fit the column LDS, so one round of blocks covers C3)
+  if (ty == 0) {
+    for (int w = 32; w > 0; w >>= 1) {
+      na = na + __shfl_down(na, w);
+      nb = nb + __shfl_down(nb, w);
+    }
+    if (tx == 0) {
+      f.red[2 * (f.red_off + bb)] = na;
+      f.red[2 * (f.red_off + bb) + 1] = nb;
+    }
   }
   PT_PRINT(1);
 }
@@ -1195,7 +1203,10 @@ __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFi
 // reference's order.  Blocks [nproj, nproj + 2 kz) run the serial negative-moisture sweeps
 // (one plane each, usually an immediate exit).
 #define SLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * g.plane)
-__global__ __launch_bounds__(512, 5) void k_split_project(
+#ifndef SP_LB
+#define SP_LB 5
+#endif
+__global__ __launch_bounds__(512, SP_LB) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
