@@ -1705,18 +1705,24 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const int c = t.cur;
       dim3 gr = grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
+      const int adv = (int)(q + 1 == tiles.size());
       if (fuse_bdy) {
         // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
         // levels, 4 per block
         const unsigned per = 4 * gr.x * gr.y;
         gr.z += (6 * bdy_chunks(g) * kz + per - 1) / per;
-        KLAUNCH(k_split_correct_bdy, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, ds,
-                (int)(q + 1 == tiles.size()), red, red_total, bdy_args(t, 1));
+        const BdyArgs ba = bdy_args(t, 1);
+#define RCM_SCB(NS_) KLAUNCH(k_split_correct_bdy<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, \
+                             ds, adv, red, red_total, ba)
+        switch (ns) { case 1: RCM_SCB(1); break; case 2: RCM_SCB(2); break; case 3: RCM_SCB(3); break; default: RCM_SCB(4); }
+#undef RCM_SCB
+      } else {
+#define RCM_SC(NS_) KLAUNCH(k_split_correct<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd,   \
+                            t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], ds, adv, \
+                            red, red_total, dflags)
+        switch (ns) { case 1: RCM_SC(1); break; case 2: RCM_SC(2); break; case 3: RCM_SC(3); break; default: RCM_SC(4); }
+#undef RCM_SC
       }
-      else
-        KLAUNCH(k_split_correct, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, t.psa_[c], t.psb_[c],
-                t.a1t[c], t.a2t[c], t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], ds, (int)(q + 1 == tiles.size()), red,
-                red_total, dflags);
     }
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;

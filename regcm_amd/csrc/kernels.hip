@@ -1086,7 +1086,10 @@ __device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, do
 // pairs start at even j - j0); the second point of a pair may fall in the row padding.
 #define LD2(a, o) (*(const double2*)((const char*)(a) + (uint32_t)(o)))
 #define ST2(a, o, v) (*(double2*)((char*)(a) + (uint32_t)(o)) = (v))
-__global__ __launch_bounds__(256) void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f) {
+#ifndef QF_LB
+#define QF_LB 1
+#endif
+__global__ __launch_bounds__(256, QF_LB) void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f) {
   PT_DECL
   const int jp = g.j0 + 2 * (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int i = g.i0 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
@@ -1520,7 +1523,7 @@ __device__ __forceinline__ int bdy_chunks_d(const Geom& g) { return (max(g.jde2 
 // row/column), which the thread correcting that interior point writes from its registers.
 // The clock is advanced by k_bdyval_qc (advance = 2 here: noise sums only), so the bdyval time
 // level is formed from the clock before the step's advance.
-template <bool BDY>
+template <bool BDY, int NS>
 __device__ __forceinline__ void split_correct_body(
     const Geom& g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum,
     const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
@@ -1580,7 +1583,7 @@ __device__ __forceinline__ void split_correct_body(
   if (jp > g.jdx2() || i > g.idx2()) return;
   const uint32_t o2 = g.o2(jp, i), o3 = o2 + (uint32_t)(k - 1) * g.L8;
   const double gnu1 = c->gnu1;
-  const int ns = c->nsplit;
+  constexpr int ns = NS;       // c->nsplit (the launch picks the instance)
   const int jd2 = g.br ? g.jdi2 : g.jde2 + 1, id2 = g.bt ? g.idi2 : g.ide2 + 1;
   const bool ici = in(i, g.ice1, g.icx2()), idi = in(i, g.idi1, id2);
   const bool ci0 = ici && in(jp, g.jce1, g.jcx2()) && g.gci(jp, i);
@@ -1589,14 +1592,13 @@ __device__ __forceinline__ void split_correct_body(
   // every operand is loaded before the first store (the state buffers are not __restrict__:
   // a store would order the later loads behind it)
   const bool cx = ci0 || ci1, dx = di0 || di1;
-  double dd[2][MAXSPLIT];
+  double dd[2][NS];
   double2 pa{}, pb{}, t1{}, t2{}, u1{}, v1{}, u2{}, v2{}, pd{}, md{};
-  double2 h0[MAXSPLIT], hs[MAXSPLIT];
-  double hw[MAXSPLIT], hsw[MAXSPLIT];
+  double2 h0[NS], hs[NS];
+  double hw[NS], hsw[NS];
   if (cx) {
 #pragma unroll
-    for (int l = 1; l <= MAXSPLIT; l++) {
-      if (l > ns) break;
+    for (int l = 1; l <= NS; l++) {
       const double2 d = LD2(ddsum, o2 + (uint32_t)(l - 1) * g.L8);
       dd[0][l - 1] = d.x; dd[1][l - 1] = d.y;
     }
@@ -1607,8 +1609,7 @@ __device__ __forceinline__ void split_correct_body(
     u1 = LD2(a1u, o3); v1 = LD2(a1v, o3); u2 = LD2(a2u, o3); v2 = LD2(a2v, o3);
     pd = LD2(psdota, o2); md = LD2(msfd, o2);
 #pragma unroll
-    for (int l = 1; l <= MAXSPLIT; l++) {
-      if (l > ns) break;
+    for (int l = 1; l <= NS; l++) {
       const uint32_t lo = o2 + (uint32_t)(l - 1) * g.L8;
       // dhsum at (jp-1..jp+1, i-1..i)
       h0[l - 1] = LD2(dhsum, lo); hs[l - 1] = LD2(dhsum, lo - g.P8);
@@ -1638,8 +1639,7 @@ __device__ __forceinline__ void split_correct_body(
   if (dx) {
     const double fac0 = pd.x / (c->dx2 * md.x), fac1 = pd.y / (c->dx2 * md.y);
 #pragma unroll
-    for (int l = 1; l <= MAXSPLIT; l++) {
-      if (l > ns) break;
+    for (int l = 1; l <= NS; l++) {
       const double zm = c->zmatx[l - 1][k - 1], gnuzm = gnu1 * zm;
       if (di0) {
         const double x = fac0 * (h0[l - 1].x + hs[l - 1].x - hw[l - 1] - hsw[l - 1]);
@@ -1674,12 +1674,16 @@ __device__ __forceinline__ void split_correct_body(
 }
 #undef SLOT
 
-__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
+#ifndef SCOR_LB
+#define SCOR_LB 4
+#endif
+template <int NS>
+__global__ __launch_bounds__(256, SCOR_LB) void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                 const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
                                 double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
                                 int advance, const double* __restrict__ red, int red_total, FlagSnap* ring) {
-  split_correct_body<false>(g, c, ddsum, dhsum, psdota, msfd, psa, psb, a1t, a2t, a1u, a1v, a2u, a2v, s, advance,
+  split_correct_body<false, NS>(g, c, ddsum, dhsum, psdota, msfd, psa, psb, a1t, a2t, a1u, a1v, a2u, a2v, s, advance,
                             red, red_total, ring, BdyArgs{});
 }
 
@@ -1816,13 +1820,32 @@ __device__ __forceinline__ void bdyval_body(const Geom& g, double xt, bool integ
 }
 
 
-__global__ void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
+template <int NS>
+__global__ __launch_bounds__(256, SCOR_LB) void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
                                     const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                     const double* __restrict__ msfd, StepState* s, int advance,
                                     const double* __restrict__ red, int red_total, BdyArgs a) {
-  split_correct_body<true>(g, c, ddsum, dhsum, psdota, msfd, a.psa, a.psb, a.a1t, a.a2t, a.a1u, a.a1v, a.a2u, a.a2v,
+  split_correct_body<true, NS>(g, c, ddsum, dhsum, psdota, msfd, a.psa, a.psb, a.a1t, a.a2t, a.a1u, a.a1v, a.a2u, a.a2v,
                            s, advance ? 2 : 0, red, red_total, nullptr, a);
 }
+
+// one instance per nsplit (1..MAXSPLIT): the mode loops unroll and only the split slots in
+// use hold registers (114 -> fewer VGPRs at nsplit = 2)
+#define RCM_SPLIT_INST(NS_)                                                                                   \
+  template __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct<NS_>(Geom, const Consts* __restrict__, const double* __restrict__, \
+                                                const double* __restrict__, const double* __restrict__,       \
+                                                const double* __restrict__, double*, double*, double*, double*, \
+                                                double*, double*, double*, double*, StepState*, int,          \
+                                                const double* __restrict__, int, FlagSnap*);                 \
+  template __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct_bdy<NS_>(Geom, const Consts* __restrict__, const double* __restrict__, \
+                                                    const double* __restrict__, const double* __restrict__,      \
+                                                    const double* __restrict__, StepState*, int,                 \
+                                                    const double* __restrict__, int, BdyArgs);
+RCM_SPLIT_INST(1)
+RCM_SPLIT_INST(2)
+RCM_SPLIT_INST(3)
+RCM_SPLIT_INST(4)
+#undef RCM_SPLIT_INST
 
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a) {
   const int x = (int)(blockIdx.x * blockDim.x + threadIdx.x);

@@ -80,7 +80,8 @@ __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_fused(Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
-__global__ void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring);
+template <int NS>
+__global__ __launch_bounds__(256) void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring);
 // pointers of bdyval (k_bdyval_set)
 struct BdyArgs {
   double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc, *psa, *psb;
@@ -92,7 +93,8 @@ struct BdyArgs {
 __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a);
 // 64-point chunks of the longest boundary line, one point past the tile included
 inline int bdy_chunks(const Geom& g) { return (std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64; }
-__global__ void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, StepState* s, int advance, const double* __restrict__ red, int red_total, BdyArgs a);
+template <int NS>
+__global__ __launch_bounds__(256) void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, StepState* s, int advance, const double* __restrict__ red, int red_total, BdyArgs a);
 __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance, FlagSnap* ring);
 __global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring);
 __global__ void k_err_gather(const StepState* __restrict__ s, int32_t* derr);
