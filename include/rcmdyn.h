@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RCMDYN_ABI_VERSION 4
+#define RCMDYN_ABI_VERSION 5
 #define RCMDYN_MAXKZ 64
 #define RCMDYN_MAXSPLIT 4
 
@@ -116,8 +116,11 @@ typedef struct rcmdyn_config {
    * and filters (Main/mod_tendency.F90:515-544, 1414-1425, 1545-1548) and bounds
    * (Main/mod_bdycod.F90:1166-1306, 2415-2530); uwparam nuk [5] (its diffusion factor,
    * Main/mod_params.F90:480); tkemin (uwtkemin = 1e-3, Main/pbllib/mod_pbl_uwtcm.F90:86,
-   * Main/mod_pbl_interface.F90:68) */
-  int32_t ibltyp, tke_reserved;
+   * Main/mod_pbl_interface.F90:68).  uwparam iuwvadv [0]: with ibltyp = 2, 1 selects the
+   * PBL-aware vertical flux of the hydrometeors (vadv4d ind = 3, iqxvadv = 3,
+   * Main/mod_tendency.F90:148-154, Main/mod_advection.F90:917-961), which reads the host's
+   * KPBL field; ignored unless ibltyp = 2, as in the reference */
+  int32_t ibltyp, iuwvadv;
   double nuk, tkemin;
 } rcmdyn_config;
 
@@ -179,6 +182,12 @@ enum rcmdyn_field {
    * levels (Main/mod_atm_interface.F90), and the pc_physic tendency the UW scheme produces
    * (put, like the *PHY fields; added to the advective tendency, :530-531) */
   RCMDYN_ATM1_TKE, RCMDYN_ATM2_TKE, RCMDYN_TKEPHY,
+  /* kpbl (put, ibltyp = 2): the PBL-top level index per cross point that the UW scheme sets
+   * each step (Main/mod_atm_interface.F90:136, 1135: jci1:jci2 x ici1:ici2), as doubles
+   * holding integers; read by the iuwvadv = 1 vertical flux.  A value above kz is refused
+   * ('kpbl is greater than kz', Main/mod_advection.F90:923-925); below 4 the column keeps
+   * the plain interpolated flux.  Zero until put. */
+  RCMDYN_KPBL,
   RCMDYN_NFIELDS
 };
 

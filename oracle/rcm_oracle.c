@@ -11,7 +11,7 @@
  *
  * Scope (defaults assumed): idynamic=1, upstream_mode and
  * stability_enhance on, idiffu=1, iboudy=5 (or 1), ipgf=0, nsplit from config,
- * nqx=2 (qv,qc), isladvec=0/1, ibltyp!=2, ichem=0, idiag=0, iboudy time-dependent.
+ * nqx=2 (qv,qc), isladvec=0/1, ibltyp=1/2 (iuwvadv 0/1), ichem=0, idiag=0, iboudy time-dependent.
  *
  * Parity unpinned: no execution of the reference is available (netCDF-Fortran absent),
  * no golden vectors exist in the reference tree.
@@ -127,6 +127,7 @@ struct orc {
   double *phy[7], *atms[22];
   /* UW PBL TKE (ibltyp = 2): atm1/atm2 tke, atmc%tke, tkedyn, tkeps, the pc_physic tendency */
   double *a1tke, *a2tke, *ctke, *tkedyn, *tkeps, *tkephy;
+  double* kpbl;      /* ibltyp = 2: the UW scheme's PBL-top level (put; iuwvadv = 1 reads it) */
   /* bdyin: raw record (u, v, t, qv, ps, pp, w), coupled b1 (same order), NH atm0%psdot */
   double *bin[7], *bb1[7], *psdot0;
   double rhmin, rhmax;
@@ -401,6 +402,7 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   if (cfg->ibltyp == 2) {
     o->a1tke = alloc3(o, kp); o->a2tke = alloc3(o, kp); o->ctke = alloc3(o, kp);
     o->tkedyn = alloc3(o, kp); o->tkeps = alloc3(o, kp); o->tkephy = alloc3(o, kp);
+    o->kpbl = alloc3(o, 1);
     if (!o->nh) o->xkcf = alloc3(o, kp);
   }
   if (o->nh) { o->phy[5] = alloc3(o, kz); o->phy[6] = alloc3(o, kp); }
@@ -449,6 +451,7 @@ void orc_destroy(orc_t* o) {
   for (size_t p = 0; p < sizeof(nhp) / sizeof(nhp[0]); p++) free(*nhp[p]);
   for (int q = 0; q < 7; q++) free(o->phy[q]);
   free(o->a1tke); free(o->a2tke); free(o->ctke); free(o->tkedyn); free(o->tkeps); free(o->tkephy);
+  free(o->kpbl);
   /* xkcf (also allocated for the hydrostatic core with ibltyp = 2) is in the list above */
   for (int q = 0; q < 22; q++) free(o->atms[q]);
   for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
@@ -508,6 +511,7 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     *nk = o->kz + 1;
     return f == RCMDYN_ATM1_TKE ? o->a1tke : f == RCMDYN_ATM2_TKE ? o->a2tke : o->tkephy;
   }
+  if (f == RCMDYN_KPBL) { *nk = 1; return o->kpbl; }
   switch (f) {
     case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
     case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
@@ -1198,9 +1202,53 @@ static void vadvqv(orc_t* o) {                                     /* :811-836 *
       }
 }
 
-static void vadv4d_qc(orc_t* o) {                                  /* :859-961, ind = 1 */
+/* vadv4d ind = 3 (iqxvadv = 3: ibltyp = 2 with iuwvadv = 1, Main/mod_tendency.F90:148-154),
+ * Main/mod_advection.F90:917-957: fg = twt-interpolated f on every interface, the PBL-top
+ * rule at kpb - 1 and kpb, then fg * svv.  fg is zeroed by the caller (:860). */
+static void vadv4d_qc_uw(orc_t* o, const double* f) {
+  for (int i = o->ici1; i <= o->ici2; i++)                            /* :918-920 */
+    for (int j = o->jci1; j <= o->jci2; j++)
+      for (int k = 2; k <= o->kz; k++)
+        A3(o->fg, j, i, k) = o->twt1[k] * A3(f, j, i, k) + o->twt2[k] * A3(f, j, i, k - 1);
+  for (int i = o->ici1; i <= o->ici2; i++)
+    for (int j = o->jci1; j <= o->jci2; j++) {
+      const int kpb = (int)A2(o->kpbl, j, i);
+      if (kpb > o->kz) {                                              /* :923-925 (refused at put) */
+        fprintf(stderr, "oracle: kpbl is greater than kz\n");
+        abort();
+      }
+      if (kpb >= 4) {                                                 /* :926-955 */
+        double slope;
+        int k = kpb - 2;
+        if ((A3(f, j, i, k + 1) - A3(f, j, i, k)) > d_zero && (A3(f, j, i, k) - A3(f, j, i, k - 1)) > d_zero) {
+          slope = dmin((A3(f, j, i, k + 1) - A3(f, j, i, k)) / (o->hsigma[k + 1] - o->hsigma[k]),
+                        (A3(f, j, i, k) - A3(f, j, i, k - 1)) / (o->hsigma[k] - o->hsigma[k - 1]));
+        } else if ((A3(f, j, i, k + 1) - A3(f, j, i, k)) < d_zero && (A3(f, j, i, k) - A3(f, j, i, k - 1)) < d_zero) {
+          slope = dmax((A3(f, j, i, k + 1) - A3(f, j, i, k)) / (o->hsigma[k + 1] - o->hsigma[k]),
+                        (A3(f, j, i, k) - A3(f, j, i, k - 1)) / (o->hsigma[k] - o->hsigma[k - 1]));
+        } else {
+          slope = d_zero;
+        }
+        k = kpb;
+        A3(o->fg, j, i, k - 1) = A3(f, j, i, k - 2) + slope * (o->sigma[k - 1] - o->hsigma[k - 2]);
+        if (fabs(A3(f, j, i, k - 2) + slope * (o->hsigma[k - 1] - o->hsigma[k - 2]) - A3(f, j, i, k)) >
+            fabs(A3(f, j, i, k - 1) - A3(f, j, i, k))) {
+          A3(o->fg, j, i, k) = A3(f, j, i, k);
+        } else {
+          A3(o->fg, j, i, k) = A3(f, j, i, k - 2) + slope * (o->sigma[k] - o->hsigma[k - 2]);
+        }
+      }
+    }
+  for (int k = 2; k <= o->kz; k++)                                    /* :957 */
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) A3(o->fg, j, i, k) = A3(o->fg, j, i, k) * A3(o->qdot, j, i, k);
+}
+
+static void vadv4d_qc(orc_t* o) {                          /* :859-961, ind = 1 (or 3: iuwvadv) */
   const double* f = o->a1q[1];
   memset(o->fg, 0, sizeof(double) * o->plane * o->kz);
+  if (o->cfg.ibltyp == 2 && o->cfg.iuwvadv == 1) vadv4d_qc_uw(o, f);
+  else
   for (int k = 2; k <= o->kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {

@@ -17,7 +17,7 @@ import numpy as np
 
 MAXKZ = 64
 MAXSPLIT = 4
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # Share/mod_sigma.F90:88-152 -- the hard-coded sigma tables (data, cited).
 SIGMA_TABLES = {
@@ -74,7 +74,7 @@ class RcmdynConfig(ctypes.Structure):
         ("nh_dtsmax", ctypes.c_double), ("nh_xmsf", ctypes.c_double),
         ("rhmin", ctypes.c_double), ("rhmax", ctypes.c_double),
         ("isladvec", ctypes.c_int32), ("iqmsl", ctypes.c_int32),
-        ("ibltyp", ctypes.c_int32), ("tke_reserved", ctypes.c_int32),
+        ("ibltyp", ctypes.c_int32), ("iuwvadv", ctypes.c_int32),
         ("nuk", ctypes.c_double), ("tkemin", ctypes.c_double),
     ]
 
@@ -97,12 +97,12 @@ FIELD_NAMES = [
     "ATMS_TV3D", "ATMS_PB3D", "ATMS_PF3D", "ATMS_PS2D", "ATMS_RHOX2D", "ATMS_TH3D", "ATMS_RHOB3D",
     "ATMS_TP3D", "ATMS_WPX3D", "ATMS_WB3D", "ATMS_ZQ", "ATMS_ZA", "ATMS_DZQ", "ATMS_QSB3D", "ATMS_RHB3D",
     "XUB_B1", "XVB_B1", "XTB_B1", "XQB_B1", "XPSB_B1", "XPPB_B1", "XWWB_B1", "ATM0_PSDOT",
-    "ATM1_TKE", "ATM2_TKE", "TKEPHY",
+    "ATM1_TKE", "ATM2_TKE", "TKEPHY", "KPBL",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
          "PTEN", "PSDOTA", "ATM0_PS", "DPSDXM", "DPSDYM", "EF", "DDX", "DDY", "DMDX", "DMDY",
-         "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D", "XPSB_B1", "ATM0_PSDOT"}
+         "EX", "CRX", "CRY", "ATMS_PS2D", "ATMS_RHOX2D", "XPSB_B1", "ATM0_PSDOT", "KPBL"}
 FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM0_RHOF",
                "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ", "XWWB_B1",
                "ATM1_TKE", "ATM2_TKE", "TKEPHY"}
@@ -181,6 +181,7 @@ class RunConfig:
     iqmsl: int = 1
     ibltyp: int = 1                  # physicsparam; 2 = UW PBL (TKE advected by the dyn step)
     nuk: float = 5.0                 # uwparam, Main/mod_params.F90:480
+    iuwvadv: int = 0                 # uwparam; 1 with ibltyp = 2: PBL-aware qc vertical flux (vadv4d ind = 3)
     tkemin: float = 1.0e-3           # uwtkemin, Main/pbllib/mod_pbl_uwtcm.F90:86
     nhbet: float = 0.4
     nhxkd: float = 0.1
@@ -278,6 +279,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.rhmin, c.rhmax = rc.rhmin, rc.rhmax
     c.isladvec, c.iqmsl = rc.isladvec, rc.iqmsl
     c.ibltyp, c.nuk, c.tkemin = rc.ibltyp, rc.nuk, rc.tkemin
+    c.iuwvadv = rc.iuwvadv
     if rc.idynamic == 2:
         c.nh_dtsmax = split["nh_dtsmax"]
         c.nh_xmsf = split["nh_xmsf"]

@@ -96,4 +96,31 @@ __device__ __forceinline__ double psc2psd_global(const Geom& g, const double* pc
   return F2(pc, (j == 1) ? 1 : jx - 1, (i == 1) ? 1 : iy - 1);
 }
 
+// vadv4d ind = 3 (iuwvadv = 1 with ibltyp = 2, Main/mod_advection.F90:917-957): the hydrometeor
+// interface value at interface kk (2..kz) before the svv factor.  The linear interpolation
+// twt(kk,1) f(kk) + twt(kk,2) f(kk-1), replaced at kpb - 1 and kpb (kpb >= 4) by the PBL-top
+// rule: a slope from the layer above the ambiguous one (levels kpb-3..kpb-1, zero unless f is
+// monotone there), extended from f(kpb-2) to the interfaces; at kpb the extension is kept only
+// if it does not overshoot f(kpb) by more than f(kpb-1) does.  fk(k) reads f at level k of the
+// column (called only on the two replaced interfaces).
+template <class FK>
+__device__ __forceinline__ double uw_fg(const Consts* c, int kk, int kpb, double fkk, double fkm, FK fk) {
+  if (kpb >= 4 && (kk == kpb - 1 || kk == kpb)) {
+    const int k0 = kpb - 2;
+    const double fp = fk(k0 + 1), f0 = fk(k0), fm = fk(k0 - 1), fb = fk(kpb);
+    double slope;
+    if ((fp - f0) > d_zero && (f0 - fm) > d_zero)
+      slope = dmin((fp - f0) / (c->hsigma[k0 + 1] - c->hsigma[k0]), (f0 - fm) / (c->hsigma[k0] - c->hsigma[k0 - 1]));
+    else if ((fp - f0) < d_zero && (f0 - fm) < d_zero)
+      slope = dmax((fp - f0) / (c->hsigma[k0 + 1] - c->hsigma[k0]), (f0 - fm) / (c->hsigma[k0] - c->hsigma[k0 - 1]));
+    else
+      slope = d_zero;
+    // f(kpb-2) = f0, f(kpb-1) = fp
+    if (kk == kpb - 1) return f0 + slope * (c->sigma[kpb - 1] - c->hsigma[kpb - 2]);
+    if (fabs(f0 + slope * (c->hsigma[kpb - 1] - c->hsigma[kpb - 2]) - fb) > fabs(fp - fb)) return fb;
+    return f0 + slope * (c->sigma[kpb] - c->hsigma[kpb - 2]);
+  }
+  return c->twt1[kk] * fkk + c->twt2[kk] * fkm;
+}
+
 }  // namespace rcm

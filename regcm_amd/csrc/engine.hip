@@ -375,6 +375,7 @@ struct rcmdyn_engine {
     c.dds[1] = 0.0; c.dds[kz + 1] = 0.0;                            // Main/mod_advection.F90:101-105
     for (int k = 2; k <= kz; k++) c.dds[k] = 1.0 / (c.dsigma[k] + c.dsigma[k - 1]);
     c.ibltyp = cfg.ibltyp; c.nuk = cfg.nuk; c.tkemin = cfg.tkemin;
+    c.iqxvadv = (cfg.ibltyp == 2 && cfg.iuwvadv == 1) ? 3 : 1;
   }
 
   double* dalloc(Tile& t, size_t n) {
@@ -430,6 +431,7 @@ struct rcmdyn_engine {
     if (cfg.isladvec == 1) { t.slqv = dalloc(t, P3); t.slqc = dalloc(t, P3); }
     if (cfg.ibltyp == 2) {
       t.a1tke = dalloc(t, P * (kz + 1)); t.a2tke = dalloc(t, P * (kz + 1)); t.ctke = dalloc(t, P * (kz + 1));
+      t.kpbl = dalloc(t, P);
     }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     t.depplane = talloc<int>(t, 2 * kz);
@@ -557,6 +559,7 @@ struct rcmdyn_engine {
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.ppphy = t.phy[5]; f.wphy = t.phy[6];
     f.slqv = t.slqv; f.slqc = t.slqc;
+    f.kpbl = hc.iqxvadv == 3 ? t.kpbl : nullptr;
     return f;
   }
 
@@ -574,6 +577,7 @@ struct rcmdyn_engine {
     if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
+    if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
     // dynparam's upstream_mode (default .true., Main/mod_params.F90:646): the centred
@@ -833,6 +837,7 @@ struct rcmdyn_engine {
       nk = cfg.kz + 1;
       return f == RCMDYN_ATM1_TKE ? t.a1tke : f == RCMDYN_ATM2_TKE ? t.a2tke : t.tkephy;
     }
+    if (f == RCMDYN_KPBL) { nk = 1; return t.kpbl; }
     if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
       if (cfg.idynamic != 2) return nullptr;
       NHFields& h = nhf[&t - tiles.data()];
@@ -897,11 +902,19 @@ struct rcmdyn_engine {
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
     const bool phyf = f >= RCMDYN_TPHY && f <= RCMDYN_WPHY;
     const bool binf = f >= RCMDYN_XUB_B1 && f <= RCMDYN_ATM0_PSDOT;
-    const bool tkef = f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY;
+    const bool tkef = (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) || f == RCMDYN_KPBL;
     if (f < 0 || f >= RCMDYN_NFIELDS || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) ||
         (f > RCMDYN_CRY && !phyf && !binf && !tkef))
       throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
-    if (tkef && cfg.ibltyp != 2) throw std::runtime_error("rcmdyn_put: TKE fields need ibltyp=2 (UW PBL)");
+    if (tkef && cfg.ibltyp != 2) throw std::runtime_error("rcmdyn_put: TKE/kpbl fields need ibltyp=2 (UW PBL)");
+    if (f == RCMDYN_KPBL) {
+      // vadv4d ind = 3 stops on a PBL top above the model (Main/mod_advection.F90:923-925)
+      const size_t n = (size_t)(j2 - j1 + 1) * (i2 - i1 + 1) * std::max(1, k2 - k1 + 1);
+      for (size_t q = 0; q < n; q++) {
+        if (src[q] > cfg.kz) throw std::runtime_error("rcmdyn_put: kpbl is greater than kz");
+        if (src[q] != std::floor(src[q])) throw std::runtime_error("rcmdyn_put: kpbl must hold integers");
+      }
+    }
     if (f == RCMDYN_TKEPHY && !tiles.empty() && !tiles[0].tkephy) {
       HIPCHK(hipStreamSynchronize(stream));
       for (auto& t : tiles) t.tkephy = dalloc(t, t.g.plane * (cfg.kz + 1));
@@ -1043,8 +1056,8 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY && !tiles[0].phy[0])
       throw std::runtime_error("rcmdyn_get: no physics tendencies were put");
-    if (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY && cfg.ibltyp != 2)
-      throw std::runtime_error("rcmdyn_get: TKE fields need ibltyp=2 (UW PBL)");
+    if (((f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) || f == RCMDYN_KPBL) && cfg.ibltyp != 2)
+      throw std::runtime_error("rcmdyn_get: TKE/kpbl fields need ibltyp=2 (UW PBL)");
     if (f == RCMDYN_TKEPHY && !tiles[0].tkephy) throw std::runtime_error("rcmdyn_get: no TKE tendency was put");
     HIPCHK(hipStreamSynchronize(stream));
     check_now();
@@ -1390,6 +1403,7 @@ struct rcmdyn_engine {
       f.omega = t.omega; f.xkcs = t.xkcs;
     }
     if (cfg.ibltyp == 2) f.xkcs = t.xkcs;     // the TKE diffusion reads xkcf from it
+    if (hc.iqxvadv == 3) f.kpbl = t.kpbl;    // vadv4d ind = 3 of qc
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.red = red; f.red_off = t.red_off;
     return f;

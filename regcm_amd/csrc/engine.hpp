@@ -80,7 +80,9 @@ struct Geom {
 struct Consts {
   int kz, nsplit, iboudy, nspgx, stability_enhance, present_qc, ipgf, idiffu;
   int isladvec, iqmsl;                 // semi-Lagrangian moisture advection (physicsparam)
-  int ibltyp, tke_pad;                 // 2: UW PBL TKE advected/diffused/filtered (tke.hip)
+  int ibltyp, iqxvadv;                 // 2: UW PBL TKE advected/diffused/filtered (tke.hip);
+                                       // iqxvadv: vadv4d ind of the hydrometeors (3: ibltyp = 2
+                                       // with iuwvadv = 1, Main/mod_tendency.F90:148-154; else 1)
   double nuk, tkemin;
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
@@ -147,6 +149,7 @@ struct Tile {
   // ibltyp = 2: atm1/atm2 tke (decoupled, kz+1 levels), the forecast atmc%tke, and the UW
   // scheme's tendency (allocated on its first put)
   double *a1tke = nullptr, *a2tke = nullptr, *ctke = nullptr, *tkephy = nullptr;
+  double* kpbl = nullptr;          // ibltyp = 2: the UW scheme's PBL-top level (put, 2-D)
   double *cqv, *cqc, *fqv, *fqc;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;

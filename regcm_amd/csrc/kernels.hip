@@ -1002,7 +1002,13 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
                           : d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXQC, 0, 0),
                                                H1T(sXQC, -1, 0), H1T(sXQC, 1, 0), H1T(sXQC, 0, -1),
                                                H1T(sXQC, 0, 1), 0);
-  {
+  if (f.kpbl) {
+    // vadv4d ind = 3 (iuwvadv = 1): no positivity threshold, the PBL-top rule at kpbl
+    const int kpb = (int)LD(f.kpbl, o2);
+    auto fk = [&](int kk) { return LD(f.a1qc, o2 + (uint32_t)(kk - 1) * L8); };
+    if (k >= 2) tc = tc + (uw_fg(c, k, kpb, qc1, qc1m, fk) * q0) * c->xds[k];
+    if (k + 1 <= kz) tc = tc - (uw_fg(c, k + 1, kpb, qc1p, qc1, fk) * q1) * c->xds[k];
+  } else {
     const double thr = MINQQ * MINQQ * ps;
     const double c0 = qc1;
     if (k >= 2) {

@@ -47,6 +47,7 @@ struct Fields {
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy;
+  const double* kpbl;          // iuwvadv = 1 (ibltyp = 2): the PBL-top level, vadv4d ind = 3 of qc
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
   int red_off;                 // this tile's first partial
 };

@@ -512,9 +512,12 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double cd = d_zero + (c->isladvec ? F3(f.slqc, j, i, k)
                                       : hadx(f.a1qc, 2, u1, u2, v1, v2, 0));
     const double thr = MINQQ * MINQQ * ps;
+    const int kpb = f.kpbl ? (int)F2(f.kpbl, j, i) : 0;
     auto cflux = [&](int kk) {
       const double svv = F3(f.qdot, j, i, kk);
       const double fk = F3(f.a1qc, j, i, kk), fkm = F3(f.a1qc, j, i, kk - 1);
+      // vadv4d ind = 3 (iuwvadv = 1): no threshold, the PBL-top rule at kpbl
+      if (f.kpbl) return uw_fg(c, kk, kpb, fk, fkm, [&](int q) { return F3(f.a1qc, j, i, q); }) * svv;
       if (svv > d_zero) return (fkm > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
       return (fk > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
     };

@@ -34,6 +34,8 @@ struct NHFields {
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy, *ppphy, *wphy;
   // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv; null otherwise)
   const double *slqv, *slqc;
+  // iuwvadv = 1 (ibltyp = 2): the PBL-top level of vadv4d ind = 3 (null otherwise)
+  const double* kpbl;
   // forecasts (atmc) and fixed moisture
   double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
   int* depplane;

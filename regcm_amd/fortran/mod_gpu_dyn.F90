@@ -11,7 +11,7 @@ module mod_gpu_dyn
   implicit none
   private
 
-  integer, parameter, public :: rcmdyn_abi_version = 4
+  integer, parameter, public :: rcmdyn_abi_version = 5
   integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
 
   ! field ids (enum rcmdyn_field)
@@ -40,7 +40,7 @@ module mod_gpu_dyn
     ! device bdyin: the next ICBC record as read_icbc returns it; NH atm0%psdot
     f_xub_b1 = 97, f_xvb_b1 = 98, f_xtb_b1 = 99, f_xqb_b1 = 100, f_xpsb_b1 = 101, &
     f_xppb_b1 = 102, f_xwwb_b1 = 103, f_atm0_psdot = 104, &
-    f_atm1_tke = 105, f_atm2_tke = 106, f_tkephy = 107
+    f_atm1_tke = 105, f_atm2_tke = 106, f_tkephy = 107, f_kpbl = 108
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -71,8 +71,8 @@ module mod_gpu_dyn
     real(c_double) :: rhmin, rhmax
     ! physicsparam isladvec, iqmsl (semi-Lagrangian moisture advection)
     integer(c_int32_t) :: isladvec, iqmsl
-    ! physicsparam ibltyp (2 = UW PBL TKE in the dyn step), uwparam nuk, tkemin (uwtkemin)
-    integer(c_int32_t) :: ibltyp, tke_reserved
+    ! physicsparam ibltyp (2 = UW PBL TKE in the dyn step), uwparam iuwvadv, nuk, tkemin (uwtkemin)
+    integer(c_int32_t) :: ibltyp, iuwvadv
     real(c_double) :: nuk, tkemin
   end type rcmdyn_config
 

@@ -857,6 +857,117 @@ def test_hydrostatic_temperature_tendency_matches_numpy_restatement():
         np.testing.assert_allclose(got, want, rtol=1e-10, atol=1e-11 * np.abs(want).max(), err_msg=name)
 
 
+def _uw_kpbl(rc, seed=5):
+    """A PBL-top field for iuwvadv = 1: every value 1..kz, most columns >= 4 (the rule acts)."""
+    rng = np.random.default_rng(seed)
+    k = rng.integers(1, rc.kz + 1, size=(1, rc.iy, rc.jx)).astype(np.float64)
+    return k
+
+
+def _uw_qc_state(rc, state, seed=6):
+    """A cloud layer with level-to-level structure, so the PBL-top slopes take every branch
+    (monotone up, monotone down, mixed) across the columns."""
+    rng = np.random.default_rng(seed)
+    st = dict(state)
+    for a1, a2 in (("ATM1_QC", "ATM1_QV"), ("ATM2_QC", "ATM2_QV")):
+        st[a1] = state[a2] * rng.uniform(0.0, 0.02, size=state[a2].shape)
+    return st
+
+
+@pytest.mark.parametrize("idynamic", [1, 2])
+def test_uw_vertical_flux_matches_numpy_restatement(idynamic):
+    """vadv4d ind = 3 (ibltyp = 2 with iuwvadv = 1, Main/mod_tendency.F90:148-154,
+    Main/mod_advection.F90:917-961) against an independent NumPy restatement: the first step's
+    qc tendency with iuwvadv = 1 minus the one with iuwvadv = 0 is the difference of the two
+    vertical fluxes (everything else in the qc chain is the same computation): the
+    twt-interpolated interface values, replaced at kpbl - 1 and kpbl by the PBL-top slope rule
+    for kpbl >= 4, times qdot, against ind = 1's thresholded form."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    if idynamic == 1:
+        rc = dataclasses.replace(CONFIGS["C1"], ibltyp=2)
+        data = icbc.generate(rc)
+    else:
+        rc = dataclasses.replace(CONFIGS["N1"], ibltyp=2)
+        data = icbc.generate_nh(rc)
+    st = _uw_qc_state(rc, data["state"])
+    st.update(icbc.tke_state(rc))
+    kpbl = _uw_kpbl(rc)
+    out = {}
+    for uw in (0, 1):
+        o = OracleCore(dataclasses.replace(rc, iuwvadv=uw), data["split"])
+        o.put_state(st)
+        o.put("KPBL", kpbl)
+        o.bdyval()
+        f = o.get("ATM1_QC")
+        psa = o.get("PSA")[0]
+        o.tend()
+        out[uw] = o.get("QCTEN")
+        qdot = o.get("QDOT")
+        o.close()
+    kz = rc.kz
+    sig = np.asarray(rc.sigma)
+    hsig = (sig[1:] + sig[:-1]) * 0.5
+    dsig = sig[1:] - sig[:-1]
+    xds = 1.0 / dsig
+    twt1 = np.zeros(kz + 1); twt2 = np.zeros(kz + 1)
+    for k in range(2, kz + 1):
+        twt1[k] = (sig[k - 1] - hsig[k - 2]) / (hsig[k - 1] - hsig[k - 2])
+        twt2[k] = 1.0 - twt1[k]
+    F = lambda k: f[k - 1]                        # noqa: E731  (1-based level, [i, j] plane)
+    H = lambda k: hsig[k - 1]                     # noqa: E731
+    S = lambda k: sig[k - 1]                      # noqa: E731
+    # ind = 1
+    fg1 = np.zeros((kz + 1,) + psa.shape)
+    thr = 1.0e-8 * 1.0e-8 * psa
+    for k in range(2, kz + 1):
+        svv = qdot[k - 1]
+        lin = svv * (twt1[k] * F(k) + twt2[k] * F(k - 1))
+        fg1[k] = np.where(svv > 0.0, np.where(F(k - 1) > thr, lin, 0.0), np.where(F(k) > thr, lin, 0.0))
+    # ind = 3, column by column as the reference loops
+    fg3 = np.zeros_like(fg1)
+    for k in range(2, kz + 1):
+        fg3[k] = twt1[k] * F(k) + twt2[k] * F(k - 1)
+    kp = kpbl[0].astype(int)
+    ni, nj = psa.shape
+    for i in range(ni):
+        for j in range(nj):
+            kpb = kp[i, j]
+            if kpb < 4:
+                continue
+            col = lambda k: F(k)[i, j]            # noqa: E731
+            k = kpb - 2
+            d1, d0 = col(k + 1) - col(k), col(k) - col(k - 1)
+            if d1 > 0.0 and d0 > 0.0:
+                slope = min(d1 / (H(k + 1) - H(k)), d0 / (H(k) - H(k - 1)))
+            elif d1 < 0.0 and d0 < 0.0:
+                slope = max(d1 / (H(k + 1) - H(k)), d0 / (H(k) - H(k - 1)))
+            else:
+                slope = 0.0
+            k = kpb
+            fg3[k - 1][i, j] = col(k - 2) + slope * (S(k - 1) - H(k - 2))
+            if abs(col(k - 2) + slope * (H(k - 1) - H(k - 2)) - col(k)) > abs(col(k - 1) - col(k)):
+                fg3[k][i, j] = col(k)
+            else:
+                fg3[k][i, j] = col(k - 2) + slope * (S(k) - H(k - 2))
+    for k in range(2, kz + 1):
+        fg3[k] = fg3[k] * qdot[k - 1]
+
+    def ten(fg):
+        t = np.zeros((kz,) + psa.shape)
+        for k in range(2, kz + 1):
+            t[k - 2] -= fg[k] * xds[k - 2]
+            t[k - 1] += fg[k] * xds[k - 1]
+        return t
+    want = ten(fg3) - ten(fg1)
+    got = out[1] - out[0]
+    sc = (slice(None), slice(1, rc.iy - 2), slice(1, rc.jx - 2))     # ici x jci
+    assert np.abs(want[sc]).max() > 0.0
+    changed = np.abs(want[sc]) > 0.0
+    assert changed.any() and not changed.all()
+    np.testing.assert_allclose(got[sc], want[sc], rtol=1e-9, atol=1e-12 * np.abs(out[0][sc]).max())
+
+
 def test_hydrostatic_wind_tendency_matches_numpy_restatement():
     """The hydrostatic u, v tendencies of the first step against an independent NumPy
     restatement of the reference (C1, no diffusion, dot points off the band): hadvuv's

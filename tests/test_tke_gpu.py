@@ -172,3 +172,82 @@ def test_tke_restart_bit_identical(tke_c1):
     rst.step(3)
     for n in names:
         assert np.array_equal(rst.get(n), ref.get(n)), n
+
+
+def _uw(rc, data):
+    """iuwvadv = 1 state: a structured cloud layer and a PBL-top field (tests/test_oracle_cpu.py)."""
+    from tests.test_oracle_cpu import _uw_kpbl, _uw_qc_state
+    return dataclasses.replace(rc, iuwvadv=1), _uw_qc_state(rc, data["state"]), _uw_kpbl(rc)
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_uw_vertical_flux_parity(tke_c1, tke_n1, core):
+    """iuwvadv = 1 (vadv4d ind = 3 of qc with the host's kpbl, Main/mod_advection.F90:917-961):
+    the engine against the oracle, both cores, with a new kpbl put between the steps as the UW
+    scheme does; the qc tendency differs from iuwvadv = 0's.  One step within 1e-11.  Later
+    steps are held to the oracle's own spread under a 1e-14 perturbation of t: the rule's
+    overshoot test at kpbl compares |f(kpb-2) + slope dh - f(kpb)| with |f(kpb-1) - f(kpb)|,
+    which are the same number whenever the min/max picks the upper layer's gradient, so an
+    ulp of input difference (the log/pow of the PGF reach qdot) decides that branch."""
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    rc, data = tke_c1 if core == "hydrostatic" else tke_n1
+    rcu, st, kpbl = _uw(rc, data)
+    kpbl2 = np.roll(kpbl, 3, axis=-1)
+
+    def start(cls, state):
+        c = cls(rcu, data["split"])
+        c.put_state(state)
+        for name, a in icbc.tke_state(rcu).items():
+            c.put(name, a)
+        c.put("KPBL", kpbl)
+        c.bdyval()
+        return c
+    o, e = start(OracleCore, st), start(DynCore, st)
+    stp = dict(st)
+    stp["ATM1_T"] = st["ATM1_T"] * (1.0 + 1e-14)
+    p = start(OracleCore, stp)
+    for n, c in enumerate((o, e, p)):
+        c.step(1)
+        if n < 2:
+            for name in STATE_FIELDS:
+                err = relerr(e.get(name), o.get(name), rcu, name) if n == 1 else 0.0
+                assert err < 1e-11, (name, err)
+    for c in (o, e, p):
+        c.put("KPBL", kpbl2)
+        c.step(3)
+    for name in STATE_FIELDS:
+        err = relerr(e.get(name), o.get(name), rcu, name)
+        spread = relerr(p.get(name), o.get(name), rcu, name)
+        assert err <= max(1e-10, 100.0 * spread), (name, err, spread)
+    base = DynCore(rc, data["split"])
+    base.put_state(st)
+    for name, a in icbc.tke_state(rc).items():
+        base.put(name, a)
+    base.bdyval()
+    base.step(4)
+    assert not np.array_equal(base.get("ATM1_QC"), e.get("ATM1_QC"))
+
+
+def test_uw_decomposition_and_refusal(tke_c1):
+    """iuwvadv = 1 is bit-identical on 2 x 2 tiles; a kpbl above kz is refused at the put
+    ('kpbl is greater than kz', Main/mod_advection.F90:923-925)."""
+    from regcm_amd.dycore import DynCore, EngineError
+    rc, data = tke_c1
+    rcu, st, kpbl = _uw(rc, data)
+    runs = []
+    for nproc in ((1, 1), (2, 2)):
+        e = DynCore(rcu, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+        e.put_state(st)
+        for name, a in icbc.tke_state(rcu).items():
+            e.put(name, a)
+        e.put("KPBL", kpbl)
+        e.bdyval()
+        e.step(4)
+        runs.append(e)
+    for name in STATE_FIELDS:
+        assert np.array_equal(runs[0].get(name), runs[1].get(name)), name
+    bad = kpbl.copy()
+    bad[0, 5, 5] = rcu.kz + 1
+    with pytest.raises(EngineError, match="kpbl is greater than kz"):
+        runs[0].put("KPBL", bad)
