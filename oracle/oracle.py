@@ -44,6 +44,8 @@ def lib():
         L.orc_frame_info.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         L.orc_put.argtypes = [P, i, dp, i, i, i, i, i, i]
         L.orc_get.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_get_work.restype = i
+        L.orc_get_work.argtypes = [P, ctypes.c_char_p, dp, ctypes.c_size_t]
         L.orc_set_time.argtypes = [P, ctypes.c_longlong, ctypes.c_double, ctypes.c_double]
         L.orc_get_time.argtypes = [P, ctypes.POINTER(ctypes.c_longlong),
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
@@ -119,6 +121,20 @@ class OracleCore:
     def put_state(self, st):
         for name, arr in st.items():
             self.put(name, arr)
+
+    def get_work(self, name):
+        """An internal work array (orc_get_work) on the global (iy, jx) grid of a one-tile
+        oracle: [k][i][j], global 1-based (j, i) at [.., i-1, j-1]."""
+        info = (ctypes.c_int * 16)()
+        lib().orc_frame_info(self.h, info)
+        j0, i0, nj, ni = info[0], info[1], info[2], info[3]
+        buf = np.zeros((self.rc.kz + 1) * ni * nj)
+        nk = lib().orc_get_work(self.h, name.encode(), buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                buf.size)
+        if not nk:
+            raise KeyError(name)
+        fr = buf[: nk * ni * nj].reshape(nk, ni, nj)
+        return fr[:, 1 - i0: 1 - i0 + self.rc.iy, 1 - j0: 1 - j0 + self.rc.jx].copy()
 
     def set_time(self, lcount, dt, xbctime):
         lib().orc_set_time(self.h, lcount, dt, xbctime)

@@ -582,6 +582,22 @@ int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int 
   return 0;
 }
 
+/* Test hook: a copy of one internal work array over the whole frame ([k][i][j], nk levels,
+ * the layout of orc_frame_info), for the NumPy restatement checks of terms that no rcmdyn
+ * field exports (the NH pp/w tendencies after tend, as sound leaves them).  Returns nk, or
+ * 0 for an unknown name or a too small buffer. */
+int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
+  const double* a = NULL;
+  int nk = o->kz;
+  if (!strcmp(name, "uten")) a = o->uten;
+  else if (!strcmp(name, "vten")) a = o->vten;
+  else if (o->nh && !strcmp(name, "ppten")) a = o->ppten;
+  else if (o->nh && !strcmp(name, "wten")) { a = o->wten; nk = o->kz + 1; }
+  if (!a || cap < o->plane * (size_t)nk) return 0;
+  memcpy(dst, a, sizeof(double) * o->plane * (size_t)nk);
+  return nk;
+}
+
 int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
   int nk; double* a = field_ptr(o, field, &nk);
   if (!a) return 1;

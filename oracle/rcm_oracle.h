@@ -18,6 +18,7 @@
  */
 #ifndef RCM_ORACLE_H
 #define RCM_ORACLE_H
+#include <stddef.h>
 #include "../include/rcmdyn.h"
 
 #ifdef __cplusplus
@@ -53,6 +54,9 @@ void orc_set_exchange(orc_t* o, orc_exchange_fn fn, orc_exchange_bdy_fn bfn, voi
 void orc_frame_info(const orc_t* o, int info[16]);
 int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int i2, int k1, int k2);
 int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2);
+/* test hook: copy of an internal work array ("uten", "vten", NH "ppten", "wten") over the
+ * whole frame; returns its level count, 0 if unknown or cap (doubles) is too small */
+int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap);
 void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
 void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);
 int orc_tend(orc_t* o);     /* returns 1 on CFL violation (NaN ptntot) */

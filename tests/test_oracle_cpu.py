@@ -968,6 +968,184 @@ def test_uw_vertical_flux_matches_numpy_restatement(idynamic):
     np.testing.assert_allclose(got[sc], want[sc], rtol=1e-9, atol=1e-12 * np.abs(out[0][sc]).max())
 
 
+def _nh_tend_pair(base, on):
+    """The N1 NH oracle's first-step tendencies for two option sets (the state after bdyval,
+    and TTEN/QVTEN/QCTEN of each run)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    res = []
+    for opts in (base, on):
+        rc = dataclasses.replace(CONFIGS["N1"], **opts)
+        data = icbc.generate_nh(rc)
+        o = OracleCore(rc, data["split"])
+        o.put_state(data["state"])
+        o.bdyval()
+        g = {n: o.get(n) for n in ("ATM2_U", "ATM2_V", "ATM2_T", "ATM2_QV", "ATM2_W", "ATM2_PP", "PSA", "PSB", "HT",
+                                    "ATM0_Z", "ATM0_ZF", "XTB_B0", "XTB_BT", "XQB_B0", "XQB_BT", "XPPB_B0",
+                                    "XPPB_BT", "XUB_B0", "XUB_BT", "XVB_B0", "XVB_BT")}
+        g["time"] = o.get_time()
+        o.tend()
+        g["out"] = {n: o.get(n) for n in ("TTEN", "QVTEN", "QCTEN")}
+        # u, v, pp, w tendencies as tend leaves them for sound: decoupled (x 1/p*) and scaled by
+        # the acoustic step dts (Main/mod_tendency.F90:478-499, Main/mod_sound.F90:229-245)
+        g["work"] = {n: o.get_work(n) for n in ("uten", "vten", "ppten", "wten")}
+        lc, dt, _ = g["time"]
+        istep = max(2, int(dt / data["split"]["nh_dtsmax"]))
+        if lc > 0:
+            istep = max(istep, 4)
+        g["dts"] = dt / istep
+        o.close()
+        res.append((rc, g))
+    return res
+
+
+def test_nh_diffusion_matches_numpy_restatement():
+    """The NH horizontal diffusion of t and qv (Main/mod_tendency.F90:1514-1527) against an
+    independent NumPy restatement: calc_coeff's NH Smagorinsky coefficient with the dw/dz term
+    and the topographic background (Main/mod_diffusion.F90:100-140, 168-251: xkhz = ckh dx,
+    xkhmax = 2 dx^2/(64 dt), dydc = adyndif vonkar^2 dx/4, the b-level winds ubd3d/vbd3d =
+    atm2/psdotb and wb3d = atm2%w/psb of mkslice, Main/mod_slice.F90:176-181, 261-263), scaled
+    by rdxsq psb, then diffu_x3d of tb3d and diffu_x4d3d of qxb3d (:658-790, 805-): the
+    fourth-order interior operator and the second-order rows on the boundary ring (the corners
+    take both rows).  Checked as the difference of the first-step tendencies with ckh =
+    adyndif = 1 and with both 0 (xkc = 0); everything else is the same computation."""
+    from regcm_amd import constants as C
+    (rc, g0), (_, g1) = _nh_tend_pair({"ckh": 0.0, "adyndif": 0.0, "ifrayd": 0}, {"ifrayd": 0})
+    kz, jx, iy = rc.kz, rc.jx, rc.iy
+    dx = rc.ds * 1000.0
+    dxsq = dx * dx
+    xkhz = 1.0 * dx
+    xkhmax = 2.0 * (dxsq / (64.0 * rc.dt))
+    dydc = 1.0 * 0.4 * 0.4 * dx * 0.25
+    pb = g1["PSB"][0]
+    rpsb = np.divide(1.0, pb, out=np.zeros_like(pb), where=pb > 0)
+    # interior dot points' psdotb (4-point mean; calc_coeff at ci points reads only those)
+    psd = np.zeros_like(pb)
+    psd[1:, 1:] = (pb[1:, 1:] + pb[:-1, 1:] + pb[1:, :-1] + pb[:-1, :-1]) * 0.25
+    rpsd = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0)
+    ud, vd = g1["ATM2_U"] * rpsd[None], g1["ATM2_V"] * rpsd[None]
+    wx = g1["ATM2_W"] * rpsb[None]
+    ht = g1["HT"][0]
+    J = np.arange(2, jx - 1)          # jci (1-based)
+    I = np.arange(2, iy - 1)
+
+    def at(a, dj=0, di=0):
+        return a[..., (I + di - 1)[:, None], (J + dj - 1)[None, :]]
+    if rc.diffu_hgtf == 1:
+        hg = [np.abs((at(ht) - at(ht, 0, -1)) / dx), np.abs((at(ht) - at(ht, 0, 1)) / dx),
+              np.abs((at(ht) - at(ht, -1, 0)) / dx), np.abs((at(ht) - at(ht, 1, 0)) / dx)]
+        hgmax = np.maximum(np.maximum(hg[0], hg[1]), np.maximum(hg[2], hg[3])) * C.regrav * 1.0e3
+        hgfact = xkhz / (1.0 + hgmax * hgmax)
+    else:                          # the NH default (dynparam, Main/mod_params.F90:648-652)
+        hgfact = np.full(at(ht).shape, xkhz)
+    dudx = at(ud, 1, 0) + at(ud, 1, 1) - at(ud) - at(ud, 0, 1)
+    dvdx = at(vd, 1, 0) + at(vd, 1, 1) - at(vd) - at(vd, 0, 1)
+    dudy = at(ud, 0, 1) + at(ud, 1, 1) - at(ud) - at(ud, 1, 0)
+    dvdy = at(vd, 0, 1) + at(vd, 1, 1) - at(vd) - at(vd, 1, 0)
+    dwdz = at(wx)[:kz] - at(wx)[1:kz + 1]
+    duv = np.sqrt(np.maximum((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, 0.0))
+    xkc = np.minimum(hgfact[None] + dydc * duv, xkhmax) * (1.0 / dxsq) * at(pb)[None]
+
+    def diffu(f, xk):
+        """diffu_x3d / diffu_x4d3d / diffu_x3df (fac = 1) on the jci x ici points with the
+        coefficient xk of nk levels."""
+        out = np.zeros((xk.shape[0], len(I), len(J)))
+        f = f[: xk.shape[0]]
+        c1, c2, c3 = 1.0, -4.0, 12.0
+        inner = (slice(None), slice(1, -1), slice(1, -1))
+        four = (c1 * (at(f, 2, 0) + at(f, -2, 0) + at(f, 0, 2) + at(f, 0, -2)) +
+                c2 * (at(f, 1, 0) + at(f, -1, 0) + at(f, 0, 1) + at(f, 0, -1)) + c3 * at(f))
+        out[inner] = out[inner] - xk[inner] * four[inner]
+        two = c1 * (at(f, 1, 0) + at(f, -1, 0) + at(f, 0, 1) + at(f, 0, -1)) + c2 * at(f)
+        for sl in ((slice(None), slice(None), 0), (slice(None), slice(None), -1),
+                   (slice(None), 0, slice(None)), (slice(None), -1, slice(None))):
+            out[sl] = out[sl] + xk[sl] * two[sl]
+        return out
+    tb = g1["ATM2_T"] * rpsb[None]
+    qb = np.maximum(g1["ATM2_QV"] * rpsb[None], 1.0e-8)
+    for name, f in (("QVTEN", qb), ("TTEN", tb)):
+        want = diffu(f, xkc)
+        got = at(g1["out"][name]) - at(g0["out"][name])
+        scale = np.abs(at(g1["out"][name])).max()
+        assert np.abs(want).max() > 1e-6 * scale, name
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12 * scale, err_msg=name)
+    # pp: diffu_x3d of ppb3d = atm2%pp/psb with xkc; w: diffu_x3df of wb3d with xkcf, kz+1
+    # levels (Main/mod_diffusion.F90:523-656): xkcf(1) = xkc(1), xkcf(k+1) = xkc(k)
+    # (:232-235), scaled the same way; both then x 1/psa x dts as tend and sound leave them
+    fac = (1.0 / at(g1["PSA"])[0]) * g1["dts"]
+    xkcf = np.concatenate([xkc[:1], xkc], axis=0)
+    for name, f, xk in (("ppten", g1["ATM2_PP"] * rpsb[None], xkc), ("wten", wx, xkcf)):
+        want = diffu(f, xk) * fac[None]
+        got = at(g1["work"][name]) - at(g0["work"][name])
+        scale = np.abs(at(g1["work"][name])).max()
+        assert np.abs(want).max() > 1e-6 * scale, name
+        np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-12 * scale, err_msg=name)
+
+
+def test_nh_rayleigh_damping_matches_numpy_restatement():
+    """raydamp of t, qv, u, v, pp and w (ifrayd = 1, Main/mod_tendency.F90:356-364, 466-477; raydamp3 / raydampqv,
+    Main/mod_bdycod.F90:5021-5085 with tau, :5108-5116) against an independent NumPy
+    restatement: on levels 1..rayndamp, tau(za(k), za(1)) = rayalpha0 sin^2(pi/2 (1 - (za(1) -
+    za(k))/rayhd)) above za(1) - rayhd, else 0, times (b0 + (xbctime + dt) bt - atm2) (za =
+    atm0%z, Main/mod_atm_interface.F90:975).  Checked as the difference of the first-step
+    tendencies with ifrayd = 1 and 0."""
+    (rc, g0), (_, g1) = _nh_tend_pair({"ifrayd": 0}, {"ifrayd": 1})
+    kz, jx, iy = rc.kz, rc.jx, rc.iy
+    _, dt, xbc = g1["time"]
+    xt = xbc + dt
+    z = g1["ATM0_Z"]
+    ztop = z[0]
+    halfpi = np.pi * 0.5                                       # Share/mod_constants.F90 halfpi = mathpi/2
+    sl = (slice(None), slice(1, iy - 2), slice(1, jx - 2))     # ici x jci
+    for name, b0, bt, var in (("TTEN", "XTB_B0", "XTB_BT", "ATM2_T"), ("QVTEN", "XQB_B0", "XQB_BT", "ATM2_QV")):
+        want = np.zeros((kz, iy, jx))
+        for k in range(min(kz, rc.rayndamp)):
+            zk = z[k]
+            tau = np.where(zk > ztop - rc.rayhd,
+                           rc.rayalpha0 * np.sin(halfpi * (1.0 - (ztop - zk) / rc.rayhd)) ** 2, 0.0)
+            want[k] = tau * ((g1[b0][k] + xt * g1[bt][k]) - g1[var][k])
+        got = g1["out"][name] - g0["out"][name]
+        scale = np.abs(g1["out"][name][sl]).max()
+        # (the synthetic qv is near minqq on the damped top levels: a small but non-zero term)
+        assert np.abs(want[sl]).max() > (1e-6 * scale if name == "TTEN" else 0.0), name
+        np.testing.assert_allclose(got[sl], want[sl], rtol=1e-9, atol=1e-12 * np.abs(want[sl]).max(),
+                                   err_msg=name)
+    # pp toward its boundary data (raydamp3), w toward 0 on the full levels with zq = atm0%zf
+    # (raydamp3f, :5005-5019), both x 1/psa x dts; u, v at dot points with z averaged from the
+    # four cross neighbours (raydampuv, :4953-4983), x 1/psdota x dts
+    fac = np.divide(1.0, g1["PSA"][0], out=np.zeros_like(g1["PSA"][0]), where=g1["PSA"][0] > 0) * g1["dts"]
+    zf = g1["ATM0_ZF"]
+    for name, nk, zz, bval, var in (
+            ("ppten", kz, z, g1["XPPB_B0"] + xt * g1["XPPB_BT"], g1["ATM2_PP"]),
+            ("wten", kz + 1, zf, 0.0 * g1["ATM2_W"], g1["ATM2_W"])):
+        want = np.zeros((nk, iy, jx))
+        for k in range(min(nk, rc.rayndamp)):
+            tau = np.where(zz[k] > zz[0] - rc.rayhd,
+                           rc.rayalpha0 * np.sin(halfpi * (1.0 - (zz[0] - zz[k]) / rc.rayhd)) ** 2, 0.0)
+            want[k] = tau * (bval[k] - var[k]) * fac
+        got = g1["work"][name] - g0["work"][name]
+        scale = np.abs(g1["work"][name][sl]).max()
+        assert np.abs(want[sl]).max() > 1e-6 * scale, name
+        np.testing.assert_allclose(got[sl], want[sl], rtol=1e-9, atol=1e-12 * scale, err_msg=name)
+    pa = g1["PSA"][0]
+    psd = np.zeros_like(pa)
+    psd[1:, 1:] = (pa[1:, 1:] + pa[:-1, 1:] + pa[1:, :-1] + pa[:-1, :-1]) * 0.25
+    dfac = np.divide(1.0, psd, out=np.zeros_like(psd), where=psd > 0) * g1["dts"]
+    zd = np.zeros_like(z)
+    zd[:, 1:, 1:] = 0.25 * (z[:, 1:, 1:] + z[:, 1:, :-1] + z[:, :-1, 1:] + z[:, :-1, :-1])
+    dl = (slice(None), slice(1, iy - 1), slice(1, jx - 1))     # idi x jdi
+    for name, b0, bt, var in (("uten", "XUB_B0", "XUB_BT", "ATM2_U"), ("vten", "XVB_B0", "XVB_BT", "ATM2_V")):
+        want = np.zeros((kz, iy, jx))
+        for k in range(min(kz, rc.rayndamp)):
+            tau = np.where(zd[k] > zd[0] - rc.rayhd,
+                           rc.rayalpha0 * np.sin(halfpi * (1.0 - (zd[0] - zd[k]) / rc.rayhd)) ** 2, 0.0)
+            want[k] = tau * ((g1[b0][k] + xt * g1[bt][k]) - g1[var][k]) * dfac
+        got = g1["work"][name] - g0["work"][name]
+        scale = np.abs(g1["work"][name][dl]).max()
+        assert np.abs(want[dl]).max() > 1e-6 * scale, name
+        np.testing.assert_allclose(got[dl], want[dl], rtol=1e-9, atol=1e-12 * scale, err_msg=name)
+
+
 def test_hydrostatic_wind_tendency_matches_numpy_restatement():
     """The hydrostatic u, v tendencies of the first step against an independent NumPy
     restatement of the reference (C1, no diffusion, dot points off the band): hadvuv's
