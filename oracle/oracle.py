@@ -44,6 +44,7 @@ def lib():
         L.orc_frame_info.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         L.orc_put.argtypes = [P, i, dp, i, i, i, i, i, i]
         L.orc_get.argtypes = [P, i, dp, i, i, i, i, i, i]
+        L.orc_set_sound_probe.argtypes = [P, i]
         L.orc_get_work.restype = i
         L.orc_get_work.argtypes = [P, ctypes.c_char_p, dp, ctypes.c_size_t]
         L.orc_set_time.argtypes = [P, ctypes.c_longlong, ctypes.c_double, ctypes.c_double]
@@ -121,6 +122,9 @@ class OracleCore:
     def put_state(self, st):
         for name, arr in st.items():
             self.put(name, arr)
+
+    def set_sound_probe(self, nsub):
+        lib().orc_set_sound_probe(self.h, nsub)
 
     def get_work(self, name):
         """An internal work array (orc_get_work) on the global (iy, jx) grid of a one-tile

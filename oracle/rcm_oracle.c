@@ -128,6 +128,7 @@ struct orc {
   /* UW PBL TKE (ibltyp = 2): atm1/atm2 tke, atmc%tke, tkedyn, tkeps, the pc_physic tendency */
   double *a1tke, *a2tke, *ctke, *tkedyn, *tkeps, *tkephy;
   double* kpbl;      /* ibltyp = 2: the UW scheme's PBL-top level (put; iuwvadv = 1 reads it) */
+  int sound_probe;   /* test hook (orc_set_sound_probe): sound returns after this many sub-steps */
   /* bdyin: raw record (u, v, t, qv, ps, pp, w), coupled b1 (same order), NH atm0%psdot */
   double *bin[7], *bb1[7], *psdot0;
   double rhmin, rhmax;
@@ -246,6 +247,7 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
    * radiative condition (Main/mod_sound.F90:496-497): orc_set_gather, before the first step */
   if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
+  o->sound_probe = -1;
   o->cfg = *cfg;
   o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
   o->nsplit = cfg->nsplit; o->nqx = 2;
@@ -593,10 +595,21 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
   else if (!strcmp(name, "vten")) a = o->vten;
   else if (o->nh && !strcmp(name, "ppten")) a = o->ppten;
   else if (o->nh && !strcmp(name, "wten")) { a = o->wten; nk = o->kz + 1; }
+  /* sound's state (atmc%u, v, pp, w, the pi of the last sub-step) and what it reads */
+  else if (o->nh && !strcmp(name, "cu")) a = o->cu;
+  else if (o->nh && !strcmp(name, "cv")) a = o->cv;
+  else if (o->nh && !strcmp(name, "cpp")) a = o->cpp;
+  else if (o->nh && !strcmp(name, "cw")) { a = o->cw; nk = o->kz + 1; }
+  else if (o->nh && !strcmp(name, "pi")) a = o->s_pi;
+  else if (o->nh && !strcmp(name, "pr1")) a = o->pr1;
+  else if (o->nh && !strcmp(name, "rho1")) a = o->rho1;
+  else if (o->nh && !strcmp(name, "cqv")) a = o->cq[0];
   if (!a || cap < o->plane * (size_t)nk) return 0;
   memcpy(dst, a, sizeof(double) * o->plane * (size_t)nk);
   return nk;
 }
+
+void orc_set_sound_probe(orc_t* o, int nsub) { o->sound_probe = nsub; }
 
 int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
   int nk; double* a = field_ptr(o, field, &nk);
@@ -2438,6 +2451,7 @@ static int nh_sound(orc_t* o) {
   int day_alarm = (o->lcount == 0) || !o->tmask_valid ||
                   (floor(tnow / 86400.0) != floor((tnow - o->dtsec) / 86400.0));
   double cflmax = d_zero;
+  if (o->sound_probe == 0) return 0;           /* test hook: the state at sub-step 1's start */
   double* e = o->s_e; double* f = o->s_f; double* wo = o->s_wo; double* spi = o->s_pi;
   double *aa = o->s_aa, *b = o->s_b, *c = o->s_c, *rhs = o->s_rhs, *ca = o->s_ca, *g1 = o->s_g1, *g2 = o->s_g2;
   double *ptend = o->s_ptend, *pxup = o->s_pxup, *pyvp = o->s_pyvp, *tk = o->s_tk, *cc = o->s_cc;
@@ -2659,6 +2673,7 @@ static int nh_sound(orc_t* o) {
           A3(o->a2t, j, i, k) = A3(o->a2t, j, i, k) + o->cfg.gnu1 * dpterm;
           A3(o->a1t, j, i, k) = A3(o->a1t, j, i, k) + dpterm;
         }
+    if (o->sound_probe == it) { o->nh_cfl = cflmax; return 0; }   /* test hook: stop here */
   }
   o->nh_cfl = cflmax;
   /* time filters (:686-702) */

@@ -57,6 +57,9 @@ int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, in
 /* test hook: copy of an internal work array ("uten", "vten", NH "ppten", "wten") over the
  * whole frame; returns its level count, 0 if unknown or cap (doubles) is too small */
 int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap);
+/* test hook: the NH sound returns after nsub sub-steps (0: right after its set-up), before
+ * the time filters, so a test can check one sub-step; -1 (default) runs sound whole */
+void orc_set_sound_probe(orc_t* o, int nsub);
 void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
 void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);
 int orc_tend(orc_t* o);     /* returns 1 on CFL violation (NaN ptntot) */

@@ -1316,3 +1316,183 @@ def test_nh_oracle_threads_match_single_tile(nthreads, variant):
     names = STATE_FIELDS[:12] + NH_STATE_FIELDS + (["ATM1_TKE", "ATM2_TKE"] if rc.ibltyp == 2 else [])
     for name in names:
         assert np.array_equal(par.get(name), ref.get(name)), name
+
+
+def test_nh_sound_substep_matches_numpy_restatement():
+    """One acoustic sub-step of sound (Main/mod_sound.F90:249-682, the first sub-step of the
+    first step, upper radiative condition off: ifupr = 0) against an independent NumPy
+    restatement, from the state sound starts with (the oracle stopped right after sound's
+    set-up, orc_set_sound_probe(0)) to the state after the sub-step (probe 1): dp'/dp0, the
+    pressure-gradient update of u and v (:266-296), the lower boundary w and the lid, the
+    coefficients cc, cdd, cj, ca, g1, g2 and the Ikawa tridiagonal (a, b, c, rhs; :322-457),
+    the pp predictor (:459-468), the upward elimination and the downward w sweep
+    (:470-479, 566-573), the zero-gradient w on the boundary ring (:577-607), the new pp, pi
+    and the dp'/dt temperature correction of atm1 and atm2 t (:661-680)."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    from regcm_amd import constants as C
+    rc = dataclasses.replace(CONFIGS["N1"], ifupr=0)
+    data = icbc.generate_nh(rc)
+    runs = []
+    for probe in (0, 1):
+        o = OracleCore(rc, data["split"])
+        o.put_state(data["state"])
+        o.bdyval()
+        o.set_sound_probe(probe)
+        _, dt, _ = o.get_time()
+        o.tend()
+        r = {n: o.get_work(n) for n in ("cu", "cv", "cpp", "cw", "pi", "pr1", "rho1", "cqv", "uten", "vten",
+                                        "ppten", "wten")}
+        r.update({n: o.get(n) for n in ("ATM1_T", "ATM2_T", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_PS",
+                                         "HT", "MSFX", "MSFD", "DPRDDX", "DPRDDY", "PSB")})
+        r["dt"] = dt
+        o.close()
+        runs.append(r)
+    a, b = runs
+    kz, jx, iy = rc.kz, rc.jx, rc.iy
+    kp = kz + 1
+    dt = a["dt"]
+    istep = max(2, int(dt / data["split"]["nh_dtsmax"]))
+    dts = dt / istep
+    dx = rc.ds * 1000.0
+    sig = np.asarray(rc.sigma)
+    dsig = np.concatenate([[0.0], sig[1:] - sig[:-1]])            # dsigma(k) at [k]
+    egrav, regrav = C.egrav, C.regrav
+    rgas, cpd = C.rgas, 3.5 * C.rgas
+    xgamma = 1.0 / (1.0 - rgas * (1.0 / cpd))                      # Main/mod_sound.F90:77
+    bet = rc.nhbet
+    bp, bm = (1.0 + bet) * 0.5, (1.0 - bet) * 0.5
+    bpxbp, bpxbm = bp * bp, bp * bm
+
+    def F(x):                                                      # 1-based [k][i][j] views
+        return lambda k, i, j: x[k - 1][i - 1][j - 1]
+    u = a["cu"].copy(); v = a["cv"].copy(); pp = a["cpp"].copy(); w = a["cw"].copy()
+    pr0, t0, rho0 = a["ATM0_PR"], a["ATM0_T"], a["ATM0_RHO"]
+    ps0 = a["ATM0_PS"][0]
+    pr1, rho1 = a["pr1"], a["rho1"]
+    ht, msfx, msfd = a["HT"][0], a["MSFX"][0], a["MSFD"][0]
+    psb = a["PSB"][0]
+    rpsb = np.divide(1.0, psb, out=np.zeros_like(psb), where=psb > 0)
+    a2t = a["ATM2_T"]
+    JE, IE = slice(0, jx - 1), slice(0, iy - 1)                   # jce, ice (0-based)
+    # dp'/dp0 on the cross points (atmc%t as sound's scratch, :258-263)
+    cdt = np.zeros_like(pp)
+    for k in range(1, kz + 1):
+        km1, kp1 = max(1, k - 1), min(kz, k + 1)
+        cdt[k - 1][IE, JE] = (pp[km1 - 1][IE, JE] - pp[kp1 - 1][IE, JE]) / (pr0[km1 - 1][IE, JE] - pr0[kp1 - 1][IE, JE])
+    # u, v on jdi x idi (:266-296)
+    D = (slice(None), slice(1, iy - 1), slice(1, jx - 1))
+
+    def sh(x, dj, di):                                             # x at (j+dj, i+di), on D
+        return x[:, 1 + di: iy - 1 + di, 1 + dj: jx - 1 + dj]
+    rho = 0.25 * (sh(rho1, 0, 0) + sh(rho1, -1, 0) + sh(rho1, 0, -1) + sh(rho1, -1, -1))
+    dpp = 0.25 * (sh(cdt, 0, 0) + sh(cdt, -1, 0) + sh(cdt, 0, -1) + sh(cdt, -1, -1))
+    chh = 0.5 * dts / (rho * dx) / msfd[1:iy - 1, 1:jx - 1][None]
+    u[D] = u[D] - chh * (sh(pp, 0, 0) - sh(pp, -1, 0) + sh(pp, 0, -1) - sh(pp, -1, -1) - a["DPRDDX"][D] * dpp)
+    v[D] = v[D] - chh * (sh(pp, 0, 0) - sh(pp, 0, -1) + sh(pp, -1, 0) - sh(pp, -1, -1) - a["DPRDDY"][D] * dpp)
+    u[D] = u[D] + a["uten"][D]
+    v[D] = v[D] + a["vten"][D]
+    np.testing.assert_allclose(b["cu"][D], u[D], rtol=1e-13, atol=1e-13 * np.abs(u[D]).max(), err_msg="u")
+    np.testing.assert_allclose(b["cv"][D], v[D], rtol=1e-13, atol=1e-13 * np.abs(v[D]).max(), err_msg="v")
+    # the semi-implicit w / pp solve, column by column on jci x ici
+    U, V, P, W, R0, R1, P0, P1, T0 = F(u), F(v), F(pp), F(w), F(rho0), F(rho1), F(pr0), F(pr1), F(t0)
+    wnew = w.copy()
+    ppnew = pp.copy()
+    pinew = np.zeros_like(pp)
+    a1t, a2tn = a["ATM1_T"].copy(), a["ATM2_T"].copy()
+    for i in range(2, iy - 1):
+        for j in range(2, jx - 1):
+            wo = [None] + [W(k, i, j) for k in range(1, kp + 1)]
+            e = [0.0] * (kp + 1); f = [0.0] * (kp + 1)
+            cc = [0.0] * (kz + 1); cdd = [0.0] * (kz + 1); cj = [0.0] * (kz + 1); ca = [0.0] * (kz + 1)
+            g1 = [0.0] * (kz + 1); g2 = [0.0] * (kz + 1); aa = [0.0] * (kz + 1); bb = [0.0] * (kz + 1)
+            cq = [0.0] * (kz + 1); tk = [0.0] * (kz + 1); px = [0.0] * (kz + 1); py = [0.0] * (kz + 1)
+            pt = [0.0] * (kz + 1); rhs = [0.0] * (kz + 1)
+            wk = list(wo)
+            wk[kp] = 0.5 * 0.25 * regrav * (
+                (V(kz, i + 1, j) + V(kz, i, j) + V(kz, i + 1, j + 1) + V(kz, i, j + 1)) * (ht[i, j - 1] - ht[i - 2, j - 1]) +
+                (U(kz, i + 1, j) + U(kz, i, j) + U(kz, i + 1, j + 1) + U(kz, i, j + 1)) * (ht[i - 1, j] - ht[i - 1, j - 2])
+            ) / (dx * msfx[i - 1, j - 1])
+            e[kz] = 0.0
+            f[kz] = wk[kp]
+            mx = msfx[i - 1, j - 1]
+            md = lambda jj, ii: msfd[ii - 1, jj - 1]                  # noqa: E731
+            for k in range(1, kz + 1):
+                km1, kp1 = max(1, k - 1), min(k + 1, kz)
+                tk[k] = (0.5 * ps0[i - 1, j - 1] * T0(k, i, j)) / (xgamma * P0(k, i, j) * a2t[k - 1][i - 1][j - 1] *
+                                                                   rpsb[i - 1, j - 1])
+                cc[k] = xgamma * P1(k, i, j) * dts / (dx * mx)
+                cdd[k] = xgamma * P1(k, i, j) * R0(k, i, j) * egrav * dts / (ps0[i - 1, j - 1] * dsig[k])
+                cj[k] = 0.5 * R0(k, i, j) * egrav * dts
+                if k == 1:
+                    px[k] = 0.0625 * (P0(1, i, j + 1) - P0(1, i, j - 1)) * (
+                        U(1, i, j) + U(1, i, j + 1) + U(1, i + 1, j) + U(1, i + 1, j + 1) -
+                        U(2, i, j) - U(2, i, j + 1) - U(2, i + 1, j) - U(2, i + 1, j + 1)) / (P0(1, i, j) - P0(2, i, j))
+                    py[k] = 0.0625 * (P0(1, i + 1, j) - P0(1, i - 1, j)) * (
+                        V(1, i, j) + V(1, i, j + 1) + V(1, i + 1, j) + V(1, i + 1, j + 1) -
+                        V(2, i, j) - V(2, i, j + 1) - V(2, i + 1, j) - V(2, i + 1, j + 1)) / (P0(1, i, j) - P0(2, i, j))
+                    continue
+                rofac = (dsig[km1] * R0(k, i, j) + dsig[k] * R0(km1, i, j)) / (dsig[km1] * R1(k, i, j) + dsig[k] * R1(km1, i, j))
+                ca[k] = egrav * dts / (P0(k, i, j) - P0(km1, i, j)) * rofac
+                g1[k] = 1.0 - dsig[km1] * tk[k]
+                g2[k] = 1.0 + dsig[k] * tk[km1]
+                cq[k] = -ca[k] * (cdd[km1] - cj[km1]) * g2[k] * bpxbp
+                bb[k] = 1.0 + ca[k] * (g1[k] * (cdd[k] - cj[k]) + g2[k] * (cdd[km1] + cj[km1])) * bpxbp
+                aa[k] = -ca[k] * (cdd[k] + cj[k]) * g1[k] * bpxbp
+                py[k] = 0.125 * (P0(k, i + 1, j) - P0(k, i - 1, j)) * (
+                    V(km1, i, j) + V(km1, i, j + 1) + V(km1, i + 1, j) + V(km1, i + 1, j + 1) -
+                    V(kp1, i, j) - V(kp1, i, j + 1) - V(kp1, i + 1, j) - V(kp1, i + 1, j + 1)) / (P0(km1, i, j) - P0(kp1, i, j))
+                px[k] = 0.125 * (P0(k, i, j + 1) - P0(k, i, j - 1)) * (
+                    U(km1, i, j) + U(km1, i, j + 1) + U(km1, i + 1, j) + U(km1, i + 1, j + 1) -
+                    U(kp1, i, j) - U(kp1, i, j + 1) - U(kp1, i + 1, j) - U(kp1, i + 1, j + 1)) / (P0(km1, i, j) - P0(kp1, i, j))
+            py[kz] = py[kz] * 0.5
+            px[kz] = px[kz] * 0.5
+            for k in range(1, kz + 1):
+                div = (V(k, i + 1, j) * md(j, i + 1) - V(k, i, j) * md(j, i) + V(k, i + 1, j + 1) * md(j + 1, i + 1) -
+                       V(k, i, j + 1) * md(j + 1, i) + U(k, i, j + 1) * md(j + 1, i) - U(k, i, j) * md(j, i) +
+                       U(k, i + 1, j + 1) * md(j + 1, i + 1) - U(k, i + 1, j) * md(j, i + 1))
+                pt[k] = a["ppten"][k - 1][i - 1][j - 1] - 0.5 * cc[k] * (div / mx - 2.0 * (py[k] + px[k]))
+            for k in range(2, kz + 1):
+                rhs[k] = wk[k] + a["wten"][k - 1][i - 1][j - 1] + ca[k] * (
+                    bpxbm * ((cdd[k - 1] - cj[k - 1]) * g2[k] * wo[k - 1] -
+                             ((cdd[k - 1] + cj[k - 1]) * g2[k] + (cdd[k] - cj[k]) * g1[k]) * wo[k] +
+                             (cdd[k] + cj[k]) * g1[k] * wo[k + 1]) +
+                    (P(k, i, j) * g1[k] - P(k - 1, i, j) * g2[k]) + (g1[k] * pt[k] - g2[k] * pt[k - 1]) * bp)
+            pold = [None] + [P(k, i, j) for k in range(1, kz + 1)]
+            pc = [None] + [pold[k] + pt[k] + (cj[k] * (wo[k + 1] + wo[k]) + cdd[k] * (wo[k + 1] - wo[k])) * bm
+                           for k in range(1, kz + 1)]
+            for k in range(kz, 1, -1):
+                den = aa[k] * e[k] + bb[k]
+                e[k - 1] = -cq[k] / den
+                f[k - 1] = (rhs[k] - f[k] * aa[k]) / den
+            wk[1] = 0.0
+            for k in range(1, kz + 1):
+                wk[k + 1] = e[k] * wk[k] + f[k]
+            for k in range(1, kp + 1):
+                wnew[k - 1][i - 1][j - 1] = wk[k]
+            for k in range(1, kz + 1):
+                cddt = xgamma * P1(k, i, j) * R0(k, i, j) * egrav * dts / (ps0[i - 1, j - 1] * dsig[k])
+                cjt = R0(k, i, j) * egrav * dts * 0.5
+                pn = pc[k] + (cjt * (wk[k + 1] + wk[k]) + cddt * (wk[k + 1] - wk[k])) * bp
+                ppnew[k - 1][i - 1][j - 1] = pn
+                pinew[k - 1][i - 1][j - 1] = pn - pold[k] - a["ppten"][k - 1][i - 1][j - 1]
+                cpm = cpd * (1.0 + 0.80 * a["cqv"][k - 1][i - 1][j - 1])
+                dpterm = psb[i - 1, j - 1] * (pn - pold[k]) / (cpm * R1(k, i, j))
+                a2tn[k - 1][i - 1][j - 1] = a2tn[k - 1][i - 1][j - 1] + rc.gnu1 * dpterm
+                a1t[k - 1][i - 1][j - 1] = a1t[k - 1][i - 1][j - 1] + dpterm
+    # zero-gradient w on the boundary ring (:577-607): bottom/top rows, then left/right columns
+    wnew[:, 0, 1:jx - 2] = wnew[:, 1, 1:jx - 2]
+    wnew[:, 0, 0] = wnew[:, 1, 1]
+    wnew[:, 0, jx - 2] = wnew[:, 1, jx - 3]
+    wnew[:, iy - 2, 1:jx - 2] = wnew[:, iy - 3, 1:jx - 2]
+    wnew[:, iy - 2, 0] = wnew[:, iy - 3, 1]
+    wnew[:, iy - 2, jx - 2] = wnew[:, iy - 3, jx - 3]
+    wnew[:, 1:iy - 2, 0] = wnew[:, 1:iy - 2, 1]
+    wnew[:, 1:iy - 2, jx - 2] = wnew[:, 1:iy - 2, jx - 3]
+    CI = (slice(None), slice(1, iy - 2), slice(1, jx - 2))
+    CE = (slice(None), slice(0, iy - 1), slice(0, jx - 1))
+    for name, want, got, sl in (("w", wnew, b["cw"], CE), ("pp", ppnew, b["cpp"], CI), ("pi", pinew, b["pi"], CI),
+                                ("atm1 t", a1t, b["ATM1_T"], CI), ("atm2 t", a2tn, b["ATM2_T"], CI)):
+        assert np.abs(want[sl]).max() > 0.0, name
+        np.testing.assert_allclose(got[sl], want[sl], rtol=1e-11, atol=1e-12 * np.abs(want[sl]).max(), err_msg=name)
+    assert not np.array_equal(b["cpp"][CI], a["cpp"][CI]) and not np.array_equal(b["cw"][CE], a["cw"][CE])
