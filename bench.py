@@ -204,7 +204,11 @@ def main():
     t_step = wall / args.steps
     sypd = rc.dt / (365.0 * t_step)
     # the drop-in call sequence of INTEGRATION.md section 4 (RCM_run: rcmdyn_tend then
-    # rcmdyn_bdyval per step through the C-ABI, each replaying its own graph), same K steps
+    # rcmdyn_bdyval per step through the C-ABI, each replaying its own graph), same K steps,
+    # after two untimed pairs that capture its graphs (one per ping-pong parity)
+    for _ in range(2):
+        eng.tend()
+        eng.bdyval()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):

@@ -603,7 +603,8 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
   else if (o->nh && !strcmp(name, "pi")) a = o->s_pi;
   else if (o->nh && !strcmp(name, "pr1")) a = o->pr1;
   else if (o->nh && !strcmp(name, "rho1")) a = o->rho1;
-  else if (o->nh && !strcmp(name, "cqv")) a = o->cq[0];
+  else if (!strcmp(name, "cqv")) a = o->cq[0];
+  else if (!strcmp(name, "cqc")) a = o->cq[1];
   if (!a || cap < o->plane * (size_t)nk) return 0;
   memcpy(dst, a, sizeof(double) * o->plane * (size_t)nk);
   return nk;

@@ -275,6 +275,13 @@ struct rcmdyn_engine {
     return v && *v && std::strcmp(v, "0") != 0;
   }();
   bool fuse_bdy = false;      // set by step_once for the tend + bdyval pair it runs
+  // the hydrostatic step without k_qfilter (its work in k_columns, k_scalars and the extra
+  // blocks of k_split_project / k_split_correct); RCMDYN_NO_QFUSE=1 launches k_qfilter
+  const bool no_qfuse = [] {
+    const char* v = std::getenv("RCMDYN_NO_QFUSE");
+    return v && *v && std::strcmp(v, "0") != 0;
+  }();
+  bool qfuse() const { return cfg.idynamic != 2 && !no_qfuse; }
   std::string err;
   std::unique_ptr<Comm> comm;
   // RCMDYN_FORCE_RCCL=1: the halo messages between tiles held by this engine travel as RCCL
@@ -435,6 +442,10 @@ struct rcmdyn_engine {
     }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     t.depplane = talloc<int>(t, 2 * kz);
+    if (cfg.idynamic != 2) {
+      t.negcnt = talloc<int>(t, 1);
+      t.neglist = talloc<uint32_t>(t, 2 * P3);     // every (point, level, qv|qc) at most once
+    }
     t.deld = dalloc(t, P * 3 * ns); t.delh = dalloc(t, P * 3 * ns);
     t.ddsum = dalloc(t, P * ns); t.dhsum = dalloc(t, P * ns);
     t.uu = dalloc(t, P); t.vv = dalloc(t, P);
@@ -1406,6 +1417,7 @@ struct rcmdyn_engine {
     if (hc.iqxvadv == 3) f.kpbl = t.kpbl;    // vadv4d ind = 3 of qc
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.red = red; f.red_off = t.red_off;
+    f.qfuse = qfuse() ? 1 : 0; f.negcnt = t.negcnt; f.neglist = t.neglist;
     return f;
   }
 
@@ -1661,8 +1673,9 @@ struct rcmdyn_engine {
     tke_step();
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
+    // (qfuse: done by k_columns, k_scalars and the extra blocks below)
     each([&](Tile& t) {
-      KLAUNCH(k_qfilter, grid3((t.g.nj + 1) / 2, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
+      if (!qfuse()) KLAUNCH(k_qfilter, grid3((t.g.nj + 1) / 2, t.g.ni, kz), BLK, 0, stream, t.g, dc, fields(t));
       t.cur = 1 - t.cur;
     });
     // splitf, Main/mod_split.F90:243-461
@@ -1671,13 +1684,15 @@ struct rcmdyn_engine {
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
-      QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
-             t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.depplane};
+      const QFix q = qfix(t);
       const int nxp = (g.jdx2() - g.jde1 + 64) / 64, nproj = nxp * (g.idx2() - g.ide1 + 1);
-      KLAUNCH(k_split_project, dim3(nproj + 2 * kz), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
+      // extra blocks: qfuse the parallel fix of the listed negatives (grid-stride), else the
+      // serial sweeps of the planes k_qfilter flagged
+      const int nextra = qfuse() ? NEGFIX_BLOCKS : 2 * kz;
+      KLAUNCH(k_split_project, dim3(nproj + nextra), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q, t.gw, wide ? t.wdeld : nullptr,
-                         t.wdelh, t.wpsdota, t.wpsa);
+                         t.wdelh, t.wpsdota, t.wpsa, t.a2u[o], t.a2v[o]);
     });
     // spstep, :463-669: forward step then leapfrog, two time slots + forcing slot 3
     if (wide) {
@@ -1720,6 +1735,10 @@ struct rcmdyn_engine {
       const int c = t.cur;
       dim3 gr = grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
       const int adv = (int)(q + 1 == tiles.size());
+      // qfuse: trailing z slices run the serial sweeps of the flagged moisture planes
+      const QFix qf = qfix(t);
+      const int nser = qfuse() ? (int)((2 * kz + gr.x * gr.y - 1) / (gr.x * gr.y)) : 0;
+      gr.z += nser;
       if (fuse_bdy) {
         // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
         // levels, 4 per block
@@ -1727,13 +1746,13 @@ struct rcmdyn_engine {
         gr.z += (6 * bdy_chunks(g) * kz + per - 1) / per;
         const BdyArgs ba = bdy_args(t, 1);
 #define RCM_SCB(NS_) KLAUNCH(k_split_correct_bdy<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, \
-                             ds, adv, red, red_total, ba)
+                             ds, adv, red, red_total, ba, qf, nser)
         switch (ns) { case 1: RCM_SCB(1); break; case 2: RCM_SCB(2); break; case 3: RCM_SCB(3); break; default: RCM_SCB(4); }
 #undef RCM_SCB
       } else {
 #define RCM_SC(NS_) KLAUNCH(k_split_correct<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd,   \
                             t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], ds, adv, \
-                            red, red_total, dflags)
+                            red, red_total, dflags, qf, nser)
         switch (ns) { case 1: RCM_SC(1); break; case 2: RCM_SC(2); break; case 3: RCM_SC(3); break; default: RCM_SC(4); }
 #undef RCM_SC
       }
@@ -1756,6 +1775,17 @@ struct rcmdyn_engine {
       KLAUNCH(k_spstep_update, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, 1), BLK, 0, stream, g, dc,
                          l, n0, n1, nn, leap, t.uu, t.vv, t.mapf, t.psa_[t.cur], t.deld, t.delh, t.ddsum, t.dhsum);
     });
+  }
+
+  // the moisture fix-up operands for the current parity (after the flip of tend_post): the
+  // forecasts and fixed values, the old (o*) and new (n*) q buffers, the filtered p*
+  QFix qfix(Tile& t) {
+    const int c = t.cur, o = 1 - c;
+    QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
+           t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.psc, t.psa_[o], t.psb_[o],
+           t.depplane, nullptr, nullptr};
+    if (qfuse()) { q.negcnt = t.negcnt; q.neglist = t.neglist; }
+    return q;
   }
 
   BdyArgs bdy_args(Tile& t, int set_ps) {

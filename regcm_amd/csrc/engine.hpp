@@ -152,6 +152,8 @@ struct Tile {
   double* kpbl = nullptr;          // ibltyp = 2: the UW scheme's PBL-top level (put, 2-D)
   double *cqv, *cqc, *fqv, *fqc;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
+  int* negcnt = nullptr;           // hydrostatic qfuse: the negative forecasts k_scalars listed
+  uint32_t* neglist = nullptr;
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;
   // diagnostics of the last tend
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;

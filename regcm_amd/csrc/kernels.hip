@@ -67,6 +67,74 @@ __device__ __forceinline__ void nudge_coef(const Consts* c, int ib, int k, doubl
   else { xf = c->hefc[ib][k]; xg = c->hegc[ib][k]; }
 }
 
+// qfuse: copies of the values at (j, i), levels k0, k0+dk, .. <= kz, that no update kernel of
+// the step writes into the next buffers (k_qfilter's copies): u, v outside k_momentum's dot
+// set, t outside k_scalars' cross set, qv, qc outside the owned interior (the moisture fix's
+// set).  On a ghost point (the column box's one-point ring; k_columns runs before the atm2
+// part of the prologue exchange has landed) only atm1 is copied: the atm2 ghost values this
+// step still reads (a2 u, v on the boundary lines, in k_split_project's divergence) are read
+// from the current buffers there (k_split_project), and the next step's exchange rewrites
+// the rest before any read.
+__device__ __forceinline__ void keep_point(const Geom& g, const Fields& f, int j, int i, int k0, int dk, int kz) {
+  const bool own = in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2);
+  const int jd2 = g.br ? g.jdi2 : g.jde2 + 1, id2 = g.bt ? g.idi2 : g.ide2 + 1;
+  const bool uvk = !(in(j, g.jdi1, jd2) && in(i, g.idi1, id2));
+  const bool tk = !(in(i, g.icx1(), g.icx2()) && in(j, g.jcx1(), g.jcx2()) && g.gci(j, i));
+  const bool qk = !(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2));
+  if (!uvk && !tk && !qk) return;
+  for (int k = k0; k <= kz; k += dk) {
+    const long p = (long)(k - 1) * g.plane + g.ix(j, i);
+    if (uvk) { f.b1u[p] = f.a1u[p]; f.b1v[p] = f.a1v[p]; }
+    if (tk) f.b1t[p] = f.a1t[p];
+    if (qk) { f.b1qv[p] = f.a1qv[p]; f.b1qc[p] = f.a1qc[p]; }
+    if (!own) continue;
+    if (uvk) { f.b2u[p] = f.a2u[p]; f.b2v[p] = f.a2v[p]; }
+    if (tk) f.b2t[p] = f.a2t[p];
+    if (qk) { f.b2qv[p] = f.a2qv[p]; f.b2qc[p] = f.a2qc[p]; }
+  }
+}
+
+// negative-moisture fix helpers (K6 below)
+__device__ __forceinline__ double negfix_sum(const Geom& g, const double* sv, const double* fx, int j, int i, int k,
+                                             bool use_fixed) {
+  double sum = 0.0;
+  for (int ii = i - 1; ii <= i + 1; ii++)
+    for (int jj = j - 1; jj <= j + 1; jj++) {
+      double v = F3(sv, jj, ii, k);
+      if (use_fixed) {
+        const bool pred = (ii < i) || (ii == i && jj < j);
+        if (pred && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) v = F3(fx, jj, ii, k);
+      }
+      sum = sum + fabs(v);
+    }
+  return 0.01 * sum / 9.0;
+}
+
+__device__ __forceinline__ bool negfix_dependent(const Geom& g, const double* sv, int j, int i, int k) {
+#define NEG(J, I) (in(J, g.jci1, g.jci2) && in(I, g.ici1, g.ici2) && F3(sv, J, I, k) < d_zero)
+  return NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
+#undef NEG
+}
+
+// RAW filters of one point (filter_raw_qv / filter_raw_4d) with the filtered p*
+__device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, double o1, double o2v, double pa,
+                                           double pb, double& n1, double& n2) {
+  const double beta = 0.53;
+  if (n == 0) {
+    const double d = c->gnu1 * (fq + o2v - d_two * o1);
+    n2 = dmax(o1 + beta * d, MINQQ * pa);
+    n1 = dmax(fq + (beta - d_one) * d, MINQQ * pb);
+  } else {
+    const double d = c->gnu2 * (fq + o2v - d_two * o1);
+    double m = o1 + beta * d;
+    double q = fq + (beta - d_one) * d;
+    if (m < d_zero) m = d_zero;
+    if (q < d_zero) q = d_zero;
+    n2 = m;
+    n1 = q;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // K2. Column work, 64 columns (j) of one row i per block:
 //    compute_omega column part, Main/mod_tendency.F90:1123-1156 (pten, qdot k-scan),
@@ -93,13 +161,18 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   PT_DECL
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
-  if (bb >= ncol) {                                      // surface pressures outside the box
+  if (bb >= ncol) {
+    // surface pressures (and with qfuse the copy of p*) on the frame points outside the column
+    // box, all ghost points
     const int q = (bb - ncol) * 512 + (int)threadIdx.x;
     const int jj = g.j0 + q % g.nj, ii = g.i0 + q / g.nj;
-    if (ii < g.i0 + g.ni && !(in(jj, g.jdx1(), g.jdx2()) && in(ii, g.idx1(), g.idx2())))
+    if (ii < g.i0 + g.ni && !(in(jj, g.jdx1(), g.jdx2()) && in(ii, g.idx1(), g.idx2()))) {
       surface_pressures_at(g, f, jj, ii);
+      if (f.qfuse) { F2(f.bpsa, jj, ii) = F2(f.psa, jj, ii); F2(f.bpsb, jj, ii) = F2(f.psb, jj, ii); }
+    }
     return;
   }
+  if (f.qfuse && bb == 0 && threadIdx.x == 0) *f.negcnt = 0;  // k_scalars appends after this
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
@@ -118,6 +191,9 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   const uint32_t o2 = valid ? g.o2(j, i) : 0u;
   const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
   if (valid && ty == 7) surface_pressures_at(g, f, j, i);
+  // qfuse: the points k_momentum / k_scalars / the moisture fix leave alone keep their values
+  // in the next buffers (k_qfilter's copies), one level group per wavefront
+  if (valid && f.qfuse) keep_point(g, f, j, i, ty + 1, 8, kz);
   double rp = 0.0;
   if (ce) {
     // phase 1: umc/vmc = atm1 * msfd (decouple :880-890); xqv/xqc decoupled moisture (:1000-1016)
@@ -166,6 +242,7 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   double na = 0.0, nb = 0.0;
   if (valid && ty == 0) {
     double pt = d_zero;
+    if (!ce && f.qfuse) { ST(f.bpsa, o2, LD(f.psa, o2)); ST(f.bpsb, o2, LD(f.psb, o2)); }
     if (!ce) {
       for (int k = 1; k <= kz + 1; k++) ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, d_zero);
     } else {
@@ -198,6 +275,18 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
       ST(f.ptenn, o2, pt);
       const double pc = psbv + pt * dt;
       ST(f.psc, o2, pc);
+      if (f.qfuse) {
+        // the RA filter of p* (Main/mod_tendency.F90:420, filter_ra_2d) into the next buffers
+        const double pa = LD(f.psa, o2);
+        if (ci) {
+          const double d = c->gnu1 * (pc + psbv - d_two * pa);
+          ST(f.bpsb, o2, pa + d);
+          ST(f.bpsa, o2, pc);
+        } else {
+          ST(f.bpsa, o2, pa);
+          ST(f.bpsb, o2, psbv);
+        }
+      }
       if (s->lcount > 0 && ci && own) {
         na = fabs(pt);
         nb = fabs((pc + psbv - d_two * LD(f.psa, o2)) / (dt * dt * d_rfour));
@@ -767,6 +856,27 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
   } while (0)
 
+// qfuse, k_scalars at an owned point: k_qfilter's work for one moisture forecast fq (n = 0 qv,
+// 1 qc).  A non-negative forecast is final (the negative-moisture fix, Main/mod_tendency.F90:
+// 382-393, rewrites negative ones only), so its RAW filter (:424-427) against the RA-filtered
+// p* (:420: psc, psa + gnu1 (psc + psb - 2 psa)) is done here into the next buffers; a
+// negative one is listed for k_split_project's fix-up blocks.  The atm1/atm2 values are
+// loaded again here (lines the thread read before): holding them from the vertical fluxes on
+// costs k_scalars registers.
+__device__ __forceinline__ void scalars_qraw(const Consts* __restrict__ c, const Fields& f, int n, double fq,
+                                          uint32_t o2, uint32_t o3, double ps, double pb) {
+  if (fq < d_zero) {
+    f.neglist[atomicAdd(f.negcnt, 1)] = (o3 >> 3) * 2u + (uint32_t)n;
+    return;
+  }
+  const double psc = LD(f.psc, o2);
+  const double pbn = ps + c->gnu1 * (psc + pb - d_two * ps);
+  double n1, n2;
+  raw_filter(c, n, fq, LD(n ? f.a1qc : f.a1qv, o3), LD(n ? f.a2qc : f.a2qv, o3), psc, pbn, n1, n2);
+  ST(n ? f.b1qc : f.b1qv, o3, n1);
+  ST(n ? f.b2qc : f.b2qv, o3, n2);
+}
+
 __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __restrict__ c,
                                                     const StepState* __restrict__ s, Fields f) {
   __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
@@ -996,6 +1106,16 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
     tq = tq + rfac * (xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0));
   }
   DIFFU_X(tq, sQVB);
+  // the qv sums and forecast (and with qfuse its RAW filter) before the qc chain, so the qv
+  // operands are dead while it runs
+  tq = ((spq + tq) + (f.qvphy ? LD(f.qvphy, o3) : d_zero)) + d_zero;
+  if (f.qvten) ST(f.qvten, o3, tq);
+  const bool qown = f.qfuse && in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2);
+  {
+    const double fcqv = qv2 + dt * tq;
+    ST(f.cqv, o3, fcqv);
+    if (qown) scalars_qraw(c, f, 0, fcqv, o2, o3, ps, pb);
+  }
   // ================= qc
   // hadvqx, or the semi-Lagrangian start of qxdyn (:1378-1380)
   double tc = c->isladvec ? LD(f.slqc, o3)
@@ -1027,11 +1147,13 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
   DIFFU_X(tc, sQCB);
 #undef DT
 #undef H1T
-  tq = ((spq + tq) + (f.qvphy ? LD(f.qvphy, o3) : d_zero)) + d_zero;
   tc = ((d_zero + tc) + (f.qcphy ? LD(f.qcphy, o3) : d_zero)) + d_zero;
-  if (f.qvten) { ST(f.qvten, o3, tq); ST(f.qcten, o3, tc); }
-  ST(f.cqv, o3, qv2 + dt * tq);
-  ST(f.cqc, o3, qc2 + dt * tc);
+  if (f.qcten) ST(f.qcten, o3, tc);
+  {
+    const double fcqc = qc2 + dt * tc;
+    ST(f.cqc, o3, fcqc);
+    if (qown) scalars_qraw(c, f, 1, fcqc, o2, o3, ps, pb);
+  }
   PT_PRINT(3);
 }
 #undef DIFFU_X
@@ -1048,45 +1170,6 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
 // k_split_project (nothing in splitf reads moisture).  Fixed values are stored only for
 // negative points: a fixed predecessor is (cq < 0 ? fq : cq).  p* is filtered on the fly by
 // every thread and stored by the k = 1 threads into the next p* buffers.
-__device__ __forceinline__ double negfix_sum(const Geom& g, const double* sv, const double* fx, int j, int i, int k,
-                                             bool use_fixed) {
-  double sum = 0.0;
-  for (int ii = i - 1; ii <= i + 1; ii++)
-    for (int jj = j - 1; jj <= j + 1; jj++) {
-      double v = F3(sv, jj, ii, k);
-      if (use_fixed) {
-        const bool pred = (ii < i) || (ii == i && jj < j);
-        if (pred && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) v = F3(fx, jj, ii, k);
-      }
-      sum = sum + fabs(v);
-    }
-  return 0.01 * sum / 9.0;
-}
-
-__device__ __forceinline__ bool negfix_dependent(const Geom& g, const double* sv, int j, int i, int k) {
-#define NEG(J, I) (in(J, g.jci1, g.jci2) && in(I, g.ici1, g.ici2) && F3(sv, J, I, k) < d_zero)
-  return NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
-#undef NEG
-}
-
-// RAW filters of one point (filter_raw_qv / filter_raw_4d) with the filtered p*
-__device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, double o1, double o2v, double pa,
-                                           double pb, double& n1, double& n2) {
-  const double beta = 0.53;
-  if (n == 0) {
-    const double d = c->gnu1 * (fq + o2v - d_two * o1);
-    n2 = dmax(o1 + beta * d, MINQQ * pa);
-    n1 = dmax(fq + (beta - d_one) * d, MINQQ * pb);
-  } else {
-    const double d = c->gnu2 * (fq + o2v - d_two * o1);
-    double m = o1 + beta * d;
-    double q = fq + (beta - d_one) * d;
-    if (m < d_zero) m = d_zero;
-    if (q < d_zero) q = d_zero;
-    n2 = m;
-    n1 = q;
-  }
-}
 
 // Two adjacent points (j, j+1) per thread with 16-byte accesses (rows start 128-B aligned and
 // pairs start at even j - j0); the second point of a pair may fall in the row padding.
@@ -1192,8 +1275,11 @@ __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFi
           const double v = negfix_sum(g, sv, fx, jj, i, k, true);
           F3(fx, jj, i, k) = v;
           double n1, n2;
-          raw_filter(c, n, v, F3(n ? q.o1qc : q.o1qv, jj, i, k), F3(n ? q.o2qc : q.o2qv, jj, i, k),
-                     F2(q.psa, jj, i), F2(q.psb, jj, i), n1, n2);
+          // the RA-filtered p* of the step (Main/mod_tendency.F90:420), formed again from psc and
+          // the step's p* (with qfuse k_split_correct corrects psa/psb beside this sweep)
+          const double pc = F2(q.psc, jj, i), po = F2(q.opsa, jj, i);
+          raw_filter(c, n, v, F3(n ? q.o1qc : q.o1qv, jj, i, k), F3(n ? q.o2qc : q.o2qv, jj, i, k), pc,
+                     po + c->gnu1 * (pc + F2(q.opsb, jj, i) - d_two * po), n1, n2);
           F3(n ? q.n1qc : q.n1qv, jj, i, k) = n1;
           F3(n ? q.n2qc : q.n2qv, jj, i, k) = n2;
         }
@@ -1201,6 +1287,35 @@ __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFi
     }
   }
   if (lane == 0) q.depplane[plane_id] = 0;
+}
+
+// qfuse: k_qfilter's fix of the negative forecasts k_scalars listed, one entry per thread
+// (grid-stride over the list): an independent negative point (no negative sweep-predecessor)
+// is fixed and RAW-filtered here, a dependent one flags its plane for the serial sweep
+// (k_split_correct's extra blocks, after this launch)
+__device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int t0, int stride) {
+  const int cnt = *q.negcnt;
+  for (int e = t0; e < cnt; e += stride) {
+    const uint32_t w = q.neglist[e];
+    const int n = (int)(w & 1u);
+    const long el = (long)(w >> 1);
+    const int k = (int)(el / g.plane) + 1;
+    const long r = el % g.plane;
+    const int i = g.i0 + (int)(r / g.pitch), j = g.j0 + (int)(r % g.pitch);
+    const double* sv = n ? q.cqc : q.cqv;
+    if (negfix_dependent(g, sv, j, i, k)) {
+      atomicOr(&q.depplane[n * c->kz + (k - 1)], 1);
+      continue;
+    }
+    double* fx = n ? q.fqc : q.fqv;
+    const double v = negfix_sum(g, sv, fx, j, i, k, false);
+    F3(fx, j, i, k) = v;
+    double n1, n2;
+    raw_filter(c, n, v, F3(n ? q.o1qc : q.o1qv, j, i, k), F3(n ? q.o2qc : q.o2qv, j, i, k), F2(q.psa, j, i),
+               F2(q.psb, j, i), n1, n2);
+    F3(n ? q.n1qc : q.n1qv, j, i, k) = n1;
+    F3(n ? q.n2qc : q.n2qv, j, i, k) = n2;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1221,11 +1336,12 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
     const double* __restrict__ msfd, const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
     double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw, double* wdeld, double* wdelh,
-    double* wpsdota, double* wpsa) {
+    double* wpsdota, double* wpsa, const double* __restrict__ o2u, const double* __restrict__ o2v) {
   extern __shared__ double lds[];                        // 4 x kz x 64
   const int b = blockIdx.x;
   if (b >= nproj) {
-    if (threadIdx.x < 64) negfix_serial_plane(g, c, qf, b - nproj);
+    if (qf.negcnt) negfix_list(g, c, qf, (b - nproj) * 512 + (int)threadIdx.x, ((int)gridDim.x - nproj) * 512);
+    else if (threadIdx.x < 64) negfix_serial_plane(g, c, qf, b - nproj);
     return;
   }
   PT_DECL
@@ -1251,12 +1367,23 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
   }
   if (ce) {
     const double m00 = F2(msfd, j, i), m10 = F2(msfd, j + 1, i), m01 = F2(msfd, j, i + 1), m11 = F2(msfd, j + 1, i + 1);
+    // qfuse: a ghost dot point k_momentum does not update (the boundary lines' ring points)
+    // was not copied into the next atm2 buffers (keep_point): read it from the step's own
+    const int jd2 = g.br ? g.jdi2 : g.jde2 + 1, id2 = g.bt ? g.idi2 : g.ide2 + 1;
+    auto old_at = [&](int jj, int ii) {
+      return qf.negcnt && !(in(jj, g.jde1, g.jde2) && in(ii, g.ide1, g.ide2)) &&
+             !(in(jj, g.jdi1, jd2) && in(ii, g.idi1, id2));
+    };
+    const double* U01 = old_at(j, i + 1) ? o2u : a2u; const double* V01 = old_at(j, i + 1) ? o2v : a2v;
+    const double* U11 = old_at(j + 1, i + 1) ? o2u : a2u; const double* V11 = old_at(j + 1, i + 1) ? o2v : a2v;
+    const double* U10 = old_at(j + 1, i) ? o2u : a2u; const double* V10 = old_at(j + 1, i) ? o2v : a2v;
     for (int k = ty + 1; k <= kz; k += 8) {
-#define DIV(U, V) (-(F3(U, j, i + 1, k) * m01) + (F3(U, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) + \
-                   (F3(U, j + 1, i, k) * m10) + (F3(V, j, i + 1, k) * m01) + (F3(V, j + 1, i + 1, k) * m11) - \
-                   (F3(V, j, i, k) * m00) - (F3(V, j + 1, i, k) * m10))
-      sD1[(k - 1) * 64 + tx] = DIV(a1u, a1v);
-      sD2[(k - 1) * 64 + tx] = DIV(a2u, a2v);
+#define DIV(U, V, U01, U11, U10, V01, V11, V10)                                                            \
+  (-(F3(U01, j, i + 1, k) * m01) + (F3(U11, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) +                \
+   (F3(U10, j + 1, i, k) * m10) + (F3(V01, j, i + 1, k) * m01) + (F3(V11, j + 1, i + 1, k) * m11) -            \
+   (F3(V, j, i, k) * m00) - (F3(V10, j + 1, i, k) * m10))
+      sD1[(k - 1) * 64 + tx] = DIV(a1u, a1v, a1u, a1u, a1u, a1v, a1v, a1v);
+      sD2[(k - 1) * 64 + tx] = DIV(a2u, a2v, U01, U11, U10, V01, V11, V10);
 #undef DIV
       sT1[(k - 1) * 64 + tx] = F3(a1t, j, i, k);
       sT2[(k - 1) * 64 + tx] = F3(a2t, j, i, k);
@@ -1534,12 +1661,20 @@ __device__ __forceinline__ void split_correct_body(
     const Geom& g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum,
     const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
     double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance,
-    const double* __restrict__ red, int red_total, FlagSnap* ring, const BdyArgs& ba) {
+    const double* __restrict__ red, int red_total, FlagSnap* ring, const BdyArgs& ba, const QFix& qf, int nser) {
+  // qfuse: the serial sweeps of the planes k_split_project flagged, in trailing z slices (one
+  // wavefront per plane)
+  if (nser && (int)blockIdx.z >= (int)gridDim.z - nser) {
+    const int plane = (((int)blockIdx.z - ((int)gridDim.z - nser)) * (int)gridDim.y + (int)blockIdx.y) *
+                          (int)gridDim.x + (int)blockIdx.x;
+    if (threadIdx.y == 0 && plane < 2 * c->kz) negfix_serial_plane(g, c, qf, plane);
+    return;
+  }
   // bdyval blocks first: the leading z slices (blockIdx.z < zbdy) are dispatched before any
   // correction block, so their latency chain overlaps the corrections instead of trailing
   // them; 4 (line, chunk, level) items of 64 points per block
   const int kz = c->kz;
-  const int zbdy = BDY ? (int)gridDim.z - kz : 0;
+  const int zbdy = BDY ? (int)gridDim.z - nser - kz : 0;
   if (BDY && (int)blockIdx.z < zbdy) {
     const int nchunk = bdy_chunks_d(g);
     const int item = (((int)blockIdx.z * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x) * 4 +
@@ -1688,9 +1823,10 @@ __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct(Geom g, const Co
                                 const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                 const double* __restrict__ msfd, double* psa, double* psb, double* a1t,
                                 double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s,
-                                int advance, const double* __restrict__ red, int red_total, FlagSnap* ring) {
+                                int advance, const double* __restrict__ red, int red_total, FlagSnap* ring, QFix qf,
+                                int nser) {
   split_correct_body<false, NS>(g, c, ddsum, dhsum, psdota, msfd, psa, psb, a1t, a2t, a1u, a1v, a2u, a2v, s, advance,
-                            red, red_total, ring, BdyArgs{});
+                            red, red_total, ring, BdyArgs{}, qf, nser);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1830,9 +1966,9 @@ template <int NS>
 __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum,
                                     const double* __restrict__ dhsum, const double* __restrict__ psdota,
                                     const double* __restrict__ msfd, StepState* s, int advance,
-                                    const double* __restrict__ red, int red_total, BdyArgs a) {
+                                    const double* __restrict__ red, int red_total, BdyArgs a, QFix qf, int nser) {
   split_correct_body<true, NS>(g, c, ddsum, dhsum, psdota, msfd, a.psa, a.psb, a.a1t, a.a2t, a.a1u, a.a1v, a.a2u, a.a2v,
-                           s, advance ? 2 : 0, red, red_total, nullptr, a);
+                           s, advance ? 2 : 0, red, red_total, nullptr, a, qf, nser);
 }
 
 // one instance per nsplit (1..MAXSPLIT): the mode loops unroll and only the split slots in
@@ -1842,11 +1978,11 @@ __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct_bdy(Geom g, cons
                                                 const double* __restrict__, const double* __restrict__,       \
                                                 const double* __restrict__, double*, double*, double*, double*, \
                                                 double*, double*, double*, double*, StepState*, int,          \
-                                                const double* __restrict__, int, FlagSnap*);                 \
+                                                const double* __restrict__, int, FlagSnap*, QFix, int);      \
   template __global__ __launch_bounds__(256, SCOR_LB) void k_split_correct_bdy<NS_>(Geom, const Consts* __restrict__, const double* __restrict__, \
                                                     const double* __restrict__, const double* __restrict__,      \
                                                     const double* __restrict__, StepState*, int,                 \
-                                                    const double* __restrict__, int, BdyArgs);
+                                                    const double* __restrict__, int, BdyArgs, QFix, int);
 RCM_SPLIT_INST(1)
 RCM_SPLIT_INST(2)
 RCM_SPLIT_INST(3)

@@ -12,6 +12,8 @@ struct Seg {
   long off;
 };
 constexpr int MAXSEG = 64;
+// k_split_project's extra blocks for the listed negative moisture forecasts (qfuse)
+constexpr int NEGFIX_BLOCKS = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
@@ -48,6 +50,13 @@ struct Fields {
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy;
   const double* kpbl;          // iuwvadv = 1 (ibltyp = 2): the PBL-top level, vadv4d ind = 3 of qc
+  // qfuse (the step without k_qfilter): k_columns filters p* into bpsa/bpsb and copies the
+  // points the update kernels do not write into the next buffers; k_scalars RAW-filters the
+  // non-negative moisture forecasts into b1q/b2q and appends the negative ones to neglist
+  // (element offset * 2 + n) for k_split_project's fix-up blocks
+  int qfuse;
+  int* negcnt;
+  uint32_t* neglist;
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
   int red_off;                 // this tile's first partial
 };
@@ -60,7 +69,14 @@ struct QFix {
   const double *o1qv, *o1qc, *o2qv, *o2qc;
   double *n1qv, *n1qc, *n2qv, *n2qc;
   const double *psa, *psb;
+  // the step's p* before its RA filter and psc: the serial sweep (in k_split_correct with
+  // qfuse, beside the split corrections of psa/psb) forms the filtered p* from them
+  const double *psc, *opsa, *opsb;
   int* depplane;
+  // qfuse: the negative forecasts k_scalars listed (k_split_project fixes the independent ones
+  // in parallel; the serial sweeps of the flagged planes run in k_split_correct)
+  const int* negcnt;
+  const uint32_t* neglist;
 };
 
 __global__ void k_surface_pressures(Geom g, Fields f);
@@ -76,13 +92,14 @@ __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const doub
                                 const double* __restrict__ psb, const double* __restrict__ msfd,
                                 const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
                                 double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw,
-                                double* wdeld, double* wdelh, double* wpsdota, double* wpsa);
+                                double* wdeld, double* wdelh, double* wpsdota, double* wpsa,
+                                const double* __restrict__ o2u, const double* __restrict__ o2v);
 __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_fused(Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
 template <int NS>
-__global__ __launch_bounds__(256) void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring);
+__global__ __launch_bounds__(256) void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring, QFix qf, int nser);
 // pointers of bdyval (k_bdyval_set)
 struct BdyArgs {
   double *a1u, *a1v, *a1t, *a1qv, *a1qc, *a2u, *a2v, *a2t, *a2qv, *a2qc, *psa, *psb;
@@ -95,7 +112,7 @@ __global__ void k_bdyval_set(Geom g, const StepState* __restrict__ s, BdyArgs a)
 // 64-point chunks of the longest boundary line, one point past the tile included
 inline int bdy_chunks(const Geom& g) { return (std::max(g.jde2 - g.jde1, g.ide2 - g.ide1) + 65) / 64; }
 template <int NS>
-__global__ __launch_bounds__(256) void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, StepState* s, int advance, const double* __restrict__ red, int red_total, BdyArgs a);
+__global__ __launch_bounds__(256) void k_split_correct_bdy(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, StepState* s, int advance, const double* __restrict__ red, int red_total, BdyArgs a, QFix qf, int nser);
 __global__ void k_bdyval_qc(Geom g, int do_qc, int do_qv, double* a1qc, double* a1qv, const double* __restrict__ psa, Slices sl, long slen, StepState* s, double dtsec, int advance, FlagSnap* ring);
 __global__ void k_flag_snapshot(const StepState* __restrict__ s, FlagSnap* ring);
 __global__ void k_err_gather(const StepState* __restrict__ s, int32_t* derr);

@@ -231,11 +231,47 @@ def test_kernel_times_hook(c1_data):
     for name, v in kt.items():          # level-marching forms: k_scalars_km<opt> -> k_scalars
         b = name.split("<")[0]
         base[b[:-3] if b.endswith("_km") else b] = v
-    # rcmdyn_step's step: bdyval's boundary lines run inside k_split_correct_bdy
-    for k in ("k_momentum", "k_scalars", "k_columns", "k_qfilter", "k_split_project",
+    # rcmdyn_step's step: bdyval's boundary lines run inside k_split_correct_bdy, k_qfilter's
+    # work in k_columns / k_scalars / the extra blocks of k_split_project and k_split_correct
+    for k in ("k_momentum", "k_scalars", "k_columns", "k_split_project",
               "k_spstep_fused", "k_split_correct_bdy", "k_bdyval_qc"):
         assert k in base and base[k][0] == 3 and base[k][1] > 0.0, k
-    assert "k_bdyval_set" not in base and "k_split_correct" not in base, sorted(base)
+    for k in ("k_bdyval_set", "k_split_correct", "k_qfilter"):
+        assert k not in base, sorted(base)
+
+
+QFUSE_CASES = [({}, (1, 1)), ({}, (2, 2)), ({}, (1, 3)), ({"iboudy": 4}, (2, 1)), ({"isladvec": 1}, (2, 2)),
+               ({"ibltyp": 2}, (1, 1))]
+
+
+@pytest.mark.parametrize("variant,nproc", QFUSE_CASES, ids=lambda x: str(x))
+def test_qfilter_fusion_equals_qfilter(c1_data, monkeypatch, variant, nproc):
+    """The step without k_qfilter (qfuse: p*'s RA filter and the copies in k_columns, the RAW
+    filter of non-negative moisture in k_scalars, the listed negatives fixed in the extra
+    blocks of k_split_project and k_split_correct) is bit-identical to the k_qfilter step
+    (RCMDYN_NO_QFUSE), eager and graph-replayed, with a state that forces clusters of dependent
+    negative qv (the serial sweep) and on decompositions."""
+    import dataclasses
+    from regcm_amd.dycore import DynCore
+    rc, data = c1_data
+    rcv = dataclasses.replace(rc, **variant)
+    st = {k: v.copy() for k, v in data["state"].items()}
+    # dry columns with alternating signs in the forecast: rows of negative qv on a few levels
+    st["ATM1_QV"][5:8, 10:14, 10:30] = -1e-7 * st["PSA"][0][10:14, 10:30]
+    st["ATM2_QV"][5:8, 10:14, 10:30] = -2e-7 * st["PSA"][0][10:14, 10:30]
+    if rcv.ibltyp == 2:
+        st.update(icbc.tke_state(rcv))
+    fused = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    monkeypatch.setenv("RCMDYN_NO_QFUSE", "1")
+    sep = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    for e in (fused, sep):
+        e.put_state(st)
+        e.bdyval()
+        e.step(5)
+    assert fused.get_time() == sep.get_time()
+    for name in list(STATE_FIELDS) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
+        assert np.array_equal(fused.get(name), sep.get(name)), name
+    assert np.array_equal(fused.reductions(), sep.reductions())
 
 
 FUSE_CASES = [({}, (1, 1)), ({}, (2, 2)), ({}, (1, 3)), ({"iboudy": 4}, (1, 1)), ({"iboudy": 4}, (2, 2)),
