@@ -282,6 +282,15 @@ struct rcmdyn_engine {
     return v && *v && std::strcmp(v, "0") != 0;
   }();
   bool qfuse() const { return cfg.idynamic != 2 && !no_qfuse; }
+  // halo/compute overlap of the hydrostatic prologue exchange (Part, kernels.hpp) on a
+  // decomposed domain; RCMDYN_NO_OVERLAP=1: the atm1/p* part first, then the atm2 part beside
+  // k_columns only
+  const bool no_overlap = [] {
+    const char* v = std::getenv("RCMDYN_NO_OVERLAP");
+    return v && *v && std::strcmp(v, "0") != 0;
+  }();
+  bool overlap() const { return ntiles > 1 && cfg.idynamic != 2 && !no_overlap; }
+  bool post_inner = false;    // tend_pre ran part 1 of k_momentum / k_scalars
   std::string err;
   std::unique_ptr<Comm> comm;
   // RCMDYN_FORCE_RCCL=1: the halo messages between tiles held by this engine travel as RCCL
@@ -473,6 +482,7 @@ struct rcmdyn_engine {
     // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
     t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
     t.nred = t.ncolx * (g.idx2() - g.idx1() + 1);
+    if (overlap()) setup_overlap(t);
     t.red_off = red_total;
     red_total += t.nred;
     if (cfg.idynamic == 2) setup_nh(t);
@@ -1387,6 +1397,40 @@ struct rcmdyn_engine {
     }
   }
 
+  // R of a tile: the column-box points whose k_columns work reads no ghost point toward a
+  // neighbour (atm1 at j+1 / i+1, p* at +-1, psdot's j-1 / i-1), i.e. the owned points one in
+  // from every side that has a neighbour; and the k_momentum / k_scalars blocks whose staged
+  // halo-2 tile lies in R (their part-1 blocks, the same test as part_skip)
+  void setup_overlap(Tile& t) {
+    const Geom& g = t.g;
+    t.rja = g.bl ? g.jdx1() : g.jde1 + 1;
+    t.rjb = g.br ? g.jdx2() : g.jde2 - 1;
+    t.ria = g.bb ? g.idx1() : g.ide1 + 1;
+    t.rib = g.bt ? g.idx2() : g.ide2 - 1;
+    if (t.rja > t.rjb || t.ria > t.rib) return;
+    const long box = (long)(g.jdx2() - g.jdx1() + 1) * (g.idx2() - g.idx1() + 1);
+    const long rin = (long)(t.rjb - t.rja + 1) * (t.rib - t.ria + 1);
+    t.rnxb = (t.rjb - t.rja + 64) / 64;
+    t.nint = t.rnxb * (t.rib - t.ria + 1);
+    t.nring = (int)((box - rin + 63) / 64);
+    t.nred = t.nint + t.nring;
+    auto inner = [&](int J0, int I0, int bj, int bi) {
+      return J0 - 2 >= t.rja && J0 + bj + 1 <= t.rjb && I0 - 2 >= t.ria && I0 + bi + 1 <= t.rib;
+    };
+    const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
+    for (int by = 0; by < (mi2 - g.idi1 + MBI) / MBI; by++)
+      for (int bx = 0; bx < (mj2 - g.jdi1 + MBJ) / MBJ; bx++)
+        t.mom_in = t.mom_in || inner(g.jdi1 + bx * MBJ, g.idi1 + by * MBI, MBJ, MBI);
+    for (int by = 0; by < (g.icx2() - g.icx1() + SBI) / SBI; by++)
+      for (int bx = 0; bx < (g.jcx2() - g.jcx1() + SBJ) / SBJ; bx++)
+        t.sca_in = t.sca_in || inner(g.jcx1() + bx * SBJ, g.icx1() + by * SBI, SBJ, SBI);
+  }
+  Fields fields(Tile& t, int part) {
+    Fields f = fields(t);
+    f.pt = Part{part, t.rja, t.rjb, t.ria, t.rib, t.rnxb, t.nint};
+    return f;
+  }
+
   // dynamic LDS of the two-phase column kernels: 4 x kz x 64 doubles
   size_t col_lds() const { return sizeof(double) * 4 * 64 * (size_t)cfg.kz; }
 
@@ -1608,14 +1652,16 @@ struct rcmdyn_engine {
   void tend(int phase = TEND_ALL, bool slice = false) {
     if (cfg.idynamic == 2) nh_tend(phase, slice);
     else {
-      if (phase & TEND_PRE) tend_pre(slice);
+      // part 1 of k_momentum / k_scalars beside the prologue exchange only in a whole tend (no
+      // host work between) without the semi-Lagrangian pass that precedes them
+      if (phase & TEND_PRE) tend_pre(slice, phase == TEND_ALL && !slice && cfg.isladvec != 1);
       if (phase & TEND_POST) tend_post();
     }
     // the hydrostatic step's snapshot is written by k_split_correct's clock lane
     if ((phase & TEND_POST) && cfg.idynamic == 2) KLAUNCH(k_flag_snapshot, dim3(1), dim3(64), 0, stream, ds, dflags);
   }
 
-  void tend_pre(bool slice) {
+  void tend_pre(bool slice, bool with_post = false) {
     const int kz = cfg.kz;
     // One exchange point for the whole prologue (Main/mod_tendency.F90:815-1116,
     // Main/mod_slice.F90:102-300): the decoupled fields are recomputed where read, so their
@@ -1631,21 +1677,52 @@ struct rcmdyn_engine {
                              {FK::A2QC, kz, 3}};
     // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
     if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro2.push_back({FK::A2TKE, kz + 1, 2}); }
-    fork_point();
-    xchv(pro);
-    fork_after_exchange();
-    xch_begin(pro2);
-    ghosts_stale = false;
     // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
     // geopotential in one launch (calc_coeff is formed where it is read, in k_momentum and
     // k_scalars)
-    each([&](Tile& t) {
+    auto columns = [&](Tile& t, int part, int ncol, bool ring) {
       const Geom& g = t.g;
-      const int nsp = (int)((g.nj * (long)g.ni + 511) / 512);
-      KLAUNCH(k_columns, dim3(t.nred + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t), t.ncolx, t.nred);
-    });
-    xch_join();
+      const int nsp = ring ? (int)((g.nj * (long)g.ni + 511) / 512) : 0;
+      KLAUNCH(k_columns, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
+    };
+    if (overlap()) {
+      // the whole exchange on the second stream; meanwhile part 1 of k_columns and, in a whole
+      // step (k_momentum / k_scalars follow with no host work between), of k_momentum and
+      // k_scalars; part 2 of each after the join
+      pro.insert(pro.end(), pro2.begin(), pro2.end());
+      fork_point();
+      xch_begin(pro);
+      ghosts_stale = false;
+      each([&](Tile& t) { if (t.nint) columns(t, 1, t.nint, false); });
+      post_inner = with_post;
+      if (with_post) each([&](Tile& t) { post_launch(t, 1); });
+      xch_join();
+      each([&](Tile& t) { columns(t, t.nint ? 2 : 0, t.nint ? t.nring : t.nred, true); });
+    } else {
+      fork_point();
+      xchv(pro);
+      fork_after_exchange();
+      xch_begin(pro2);
+      ghosts_stale = false;
+      each([&](Tile& t) { columns(t, 0, t.nred, true); });
+      xch_join();
+    }
     if (slice) run_slice();
+  }
+
+  // k_momentum and k_scalars of one tile: part 1 the blocks in R (when it has any), part 2 the
+  // others; part 0 all
+  void post_launch(Tile& t, int part) {
+    const Geom& g = t.g;
+    const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
+    const int pm = part == 0 ? 0 : (t.nint && t.mom_in ? part : (part == 1 ? -1 : 0));
+    const int ps = part == 0 ? 0 : (t.nint && t.sca_in ? part : (part == 1 ? -1 : 0));
+    if (pm >= 0)
+      KLAUNCH(k_momentum, dim3((mj2 - g.jdi1 + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, cfg.kz), dim3(MBT), 0,
+              stream, g, dc, ds, fields(t, pm));
+    if (ps >= 0)
+      KLAUNCH(k_scalars, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, cfg.kz),
+              dim3(SBT), 0, stream, g, dc, ds, fields(t, ps));
   }
 
   void tend_post() {
@@ -1660,16 +1737,9 @@ struct rcmdyn_engine {
       });
       xch({{FK::SLQV, kz}, {FK::SLQC, kz}}, 1, 0);
     }
-    // fused tendencies + forecast + time filter
-    each([&](Tile& t) {
-      const Geom& g = t.g;
-      const Fields f = fields(t);
-      const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
-      KLAUNCH(k_momentum, dim3((mj2 - g.jdi1 + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, kz), dim3(MBT), 0,
-              stream, g, dc, ds, f);
-      KLAUNCH(k_scalars, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, kz), dim3(SBT),
-              0, stream, g, dc, ds, f);
-    });
+    // fused tendencies + forecast + time filter (part 2 when tend_pre ran part 1)
+    each([&](Tile& t) { post_launch(t, post_inner ? 2 : 0); });
+    post_inner = false;
     tke_step();
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current

@@ -180,6 +180,11 @@ struct Tile {
   double *sbuf2 = nullptr, *rbuf2 = nullptr;   // of the exchange on the engine's second stream
   int red_off = 0, nred = 0;       // this tile's slice of the engine's reduction partials
   int ncolx = 0;                   // k_columns blocks per row
+  // halo/compute overlap (Part, kernels.hpp): the rectangle R of points no exchange writes,
+  // k_columns' part 1 / part 2 block counts (nint = 0: no split, part 0), and whether any
+  // k_momentum / k_scalars block lies in R
+  int rja = 0, rjb = -1, ria = 0, rib = -1, rnxb = 0, nint = 0, nring = 0;
+  bool mom_in = false, sca_in = false;
   std::vector<void*> allocs;
 };
 

@@ -152,6 +152,44 @@ __device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, do
 #ifndef COL_LB
 #define COL_LB 6
 #endif
+// the column of lane tx in column block bb: part 0 the rows of the column box, part 1 the
+// rows of R, part 2 the column box less R as one list (rows below R, the strips left and right
+// of R, rows above R); false past the end
+__device__ __forceinline__ bool column_of(const Geom& g, const Part& p, int bb, int tx, int nxb, int& j, int& i) {
+  const int J1 = g.jdx1(), J2 = g.jdx2(), I1 = g.idx1(), I2 = g.idx2();
+  if (p.part == 1) {
+    j = p.ja + (bb % p.nxb) * 64 + tx;
+    i = p.ia + bb / p.nxb;
+    return j <= p.jb;
+  }
+  if (p.part == 2) {
+    const int W = J2 - J1 + 1, wl = p.ja - J1, wm = wl + (J2 - p.jb);
+    const int nb = (p.ia - I1) * W, nm = (p.ib - p.ia + 1) * wm, nt = (I2 - p.ib) * W;
+    int q = bb * 64 + tx;
+    j = J1; i = I1;
+    if (q < nb) { i = I1 + q / W; j = J1 + q % W; return true; }
+    q -= nb;
+    if (q < nm) {
+      const int c = q % wm;
+      i = p.ia + q / wm;
+      j = c < wl ? J1 + c : p.jb + 1 + (c - wl);
+      return true;
+    }
+    q -= nm;
+    if (q < nt) { i = p.ib + 1 + q / W; j = J1 + q % W; return true; }
+    return false;
+  }
+  j = J1 + (bb % nxb) * 64 + tx;
+  i = I1 + bb / nxb;
+  return j <= J2;
+}
+// part 1 / part 2 membership of a block whose reads span [j1, j2] x [i1, i2]: true when this
+// launch's part does not run it
+__device__ __forceinline__ bool part_skip(const Part& p, int j1, int j2, int i1, int i2) {
+  if (!p.part) return false;
+  const bool inner = j1 >= p.ja && j2 <= p.jb && i1 >= p.ia && i2 <= p.ib;
+  return inner != (p.part == 1);
+}
 #ifndef COL_KU
 #define COL_KU 1
 #endif
@@ -172,14 +210,15 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
     }
     return;
   }
-  if (f.qfuse && bb == 0 && threadIdx.x == 0) *f.negcnt = 0;  // k_scalars appends after this
+  // k_scalars appends after this (part 2 follows part 1 and the k_scalars blocks of part 1)
+  if (f.qfuse && bb == 0 && threadIdx.x == 0 && f.pt.part != 2) *f.negcnt = 0;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
   // columns compute exactly what their owners do (qdot, phi, pten and the new p* there replace
   // the reference's exchanges of them).
-  const int j = g.jdx1() + (bb % nxb) * 64 + tx, i = g.idx1() + bb / nxb;
-  const bool valid = j <= g.jdx2();
+  int j, i;
+  const bool valid = column_of(g, f.pt, bb, tx, nxb, j, i);
   const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const bool ce = valid && in(j, g.jcx1(), g.jcx2()) && in(i, g.icx1(), g.icx2());
   const bool ci = ce && g.gci(j, i);
@@ -194,6 +233,7 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   // qfuse: the points k_momentum / k_scalars / the moisture fix leave alone keep their values
   // in the next buffers (k_qfilter's copies), one level group per wavefront
   if (valid && f.qfuse) keep_point(g, f, j, i, ty + 1, 8, kz);
+  PT_MARK();
   double rp = 0.0;
   if (ce) {
     // phase 1: umc/vmc = atm1 * msfd (decouple :880-890); xqv/xqc decoupled moisture (:1000-1016)
@@ -231,11 +271,13 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
       sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
       }
     }
+    PT_MARK();
     // the hypsometric log ratios in a loop of their own (no loads in flight there: the log's
     // polynomial constants stay in registers without spilling)
     for (int k = ty + 1; k <= kz; k += 8)
       sLG[(k - 1) * 64 + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
                                         : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
+    PT_MARK();
   }
   __syncthreads();
   PT_MARK();
@@ -323,8 +365,9 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
       nb = nb + __shfl_down(nb, w);
     }
     if (tx == 0) {
-      f.red[2 * (f.red_off + bb)] = na;
-      f.red[2 * (f.red_off + bb) + 1] = nb;
+      const int slot = f.red_off + (f.pt.part == 2 ? f.pt.rbase : 0) + bb;
+      f.red[2 * slot] = na;
+      f.red[2 * slot + 1] = nb;
     }
   }
   PT_PRINT(1);
@@ -495,6 +538,7 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
   const int tid = threadIdx.x;
   PT_DECL
   const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
+  if (part_skip(f.pt, J0 - 2, J0 + MBJ + 1, I0 - 2, I0 + MBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
   const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;
@@ -887,6 +931,7 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
   // the tile's cross points and its ghost ring (k_qfilter's moisture fix reads the forecasts
   // there); boundary branches test global indices
   const int J0 = g.jcx1() + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
+  if (part_skip(f.pt, J0 - 2, J0 + SBJ + 1, I0 - 2, I0 + SBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
   const int jlo = g.j0, jhi = g.j0 + g.nj - 1, ilo = g.i0, ihi = g.i0 + g.ni - 1;

@@ -30,6 +30,17 @@ struct SegList {
 // boundary slices, order documented at k_bdyval_set
 struct Slices { double* s[16]; };
 
+// Halo/compute overlap of a decomposed tile: while the prologue exchange is in
+// flight on the second stream, part 1 runs the blocks of k_columns / k_momentum / k_scalars
+// whose reads all lie in R = [ja, jb] x [ia, ib], points no exchange writes and whose k_columns
+// outputs part 1 itself forms; part 2 runs the others after the join; part 0 every block.
+// k_columns maps its part 1 blocks onto the rows of R (nxb blocks of 64 columns per row) and
+// its part 2 blocks onto the rest of the column box as one list (rbase: part 1's block count,
+// so each block keeps its own noise partial).
+struct Part {
+  int part, ja, jb, ia, ib, nxb, rbase;
+};
+
 // Every device buffer of one tile for one ping-pong parity: a* are the current time levels,
 // b* the buffers the fused update kernels write the next time levels into.  Passed by value
 // (kernel argument segment -> SGPRs); all fields share the frame, so one 32-bit byte offset
@@ -59,6 +70,7 @@ struct Fields {
   uint32_t* neglist;
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
   int red_off;                 // this tile's first partial
+  Part pt;                     // the launch's overlap part (k_columns, k_momentum, k_scalars)
 };
 
 // serial negative-moisture fix-up of k_split_project's extra blocks: the q fields before

@@ -185,6 +185,37 @@ def test_decomposition_invariance_c3(nproc):
         assert np.array_equal(ref.get(name), til.get(name)), name
 
 
+@pytest.mark.parametrize("mode", ["step", "dropin", "serial"])
+def test_overlap_parts_bit_identical(monkeypatch, mode):
+    """Halo/compute overlap: on a decomposed domain the whole prologue exchange
+    runs on the second stream while part 1 of k_columns (and, in rcmdyn_step, of k_momentum
+    and k_scalars: the blocks whose staged tile reads no point an exchange writes) computes;
+    part 2 follows the join.  C3 on 1 x 2 tiles (192 x 96: k_momentum / k_scalars have part-1
+    blocks) is bit-identical to one tile, through rcmdyn_step, through the drop-in
+    tend + bdyval pair (k_columns split only) and with the split off (RCMDYN_NO_OVERLAP)."""
+    from regcm_amd.dycore import DynCore
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    ref = DynCore(rc, data["split"])
+    if mode == "serial":
+        monkeypatch.setenv("RCMDYN_NO_OVERLAP", "1")
+    til = DynCore(rc, data["split"], nproc_j=1, nproc_i=2)
+    for e in (ref, til):
+        e.put_state(data["state"])
+        e.bdyval()
+    ref.step(5)
+    if mode == "dropin":
+        for _ in range(5):
+            til.tend()
+            til.bdyval()
+    else:
+        til.step(5)
+    for name in STATE_FIELDS:
+        assert np.array_equal(ref.get(name), til.get(name)), name
+    a, b = ref.reductions(), til.reductions()
+    assert np.allclose(a[:2], b[:2], rtol=1e-12, atol=0), (a, b)   # the partials in another order
+
+
 def test_c2_ten_steps():
     rc = CONFIGS["C2"]
     data = icbc.generate(rc)
