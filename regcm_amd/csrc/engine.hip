@@ -300,8 +300,9 @@ struct rcmdyn_engine {
   // halo/compute overlap: the second stream carries the atm2 part of the prologue exchange
   // while the first computes what needs only atm1 and p* (xch_begin / xch_join)
   hipStream_t stream2 = nullptr;
-  hipEvent_t evfork = nullptr, evjoin = nullptr;
-  bool join_pending = false;
+  // two exchanges may be in flight on the second stream at once (joined separately, slot 0/1)
+  hipEvent_t evfork = nullptr, evjoin[2] = {nullptr, nullptr};
+  bool join_pending[2] = {false, false};
   bool on2 = false;           // an exchange is being issued on stream2 (its staging buffers)
   // plan-only engine (rcmdyn_exchange_plan): host logic only, no device call; the exchanges and
   // collectives a rank would issue are logged by a PlanComm
@@ -678,7 +679,7 @@ struct rcmdyn_engine {
     if (ntiles > 1) {
       HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&evfork, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&evjoin, hipEventDisableTiming));
+      for (hipEvent_t& e : evjoin) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
   }
 
@@ -701,7 +702,8 @@ struct rcmdyn_engine {
     if (red) (void)hipFree(red);
 
     if (evfork) (void)hipEventDestroy(evfork);
-    if (evjoin) (void)hipEventDestroy(evjoin);
+    for (hipEvent_t e : evjoin)
+      if (e) (void)hipEventDestroy(e);
     if (stream2) (void)hipStreamDestroy(stream2);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1262,7 +1264,7 @@ struct rcmdyn_engine {
   void fork_after_exchange() {
     if (comm && comm->shared_channels()) fork_point();
   }
-  void xch_begin(std::vector<XField> fs) {
+  void xch_begin(std::vector<XField> fs, int slot = 0) {
     if (ntiles == 1) return;
     DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
     std::swap(stream, stream2);
@@ -1276,13 +1278,13 @@ struct rcmdyn_engine {
     }
     on2 = false;
     std::swap(stream, stream2);
-    DHIPCHK(hipEventRecord(evjoin, stream2));
-    join_pending = true;
+    DHIPCHK(hipEventRecord(evjoin[slot], stream2));
+    join_pending[slot] = true;
   }
-  void xch_join() {
-    if (!join_pending) return;
-    DHIPCHK(hipStreamWaitEvent(stream, evjoin, 0));
-    join_pending = false;
+  void xch_join(int slot = 0) {
+    if (!join_pending[slot]) return;
+    DHIPCHK(hipStreamWaitEvent(stream, evjoin[slot], 0));
+    join_pending[slot] = false;
   }
 
   // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
@@ -1491,6 +1493,10 @@ struct rcmdyn_engine {
     const int kz = cfg.kz, kp = kz + 1;
     const int istep = nh_istep();
     const bool alarm = nh_day_alarm();
+    // halo/compute overlap of a whole tend on a decomposed domain: the cr/qdot/xkcr exchange
+    // on the second stream beside k_nh_tend_c (which reads them at its own point only), the
+    // cqv/cqc exchange beside k_nh_tend_d (which does not read them)
+    const bool ovl = ntiles > 1 && !no_overlap && phase == TEND_ALL && !slice && cfg.isladvec != 1;
     struct Grids { dim3 fr, ce1, cek, ci1, cik, cik1, di1, dik; };
     auto grids = [&](const Geom& g) {
       const int nce_j = g.jce2 - g.jce1 + 1, nce_i = g.ice2 - g.ice1 + 1;
@@ -1529,7 +1535,12 @@ struct rcmdyn_engine {
       const Grids q = grids(g);
       KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
     });
-    xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
+    if (ovl) {
+      fork_point();
+      xch_begin({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}}, 0);
+    } else {
+      xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
+    }
     if (slice) run_slice();
     }
     if (!(phase & TEND_POST)) return;
@@ -1548,16 +1559,23 @@ struct rcmdyn_engine {
       if (cfg.isladvec == 1)
         KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
       // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
-      {
-        const dim3 gd((g.jdi2 - g.jdi1 + 64) / 64, (g.idi2 - g.idi1 + TD_I) / TD_I, kz),
-            gc((g.nj + TC_J - 1) / TC_J, (g.ni + TC_I - 1) / TC_I, kp);
-        KLAUNCH(k_nh_tend_d, NH_ZFIRST ? dim3(gd.z, gd.x, gd.y) : gd, dim3(64, TD_I), 0, stream, g, dc, ds, f, istep);
-        KLAUNCH(k_nh_tend_c, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
-                (int)diag, istep);
+      if (!ovl) {
+        tend_d_launch(t, f, istep);
+        tend_c_launch(t, f, istep);
       }
     });
-    tke_step();
-    xch({{FK::CQV, kz}, {FK::CQC, kz}});
+    if (ovl) {
+      each([&](Tile& t) { tend_c_launch(t, nhfields(t), istep); });
+      fork_point();
+      xch_begin({{FK::CQV, kz}, {FK::CQC, kz}}, 1);
+      xch_join(0);
+      each([&](Tile& t) { tend_d_launch(t, nhfields(t), istep); });
+      xch_join(1);
+      tke_step();
+    } else {
+      tke_step();
+      xch({{FK::CQV, kz}, {FK::CQC, kz}});
+    }
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
@@ -1570,12 +1588,31 @@ struct rcmdyn_engine {
     // sound, Main/mod_sound.F90:163-718
     for (int it = 1; it <= istep; it++) {
       // part A: sub-step 1 in k_nh_tfilter_a1, the later ones in the previous k_nh_sound_cd
-      xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
-      each([&](Tile& t) {
+      // the dp'/dp0, pp exchange beside part 1 of k_nh_sound_uv (the points that read no ghost),
+      // then the strip of the others
+      auto sound_uv = [&](Tile& t, int part) {
         const Geom& g = t.g;
+        const int fin = (int)(it == istep), first = (int)(it == 1);
+        if (part == 2) {
+          const int n = (g.bl ? 0 : g.ide2 - g.ide1 + 1) + (g.bb ? 0 : g.jde2 - g.jde1 + (g.bl ? 0 : 1));
+          if (n > 0)
+            KLAUNCH(k_nh_sound_uv, dim3((n + 127) / 128, kz), dim3(128), 0, stream, g, dc, ds, nhfields(t), istep,
+                    fin, first, 2);
+          return;
+        }
         KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, dc, ds,
-                nhfields(t), istep, (int)(it == istep), (int)(it == 1));
-      });
+                nhfields(t), istep, fin, first, part);
+      };
+      if (ntiles > 1 && !no_overlap) {
+        fork_point();
+        xch_begin({{FK::NCDT, kz}, {FK::NCPP, kz}}, 0);
+        each([&](Tile& t) { sound_uv(t, 1); });
+        xch_join(0);
+        each([&](Tile& t) { sound_uv(t, 2); });
+      } else {
+        xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
+        each([&](Tile& t) { sound_uv(t, 0); });
+      }
       xch({{FK::NCU, kz}, {FK::NCV, kz}});
       each([&](Tile& t) {
         const Geom& g = t.g;
@@ -1615,6 +1652,18 @@ struct rcmdyn_engine {
     KLAUNCH(k_nh_advance, dim3(1), dim3(256), 0, stream, dc, ds, nhf[0]);
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+
+  void tend_d_launch(Tile& t, const NHFields& f, int istep) {
+    const Geom& g = t.g;
+    const dim3 gd((g.jdi2 - g.jdi1 + 64) / 64, (g.idi2 - g.idi1 + TD_I) / TD_I, cfg.kz);
+    KLAUNCH(k_nh_tend_d, NH_ZFIRST ? dim3(gd.z, gd.x, gd.y) : gd, dim3(64, TD_I), 0, stream, g, dc, ds, f, istep);
+  }
+  void tend_c_launch(Tile& t, const NHFields& f, int istep) {
+    const Geom& g = t.g;
+    const dim3 gc((g.nj + TC_J - 1) / TC_J, (g.ni + TC_I - 1) / TC_I, cfg.kz + 1);
+    KLAUNCH(k_nh_tend_c, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
+            (int)diag, istep);
   }
 
   // bdyval, non-hydrostatic: u, v, t, qv as the hydrostatic core (p* untouched), pp and w,

@@ -822,9 +822,9 @@ __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f
 }
 
 // substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
-__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
-                              int istep, int fin, int first) {
-  THREAD_POINT(g.jde1, g.ide1);
+__device__ __forceinline__ void nh_sound_uv_at(const Geom& g, const Consts* __restrict__ c,
+                                               const StepState* __restrict__ s, const NHFields& f, int istep,
+                                               int fin, int first, int j, int i, int k) {
   // sub-step 1: the loop's initial u, v = atm2 / psdotb (:217-228), formed here; on the dot
   // frame's boundary ring they stay so for the whole loop
   auto init_u = [&](int jj, int ii) { return F3(f.a2u, jj, ii, k) / F2(f.psdotb, jj, ii); };
@@ -860,6 +860,30 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
     F3(f.a2v, j, i, k) = F3(f.a1v, j, i, k) + d;
     F3(f.a1v, j, i, k) = vv;
   }
+}
+
+// Halo/compute overlap of the dp'/dp0, pp exchange: a dot point reads them at j-1 and i-1, so
+// only the column j = jde1 and the row i = ide1 read ghost points (on sides with a neighbour).
+// part 1 runs every other point while the exchange is in flight, part 2 that strip as a list
+// (1-D blocks, blockIdx.y = level) after the join; part 0 every point.
+__device__ __forceinline__ bool nh_uv_strip(const Geom& g, int j, int i) {
+  return (!g.bl && j == g.jde1) || (!g.bb && i == g.ide1);
+}
+__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                              int istep, int fin, int first, int part) {
+  if (part == 2) {
+    const int ni = g.ide2 - g.ide1 + 1, nj = g.jde2 - g.jde1 + 1;
+    const int ncol = g.bl ? 0 : ni, nrow = g.bb ? 0 : nj - (g.bl ? 0 : 1);
+    const int q = (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
+    if (q >= ncol + nrow) return;
+    const int j = q < ncol ? g.jde1 : g.jde1 + (g.bl ? 0 : 1) + (q - ncol);
+    const int i = q < ncol ? g.ide1 + q : g.ide1;
+    nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
+    return;
+  }
+  THREAD_POINT(g.jde1, g.ide1);
+  if (part == 1 && nh_uv_strip(g, j, i)) return;
+  nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
 }
 
 // cu, cv at the dot points (j,i), (j+1,i), (j,i+1), (j+1,i+1) around a cross point, one level

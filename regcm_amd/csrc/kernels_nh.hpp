@@ -73,7 +73,7 @@ __global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepStat
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f);
-__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int fin, int first);
+__global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int fin, int first, int part);
 __global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);

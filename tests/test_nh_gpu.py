@@ -150,6 +150,33 @@ def test_nh_decomposition_invariance(nh_data, nproc):
         assert np.array_equal(ref.get(name), til.get(name)), name
 
 
+@pytest.mark.parametrize("mode", ["dropin", "serial"])
+def test_nh_overlap_modes(nh_data, monkeypatch, mode):
+    """The NH halo/compute overlap (cr/qdot/xkcr beside k_nh_tend_c, cqv/cqc beside
+    k_nh_tend_d, dp'/dp0 and pp beside part 1 of k_nh_sound_uv, the strip after the join) is
+    bit-identical to one tile through the drop-in pair (tend's exchanges on the first stream,
+    the sound loop's overlapped) and with it off (RCMDYN_NO_OVERLAP=1); the default is
+    test_nh_decomposition_invariance."""
+    from regcm_amd.dycore import DynCore
+    rc, data = nh_data
+    ref = DynCore(rc, data["split"])
+    if mode == "serial":
+        monkeypatch.setenv("RCMDYN_NO_OVERLAP", "1")
+    til = DynCore(rc, data["split"], nproc_j=2, nproc_i=2)
+    for e in (ref, til):
+        e.put_state(data["state"])
+        e.bdyval()
+    ref.step(6)
+    if mode == "dropin":
+        for _ in range(6):
+            til.tend()
+            til.bdyval()
+    else:
+        til.step(6)
+    for name in NH_FIELDS:
+        assert np.array_equal(ref.get(name), til.get(name)), name
+
+
 @pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
 def test_nh_variant_decomposition(nh_data, variant):
     from regcm_amd.dycore import DynCore
