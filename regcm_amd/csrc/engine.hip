@@ -1729,9 +1729,16 @@ struct rcmdyn_engine {
     // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
     // geopotential in one launch (calc_coeff is formed where it is read, in k_momentum and
     // k_scalars)
+    // ring: the trailing blocks too (the frame points outside the column box, then with qfuse
+    // the copies of keep_point on the box's two outer rows and columns, every level)
     auto columns = [&](Tile& t, int part, int ncol, bool ring) {
       const Geom& g = t.g;
-      const int nsp = ring ? (int)((g.nj * (long)g.ni + 511) / 512) : 0;
+      int nsp = 0;
+      if (ring) {
+        const int W = g.jdx2() - g.jdx1() + 1, H = g.idx2() - g.idx1() + 1;
+        const long nkeep = qfuse() ? (long)(4 * W + 4 * std::max(H - 4, 0)) * kz : 0;
+        nsp = (int)((g.nj * (long)g.ni + 511) / 512 + (nkeep + 511) / 512);
+      }
       KLAUNCH(k_columns, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
     };
     if (overlap()) {

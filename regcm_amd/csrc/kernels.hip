@@ -199,6 +199,31 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   PT_DECL
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
+  const int nsp = (g.nj * g.ni + 511) / 512;
+  if (bb >= ncol + nsp) {
+    // qfuse: the copies of keep_point on the two outer rows and columns of the column box (every
+    // point that has one), one (point, level) per thread; in blocks of their own so that the 2
+    // in 3 column blocks with such points do not wait on them (+8 us at C3 when they did)
+    const int J1 = g.jdx1(), J2 = g.jdx2(), I1 = g.idx1(), I2 = g.idx2();
+    const int W = J2 - J1 + 1, H = I2 - I1 + 1;
+    const int nb = 4 * W + 4 * (H > 4 ? H - 4 : 0);
+    const int q = (bb - ncol - nsp) * 512 + (int)threadIdx.x;
+    const int k = q / nb + 1, p = q % nb;
+    if (k > c->kz) return;
+    int jj, ii;
+    if (p < 4 * W) {
+      const int r = p / W;
+      ii = r < 2 ? I1 + r : I2 - (3 - r);
+      jj = J1 + p % W;
+    } else {
+      const int r = (p - 4 * W) % 4;
+      ii = I1 + 2 + (p - 4 * W) / 4;
+      jj = r < 2 ? J1 + r : J2 - (3 - r);
+    }
+    // a narrow box visits some points twice: the copies are idempotent
+    if (in(jj, J1, J2) && in(ii, I1, I2)) keep_point(g, f, jj, ii, k, 1, k);
+    return;
+  }
   if (bb >= ncol) {
     // surface pressures (and with qfuse the copy of p*) on the frame points outside the column
     // box, all ghost points
@@ -230,9 +255,6 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   const uint32_t o2 = valid ? g.o2(j, i) : 0u;
   const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
   if (valid && ty == 7) surface_pressures_at(g, f, j, i);
-  // qfuse: the points k_momentum / k_scalars / the moisture fix leave alone keep their values
-  // in the next buffers (k_qfilter's copies), one level group per wavefront
-  if (valid && f.qfuse) keep_point(g, f, j, i, ty + 1, 8, kz);
   PT_MARK();
   double rp = 0.0;
   if (ce) {
