@@ -1742,6 +1742,7 @@ __device__ __forceinline__ void split_correct_body(
   // them; 4 (line, chunk, level) items of 64 points per block
   const int kz = c->kz;
   const int zbdy = BDY ? (int)gridDim.z - nser - kz : 0;
+  PT_DECL
   if (BDY && (int)blockIdx.z < zbdy) {
     const int nchunk = bdy_chunks_d(g);
     const int item = (((int)blockIdx.z * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x) * 4 +
@@ -1750,6 +1751,7 @@ __device__ __forceinline__ void split_correct_body(
     const int line = item % 6, chunk = (item / 6) % nchunk, k = item / (6 * nchunk) + 1;
     const double xt = s->xbctime + ((s->lcount + 1 == 2) ? d_two * c->dtsec : s->dt);
     bdyval_point(g, xt, true, ba, line, chunk * 64 + (int)threadIdx.x, k, false);
+    PT_PRINT(6);
     return;
   }
   const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1864,6 +1866,7 @@ __device__ __forceinline__ void split_correct_body(
     else if (di0) { ST(a1u, o3, u1.x); ST(a1v, o3, v1.x); ST(a2u, o3, u2.x); ST(a2v, o3, v2.x); }
     else { ST(a1u, o3 + 8u, u1.y); ST(a1v, o3 + 8u, v1.y); ST(a2u, o3 + 8u, u2.y); ST(a2v, o3 + 8u, v2.y); }
   }
+  PT_PRINT(7);
   if (!BDY) return;
   const Slices& sl = ba.sl;
   const long slen = ba.slen;

@@ -20,7 +20,8 @@ from regcm_amd import icbc  # noqa: E402
 from regcm_amd.config import CONFIGS  # noqa: E402
 from regcm_amd.dycore import DynCore, lib  # noqa: E402
 
-NAMES = {1: "k_columns", 2: "k_momentum", 3: "k_scalars", 4: "k_qfilter", 5: "k_split_project"}
+NAMES = {1: "k_columns", 2: "k_momentum", 3: "k_scalars", 4: "k_qfilter", 5: "k_split_project",
+         6: "split_corr bdy", 7: "split_corr cor"}
 REC = np.dtype([("kid", "i4"), ("bx", "i4"), ("by", "i4"), ("bz", "i4"), ("n", "i4"), ("pad", "i4"),
                 ("t", "i8", (8,))])
 
