@@ -11,12 +11,16 @@ regcm_amd/csrc/kernels.hip with tendency diagnostics off:
   k_momentum    reads atm1 u,v,t,qv, atm2 u,v, qdot, xkc, phi (9) + u,v b0/bt in band (4 f_b);
                 writes next atm1/atm2 u,v (4); 2-D: msfd msfx-derived dmsf coriol rpsa rpsda rpsdb
                 psa psdota psdotb (9)
-  k_scalars     reads atm1 u,v,t,qv,qc, atm2 t,qv,qc, qdot, xkc (10) + t,q b0/bt in band (4 f_b);
-                writes next atm1/atm2 t, cqv, cqc (4); 2-D: 12
-  k_columns     reads atm1 u,v,t,qv,qc, atm2 u,v (7); writes qdot, phi, xkc (3); 2-D: 12
-  k_qfilter     reads cqv,cqc, atm1/atm2 qv,qc (6); writes next atm1/atm2 qv,qc (4); 2-D: 5
+  k_scalars     reads atm1 u,v,t,qv,qc, atm2 u,v (xkc), atm2 t,qv,qc, qdot (11) + t,q b0/bt in
+                band (4 f_b); writes next atm1/atm2 t, cqv, cqc and (qfuse, the RAW filter of
+                the non-negative forecasts) next atm1/atm2 qv, qc (8); 2-D: 12 + psc
+  k_columns     reads atm1 u,v,t,qv,qc (5); writes qdot, phi (2); 2-D: 12 + (qfuse) the
+                RA-filtered p* into the next buffers (2); the keep copies are O(perimeter)
+  k_qfilter     (RCMDYN_NO_QFUSE) reads cqv,cqc, atm1/atm2 qv,qc (6); writes next atm1/atm2
+                qv,qc (4); 2-D: 5
   k_split_project reads atm1/atm2 u,v,t (6); 2-D: 3 nsplit slots x 2 + 8
-  k_split_correct read-modify-write atm1/atm2 t,u,v (12); 2-D: 2 nsplit + 4
+  k_split_correct read-modify-write atm1/atm2 t,u,v (12); 2-D: 2 nsplit + 4 (the bdyval blocks of
+                k_split_correct_bdy move O(perimeter) more)
 """
 from __future__ import annotations
 
@@ -28,8 +32,8 @@ def band_fraction(jx: int, iy: int, nspgx: int) -> float:
 # (3-D fields, 3-D fields in the band only, 2-D fields)
 KERNEL_FIELDS = {
     "k_momentum": (13, 4, 9),
-    "k_scalars": (14, 4, 12),
-    "k_columns": (10, 0, 12),
+    "k_scalars": (19, 4, 13),
+    "k_columns": (7, 0, 14),
     "k_qfilter": (10, 0, 5),
     "k_split_project": (6, 0, 20),
     "k_split_correct": (12, 0, 8),
