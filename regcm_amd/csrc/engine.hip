@@ -1286,6 +1286,25 @@ struct rcmdyn_engine {
     DHIPCHK(hipStreamWaitEvent(stream, evjoin[slot], 0));
     join_pending[slot] = false;
   }
+  // The round-3 overlap form: every exchange stays on the engine's stream (RCCL calls are
+  // captured on the capture's origin stream only; the RCCL 2.26 that torch bundles crashed a
+  // captured step whose first exchange ran on the forked stream), and the kernels that read no
+  // point of it run on the second stream: side_begin forks the second stream from the engine's
+  // at this point and sends the following launches there, side_end records their completion
+  // (slot) and sends launches back, side_join makes the engine's stream wait for them.
+  void side_begin() {
+    if (ntiles == 1) return;
+    DHIPCHK(hipEventRecord(evfork, stream));
+    DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
+    std::swap(stream, stream2);
+  }
+  void side_end(int slot) {
+    if (ntiles == 1) return;
+    DHIPCHK(hipEventRecord(evjoin[slot], stream));
+    std::swap(stream, stream2);
+    join_pending[slot] = true;
+  }
+  void side_join(int slot) { xch_join(slot); }
 
   // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
   void xch_delh_slot(int l, int src) {
@@ -1535,12 +1554,8 @@ struct rcmdyn_engine {
       const Grids q = grids(g);
       KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
     });
-    if (ovl) {
-      fork_point();
-      xch_begin({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}}, 0);
-    } else {
-      xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
-    }
+    // ovl: the exchange is issued in TEND_POST, after k_nh_tend_c went to the second stream
+    if (!ovl) xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
     if (slice) run_slice();
     }
     if (!(phase & TEND_POST)) return;
@@ -1565,12 +1580,18 @@ struct rcmdyn_engine {
       }
     });
     if (ovl) {
+      // second stream: k_nh_tend_c, then (after the cr/qdot/xkcr exchange) k_nh_tend_d; the
+      // engine's stream: that exchange, then (after k_nh_tend_c) the cqv/cqc exchange
+      side_begin();
       each([&](Tile& t) { tend_c_launch(t, nhfields(t), istep); });
-      fork_point();
-      xch_begin({{FK::CQV, kz}, {FK::CQC, kz}}, 1);
-      xch_join(0);
+      side_end(0);
+      xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
+      side_begin();
       each([&](Tile& t) { tend_d_launch(t, nhfields(t), istep); });
-      xch_join(1);
+      side_end(1);
+      side_join(0);
+      xch({{FK::CQV, kz}, {FK::CQC, kz}});
+      side_join(1);
       tke_step();
     } else {
       tke_step();
@@ -1604,10 +1625,11 @@ struct rcmdyn_engine {
                 nhfields(t), istep, fin, first, part);
       };
       if (ntiles > 1 && !no_overlap) {
-        fork_point();
-        xch_begin({{FK::NCDT, kz}, {FK::NCPP, kz}}, 0);
+        side_begin();
         each([&](Tile& t) { sound_uv(t, 1); });
-        xch_join(0);
+        side_end(0);
+        xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
+        side_join(0);
         each([&](Tile& t) { sound_uv(t, 2); });
       } else {
         xch({{FK::NCDT, kz}, {FK::NCPP, kz}});
@@ -1746,13 +1768,14 @@ struct rcmdyn_engine {
       // step (k_momentum / k_scalars follow with no host work between), of k_momentum and
       // k_scalars; part 2 of each after the join
       pro.insert(pro.end(), pro2.begin(), pro2.end());
-      fork_point();
-      xch_begin(pro);
-      ghosts_stale = false;
+      side_begin();
       each([&](Tile& t) { if (t.nint) columns(t, 1, t.nint, false); });
       post_inner = with_post;
       if (with_post) each([&](Tile& t) { post_launch(t, 1); });
-      xch_join();
+      side_end(0);
+      xchv(pro);
+      ghosts_stale = false;
+      side_join(0);
       each([&](Tile& t) { columns(t, t.nint ? 2 : 0, t.nint ? t.nring : t.nred, true); });
     } else {
       fork_point();

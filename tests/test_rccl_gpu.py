@@ -126,3 +126,46 @@ def test_rccl_job_wide_cfl_stop(c1_data, monkeypatch):
     with pytest.raises(EngineError, match=r"CFL VIOLATION \(job, by step (8|16)\)"):
         e.step(100)
     assert e.get_time()[0] <= 24
+
+
+TORCH_FIRST = r"""
+import sys
+import numpy as np
+import torch  # noqa: F401  (loads torch's bundled librccl.so.1 / libamdhip64 before the engine)
+sys.path.insert(0, sys.argv[1])
+from regcm_amd.config import CONFIGS, STATE_FIELDS
+from regcm_amd import icbc
+from regcm_amd.dycore import DynCore, runtime_info
+print(runtime_info())
+rc = CONFIGS["C1"]
+data = icbc.generate(rc)
+engs = []
+for nproc in ((1, 1), (2, 2)):
+    e = DynCore(rc, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    e.put_state(data["state"])
+    e.bdyval()
+    e.step(6)
+    engs.append(e)
+for name in STATE_FIELDS:
+    assert np.array_equal(engs[0].get(name), engs[1].get(name)), name
+print("torch-first ok")
+"""
+
+
+def test_rccl_graph_under_torch_rccl(tmp_path):
+    """A process that imported torch before the engine binds torch's bundled RCCL (2.26, same
+    soname as /opt/rocm's 2.27; the pytest run that collects the CPU tests is one).  The
+    decomposed, overlapped, graph-captured step over RCCL self-communication must run and stay
+    bit-identical there too: every exchange is captured on the origin stream (side_begin in
+    engine.hip).  In a child process, so a crash fails this test instead of the run."""
+    import os
+    import subprocess
+    import sys
+    script = tmp_path / "torch_first.py"
+    script.write_text(TORCH_FIRST)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RCMDYN_FORCE_RCCL="1")
+    p = subprocess.run([sys.executable, str(script), root], capture_output=True, text=True, timeout=240, env=env)
+    print(p.stdout[-2000:], p.stderr[-2000:])
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])
+    assert "torch-first ok" in p.stdout
