@@ -59,7 +59,22 @@ def test_hydrostatic_plans_match(name, nranks):
     pl = plans(rc, data["split"], cj, ci, 3)
     msgs, ncoll = check_plans(pl, cj, ci)
     assert msgs > 0 and ncoll >= 1
-    # both channels carry traffic: the prologue's atm2 part travels on the second stream
+    # the overlapped schedule issues every exchange on the engine's stream (channel 0; the
+    # kernels that read no ghost point run on the second stream)
+    assert all((p[:, 2] == 0).all() for p in pl)
+
+
+@pytest.mark.parametrize("name,nranks", [("C3", 8), ("C1", 4)])
+def test_hydrostatic_plans_match_no_overlap(monkeypatch, name, nranks):
+    """RCMDYN_NO_OVERLAP=1 (round 2's schedule): the prologue's atm2 part travels on the second
+    stream (channel 1), ordered after the first stream's atm1/p* part on the shared
+    communicator; the plans still match rank to rank."""
+    monkeypatch.setenv("RCMDYN_NO_OVERLAP", "1")
+    rc = CONFIGS[name]
+    data = icbc.generate(rc)
+    cj, ci = set_nproc(nranks, rc.jx, rc.iy)
+    pl = plans(rc, data["split"], cj, ci, 3)
+    check_plans(pl, cj, ci)
     assert any((p[:, 2] == 1).any() for p in pl)
 
 
