@@ -1739,9 +1739,10 @@ struct rcmdyn_engine {
     // exchanges become exchanges of atm1 (width 1) and atm2 (idif = 2); p* travels 3 wide so
     // psdot and its reciprocals are formed on the ghost ring locally (no psdot exchanges).
     // atm1 travels 2 wide and atm2 3 wide: one more than the reference's widths, for the
-    // ghost rings the kernels below compute in place of the later exchanges
-    // The atm2 part travels on the second stream while k_surface_pressures and k_columns,
-    // which read only atm1 and p*, run (halo/compute overlap); joined before k_momentum.
+    // ghost rings the kernels below compute in place of the later exchanges.
+    // Halo/compute overlap (overlap()): the exchange on the engine's stream, part 1 of
+    // k_columns (and of k_momentum / k_scalars) on the second; RCMDYN_NO_OVERLAP: the atm2 part
+    // on the second stream beside k_columns, which reads only atm1 and p*.
     std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2},
                             {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}};
     std::vector<XField> pro2{{FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
