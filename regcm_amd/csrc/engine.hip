@@ -1854,10 +1854,10 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         dim3 gr((g.jcx2() - g.jcx1() + SPB) / SPB, (g.icx2() - g.icx1() + SPB) / SPB, ns);
         if (ntiles > 1)
-          KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
+          KLAUNCH(k_spstep_fused, gr, dim3(SPR, SPR), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
                   t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
         else
-          KLAUNCH(k_spstep_fused, gr, dim3(32, 16), 0, stream, g, g, dc, t.deld, t.delh, t.msfx, t.msfd,
+          KLAUNCH(k_spstep_fused, gr, dim3(SPR, SPR), 0, stream, g, g, dc, t.deld, t.delh, t.msfx, t.msfd,
                   t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
       });
     } else {

@@ -1590,12 +1590,15 @@ __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int
 // exact (halo values are recomputed redundantly and the contaminated rim never reaches it).
 // Per point the operations are those of k_spstep_grad/k_spstep_update, so results are
 // bit-identical to the two-kernel-per-substep path (Main/mod_split.F90:463-669).
-constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;
+// One thread per region point (SPR x SPR = 1024): each sub-step is then one pass of the
+// block with no per-thread loop over rows, the shortest chain of the m2 dependent sub-steps.
+// (8 x 8 owned blocks on small tiles, a 24 x 24 region, measured no faster: the chain's
+// latency is the sub-steps' barriers, not the region size.)
 // Inputs (deld/delh slots, msfx, msfd, psdota, mapf, psa) are addressed through frame w, which
 // for a tile of a decomposition is a wide frame whose ghost ring holds its neighbours' values
 // to depth SPH (one width-SPH exchange per step instead of three per sub-step); the masks use
 // global indices so ghost points evolve exactly as on their owning tile.  Outputs use frame g.
-__global__ __launch_bounds__(512) void k_spstep_fused(
+__global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
     Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
     const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota,
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
@@ -1606,7 +1609,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   // tile, the depth of the wide exchange.
   const int J1 = g.jcx1() + blockIdx.x * SPB, I1 = g.icx1() + blockIdx.y * SPB;
   const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
-  const int tx = threadIdx.x, ty = threadIdx.y;        // 32 x 16
+  const int tx = threadIdx.x, ty = threadIdx.y;        // R x R, one region point each
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
   const int m2 = (int)aam * 2;
   const double dtau2 = dtau * d_two, rdx2 = d_one / c->dx2;
@@ -1615,14 +1618,14 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   const double* H1 = WSLOT(delh, l, 1); const double* H2 = WSLOT(delh, l, 2); const double* H3 = WSLOT(delh, l, 3);
 #undef WSLOT
   const int gjx = g.gjx, giy = g.giy;
-  // per-thread points: (tx, ty + 16 r), r = 0..1; d3/m2, h3/m2 (forward step) and d3/aam,
-  // h3/aam (leapfrog) are loop-invariant and formed once
-  constexpr int NR = 2;
+  // the thread's region point (tx, ty); d3/m2, h3/m2 (forward step) and d3/aam, h3/aam
+  // (leapfrog) are loop-invariant and formed once
+  constexpr int NR = 1;
   double d3f[NR], h3f[NR], d3l[NR], h3l[NR], ps[NR], mf[NR], ufac[NR], msd[NR], sd[NR], sh[NR];
   bool ce[NR], ci[NR], bnd[NR], di[NR], own[NR];
   const double m2d = (double)m2;
   for (int r = 0; r < NR; r++) {
-    const int lj = tx, li = ty + 16 * r, j = jr0 + lj, i = ir0 + li;
+    const int lj = tx, li = ty + SPR * r, j = jr0 + lj, i = ir0 + li;
     // region points outside frame w (a partial last block) lie in the contaminated rim: they
     // are read as zero and never reach an output point
     const bool inw = in(j, w.j0, w.j0 + w.nj - 1) && in(i, w.i0, w.i0 + w.ni - 1);
@@ -1647,7 +1650,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
   }
   double pda[NR];
   for (int r = 0; r < NR; r++) {
-    const int j = jr0 + tx, i = ir0 + ty + 16 * r;
+    const int j = jr0 + tx, i = ir0 + ty + SPR * r;
     pda[r] = di[r] ? psdota[w.ix(j, i)] : 0.0;
   }
   __syncthreads();
@@ -1656,7 +1659,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
     const int src = (n == 1) ? n0 : n1;
     // gradient of delh(src) at dot points -> (uu, vv)
     for (int r = 0; r < NR; r++) {
-      const int lj = tx, li = ty + 16 * r;
+      const int lj = tx, li = ty + SPR * r;
       if (di[r] && lj >= 1 && li >= 1) {
         const double a = Hs[src][li][lj], b = Hs[src][li - 1][lj], cc = Hs[src][li][lj - 1], dd = Hs[src][li - 1][lj - 1];
         double w1 = (a + b - cc - dd) / ufac[r];
@@ -1670,7 +1673,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
     __syncthreads();
     const int nn = (n == 1) ? n1 : n0;                  // forward writes n1; leapfrog n2 = n0
     for (int r = 0; r < NR; r++) {
-      const int lj = tx, li = ty + 16 * r;
+      const int lj = tx, li = ty + SPR * r;
       if (ci[r] && lj + 1 < SPR && li + 1 < SPR) {
         const double w3 = rdx2 * mf[r] *
             (-U[li + 1][lj] + U[li + 1][lj + 1] - U[li][lj] + U[li][lj + 1] +
@@ -1700,7 +1703,7 @@ __global__ __launch_bounds__(512) void k_spstep_fused(
     else { /* forward step: n0 = 1, n1 = 2 stay; the leapfrog loop starts with n2 = n0 */ }
   }
   for (int r = 0; r < NR; r++) {
-    const int j = jr0 + tx, i = ir0 + ty + 16 * r;
+    const int j = jr0 + tx, i = ir0 + ty + SPR * r;
     if (own[r] && in(j, g.jdx1(), g.jdx2()) && in(i, g.idx1(), g.idx2())) {
       const long q = (long)(l - 1) * g.plane + g.ix(j, i);
       ddsum[q] = ce[r] ? sd[r] : d_zero;

@@ -16,6 +16,7 @@ constexpr int MAXSEG = 64;
 constexpr int NEGFIX_BLOCKS = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
+constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level)
