@@ -56,7 +56,8 @@ typedef struct rcmdyn_config {
   /* dynamics options (defaults in brackets) */
   int32_t idynamic;             /* [1] hydrostatic, 2 = non-hydrostatic (MM5-type, sound) */
   int32_t iboudy;               /* [5] exponential relaxation (1 = linear) */
-  int32_t idiffu;               /* [1] 4th-order diffusion */
+  int32_t idiffu;               /* [1] 1: 4th-order, 2: 9-point, 3: 6th-order flux-limited on each
+                                   tile's last interior column (Main/mod_diffusion.F90:412-942) */
   int32_t ipgf;                 /* [0] */
   int32_t nsplit;               /* [2] */
   int32_t nspgx, nspgd;         /* [12,12] boundary relaxation band width */

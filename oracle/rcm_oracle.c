@@ -41,6 +41,8 @@ static const double beta_hyd = 1.0 - 2.0 * 0.0; /* :320 */
 static const double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
 /* second-order (9-point) scheme of idiffu = 2, Main/mod_diffusion.F90:63-65 */
 static const double o4_c1 = 4.0 / 6.0, o4_c2 = 1.0 / 6.0, o4_c3 = -20.0 / 6.0;
+/* sixth-order flux-limited scheme of idiffu = 3, Main/mod_diffusion.F90:75-78 */
+static const double h4_c1 = 10.0, h4_c2 = -5.0, h4_c3 = 1.0, diff_6th_factor = 0.12;
 
 /* reference-atmosphere constants of the ipgf = 1 pressure gradient, Share/mod_constants.F90:359-362 */
 static const double T00PG = 287.0, P00PG = 101.325, ALAM = 6.5e-3;
@@ -271,8 +273,10 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   o->jde1ga = o->jde1 - gl; o->jde2ga = o->jde2 + gr; o->ide1ga = o->ide1 - gbm; o->ide2ga = o->ide2 + gt;
   o->jce1ga = o->jce1 - gl; o->jce2ga = o->jce2 + gr; o->ice1ga = o->ice1 - gbm; o->ice2ga = o->ice2 + gt;
   o->jci1ga = o->jci1 - gl; o->jci2ga = o->jci2 + gr; o->ici1ga = o->ici1 - gbm; o->ici2ga = o->ici2 + gt;
-  o->jde1gb = o->jde1 - 2 * gl; o->jde2gb = o->jde2 + 2 * gr; o->ide1gb = o->ide1 - 2 * gbm; o->ide2gb = o->ide2 + 2 * gt;
-  o->jce1gb = o->jce1 - 2 * gl; o->jce2gb = o->jce2 + 2 * gr; o->ice1gb = o->ice1 - 2 * gbm; o->ice2gb = o->ice2 + 2 * gt;
+  /* the slice frames: gb (2 deep), gc (3 deep) with idiffu = 3 (Main/mod_atm_interface.F90:1001-1028) */
+  const int gs = cfg->idiffu == 3 ? 3 : 2;
+  o->jde1gb = o->jde1 - gs * gl; o->jde2gb = o->jde2 + gs * gr; o->ide1gb = o->ide1 - gs * gbm; o->ide2gb = o->ide2 + gs * gt;
+  o->jce1gb = o->jce1 - gs * gl; o->jce2gb = o->jce2 + gs * gr; o->ice1gb = o->ice1 - gs * gbm; o->ice2gb = o->ice2 + gs * gt;
   o->j0 = o->jde1 - GO; o->i0 = o->ide1 - GO;
   o->nj = (o->jde2 - o->jde1 + 1) + 2 * GO; o->ni = (o->ide2 - o->ide1 + 1) + 2 * GO;
   o->plane = (size_t)o->nj * (size_t)o->ni;
@@ -405,8 +409,8 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
     o->a1tke = alloc3(o, kp); o->a2tke = alloc3(o, kp); o->ctke = alloc3(o, kp);
     o->tkedyn = alloc3(o, kp); o->tkeps = alloc3(o, kp); o->tkephy = alloc3(o, kp);
     o->kpbl = alloc3(o, 1);
-    if (!o->nh) o->xkcf = alloc3(o, kp);
   }
+  if (!o->nh && (cfg->ibltyp == 2 || cfg->idiffu == 3)) o->xkcf = alloc3(o, kp);
   if (o->nh) { o->phy[5] = alloc3(o, kz); o->phy[6] = alloc3(o, kp); }
   for (int q = 0; q < 22; q++) o->atms[q] = alloc3(o, atms_levels(q, kz));
   for (int q = 0; q < 4; q++) { o->bin[q] = alloc3(o, kz); o->bb1[q] = alloc3(o, kz); }
@@ -454,7 +458,7 @@ void orc_destroy(orc_t* o) {
   for (int q = 0; q < 7; q++) free(o->phy[q]);
   free(o->a1tke); free(o->a2tke); free(o->ctke); free(o->tkedyn); free(o->tkeps); free(o->tkephy);
   free(o->kpbl);
-  /* xkcf (also allocated for the hydrostatic core with ibltyp = 2) is in the list above */
+  /* xkcf (also allocated for the hydrostatic core with ibltyp = 2 or idiffu = 3) is in the list above */
   for (int q = 0; q < 22; q++) free(o->atms[q]);
   for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
   free(o->psdot0);
@@ -675,6 +679,65 @@ static void psc2psd(orc_t* o, const double* pc, double* pd) {
   if (o->bt && o->br) A2(pd, o->jde2, o->ide2) = A2(pc, o->jce2, o->ice2);
 }
 
+/* the exchange width idif of the diffused fields (Main/mod_params.F90:1965-1977): 2 for
+ * idiffu = 1, 3 for idiffu = 3; idiffu = 2 (idif = 1) keeps 2, a superset */
+static int idw(const orc_t* o) { return o->cfg.idiffu == 3 ? 3 : 2; }
+
+/* calc_coeff idiffu = 3 (Main/mod_diffusion.F90:174-183): diff_6th_coef * p*b on every level
+ * (xkcf on kz + 1 of them), diff_6th_coef * p*dotb on the dot points; no exchange */
+static void calc_coeff6(orc_t* o) {
+  int kz = o->kz;
+  const double coef = diff_6th_factor * 0.015625 / (2.0 * o->dtsec);   /* :154 */
+  memset(o->xkc, 0, sizeof(double) * o->plane * kz);
+  memset(o->xkd, 0, sizeof(double) * o->plane * kz);
+  memset(o->xkcf, 0, sizeof(double) * o->plane * (kz + 1));
+  for (int k = 1; k <= kz + 1; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      for (int j = o->jci1; j <= o->jci2; j++) {
+        if (k <= kz) A3(o->xkc, j, i, k) = coef * A2(o->psb, j, i);
+        A3(o->xkcf, j, i, k) = coef * A2(o->psb, j, i);
+      }
+  for (int k = 1; k <= kz; k++)
+    for (int i = o->idi1; i <= o->idi2; i++)
+      for (int j = o->jdi1; j <= o->jdi2; j++) A3(o->xkd, j, i, k) = coef * A2(o->psdotb, j, i);
+}
+
+/* the bracket ((fx_p1 - fx_p0) + (fy_p1 - fy_p0)) of the idiffu = 3 scheme at (j, i, k),
+ * Main/mod_diffusion.F90:428-470 (dot, f / msfd in the fluxes and the limiter) and 618-648
+ * (cross, f in the fluxes, f / msfd in the limiter); neighbours clamped to 1..jmax, 1..imax */
+static double diffu6_bracket(orc_t* o, const double* f, int j, int i, int k, int jmax, int imax, int dot) {
+  const double* m = o->msfd;
+  const int jm1 = j - 1 < 1 ? 1 : j - 1, jm2 = j - 2 < 1 ? 1 : j - 2, jm3 = j - 3 < 1 ? 1 : j - 3;
+  const int jp1 = j + 1 > jmax ? jmax : j + 1, jp2 = j + 2 > jmax ? jmax : j + 2, jp3 = j + 3 > jmax ? jmax : j + 3;
+  const int im1 = i - 1 < 1 ? 1 : i - 1, im2 = i - 2 < 1 ? 1 : i - 2, im3 = i - 3 < 1 ? 1 : i - 3;
+  const int ip1 = i + 1 > imax ? imax : i + 1, ip2 = i + 2 > imax ? imax : i + 2, ip3 = i + 3 > imax ? imax : i + 3;
+#define FV(J, I) (dot ? A3(f, J, I, k) / A2(m, J, I) : A3(f, J, I, k))
+#define LV(J, I) (A3(f, J, I, k) / A2(m, J, I))
+  double x0 = h4_c1 * (FV(j, i) - FV(jm1, i)) + h4_c2 * (FV(jp1, i) - FV(jm2, i)) + h4_c3 * (FV(jp2, i) - FV(jm3, i));
+  if (x0 * (LV(j, i) - LV(jm1, i)) <= d_zero) x0 = d_zero;
+  double x1 = h4_c1 * (FV(jp1, i) - FV(j, i)) + h4_c2 * (FV(jp2, i) - FV(jm1, i)) + h4_c3 * (FV(jp3, i) - FV(jm2, i));
+  if (x1 * (LV(jp1, i) - LV(j, i)) <= d_zero) x1 = d_zero;
+  double y0 = h4_c1 * (FV(j, i) - FV(j, im1)) + h4_c2 * (FV(j, ip1) - FV(j, im2)) + h4_c3 * (FV(j, ip2) - FV(j, im3));
+  if (y0 * (LV(j, i) - LV(j, im1)) <= d_zero) y0 = d_zero;
+  double y1 = h4_c1 * (FV(j, ip1) - FV(j, i)) + h4_c2 * (FV(j, ip2) - FV(j, im1)) + h4_c3 * (FV(j, ip3) - FV(j, im2));
+  if (y1 * (LV(j, ip1) - LV(j, i)) <= d_zero) y1 = d_zero;
+#undef FV
+#undef LV
+  return (x1 - x0) + (y1 - y0);
+}
+
+/* diffu_x3d / diffu_x4d3d / diffu_x3df idiffu = 3 (Main/mod_diffusion.F90:602-651, 736-785,
+ * 893-942): the tile's column j = jci2 only, levels 1..nk; fac multiplies the coefficient
+ * (x3df; 1 for the other two).  x3df reads xkc on kz + 1 levels, one past its allocation; the
+ * coefficient is diff_6th_coef * p*b on every level, which xkcf holds. */
+static void diffu_x6(orc_t* o, double* ften, const double* f, int nk, double fac) {
+  const int j = o->jci2;
+  for (int k = 1; k <= nk; k++)
+    for (int i = o->ici1; i <= o->ici2; i++)
+      A3(ften, j, i, k) = A3(ften, j, i, k) + fac * A3(o->xkcf, j, i, k) *
+          diffu6_bracket(o, f, j, i, k, o->jx - 1, o->iy - 1, 0);
+}
+
 /* surface_pressures, Main/mod_tendency.F90:815-834 */
 static void surface_pressures(orc_t* o) {
   xch(o, o->psa, 1, 1, 0);
@@ -682,11 +745,11 @@ static void surface_pressures(orc_t* o) {
     for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->rpsa, j, i) = d_one / A2(o->psa, j, i);
   psc2psd(o, o->psa, o->psdota);
   xch(o, o->psdota, 1, 1, 0);
-  xch(o, o->psb, 1, 2, 0);
+  xch(o, o->psb, 1, idw(o), 0);
   for (int i = o->ice1; i <= o->ice2; i++)
     for (int j = o->jce1; j <= o->jce2; j++) A2(o->rpsb, j, i) = d_one / A2(o->psb, j, i);
   psc2psd(o, o->psb, o->psdotb);
-  xch(o, o->psdotb, 1, 2, 0);
+  xch(o, o->psdotb, 1, idw(o), 0);
 }
 
 /* decouple, Main/mod_tendency.F90:852-1116 (hydrostatic branches) */
@@ -801,12 +864,12 @@ static void decouple(orc_t* o) {
         A3(o->xtv, j, i, k) = A3(o->xt, j, i, k) * (d_one + c_ep1 * A3(o->xq[0], j, i, k));
       }
   /* atm1%pr/rho (:1037-1040) and atm2%pr (:1094-1096) feed only physics: skipped */
-  xch(o, o->a2u, kz, 2, 0); xch(o, o->a2v, kz, 2, 0); xch(o, o->a2t, kz, 2, 0);
+  xch(o, o->a2u, kz, idw(o), 0); xch(o, o->a2v, kz, idw(o), 0); xch(o, o->a2t, kz, idw(o), 0);
   if (o->cfg.ibltyp == 2) {                                      /* :871, 1079 */
-    xch(o, o->a1tke, kz + 1, 1, 0); xch(o, o->a2tke, kz + 1, 2, 0);
+    xch(o, o->a1tke, kz + 1, 1, 0); xch(o, o->a2tke, kz + 1, idw(o), 0);
   }
   {                                                              /* :1073-1077 */
-    int w = o->cfg.isladvec == 1 ? 4 : 2;                         /* max(idif, 4) */
+    int w = o->cfg.isladvec == 1 ? 4 : idw(o);                    /* max(idif, 4) */
     xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
   }
 }
@@ -1051,6 +1114,7 @@ forecast:
 
 /* calc_coeff, Main/mod_diffusion.F90:169-251 (idiffu = 1, idynamic = 1) */
 static void calc_coeff(orc_t* o) {
+  if (o->cfg.idiffu == 3) { calc_coeff6(o); return; }
   int kz = o->kz;
   memset(o->xkc, 0, sizeof(double) * o->plane * kz);
   memset(o->xkd, 0, sizeof(double) * o->plane * kz);
@@ -1525,6 +1589,7 @@ static void boundary(orc_t* o) {
 
 /* diffusion, Main/mod_tendency.F90:1515-1526 -> diffu_d, diffu_x3d, diffu_x4d */
 static void diffu_x(orc_t* o, double* ften, const double* f, double fac) {
+  if (o->cfg.idiffu == 3) { diffu_x6(o, ften, f, o->kz, d_one); return; }
   if (o->cfg.idiffu == 2) {
     /* diffu_x3d / diffu_x4d3d idiffu = 2, Main/mod_diffusion.F90:726-735, 881-891 */
     for (int k = 1; k <= o->kz; k++)
@@ -1558,6 +1623,17 @@ static void diffu_x(orc_t* o, double* ften, const double* f, double fac) {
 
 static void diffu_d(orc_t* o) {                                    /* :281-385 */
   const double* m = o->msfd;
+  if (o->cfg.idiffu == 3) {                                        /* :412-516, j = jdi2 */
+    const int j = o->jdi2;
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->idi1; i <= o->idi2; i++) {
+        A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A3(o->xkd, j, i, k) *
+            diffu6_bracket(o, o->ubd, j, i, k, o->jx, o->iy, 1);
+        A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) + A3(o->xkd, j, i, k) *
+            diffu6_bracket(o, o->vbd, j, i, k, o->jx, o->iy, 1);
+      }
+    return;
+  }
 #define UM(a, J, I) (A3(a, J, I, k) / A2(m, J, I))
   if (o->cfg.idiffu == 2) {                                        /* :386-411 */
     for (int k = 1; k <= o->kz; k++)
@@ -1909,7 +1985,7 @@ static void nh_surface_pressures(orc_t* o) {
   psc2psd(o, o->psa, o->psdota);
   xch(o, o->psdota, 1, 1, 0);
   psc2psd(o, o->psb, o->psdotb);
-  xch(o, o->psdotb, 1, 2, 0);
+  xch(o, o->psdotb, 1, idw(o), 0);
   for (int i = o->ice1ga; i <= o->ice2ga; i++)
     for (int j = o->jce1ga; j <= o->jce2ga; j++) A2(o->rpsa, j, i) = d_one / A2(o->psa, j, i);
   for (int i = o->ice1; i <= o->ice2; i++)
@@ -1948,7 +2024,7 @@ static void nh_decouple(orc_t* o) {
       for (int j = o->jci1; j <= o->jci2; j++)
         A3(o->xpr, j, i, k) = (A3(o->xtv, j, i, k) - A3(o->t0, j, i, k) -
                                A3(o->xpp, j, i, k) / (c_cpd * A3(o->rho0, j, i, k))) / A3(o->xt, j, i, k);
-  xch(o, o->a2pp, kz, 2, 0); xch(o, o->a2w, kp, 2, 0);
+  xch(o, o->a2pp, kz, idw(o), 0); xch(o, o->a2w, kp, idw(o), 0);
 }
 
 /* compute_omega NH (:1157-1192, :1216-1223) */
@@ -2019,6 +2095,7 @@ static void nh_mkslice(orc_t* o) {
 
 /* calc_coeff NH (Main/mod_diffusion.F90:215-250) */
 static void nh_calc_coeff(orc_t* o) {
+  if (o->cfg.idiffu == 3) { calc_coeff6(o); return; }
   int kz = o->kz, kp = kz + 1;
   memset(o->xkc, 0, sizeof(double) * o->plane * kz);
   memset(o->xkd, 0, sizeof(double) * o->plane * kz);
@@ -2273,6 +2350,7 @@ static void nh_sponge3d(orc_t* o, const double* bt, double* ften, int nk) {
 
 /* diffu_x3d / diffu_x3df on nk levels with coefficient xk (Main/mod_diffusion.F90:523-790) */
 static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* xk, int nk, double fac) {
+  if (o->cfg.idiffu == 3) { diffu_x6(o, ften, f, nk, fac); return; }
   if (o->cfg.idiffu == 2) {
     for (int k = 1; k <= nk; k++)
       for (int i = o->ici1; i <= o->ici2; i++)

@@ -22,6 +22,7 @@ static constexpr double d_half = 0.5, d_rfour = 0.25, d_1000 = 1000.0;
 static constexpr double MINQQ = 1.0e-8, DLOWVAL = 1.0e-20;
 static constexpr double z4_c1 = 1.0, z4_c2 = -4.0, z4_c3 = 12.0;
 static constexpr double o4_c1 = 4.0 / 6.0, o4_c2 = 1.0 / 6.0, o4_c3 = -20.0 / 6.0;  // idiffu = 2
+static constexpr double h4_c1 = 10.0, h4_c2 = -5.0, h4_c3 = 1.0;                   // idiffu = 3
 static constexpr double T00PG = 287.0, P00PG = 101.325;   // ipgf = 1, Share/mod_constants.F90:359-360
 
 __device__ __forceinline__ double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }

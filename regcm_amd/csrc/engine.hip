@@ -216,7 +216,9 @@ enum class FK {
   // semi-Lagrangian moisture tendency starts
   SLQV, SLQC,
   // UW PBL TKE (ibltyp = 2)
-  A1TKE, A2TKE
+  A1TKE, A2TKE,
+  // idiffu = 3 column terms
+  D6U, D6V, D6T, D6QV, D6QC
 };
 
 struct rcmdyn_engine {
@@ -289,7 +291,8 @@ struct rcmdyn_engine {
     const char* v = std::getenv("RCMDYN_NO_OVERLAP");
     return v && *v && std::strcmp(v, "0") != 0;
   }();
-  bool overlap() const { return ntiles > 1 && cfg.idynamic != 2 && !no_overlap; }
+  // (idiffu = 3: the column terms are formed after the whole exchange, so no overlap)
+  bool overlap() const { return ntiles > 1 && cfg.idynamic != 2 && cfg.idiffu != 3 && !no_overlap; }
   bool post_inner = false;    // tend_pre ran part 1 of k_momentum / k_scalars
   std::string err;
   std::unique_ptr<Comm> comm;
@@ -346,6 +349,7 @@ struct rcmdyn_engine {
     c.ul = cfg.uoffc * 0.5 * cfg.dtsec / c.dx;                       // :106 (init dt)
     c.xkhmax = c.dxsq / (64.0 * cfg.dtsec);                          // Main/mod_diffusion.F90:104
     c.dydc = cfg.adyndif * VONKAR * VONKAR * c.dx * 0.25;
+    c.diff6 = 0.12 * 0.015625 / (2.0 * cfg.dtsec);                    // Main/mod_diffusion.F90:78, 154
     c.xkhz = cfg.ckh * 1.5e-3 * c.dxsq / cfg.dtsec;
     const double fnudge = (cfg.bdy_nm > 0) ? cfg.bdy_nm : 0.1 / cfg.dtsec;   // Main/mod_bdycod.F90:204-215
     const double gnudge = (cfg.bdy_dm > 0) ? cfg.bdy_dm : 1.0 / (cfg.dtsec * 50.0);
@@ -446,6 +450,7 @@ struct rcmdyn_engine {
     t.qdot = dalloc(t, P * (kz + 1));
     t.phi = dalloc(t, P3);
     if (cfg.isladvec == 1) { t.slqv = dalloc(t, P3); t.slqc = dalloc(t, P3); }
+    if (cfg.idiffu == 3) for (double*& d : t.d6) d = dalloc(t, P3);
     if (cfg.ibltyp == 2) {
       t.a1tke = dalloc(t, P * (kz + 1)); t.a2tke = dalloc(t, P * (kz + 1)); t.ctke = dalloc(t, P * (kz + 1));
       t.kpbl = dalloc(t, P);
@@ -594,7 +599,9 @@ struct rcmdyn_engine {
       if (!(cfg.nh_dtsmax > 0.0) || !(cfg.nh_xmsf > 0.0))
         throw std::runtime_error("rcmdyn: nh_dtsmax / nh_xmsf (init_sound) must be set for idynamic=2");
     }
-    if (cfg.idiffu != 1 && cfg.idiffu != 2) throw std::runtime_error("rcmdyn: idiffu must be 1 or 2");
+    if (cfg.idiffu < 1 || cfg.idiffu > 3) throw std::runtime_error("rcmdyn: idiffu must be 1, 2 or 3");
+    if (cfg.idiffu == 3 && (cfg.idynamic != 1 || cfg.ibltyp == 2))
+      throw std::runtime_error("rcmdyn: idiffu = 3 is built for the hydrostatic core without UW TKE");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
@@ -820,6 +827,8 @@ struct rcmdyn_engine {
       case FK::WWB1: return t.bb1[6];
       case FK::SLQV: return t.slqv; case FK::SLQC: return t.slqc;
       case FK::A1TKE: return t.a1tke; case FK::A2TKE: return t.a2tke;
+      case FK::D6U: return t.d6[0]; case FK::D6V: return t.d6[1]; case FK::D6T: return t.d6[2];
+      case FK::D6QV: return t.d6[3]; case FK::D6QC: return t.d6[4];
       default: break;
     }
     const NHFields& h = nhf[&t - tiles.data()];
@@ -1473,6 +1482,7 @@ struct rcmdyn_engine {
     f.rpsa = t.rpsa; f.rpsb = t.rpsb; f.rpsda = t.rpsda; f.rpsdb = t.rpsdb; f.psc = t.psc;
     f.psdota = t.psdota; f.psdotb = t.psdotb; f.pten = t.pten; f.ptenn = t.pten + t.g.plane;
     f.qdot = t.qdot; f.phi = t.phi; f.slqv = t.slqv; f.slqc = t.slqc; f.cqv = t.cqv; f.cqc = t.cqc; f.fqv = t.fqv; f.fqc = t.fqc;
+    f.d6u = t.d6[0]; f.d6v = t.d6[1]; f.d6t = t.d6[2]; f.d6qv = t.d6[3]; f.d6qc = t.d6[4];
     f.depplane = t.depplane;
     if (diag) {
       f.tten = t.tten; f.uten = t.uten; f.vten = t.vten; f.qvten = t.qvten; f.qcten = t.qcten;
@@ -1743,8 +1753,9 @@ struct rcmdyn_engine {
     // Halo/compute overlap (overlap()): the exchange on the engine's stream, part 1 of
     // k_columns (and of k_momentum / k_scalars) on the second; RCMDYN_NO_OVERLAP: the atm2 part
     // on the second stream beside k_columns, which reads only atm1 and p*.
-    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2}, {FK::A1T, kz, 2},
-                            {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}};
+    // (idiffu = 3: p*b 4 wide, for p*dotb on k_diffu6's 3-deep dot ghost rings)
+    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, cfg.idiffu == 3 ? 4 : 3}, {FK::A1U, kz, 2}, {FK::A1V, kz, 2},
+                            {FK::A1T, kz, 2}, {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}};
     std::vector<XField> pro2{{FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
                              {FK::A2QC, kz, 3}};
     // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
@@ -1787,7 +1798,19 @@ struct rcmdyn_engine {
       each([&](Tile& t) { columns(t, 0, t.nred, true); });
       xch_join();
     }
+    if (cfg.idiffu == 3) diffu6();
     if (slice) run_slice();
+  }
+
+  // idiffu = 3: the column terms of every tile, then (decomposed) one width-1 exchange so the
+  // ring k_momentum / k_scalars compute holds the left neighbour's column as it computes it
+  void diffu6() {
+    const int kz = cfg.kz;
+    each([&](Tile& t) {
+      const Geom& g = t.g;
+      KLAUNCH(k_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kz, 4), dim3(64), 0, stream, g, dc, fields(t));
+    });
+    if (ntiles > 1) xch({{FK::D6U, kz}, {FK::D6V, kz}, {FK::D6T, kz}, {FK::D6QV, kz}, {FK::D6QC, kz}});
   }
 
   // k_momentum and k_scalars of one tile: part 1 the blocks in R (when it has any), part 2 the

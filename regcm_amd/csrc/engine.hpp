@@ -86,6 +86,7 @@ struct Consts {
   double nuk, tkemin;
   double pgfaa1;                       // ipgf = 1 reference-atmosphere exponent alam*rgas*regrav
   double dx, dx2, dx4, dx8, dx16, dxsq, rdxsq, ptop, ul, xkhmax, dydc, xkhz;
+  double diff6;                     // idiffu = 3: diff_6th_coef (Main/mod_diffusion.F90:154)
   double gnu1, gnu2, dtsec, t_extrema, q_rel_extrema;
   double rgas, cpd, c287, ep1, regrav, rovcp;
   double sigma[MAXKZ + 2], hsigma[MAXKZ + 1], dsigma[MAXKZ + 1];
@@ -146,6 +147,9 @@ struct Tile {
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten;
   double *qdot, *phi;
   double *slqv = nullptr, *slqc = nullptr;   // isladvec = 1: k_sladv output
+  // idiffu = 3: the sixth-order terms of the tile's j = jdi2 / jci2 column (k_diffu6), frame
+  // planes so one width-1 exchange hands the left neighbour's column to the ring: u, v, t, qv, qc
+  double* d6[5] = {};
   // ibltyp = 2: atm1/atm2 tke (decoupled, kz+1 levels), the forecast atmc%tke, and the UW
   // scheme's tendency (allocated on its first put)
   double *a1tke = nullptr, *a2tke = nullptr, *ctke = nullptr, *tkephy = nullptr;

@@ -781,7 +781,12 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
 #undef FGV
   }
   // diffu_d (idiffu = 1); xkd from calc_coeff (Main/mod_diffusion.F90:237-248)
-  {
+  if (c->idiffu == 3) {                     // the column term of k_diffu6
+    if (j == g.jdi2 || (!g.bl && j == g.jde1 - 1)) {
+      ut = ut + LD(f.d6u, o3);
+      vt = vt + LD(f.d6v, o3);
+    }
+  } else {
     double xkd = d_rfour * (sXK[a0][b0] + sXK[a0 - 1][b0 - 1] + sXK[a0 - 1][b0] + sXK[a0][b0 - 1]);
     xkd = xkd * c->rdxsq * pdotb;
 #define UM(S, dj, di) S[a2 + (di)][b2 + (dj)]
@@ -896,10 +901,70 @@ __device__ __forceinline__ double hadv_flux(const Consts* c, double xm, double p
   return fg;
 }
 
+// idiffu = 3, the sixth-order flux-limited scheme (Main/mod_diffusion.F90:412-516 diffu_d,
+// 736-785 diffu_x3d, 893-942 diffu_x4d3d).  The reference applies it on one column of each
+// tile, j = jdi2 (dot) / jci2 (cross), every row of the interior, with neighbour indices
+// clamped to the global domain (1..jx, 1..iy on dot points; 1..jx-1, 1..iy-1 on cross points).
+// fv gives the field in the fluxes, lv the field over msfd in the limiter.
+template <class FV, class LV>
+__device__ __forceinline__ double diffu6_bracket(int j, int i, int jmax, int imax, FV fv, LV lv) {
+  const int jm1 = max(j - 1, 1), jm2 = max(j - 2, 1), jm3 = max(j - 3, 1);
+  const int jp1 = min(j + 1, jmax), jp2 = min(j + 2, jmax), jp3 = min(j + 3, jmax);
+  const int im1 = max(i - 1, 1), im2 = max(i - 2, 1), im3 = max(i - 3, 1);
+  const int ip1 = min(i + 1, imax), ip2 = min(i + 2, imax), ip3 = min(i + 3, imax);
+  double x0 = h4_c1 * (fv(j, i) - fv(jm1, i)) + h4_c2 * (fv(jp1, i) - fv(jm2, i)) + h4_c3 * (fv(jp2, i) - fv(jm3, i));
+  if (x0 * (lv(j, i) - lv(jm1, i)) <= d_zero) x0 = d_zero;
+  double x1 = h4_c1 * (fv(jp1, i) - fv(j, i)) + h4_c2 * (fv(jp2, i) - fv(jm1, i)) + h4_c3 * (fv(jp3, i) - fv(jm2, i));
+  if (x1 * (lv(jp1, i) - lv(j, i)) <= d_zero) x1 = d_zero;
+  double y0 = h4_c1 * (fv(j, i) - fv(j, im1)) + h4_c2 * (fv(j, ip1) - fv(j, im2)) + h4_c3 * (fv(j, ip2) - fv(j, im3));
+  if (y0 * (lv(j, i) - lv(j, im1)) <= d_zero) y0 = d_zero;
+  double y1 = h4_c1 * (fv(j, ip1) - fv(j, i)) + h4_c2 * (fv(j, ip2) - fv(j, im1)) + h4_c3 * (fv(j, ip3) - fv(j, im2));
+  if (y1 * (lv(j, ip1) - lv(j, i)) <= d_zero) y1 = d_zero;
+  return (x1 - x0) + (y1 - y0);
+}
+
+// The column terms, once per tend (blockIdx.z: 0 u and v, 1 t, 2 qv, 3 qc; blockIdx.y = level):
+// the coefficient (calc_coeff, :174-183: diff_6th_coef * p*dotb on dot points, * p*b on cross
+// points) times the bracket, from the decoupled atm2 fields mkslice forms (ubd3d = u * 1/p*dotb,
+// tb3d = t * 1/p*b, qxb3d clamped; Main/mod_slice.F90:163-183) on the 3-deep ghost rings the
+// exchange of width idif = 3 fills.  k_momentum / k_scalars add them at the column's points in
+// the reference's place of the diffusion term.
+__global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f) {
+  const int i = g.ide1 + (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
+  const int q = (int)blockIdx.z;
+  const double* ps = f.psb;
+  if (q == 0) {
+    const int j = g.jdi2;
+    if (!in(i, g.idi1, g.idi2)) return;
+    auto rd = [&](int jj, int ii) { return d_one / psc2psd_global(g, ps, jj, ii); };
+    auto uu = [&](int jj, int ii) { return F3(f.a2u, jj, ii, k) * rd(jj, ii) / F2(f.msfd, jj, ii); };
+    auto vv = [&](int jj, int ii) { return F3(f.a2v, jj, ii, k) * rd(jj, ii) / F2(f.msfd, jj, ii); };
+    const double xkd = c->diff6 * psc2psd_global(g, ps, j, i);
+    F3(f.d6u, j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, uu, uu);
+    F3(f.d6v, j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, vv, vv);
+    return;
+  }
+  const int j = g.jci2;
+  if (!in(i, g.ici1, g.ici2)) return;
+  const double* a = q == 1 ? f.a2t : (q == 2 ? f.a2qv : f.a2qc);
+  const double lo = q == 2 ? MINQQ : d_zero;
+  auto fv = [&](int jj, int ii) {
+    const double v = F3(a, jj, ii, k) * (d_one / F2(ps, jj, ii));
+    return q == 1 ? v : dmax(v, lo);
+  };
+  auto lv = [&](int jj, int ii) { return fv(jj, ii) / F2(f.msfd, jj, ii); };
+  const double xkc = d_one * (c->diff6 * F2(ps, j, i));
+  F3(q == 1 ? f.d6t : (q == 2 ? f.d6qv : f.d6qc), j, i, k) = xkc * diffu6_bracket(j, i, g.gjx - 1, g.giy - 1, fv, lv);
+}
+
 // diffu_x (idiffu = 1) at one point from a halo-2 LDS tile, Main/mod_diffusion.F90:673-713
 #define H2T(S, dj, di) S[a2 + (di)][b2 + (dj)]
-#define DIFFU_X(ften, S)                                                                          \
+#define DIFFU_X(ften, S, D6)                                                                      \
   do {                                                                                            \
+    if (c->idiffu == 3) {                   /* the column term of k_diffu6 */                     \
+      if (j == g.jci2 || (!g.bl && j == g.jce1 - 1)) ften = ften + LD(D6, o3);                    \
+      break;                                                                                      \
+    }                                                                                             \
     if (c->idiffu == 2) {                   /* 9-point scheme, :726-735, 881-891 */               \
       ften = ften + d_one * xkcs *                                                                \
           (o4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + H2T(S, 0, 1) + H2T(S, 0, -1)) +                \
@@ -1130,7 +1195,7 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
       td = relax(td, xf, xg, FGT(0, 0), FGT(-1, 0), FGT(1, 0), FGT(0, -1), FGT(0, 1));
 #undef FGT
     }
-    DIFFU_X(td, sTB);
+    DIFFU_X(td, sTB, f.d6t);
     // tten + tdyn + tphy (:285-288), then the SUBEX condensation term (:332-341, stubbed)
     // (pc_physic of the coupling seam, loaded here to keep registers free: absent = 0)
     const double tt = ((spt + td) + (f.tphy ? LD(f.tphy, o3) : d_zero)) + d_zero;
@@ -1172,7 +1237,7 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
 #undef FGQ
     tq = tq + rfac * (xf * f0 - xg * (f1 + f2 + f3 + f4 - d_four * f0));
   }
-  DIFFU_X(tq, sQVB);
+  DIFFU_X(tq, sQVB, f.d6qv);
   // the qv sums and forecast (and with qfuse its RAW filter) before the qc chain, so the qv
   // operands are dead while it runs
   tq = ((spq + tq) + (f.qvphy ? LD(f.qvphy, o3) : d_zero)) + d_zero;
@@ -1211,7 +1276,7 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
       tc = tc - fl * c->xds[k];
     }
   }
-  DIFFU_X(tc, sQCB);
+  DIFFU_X(tc, sQCB, f.d6qc);
 #undef DT
 #undef H1T
   tc = ((d_zero + tc) + (f.qcphy ? LD(f.qcphy, o3) : d_zero)) + d_zero;

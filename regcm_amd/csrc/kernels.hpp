@@ -57,6 +57,7 @@ struct Fields {
   double *rpsa, *rpsb, *rpsda, *rpsdb, *psc, *psdota, *psdotb, *pten, *ptenn;
   double *qdot, *phi, *cqv, *cqc, *fqv, *fqc;
   double *slqv, *slqc;         // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv)
+  double *d6u, *d6v, *d6t, *d6qv, *d6qc;   // idiffu = 3 column terms (k_diffu6)
   int* depplane;
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
@@ -96,6 +97,7 @@ __global__ void k_surface_pressures(Geom g, Fields f);
 __global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb, int ncol);
 __global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,

@@ -78,7 +78,7 @@ def test_hydrostatic_plans_match_no_overlap(monkeypatch, name, nranks):
     assert any((p[:, 2] == 1).any() for p in pl)
 
 
-@pytest.mark.parametrize("variant", [{"isladvec": 1}, {"ibltyp": 2}, {"iboudy": 4}, {"idiffu": 2}],
+@pytest.mark.parametrize("variant", [{"isladvec": 1}, {"ibltyp": 2}, {"iboudy": 4}, {"idiffu": 2}, {"idiffu": 3}],
                          ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
 def test_hydrostatic_variant_plans_match(variant):
     rc = dataclasses.replace(CONFIGS["C1"], **variant)

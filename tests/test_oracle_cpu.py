@@ -163,7 +163,7 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     base.step(10)
     ref = base.get("ATM1_T")
     refq = base.get("ATM1_QV")
-    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"isladvec": 1}):
+    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])
         o.put_state(data["state"])
@@ -1496,3 +1496,101 @@ def test_nh_sound_substep_matches_numpy_restatement():
         assert np.abs(want[sl]).max() > 0.0, name
         np.testing.assert_allclose(got[sl], want[sl], rtol=1e-11, atol=1e-12 * np.abs(want[sl]).max(), err_msg=name)
     assert not np.array_equal(b["cpp"][CI], a["cpp"][CI]) and not np.array_equal(b["cw"][CE], a["cw"][CE])
+
+
+# ---- idiffu = 3: the sixth-order flux-limited column scheme ---------------------------------
+
+def _psc2psd_np(pc):
+    """psc2psd on the global grid, Main/mpplib/mod_mppparam.F90:13811-13862 (pc[i-1, j-1])."""
+    iy, jx = pc.shape
+    pd = np.empty_like(pc)
+    P = lambda j, i: pc[i - 1, j - 1]  # noqa: E731
+    for i in range(1, iy + 1):
+        for j in range(1, jx + 1):
+            jin, iin = 2 <= j <= jx - 1, 2 <= i <= iy - 1
+            if jin and iin:
+                v = (P(j, i) + P(j, i - 1) + P(j - 1, i) + P(j - 1, i - 1)) * 0.25
+            elif jin and i == iy:
+                v = (P(j, iy - 1) + P(j - 1, iy - 1)) * 0.5
+            elif jin and i == 1:
+                v = (P(j, 1) + P(j - 1, 1)) * 0.5
+            elif iin and j == 1:
+                v = (P(1, i) + P(1, i - 1)) * 0.5
+            elif iin and j == jx:
+                v = (P(jx - 1, i) + P(jx - 1, i - 1)) * 0.5
+            else:
+                v = P(1 if j == 1 else jx - 1, 1 if i == 1 else iy - 1)
+            pd[i - 1, j - 1] = v
+    return pd
+
+
+def _diffu6_np(fv, lv, j, i, jmax, imax):
+    """The bracket of Main/mod_diffusion.F90:428-470 / 618-648 at 1-based (j, i); fv, lv
+    index [i-1, j-1]."""
+    F = lambda jj, ii: fv[ii - 1, jj - 1]  # noqa: E731
+    L = lambda jj, ii: lv[ii - 1, jj - 1]  # noqa: E731
+    jm = [max(j - d, 1) for d in (1, 2, 3)]
+    jp = [min(j + d, jmax) for d in (1, 2, 3)]
+    im = [max(i - d, 1) for d in (1, 2, 3)]
+    ip = [min(i + d, imax) for d in (1, 2, 3)]
+    x0 = 10.0 * (F(j, i) - F(jm[0], i)) + -5.0 * (F(jp[0], i) - F(jm[1], i)) + 1.0 * (F(jp[1], i) - F(jm[2], i))
+    x0 = 0.0 if x0 * (L(j, i) - L(jm[0], i)) <= 0.0 else x0
+    x1 = 10.0 * (F(jp[0], i) - F(j, i)) + -5.0 * (F(jp[1], i) - F(jm[0], i)) + 1.0 * (F(jp[2], i) - F(jm[1], i))
+    x1 = 0.0 if x1 * (L(jp[0], i) - L(j, i)) <= 0.0 else x1
+    y0 = 10.0 * (F(j, i) - F(j, im[0])) + -5.0 * (F(j, ip[0]) - F(j, im[1])) + 1.0 * (F(j, ip[1]) - F(j, im[2]))
+    y0 = 0.0 if y0 * (L(j, i) - L(j, im[0])) <= 0.0 else y0
+    y1 = 10.0 * (F(j, ip[0]) - F(j, i)) + -5.0 * (F(j, ip[1]) - F(j, im[0])) + 1.0 * (F(j, ip[2]) - F(j, im[1]))
+    y1 = 0.0 if y1 * (L(j, ip[0]) - L(j, i)) <= 0.0 else y1
+    return (x1 - x0) + (y1 - y0)
+
+
+def test_oracle_idiffu3_column_restatement(c1_data):
+    """idiffu = 3 in the oracle against a NumPy restatement of Main/mod_diffusion.F90:412-516
+    (diffu_d) and calc_coeff's :174-183: the u, v tendencies of one tend differ from a run
+    whose diffusion is zero (idiffu = 1 with ckh = adyndif = 0) by diff_6th_coef * p*dotb *
+    the bracket of u / msfd, on the column j = jdi2 only; and the qv forecast by the same for
+    qxb3d (limiter on qxb3d / msfd) times the forecast's time step, on j = jci2 only."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    rc, data = c1_data
+    r3 = dataclasses.replace(rc, idiffu=3)
+    r0 = dataclasses.replace(rc, idiffu=1, ckh=0.0, adyndif=0.0)
+    out = {}
+    for key, r in (("d6", r3), ("zero", r0)):
+        o = OracleCore(r, data["split"])
+        o.put_state(data["state"])
+        o.bdyval()
+        st = {n: o.get(n) for n in ("ATM2_U", "ATM2_V", "ATM2_QV", "PSB")}
+        o.tend()
+        out[key] = {n: o.get_work(n) for n in ("uten", "vten", "cqv")}
+    jx, iy, kz = rc.jx, rc.iy, rc.kz
+    coef = 0.12 * 0.015625 / (2.0 * rc.dt)
+    psb = st["PSB"][0]
+    psd = _psc2psd_np(psb)
+    msfd = data["state"]["MSFD"][0]
+    jd, jc = jx - 1, jx - 2                       # jdi2, jci2 of one tile
+    for name, a2 in (("uten", st["ATM2_U"]), ("vten", st["ATM2_V"])):
+        d = out["d6"][name] - out["zero"][name]
+        assert not np.any(np.delete(d, jd - 1, axis=2)), name
+        worst = 0.0
+        for k in range(kz):
+            um = (a2[k] * (1.0 / psd)) / msfd
+            for i in range(2, iy):
+                term = (coef * psd[i - 1, jd - 1]) * _diffu6_np(um, um, jd, i, jx, iy)
+                worst = max(worst, abs(d[k, i - 1, jd - 1] - term) / max(abs(term), 1e-30))
+        assert worst < 1e-8, (name, worst)
+    d = out["d6"]["cqv"] - out["zero"]["cqv"]
+    assert not np.any(np.delete(d, jc - 1, axis=2))
+    ratios = []
+    for k in range(kz):
+        with np.errstate(divide="ignore", invalid="ignore"):     # p*b is 0 on the dot-only row/column
+            qb = np.maximum(st["ATM2_QV"][k] * (1.0 / psb), 1e-8)
+        for i in range(2, iy - 1):
+            term = (coef * psb[i - 1, jc - 1]) * _diffu6_np(qb, qb / msfd, jc, i, jx - 1, iy - 1)
+            if abs(term) > 1e-14:
+                ratios.append(d[k, i - 1, jc - 1] / term)
+    ratios = np.array(ratios)
+    assert ratios.size > 10
+    dt2 = ratios.mean()
+    assert any(abs(dt2 - x) < 1e-6 * x for x in (rc.dt, 2.0 * rc.dt)), dt2
+    assert np.max(np.abs(ratios - dt2)) < 1e-6 * dt2

@@ -378,7 +378,11 @@ def test_negative_moisture_serial_sweep(c1_data):
 
 
 # namelist options beyond the defaults, each against the oracle and under decomposition
-VARIANTS = [{"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"isladvec": 1}, {"isladvec": 1, "iqmsl": 0}]
+VARIANTS = [{"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
+            {"isladvec": 1, "iqmsl": 0}]
+# idiffu = 3 acts on each tile's last interior column, so its result depends on the
+# decomposition as the reference's does (test_idiffu3_tiles_match_oracle_tiles)
+DECOMP_VARIANTS = [v for v in VARIANTS if v.get("idiffu") != 3]
 
 
 def _variant_id(v):
@@ -416,7 +420,7 @@ def test_variant_parity(c1_data, variant):
         assert err <= max(1e-9, 100.0 * spread), (name, err, spread)
 
 
-@pytest.mark.parametrize("variant", VARIANTS, ids=_variant_id)
+@pytest.mark.parametrize("variant", DECOMP_VARIANTS, ids=_variant_id)
 def test_variant_decomposition(c1_data, variant):
     import dataclasses
     from regcm_amd.dycore import DynCore
@@ -430,6 +434,39 @@ def test_variant_decomposition(c1_data, variant):
         e.step(6)
     for name in STATE_FIELDS:
         assert np.array_equal(ref.get(name), til.get(name)), name
+
+
+@pytest.mark.parametrize("nthreads,transport", [(2, "copy"), (3, "copy"), (4, "copy"), (4, "rccl")])
+def test_idiffu3_tiles_match_oracle_tiles(c1_data, monkeypatch, nthreads, transport):
+    """idiffu = 3 on a decomposed domain: the reference applies the sixth-order term on every
+    tile's own column j = jdi2 / jci2 (Main/mod_diffusion.F90:421, 611, 745, 902), so the engine's
+    tiles are checked against the oracle run as the same set_nproc tiles (oracle/orc_par.c),
+    1 step < 1e-12, 3 steps < 1e-11; the column terms reach the neighbour's ring through their
+    own exchange (also over RCCL), and the result differs from one tile."""
+    import dataclasses
+    from oracle.oracle import OracleParallel
+    from regcm_amd.config import set_nproc
+    from regcm_amd.dycore import DynCore
+    rc, data = c1_data
+    rcv = dataclasses.replace(rc, idiffu=3)
+    cj, ci = set_nproc(nthreads, rc.jx, rc.iy)
+    if transport == "rccl":
+        monkeypatch.setenv("RCMDYN_FORCE_RCCL", "1")
+    o = OracleParallel(rcv, data["split"], nthreads=nthreads)
+    e = DynCore(rcv, data["split"], nproc_j=cj, nproc_i=ci)
+    one = DynCore(rcv, data["split"])
+    for x in (o, e, one):
+        x.put_state(data["state"])
+        x.bdyval()
+    for nsteps, tol in ((1, 1e-12), (2, 1e-11)):
+        o.step(nsteps)
+        e.step(nsteps)
+        for name in STATE_FIELDS:
+            err = relerr(e.get(name), o.get(name), rcv, name)
+            assert err < tol, (name, err, nsteps)
+    one.step(3)
+    if cj > 1:
+        assert not np.array_equal(one.get("ATM1_QV"), e.get("ATM1_QV"))
 
 
 @pytest.mark.parametrize("iy", [300, 560])
