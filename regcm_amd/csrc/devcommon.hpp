@@ -97,6 +97,28 @@ __device__ __forceinline__ double psc2psd_global(const Geom& g, const double* pc
   return F2(pc, (j == 1) ? 1 : jx - 1, (i == 1) ? 1 : iy - 1);
 }
 
+// idiffu = 3, the sixth-order flux-limited scheme (Main/mod_diffusion.F90:412-516 diffu_d,
+// 736-785 diffu_x3d, 893-942 diffu_x4d3d).  The reference applies it on one column of each
+// tile, j = jdi2 (dot) / jci2 (cross), every row of the interior, with neighbour indices
+// clamped to the global domain (1..jx, 1..iy on dot points; 1..jx-1, 1..iy-1 on cross points).
+// fv gives the field in the fluxes, lv the field over msfd in the limiter.
+template <class FV, class LV>
+__device__ __forceinline__ double diffu6_bracket(int j, int i, int jmax, int imax, FV fv, LV lv) {
+  const int jm1 = max(j - 1, 1), jm2 = max(j - 2, 1), jm3 = max(j - 3, 1);
+  const int jp1 = min(j + 1, jmax), jp2 = min(j + 2, jmax), jp3 = min(j + 3, jmax);
+  const int im1 = max(i - 1, 1), im2 = max(i - 2, 1), im3 = max(i - 3, 1);
+  const int ip1 = min(i + 1, imax), ip2 = min(i + 2, imax), ip3 = min(i + 3, imax);
+  double x0 = h4_c1 * (fv(j, i) - fv(jm1, i)) + h4_c2 * (fv(jp1, i) - fv(jm2, i)) + h4_c3 * (fv(jp2, i) - fv(jm3, i));
+  if (x0 * (lv(j, i) - lv(jm1, i)) <= d_zero) x0 = d_zero;
+  double x1 = h4_c1 * (fv(jp1, i) - fv(j, i)) + h4_c2 * (fv(jp2, i) - fv(jm1, i)) + h4_c3 * (fv(jp3, i) - fv(jm2, i));
+  if (x1 * (lv(jp1, i) - lv(j, i)) <= d_zero) x1 = d_zero;
+  double y0 = h4_c1 * (fv(j, i) - fv(j, im1)) + h4_c2 * (fv(j, ip1) - fv(j, im2)) + h4_c3 * (fv(j, ip2) - fv(j, im3));
+  if (y0 * (lv(j, i) - lv(j, im1)) <= d_zero) y0 = d_zero;
+  double y1 = h4_c1 * (fv(j, ip1) - fv(j, i)) + h4_c2 * (fv(j, ip2) - fv(j, im1)) + h4_c3 * (fv(j, ip3) - fv(j, im2));
+  if (y1 * (lv(j, ip1) - lv(j, i)) <= d_zero) y1 = d_zero;
+  return (x1 - x0) + (y1 - y0);
+}
+
 // vadv4d ind = 3 (iuwvadv = 1 with ibltyp = 2, Main/mod_advection.F90:917-957): the hydrometeor
 // interface value at interface kk (2..kz) before the svv factor.  The linear interpolation
 // twt(kk,1) f(kk) + twt(kk,2) f(kk-1), replaced at kpb - 1 and kpb (kpb >= 4) by the PBL-top

@@ -450,7 +450,8 @@ struct rcmdyn_engine {
     t.qdot = dalloc(t, P * (kz + 1));
     t.phi = dalloc(t, P3);
     if (cfg.isladvec == 1) { t.slqv = dalloc(t, P3); t.slqc = dalloc(t, P3); }
-    if (cfg.idiffu == 3) for (double*& d : t.d6) d = dalloc(t, P3);
+    if (cfg.idiffu == 3)
+      for (int q = 0; q < (cfg.idynamic == 2 ? 7 : 5); q++) t.d6[q] = dalloc(t, P * (kz + 1));
     if (cfg.ibltyp == 2) {
       t.a1tke = dalloc(t, P * (kz + 1)); t.a2tke = dalloc(t, P * (kz + 1)); t.ctke = dalloc(t, P * (kz + 1));
       t.kpbl = dalloc(t, P);
@@ -544,6 +545,7 @@ struct rcmdyn_engine {
     TkeArgs a{};
     a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.msfd = t.msfd; a.xmsf = t.xmsf; a.psa = t.psa_[c]; a.rpsa = t.rpsa;
     a.qdot = t.qdot; a.tkephy = t.tkephy; a.a1tke = t.a1tke; a.a2tke = t.a2tke; a.ctke = t.ctke;
+    a.psb = t.psb_[c];
     if (cfg.idynamic == 2) { a.xk = nhf[&t - tiles.data()].xkcr; a.xkpb = t.psb_[t.cur]; a.xk_half = 0; }
     else { a.xk = t.xkcs; a.xk_half = 1; }
     return a;
@@ -586,6 +588,8 @@ struct rcmdyn_engine {
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.ppphy = t.phy[5]; f.wphy = t.phy[6];
     f.slqv = t.slqv; f.slqc = t.slqc;
+    f.d6u = t.d6[0]; f.d6v = t.d6[1]; f.d6t = t.d6[2]; f.d6qv = t.d6[3]; f.d6qc = t.d6[4];
+    f.d6pp = t.d6[5]; f.d6w = t.d6[6];
     f.kpbl = hc.iqxvadv == 3 ? t.kpbl : nullptr;
     return f;
   }
@@ -600,8 +604,6 @@ struct rcmdyn_engine {
         throw std::runtime_error("rcmdyn: nh_dtsmax / nh_xmsf (init_sound) must be set for idynamic=2");
     }
     if (cfg.idiffu < 1 || cfg.idiffu > 3) throw std::runtime_error("rcmdyn: idiffu must be 1, 2 or 3");
-    if (cfg.idiffu == 3 && (cfg.idynamic != 1 || cfg.ibltyp == 2))
-      throw std::runtime_error("rcmdyn: idiffu = 3 is built for the hydrostatic core without UW TKE");
     if (cfg.ipgf != 0 && cfg.ipgf != 1) throw std::runtime_error("rcmdyn: ipgf must be 0 or 1");
     if (cfg.isladvec != 0 && cfg.isladvec != 1) throw std::runtime_error("rcmdyn: isladvec must be 0 or 1");
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
@@ -1538,13 +1540,15 @@ struct rcmdyn_engine {
     if (phase & TEND_PRE) {
     // isladvec = 1: k_sladv forms ud*msfd two points out (the reference exchanges atmx%ud 2
     // wide, :995-997) and interpolates atm2 qx up to three points out (max(idif, 4), :1073-1075)
-    const int wu = cfg.isladvec == 1 ? 2 : 1, wq = cfg.isladvec == 1 ? 3 : 2;
+    // idiffu = 3: atm2 idif = 3 wide, p*b 4 wide (p*dotb on k_nh_diffu6's 3-deep dot rings)
+    const int wd = cfg.idiffu == 3 ? 3 : 2;
+    const int wu = cfg.isladvec == 1 ? 2 : 1, wq = std::max(cfg.isladvec == 1 ? 3 : 2, wd);
     // atm2 on the second stream, overlapped with decouple and compute_omega (atm1 only)
-    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, 3}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz},
+    std::vector<XField> pro{{FK::PSA, 1, 3}, {FK::PSB, 1, wd + 1}, {FK::A1U, kz, wu}, {FK::A1V, kz, wu}, {FK::A1T, kz},
                             {FK::A1QV, kz}, {FK::A1QC, kz}, {FK::A1PP, kz}, {FK::A1W, kp}};
-    std::vector<XField> pro2{{FK::A2U, kz, 2}, {FK::A2V, kz, 2}, {FK::A2T, kz, 2}, {FK::A2QV, kz, wq},
-                             {FK::A2QC, kz, wq}, {FK::A2PP, kz, 2}, {FK::A2W, kp, 2}};
-    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro2.push_back({FK::A2TKE, kp, 2}); }
+    std::vector<XField> pro2{{FK::A2U, kz, wd}, {FK::A2V, kz, wd}, {FK::A2T, kz, wd}, {FK::A2QV, kz, wq},
+                             {FK::A2QC, kz, wq}, {FK::A2PP, kz, wd}, {FK::A2W, kp, wd}};
+    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro2.push_back({FK::A2TKE, kp, wd}); }
     fork_point();
     xchv(pro);
     fork_after_exchange();
@@ -1558,6 +1562,11 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_omega, q.ce1, BLK, 0, stream, g, dc, f);
     });
     xch_join();
+    if (cfg.idiffu == 3)       // the tendency kernels compute owned points only: no exchange
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        KLAUNCH(k_nh_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kp, 6), dim3(64), 0, stream, g, dc, nhfields(t));
+      });
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
@@ -1759,7 +1768,10 @@ struct rcmdyn_engine {
     std::vector<XField> pro2{{FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
                              {FK::A2QC, kz, 3}};
     // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
-    if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kz + 1, 1}); pro2.push_back({FK::A2TKE, kz + 1, 2}); }
+    if (cfg.ibltyp == 2) {
+      pro.push_back({FK::A1TKE, kz + 1, 1});
+      pro2.push_back({FK::A2TKE, kz + 1, cfg.idiffu == 3 ? 3 : 2});
+    }
     // surface_pressures + 2-D reciprocals (:815-834), compute_omega columns, new_pressure,
     // geopotential in one launch (calc_coeff is formed where it is read, in k_momentum and
     // k_scalars)

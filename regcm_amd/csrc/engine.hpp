@@ -148,8 +148,9 @@ struct Tile {
   double *qdot, *phi;
   double *slqv = nullptr, *slqc = nullptr;   // isladvec = 1: k_sladv output
   // idiffu = 3: the sixth-order terms of the tile's j = jdi2 / jci2 column (k_diffu6), frame
-  // planes so one width-1 exchange hands the left neighbour's column to the ring: u, v, t, qv, qc
-  double* d6[5] = {};
+  // planes so one width-1 exchange hands the left neighbour's column to the ring: u, v, t, qv,
+  // qc (and NH pp, w on kz + 1 planes)
+  double* d6[7] = {};
   // ibltyp = 2: atm1/atm2 tke (decoupled, kz+1 levels), the forecast atmc%tke, and the UW
   // scheme's tendency (allocated on its first put)
   double *a1tke = nullptr, *a2tke = nullptr, *ctke = nullptr, *tkephy = nullptr;

@@ -224,6 +224,47 @@ __device__ __forceinline__ double diffx_at(const Geom& g, const Consts* c, doubl
   return ften;
 }
 
+// idiffu = 3 (Main/mod_diffusion.F90:412-516, 602-651, 736-785, 893-942): the sixth-order
+// terms of the tile's column, j = jdi2 for u, v and j = jci2 for t, qv, qc, pp (levels 1..kz)
+// and w (1..kz+1; diffu_x3df reads xkc on level kz+1, one past its kz levels -- the
+// coefficient is diff_6th_coef * p*b on every level, as xkcf holds it), from the decoupled
+// atm2 fields of mkslice (Main/mod_slice.F90:163-183, 215-238).  blockIdx.z: 0 u and v, 1 t,
+// 2 qv, 3 qc, 4 pp, 5 w; blockIdx.y = level.  k_nh_tend_c / k_nh_tend_d add them in the
+// reference's place of the diffusion term.
+__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f) {
+  const int i = g.ide1 + (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
+  const int q = (int)blockIdx.z, kz = c->kz;
+  const double* ps = f.psb;
+  double* d6 = const_cast<double*>(q == 0 ? f.d6u : q == 1 ? f.d6t : q == 2 ? f.d6qv : q == 3 ? f.d6qc
+                                                   : q == 4 ? f.d6pp : f.d6w);
+  if (k > (q == 5 ? kz + 1 : kz)) return;
+  if (q == 0) {
+    const int j = g.jdi2;
+    if (!in(i, g.idi1, g.idi2)) return;
+    auto rd = [&](int jj, int ii) { return d_one / psc2psd_global(g, ps, jj, ii); };
+    auto uu = [&](int jj, int ii) { return F3(f.a2u, jj, ii, k) * rd(jj, ii) / F2(f.msfd, jj, ii); };
+    auto vv = [&](int jj, int ii) { return F3(f.a2v, jj, ii, k) * rd(jj, ii) / F2(f.msfd, jj, ii); };
+    const double xkd = c->diff6 * psc2psd_global(g, ps, j, i);
+    F3(d6, j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, uu, uu);
+    F3(const_cast<double*>(f.d6v), j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, vv, vv);
+    return;
+  }
+  const int j = g.jci2;
+  if (!in(i, g.ici1, g.ici2)) return;
+  const double* a = q == 1 ? f.a2t : q == 2 ? f.a2qv : q == 3 ? f.a2qc : q == 4 ? f.a2pp : f.a2w;
+  auto fv = [&](int jj, int ii) {
+    const double v = F3(a, jj, ii, k) * (d_one / F2(ps, jj, ii));
+    return q == 2 ? dmax(v, MINQQ) : (q == 3 ? dmax(v, d_zero) : v);
+  };
+  auto lv = [&](int jj, int ii) { return fv(jj, ii) / F2(f.msfd, jj, ii); };
+  const double xkc = d_one * (c->diff6 * F2(ps, j, i));
+  F3(d6, j, i, k) = xkc * diffu6_bracket(j, i, g.gjx - 1, g.giy - 1, fv, lv);
+}
+// the column term where k_nh_tend_c / k_nh_tend_d add diffusion
+__device__ __forceinline__ double diff6_add(const Geom& g, double ften, const double* d6, int jc, int j, int i, int k) {
+  return j == jc ? ften + F3(d6, j, i, k) : ften;
+}
+
 // tau, Main/mod_bdycod.F90:5115-5123
 __device__ __forceinline__ double nh_tau(const Consts* c, double z, double zmax) {
   if (z > zmax - c->rayhd) {
@@ -418,7 +459,8 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double wt0 = d_zero;
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
     if (nudge) RELAX5(wd, f.wwb0, f.wwbt, f.a2w);
-    wd = diffx_l(g, c, wd, sT[4], F3(f.xkcr, j, i, (k == 1) ? 1 : k - 1) * c->rdxsq * pbs, j, i, ti, tj);   // xkcf
+    wd = c->idiffu == 3 ? diff6_add(g, wd, f.d6w, g.jci2, j, i, k)
+                        : diffx_l(g, c, wd, sT[4], F3(f.xkcr, j, i, (k == 1) ? 1 : k - 1) * c->rdxsq * pbs, j, i, ti, tj);   // xkcf
     double wt = wt0 + wd + PHY(wphy);
     // raydamp3f and decoupling before sound (:466-499), sound's acoustic-step scaling (:229-245)
     if (c->ifrayd == 1 && k <= c->rayndamp)
@@ -442,7 +484,7 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double pt0 = d_zero;
     if (sponge) pt0 = wsp * d_zero + (d_one - wsp) * F3(f.ppbt, j, i, k);
     if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
-    pd = diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
+    pd = c->idiffu == 3 ? diff6_add(g, pd, f.d6pp, g.jci2, j, i, k) : diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
     double pt = pt0 + pd + PHY(ppphy);
     if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3, decoupling, acoustic-step scaling
       pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
@@ -468,7 +510,7 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double tt0 = d_zero;
     if (sponge) tt0 = wsp * d_zero + (d_one - wsp) * F3(f.tbt, j, i, k);
     if (nudge) RELAX5(td, f.tb0, f.tbt, f.a2t);
-    td = diffx_l(g, c, td, sT[0], xkc, j, i, ti, tj);
+    td = c->idiffu == 3 ? diff6_add(g, td, f.d6t, g.jci2, j, i, k) : diffx_l(g, c, td, sT[0], xkc, j, i, ti, tj);
     double tt = tt0 + td + PHY(tphy);
     tt = tt + 0.0;
     if (ray) tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
@@ -499,7 +541,7 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
 #undef FQ
       qd = qd + rfac * (xf * q0 - xg * (q1 + q2 + q3 + q4 - d_four * q0));
     }
-    qd = diffx_l(g, c, qd, sT[1], xkc, j, i, ti, tj);
+    qd = c->idiffu == 3 ? diff6_add(g, qd, f.d6qv, g.jci2, j, i, k) : diffx_l(g, c, qd, sT[1], xkc, j, i, ti, tj);
     double qv = qt0 + qd + PHY(qvphy);
     qv = qv + 0.0;
     if (ray) qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
@@ -524,7 +566,7 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     if (k >= 2) cd = cd + cflux(k) * c->xds[k];
     if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
     cd = cd + xqcat(k) * cr;
-    cd = diffx_l(g, c, cd, sT[2], xkc, j, i, ti, tj);
+    cd = c->idiffu == 3 ? diff6_add(g, cd, f.d6qc, g.jci2, j, i, k) : diffx_l(g, c, cd, sT[2], xkc, j, i, ti, tj);
     double qc = d_zero + cd + PHY(qcphy);
     qc = qc + 0.0;
     if (wdiag) F3(f.qcten, j, i, k) = qc;
@@ -661,7 +703,9 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
     for (int pass = 0; pass < 2; pass++) {
       double (*b)[TDW] = pass ? sBV : sBU;
       double t = pass ? vd : ud;
-      if (c->idiffu == 2) {
+      if (c->idiffu == 3) {                 // the column term of k_nh_diffu6
+        t = diff6_add(g, t, pass ? f.d6v : f.d6u, g.jdi2, j, i, k);
+      } else if (c->idiffu == 2) {
         t = t + xkd * (o4_c1 * (UM(b, j + 1, i) + UM(b, j - 1, i) + UM(b, j, i + 1) + UM(b, j, i - 1)) +
                        o4_c2 * (UM(b, j + 1, i + 1) + UM(b, j - 1, i - 1) + UM(b, j - 1, i + 1) + UM(b, j + 1, i - 1)) +
                        o4_c3 * (UM(b, j, i)));

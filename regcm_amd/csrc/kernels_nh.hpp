@@ -34,6 +34,8 @@ struct NHFields {
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy, *ppphy, *wphy;
   // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv; null otherwise)
   const double *slqv, *slqc;
+  // idiffu = 3: the column terms of k_nh_diffu6 (u, v, t, qv, qc, pp, w; null otherwise)
+  const double *d6u, *d6v, *d6t, *d6qv, *d6qc, *d6pp, *d6w;
   // iuwvadv = 1 (ibltyp = 2): the PBL-top level of vadv4d ind = 3 (null otherwise)
   const double* kpbl;
   // forecasts (atmc) and fixed moisture
@@ -65,6 +67,7 @@ constexpr int NH_CFL_SLOTS = 1024;
 #define NH_ZFIRST 1
 #endif
 
+__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);

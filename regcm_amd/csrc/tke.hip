@@ -58,7 +58,13 @@ __global__ void k_tke_tend(Geom g, const Consts* __restrict__ c, const StepState
                     : a.xk_half ? F3(a.xk, j, i, k > 1 ? k - 1 : 1) : F3(a.xk, j, i, k);
     const double fac = c->nuk;
 #define X(dj, di) F3(x, j + (dj), i + (di), k)
-    if (c->idiffu == 2) {
+    if (c->idiffu == 3) {                   // :602-651, the tile's column j = jci2 only (fac * xkc)
+      if (j == g.jci2) {
+        auto fv = [&](int jj, int ii) { return F3(x, jj, ii, k); };
+        auto lv = [&](int jj, int ii) { return F3(x, jj, ii, k) / F2(a.msfd, jj, ii); };
+        ften = ften + fac * (c->diff6 * F2(a.psb, j, i)) * diffu6_bracket(j, i, g.gjx - 1, g.giy - 1, fv, lv);
+      }
+    } else if (c->idiffu == 2) {
       ften = ften + fac * xk * (o4_c1 * (X(1, 0) + X(-1, 0) + X(0, 1) + X(0, -1)) +
                                 o4_c2 * (X(1, 1) + X(-1, -1) + X(-1, 1) + X(1, -1)) + o4_c3 * X(0, 0));
     } else {

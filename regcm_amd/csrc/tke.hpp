@@ -11,6 +11,7 @@ namespace rcm {
 struct TkeArgs {
   const double *a1u, *a1v, *msfd, *xmsf, *psa, *rpsa, *qdot, *xk, *tkephy;
   const double* xkpb;   // NH: xk is the unscaled xkcr, scaled here by rdxsq * p*(b) (xkcf)
+  const double* psb;    // idiffu = 3: xkc = diff_6th_coef * p*b
   double *a1tke, *a2tke, *ctke;
   int xk_half;
 };

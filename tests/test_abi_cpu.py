@@ -107,7 +107,7 @@ def test_create_without_gpu_fails_loudly():
 
 
 @pytest.mark.parametrize("opt,msg", [({"upstream_mode": 0}, "upstream_mode"),
-                                     ({"idiffu": 4}, "idiffu"), ({"idiffu": 3, "ibltyp": 2}, "idiffu"),
+                                     ({"idiffu": 4}, "idiffu"), ({"idiffu": 0}, "idiffu"),
                                      ({"iboudy": 3}, "iboudy"),
                                      ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv")])
 def test_create_refuses_unbuilt_options(opt, msg):

@@ -117,7 +117,9 @@ def test_nh_rest_state():
         assert np.abs(e.get(n)[:, :-1, :-1] / ps).max() < lim, n
 
 
-NH_VARIANTS = [{"iboudy": 4}, {"idiffu": 2}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1}]
+NH_VARIANTS = [{"iboudy": 4}, {"idiffu": 2}, {"idiffu": 3}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1}]
+# idiffu = 3 depends on the decomposition as the reference's does (test_nh_idiffu3_tiles)
+NH_DECOMP_VARIANTS = [v for v in NH_VARIANTS if v.get("idiffu") != 3]
 
 
 @pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
@@ -177,7 +179,7 @@ def test_nh_overlap_modes(nh_data, monkeypatch, mode):
         assert np.array_equal(ref.get(name), til.get(name)), name
 
 
-@pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
+@pytest.mark.parametrize("variant", NH_DECOMP_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
 def test_nh_variant_decomposition(nh_data, variant):
     from regcm_amd.dycore import DynCore
     rc, data = nh_data
@@ -190,3 +192,26 @@ def test_nh_variant_decomposition(nh_data, variant):
         e.step(6)
     for name in NH_FIELDS:
         assert np.array_equal(ref.get(name), til.get(name)), name
+
+
+@pytest.mark.parametrize("nthreads", [2, 4])
+def test_nh_idiffu3_tiles(nh_data, nthreads):
+    """NH idiffu = 3 on set_nproc tiles against the oracle run as the same tiles: the
+    sixth-order terms of u, v, t, qv, qc, pp and w (kz + 1 levels) on every tile's own column."""
+    from oracle.oracle import OracleParallel
+    from regcm_amd.config import set_nproc
+    from regcm_amd.dycore import DynCore
+    rc, data = nh_data
+    rcv = dataclasses.replace(rc, idiffu=3)
+    cj, ci = set_nproc(nthreads, rc.jx, rc.iy)
+    o = OracleParallel(rcv, data["split"], nthreads=nthreads)
+    e = DynCore(rcv, data["split"], nproc_j=cj, nproc_i=ci)
+    for x in (o, e):
+        x.put_state(data["state"])
+        x.bdyval()
+    for nsteps, tol in ((1, 1e-11), (2, 1e-10)):
+        o.step(nsteps)
+        e.step(nsteps)
+        for name in NH_FIELDS:
+            err = relerr(e.get(name), o.get(name), rcv, name)
+            assert err < tol, (name, err, nsteps)

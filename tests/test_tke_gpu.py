@@ -66,7 +66,7 @@ def test_tke_init_bdyval_exact(tke_c1):
         assert np.array_equal(e.get(name), o.get(name)), name
 
 
-@pytest.mark.parametrize("variant", [{}, {"idiffu": 2}, {"iboudy": 4}],
+@pytest.mark.parametrize("variant", [{}, {"idiffu": 2}, {"idiffu": 3}, {"iboudy": 4}],
                          ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()) or "default")
 def test_tke_parity(tke_c1, variant):
     rc, data = tke_c1
@@ -137,6 +137,24 @@ def test_nh_tke_parity(tke_n1):
     ref.step(4)
     for name in TKE_STATE_FIELDS + NH_STATE_FIELDS:
         assert np.array_equal(til.get(name), ref.get(name)), name
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_tke_idiffu3_tiles_match_oracle_tiles(tke_c1, tke_n1, core):
+    """idiffu = 3 with the TKE (diffu_x3df of atm2 tke with nuk on each tile's column j = jci2,
+    Main/mod_diffusion.F90:602-651) on 2 x 2 tiles against the oracle run as the same tiles."""
+    from oracle.oracle import OracleParallel
+    from regcm_amd.dycore import DynCore
+    rc, data = tke_c1 if core == "hydrostatic" else tke_n1
+    rc = dataclasses.replace(rc, idiffu=3)
+    o = start(OracleParallel(rc, data["split"], nthreads=4), rc, data)
+    e = start(DynCore(rc, data["split"], nproc_j=2, nproc_i=2), rc, data)
+    tol = 1e-11 if core == "hydrostatic" else 1e-10
+    o.step(2)
+    e.step(2)
+    for name in TKE_STATE_FIELDS:
+        err = relerr(e.get(name), o.get(name), rc, name)
+        assert err < tol, (name, err)
 
 
 def test_tke_errors(c1_data, tke_c1):
