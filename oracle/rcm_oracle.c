@@ -1184,10 +1184,17 @@ static void hadvuv(orc_t* o) {                                     /* :203-233 *
         double ff2 = ul * (A3(u, j - 1, i, k) + A3(u, j, i, k));
         double ff3 = ul * (A3(v, j, i + 1, k) + A3(v, j, i, k));
         double ff4 = ul * (A3(v, j, i - 1, k) + A3(v, j, i, k));
-        ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
-        ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
-        vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
-        vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        if (o->cfg.upstream_mode) {
+          ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+          ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+          vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+          vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        } else {                    /* centred, upstream_mode = .false. (:152-155, :183-186) */
+          ucmonb = ucmona + ucmonb;
+          ucmonc = ucmonc + ucmona;
+          vcmonb = vcmona + vcmonb;
+          vcmonc = vcmonc + vcmona;
+        }
         double dm = A2(o->dmsf, j, i);
         A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) - dm *
             ((A3(u, j + 1, i, k) + A3(u, j, i, k)) * ucmonb - (A3(u, j, i, k) + A3(u, j - 1, i, k)) * ucmonc +
@@ -1213,7 +1220,8 @@ static void vadvuv(orc_t* o) {                                     /* :286-299 *
       }
 }
 
-/* upstream flux form shared by hadvt/hadvqv/hadvqx (:337-351, :547-561, :639-653) */
+/* upstream flux form shared by hadvt/hadvqv/hadvqx (:337-351, :547-561, :639-653); the
+ * centred form of upstream_mode = .false. (:322-335, :532-545, :624-637) */
 static void hadv_scalar(orc_t* o, const double* f, double* ften, int limiter /*0 none,1 t,2 q*/) {
   double ul = o->ul;
   for (int k = 1; k <= o->kz; k++)
@@ -1226,6 +1234,12 @@ static void hadv_scalar(orc_t* o, const double* f, double* ften, int limiter /*0
         double fx2 = (d_one + f1) * A3(f, j, i, k) + (d_one - f1) * A3(f, j + 1, i, k);
         double fy1 = (d_one + f2) * A3(f, j, i - 1, k) + (d_one - f2) * A3(f, j, i, k);
         double fy2 = (d_one + f2) * A3(f, j, i, k) + (d_one - f2) * A3(f, j, i + 1, k);
+        if (!o->cfg.upstream_mode) {  /* centred (:323-332, :414-423, :443-446, :533-542, :625-634) */
+          fx1 = A3(f, j - 1, i, k) + A3(f, j, i, k);
+          fx2 = A3(f, j, i, k) + A3(f, j + 1, i, k);
+          fy1 = A3(f, j, i - 1, k) + A3(f, j, i, k);
+          fy2 = A3(f, j, i, k) + A3(f, j, i + 1, k);
+        }
         A3(o->fg, j, i, k) = -A2(o->xmsf, j, i) *
             (A3(o->uavg2, j, i, k) * fx2 - A3(o->uavg1, j, i, k) * fx1 +
              A3(o->vavg2, j, i, k) * fy2 - A3(o->vavg1, j, i, k) * fy1);
@@ -2157,10 +2171,17 @@ static void nh_hadvuv(orc_t* o) {
         double ff2 = ul * (A3(u, j - 1, i, k) + A3(u, j, i, k));
         double ff3 = ul * (A3(v, j, i + 1, k) + A3(v, j, i, k));
         double ff4 = ul * (A3(v, j, i - 1, k) + A3(v, j, i, k));
-        ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
-        ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
-        vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
-        vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        if (o->cfg.upstream_mode) {
+          ucmonb = (d_one + ff1) * ucmona + (d_one - ff1) * ucmonb;
+          ucmonc = (d_one + ff2) * ucmonc + (d_one - ff2) * ucmona;
+          vcmonb = (d_one + ff3) * vcmona + (d_one - ff3) * vcmonb;
+          vcmonc = (d_one + ff4) * vcmonc + (d_one - ff4) * vcmona;
+        } else {                    /* centred, upstream_mode = .false. (:152-155, :183-186) */
+          ucmonb = ucmona + ucmonb;
+          ucmonc = ucmonc + ucmona;
+          vcmonb = vcmona + vcmonb;
+          vcmonc = vcmonc + vcmona;
+        }
         A3(o->udyn, j, i, k) = A3(o->udyn, j, i, k) + A3(u, j, i, k) * diag - dm *
             (A3(u, j + 1, i, k) * ucmonb - A3(u, j - 1, i, k) * ucmonc + A3(u, j, i + 1, k) * vcmonb - A3(u, j, i - 1, k) * vcmonc);
         A3(o->vdyn, j, i, k) = A3(o->vdyn, j, i, k) + A3(v, j, i, k) * diag - dm *
@@ -2186,6 +2207,12 @@ static void nh_hadv3d_w(orc_t* o, const double* f, double* ften) {
         double fx2 = (d_one + f1) * A3(f, j, i, k) + (d_one - f1) * A3(f, j + 1, i, k);
         double fy1 = (d_one + f2) * A3(f, j, i - 1, k) + (d_one - f2) * A3(f, j, i, k);
         double fy2 = (d_one + f2) * A3(f, j, i, k) + (d_one - f2) * A3(f, j, i + 1, k);
+        if (!o->cfg.upstream_mode) {  /* centred (:323-332, :414-423, :443-446, :533-542, :625-634) */
+          fx1 = A3(f, j - 1, i, k) + A3(f, j, i, k);
+          fx2 = A3(f, j, i, k) + A3(f, j + 1, i, k);
+          fy1 = A3(f, j, i - 1, k) + A3(f, j, i, k);
+          fy2 = A3(f, j, i, k) + A3(f, j, i + 1, k);
+        }
         A3(ften, j, i, k) = A3(ften, j, i, k) - A2(o->xmsf, j, i) * (uaz2 * fx2 - uaz1 * fx1 + vaz2 * fy2 - vaz1 * fy1);
       }
 }

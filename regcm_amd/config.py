@@ -153,7 +153,7 @@ class RunConfig:
     nspgx: Optional[int] = None
     nspgd: Optional[int] = None
     diffu_hgtf: int = 1
-    upstream_mode: int = 1           # dynparam; .false. (centred advection) is refused
+    upstream_mode: int = 1           # dynparam; 0 = .false. (centred advection)
     gnu1: float = 0.0625
     gnu2: float = 0.0625
     uoffc: float = 0.25

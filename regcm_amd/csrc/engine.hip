@@ -346,7 +346,12 @@ struct rcmdyn_engine {
       c.qcon[k] = (c.sigma[k] - c.hsigma[k]) / (c.hsigma[k - 1] - c.hsigma[k]);
     }
     for (int k = 1; k <= kz; k++) c.xds[k] = 1.0 / c.dsigma[k];  // Main/mod_advection.F90:100
-    c.ul = cfg.uoffc * 0.5 * cfg.dtsec / c.dx;                       // :106 (init dt)
+    // :106 (init dt).  upstream_mode = .false. selects the centred branches of hadvuv, hadvt,
+    // hadv3d, hadvqv, hadvqx (Main/mod_advection.F90:141-201, 322-335, 409-460, 532-545,
+    // 624-637): each is the upstream expression with ul = 0, term for term -- (1 + 0) a +
+    // (1 - 0) b evaluates to exactly a + b, f1 = f2 = ff1..ff4 = +-0 -- so ul = 0 is the
+    // centred scheme bit for bit
+    c.ul = cfg.upstream_mode ? cfg.uoffc * 0.5 * cfg.dtsec / c.dx : 0.0;
     c.xkhmax = c.dxsq / (64.0 * cfg.dtsec);                          // Main/mod_diffusion.F90:104
     c.dydc = cfg.adyndif * VONKAR * VONKAR * c.dx * 0.25;
     c.diff6 = 0.12 * 0.015625 / (2.0 * cfg.dtsec);                    // Main/mod_diffusion.F90:78, 154
@@ -611,10 +616,10 @@ struct rcmdyn_engine {
     if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
     if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
       throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
-    // dynparam's upstream_mode (default .true., Main/mod_params.F90:646): the centred
-    // advection branches (Main/mod_advection.F90:141,322,409,532,624,682) are not built
-    if (cfg.upstream_mode != 1)
-      throw std::runtime_error("rcmdyn: upstream_mode = .false. (centred advection) is not supported");
+    // dynparam's upstream_mode (default .true., Main/mod_params.F90:646); .false. runs the
+    // centred branches (Main/mod_advection.F90:141,322,409,532,624; see c.ul)
+    if (cfg.upstream_mode != 0 && cfg.upstream_mode != 1)
+      throw std::runtime_error("rcmdyn: upstream_mode must be 0 or 1");
     if (cfg.stability_enhance != 0 && cfg.stability_enhance != 1)
       throw std::runtime_error("rcmdyn: stability_enhance must be 0 or 1");
     if (cfg.kz < 2 || cfg.kz > MAXKZ) throw std::runtime_error("rcmdyn: kz out of range");

@@ -106,7 +106,7 @@ def test_create_without_gpu_fails_loudly():
         dycore.DynCore(rc, data["split"])
 
 
-@pytest.mark.parametrize("opt,msg", [({"upstream_mode": 0}, "upstream_mode"),
+@pytest.mark.parametrize("opt,msg", [({"upstream_mode": 2}, "upstream_mode"),
                                      ({"idiffu": 4}, "idiffu"), ({"idiffu": 0}, "idiffu"),
                                      ({"iboudy": 3}, "iboudy"),
                                      ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv")])

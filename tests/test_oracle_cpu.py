@@ -163,7 +163,8 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     base.step(10)
     ref = base.get("ATM1_T")
     refq = base.get("ATM1_QV")
-    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1}):
+    for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
+                    {"upstream_mode": 0}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])
         o.put_state(data["state"])
@@ -1594,3 +1595,31 @@ def test_oracle_idiffu3_column_restatement(c1_data):
     dt2 = ratios.mean()
     assert any(abs(dt2 - x) < 1e-6 * x for x in (rc.dt, 2.0 * rc.dt)), dt2
     assert np.max(np.abs(ratios - dt2)) < 1e-6 * dt2
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_centred_advection_equals_upstream_without_offcentring(core, c1_data):
+    """upstream_mode = .false. (the centred branches of Main/mod_advection.F90:141-201, 322-335,
+    409-460, 532-545, 624-637, restated as written in the oracle) is bit for bit the upstream
+    form with uoffc = 0: the identity the engine's centred mode (ul = 0) rests on."""
+    import dataclasses
+    from oracle.oracle import OracleCore
+    from regcm_amd.config import CONFIGS, NH_STATE_FIELDS, STATE_FIELDS
+    from regcm_amd import icbc
+    if core == "hydrostatic":
+        rc, data = c1_data
+        names = STATE_FIELDS
+    else:
+        rc = CONFIGS["N1"]
+        data = icbc.generate_nh(rc)
+        names = list(STATE_FIELDS) + list(NH_STATE_FIELDS)
+    runs = []
+    for kw in ({"upstream_mode": 0}, {"uoffc": 0.0}, {}):
+        o = OracleCore(dataclasses.replace(rc, **kw), data["split"])
+        o.put_state(data["state"])
+        o.bdyval()
+        o.step(4)
+        runs.append({n: o.get(n) for n in names})
+    for n in names:
+        assert np.array_equal(runs[0][n], runs[1][n]), n
+    assert any(not np.array_equal(runs[0][n], runs[2][n]) for n in names)
