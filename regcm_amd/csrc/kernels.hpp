@@ -20,9 +20,15 @@ constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level)
-constexpr int MBJ = 64, MBI = 8, MBT = MBJ * MBI;
+#ifndef RCM_MBI
+#define RCM_MBI 8
+#endif
+constexpr int MBJ = 64, MBI = RCM_MBI, MBT = MBJ * MBI;
 // LDS-tiled scalar (t, qv, qc) block (cross points j x i at one level)
-constexpr int SBJ = 64, SBI = 8, SBT = SBJ * SBI;
+#ifndef RCM_SBI
+#define RCM_SBI 8
+#endif
+constexpr int SBJ = 64, SBI = RCM_SBI, SBT = SBJ * SBI;
 struct SegList {
   Seg s[MAXSEG];
   int n;
