@@ -104,6 +104,15 @@ def test_nonhydrostatic_plans_match(name, nranks, nsteps):
     assert ncoll >= 2          # the day-alarm sums and the step-flag reduction
 
 
+@pytest.mark.parametrize("variant", [{"idiffu": 3}, {"idiffu": 3, "ibltyp": 2}, {"upstream_mode": 0}],
+                         ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
+def test_nonhydrostatic_variant_plans_match(variant):
+    """NH variants with other exchange widths (idiffu = 3: atm2 3 wide, p*b 4 wide)."""
+    rc = dataclasses.replace(CONFIGS["N1"], **variant)
+    data = icbc.generate_nh(CONFIGS["N1"])
+    check_plans(plans(rc, data["split"], 2, 2, 2), 2, 2)
+
+
 def test_c5_eight_rank_plan_matches():
     """C5 on 2 x 4 tiles (BASELINE's 8-GPU NH configuration).  The plan depends on the split
     constants only through spinit (sigma, ptop, kz, dt, nsplit: N2's are C5's) and istep."""
