@@ -67,6 +67,8 @@ def main():
         wb = w * 1024.0 * (rw or 1.0)
         res["kernels"][k] = {"read_bytes_per_launch": rb, "write_bytes_per_launch": wb,
                              "hbm_bytes_per_launch": rb + wb, "counters": extra.get(k, {})}
+    if not res["kernels"] or rf is None or rw is None:
+        sys.exit(f"pmc_summary: no counter data under {base}; nothing written")
     out = os.path.join(ROOT, "profiles", "pmc_traffic.json" if cfg == "C3" else f"pmc_traffic_{cfg}.json")
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1, sort_keys=True)
