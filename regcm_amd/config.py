@@ -168,6 +168,7 @@ class RunConfig:
     bdy_dm: float = -1.0
     ibdyfrq: int = 6
     present_qc: int = 0
+    stability_enhance: int = 1       # dynparam (Main/mod_params.F90:646); 0 drops the extrema limiters
     name: str = ""
     idynamic: int = 1
     ifupr: int = 1
@@ -244,7 +245,7 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.nspgx, c.nspgd = rc.nspgx, rc.nspgd
     c.diffu_hgtf = rc.diffu_hgtf
     c.upstream_mode = rc.upstream_mode
-    c.stability_enhance = 1
+    c.stability_enhance = rc.stability_enhance
     c.present_qc = rc.present_qc
     c.ds, c.dtsec, c.ptop = rc.ds, rc.dt, rc.ptop
     c.gnu1, c.gnu2, c.uoffc = rc.gnu1, rc.gnu2, rc.uoffc

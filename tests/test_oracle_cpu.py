@@ -164,7 +164,7 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     ref = base.get("ATM1_T")
     refq = base.get("ATM1_QV")
     for variant in ({"iboudy": 4}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
-                    {"upstream_mode": 0}):
+                    {"upstream_mode": 0}, {"stability_enhance": 0}, {"diffu_hgtf": 0}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])
         o.put_state(data["state"])
