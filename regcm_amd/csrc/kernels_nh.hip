@@ -235,8 +235,7 @@ __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f) {
   const int i = g.ide1 + (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
   const int q = (int)blockIdx.z, kz = c->kz;
   const double* ps = f.psb;
-  double* d6 = const_cast<double*>(q == 0 ? f.d6u : q == 1 ? f.d6t : q == 2 ? f.d6qv : q == 3 ? f.d6qc
-                                                   : q == 4 ? f.d6pp : f.d6w);
+  double* d6 = q == 0 ? f.d6u : q == 1 ? f.d6t : q == 2 ? f.d6qv : q == 3 ? f.d6qc : q == 4 ? f.d6pp : f.d6w;
   if (k > (q == 5 ? kz + 1 : kz)) return;
   if (q == 0) {
     const int j = g.jdi2;
@@ -246,7 +245,7 @@ __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f) {
     auto vv = [&](int jj, int ii) { return F3(f.a2v, jj, ii, k) * rd(jj, ii) / F2(f.msfd, jj, ii); };
     const double xkd = c->diff6 * psc2psd_global(g, ps, j, i);
     F3(d6, j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, uu, uu);
-    F3(const_cast<double*>(f.d6v), j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, vv, vv);
+    F3(f.d6v, j, i, k) = xkd * diffu6_bracket(j, i, g.gjx, g.giy, vv, vv);
     return;
   }
   const int j = g.jci2;

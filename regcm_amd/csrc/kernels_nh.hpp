@@ -35,7 +35,7 @@ struct NHFields {
   // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv; null otherwise)
   const double *slqv, *slqc;
   // idiffu = 3: the column terms of k_nh_diffu6 (u, v, t, qv, qc, pp, w; null otherwise)
-  const double *d6u, *d6v, *d6t, *d6qv, *d6qc, *d6pp, *d6w;
+  double *d6u, *d6v, *d6t, *d6qv, *d6qc, *d6pp, *d6w;
   // iuwvadv = 1 (ibltyp = 2): the PBL-top level of vadv4d ind = 3 (null otherwise)
   const double* kpbl;
   // forecasts (atmc) and fixed moisture
