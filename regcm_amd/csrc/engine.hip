@@ -502,10 +502,15 @@ struct rcmdyn_engine {
     std::vector<int8_t> rg;
     std::vector<int16_t> ib;
     if (dry) return;
+    // iboudy = 3 (inflow/outflow) relaxes nothing (Main/mod_tendency.F90:1434-1510): an empty
+    // band turns every nudging and sponge branch of the kernels off
+    const bool band = cfg.iboudy != 3;
     setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgx, false, rg, ib);
+    if (!band) std::fill(rg.begin(), rg.end(), (int8_t)0);
     HIPCHK(hipMemcpy(t.rgcr, rg.data(), P, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(t.ibcr, ib.data(), P * 2, hipMemcpyHostToDevice));
     setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgd, true, rg, ib);
+    if (!band) std::fill(rg.begin(), rg.end(), (int8_t)0);
     HIPCHK(hipMemcpy(t.rgdt, rg.data(), P, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(t.ibdt, ib.data(), P * 2, hipMemcpyHostToDevice));
   }
@@ -614,8 +619,8 @@ struct rcmdyn_engine {
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
-    if (cfg.iboudy != 5 && cfg.iboudy != 1 && cfg.iboudy != 4)
-      throw std::runtime_error("rcmdyn: iboudy must be 1, 4 or 5");
+    if (cfg.iboudy < 1 || cfg.iboudy > 5 || cfg.iboudy == 2)
+      throw std::runtime_error("rcmdyn: iboudy must be 1, 3, 4 or 5");
     // dynparam's upstream_mode (default .true., Main/mod_params.F90:646); .false. runs the
     // centred branches (Main/mod_advection.F90:141,322,409,532,624; see c.ul)
     if (cfg.upstream_mode != 0 && cfg.upstream_mode != 1)
@@ -1733,7 +1738,7 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       const int c = t.cur;
-      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
+      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 3 || cfg.iboudy == 4),
               t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()), dflags);
     }
     tke_bdyval();
@@ -2009,7 +2014,7 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       const int adv = q + 1 == tiles.size() ? (fuse_bdy ? 2 : 1) : 0;
-      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 4),
+      KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 3 || cfg.iboudy == 4),
               t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec, adv, dflags);
     }
     tke_bdyval();

@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void k_sladv(Geom g, const Consts* __restrict_
   if (j > g.jci2 || i > g.ici2) return;
   const uint32_t P8 = g.P8, L8 = g.L8, kof = (uint32_t)(k - 1) * L8;
   (void)P8;
-  const bool ib4 = c->iboudy == 4;
+  const bool ib4 = c->iboudy == 3 || c->iboudy == 4;     // inflow/outflow boundary winds
   auto ua = [&](int jj, int ii) {
     const uint32_t q2 = g.o2(jj, ii);
     double ud;
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
     if (t < TW1 * TH1) {
       const bool ok = aok[n];
       double ud = ok ? au[n] * ar[n] : 0.0, vd = ok ? av[n] * ar[n] : 0.0;
-      if (c->iboudy == 4 && ok) {
+      if ((c->iboudy == 3 || c->iboudy == 4) && ok) {
         const int jg = J0 - 1 + jj, ig = I0 - 1 + ii;
         if (jg == 1 || jg == g.gjx || ig == 1 || ig == g.giy) {
           const double2 bb = udvd_bdy(g, f, jg, ig, kof);

@@ -52,7 +52,7 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
     const double r = F2(rpsda, jj, ii);
     return make_double2(F3(a1u, jj, ii, k) * r, F3(a1v, jj, ii, k) * r);
   };
-  if (iboudy != 4) return base(j, i);
+  if (iboudy != 3 && iboudy != 4) return base(j, i);
   // global boundary lines (a ghost point on them carries the value its owner computes and
   // the reference exchanges)
   auto we = [&](int jj, int ii) {
