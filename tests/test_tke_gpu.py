@@ -66,7 +66,7 @@ def test_tke_init_bdyval_exact(tke_c1):
         assert np.array_equal(e.get(name), o.get(name)), name
 
 
-@pytest.mark.parametrize("variant", [{}, {"idiffu": 2}, {"idiffu": 3}, {"iboudy": 4}, {"upstream_mode": 0}],
+@pytest.mark.parametrize("variant", [{}, {"idiffu": 2}, {"idiffu": 3}, {"iboudy": 4}, {"iboudy": 3}, {"upstream_mode": 0}],
                          ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()) or "default")
 def test_tke_parity(tke_c1, variant):
     rc, data = tke_c1
