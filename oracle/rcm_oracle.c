@@ -1084,7 +1084,7 @@ static void new_pressure(orc_t* o) {
         }
     goto forecast;
   }
-  if (o->cfg.iboudy == 3) goto forecast;        /* inflow/outflow: no p* relaxation (:1434-1438) */
+  if (o->cfg.iboudy == 2 || o->cfg.iboudy == 3) goto forecast;   /* no p* relaxation (:1434-1438) */
   for (int i = o->ice1ga; i <= o->ice2ga; i++)
     for (int j = o->jce1ga; j <= o->jce2ga; j++)
       A3(o->fg1, j, i, 1) = (A2(o->pb0, j, i) + xt * A2(o->pbt, j, i)) - A2(o->psb, j, i);
@@ -1549,7 +1549,7 @@ static void boundary(orc_t* o) {
   int kz = o->kz;
   double xt = o->xbctime + o->dt;
   if (o->cfg.iboudy == 4) { sponge_all(o); return; }
-  if (o->cfg.iboudy == 3) return;               /* inflow/outflow: no relaxation (:1464-1480) */
+  if (o->cfg.iboudy == 2 || o->cfg.iboudy == 3) return;   /* no relaxation (:1464-1480) */
   /* nudge3d(atm2%t, xtb, tdyn), Main/mod_bdycod.F90:4218-4406 */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ice1ga; i <= o->ice2ga; i++)
@@ -2884,7 +2884,7 @@ static int nh_tend(orc_t* o) {
     sponge_all(o);
     nh_sponge3d(o, o->ppbt, o->ppten, kz);
     nh_sponge3d(o, o->wwbt, o->wten, kp);
-  } else if (o->cfg.iboudy != 3) {                /* iboudy = 3: no relaxation (:1494-1500) */
+  } else if (o->cfg.iboudy == 1 || o->cfg.iboudy == 5) {   /* 2, 3: no relaxation (:1494-1500) */
     boundary(o);
     nh_nudge3d(o, o->a2pp, o->ppb0, o->ppbt, o->ppdyn, kz);
     nh_nudge3d(o, o->a2w, o->wwb0, o->wwbt, o->wdyn, kp);

@@ -502,9 +502,9 @@ struct rcmdyn_engine {
     std::vector<int8_t> rg;
     std::vector<int16_t> ib;
     if (dry) return;
-    // iboudy = 3 (inflow/outflow) relaxes nothing (Main/mod_tendency.F90:1434-1510): an empty
-    // band turns every nudging and sponge branch of the kernels off
-    const bool band = cfg.iboudy != 3;
+    // iboudy = 2 (time-dependent) and 3 (inflow/outflow) relax nothing (Main/mod_tendency.F90:
+    // 1434-1510): an empty band turns every nudging and sponge branch of the kernels off
+    const bool band = cfg.iboudy != 2 && cfg.iboudy != 3;
     setup_boundaries(g, cfg.jx, cfg.iy, cfg.nspgx, false, rg, ib);
     if (!band) std::fill(rg.begin(), rg.end(), (int8_t)0);
     HIPCHK(hipMemcpy(t.rgcr, rg.data(), P, hipMemcpyHostToDevice));
@@ -619,8 +619,7 @@ struct rcmdyn_engine {
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
-    if (cfg.iboudy < 1 || cfg.iboudy > 5 || cfg.iboudy == 2)
-      throw std::runtime_error("rcmdyn: iboudy must be 1, 3, 4 or 5");
+    if (cfg.iboudy < 1 || cfg.iboudy > 5) throw std::runtime_error("rcmdyn: iboudy must be 1 to 5");
     // dynparam's upstream_mode (default .true., Main/mod_params.F90:646); .false. runs the
     // centred branches (Main/mod_advection.F90:141,322,409,532,624; see c.ul)
     if (cfg.upstream_mode != 0 && cfg.upstream_mode != 1)

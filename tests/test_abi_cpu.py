@@ -108,7 +108,7 @@ def test_create_without_gpu_fails_loudly():
 
 @pytest.mark.parametrize("opt,msg", [({"upstream_mode": 2}, "upstream_mode"),
                                      ({"idiffu": 4}, "idiffu"), ({"idiffu": 0}, "idiffu"),
-                                     ({"iboudy": 2}, "iboudy"),
+                                     ({"iboudy": 0}, "iboudy"),
                                      ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv")])
 def test_create_refuses_unbuilt_options(opt, msg):
     """A drop-in refuses what it does not compute: option values whose reference branches are

@@ -117,7 +117,7 @@ def test_nh_rest_state():
         assert np.abs(e.get(n)[:, :-1, :-1] / ps).max() < lim, n
 
 
-NH_VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"idiffu": 2}, {"idiffu": 3}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1},
+NH_VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"idiffu": 2}, {"idiffu": 3}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1},
                {"upstream_mode": 0}, {"stability_enhance": 0}]
 # idiffu = 3 depends on the decomposition as the reference's does (test_nh_idiffu3_tiles)
 NH_DECOMP_VARIANTS = [v for v in NH_VARIANTS if v.get("idiffu") != 3]

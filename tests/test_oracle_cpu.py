@@ -163,7 +163,7 @@ def test_oracle_option_variants_change_the_solution(c1_data):
     base.step(10)
     ref = base.get("ATM1_T")
     refq = base.get("ATM1_QV")
-    for variant in ({"iboudy": 4}, {"iboudy": 3}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
+    for variant in ({"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
                     {"upstream_mode": 0}, {"stability_enhance": 0}, {"diffu_hgtf": 0}):
         rcv = dataclasses.replace(rc, **variant)
         o = OracleCore(rcv, data["split"])

@@ -378,7 +378,7 @@ def test_negative_moisture_serial_sweep(c1_data):
 
 
 # namelist options beyond the defaults, each against the oracle and under decomposition
-VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 1}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
+VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"iboudy": 1}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
             {"isladvec": 1, "iqmsl": 0}, {"upstream_mode": 0}, {"stability_enhance": 0}, {"diffu_hgtf": 0}]
 # idiffu = 3 acts on each tile's last interior column, so its result depends on the
 # decomposition as the reference's does (test_idiffu3_tiles_match_oracle_tiles)
