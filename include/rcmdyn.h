@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define RCMDYN_ABI_VERSION 5
+#define RCMDYN_ABI_VERSION 6
 #define RCMDYN_MAXKZ 64
 #define RCMDYN_MAXSPLIT 4
 
@@ -123,6 +123,22 @@ typedef struct rcmdyn_config {
    * KPBL field; ignored unless ibltyp = 2, as in the reference */
   int32_t ibltyp, iuwvadv;
   double nuk, tkemin;
+  /* ABI 6.  physicsparam ipptls [1] and nqx, the number of moisture species param sets from
+   * it (Main/mod_params.F90:1358-1366): nqx = 2 (qv, qc) for ipptls = 1 (SUBEX), nqx = 5 (qv,
+   * qc, qi, qr, qs) for ipptls = 2 (WSM5 / Nogherotto-Tompkins).  Every hydrometeor
+   * n = iqfrst..iqlst (qc and, with nqx = 5, qi, qr, qs) gets the qc chain of the dyn step:
+   * hadvqx, vadv4d, diffu_x4d, the forecast and negative-value fix, filter_raw_4d with the zero
+   * floor, bdyval's boundary copies and inflow/outflow lines; the total water load qcd (the sum
+   * of the hydrometeors, Main/mod_tendency.F90:1107-1115) enters the geopotential's tvfac and
+   * the NH water loading.  ipptls = 0 (no moisture scheme: the hydrometeor tendencies are never
+   * summed, :331) and an nqx that does not match ipptls are refused. */
+  int32_t ipptls, nqx;
+  /* Options of the reference that this engine does not compute; a non-zero value is refused
+   * at rcmdyn_create ('not supported'): i_band = 1 (tropical band, periodic in j) and
+   * i_crm = 1 (cloud-resolving, periodic in j and i), set_nproc's periodic decompositions
+   * (Main/mpplib/mod_mppparam.F90:1062-1063, 1131-1132, 1224-1257); ichem = 1 (chemical tracers
+   * advected, diffused and nudged by tend, Main/mod_tendency.F90:164, 198, 275, 548, 873). */
+  int32_t i_band, i_crm, ichem;
 } rcmdyn_config;
 
 /* Field identifiers for put/get.  3-D fields have k = 1..kz unless noted. */
@@ -189,6 +205,13 @@ enum rcmdyn_field {
    * ('kpbl is greater than kz', Main/mod_advection.F90:923-925); below 4 the column keeps
    * the plain interpolated flux.  Zero until put. */
   RCMDYN_KPBL,
+  /* ABI 6, nqx = 5 only (refused otherwise): the atm1/atm2 ice, rain and snow mixing ratios
+   * qx(:,:,:,iqi|iqr|iqs), coupled with p* like qc; their pc_physic tendencies (put, like the
+   * *PHY fields, :332-335); the mkslice export qxb3d(iqi|iqr|iqs) (get, like ATMS_QCB3D,
+   * Main/mod_slice.F90:193-195) */
+  RCMDYN_ATM1_QI, RCMDYN_ATM1_QR, RCMDYN_ATM1_QS, RCMDYN_ATM2_QI, RCMDYN_ATM2_QR, RCMDYN_ATM2_QS,
+  RCMDYN_QIPHY, RCMDYN_QRPHY, RCMDYN_QSPHY,
+  RCMDYN_ATMS_QXB3D_QI, RCMDYN_ATMS_QXB3D_QR, RCMDYN_ATMS_QXB3D_QS,
   RCMDYN_NFIELDS
 };
 

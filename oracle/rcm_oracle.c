@@ -11,7 +11,8 @@
  *
  * Scope (defaults assumed): idynamic=1, upstream_mode and
  * stability_enhance on, idiffu=1, iboudy=5 (or 1), ipgf=0, nsplit from config,
- * nqx=2 (qv,qc), isladvec=0/1, ibltyp=1/2 (iuwvadv 0/1), ichem=0, idiag=0, iboudy time-dependent.
+ * nqx = 2 (qv, qc) or 5 (qv, qc, qi, qr, qs: ipptls >= 2, Main/mod_params.F90:1358-1366),
+ * isladvec=0/1, ibltyp=1/2 (iuwvadv 0/1), ichem=0, idiag=0, iboudy time-dependent.
  *
  * Parity unpinned: no execution of the reference is available (netCDF-Fortran absent),
  * no golden vectors exist in the reference tree.
@@ -59,6 +60,7 @@ static void init_constants(void) {
   c_pgfaa1 = ALAM * c_rgas * c_regrav;       /* :362 */
 }
 
+#define NQ 5   /* moisture species at most: qv, qc, qi, qr, qs (iqv = 0 .. iqs = 4 here) */
 #define GO 4   /* frame ghost width (covers ga/gb/gc halos and the isladvec = 1 exchange, 4 wide) */
 
 struct orc {
@@ -91,20 +93,21 @@ struct orc {
   signed char *rg_cr, *rg_dt;
   int *ib_cr, *ib_dt;
   /* state */
-  double *a1u, *a1v, *a1t, *a1q[2], *a2u, *a2v, *a2t, *a2q[2];
+  double *a1u, *a1v, *a1t, *a1q[NQ], *a2u, *a2v, *a2t, *a2q[NQ];
   double *psa, *psb, *psc, *psdota, *psdotb, *dstor, *hstor;
   double *msfx, *msfd, *xmsf, *dmsf, *coriol, *ht, *hgfact, *map;
   double *ub0, *ubt, *vb0, *vbt, *tb0, *tbt, *qb0, *qbt, *pb0, *pbt;
   /* work */
   double *rpsa, *rpsb, *rpsc, *rpsda, *srpsb, *rpsdotb;
-  double *uc, *vc, *umc, *vmc, *ud, *vd, *xt, *xq[2], *xtv;
+  double *uc, *vc, *umc, *vmc, *ud, *vd, *xt, *xq[NQ], *xtv;
+  double *qcd;                              /* nqx = 5: the total water load (decouple :1107-1115) */
   double *cr, *pten, *qdot, *omega, *dummy;
-  double *ubd, *vbd, *tb3d, *qb3d[2], *pb3d, *pf3d;
+  double *ubd, *vbd, *tb3d, *qb3d[NQ], *pb3d, *pf3d;
   double *xkc, *xkd;
-  double *tten, *tdyn, *uten, *udyn, *vten, *vdyn, *qten[2], *qdyn[2];
+  double *tten, *tdyn, *uten, *udyn, *vten, *vdyn, *qten[NQ], *qdyn[NQ];
   double *fg, *uavg1, *uavg2, *vavg1, *vavg2, *dotqdot;
   double *fg1, *fg2;
-  double *ct, *cq[2], *cu, *cv;
+  double *ct, *cq[NQ], *cu, *cv;
   double *td, *tvfac, *phi;
   double *deld, *delh, *ddsum, *dhsum, *xdelh, *work, *uu, *vv, *uuu, *vvv;
   /* boundary slices (Main/mod_bdycod.F90:58-61): indexed by frame j or i, then k */
@@ -127,6 +130,7 @@ struct orc {
   /* physics coupling seam: pc_physic tendencies t, qv, qc, u, v, pp, w and the atms export
    * (rcmdyn_field TPHY.. and ATMS_UBX3D.. order) */
   double *phy[7], *atms[22];
+  double *phyx[3], *atmsx[3];               /* nqx = 5: qi, qr, qs pc_physic tendencies, qxb3d export */
   /* UW PBL TKE (ibltyp = 2): atm1/atm2 tke, atmc%tke, tkedyn, tkeps, the pc_physic tendency */
   double *a1tke, *a2tke, *ctke, *tkedyn, *tkeps, *tkephy;
   double* kpbl;      /* ibltyp = 2: the UW scheme's PBL-top level (put; iuwvadv = 1 reads it) */
@@ -248,11 +252,14 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   /* a non-hydrostatic tile of a decomposition needs the whole-domain gather of sound's upper
    * radiative condition (Main/mod_sound.F90:496-497): orc_set_gather, before the first step */
   if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
+  /* nqx from ipptls >= 1 (Main/mod_params.F90:1358-1366); band, CRM, chemistry not restated */
+  if (cfg->ipptls < 1 || cfg->nqx != (cfg->ipptls > 1 ? 5 : 2) || cfg->i_band || cfg->i_crm || cfg->ichem)
+    return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
   o->sound_probe = -1;
   o->cfg = *cfg;
   o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
-  o->nsplit = cfg->nsplit; o->nqx = 2;
+  o->nsplit = cfg->nsplit; o->nqx = cfg->nqx;
   int ext[8], bdy[4];
   tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy);
   o->bl = bdy[0]; o->br = bdy[1]; o->bb = bdy[2]; o->bt = bdy[3];
@@ -350,10 +357,14 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   setup_boundaries(o, 1, o->rg_dt, o->ib_dt);
   o->a1u = alloc3(o, kz); o->a1v = alloc3(o, kz); o->a1t = alloc3(o, kz);
   o->a2u = alloc3(o, kz); o->a2v = alloc3(o, kz); o->a2t = alloc3(o, kz);
-  for (int n = 0; n < 2; n++) {
+  for (int n = 0; n < o->nqx; n++) {
     o->a1q[n] = alloc3(o, kz); o->a2q[n] = alloc3(o, kz); o->xq[n] = alloc3(o, kz);
     o->qb3d[n] = alloc3(o, kz); o->qten[n] = alloc3(o, kz); o->qdyn[n] = alloc3(o, kz);
     o->cq[n] = alloc3(o, kz);
+  }
+  if (o->nqx > 2) {
+    o->qcd = alloc3(o, kz);
+    for (int q = 0; q < 3; q++) { o->phyx[q] = alloc3(o, kz); o->atmsx[q] = alloc3(o, kz); }
   }
   o->psa = alloc3(o, 1); o->psb = alloc3(o, 1); o->psc = alloc3(o, 1);
   o->psdota = alloc3(o, 1); o->psdotb = alloc3(o, 1);
@@ -463,10 +474,12 @@ void orc_destroy(orc_t* o) {
   for (int q = 0; q < 7; q++) { free(o->bin[q]); free(o->bb1[q]); }
   free(o->psdot0);
   free(o->s_tr);
-  for (int n = 0; n < 2; n++) {
+  for (int n = 0; n < NQ; n++) {
     free(o->a1q[n]); free(o->a2q[n]); free(o->xq[n]); free(o->qb3d[n]);
     free(o->qten[n]); free(o->qdyn[n]); free(o->cq[n]);
   }
+  free(o->qcd);
+  for (int q = 0; q < 3; q++) { free(o->phyx[q]); free(o->atmsx[q]); }
   free(o->rg_cr); free(o->rg_dt); free(o->ib_cr); free(o->ib_dt);
   free(o);
 }
@@ -518,6 +531,13 @@ static double* field_ptr(orc_t* o, int f, int* nk) {
     return f == RCMDYN_ATM1_TKE ? o->a1tke : f == RCMDYN_ATM2_TKE ? o->a2tke : o->tkephy;
   }
   if (f == RCMDYN_KPBL) { *nk = 1; return o->kpbl; }
+  if (f >= RCMDYN_ATM1_QI && f <= RCMDYN_ATMS_QXB3D_QS) {     /* nqx = 5 only */
+    if (o->nqx < 5) return NULL;
+    if (f <= RCMDYN_ATM1_QS) return o->a1q[2 + f - RCMDYN_ATM1_QI];
+    if (f <= RCMDYN_ATM2_QS) return o->a2q[2 + f - RCMDYN_ATM2_QI];
+    if (f <= RCMDYN_QSPHY) return o->phyx[f - RCMDYN_QIPHY];
+    return o->atmsx[f - RCMDYN_ATMS_QXB3D_QI];
+  }
   switch (f) {
     case RCMDYN_ATM1_U: return o->a1u;   case RCMDYN_ATM1_V: return o->a1v;
     case RCMDYN_ATM1_T: return o->a1t;   case RCMDYN_ATM1_QV: return o->a1q[0];
@@ -609,6 +629,13 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
   else if (o->nh && !strcmp(name, "rho1")) a = o->rho1;
   else if (!strcmp(name, "cqv")) a = o->cq[0];
   else if (!strcmp(name, "cqc")) a = o->cq[1];
+  else if (o->nqx > 2 && !strcmp(name, "cqi")) a = o->cq[2];
+  else if (o->nqx > 2 && !strcmp(name, "cqr")) a = o->cq[3];
+  else if (o->nqx > 2 && !strcmp(name, "cqs")) a = o->cq[4];
+  else if (o->nqx > 2 && !strcmp(name, "qcd")) a = o->qcd;
+  else if (o->nqx > 2 && !strcmp(name, "qteni")) a = o->qten[2];   /* the total tendencies (sums) */
+  else if (o->nqx > 2 && !strcmp(name, "qtenr")) a = o->qten[3];
+  else if (o->nqx > 2 && !strcmp(name, "qtens")) a = o->qten[4];
   if (!a || cap < o->plane * (size_t)nk) return 0;
   memcpy(dst, a, sizeof(double) * o->plane * (size_t)nk);
   return nk;
@@ -758,7 +785,7 @@ static void decouple(orc_t* o) {
   for (int i = o->ide1ga; i <= o->ide2ga; i++)
     for (int j = o->jde1ga; j <= o->jde2ga; j++) A2(o->rpsda, j, i) = d_one / A2(o->psdota, j, i);
   xch(o, o->a1u, kz, 1, 0); xch(o, o->a1v, kz, 1, 0); xch(o, o->a1t, kz, 1, 0);
-  xch(o, o->a1q[0], kz, 1, 0); xch(o, o->a1q[1], kz, 1, 0);
+  for (int n = 0; n < o->nqx; n++) xch(o, o->a1q[n], kz, 1, 0);
   for (int k = 1; k <= kz; k++)                                   /* :879-884 */
     for (int i = o->ide1ga; i <= o->ide2ga; i++)
       for (int j = o->jde1ga; j <= o->jde2ga; j++) {
@@ -860,7 +887,8 @@ static void decouple(orc_t* o) {
         double rp = A2(o->rpsa, j, i);
         A3(o->xt, j, i, k) = A3(o->a1t, j, i, k) * rp;
         A3(o->xq[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) * rp, MINQQ);
-        A3(o->xq[1], j, i, k) = dmax(A3(o->a1q[1], j, i, k) * rp, d_zero);
+        for (int n = 1; n < o->nqx; n++)                          /* n = iqfrst .. iqlst */
+          A3(o->xq[n], j, i, k) = dmax(A3(o->a1q[n], j, i, k) * rp, d_zero);
         A3(o->xtv, j, i, k) = A3(o->xt, j, i, k) * (d_one + c_ep1 * A3(o->xq[0], j, i, k));
       }
   /* atm1%pr/rho (:1037-1040) and atm2%pr (:1094-1096) feed only physics: skipped */
@@ -870,9 +898,19 @@ static void decouple(orc_t* o) {
   }
   {                                                              /* :1073-1077 */
     int w = o->cfg.isladvec == 1 ? 4 : idw(o);                    /* max(idif, 4) */
-    xch(o, o->a2q[0], kz, w, 0); xch(o, o->a2q[1], kz, w, 0);
+    for (int n = 0; n < o->nqx; n++) xch(o, o->a2q[n], kz, w, 0);
+  }
+  if (o->nqx > 2) {                                              /* total water load, :1107-1115 */
+    memset(o->qcd, 0, sizeof(double) * o->plane * kz);
+    for (int n = 1; n < o->nqx; n++)
+      for (int k = 1; k <= kz; k++)
+        for (int i = o->ice1; i <= o->ice2; i++)
+          for (int j = o->jce1; j <= o->jce2; j++) A3(o->qcd, j, i, k) = A3(o->qcd, j, i, k) + A3(o->xq[n], j, i, k);
   }
 }
+/* qcd of decouple: the total hydrometeor load for nqx = 5, else an alias of atmx%qx(iqc)
+ * (Main/mod_tendency.F90:117-121) */
+static const double* qcd_of(const orc_t* o) { return o->nqx > 2 ? o->qcd : o->xq[1]; }
 
 /* compute_omega, Main/mod_tendency.F90:1118-1215 (hydrostatic) */
 static void compute_omega(orc_t* o) {
@@ -936,7 +974,7 @@ static void mkslice(orc_t* o) {
         double rp = A2(o->srpsb, j, i);
         A3(o->tb3d, j, i, k) = A3(o->a2t, j, i, k) * rp;
         A3(o->qb3d[0], j, i, k) = dmax(A3(o->a2q[0], j, i, k) * rp, MINQQ);
-        A3(o->qb3d[1], j, i, k) = dmax(A3(o->a2q[1], j, i, k) * rp, d_zero);
+        for (int n = 1; n < o->nqx; n++) A3(o->qb3d[n], j, i, k) = dmax(A3(o->a2q[n], j, i, k) * rp, d_zero);
       }
   for (int k = 1; k <= kz; k++)
     for (int i = o->ice1; i <= o->ice2; i++)
@@ -998,6 +1036,7 @@ static void slice_export(orc_t* o) {
         A3(s[S_QCB], j, i, k) = qc;
         A3(s[S_TV], j, i, k) = tb * (d_one + c_ep1 * qv - qc);
         A3(s[S_PB], j, i, k) = A3(o->pb3d, j, i, k);
+        for (int n = 2; n < o->nqx; n++) A3(o->atmsx[n - 2], j, i, k) = A3(o->qb3d[n], j, i, k);
       }
   for (int k = 1; k <= kp; k++)                                    /* :215-234 */
     for (int i = o->ice1; i <= o->ice2; i++)
@@ -1353,8 +1392,8 @@ static void vadv4d_qc_uw(orc_t* o, const double* f) {
       for (int j = o->jci1; j <= o->jci2; j++) A3(o->fg, j, i, k) = A3(o->fg, j, i, k) * A3(o->qdot, j, i, k);
 }
 
-static void vadv4d_qc(orc_t* o) {                          /* :859-961, ind = 1 (or 3: iuwvadv) */
-  const double* f = o->a1q[1];
+static void vadv4d_qx(orc_t* o, int n) {      /* :859-961, ind = 1 (or 3: iuwvadv), one hydrometeor */
+  const double* f = o->a1q[n];
   memset(o->fg, 0, sizeof(double) * o->plane * o->kz);
   if (o->cfg.ibltyp == 2 && o->cfg.iuwvadv == 1) vadv4d_qc_uw(o, f);
   else
@@ -1373,7 +1412,7 @@ static void vadv4d_qc(orc_t* o) {                          /* :859-961, ind = 1 
   for (int i = o->ici1; i <= o->ici2; i++)
     for (int j = o->jci1; j <= o->jci2; j++)
       for (int k = 2; k <= o->kz; k++) {
-        double* t = o->qdyn[1];
+        double* t = o->qdyn[n];
         A3(t, j, i, k - 1) = A3(t, j, i, k - 1) - A3(o->fg, j, i, k) * o->xds[k - 1];
         A3(t, j, i, k) = A3(t, j, i, k) + A3(o->fg, j, i, k) * o->xds[k];
       }
@@ -1441,7 +1480,7 @@ static int sl_advection(orc_t* o) {
         double ducapdx = (ucapf - ucapi) / o->dx;
         double dvcapdy = (vcapf - vcapi) / o->dx;
         double hdvg = (ducapdx + dvcapdy) / (A2(o->msfx, j, i) * A2(o->msfx, j, i));
-        for (int n = 0; n < 2; n++) {
+        for (int n = 0; n < o->nqx; n++) {
           const double* var = o->a2q[n];
 #define V(J, I) A3(var, J, I, k)
           double bl1 = alfax * V(xm1, yp1) + (d_one - alfax) * V(xnd, yp1);
@@ -1477,16 +1516,17 @@ static int advection(orc_t* o) {
   hadv_scalar(o, o->xt, o->tdyn, 1);      /* hadvt */
   vadv3d_t(o);
   if (o->cfg.isladvec == 1) {
-    /* slhadv_x / hdvg_x of qv and qc (:1361-1363, 1378-1380); the reference runs the qv
-     * pass, then vadv of qv, then the qc pass: the passes touch disjoint qxdyn planes */
+    /* slhadv_x / hdvg_x of qv and the hydrometeors (:1361-1363, 1378-1380); the reference runs
+     * the qv pass, then vadv of qv, then the qx pass: the passes touch disjoint qxdyn planes */
     bad = sl_advection(o);
     vadvqv(o);
   } else {
     hadv_scalar(o, o->xq[0], o->qdyn[0], 2); /* hadvqv */
     vadvqv(o);                               /* all(icup /= 1) */
-    hadv_scalar(o, o->xq[1], o->qdyn[1], 0); /* hadvqx */
+    for (int n = 1; n < o->nqx; n++)         /* hadvqx, n = iqfrst .. iqlst (:1382) */
+      hadv_scalar(o, o->xq[n], o->qdyn[n], 0);
   }
-  vadv4d_qc(o);
+  for (int n = 1; n < o->nqx; n++) vadv4d_qx(o, n);   /* vadv iqfrst .. iqlst (:1388) */
   return bad;
 }
 
@@ -1742,7 +1782,7 @@ static void pressure_gradient_force(orc_t* o) {
   for (int k = 1; k <= kz; k++)
     for (int i = o->ice1; i <= o->ice2; i++)
       for (int j = o->jce1; j <= o->jce2; j++)
-        A3(o->tvfac, j, i, k) = d_one / (d_one + A3(o->xq[1], j, i, k) / (d_one + A3(o->xq[0], j, i, k)));
+        A3(o->tvfac, j, i, k) = d_one / (d_one + A3(qcd_of(o), j, i, k) / (d_one + A3(o->xq[0], j, i, k)));
   for (int i = o->ice1; i <= o->ice2; i++)
     for (int j = o->jce1; j <= o->jce2; j++) {
       double rp = A2(o->rpsa, j, i);
@@ -2277,9 +2317,9 @@ static int nh_advection(orc_t* o) {
   } else {
     hadv_scalar(o, o->xq[0], o->qdyn[0], 2);
     vadvqv(o);
-    hadv_scalar(o, o->xq[1], o->qdyn[1], 0);
+    for (int n = 1; n < o->nqx; n++) hadv_scalar(o, o->xq[n], o->qdyn[n], 0);
   }
-  vadv4d_qc(o);
+  for (int n = 1; n < o->nqx; n++) vadv4d_qx(o, n);
   return bad;
 }
 
@@ -2316,7 +2356,7 @@ static void nh_adiabatic(orc_t* o) {
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
         A3(o->ppdyn, j, i, k) = A3(o->ppdyn, j, i, k) + A3(o->xpp, j, i, k) * A3(o->cr, j, i, k);
-  for (int n = 0; n < 2; n++)
+  for (int n = 0; n < o->nqx; n++)              /* :1615-1617, n = 1 .. nqx */
     for (int k = 1; k <= kz; k++)
       for (int i = o->ici1; i <= o->ici2; i++)
         for (int j = o->jci1; j <= o->jci2; j++)
@@ -2340,11 +2380,12 @@ static void nh_adiabatic(orc_t* o) {
             (uaq * uaq + vaq * vaq) * NH_REARTHRAD * A2(o->rpsa, j, i) +
             A3(o->xw, j, i, k) * (o->twt1[k] * A3(o->cr, j, i, k) + o->twt2[k] * A3(o->cr, j, i, k - 1));
       }
-  for (int k = 2; k <= kz; k++)                 /* water loading, qcd = atmx%qx(iqc) */
+  const double* qcd = qcd_of(o);                /* water loading (:1662-1671): qcd, the load */
+  for (int k = 2; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
         A3(o->wdyn, j, i, k) = A3(o->wdyn, j, i, k) - EGRAV * A2(o->psa, j, i) *
-            (o->twt2[k] * A3(o->xq[1], j, i, k - 1) + o->twt1[k] * A3(o->xq[1], j, i, k));
+            (o->twt2[k] * A3(qcd, j, i, k - 1) + o->twt1[k] * A3(qcd, j, i, k));
 }
 
 /* nudge3d on nk levels (Main/mod_bdycod.F90:4218-4406; hefc(ib, min(k,kz)) for kz+1) */
@@ -2829,6 +2870,55 @@ static int nh_sound(orc_t* o) {
   return (cflmax > d_one) ? 1 : 0;
 }
 
+/* The hydrometeors of nqx = 5 beyond qc (qi, qr, qs: n = 2 .. nqx-1 here): their sums
+ * qxten + qxdyn + qxphy (Main/mod_tendency.F90:332-335, n = iqfrst..iqlst; qc's is summed with
+ * t and qv at each core's place) */
+static void qx_sums(orc_t* o) {
+  for (int n = 2; n < o->nqx; n++)
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->qten[n], j, i, k) = A3(o->qten[n], j, i, k) + A3(o->qdyn[n], j, i, k) + A3(o->phyx[n - 2], j, i, k);
+}
+/* forecast of every species, the exchange of atmc%qx and the negative-moisture fix, :375-393 */
+static void qx_forecast_fix(orc_t* o) {
+  int kz = o->kz;
+  for (int n = 0; n < o->nqx; n++) {
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ice1; i <= o->ice2; i++)
+        for (int j = o->jce1; j <= o->jce2; j++) A3(o->cq[n], j, i, k) = A3(o->a2q[n], j, i, k);
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          A3(o->cq[n], j, i, k) = A3(o->cq[n], j, i, k) + o->dt * A3(o->qten[n], j, i, k);
+  }
+  for (int n = 0; n < o->nqx; n++) xch(o, o->cq[n], kz, 1, 0);
+  for (int n = 0; n < o->nqx; n++)
+    for (int k = 1; k <= kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++)
+          if (A3(o->cq[n], j, i, k) < d_zero) {
+            double s = 0.0;
+            for (int ii = i - 1; ii <= i + 1; ii++)
+              for (int jj = j - 1; jj <= j + 1; jj++) s = s + fabs(A3(o->cq[n], jj, ii, k));
+            A3(o->cq[n], j, i, k) = 0.01 * s / 9.0;
+          }
+}
+/* filter_raw_4d of the hydrometeors n = iqfrst..iqlst with the zero floor, :426-427 */
+static void qx_raw_filter(orc_t* o) {
+  double g2 = o->cfg.gnu2, beta = 0.53;
+  for (int n = 1; n < o->nqx; n++)
+    for (int k = 1; k <= o->kz; k++)
+      for (int i = o->ici1; i <= o->ici2; i++)
+        for (int j = o->jci1; j <= o->jci2; j++) {
+          double d = g2 * (A3(o->cq[n], j, i, k) + A3(o->a2q[n], j, i, k) - d_two * A3(o->a1q[n], j, i, k));
+          A3(o->a2q[n], j, i, k) = A3(o->a1q[n], j, i, k) + beta * d;
+          A3(o->a1q[n], j, i, k) = A3(o->cq[n], j, i, k) + (beta - d_one) * d;
+          if (A3(o->a2q[n], j, i, k) < d_zero) A3(o->a2q[n], j, i, k) = d_zero;
+          if (A3(o->a1q[n], j, i, k) < d_zero) A3(o->a1q[n], j, i, k) = d_zero;
+        }
+}
+
 /* tend, non-hydrostatic (Main/mod_tendency.F90:212-616 with idynamic = 2) */
 /* UW PBL TKE in tend (ibltyp = 2), both cores: hadv3d ind = 1 of atm1%tke and vadv3d of
  * tke*p* (Main/mod_tendency.F90:1414-1425, at the end of advection, with its uavg and the
@@ -2872,7 +2962,7 @@ static int nh_tend(orc_t* o) {
   memset(o->tten, 0, n3 * 8); memset(o->tdyn, 0, n3 * 8);
   memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
   memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
-  for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
+  for (int n = 0; n < o->nqx; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
   memset(o->ppten, 0, n3 * 8); memset(o->ppdyn, 0, n3 * 8);
   memset(o->wten, 0, n3p * 8); memset(o->wdyn, 0, n3p * 8);
   int slbad = nh_advection(o);
@@ -2892,8 +2982,7 @@ static int nh_tend(orc_t* o) {
   /* diffusion (:1515-1538) */
   diffu_d(o);
   diffu_x(o, o->tdyn, o->tb3d, d_one);
-  diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
-  diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
+  for (int n = 0; n < o->nqx; n++) diffu_x(o, o->qdyn[n], o->qb3d[n], d_one);   /* diffu_x4d 1..nqx */
   nh_diffu_xk(o, o->ppdyn, o->ppb3d, o->xkc, kz, d_one);
   nh_diffu_xk(o, o->wdyn, o->wb3d, o->xkcf, kp, d_one);
   /* sums (:285-314, 332-335) with the host's pc_physic tendencies (phy, 0 unless put) */
@@ -2913,7 +3002,9 @@ static int nh_tend(orc_t* o) {
         A3(o->ppten, j, i, k) = A3(o->ppten, j, i, k) + A3(o->ppdyn, j, i, k) + A3(o->phy[5], j, i, k);
         A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + A3(o->phy[2], j, i, k);
       }
-  /* condtq (:336-350) is physics: stubbed, tphy = qxphy = 0 */
+  qx_sums(o);
+  /* condtq (:336-350, ipptls = 1 only) is physics: stubbed, tphy = qxphy = 0 */
+  if (o->cfg.ipptls == 1)
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
@@ -2930,26 +3021,7 @@ static int nh_tend(orc_t* o) {
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
         A3(o->ct, j, i, k) = A3(o->a2t, j, i, k) + o->dt * A3(o->tten, j, i, k);
-  for (int n = 0; n < 2; n++) {
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ice1; i <= o->ice2; i++)
-        for (int j = o->jce1; j <= o->jce2; j++) A3(o->cq[n], j, i, k) = A3(o->a2q[n], j, i, k);
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ici1; i <= o->ici2; i++)
-        for (int j = o->jci1; j <= o->jci2; j++)
-          A3(o->cq[n], j, i, k) = A3(o->cq[n], j, i, k) + o->dt * A3(o->qten[n], j, i, k);
-  }
-  xch(o, o->cq[0], kz, 1, 0); xch(o, o->cq[1], kz, 1, 0);
-  for (int n = 0; n < 2; n++)
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ici1; i <= o->ici2; i++)
-        for (int j = o->jci1; j <= o->jci2; j++)
-          if (A3(o->cq[n], j, i, k) < d_zero) {
-            double s = 0.0;
-            for (int ii = i - 1; ii <= i + 1; ii++)
-              for (int jj = j - 1; jj <= j + 1; jj++) s = s + fabs(A3(o->cq[n], jj, ii, k));
-            A3(o->cq[n], j, i, k) = 0.01 * s / 9.0;
-          }
+  qx_forecast_fix(o);
   for (int k = 1; k <= kz; k++)                                     /* :404-411 */
     for (int i = o->idi1; i <= o->idi2; i++)
       for (int j = o->jdi1; j <= o->jdi2; j++) {
@@ -2957,7 +3029,7 @@ static int nh_tend(orc_t* o) {
         A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + A3(o->phy[4], j, i, k);
       }
   /* time filters t, qx (:422-427) */
-  double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;
+  double g1 = o->cfg.gnu1, beta = 0.53;
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
@@ -2972,15 +3044,7 @@ static int nh_tend(orc_t* o) {
         A3(o->a2q[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) + beta * d, MINQQ * A2(o->psa, j, i));
         A3(o->a1q[0], j, i, k) = dmax(A3(o->cq[0], j, i, k) + (beta - d_one) * d, MINQQ * A2(o->psb, j, i));
       }
-  for (int k = 1; k <= kz; k++)
-    for (int i = o->ici1; i <= o->ici2; i++)
-      for (int j = o->jci1; j <= o->jci2; j++) {
-        double d = g2 * (A3(o->cq[1], j, i, k) + A3(o->a2q[1], j, i, k) - d_two * A3(o->a1q[1], j, i, k));
-        A3(o->a2q[1], j, i, k) = A3(o->a1q[1], j, i, k) + beta * d;
-        A3(o->a1q[1], j, i, k) = A3(o->cq[1], j, i, k) + (beta - d_one) * d;
-        if (A3(o->a2q[1], j, i, k) < d_zero) A3(o->a2q[1], j, i, k) = d_zero;
-        if (A3(o->a1q[1], j, i, k) < d_zero) A3(o->a1q[1], j, i, k) = d_zero;
-      }
+  qx_raw_filter(o);                                                 /* filter_raw_4d */
   /* Rayleigh damping of u, v, pp, w and decoupling of the tendencies (:466-499) */
   if (o->cfg.ifrayd == 1) {
     nh_raydamp_uv(o);
@@ -3024,7 +3088,7 @@ int orc_tend(orc_t* o) {
   memset(o->tten, 0, n3 * 8); memset(o->tdyn, 0, n3 * 8);
   memset(o->uten, 0, n3 * 8); memset(o->udyn, 0, n3 * 8);
   memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
-  for (int n = 0; n < 2; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
+  for (int n = 0; n < o->nqx; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
   int slbad = advection(o);
   if (o->cfg.ibltyp == 2) tke_tend(o);
   curvature(o);
@@ -3033,44 +3097,27 @@ int orc_tend(orc_t* o) {
   /* physical_parametrizations: the host's pc_physic tendencies (phy, 0 unless put) */
   diffu_d(o);
   diffu_x(o, o->tdyn, o->tb3d, d_one);
-  diffu_x(o, o->qdyn[0], o->qb3d[0], d_one);
-  diffu_x(o, o->qdyn[1], o->qb3d[1], d_one);
-  /* sums, :285-294 and :332-349 (tphy, qxphy from the host; the SUBEX condtq terms = 0) */
+  for (int n = 0; n < o->nqx; n++) diffu_x(o, o->qdyn[n], o->qb3d[n], d_one);   /* diffu_x4d 1..nqx */
+  /* sums, :285-294 and :332-349 (tphy, qxphy from the host; the SUBEX condtq terms = 0, ipptls = 1) */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++) {
         A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + A3(o->tdyn, j, i, k) + A3(o->phy[0], j, i, k);
         A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + A3(o->qdyn[0], j, i, k) + A3(o->phy[1], j, i, k);
         A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + A3(o->qdyn[1], j, i, k) + A3(o->phy[2], j, i, k);
-        A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + 0.0;
-        A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
-        A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
+        if (o->cfg.ipptls == 1) {
+          A3(o->tten, j, i, k) = A3(o->tten, j, i, k) + 0.0;
+          A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
+          A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
+        }
       }
+  qx_sums(o);
   /* forecast t, qx, :368-393 */
   for (int k = 1; k <= kz; k++)
     for (int i = o->ici1; i <= o->ici2; i++)
       for (int j = o->jci1; j <= o->jci2; j++)
         A3(o->ct, j, i, k) = A3(o->a2t, j, i, k) + o->dt * A3(o->tten, j, i, k);
-  for (int n = 0; n < 2; n++) {
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ice1; i <= o->ice2; i++)
-        for (int j = o->jce1; j <= o->jce2; j++) A3(o->cq[n], j, i, k) = A3(o->a2q[n], j, i, k);
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ici1; i <= o->ici2; i++)
-        for (int j = o->jci1; j <= o->jci2; j++)
-          A3(o->cq[n], j, i, k) = A3(o->cq[n], j, i, k) + o->dt * A3(o->qten[n], j, i, k);
-  }
-  xch(o, o->cq[0], kz, 1, 0); xch(o, o->cq[1], kz, 1, 0);
-  for (int n = 0; n < 2; n++)
-    for (int k = 1; k <= kz; k++)
-      for (int i = o->ici1; i <= o->ici2; i++)
-        for (int j = o->jci1; j <= o->jci2; j++)
-          if (A3(o->cq[n], j, i, k) < d_zero) {
-            double s = 0.0;
-            for (int ii = i - 1; ii <= i + 1; ii++)
-              for (int jj = j - 1; jj <= j + 1; jj++) s = s + fabs(A3(o->cq[n], jj, ii, k));
-            A3(o->cq[n], j, i, k) = 0.01 * s / 9.0;
-          }
+  qx_forecast_fix(o);
   pressure_gradient_force(o);
   for (int k = 1; k <= kz; k++)                                     /* :404-411 */
     for (int i = o->idi1; i <= o->idi2; i++)
@@ -3079,7 +3126,7 @@ int orc_tend(orc_t* o) {
         A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + A3(o->phy[4], j, i, k);
       }
   /* time filters, :419-427, Main/mod_timefilter.F90 */
-  double g1 = o->cfg.gnu1, g2 = o->cfg.gnu2, beta = 0.53;
+  double g1 = o->cfg.gnu1, beta = 0.53;
   for (int i = o->ici1; i <= o->ici2; i++)                          /* filter_ra_2d */
     for (int j = o->jci1; j <= o->jci2; j++) {
       double d = g1 * (A2(o->psc, j, i) + A2(o->psb, j, i) - d_two * A2(o->psa, j, i));
@@ -3100,15 +3147,7 @@ int orc_tend(orc_t* o) {
         A3(o->a2q[0], j, i, k) = dmax(A3(o->a1q[0], j, i, k) + beta * d, MINQQ * A2(o->psa, j, i));
         A3(o->a1q[0], j, i, k) = dmax(A3(o->cq[0], j, i, k) + (beta - d_one) * d, MINQQ * A2(o->psb, j, i));
       }
-  for (int k = 1; k <= kz; k++)                                     /* filter_raw_4d */
-    for (int i = o->ici1; i <= o->ici2; i++)
-      for (int j = o->jci1; j <= o->jci2; j++) {
-        double d = g2 * (A3(o->cq[1], j, i, k) + A3(o->a2q[1], j, i, k) - d_two * A3(o->a1q[1], j, i, k));
-        A3(o->a2q[1], j, i, k) = A3(o->a1q[1], j, i, k) + beta * d;
-        A3(o->a1q[1], j, i, k) = A3(o->cq[1], j, i, k) + (beta - d_one) * d;
-        if (A3(o->a2q[1], j, i, k) < d_zero) A3(o->a2q[1], j, i, k) = d_zero;
-        if (A3(o->a1q[1], j, i, k) < d_zero) A3(o->a1q[1], j, i, k) = d_zero;
-      }
+  qx_raw_filter(o);                                                 /* filter_raw_4d */
   for (int k = 1; k <= kz; k++)                                     /* :433-440 */
     for (int i = o->idi1; i <= o->idi2; i++)
       for (int j = o->jdi1; j <= o->jdi2; j++) {
@@ -3320,7 +3359,7 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
         A3(o->a2u, o->jde1, i, k) = A3(o->a1u, o->jde1, i, k); A3(o->a2v, o->jde1, i, k) = A3(o->a1v, o->jde1, i, k); }
       for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce1, i, k) = A3(o->a1t, o->jce1, i, k);
-      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
+      for (int n = 0; n < o->nqx; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
         A3(o->a2q[n], o->jce1, i, k) = A3(o->a1q[n], o->jce1, i, k);
       if (o->nh) {
         for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2pp, o->jce1, i, k) = A3(o->a1pp, o->jce1, i, k);
@@ -3332,7 +3371,7 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int i = o->idi1; i <= o->idi2; i++) {
         A3(o->a2u, o->jde2, i, k) = A3(o->a1u, o->jde2, i, k); A3(o->a2v, o->jde2, i, k) = A3(o->a1v, o->jde2, i, k); }
       for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2t, o->jce2, i, k) = A3(o->a1t, o->jce2, i, k);
-      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
+      for (int n = 0; n < o->nqx; n++) for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++)
         A3(o->a2q[n], o->jce2, i, k) = A3(o->a1q[n], o->jce2, i, k);
       if (o->nh) {
         for (int k = 1; k <= kz; k++) for (int i = o->ici1; i <= o->ici2; i++) A3(o->a2pp, o->jce2, i, k) = A3(o->a1pp, o->jce2, i, k);
@@ -3344,7 +3383,7 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
         A3(o->a2u, j, o->ide1, k) = A3(o->a1u, j, o->ide1, k); A3(o->a2v, j, o->ide1, k) = A3(o->a1v, j, o->ide1, k); }
       for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice1, k) = A3(o->a1t, j, o->ice1, k);
-      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
+      for (int n = 0; n < o->nqx; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
         A3(o->a2q[n], j, o->ice1, k) = A3(o->a1q[n], j, o->ice1, k);
       if (o->nh) {
         for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2pp, j, o->ice1, k) = A3(o->a1pp, j, o->ice1, k);
@@ -3356,7 +3395,7 @@ void orc_bdyval(orc_t* o) {
       for (int k = 1; k <= kz; k++) for (int j = o->jde1; j <= o->jde2; j++) {
         A3(o->a2u, j, o->ide2, k) = A3(o->a1u, j, o->ide2, k); A3(o->a2v, j, o->ide2, k) = A3(o->a1v, j, o->ide2, k); }
       for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2t, j, o->ice2, k) = A3(o->a1t, j, o->ice2, k);
-      for (int n = 0; n < 2; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
+      for (int n = 0; n < o->nqx; n++) for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++)
         A3(o->a2q[n], j, o->ice2, k) = A3(o->a1q[n], j, o->ice2, k);
       if (o->nh) {
         for (int k = 1; k <= kz; k++) for (int j = o->jce1; j <= o->jce2; j++) A3(o->a2pp, j, o->ice2, k) = A3(o->a1pp, j, o->ice2, k);
@@ -3437,9 +3476,9 @@ void orc_bdyval(orc_t* o) {
       double w = SJ(o->nve, j, k) + SJ(o->nve, j + 1, k) + SJ(o->nvi, j, k) + SJ(o->nvi, j + 1, k);
       A3(q, j, o->ice2, k) = (w < d_zero) ? qext * A2(o->psa, j, o->ice2) : qint * A2(o->psa, j, o->ice2); }
   }
-  /* qc inflow/outflow (not present_qc, bdyflow), :2153-2220 */
-  if (!o->cfg.present_qc) {
-    double* q = o->a1q[1];
+  /* qx inflow/outflow of n = iqfrst .. iqlst (not present_qc, bdyflow), :2153-2220 */
+  if (!o->cfg.present_qc) for (int n = 1; n < o->nqx; n++) {
+    double* q = o->a1q[n];
     if (o->bl) for (int k = 1; k <= kz; k++) for (int i = o->ice1; i <= o->ice2; i++) {
       double qxint = A3(q, o->jci1, i, k) / A2(o->psa, o->jci1, i);
       double w = SI(o->wue, i, k) + SI(o->wue, i + 1, k) + SI(o->wui, i, k) + SI(o->wui, i + 1, k);

@@ -17,7 +17,7 @@ import numpy as np
 
 MAXKZ = 64
 MAXSPLIT = 4
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # Share/mod_sigma.F90:88-152 -- the hard-coded sigma tables (data, cited).
 SIGMA_TABLES = {
@@ -76,6 +76,8 @@ class RcmdynConfig(ctypes.Structure):
         ("isladvec", ctypes.c_int32), ("iqmsl", ctypes.c_int32),
         ("ibltyp", ctypes.c_int32), ("iuwvadv", ctypes.c_int32),
         ("nuk", ctypes.c_double), ("tkemin", ctypes.c_double),
+        ("ipptls", ctypes.c_int32), ("nqx", ctypes.c_int32),
+        ("i_band", ctypes.c_int32), ("i_crm", ctypes.c_int32), ("ichem", ctypes.c_int32),
     ]
 
 
@@ -98,6 +100,8 @@ FIELD_NAMES = [
     "ATMS_TP3D", "ATMS_WPX3D", "ATMS_WB3D", "ATMS_ZQ", "ATMS_ZA", "ATMS_DZQ", "ATMS_QSB3D", "ATMS_RHB3D",
     "XUB_B1", "XVB_B1", "XTB_B1", "XQB_B1", "XPSB_B1", "XPPB_B1", "XWWB_B1", "ATM0_PSDOT",
     "ATM1_TKE", "ATM2_TKE", "TKEPHY", "KPBL",
+    "ATM1_QI", "ATM1_QR", "ATM1_QS", "ATM2_QI", "ATM2_QR", "ATM2_QS",
+    "QIPHY", "QRPHY", "QSPHY", "ATMS_QXB3D_QI", "ATMS_QXB3D_QR", "ATMS_QXB3D_QS",
 ]
 FIELD = {n: i for i, n in enumerate(FIELD_NAMES)}
 TWO_D = {"PSA", "PSB", "MSFX", "MSFD", "CORIOL", "HT", "XPSB_B0", "XPSB_BT", "PSC",
@@ -107,10 +111,14 @@ FULL_LEVELS = {"QDOT", "ATM1_W", "ATM2_W", "XWWB_B0", "XWWB_BT", "ATM0_PF", "ATM
                "ATM0_ZF", "WPHY", "ATMS_PF3D", "ATMS_WB3D", "ATMS_ZQ", "XWWB_B1",
                "ATM1_TKE", "ATM2_TKE", "TKEPHY"}
 TKE_STATE_FIELDS = ["ATM1_TKE", "ATM2_TKE"]
+# nqx = 5 (ipptls >= 2): the ice, rain and snow hydrometeors and their physics / slice fields
+QX_STATE_FIELDS = ["ATM1_QI", "ATM1_QR", "ATM1_QS", "ATM2_QI", "ATM2_QR", "ATM2_QS"]
+QX_PHY_FIELDS = ["QIPHY", "QRPHY", "QSPHY"]
 # physics coupling seam: pc_physic tendencies (put) and the mkslice export (get)
 PHY_FIELDS = ["TPHY", "QVPHY", "QCPHY", "UPHY", "VPHY"]
 NH_PHY_FIELDS = ["PPPHY", "WPHY"]
-ATMS_FIELDS = [n for n in FIELD_NAMES if n.startswith("ATMS_")]
+ATMS_FIELDS = [n for n in FIELD_NAMES if n.startswith("ATMS_") and not n.startswith("ATMS_QXB3D")]
+QX_ATMS_FIELDS = ["ATMS_QXB3D_QI", "ATMS_QXB3D_QR", "ATMS_QXB3D_QS"]
 NH_STATE_FIELDS = ["ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"]
 NH_BDY_FIELDS = ["XPPB_B0", "XPPB_BT", "XWWB_B0", "XWWB_BT"]
 NH_STATIC_FIELDS = ["ATM0_PS", "ATM0_PR", "ATM0_T", "ATM0_RHO", "ATM0_Z", "ATM0_PF",
@@ -183,6 +191,10 @@ class RunConfig:
     ibltyp: int = 1                  # physicsparam; 2 = UW PBL (TKE advected by the dyn step)
     nuk: float = 5.0                 # uwparam, Main/mod_params.F90:480
     iuwvadv: int = 0                 # uwparam; 1 with ibltyp = 2: PBL-aware qc vertical flux (vadv4d ind = 3)
+    ipptls: int = 1                  # physicsparam; > 1 (WSM5 / NT): nqx = 5, Main/mod_params.F90:1358-1366
+    i_band: int = 0                  # dimparam / physicsparam options the engine refuses
+    i_crm: int = 0
+    ichem: int = 0
     tkemin: float = 1.0e-3           # uwtkemin, Main/pbllib/mod_pbl_uwtcm.F90:86
     nhbet: float = 0.4
     nhxkd: float = 0.1
@@ -203,6 +215,11 @@ class RunConfig:
                 setattr(self, attr, max(n, 3))
         if self.kz not in SIGMA_TABLES:
             raise ValueError(f"no sigma table for kz={self.kz}")
+
+    @property
+    def nqx(self) -> int:
+        """Moisture species: 5 (qv, qc, qi, qr, qs) for ipptls > 1, else 2 (qv, qc)."""
+        return 5 if self.ipptls > 1 else 2
 
     @property
     def sigma(self) -> np.ndarray:
@@ -281,6 +298,8 @@ def build_config(rc: RunConfig, split: dict, nproc_j: int = 1, nproc_i: int = 1,
     c.isladvec, c.iqmsl = rc.isladvec, rc.iqmsl
     c.ibltyp, c.nuk, c.tkemin = rc.ibltyp, rc.nuk, rc.tkemin
     c.iuwvadv = rc.iuwvadv
+    c.ipptls, c.nqx = rc.ipptls, rc.nqx
+    c.i_band, c.i_crm, c.ichem = rc.i_band, rc.i_crm, rc.ichem
     if rc.idynamic == 2:
         c.nh_dtsmax = split["nh_dtsmax"]
         c.nh_xmsf = split["nh_xmsf"]

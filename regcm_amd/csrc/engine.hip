@@ -218,8 +218,11 @@ enum class FK {
   // UW PBL TKE (ibltyp = 2)
   A1TKE, A2TKE,
   // idiffu = 3 column terms
-  D6U, D6V, D6T, D6QV, D6QC
+  D6U, D6V, D6T, D6QV, D6QC,
+  // nqx = 5: the hydrometeors beyond qc (qi, qr, qs), each kind in species order
+  A1QX0, A1QX1, A1QX2, A2QX0, A2QX1, A2QX2, CQX0, CQX1, CQX2, SLQX0, SLQX1, SLQX2, D6QX0, D6QX1, D6QX2
 };
+inline FK fkq(FK base, int n) { return (FK)((int)base + n); }
 
 struct rcmdyn_engine {
   rcmdyn_config cfg{};
@@ -402,6 +405,7 @@ struct rcmdyn_engine {
     for (int k = 2; k <= kz; k++) c.dds[k] = 1.0 / (c.dsigma[k] + c.dsigma[k - 1]);
     c.ibltyp = cfg.ibltyp; c.nuk = cfg.nuk; c.tkemin = cfg.tkemin;
     c.iqxvadv = (cfg.ibltyp == 2 && cfg.iuwvadv == 1) ? 3 : 1;
+    c.ipptls = cfg.ipptls; c.nqx = cfg.nqx; c.nsp = cfg.nqx - 2;
   }
 
   double* dalloc(Tile& t, size_t n) {
@@ -462,6 +466,13 @@ struct rcmdyn_engine {
       t.kpbl = dalloc(t, P);
     }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
+    for (int n = 0; n < hc.nsp; n++) {            // nqx = 5: qi, qr, qs (species.hip)
+      for (int b = 0; b < 2; b++) { t.a1qx[n][b] = dalloc(t, P3); t.a2qx[n][b] = dalloc(t, P3); }
+      t.cqx[n] = dalloc(t, P3); t.fqx[n] = dalloc(t, P3);
+      if (cfg.isladvec == 1) t.slqx[n] = dalloc(t, P3);
+      if (cfg.idiffu == 3) t.d6qx[n] = dalloc(t, P * (kz + 1));
+    }
+    if (hc.nsp) t.depx = talloc<int>(t, (size_t)hc.nsp * kz);
     t.depplane = talloc<int>(t, 2 * kz);
     if (cfg.idynamic != 2) {
       t.negcnt = talloc<int>(t, 1);
@@ -482,8 +493,9 @@ struct rcmdyn_engine {
     slen = std::max<long>(g.pitch, g.ni);
     for (int s = 0; s < 16; s++) t.sl[s] = dalloc(t, (size_t)slen * kz);
     // halo staging: 8 directions x widest exchange (the hydrostatic prologue: 5 fields 2 wide
-    // + 5 fields 3 wide + p*; at most 32 field-widths of kz+1 levels)
-    staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * 32 * (kz + 1));
+    // + 5 fields 3 wide + p*; at most 32 field-widths of kz+1 levels; nqx = 5 adds 3 fields 2
+    // wide + 3 fields 3 wide)
+    staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * (32 + 16 * (hc.nsp > 0)) * (kz + 1));
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
     if (cfg.nproc_j * cfg.nproc_i > 1) {
@@ -620,6 +632,17 @@ struct rcmdyn_engine {
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
     if (cfg.iboudy < 1 || cfg.iboudy > 5) throw std::runtime_error("rcmdyn: iboudy must be 1 to 5");
+    // physicsparam ipptls and the nqx param derives from it (Main/mod_params.F90:1358-1366)
+    if (cfg.ipptls < 1 || cfg.ipptls > 2)
+      throw std::runtime_error("rcmdyn: ipptls must be 1 or 2 (ipptls = 0 leaves the hydrometeor tendencies unsummed, "
+                               "Main/mod_tendency.F90:331: not supported)");
+    if (cfg.nqx != (cfg.ipptls > 1 ? 5 : 2))
+      throw std::runtime_error("rcmdyn: nqx must be 2 for ipptls = 1 and 5 for ipptls = 2 (Main/mod_params.F90:1358-1366)");
+    // periodic decompositions and chemical tracers are not built: refused, not ignored
+    if (cfg.i_band != 0) throw std::runtime_error("rcmdyn: i_band = 1 (periodic tropical band) is not supported");
+    if (cfg.i_crm != 0) throw std::runtime_error("rcmdyn: i_crm = 1 (periodic CRM domain) is not supported");
+    if (cfg.ichem != 0) throw std::runtime_error("rcmdyn: ichem = 1 (chemical tracers) is not supported");
+    if (cfg.idynamic == 2 && cfg.nqx > 2) throw std::runtime_error("rcmdyn: nqx = 5 for idynamic = 2: not yet");
     // dynparam's upstream_mode (default .true., Main/mod_params.F90:646); .false. runs the
     // centred branches (Main/mod_advection.F90:141,322,409,532,624; see c.ul)
     if (cfg.upstream_mode != 0 && cfg.upstream_mode != 1)
@@ -842,6 +865,16 @@ struct rcmdyn_engine {
       case FK::D6QV: return t.d6[3]; case FK::D6QC: return t.d6[4];
       default: break;
     }
+    if (f >= FK::A1QX0 && f <= FK::D6QX2) {
+      const int r = (int)f - (int)FK::A1QX0, n = r % NQXH;
+      switch (r / NQXH) {
+        case 0: return t.a1qx[n][c];
+        case 1: return t.a2qx[n][c];
+        case 2: return t.cqx[n];
+        case 3: return t.slqx[n];
+        default: return t.d6qx[n];
+      }
+    }
     const NHFields& h = nhf[&t - tiles.data()];
     switch (f) {
       case FK::A1PP: return h.a1pp; case FK::A2PP: return h.a2pp; case FK::A1W: return h.a1w;
@@ -881,6 +914,13 @@ struct rcmdyn_engine {
       return f == RCMDYN_ATM1_TKE ? t.a1tke : f == RCMDYN_ATM2_TKE ? t.a2tke : t.tkephy;
     }
     if (f == RCMDYN_KPBL) { nk = 1; return t.kpbl; }
+    if (f >= RCMDYN_ATM1_QI && f <= RCMDYN_ATMS_QXB3D_QS) {      // nqx = 5 only
+      if (hc.nsp == 0) return nullptr;
+      if (f <= RCMDYN_ATM1_QS) return t.a1qx[f - RCMDYN_ATM1_QI][c];
+      if (f <= RCMDYN_ATM2_QS) return t.a2qx[f - RCMDYN_ATM2_QI][c];
+      if (f <= RCMDYN_QSPHY) return t.phyx[f - RCMDYN_QIPHY];
+      return t.atmsx[f - RCMDYN_ATMS_QXB3D_QI];
+    }
     if (f >= RCMDYN_ATM1_PP && f <= RCMDYN_CRY) {
       if (cfg.idynamic != 2) return nullptr;
       NHFields& h = nhf[&t - tiles.data()];
@@ -943,12 +983,14 @@ struct rcmdyn_engine {
   }
 
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
-    const bool phyf = f >= RCMDYN_TPHY && f <= RCMDYN_WPHY;
+    const bool qxf = f >= RCMDYN_ATM1_QI && f <= RCMDYN_QSPHY;
+    const bool phyf = (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY) || (f >= RCMDYN_QIPHY && f <= RCMDYN_QSPHY);
     const bool binf = f >= RCMDYN_XUB_B1 && f <= RCMDYN_ATM0_PSDOT;
     const bool tkef = (f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) || f == RCMDYN_KPBL;
     if (f < 0 || f >= RCMDYN_NFIELDS || (f > RCMDYN_XPSB_BT && f < RCMDYN_ATM1_PP) ||
-        (f > RCMDYN_CRY && !phyf && !binf && !tkef))
+        (f > RCMDYN_CRY && !phyf && !binf && !tkef && !qxf))
       throw std::runtime_error("rcmdyn_put: field is read-only or unknown");
+    if (qxf && hc.nsp == 0) throw std::runtime_error("rcmdyn_put: qi/qr/qs fields need nqx = 5 (ipptls = 2)");
     if (tkef && cfg.ibltyp != 2) throw std::runtime_error("rcmdyn_put: TKE/kpbl fields need ibltyp=2 (UW PBL)");
     if (f == RCMDYN_KPBL) {
       // vadv4d ind = 3 stops on a PBL top above the model (Main/mod_advection.F90:923-925)
@@ -999,6 +1041,7 @@ struct rcmdyn_engine {
       const size_t P = t.g.plane;
       for (int q = 0; q < 5; q++) t.phy[q] = dalloc(t, P * cfg.kz);
       if (cfg.idynamic == 2) { t.phy[5] = dalloc(t, P * cfg.kz); t.phy[6] = dalloc(t, P * (cfg.kz + 1)); }
+      for (int n = 0; n < hc.nsp; n++) t.phyx[n] = dalloc(t, P * cfg.kz);
     }
     invalidate_graphs();
   }
@@ -1065,6 +1108,7 @@ struct rcmdyn_engine {
     for (auto& t : tiles) {
       if (t.atms[0]) continue;
       for (int q = 0; q < 22; q++) t.atms[q] = dalloc(t, t.g.plane * (size_t)atms_levels(q, cfg.kz));
+      for (int n = 0; n < hc.nsp; n++) t.atmsx[n] = dalloc(t, t.g.plane * (size_t)cfg.kz);
     }
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1084,6 +1128,7 @@ struct rcmdyn_engine {
       a.za = o[18]; a.dzq = o[19]; a.qsb3d = o[20]; a.rhb3d = o[21];
       a.ep2 = AMW / AMD;                                  // Share/mod_constants.F90:306
       a.rhmin = cfg.rhmin; a.rhmax = cfg.rhmax;
+      for (int n = 0; n < hc.nsp; n++) { a.a2qx[n] = t.a2qx[n][c]; a.qxb3d[n] = t.atmsx[n]; }
       KLAUNCH(k_slice, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, 1), BLK, 0, stream, g, dc, a);
     });
   }
@@ -1099,6 +1144,13 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY && !tiles[0].phy[0])
       throw std::runtime_error("rcmdyn_get: no physics tendencies were put");
+    if (f >= RCMDYN_ATM1_QI && f <= RCMDYN_ATMS_QXB3D_QS) {
+      if (hc.nsp == 0) throw std::runtime_error("rcmdyn_get: qi/qr/qs fields need nqx = 5 (ipptls = 2)");
+      if (f >= RCMDYN_QIPHY && f <= RCMDYN_QSPHY && !tiles[0].phyx[0])
+        throw std::runtime_error("rcmdyn_get: no physics tendencies were put");
+      if (f >= RCMDYN_ATMS_QXB3D_QI && !tiles[0].atmsx[0])
+        throw std::runtime_error("rcmdyn_get: no slice fields yet (rcmdyn_tend_pre_physics)");
+    }
     if (((f >= RCMDYN_ATM1_TKE && f <= RCMDYN_TKEPHY) || f == RCMDYN_KPBL) && cfg.ibltyp != 2)
       throw std::runtime_error("rcmdyn_get: TKE/kpbl fields need ibltyp=2 (UW PBL)");
     if (f == RCMDYN_TKEPHY && !tiles[0].tkephy) throw std::runtime_error("rcmdyn_get: no TKE tendency was put");
@@ -1504,7 +1556,28 @@ struct rcmdyn_engine {
     f.tphy = t.phy[0]; f.qvphy = t.phy[1]; f.qcphy = t.phy[2]; f.uphy = t.phy[3]; f.vphy = t.phy[4];
     f.red = red; f.red_off = t.red_off;
     f.qfuse = qfuse() ? 1 : 0; f.negcnt = t.negcnt; f.neglist = t.neglist;
+    for (int n = 0; n < hc.nsp; n++) f.qxa1[n] = t.a1qx[n][c];
+    if (hc.nsp) f.xkcs = t.xkcs;              // k_qx_tend's diffusion reads the scaled xkc
     return f;
+  }
+
+  // the hydrometeors beyond qc (nqx = 5) for the current parity: a* current, b* next (the
+  // hydrostatic ping-pong; the NH core updates a* in place)
+  QxArgs qx_args(Tile& t) {
+    const int c = t.cur, n1 = 1 - c;
+    QxArgs q{};
+    q.nsp = hc.nsp;
+    for (int n = 0; n < hc.nsp; n++) {
+      q.a1[n] = t.a1qx[n][c]; q.a2[n] = t.a2qx[n][c];
+      q.b1[n] = t.a1qx[n][n1]; q.b2[n] = t.a2qx[n][n1];
+      q.cq[n] = t.cqx[n]; q.fq[n] = t.fqx[n]; q.sl[n] = t.slqx[n]; q.d6[n] = t.d6qx[n]; q.phy[n] = t.phyx[n];
+    }
+    q.dep = t.depx;
+    return q;
+  }
+  // the XField entries of the hydrometeors beyond qc for one kind (A1QX0 ..), width w
+  void add_qx(std::vector<XField>& v, FK base, int nk, int w) const {
+    for (int n = 0; n < hc.nsp; n++) v.push_back({fkq(base, n), nk, w});
   }
 
   // istep of sound (Main/mod_sound.F90:201-205) for the host time mirror
@@ -1600,7 +1673,8 @@ struct rcmdyn_engine {
         HIPCHK(hipMemsetAsync(f.wten, 0, b4, stream));
       }
       if (cfg.isladvec == 1)
-        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
+        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t),
+                qx_args(t));
       // the tendency chains (advection, curvature/adiabatic, boundary, diffusion, forecast)
       if (!ovl) {
         tend_d_launch(t, f, istep);
@@ -1737,6 +1811,9 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       const int c = t.cur;
+      if (hc.nsp)
+        KLAUNCH(k_bdyval_qx, dim3(kz, hc.nsp), dim3(256), 0, stream, t.g, ds, qx_args(t), -1, (int)!cfg.present_qc,
+                t.psa_[c], slices(t), slen);
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 3 || cfg.iboudy == 4),
               t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()), dflags);
     }
@@ -1776,6 +1853,8 @@ struct rcmdyn_engine {
                             {FK::A1T, kz, 2}, {FK::A1QV, kz, 2}, {FK::A1QC, kz, 2}};
     std::vector<XField> pro2{{FK::A2U, kz, 3}, {FK::A2V, kz, 3}, {FK::A2T, kz, 3}, {FK::A2QV, kz, 3},
                              {FK::A2QC, kz, 3}};
+    add_qx(pro, FK::A1QX0, kz, 2);        // nqx = 5: qi, qr, qs with qc
+    add_qx(pro2, FK::A2QX0, kz, 3);
     // UW TKE: atm1 1 wide, atm2 idif wide (Main/mod_tendency.F90:871, 1079)
     if (cfg.ibltyp == 2) {
       pro.push_back({FK::A1TKE, kz + 1, 1});
@@ -1794,7 +1873,10 @@ struct rcmdyn_engine {
         const long nkeep = qfuse() ? (long)(4 * W + 4 * std::max(H - 4, 0)) * kz : 0;
         nsp = (int)((g.nj * (long)g.ni + 511) / 512 + (nkeep + 511) / 512);
       }
-      KLAUNCH(k_columns, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
+      if (hc.nsp)
+        KLAUNCH(k_columns<true>, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
+      else
+        KLAUNCH(k_columns<false>, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
     };
     if (overlap()) {
       // the whole exchange on the second stream; meanwhile part 1 of k_columns and, in a whole
@@ -1829,9 +1911,14 @@ struct rcmdyn_engine {
     const int kz = cfg.kz;
     each([&](Tile& t) {
       const Geom& g = t.g;
-      KLAUNCH(k_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kz, 4), dim3(64), 0, stream, g, dc, fields(t));
+      KLAUNCH(k_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kz, 4 + hc.nsp), dim3(64), 0, stream, g, dc, fields(t),
+              qx_args(t));
     });
-    if (ntiles > 1) xch({{FK::D6U, kz}, {FK::D6V, kz}, {FK::D6T, kz}, {FK::D6QV, kz}, {FK::D6QC, kz}});
+    if (ntiles > 1) {
+      std::vector<XField> d6{{FK::D6U, kz}, {FK::D6V, kz}, {FK::D6T, kz}, {FK::D6QV, kz}, {FK::D6QC, kz}};
+      add_qx(d6, FK::D6QX0, kz, 0);
+      xchv(d6);
+    }
   }
 
   // k_momentum and k_scalars of one tile: part 1 the blocks in R (when it has any), part 2 the
@@ -1857,14 +1944,36 @@ struct rcmdyn_engine {
     if (cfg.isladvec == 1) {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t));
+        KLAUNCH(k_sladv, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, kz), BLK, 0, stream, g, dc, ds, fields(t),
+                qx_args(t));
       });
-      xch({{FK::SLQV, kz}, {FK::SLQC, kz}}, 1, 0);
+      std::vector<XField> sl{{FK::SLQV, kz}, {FK::SLQC, kz}};
+      add_qx(sl, FK::SLQX0, kz, 0);
+      xchv(sl, 1, 0);
     }
     // fused tendencies + forecast + time filter (part 2 when tend_pre ran part 1)
     each([&](Tile& t) { post_launch(t, post_inner ? 2 : 0); });
     post_inner = false;
     tke_step();
+    if (hc.nsp) {
+      // nqx = 5: the hydrometeors beyond qc, their forecast (and ring), then the fix and filter
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        KLAUNCH(k_qx_tend, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, kz), dim3(SBT),
+                0, stream, g, dc, ds, fields(t), qx_args(t));
+      });
+      if (!fused) {
+        std::vector<XField> cq;
+        add_qx(cq, FK::CQX0, kz, 1);
+        xchv(cq);
+      }
+      each([&](Tile& t) {
+        const Geom& g = t.g;
+        KLAUNCH(k_qx_fix, grid3(g.jdx2() - g.jdx1() + 1, g.idx2() - g.idx1() + 1, kz), BLK, 0, stream, g, dc,
+                qx_args(t));
+        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(64), 0, stream, g, dc, qx_args(t));
+      });
+    }
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
     // negative-moisture fix + p* RA filter + qv/qc RAW filter; then the new level is current
     // (qfuse: done by k_columns, k_scalars and the extra blocks below)
@@ -2013,6 +2122,9 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       const int adv = q + 1 == tiles.size() ? (fuse_bdy ? 2 : 1) : 0;
+      if (hc.nsp)
+        KLAUNCH(k_bdyval_qx, dim3(kz, hc.nsp), dim3(256), 0, stream, t.g, ds, qx_args(t), fuse_bdy ? 1 : -1,
+                (int)!cfg.present_qc, t.psa_[t.cur], bdy_args(t, 1).sl, slen);
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 3 || cfg.iboudy == 4),
               t.a1qc[t.cur], t.a1qv[t.cur], t.psa_[t.cur], bdy_args(t, 1).sl, slen, ds, cfg.dtsec, adv, dflags);
     }

@@ -21,6 +21,7 @@ constexpr int G = 4;               // ghost ring of the frame: idif = 2 for idif
 constexpr int MAXKZ = RCMDYN_MAXKZ;
 constexpr int MAXSPLIT = RCMDYN_MAXSPLIT;
 constexpr int MAXNSP = 256;        // max boundary-band width (nspgx)
+constexpr int NQXH = 3;            // nqx = 5: the hydrometeors beyond qc (qi, qr, qs)
 
 // Index ranges of one tile, Main/mod_atm_interface.F90:181-381 (global indices).
 struct Geom {
@@ -101,6 +102,9 @@ struct Consts {
   // non-hydrostatic core (idynamic = 2): nonhydroparam and init_sound scalars
   int idynamic, ifupr, ifrayd, rayndamp;
   double rayalpha0, rayhd, nhbet, nhxkd, nh_dtsmax, nh_xmsf, xgamma, dds[MAXKZ + 2];
+  // moisture species (physicsparam ipptls, Main/mod_params.F90:1358-1366): nqx = 2 (qv, qc)
+  // or 5 (qv, qc, qi, qr, qs); nsp = nqx - 2 hydrometeors beyond qc
+  int ipptls, nqx, nsp;
 };
 
 // rcm_timer state on the device, advanced by kernels so one captured step is replayable.
@@ -156,6 +160,12 @@ struct Tile {
   double *a1tke = nullptr, *a2tke = nullptr, *ctke = nullptr, *tkephy = nullptr;
   double* kpbl = nullptr;          // ibltyp = 2: the UW scheme's PBL-top level (put, 2-D)
   double *cqv, *cqc, *fqv, *fqc;
+  // nqx = 5: the hydrometeors beyond qc (qi, qr, qs; species.hip), ping-pong like qc, their
+  // forecasts / fixed values, the flagged planes of their negative fix, the semi-Lagrangian
+  // tendency starts (isladvec = 1) and idiffu = 3 column terms
+  double *a1qx[NQXH][2] = {}, *a2qx[NQXH][2] = {};
+  double *cqx[NQXH] = {}, *fqx[NQXH] = {}, *slqx[NQXH] = {}, *d6qx[NQXH] = {};
+  int* depx = nullptr;
   int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
   int* negcnt = nullptr;           // hydrostatic qfuse: the negative forecasts k_scalars listed
   uint32_t* neglist = nullptr;
@@ -174,6 +184,7 @@ struct Tile {
   // rcmdyn_tend_pre_physics), in rcmdyn_field order
   double *phy[7] = {};
   double *atms[22] = {};
+  double *phyx[NQXH] = {}, *atmsx[NQXH] = {};   // nqx = 5: qxphy and the qxb3d export of qi, qr, qs
   // device bdyin: the raw record put by the host (u, v, t, qv, ps, pp, w) and the coupled
   // boundary data at the interval end (b1, same order), allocated on the first put of a
   // record field; NH: atm0%psdot (Pa) for the coupling of u, v

@@ -76,9 +76,22 @@ struct Fields {
   int qfuse;
   int* negcnt;
   uint32_t* neglist;
+  // nqx = 5: atm1 of the hydrometeors beyond qc (k_columns: the total water load of tvfac)
+  const double* qxa1[NQXH];
   double* red;                 // engine-wide noise-sum partials (k_columns -> k_split_correct)
   int red_off;                 // this tile's first partial
   Part pt;                     // the launch's overlap part (k_columns, k_momentum, k_scalars)
+};
+
+// nqx = 5: the hydrometeors beyond qc (qi, qr, qs) for the current (a*) and next (b*) time-level
+// buffers (species.hip; the non-hydrostatic core updates a* in place and leaves b* null)
+struct QxArgs {
+  double *a1[NQXH], *a2[NQXH], *b1[NQXH], *b2[NQXH];
+  double *cq[NQXH], *fq[NQXH];
+  double *sl[NQXH], *d6[NQXH];
+  const double* phy[NQXH];
+  int* dep;                    // per (species, level) plane: a serially dependent negative point
+  int nsp;                     // hydrometeors beyond qc (0 for nqx = 2)
 };
 
 // serial negative-moisture fix-up of k_split_project's extra blocks: the q fields before
@@ -100,10 +113,11 @@ struct QFix {
 };
 
 __global__ void k_surface_pressures(Geom g, Fields f);
+template <bool QX>
 __global__ void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, int nxb, int ncol);
-__global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f);
+__global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fields f, QxArgs q);
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
-__global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f);
+__global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f, QxArgs q);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
@@ -141,5 +155,14 @@ __global__ void k_err_publish(const int32_t* __restrict__ derr, int32_t* hslot);
 __global__ void k_prepare_static(Geom g, const Consts* __restrict__ c, int diffu_hgtf, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ ht, double* xmsf, double* dmsf, double* hgfact, double* mapf);
 __global__ void k_pack_segs(SegList L, double* __restrict__ buf, int unpack);
 __global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restrict__ src, long sstride, double* dst, long dstride);
+
+// species.hip: the hydrometeors beyond qc (nqx = 5), hydrostatic core (the ping-pong buffers)
+__global__ void k_qx_tend(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f, QxArgs q);
+__global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q);
+__global__ void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q);
+// bdyval's boundary copies and inflow/outflow of the hydrometeors beyond qc (both cores);
+// integ: 1 integrating, 0 the initial call, -1 from the step clock (lcount > 0)
+__global__ void k_bdyval_qx(Geom g, const StepState* __restrict__ s, QxArgs q, int integ, int do_qc,
+                            const double* __restrict__ psa, Slices sl, long slen);
 
 }  // namespace rcm

@@ -89,6 +89,7 @@ __global__ __launch_bounds__(256) void k_slice(Geom g, const Consts* __restrict_
     F3(a.tb3d, j, i, k) = tb;
     F3(a.qvb3d, j, i, k) = qvb;
     F3(a.qcb3d, j, i, k) = qcb;
+    for (int n = 0; n < c->nsp; n++) F3(a.qxb3d[n], j, i, k) = dmax(F3(a.a2qx[n], j, i, k) * rpsb, d_zero);
     const double tv = tb * (d_one + ep1 * qvb - qcb);
     F3(a.tv3d, j, i, k) = tv;
     // pb3d (:207-214 NH, :226-228 hydrostatic)

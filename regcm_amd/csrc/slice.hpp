@@ -13,6 +13,9 @@ struct SliceArgs {
   double *ubx3d, *vbx3d, *ubd3d, *vbd3d, *tb3d, *qvb3d, *qcb3d, *tv3d, *pb3d, *pf3d, *ps2d, *rhox2d;
   double *th3d, *rhob3d, *tp3d, *wpx3d, *wb3d, *zq, *za, *dzq, *qsb3d, *rhb3d;
   double ep2, rhmin, rhmax;
+  // nqx = 5: qxb3d of qi, qr, qs (Main/mod_slice.F90:193-195), from atm2 (null for nqx = 2)
+  const double* a2qx[NQXH];
+  double* qxb3d[NQXH];
 };
 
 __global__ void k_slice(Geom g, const Consts* __restrict__ c, SliceArgs a);

@@ -11,7 +11,7 @@ module mod_gpu_dyn
   implicit none
   private
 
-  integer, parameter, public :: rcmdyn_abi_version = 5
+  integer, parameter, public :: rcmdyn_abi_version = 6
   integer, parameter, public :: rcmdyn_maxkz = 64, rcmdyn_maxsplit = 4
 
   ! field ids (enum rcmdyn_field)
@@ -40,7 +40,11 @@ module mod_gpu_dyn
     ! device bdyin: the next ICBC record as read_icbc returns it; NH atm0%psdot
     f_xub_b1 = 97, f_xvb_b1 = 98, f_xtb_b1 = 99, f_xqb_b1 = 100, f_xpsb_b1 = 101, &
     f_xppb_b1 = 102, f_xwwb_b1 = 103, f_atm0_psdot = 104, &
-    f_atm1_tke = 105, f_atm2_tke = 106, f_tkephy = 107, f_kpbl = 108
+    f_atm1_tke = 105, f_atm2_tke = 106, f_tkephy = 107, f_kpbl = 108, &
+    ! nqx = 5 (ipptls >= 2): atm1/atm2 qx(:,:,:,iqi|iqr|iqs), their qxphy, the qxb3d export
+    f_atm1_qi = 109, f_atm1_qr = 110, f_atm1_qs = 111, f_atm2_qi = 112, f_atm2_qr = 113, &
+    f_atm2_qs = 114, f_qiphy = 115, f_qrphy = 116, f_qsphy = 117, &
+    f_atms_qxb3d_qi = 118, f_atms_qxb3d_qr = 119, f_atms_qxb3d_qs = 120
 
   type, bind(c), public :: rcmdyn_config
     integer(c_int32_t) :: abi_version
@@ -74,6 +78,10 @@ module mod_gpu_dyn
     ! physicsparam ibltyp (2 = UW PBL TKE in the dyn step), uwparam iuwvadv, nuk, tkemin (uwtkemin)
     integer(c_int32_t) :: ibltyp, iuwvadv
     real(c_double) :: nuk, tkemin
+    ! ABI 6: physicsparam ipptls and the nqx param sets from it (2, or 5 for ipptls >= 2);
+    ! i_band, i_crm, ichem (refused if set)
+    integer(c_int32_t) :: ipptls, nqx
+    integer(c_int32_t) :: i_band, i_crm, ichem
   end type rcmdyn_config
 
   interface

@@ -127,6 +127,32 @@ def generate(rc: RunConfig, seed: int = SEED, hmax: float = None) -> dict:
     return dict(state=st, split=split)
 
 
+def hydrometeor_state(rc: RunConfig, st: dict, seed: int = SEED + 5, nqx: int = 5) -> dict:
+    """Hydrometeors for the moisture-species tests, coupled with p* like the reference stores
+    them: cloud water in the lower and middle troposphere, ice aloft, rain near the surface,
+    snow in between (peaks 0.2, 0.05, 0.1, 0.08 g/kg), each times a patchy 0/1 mask so that the
+    advection of the cloud edges produces negative forecasts (the negative-moisture fix); atm2
+    a few per cent off atm1.  nqx = 2 gives qc only; nqx = 5 also qi, qr, qs."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    kz, iy, jx = rc.kz, rc.iy, rc.jx
+    hsig = (rc.sigma[1:] + rc.sigma[:-1]) * 0.5
+    ps = st["PSA"][0]
+    prof = {"QC": (2.0e-4, 0.75, 0.15), "QI": (5.0e-5, 0.30, 0.10), "QR": (1.0e-4, 0.92, 0.08),
+            "QS": (8.0e-5, 0.55, 0.12)}
+    names = ["QC"] if nqx == 2 else ["QC", "QI", "QR", "QS"]
+    out = {}
+    for nm in names:
+        peak, s0, w = prof[nm]
+        layer = peak * np.exp(-0.5 * ((hsig - s0) / w) ** 2)
+        mask = (rng.uniform(size=(kz, iy, jx)) < 0.6).astype(np.float64)
+        q = layer[:, None, None] * mask * rng.uniform(0.5, 1.5, size=(kz, iy, jx))
+        q[:, iy - 1, :] = 0.0
+        q[:, :, jx - 1] = 0.0
+        out[f"ATM1_{nm}"] = q * ps[None]
+        out[f"ATM2_{nm}"] = q * ps[None] * rng.uniform(0.95, 1.0, size=(kz, iy, jx))
+    return out
+
+
 def spinit_storage(rc: RunConfig, split: dict, st: dict):
     """dstor/hstor from atm2 (Main/mod_split.F90:192-235), single global tile."""
     jx, iy, kz, ns = rc.jx, rc.iy, rc.kz, rc.nsplit

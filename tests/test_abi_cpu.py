@@ -47,7 +47,7 @@ int main(void) {
   O(jx); O(present_qc); O(ds); O(dtbdys); O(sigma); O(zmatx); O(zmatxr); O(am); O(tau);
   O(varpa1); O(an); O(hbar); O(aam); O(dtau); O(sigmah); O(pd); O(comm_rank); O(device);
   O(comm_unique_id); O(nh_dtsmax); O(rhmin); O(rhmax); O(isladvec); O(iqmsl); O(ibltyp); O(nuk);
-  O(tkemin);
+  O(tkemin); O(ipptls); O(nqx); O(i_band); O(i_crm); O(ichem);
   return 0;
 }
 """
@@ -109,7 +109,10 @@ def test_create_without_gpu_fails_loudly():
 @pytest.mark.parametrize("opt,msg", [({"upstream_mode": 2}, "upstream_mode"),
                                      ({"idiffu": 4}, "idiffu"), ({"idiffu": 0}, "idiffu"),
                                      ({"iboudy": 0}, "iboudy"),
-                                     ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv")])
+                                     ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv"),
+                                     ({"ipptls": 0}, "ipptls"), ({"ipptls": 3}, "ipptls"),
+                                     ({"i_band": 1}, "i_band"), ({"i_crm": 1}, "i_crm"),
+                                     ({"ichem": 1}, "ichem")])
 def test_create_refuses_unbuilt_options(opt, msg):
     """A drop-in refuses what it does not compute: option values whose reference branches are
     not built fail rcmdyn_create with the option's name, before any device call (so here too)."""
@@ -133,3 +136,41 @@ def test_field_enum_matches_header_python_fortran():
     f90 = open(os.path.join(ROOT, "regcm_amd", "fortran", "mod_gpu_dyn.F90")).read()
     ids = {m.group(1).upper(): int(m.group(2)) for m in re.finditer(r"\bf_(\w+)\s*=\s*(\d+)", f90)}
     assert ids == {n: q for q, n in enumerate(FIELD_NAMES)}
+
+
+@pytest.mark.parametrize("ipptls,nqx", [(1, 5), (2, 2), (1, 3), (2, 4)])
+def test_create_refuses_nqx_not_matching_ipptls(ipptls, nqx):
+    """nqx is what param derives from ipptls (Main/mod_params.F90:1358-1366): 2 for ipptls = 1,
+    5 for ipptls = 2; any other pairing is refused before a device call."""
+    import ctypes
+    import dataclasses
+    from regcm_amd.config import CONFIGS, build_config
+    from regcm_amd import icbc
+    rc = dataclasses.replace(CONFIGS["C1"], ipptls=ipptls)
+    data = icbc.generate(CONFIGS["C1"])
+    cfg = build_config(rc, data["split"])
+    cfg.nqx = nqx
+    h = ctypes.c_void_p()
+    assert dycore.lib().rcmdyn_create(ctypes.byref(cfg), ctypes.byref(h)) != 0
+    assert b"nqx" in dycore.lib().rcmdyn_last_error(None)
+
+
+def test_exchange_plan_carries_the_hydrometeors():
+    """nqx = 5: the prologue messages grow by qi, qr, qs (atm1 2 wide, atm2 3 wide), and every
+    rank's sends still match its neighbours' receives."""
+    import dataclasses
+    import numpy as np
+    from regcm_amd.config import CONFIGS
+    from regcm_amd import icbc
+    rc = CONFIGS["C1"]
+    data = icbc.generate(rc)
+    p2 = dycore.exchange_plan(rc, data["split"], 2, 2, 0, 2)
+    p5 = dycore.exchange_plan(dataclasses.replace(rc, ipptls=2), data["split"], 2, 2, 0, 2)
+    assert p5[:, 5].sum() > p2[:, 5].sum()
+    plans = [dycore.exchange_plan(dataclasses.replace(rc, ipptls=2), data["split"], 2, 2, r, 2) for r in range(4)]
+    for a in range(4):
+        for b in range(4):
+            sa = [tuple(x[[2, 5, 6]]) for x in plans[a] if x[1] == 1 and x[3] == 0 and x[4] == b]
+            rb = [tuple(x[[2, 5, 6]]) for x in plans[b] if x[1] == 1 and x[3] == 1 and x[4] == a]
+            assert sa == rb, (a, b)
+    assert np.all(p5[:, 1] > 0)
