@@ -233,11 +233,13 @@ int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
 /* Communication plan of one rank, host-only (no GPU, no communicator): the halo messages and
  * collectives that rank cfg->comm_rank (one tile per rank: tile_first = comm_rank, tile_count
  * = 1, comm_size = nproc_j * nproc_i) issues for the first exchanges of the statics and the
- * boundary data and then nsteps x (tend + bdyval), in issue order.  Record q is
+ * boundary data, the initial bdyval after the state put (its slice exchange) and then nsteps x
+ * (tend + bdyval), in issue order.  Record q is
  * ops[7q .. 7q+6] = {call, kind, channel, dir, peer, count, signature}: call = the rank's
  * communication call number; kind 1 = one grouped send/receive (one record per message), 2 =
  * all-reduce sum (f64), 3 = all-reduce max (i32), 4 = all-reduce max (f64); channel 0/1 = the
- * RCCL communicator (one per engine stream); dir 0 send, 1 receive, -1 collective; peer = rank
+ * engine stream that issues it (over RCCL both share the job's communicator, the second
+ * ordered after the first); dir 0 send, 1 receive, -1 collective; peer = rank
  * (-1 for collectives); count = doubles (collectives: elements); signature = hash of the
  * message's box shapes (0 for collectives).  *count = records in the plan (at most cap are
  * written).  Every message A sends B must be the receive B posts from A, in the same order on

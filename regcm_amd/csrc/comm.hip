@@ -80,53 +80,13 @@ class RcclComm final : public Comm {
   bool shared_channels() const override { return comm_[1] == comm_[0]; }
 
  private:
-  // The second channel's communicator.  "one" (default): the first communicator, with the
-  // engine ordering the second stream's exchange after the first stream's (shared_channels).
-  // "init": rank 0 draws a second unique id and broadcasts it over the first communicator,
-  // every rank joins it with ncclCommInitRank; "split": ncclCommSplit.  Both second-
-  // communicator forms crash the first graph-captured step under the RCCL 2.26 that torch
-  // bundles (a process that imported torch before loading the engine binds torch's
-  // librccl.so.1, same soname as /opt/rocm's 2.27), measured with the one-rank communicator
-  // (tools/rccl_dbg.py --torch-first); one communicator runs under both.
-  void second(int size) {
-    const char* m = std::getenv("RCMDYN_RCCL_CHAN2");
-    const std::string mode = m ? m : "one";
-    if (mode == "one") { comm_[1] = comm_[0]; return; }
-    if (mode == "split") {
-      NCCLCHK(ncclCommSplit(comm_[0], 0, rank_of(comm_[0]), &comm_[1], nullptr));
-      return;
-    }
-    if (mode != "init") throw std::runtime_error("rcmdyn: RCMDYN_RCCL_CHAN2 must be init, split or one");
-    ncclUniqueId id2;
-    std::memset(&id2, 0, sizeof(id2));
-    if (size > 1) {
-      if (rank_ == 0) NCCLCHK(ncclGetUniqueId(&id2));
-      void* d = nullptr;
-      hipStream_t st = nullptr;
-      HIPCHK_C(hipMalloc(&d, sizeof(id2)));
-      try {
-        HIPCHK_C(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-        HIPCHK_C(hipMemcpy(d, &id2, sizeof(id2), hipMemcpyHostToDevice));
-        NCCLCHK(ncclBroadcast(d, d, sizeof(id2), ncclUint8, 0, comm_[0], st));
-        HIPCHK_C(hipStreamSynchronize(st));
-        HIPCHK_C(hipMemcpy(&id2, d, sizeof(id2), hipMemcpyDeviceToHost));
-      } catch (...) {
-        if (st) (void)hipStreamDestroy(st);
-        (void)hipFree(d);
-        throw;
-      }
-      (void)hipStreamDestroy(st);
-      (void)hipFree(d);
-    } else {
-      NCCLCHK(ncclGetUniqueId(&id2));
-    }
-    NCCLCHK(ncclCommInitRank(&comm_[1], size, id2, rank_));
-  }
-  static int rank_of(ncclComm_t c) {
-    int r = 0;
-    NCCLCHK(ncclCommUserRank(c, &r));
-    return r;
-  }
+  // The second channel shares the first communicator; the engine orders the second stream's
+  // exchange after the first stream's (shared_channels).  A second communicator per channel
+  // (ncclCommInitRank on a broadcast unique id, or ncclCommSplit) crashed the first graph-
+  // captured step under the RCCL 2.26 that torch bundles (a process that imported torch
+  // before loading the engine binds torch's librccl.so.1, the soname of /opt/rocm's 2.27;
+  // tools/rccl_dbg.py --torch-first) and was removed: one communicator runs under both.
+  void second(int) { comm_[1] = comm_[0]; }
   ncclComm_t comm_[NCHAN] = {nullptr, nullptr};
   int rank_ = 0;
 };

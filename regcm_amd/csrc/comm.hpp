@@ -8,10 +8,11 @@
 // of this class with the identical staging layout.
 //
 // Channels: the engine issues exchanges on two HIP streams (the second carries the part of
-// an exchange point that overlaps compute on the first).  Each stream has its own channel --
-// for RCCL its own communicator (ncclCommSplit of the job communicator) -- so the grouped
-// send/receives of the two streams never share a communicator and each communicator sees its
-// operations in the same order on every rank.
+// an exchange point that overlaps compute on the first).  Over RCCL both channels are the job's
+// one communicator (shared_channels): the engine makes the second stream's grouped send/receive
+// wait for the first stream's preceding one (fork_after_exchange / xch_join), so no two grouped
+// calls on the communicator are in flight at once and it sees its operations in the same order
+// on every rank.  The in-process loopback and the plan recorder keep two independent channels.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -54,10 +55,8 @@ class Comm {
   virtual bool shared_channels() const { return false; }
 };
 
-// one rank per tile: the communicator of the job (cfg.comm_rank / comm_size / unique id);
-// the second channel (RCMDYN_RCCL_CHAN2) shares it ("one", default; the engine orders the two
-// streams' exchanges), or gets a second communicator ("init": ncclCommInitRank on a unique id
-// rank 0 broadcasts over the first; "split": ncclCommSplit)
+// one rank per tile: the communicator of the job (cfg.comm_rank / comm_size / unique id),
+// shared by both channels (the engine orders the two streams' exchanges)
 Comm* make_rccl_comm(const rcmdyn_config& cfg);
 // a communicator of one rank that carries the halo messages between the tiles one engine
 // holds, as RCCL sends and receives to itself (RCMDYN_FORCE_RCCL=1: exercises the RCCL

@@ -220,7 +220,9 @@ enum class FK {
   // idiffu = 3 column terms
   D6U, D6V, D6T, D6QV, D6QC,
   // nqx = 5: the hydrometeors beyond qc (qi, qr, qs), each kind in species order
-  A1QX0, A1QX1, A1QX2, A2QX0, A2QX1, A2QX2, CQX0, CQX1, CQX2, SLQX0, SLQX1, SLQX2, D6QX0, D6QX1, D6QX2
+  A1QX0, A1QX1, A1QX2, A2QX0, A2QX1, A2QX2, CQX0, CQX1, CQX2, SLQX0, SLQX1, SLQX2, D6QX0, D6QX1, D6QX2,
+  // iuwvadv = 1: the PBL-top level (2-D)
+  KPBL
 };
 inline FK fkq(FK base, int n) { return (FK)((int)base + n); }
 
@@ -262,6 +264,7 @@ struct rcmdyn_engine {
   int gslot = 0;
   bool statics_dirty = true;
   bool bdy_dirty = true;
+  bool kpbl_dirty = false;    // kpbl put since the last tend: its ghost ring is stale
   bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
   bool capturing = false;
   long slen = 0;
@@ -467,7 +470,10 @@ struct rcmdyn_engine {
     }
     t.cqv = dalloc(t, P3); t.cqc = dalloc(t, P3); t.fqv = dalloc(t, P3); t.fqc = dalloc(t, P3);
     for (int n = 0; n < hc.nsp; n++) {            // nqx = 5: qi, qr, qs (species.hip)
-      for (int b = 0; b < 2; b++) { t.a1qx[n][b] = dalloc(t, P3); t.a2qx[n][b] = dalloc(t, P3); }
+      for (int b = 0; b < (cfg.idynamic == 2 ? 1 : 2); b++) {     // the NH core: in place
+        t.a1qx[n][b] = dalloc(t, P3);
+        t.a2qx[n][b] = dalloc(t, P3);
+      }
       t.cqx[n] = dalloc(t, P3); t.fqx[n] = dalloc(t, P3);
       if (cfg.isladvec == 1) t.slqx[n] = dalloc(t, P3);
       if (cfg.idiffu == 3) t.d6qx[n] = dalloc(t, P * (kz + 1));
@@ -613,6 +619,7 @@ struct rcmdyn_engine {
     f.d6u = t.d6[0]; f.d6v = t.d6[1]; f.d6t = t.d6[2]; f.d6qv = t.d6[3]; f.d6qc = t.d6[4];
     f.d6pp = t.d6[5]; f.d6w = t.d6[6];
     f.kpbl = hc.iqxvadv == 3 ? t.kpbl : nullptr;
+    for (int n = 0; n < hc.nsp; n++) f.qxa1[n] = t.a1qx[n][c];
     return f;
   }
 
@@ -642,7 +649,8 @@ struct rcmdyn_engine {
     if (cfg.i_band != 0) throw std::runtime_error("rcmdyn: i_band = 1 (periodic tropical band) is not supported");
     if (cfg.i_crm != 0) throw std::runtime_error("rcmdyn: i_crm = 1 (periodic CRM domain) is not supported");
     if (cfg.ichem != 0) throw std::runtime_error("rcmdyn: ichem = 1 (chemical tracers) is not supported");
-    if (cfg.idynamic == 2 && cfg.nqx > 2) throw std::runtime_error("rcmdyn: nqx = 5 for idynamic = 2: not yet");
+    if (const char* m = std::getenv("RCMDYN_RCCL_CHAN2"))   // the removed second-communicator modes
+      if (std::string(m) != "one") throw std::runtime_error("rcmdyn: RCMDYN_RCCL_CHAN2 must be one (or unset)");
     // dynparam's upstream_mode (default .true., Main/mod_params.F90:646); .false. runs the
     // centred branches (Main/mod_advection.F90:141,322,409,532,624; see c.ul)
     if (cfg.upstream_mode != 0 && cfg.upstream_mode != 1)
@@ -781,15 +789,19 @@ struct rcmdyn_engine {
   }
   // a failure: the stream drains, the sticky device flags are cleared (reported once) and
   // the error is raised -- the reference's fatal (Main/mod_tendency.F90:702,
-  // Main/mod_sound.F90:679-681, Main/mod_sladvection.F90:149-154)
-  [[noreturn]] void fail(int sl, long long lc, const std::string& scope) {
+  // Main/mod_sound.F90:679-681, Main/mod_sladvection.F90:149-154).  keep: a rank-local report
+  // (check_now with a communicator) leaves the flags set, so the next job-wide reduction still
+  // carries the failure to the other ranks even if this rank's host catches the error.
+  [[noreturn]] void fail(int sl, long long lc, const std::string& scope, bool keep = false) {
     HIPCHK(hipStreamSynchronize(stream));
     pending.clear();
     gpending.clear();
-    StepState st;
-    HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
-    st.nanflag = 0; st.slflag = 0;
-    HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
+    if (!keep) {
+      StepState st;
+      HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
+      st.nanflag = 0; st.slflag = 0;
+      HIPCHK(hipMemcpy(ds, &st, sizeof(st), hipMemcpyHostToDevice));
+    }
     const std::string at = " (" + scope + std::to_string(lc) + ")";
     if (sl) throw std::runtime_error("SLADVECTION: departure point beyond one grid cell" + at);
     throw std::runtime_error("CFL VIOLATION" + at);
@@ -829,7 +841,7 @@ struct rcmdyn_engine {
     if (!comm) return;
     StepState st;
     HIPCHK(hipMemcpy(&st, ds, sizeof(st), hipMemcpyDeviceToHost));
-    if (st.nanflag || st.slflag) fail(st.slflag, hs.lcount, "this rank, by step ");
+    if (st.nanflag || st.slflag) fail(st.slflag, hs.lcount, "this rank, by step ", true);
   }
 
 
@@ -863,6 +875,7 @@ struct rcmdyn_engine {
       case FK::A1TKE: return t.a1tke; case FK::A2TKE: return t.a2tke;
       case FK::D6U: return t.d6[0]; case FK::D6V: return t.d6[1]; case FK::D6T: return t.d6[2];
       case FK::D6QV: return t.d6[3]; case FK::D6QC: return t.d6[4];
+      case FK::KPBL: return t.kpbl;
       default: break;
     }
     if (f >= FK::A1QX0 && f <= FK::D6QX2) {
@@ -1028,6 +1041,7 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
     if ((f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) || (f >= RCMDYN_XPPB_B0 && f <= RCMDYN_XWWB_BT)) bdy_dirty = true;
+    if (f == RCMDYN_KPBL) kpbl_dirty = true;
     ghosts_stale = true;
     if (f >= RCMDYN_ATM0_PS && f <= RCMDYN_CRY) invalidate_graphs();
   }
@@ -1488,6 +1502,13 @@ struct rcmdyn_engine {
       bdy_dirty = false;
       invalidate_graphs();
     }
+    if (kpbl_dirty) {
+      // the physics puts kpbl on its own points (a rank puts its interior); vadv4d ind = 3 of
+      // the fused hydrostatic step reads it on the ghost ring k_scalars computes in place of
+      // the cqv/cqc exchange (Main/mod_advection.F90:898-925)
+      xch({{FK::KPBL, 1}}, 1, 0);
+      kpbl_dirty = false;
+    }
   }
 
   // R of a tile: the column-box points whose k_columns work reads no ghost point toward a
@@ -1569,7 +1590,8 @@ struct rcmdyn_engine {
     q.nsp = hc.nsp;
     for (int n = 0; n < hc.nsp; n++) {
       q.a1[n] = t.a1qx[n][c]; q.a2[n] = t.a2qx[n][c];
-      q.b1[n] = t.a1qx[n][n1]; q.b2[n] = t.a2qx[n][n1];
+      const bool nh = cfg.idynamic == 2;
+      q.b1[n] = t.a1qx[n][nh ? c : n1]; q.b2[n] = t.a2qx[n][nh ? c : n1];
       q.cq[n] = t.cqx[n]; q.fq[n] = t.fqx[n]; q.sl[n] = t.slqx[n]; q.d6[n] = t.d6qx[n]; q.phy[n] = t.phyx[n];
     }
     q.dep = t.depx;
@@ -1631,6 +1653,8 @@ struct rcmdyn_engine {
     std::vector<XField> pro2{{FK::A2U, kz, wd}, {FK::A2V, kz, wd}, {FK::A2T, kz, wd}, {FK::A2QV, kz, wq},
                              {FK::A2QC, kz, wq}, {FK::A2PP, kz, wd}, {FK::A2W, kp, wd}};
     if (cfg.ibltyp == 2) { pro.push_back({FK::A1TKE, kp, 1}); pro2.push_back({FK::A2TKE, kp, wd}); }
+    add_qx(pro, FK::A1QX0, kz, 1);
+    add_qx(pro2, FK::A2QX0, kz, wq);
     fork_point();
     xchv(pro);
     fork_after_exchange();
@@ -1647,7 +1671,8 @@ struct rcmdyn_engine {
     if (cfg.idiffu == 3)       // the tendency kernels compute owned points only: no exchange
       each([&](Tile& t) {
         const Geom& g = t.g;
-        KLAUNCH(k_nh_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kp, 6), dim3(64), 0, stream, g, dc, nhfields(t));
+        KLAUNCH(k_nh_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kp, 6 + hc.nsp), dim3(64), 0, stream, g, dc,
+                nhfields(t), qx_args(t));
       });
     each([&](Tile& t) {
       const Geom& g = t.g;
@@ -1692,17 +1717,24 @@ struct rcmdyn_engine {
       each([&](Tile& t) { tend_d_launch(t, nhfields(t), istep); });
       side_end(1);
       side_join(0);
-      xch({{FK::CQV, kz}, {FK::CQC, kz}});
+      xchv(cq_fields());
       side_join(1);
       tke_step();
     } else {
       tke_step();
-      xch({{FK::CQV, kz}, {FK::CQC, kz}});
+      xchv(cq_fields());
     }
     each([&](Tile& t) {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
       const Grids q = grids(g);
+      if (hc.nsp) {
+        // the hydrometeors beyond qc: their fix and RAW filter in place (they feed nothing
+        // else of the step; k_nh_tend_c read atm1 for the water load before)
+        KLAUNCH(k_qx_fix, grid3(g.jdx2() - g.jdx1() + 1, g.idx2() - g.idx1() + 1, kz), BLK, 0, stream, g, dc,
+                qx_args(t));      // the column box, as the hydrostatic launch: its jci x ici fix
+        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(64), 0, stream, g, dc, qx_args(t));
+      }
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
       // tend's time filters with part A of the first acoustic sub-step (sound, :163-718)
@@ -1786,8 +1818,22 @@ struct rcmdyn_engine {
   void tend_c_launch(Tile& t, const NHFields& f, int istep) {
     const Geom& g = t.g;
     const dim3 gc((g.nj + TC_J - 1) / TC_J, (g.ni + TC_I - 1) / TC_I, cfg.kz + 1);
-    KLAUNCH(k_nh_tend_c, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
-            (int)diag, istep);
+    if (hc.nsp) {
+      KLAUNCH(k_nh_tend_c<true>, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
+              (int)diag, istep);
+      // the chains of qi, qr, qs after it on the same stream
+      KLAUNCH(k_nh_qx_tend, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, cfg.kz), BLK, 0, stream, g, dc, ds, f,
+              qx_args(t));
+    } else {
+      KLAUNCH(k_nh_tend_c<false>, NH_ZFIRST ? dim3(gc.z, gc.x, gc.y) : gc, dim3(TC_J, TC_I), 0, stream, g, dc, ds, f,
+              (int)diag, istep);
+    }
+  }
+  // the forecasts exchanged after the tendency kernels (atmc%qx, :381)
+  std::vector<XField> cq_fields() const {
+    std::vector<XField> v{{FK::CQV, cfg.kz}, {FK::CQC, cfg.kz}};
+    add_qx(v, FK::CQX0, cfg.kz, 1);
+    return v;
   }
 
   // bdyval, non-hydrostatic: u, v, t, qv as the hydrostatic core (p* untouched), pp and w,
@@ -2255,10 +2301,13 @@ struct rcmdyn_engine {
     for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
   }
 
-  // rcmdyn_exchange_plan: the communication calls of prepare + nsteps x (tend + bdyval), the
-  // eager step sequence every rank runs (graph replay issues the same calls in the same order)
+  // rcmdyn_exchange_plan: the communication calls of put + bdyval + nsteps x (tend + bdyval),
+  // the drop-in's start (the initial bdyval after the state put, with its slice exchange) and
+  // the eager step sequence every rank runs (graph replay issues the same calls in the same order)
   void plan_run(int nsteps) {
     prepare();
+    ghosts_stale = true;           // as after rcmdyn_put
+    bdyval();
     for (int s = 0; s < nsteps; s++) {
       step_once();
       note_step(hs.lcount, s == nsteps - 1);
@@ -2356,20 +2405,41 @@ int guard(rcmdyn_t* h, F fn) {
 
 extern "C" {
 
-// RCMDYN_SEGV_TRACE=1: print the native backtrace of a segmentation fault (host debugging aid)
-static void segv_trace(int sig) {
+// RCMDYN_SEGV_TRACE=1 (opt-in host debugging aid): print the native backtrace of a
+// segmentation fault, then hand the signal to the handler that was installed before (Python's
+// faulthandler, a host's own), or the default action
+static struct sigaction g_prev_segv;
+static void segv_trace(int sig, siginfo_t* info, void* uc) {
   void* bt[64];
   const int n = backtrace(bt, 64);
   const char msg[] = "rcmdyn: fatal signal, native backtrace:\n";
   (void)!write(2, msg, sizeof(msg) - 1);
   backtrace_symbols_fd(bt, n, 2);
-  std::signal(sig, SIG_DFL);
+  sigaction(sig, &g_prev_segv, nullptr);
+  if (g_prev_segv.sa_flags & SA_SIGINFO) {
+    if (g_prev_segv.sa_sigaction) { g_prev_segv.sa_sigaction(sig, info, uc); return; }
+  } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+    g_prev_segv.sa_handler(sig);
+    return;
+  }
   std::raise(sig);
+}
+static void install_segv_trace() {
+  static bool done = false;
+  if (done || !std::getenv("RCMDYN_SEGV_TRACE")) return;
+  done = true;
+  void* warm[1];
+  (void)backtrace(warm, 1);           // loads the unwinder now: backtrace's first call allocates
+  struct sigaction sa {};
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO | SA_NODEFER;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
 }
 
 int rcmdyn_create(const rcmdyn_config* cfg, rcmdyn_t** out) {
   if (!cfg || !out) { g_last_error = "rcmdyn_create: null argument"; return 1; }
-  if (std::getenv("RCMDYN_SEGV_TRACE")) std::signal(SIGSEGV, segv_trace);
+  install_segv_trace();
   auto* h = new rcmdyn_engine();
   int rc = guard(h, [&] { h->create(cfg); });
   if (rc) {

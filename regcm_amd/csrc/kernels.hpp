@@ -160,6 +160,11 @@ __global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restri
 __global__ void k_qx_tend(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f, QxArgs q);
 __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q);
 __global__ void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q);
+struct NHFields;
+// the non-hydrostatic chains of the same hydrometeors (in place; k_qx_fix / k_qx_serial then
+// run with b* = a*)
+__global__ void k_nh_qx_tend(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f,
+                             QxArgs q);
 // bdyval's boundary copies and inflow/outflow of the hydrometeors beyond qc (both cores);
 // integ: 1 integrating, 0 the initial call, -1 from the step clock (lcount > 0)
 __global__ void k_bdyval_qx(Geom g, const StepState* __restrict__ s, QxArgs q, int integ, int do_qc,

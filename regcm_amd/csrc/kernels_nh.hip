@@ -15,6 +15,7 @@
 // section 4.2 lists the kernels with their roofline position.
 #include "engine.hpp"
 #include "kernels_nh.hpp"
+#include "kernels.hpp"
 #include "fastmath.hpp"
 #include "devcommon.hpp"
 
@@ -229,13 +230,15 @@ __device__ __forceinline__ double diffx_at(const Geom& g, const Consts* c, doubl
 // and w (1..kz+1; diffu_x3df reads xkc on level kz+1, one past its kz levels -- the
 // coefficient is diff_6th_coef * p*b on every level, as xkcf holds it), from the decoupled
 // atm2 fields of mkslice (Main/mod_slice.F90:163-183, 215-238).  blockIdx.z: 0 u and v, 1 t,
-// 2 qv, 3 qc, 4 pp, 5 w; blockIdx.y = level.  k_nh_tend_c / k_nh_tend_d add them in the
-// reference's place of the diffusion term.
-__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f) {
+// 2 qv, 3 qc, 4 pp, 5 w, 6.. qi, qr, qs (nqx = 5); blockIdx.y = level.  k_nh_tend_c /
+// k_nh_tend_d / k_nh_qx_tend add them in the reference's place of the diffusion term.
+__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs qx) {
   const int i = g.ide1 + (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
-  const int q = (int)blockIdx.z, kz = c->kz;
+  const int q0 = (int)blockIdx.z, kz = c->kz;
+  const int q = q0 >= 6 ? 3 : q0;                  // the species take qc's clip and stencil
   const double* ps = f.psb;
-  double* d6 = q == 0 ? f.d6u : q == 1 ? f.d6t : q == 2 ? f.d6qv : q == 3 ? f.d6qc : q == 4 ? f.d6pp : f.d6w;
+  double* d6 = q0 >= 6 ? qx.d6[q0 - 6]
+               : q == 0 ? f.d6u : q == 1 ? f.d6t : q == 2 ? f.d6qv : q == 3 ? f.d6qc : q == 4 ? f.d6pp : f.d6w;
   if (k > (q == 5 ? kz + 1 : kz)) return;
   if (q == 0) {
     const int j = g.jdi2;
@@ -250,7 +253,7 @@ __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f) {
   }
   const int j = g.jci2;
   if (!in(i, g.ici1, g.ici2)) return;
-  const double* a = q == 1 ? f.a2t : q == 2 ? f.a2qv : q == 3 ? f.a2qc : q == 4 ? f.a2pp : f.a2w;
+  const double* a = q0 >= 6 ? qx.a2[q0 - 6] : q == 1 ? f.a2t : q == 2 ? f.a2qv : q == 3 ? f.a2qc : q == 4 ? f.a2pp : f.a2w;
   auto fv = [&](int jj, int ii) {
     const double v = F3(a, jj, ii, k) * (d_one / F2(ps, jj, ii));
     return q == 2 ? dmax(v, MINQQ) : (q == 3 ? dmax(v, d_zero) : v);
@@ -320,6 +323,7 @@ constexpr int TC_NF = 5;
 #ifndef TC_W
 #define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
 #endif
+template <bool QX>
 __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
                                                    int istep) {
@@ -384,6 +388,16 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     return hadv_v(c, x[0], x[1], x[2], x[3], x[4], u1, u2, v1, v2, xmf, ps, lim);
   };
   auto xqcat = [&](int kk) { return dmax(F3(f.a1qc, j, i, kk) * r0, d_zero); };
+  // the water load qcd: qc, or with nqx = 5 the sum over iqfrst..iqlst (decouple, :1107-1115)
+  auto xqload = [&](int kk) {
+    if constexpr (QX) {
+      double w = d_zero + xqcat(kk);
+      for (int n = 0; n < NQXH; n++) w = w + dmax(F3(f.qxa1[n], j, i, kk) * r0, d_zero);
+      return w;
+    } else {
+      return xqcat(kk);
+    }
+  };
   auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
     u1 = F3(f.a1u, j, i + 1, kk) * m01 + F3(f.a1u, j, i, kk) * m00;          // umc = atm1 u * msfd
     u2 = F3(f.a1u, j + 1, i + 1, kk) * m11 + F3(f.a1u, j + 1, i, kk) * m10;
@@ -453,7 +467,7 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
           (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
           ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
           (F3(f.a1w, j, i, k) * r0) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
-      wd = wd - EGRAV_NH * ps * (c->twt2[k] * xqcat(k - 1) + c->twt1[k] * xqcat(k));
+      wd = wd - EGRAV_NH * ps * (c->twt2[k] * xqload(k - 1) + c->twt1[k] * xqload(k));
     }
     double wt0 = d_zero;
     if (sponge) wt0 = wsp * d_zero + (d_one - wsp) * F3(f.wwbt, j, i, k);
@@ -572,6 +586,11 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     F3(f.cqc, j, i, k) = F3(f.a2qc, j, i, k) + dt * qc;
   }
 }
+
+template __global__ void k_nh_tend_c<false>(Geom, const Consts* __restrict__, const StepState* __restrict__, NHFields,
+                                             int, int);
+template __global__ void k_nh_tend_c<true>(Geom, const Consts* __restrict__, const StepState* __restrict__, NHFields,
+                                            int, int);
 
 // k_nh_tend_d stages its horizontal stencil operands of one level for a 64 x 4 block plus a
 // 2-point halo in LDS, one load (and for ubd/msfd, vbd/msfd one division) per staged point:

@@ -48,6 +48,8 @@ struct NHFields {
                                  // doubles as ordered bits), reduced by k_nh_advance
   unsigned long long* cfll;      // the same for the last acoustic sub-step alone (the value
                                  // the reference reports, Main/mod_sound.F90:634-646)
+  // nqx = 5: atm1 qi, qr, qs (the water load of the adiabatic w term; null for nqx = 2)
+  const double* qxa1[NQXH];
 };
 constexpr int NH_CFL_SLOTS = 1024;
 // block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,
@@ -67,10 +69,12 @@ constexpr int NH_CFL_SLOTS = 1024;
 #define NH_ZFIRST 1
 #endif
 
-__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f);
+struct QxArgs;
+__global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs q);
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f);
+template <bool QX>
 __global__ void k_nh_tend_c(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int wdiag, int istep);
 __global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep);
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);

@@ -20,10 +20,15 @@
 //              i-major, j-minor order;
 //  k_bdyval_qx bdyval's atm2 = atm1 boundary copies, then the inflow/outflow lines.
 //
+// The non-hydrostatic core (k_nh_qx_tend) adds the atmx%qx * cr term of adiabatic
+// (Main/mod_tendency.F90:1615-1617) and updates the state in place: k_qx_fix / k_qx_serial then
+// filter into the same buffers (each thread reads and writes only its own point's levels).
+//
 // Transcendental-free: every result is bit-identical to the oracle's restatement
 // (-ffp-contract=off).
 #include "engine.hpp"
 #include "kernels.hpp"
+#include "kernels_nh.hpp"
 #include "devcommon.hpp"
 #include "qxcommon.hpp"
 
@@ -165,6 +170,80 @@ __global__ __launch_bounds__(QBT) void k_qx_tend(Geom g, const Consts* __restric
   }
 }
 
+// K_QX1 (non-hydrostatic).  The hydrometeor chains of k_nh_tend_c's qc (kernels_nh.hip) for
+// qi, qr, qs at the interior cross points (owned points only, as the NH tendency kernels):
+// hadvqx, vadv4d ind 1 / 3, + atmx%qx * cr (:1615-1617), diffu_x4d on the scaled xkcr, the
+// sums with qxphy, the forecast; the ring jce \ jci takes atm2.
+__global__ __launch_bounds__(256) void k_nh_qx_tend(Geom g, const Consts* __restrict__ c,
+                                                    const StepState* __restrict__ s, NHFields f, QxArgs q) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!(in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2))) return;
+  const int nsp = q.nsp, kz = c->kz;
+  if (!(in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))) {
+    for (int n = 0; n < nsp; n++) F3(q.cq[n], j, i, k) = F3(q.a2[n], j, i, k);
+    return;
+  }
+  const double dt = s->dt;
+  const double xmf = F2(f.xmsf, j, i), ps = F2(f.psa, j, i), pbs = F2(f.psb, j, i);
+  const double m00 = F2(f.msfd, j, i), m01 = F2(f.msfd, j, i + 1), m10 = F2(f.msfd, j + 1, i),
+               m11 = F2(f.msfd, j + 1, i + 1);
+  // start_advect's mass fluxes (umc = atm1 u * msfd)
+  const double u1 = F3(f.a1u, j, i + 1, k) * m01 + F3(f.a1u, j, i, k) * m00;
+  const double u2 = F3(f.a1u, j + 1, i + 1, k) * m11 + F3(f.a1u, j + 1, i, k) * m10;
+  const double v1 = F3(f.a1v, j + 1, i, k) * m10 + F3(f.a1v, j, i, k) * m00;
+  const double v2 = F3(f.a1v, j + 1, i + 1, k) * m11 + F3(f.a1v, j, i + 1, k) * m01;
+  const double r0 = F2(f.rpsa, j, i), rw = F2(f.rpsa, j - 1, i), re = F2(f.rpsa, j + 1, i),
+               rs = F2(f.rpsa, j, i - 1), rn = F2(f.rpsa, j, i + 1);
+  const double cr = F3(f.cr, j, i, k);
+  const double xkc = F3(f.xkcr, j, i, k) * c->rdxsq * pbs;      // calc_coeff's xkc
+  const double thr = MINQQ * MINQQ * ps;
+  const int kpb = f.kpbl ? (int)F2(f.kpbl, j, i) : 0;
+  for (int n = 0; n < nsp; n++) {
+    const double* a = q.a1[n];
+    double cd;
+    if (c->isladvec) {
+      cd = d_zero + F3(q.sl[n], j, i, k);
+    } else {
+      const double xc = dmax(F3(a, j, i, k) * r0, d_zero), xw = dmax(F3(a, j - 1, i, k) * rw, d_zero);
+      const double xe = dmax(F3(a, j + 1, i, k) * re, d_zero), xs = dmax(F3(a, j, i - 1, k) * rs, d_zero);
+      const double xn = dmax(F3(a, j, i + 1, k) * rn, d_zero);
+      cd = d_zero + hadv_flux(c, xmf, ps, u1, u2, v1, v2, xc, xw, xe, xs, xn, 0);
+    }
+    auto cflux = [&](int kk) {
+      const double svv = F3(f.qdot, j, i, kk);
+      const double fk = F3(a, j, i, kk), fkm = F3(a, j, i, kk - 1);
+      if (f.kpbl) return uw_fg(c, kk, kpb, fk, fkm, [&](int qq) { return F3(a, j, i, qq); }) * svv;
+      if (svv > d_zero) return (fkm > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+      return (fk > thr) ? svv * (c->twt1[kk] * fk + c->twt2[kk] * fkm) : d_zero;
+    };
+    if (k >= 2) cd = cd + cflux(k) * c->xds[k];
+    if (k + 1 <= kz) cd = cd - cflux(k + 1) * c->xds[k];
+    cd = cd + dmax(F3(a, j, i, k) * r0, d_zero) * cr;
+    if (c->idiffu == 3) {
+      if (j == g.jci2) cd = cd + F3(q.d6[n], j, i, k);
+    } else {
+      // diffu_x4d on mkslice's qxb3d = max(atm2 * (1/psb), 0), Main/mod_diffusion.F90:792-947
+      const double* b = q.a2[n];
+      auto fb = [&](int dj, int di) {
+        return dmax(F3(b, j + dj, i + di, k) * F2(f.rpsb, j + dj, i + di), d_zero);
+      };
+      if (c->idiffu == 2) {
+        cd = cd + d_one * xkc * (o4_c1 * (fb(1, 0) + fb(-1, 0) + fb(0, 1) + fb(0, -1)) +
+                                 o4_c2 * (fb(1, 1) + fb(-1, -1) + fb(-1, 1) + fb(1, -1)) + o4_c3 * fb(0, 0));
+      } else {
+        if (in(j, g.jcii1, g.jcii2) && in(i, g.icii1, g.icii2))
+          cd = cd - d_one * xkc * (z4_c1 * (fb(2, 0) + fb(-2, 0) + fb(0, 2) + fb(0, -2)) +
+                                   z4_c2 * (fb(1, 0) + fb(-1, 0) + fb(0, 1) + fb(0, -1)) + z4_c3 * fb(0, 0));
+        const double lap = z4_c1 * (fb(1, 0) + fb(-1, 0) + fb(0, 1) + fb(0, -1)) + z4_c2 * fb(0, 0);
+        const int nb = (g.bl && j == g.jci1) + (g.br && j == g.jci2) + (g.bb && i == g.ici1) + (g.bt && i == g.ici2);
+        for (int r = 0; r < nb; r++) cd = cd + d_one * xkc * lap;
+      }
+    }
+    const double qt = d_zero + cd + (q.phy[n] ? F3(q.phy[n], j, i, k) : d_zero);
+    F3(q.cq[n], j, i, k) = F3(q.a2[n], j, i, k) + dt * qt;
+  }
+}
+
 // K_QX2.  The negative-moisture fix (:382-393) and filter_raw_4d (:426-427, gnu2, the zero
 // floor) of the hydrometeors beyond qc on the owned interior jci x ici, into the next buffers; the
 // copies of the column box's other points (atm1, and atm2 on owned points: bdyval and the next
@@ -180,8 +259,10 @@ __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q) {
   for (int n = 0; n < q.nsp; n++) {
     const double a1 = LD(q.a1[n], o3), a2 = LD(q.a2[n], o3);
     if (!ci) {
-      ST(q.b1[n], o3, a1);
-      if (own) ST(q.b2[n], o3, a2);
+      if (q.b1[n] != q.a1[n]) {             // the NH core filters in place: nothing to keep
+        ST(q.b1[n], o3, a1);
+        if (own) ST(q.b2[n], o3, a2);
+      }
       continue;
     }
     double v = LD(q.cq[n], o3);

@@ -8,11 +8,6 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# a segmentation fault inside the engine prints its native backtrace (rcmdyn_create installs
-# the handler; engine.hip segv_trace)
-os.environ.setdefault("RCMDYN_SEGV_TRACE", "1")
-
-
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP engine C-ABI)")
 

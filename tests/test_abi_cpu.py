@@ -125,6 +125,19 @@ def test_create_refuses_unbuilt_options(opt, msg):
         dycore.DynCore(rc, data["split"])
 
 
+@pytest.mark.parametrize("mode", ["init", "split", "two"])
+def test_create_refuses_removed_rccl_channel_modes(monkeypatch, mode):
+    """RCMDYN_RCCL_CHAN2 has one mode left ("one": both streams share the job's communicator);
+    the removed second-communicator modes and any other value fail rcmdyn_create."""
+    from regcm_amd.config import CONFIGS
+    from regcm_amd import icbc
+    monkeypatch.setenv("RCMDYN_RCCL_CHAN2", mode)
+    rc = CONFIGS["C1"]
+    data = icbc.generate(rc)
+    with pytest.raises(dycore.EngineError, match="RCMDYN_RCCL_CHAN2"):
+        dycore.DynCore(rc, data["split"])
+
+
 def test_field_enum_matches_header_python_fortran():
     """rcmdyn_field order is one contract for C, the Python host and the Fortran shim."""
     from regcm_amd.config import FIELD_NAMES

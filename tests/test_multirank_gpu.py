@@ -17,8 +17,9 @@ from regcm_amd import icbc
 pytestmark = pytest.mark.gpu
 
 
-def run_ranks(rc, data, cj, ci, nsteps, group):
-    """Run nsteps on cj x ci ranks (threads); returns the engines (still open)."""
+def run_ranks(rc, data, cj, ci, nsteps, group, per_rank=None):
+    """Run nsteps on cj x ci ranks (threads); returns the engines (still open).  per_rank(e, r)
+    runs after the state put (a rank's own puts)."""
     import gc
     from regcm_amd.dycore import DynCore
     gc.collect()            # engines of earlier tests are destroyed here, not in a rank thread
@@ -34,6 +35,8 @@ def run_ranks(rc, data, cj, ci, nsteps, group):
     def work(e):
         try:
             e.put_state(data["state"])
+            if per_rank:
+                per_rank(e, engs.index(e))
             e.bdyval()
             e.step(nsteps)
             e.synchronize()
@@ -118,3 +121,36 @@ def test_job_reductions_over_ranks():
     for o in out:
         assert o is not None and o == out[0]
         assert abs(o[0] - ref[0]) <= 1e-12 * abs(ref[0]) and abs(o[1] - ref[1]) <= 1e-12 * abs(ref[1])
+
+
+def test_uw_kpbl_put_on_own_points():
+    """iuwvadv = 1 with each rank putting kpbl on its own cross points only (as the physics
+    computes it): vadv4d ind = 3 of the fused step reads kpbl on the ghost ring
+    k_scalars computes in place of the cqv/cqc exchange, so the engine exchanges a put kpbl once
+    before the next tend.  Bit-identical to the single tile with the global put."""
+    import dataclasses
+    from regcm_amd.dycore import tile_extent
+    rc = dataclasses.replace(CONFIGS["C1"], ibltyp=2, iuwvadv=1)
+    base = icbc.generate(CONFIGS["C1"])
+    st = dict(base["state"], **icbc.tke_state(rc))
+    st.update(icbc.hydrometeor_state(rc, st, nqx=2))
+    rng = np.random.default_rng(5)
+    kpbl = rng.integers(1, rc.kz + 1, size=(1, rc.iy, rc.jx)).astype(np.float64)
+    cj, ci = 2, 2
+
+    def own_kpbl(e, r):
+        ext, _ = tile_extent(rc.jx, rc.iy, cj, ci, r)
+        j1, j2, i1, i2 = ext[4], ext[5], ext[6], ext[7]
+        e.put("KPBL", kpbl[:, i1 - 1:i2, j1 - 1:j2], j1=j1, i1=i1)
+
+    data = {"split": base["split"], "state": st}
+    engs = run_ranks(rc, data, cj, ci, 4, "uwk", per_rank=own_kpbl)
+    # the reference: the same 2 x 2 tiles in one engine with the global put (the moisture fix
+    # of the cloud edges depends on the decomposition, as the reference's)
+    from regcm_amd.dycore import DynCore
+    ref = DynCore(rc, base["split"], nproc_j=cj, nproc_i=ci)
+    ref.put_state(dict(st, KPBL=kpbl))
+    ref.bdyval()
+    ref.step(4)
+    for f in STATE_FIELDS:
+        assert np.array_equal(gather(engs, f), ref.get(f)), f

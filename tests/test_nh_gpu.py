@@ -15,15 +15,16 @@ import dataclasses
 import numpy as np
 import pytest
 
-from regcm_amd.config import CONFIGS, NH_STATE_FIELDS
+from regcm_amd.config import CONFIGS, NH_STATE_FIELDS, QX_STATE_FIELDS
 from regcm_amd import icbc
+from tests.test_parity_gpu import with_species
 
 pytestmark = pytest.mark.gpu
 
 NH_FIELDS = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_U", "ATM2_V", "ATM2_T",
              "ATM2_QV", "ATM2_QC", "PSA", "PSB"] + NH_STATE_FIELDS
 CROSS = {"ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_T", "ATM2_QV", "ATM2_QC", "PSA", "PSB",
-         "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"}
+         "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"} | set(QX_STATE_FIELDS)
 
 
 def relerr(a, b, rc, name):
@@ -45,8 +46,9 @@ def make_pair(rc, data):
     from regcm_amd.dycore import DynCore
     o = OracleCore(rc, data["split"])
     e = DynCore(rc, data["split"])
-    o.put_state(data["state"])
-    e.put_state(data["state"])
+    st = with_species(rc, data["state"])
+    o.put_state(st)
+    e.put_state(st)
     o.bdyval()
     e.bdyval()
     return o, e
@@ -118,9 +120,10 @@ def test_nh_rest_state():
 
 
 NH_VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"idiffu": 2}, {"idiffu": 3}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1},
-               {"upstream_mode": 0}, {"stability_enhance": 0}]
-# idiffu = 3 depends on the decomposition as the reference's does (test_nh_idiffu3_tiles)
-NH_DECOMP_VARIANTS = [v for v in NH_VARIANTS if v.get("idiffu") != 3]
+               {"upstream_mode": 0}, {"stability_enhance": 0}, {"ipptls": 2}]
+# idiffu = 3 depends on the decomposition as the reference's does (test_nh_idiffu3_tiles), and
+# so does the fix of negative forecasts at tile edges (ipptls = 2: tests/test_species_gpu.py)
+NH_DECOMP_VARIANTS = [v for v in NH_VARIANTS if v.get("idiffu") != 3 and "ipptls" not in v]
 
 
 @pytest.mark.parametrize("variant", NH_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
@@ -128,10 +131,11 @@ def test_nh_variant_parity(nh_data, variant):
     rc, data = nh_data
     rcv = dataclasses.replace(rc, **variant)
     o, e = make_pair(rcv, data)
+    fields = NH_FIELDS + (QX_STATE_FIELDS if rcv.nqx > 2 else [])
     for nsteps, tol in ((1, 1e-11), (2, 1e-10)):
         o.step(nsteps)
         e.step(nsteps)
-        for name in NH_FIELDS:
+        for name in fields:
             err = relerr(e.get(name), o.get(name), rcv, name)
             assert err < tol, (name, err, nsteps)
 

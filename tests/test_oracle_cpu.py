@@ -1623,3 +1623,76 @@ def test_centred_advection_equals_upstream_without_offcentring(core, c1_data):
     for n in names:
         assert np.array_equal(runs[0][n], runs[1][n]), n
     assert any(not np.array_equal(runs[0][n], runs[2][n]) for n in names)
+
+
+def _species_run(rc, data, st, nsteps):
+    from oracle.oracle import OracleCore
+    o = OracleCore(rc, data["split"])
+    o.put_state(st)
+    o.bdyval()
+    o.step(nsteps)
+    return o
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_oracle_species_follow_qc_chain(c1_data, core):
+    """nqx = 5 (ipptls = 2): every hydrometeor n = iqfrst..iqlst runs qc's chain of the dyn step
+    (hadvqx, vadv4d, diffu_x4d, the NH + atmx%qx*cr, the fix, filter_raw_4d's zero floor,
+    bdyval's copies and inflow/outflow), Main/mod_tendency.F90:331-335, 375-393, 426-427,
+    1378-1388, 1526, 1615-1617; Main/mod_bdycod.F90:1143-1284, 2153-2220.  With qi = qr = qs = qc
+    at the start, the four stay bit-identical over the steps (the restatement's species loop
+    against its qc code)."""
+    import dataclasses
+    if core == "nh":
+        rc = dataclasses.replace(CONFIGS["N1"], ipptls=2)
+        data = icbc.generate_nh(rc)
+    else:
+        rc = dataclasses.replace(c1_data[0], ipptls=2)
+        data = c1_data[1]
+    st = dict(data["state"])
+    st.update(icbc.hydrometeor_state(rc, st, nqx=5))
+    for lev in ("ATM1", "ATM2"):
+        for sp in ("QI", "QR", "QS"):
+            st[f"{lev}_{sp}"] = st[f"{lev}_QC"].copy()
+    o = _species_run(rc, data, st, 3)
+    for lev in ("ATM1", "ATM2"):
+        qc = o.get(f"{lev}_QC")
+        assert np.abs(qc - st[f"{lev}_QC"]).max() > 0.0
+        for sp in ("QI", "QR", "QS"):
+            assert np.array_equal(o.get(f"{lev}_{sp}"), qc), (lev, sp)
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_oracle_species_water_load(c1_data, core):
+    """The total water load of decouple, qcd = ((qc + qi) + qr) + qs (Main/mod_tendency.F90:
+    1107-1115), is what tvfac (:2037, hydrostatic) and the NH water loading of w (:1662-1671) read:
+    an ipptls = 2 start with qi = qc, qr = qs = 0 loads 2 qc exactly, so its first step's
+    winds, temperature, p* (and NH pp, w) equal those of an ipptls = 1 start with qc doubled."""
+    import dataclasses
+    if core == "nh":
+        rc1 = CONFIGS["N1"]
+        data = icbc.generate_nh(rc1)
+        dyn = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA", "ATM1_PP", "ATM1_W"]
+    else:
+        rc1, data = c1_data
+        dyn = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "PSA"]
+    rc2 = dataclasses.replace(rc1, ipptls=2)
+    st = dict(data["state"])
+    st.update(icbc.hydrometeor_state(rc2, st, nqx=5))
+    st2 = dict(st)
+    st1 = {k: v for k, v in st.items() if k[5:] not in ("QI", "QR", "QS")}
+    for lev in ("ATM1", "ATM2"):
+        st2[f"{lev}_QI"] = st[f"{lev}_QC"].copy()
+        st2[f"{lev}_QR"] = np.zeros_like(st[f"{lev}_QC"])
+        st2[f"{lev}_QS"] = np.zeros_like(st[f"{lev}_QC"])
+        st1[f"{lev}_QC"] = 2.0 * st[f"{lev}_QC"]
+    o2 = _species_run(rc2, data, st2, 1)
+    o1 = _species_run(rc1, data, st1, 1)
+    for name in dyn:
+        assert np.array_equal(o2.get(name), o1.get(name)), name
+    # and the load matters: the same start without the species differs
+    st0 = {k: v for k, v in st1.items()}
+    for lev in ("ATM1", "ATM2"):
+        st0[f"{lev}_QC"] = st[f"{lev}_QC"]
+    o0 = _species_run(rc1, data, st0, 1)
+    assert not np.array_equal(o0.get("ATM1_U"), o1.get("ATM1_U"))

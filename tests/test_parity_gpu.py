@@ -8,13 +8,14 @@ max-norm of 1e-12 after one step, growing with the step count as stated per test
 import numpy as np
 import pytest
 
-from regcm_amd.config import CONFIGS, STATE_FIELDS
+from regcm_amd.config import CONFIGS, QX_STATE_FIELDS, STATE_FIELDS
 from regcm_amd import icbc
 
 pytestmark = pytest.mark.gpu
 
 CROSS = {"ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_T", "ATM2_QV", "ATM2_QC", "PSA", "PSB",
-         "DSTOR", "HSTOR", "PSC", "PTEN", "TTEN", "QVTEN", "QCTEN", "OMEGA", "QDOT", "XKC", "PHI"}
+         "DSTOR", "HSTOR", "PSC", "PTEN", "TTEN", "QVTEN", "QCTEN", "OMEGA", "QDOT", "XKC", "PHI"} | \
+    set(QX_STATE_FIELDS)
 
 
 def relerr(a, b, rc, name):
@@ -25,13 +26,27 @@ def relerr(a, b, rc, name):
     return float(np.max(np.abs(a - b)) / den)
 
 
+def with_species(rc, state):
+    """ipptls = 2: the state with patchy qi, qr, qs layers (icbc.hydrometeor_state)."""
+    if rc.nqx <= 2:
+        return state
+    st = dict(state)
+    st.update(icbc.hydrometeor_state(rc, st, nqx=rc.nqx))
+    return st
+
+
+def state_fields(rc):
+    return list(STATE_FIELDS) + (QX_STATE_FIELDS if rc.nqx > 2 else [])
+
+
 def make_pair(rc, data, nproc_j=1, nproc_i=1):
     from oracle.oracle import OracleCore
     from regcm_amd.dycore import DynCore
     o = OracleCore(rc, data["split"])
     e = DynCore(rc, data["split"], nproc_j=nproc_j, nproc_i=nproc_i)
-    o.put_state(data["state"])
-    e.put_state(data["state"])
+    st = with_species(rc, data["state"])
+    o.put_state(st)
+    e.put_state(st)
     o.bdyval()
     e.bdyval()
     return o, e
@@ -379,10 +394,13 @@ def test_negative_moisture_serial_sweep(c1_data):
 
 # namelist options beyond the defaults, each against the oracle and under decomposition
 VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"iboudy": 1}, {"ipgf": 1}, {"idiffu": 2}, {"idiffu": 3}, {"isladvec": 1},
-            {"isladvec": 1, "iqmsl": 0}, {"upstream_mode": 0}, {"stability_enhance": 0}, {"diffu_hgtf": 0}]
+            {"isladvec": 1, "iqmsl": 0}, {"upstream_mode": 0}, {"stability_enhance": 0}, {"diffu_hgtf": 0},
+            {"ipptls": 2}]
 # idiffu = 3 acts on each tile's last interior column, so its result depends on the
-# decomposition as the reference's does (test_idiffu3_tiles_match_oracle_tiles)
-DECOMP_VARIANTS = [v for v in VARIANTS if v.get("idiffu") != 3]
+# decomposition as the reference's does (test_idiffu3_tiles_match_oracle_tiles); so does the
+# moisture fix with negative forecasts at tile edges (ipptls = 2's cloud edges,
+# tests/test_species_gpu.py compares those against the oracle's tiles)
+DECOMP_VARIANTS = [v for v in VARIANTS if v.get("idiffu") != 3 and "ipptls" not in v]
 
 
 def _variant_id(v):
@@ -403,18 +421,18 @@ def test_variant_parity(c1_data, variant):
     for nsteps, tol in ((1, 1e-12), (2, 1e-11)):
         o.step(nsteps)
         e.step(nsteps)
-        for name in STATE_FIELDS:
+        for name in state_fields(rcv):
             err = relerr(e.get(name), o.get(name), rcv, name)
             assert err < tol, (name, err, nsteps)
     o.step(17)
     e.step(17)
-    st = {k: v.copy() for k, v in data["state"].items()}
+    st = {k: v.copy() for k, v in with_species(rcv, data["state"]).items()}
     st["ATM1_T"] = st["ATM1_T"] * (1.0 + 1e-14)
     p = OracleCore(rcv, data["split"])
     p.put_state(st)
     p.bdyval()
     p.step(20)
-    for name in STATE_FIELDS:
+    for name in state_fields(rcv):
         err = relerr(e.get(name), o.get(name), rcv, name)
         spread = relerr(p.get(name), o.get(name), rcv, name)
         assert err <= max(1e-9, 100.0 * spread), (name, err, spread)

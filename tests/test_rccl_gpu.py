@@ -60,18 +60,13 @@ def test_rccl_transport_hydrostatic(c1_data, monkeypatch, mode):
     assert np.allclose(a[:2], b[:2], rtol=1e-12, atol=0), (a, b)   # tile partials summed in another order
 
 
-@pytest.mark.parametrize("chan2", ["one", "init"])
-def test_rccl_second_channel(c1_data, monkeypatch, chan2):
-    """The second stream's communicator (RCMDYN_RCCL_CHAN2): "one" (default) both streams on
-    the first with the second stream's exchange ordered after the first's; "init" a second
-    communicator, which crashes a graph-captured step under torch's bundled RCCL 2.26, so it
-    runs eagerly here.  Bit-identical to one tile."""
+def test_rccl_shared_channel(c1_data, monkeypatch):
+    """Both streams on the job's one communicator (RCMDYN_RCCL_CHAN2=one, the only mode), the
+    second stream's exchange ordered after the first's.  Bit-identical to one tile."""
     rc, data = c1_data
     one = _engine(rc, data)
     monkeypatch.setenv("RCMDYN_FORCE_RCCL", "1")
-    monkeypatch.setenv("RCMDYN_RCCL_CHAN2", chan2)
-    if chan2 != "one":
-        monkeypatch.setenv("RCMDYN_RCCL_EAGER", "1")
+    monkeypatch.setenv("RCMDYN_RCCL_CHAN2", "one")
     dec = _engine(rc, data, 2, 2)
     one.step(6)
     dec.step(6)

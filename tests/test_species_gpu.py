@@ -276,3 +276,104 @@ def test_species_fields_refused_for_nqx2(c1_data):
         e.put("ATM1_QI", np.zeros((rc.kz, rc.iy, rc.jx)))
     with pytest.raises(EngineError, match="nqx = 5"):
         e.get("ATM2_QS")
+
+
+# ----------------------------------------------------------------- non-hydrostatic core
+# The NH chain of the species (k_nh_qx_tend): hadvqx, vadv4d, + atmx%qx * cr of adiabatic
+# (Main/mod_tendency.F90:1615-1617), diffu_x4d, the sums, the forecast, the exchange of atmc%qx,
+# the fix and filter_raw_4d in place; the total load enters the water loading of w
+# (:1662-1671).  Tolerances as tests/test_nh_gpu.py (the NH step is transcendental almost
+# everywhere: 1e-11 after one step, 1e-10 after three).
+NH_ALL = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_U", "ATM2_V", "ATM2_T", "ATM2_QV", "ATM2_QC",
+          "PSA", "PSB", "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"] + QX_STATE_FIELDS
+NH_CROSS = CROSS | {"ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W"}
+
+
+def nh_relerr(a, b, rc, name):
+    if name in NH_CROSS:
+        a = a[:, : rc.iy - 1, : rc.jx - 1]
+        b = b[:, : rc.iy - 1, : rc.jx - 1]
+    den = max(np.max(np.abs(b)), 1e-300)
+    return float(np.max(np.abs(a - b)) / den)
+
+
+@pytest.fixture(scope="module")
+def qx_n1():
+    rc = dataclasses.replace(CONFIGS["N1"], ipptls=2)
+    data = icbc.generate_nh(rc)
+    return rc, data, species_state(rc, data)
+
+
+NH_VARIANTS = [{}, {"isladvec": 1}, {"idiffu": 2}, {"idiffu": 3}, {"iboudy": 4}]
+
+
+@pytest.mark.parametrize("variant", NH_VARIANTS, ids=_vid)
+def test_nh_species_parity(qx_n1, variant):
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    rc, data, st = qx_n1
+    rcv = dataclasses.replace(rc, **variant)
+    o, e = start(OracleCore, rcv, data, st), start(DynCore, rcv, data, st)
+    for nsteps, tol in ((1, 1e-11), (2, 1e-10)):
+        o.step(nsteps)
+        e.step(nsteps)
+        for name in NH_ALL:
+            err = nh_relerr(e.get(name), o.get(name), rcv, name)
+            assert err < tol, (name, err, nsteps)
+
+
+def test_nh_species_change_the_step(qx_n1):
+    """The species' load reaches w through the water loading: an ipptls = 2 run differs from
+    ipptls = 1 with the same qv, qc."""
+    from regcm_amd.dycore import DynCore
+    rc, data, st = qx_n1
+    e = start(DynCore, rc, data, st)
+    e.step(2)
+    assert not np.array_equal(e.get("ATM1_QR"), st["ATM1_QR"])
+    rc1 = dataclasses.replace(rc, ipptls=1)
+    st1 = {k: v for k, v in st.items() if k not in QX_STATE_FIELDS}
+    e1 = start(DynCore, rc1, data, st1)
+    e1.step(2)
+    assert not np.array_equal(e.get("ATM1_W"), e1.get("ATM1_W"))
+
+
+@pytest.mark.parametrize("nthreads", [2, 4])
+def test_nh_species_tiles_match_oracle_tiles(qx_n1, nthreads):
+    """The NH core decomposed, against the oracle's same tiles (the fix's decomposition
+    dependence as test_species_tiles_match_oracle_tiles)."""
+    from oracle.oracle import OracleParallel
+    from regcm_amd.config import set_nproc
+    from regcm_amd.dycore import DynCore
+    rc, data, st = qx_n1
+    cj, ci = set_nproc(nthreads, rc.jx, rc.iy)
+    o = OracleParallel(rc, data["split"], nthreads=nthreads)
+    o.put_state(st)
+    o.bdyval()
+    e = start(DynCore, rc, data, st, (cj, ci))
+    for nsteps, tol in ((1, 1e-11), (2, 1e-10)):
+        o.step(nsteps)
+        e.step(nsteps)
+        for name in NH_ALL:
+            err = nh_relerr(e.get(name), o.get(name), rc, name)
+            assert err < tol, (name, err, nsteps)
+
+
+@pytest.mark.parametrize("env", ["RCMDYN_NO_GRAPH", "RCMDYN_NO_OVERLAP", "RCMDYN_FORCE_RCCL"])
+def test_nh_species_step_forms(qx_n1, monkeypatch, env):
+    """2 x 2 tiles: graph replay, the overlapped exchanges and the RCCL transport against the
+    drop-in call sequence with none of them, bit for bit."""
+    from regcm_amd.dycore import DynCore
+    rc, data, st = qx_n1
+    ref = start(DynCore, rc, data, st, (2, 2))
+    monkeypatch.setenv(env, "1")
+    alt = start(DynCore, rc, data, st, (2, 2))
+    ref.step(4)
+    if env == "RCMDYN_NO_GRAPH":
+        for _ in range(4):
+            alt.tend()
+            alt.bdyval()
+    else:
+        alt.step(4)
+    for name in NH_ALL:
+        same = np.array_equal(ref.get(name), alt.get(name))
+        assert same, name
