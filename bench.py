@@ -167,11 +167,19 @@ def main():
     cj, ci = set_nproc(world, rc.jx, rc.iy)
 
     from regcm_amd.dycore import DynCore, comm_unique_id, runtime_info
+    # the engine library (and with it /opt/rocm's librccl.so.1) is loaded before torch, so a
+    # multi-rank job binds that RCCL and not the copy torch bundles under the same soname
+    # (INTEGRATION.md); every rank reports what it bound
+    rt = runtime_info()
+    print(f"[bench rank {rank}/{world}] runtime: {rt}", file=sys.stderr, flush=True)
     dist = None
+    rts = [rt]
     if world > 1:
         import torch
         import torch.distributed as dist
         dist.init_process_group(backend="gloo", init_method="env://")
+        rts = [None] * world
+        dist.all_gather_object(rts, rt)
         uid = bytearray(comm_unique_id()) if rank == 0 else bytearray(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, src=0)
@@ -291,8 +299,10 @@ def main():
         "device_ms_per_step": dev_ms,
         "dropin_ms_per_step": wall_d / args.steps * 1e3,
         "dropin_note": "rcmdyn_tend + rcmdyn_bdyval per step (INTEGRATION.md section 4), timed like value",
-        "runtime": runtime_info(),
+        "runtime": rt,
     }
+    if world > 1:
+        line["runtime_per_rank"] = rts
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(rc, data, args.cpu_budget, args.cpu_threads)
     print(json.dumps(line))

@@ -187,3 +187,13 @@ def test_exchange_plan_carries_the_hydrometeors():
             rb = [tuple(x[[2, 5, 6]]) for x in plans[b] if x[1] == 1 and x[3] == 1 and x[4] == a]
             assert sa == rb, (a, b)
     assert np.all(p5[:, 1] > 0)
+
+
+def test_bench_loads_engine_before_torch():
+    """bench.py binds the engine (and /opt/rocm's librccl.so.1) before torch can load its own
+    copy under the same soname, on every rank, and reports each rank's runtime."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    body = src[src.index("def main():"):]
+    assert "import torch" not in src[:src.index("def main():")]
+    assert body.index("rt = runtime_info()") < body.index("import torch")
+    assert "runtime_per_rank" in body
