@@ -245,6 +245,12 @@ int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
  * written).  Every message A sends B must be the receive B posts from A, in the same order on
  * the same channel, which a multi-rank job needs and tests check. */
 int rcmdyn_exchange_plan(const rcmdyn_config* cfg, int32_t nsteps, int64_t* ops, int64_t cap, int64_t* count);
+/* Halo/compute overlap of the hydrostatic step, host-only (no GPU): for each of the first cap
+ * tiles this engine would own, out[6q .. 6q+5] = {k_columns points in the part-1 rectangle R,
+ * k_columns points, k_momentum points of its part-1 blocks, k_momentum points, k_scalars points
+ * of its part-1 blocks, k_scalars points}: the share of each kernel that runs beside the
+ * prologue exchange (0 when the step does not overlap: one tile, NH, idiffu = 3). */
+int rcmdyn_overlap_shares(const rcmdyn_config* cfg, int32_t* out, int32_t cap);
 
 /* State transfer (host <-> device), Fortran layout, global index bounds. */
 int rcmdyn_put(rcmdyn_t* h, int32_t field, const double* src,

@@ -1531,17 +1531,32 @@ struct rcmdyn_engine {
     auto inner = [&](int J0, int I0, int bj, int bi) {
       return J0 - 2 >= t.rja && J0 + bj + 1 <= t.rjb && I0 - 2 >= t.ria && I0 + bi + 1 <= t.rib;
     };
+    // the block columns of k_momentum / k_scalars start at j1 or, shifted back by 64 - s, at
+    // j1 + s - 64 (a partial first column): the origin that puts the most points of the tile in
+    // blocks wholly inside R (on a 96-wide tile no default-aligned 64-wide block with its halo
+    // fits, and part 1 would be empty)
     const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
-    for (int by = 0; by < (mi2 - g.idi1 + MBI) / MBI; by++)
-      for (int bx = 0; bx < (mj2 - g.jdi1 + MBJ) / MBJ; bx++)
-        t.mom_in = t.mom_in || inner(g.jdi1 + bx * MBJ, g.idi1 + by * MBI, MBJ, MBI);
-    for (int by = 0; by < (g.icx2() - g.icx1() + SBI) / SBI; by++)
-      for (int bx = 0; bx < (g.jcx2() - g.jcx1() + SBJ) / SBJ; bx++)
-        t.sca_in = t.sca_in || inner(g.jcx1() + bx * SBJ, g.icx1() + by * SBI, SBJ, SBI);
+    auto best = [&](int j1, int j2, int i1, int i2, int BJ, int BI, int& org, long& npts) {
+      long top = 0;
+      org = j1;
+      for (int sft = 0; sft < BJ; sft++) {
+        const int o = sft ? j1 + sft - BJ : j1;
+        long pts = 0;
+        for (int I0 = i1; I0 <= i2; I0 += BI)
+          for (int J0 = o; J0 <= j2; J0 += BJ)
+            if (inner(J0, I0, BJ, BI))
+              pts += (long)(std::min(J0 + BJ - 1, j2) - std::max(J0, j1) + 1) * (std::min(I0 + BI - 1, i2) - I0 + 1);
+        if (pts > top) { top = pts; org = o; }
+      }
+      npts = top;
+      return top > 0;
+    };
+    t.mom_in = best(g.jdi1, mj2, g.idi1, mi2, MBJ, MBI, t.mj0, t.mom_p1);
+    t.sca_in = best(g.jcx1(), g.jcx2(), g.icx1(), g.icx2(), SBJ, SBI, t.sj0, t.sca_p1);
   }
   Fields fields(Tile& t, int part) {
     Fields f = fields(t);
-    f.pt = Part{part, t.rja, t.rjb, t.ria, t.rib, t.rnxb, t.nint};
+    f.pt = Part{part, t.rja, t.rjb, t.ria, t.rib, t.rnxb, t.nint, t.mj0, t.sj0};
     return f;
   }
 
@@ -1974,11 +1989,12 @@ struct rcmdyn_engine {
     const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
     const int pm = part == 0 ? 0 : (t.nint && t.mom_in ? part : (part == 1 ? -1 : 0));
     const int ps = part == 0 ? 0 : (t.nint && t.sca_in ? part : (part == 1 ? -1 : 0));
+    const int mo = pm > 0 ? t.mj0 : g.jdi1, so = ps > 0 ? t.sj0 : g.jcx1();     // block-column origins
     if (pm >= 0)
-      KLAUNCH(k_momentum, dim3((mj2 - g.jdi1 + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, cfg.kz), dim3(MBT), 0,
+      KLAUNCH(k_momentum, dim3((mj2 - mo + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, cfg.kz), dim3(MBT), 0,
               stream, g, dc, ds, fields(t, pm));
     if (ps >= 0)
-      KLAUNCH(k_scalars, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, cfg.kz),
+      KLAUNCH(k_scalars, dim3((g.jcx2() - so + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, cfg.kz),
               dim3(SBT), 0, stream, g, dc, ds, fields(t, ps));
   }
 
@@ -2475,6 +2491,34 @@ int rcmdyn_exchange_plan(const rcmdyn_config* cfg, int32_t nsteps, int64_t* ops,
     std::memcpy(ops + 7 * q, v, sizeof(v));
   }
   return 0;
+}
+
+int rcmdyn_overlap_shares(const rcmdyn_config* cfg, int32_t* out, int32_t cap) {
+  if (!cfg || !out || cap < 0) {
+    g_last_error = "rcmdyn_overlap_shares: bad argument";
+    return 1;
+  }
+  std::vector<PlanOp> log;
+  auto* h = new rcmdyn_engine();
+  int rc = guard(h, [&] {
+    h->create(cfg, &log);
+    for (size_t q = 0; q < h->tiles.size() && (int)q < cap; q++) {
+      const Tile& t = h->tiles[q];
+      const Geom& g = t.g;
+      const int mj2 = g.br ? g.jdi2 : g.jde2 + 1, mi2 = g.bt ? g.idi2 : g.ide2 + 1;
+      const bool ov = h->overlap() && t.rja <= t.rjb && t.ria <= t.rib;
+      const int32_t v[6] = {
+          ov ? (int32_t)((long)(t.rjb - t.rja + 1) * (t.rib - t.ria + 1)) : 0,
+          (int32_t)((long)(g.jdx2() - g.jdx1() + 1) * (g.idx2() - g.idx1() + 1)),
+          ov ? (int32_t)t.mom_p1 : 0, (int32_t)((long)(mj2 - g.jdi1 + 1) * (mi2 - g.idi1 + 1)),
+          ov ? (int32_t)t.sca_p1 : 0, (int32_t)((long)(g.jcx2() - g.jcx1() + 1) * (g.icx2() - g.icx1() + 1))};
+      std::memcpy(out + 6 * q, v, sizeof(v));
+    }
+  });
+  if (rc) g_last_error = h->err;
+  h->destroy();
+  delete h;
+  return rc;
 }
 
 int rcmdyn_destroy(rcmdyn_t* h) {

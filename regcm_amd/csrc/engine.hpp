@@ -201,6 +201,8 @@ struct Tile {
   // k_momentum / k_scalars block lies in R
   int rja = 0, rjb = -1, ria = 0, rib = -1, rnxb = 0, nint = 0, nring = 0;
   bool mom_in = false, sca_in = false;
+  int mj0 = 0, sj0 = 0;         // the block-column origins of k_momentum / k_scalars in parts 1, 2
+  long mom_p1 = 0, sca_p1 = 0;  // points their part-1 blocks compute (rcmdyn_overlap_shares)
   std::vector<void*> allocs;
 };
 

@@ -540,7 +540,8 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
   __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
   const int tid = threadIdx.x;
   PT_DECL
-  const int J0 = g.jdi1 + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI, k = (int)blockIdx.z + 1;
+  const int J0 = (f.pt.part ? f.pt.mj0 : g.jdi1) + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI;
+  const int k = (int)blockIdx.z + 1;
   if (part_skip(f.pt, J0 - 2, J0 + MBJ + 1, I0 - 2, I0 + MBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -553,7 +554,7 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
   // the bdyuv slices read the new u, v there); boundary branches test global indices
   const int tj = tid % MBJ, ti = tid / MBJ;
   const int j = J0 + tj, i = I0 + ti;
-  const bool valid = j <= (g.br ? g.jdi2 : g.jde2 + 1) && i <= (g.bt ? g.idi2 : g.ide2 + 1);
+  const bool valid = j >= g.jdi1 && j <= (g.br ? g.jdi2 : g.jde2 + 1) && i <= (g.bt ? g.idi2 : g.ide2 + 1);
   const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jdi1, g.idi1), o3 = o2 + kof;
   const double u1c = LD(f.a1u, o3), v1c = LD(f.a1v, o3), u2c = LD(f.a2u, o3), v2c = LD(f.a2v, o3);
   const double u1m = (k >= 2) ? LD(f.a1u, o3 - L8) : 0.0, v1m = (k >= 2) ? LD(f.a1v, o3 - L8) : 0.0;
@@ -951,7 +952,8 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
   PT_DECL
   // the tile's cross points and its ghost ring (k_qfilter's moisture fix reads the forecasts
   // there); boundary branches test global indices
-  const int J0 = g.jcx1() + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI, k = (int)blockIdx.z + 1;
+  const int J0 = (f.pt.part ? f.pt.sj0 : g.jcx1()) + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI;
+  const int k = (int)blockIdx.z + 1;
   if (part_skip(f.pt, J0 - 2, J0 + SBJ + 1, I0 - 2, I0 + SBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -961,7 +963,7 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
   // this thread's point and its point operands, loaded before the staging barrier
   const int tj = tid % SBJ, ti = tid / SBJ;
   const int j = J0 + tj, i = I0 + ti;
-  const bool valid = j <= g.jcx2() && i <= g.icx2();
+  const bool valid = j >= g.jcx1() && j <= g.jcx2() && i <= g.icx2();
   const uint32_t o2 = valid ? g.o2(j, i) : g.o2(g.jce1, g.ice1), o3 = o2 + kof;
   const double t1 = LD(f.a1t, o3), t2 = LD(f.a2t, o3), qv2 = LD(f.a2qv, o3), qc2 = LD(f.a2qc, o3);
   const double qv1 = LD(f.a1qv, o3), qc1 = LD(f.a1qc, o3);

@@ -44,8 +44,10 @@ struct Slices { double* s[16]; };
 // k_columns maps its part 1 blocks onto the rows of R (nxb blocks of 64 columns per row) and
 // its part 2 blocks onto the rest of the column box as one list (rbase: part 1's block count,
 // so each block keeps its own noise partial).
+// mj0 / sj0: the j origin of k_momentum's / k_scalars' 64-wide block columns in parts 1 and 2,
+// shifted on narrow tiles so that one block column lies wholly in R (part 0: jdi1 / jcx1).
 struct Part {
-  int part, ja, jb, ia, ib, nxb, rbase;
+  int part, ja, jb, ia, ib, nxb, rbase, mj0, sj0;
 };
 
 // Every device buffer of one tile for one ping-pong parity: a* are the current time levels,

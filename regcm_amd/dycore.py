@@ -30,7 +30,7 @@ EXPORTED = [
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
     "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin", "rcmdyn_reductions", "rcmdyn_runtime_info",
-    "rcmdyn_exchange_plan",
+    "rcmdyn_exchange_plan", "rcmdyn_overlap_shares",
 ]
 
 
@@ -74,6 +74,7 @@ def lib():
     L.rcmdyn_runtime_info.argtypes = [ctypes.c_char_p, i32]
     L.rcmdyn_exchange_plan.argtypes = [ctypes.POINTER(RcmdynConfig), i32, ctypes.POINTER(ctypes.c_int64),
                                        ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    L.rcmdyn_overlap_shares.argtypes = [ctypes.POINTER(RcmdynConfig), ctypes.POINTER(i32), i32]
     L.rcmdyn_kernel_times.argtypes = [P, i32, i32, ctypes.c_char_p, ctypes.POINTER(i32), dp, ctypes.POINTER(i32)]
     _lib = L
     return L
@@ -125,6 +126,21 @@ def comm_unique_id() -> bytes:
     if lib().rcmdyn_comm_unique_id(buf):
         raise EngineError(lib().rcmdyn_last_error(None).decode())
     return bytes(buf)
+
+
+def overlap_shares(rc, split, nproc_j: int, nproc_i: int):
+    """Host-only (rcmdyn_overlap_shares): per rank of an nproc_j x nproc_i job, the points of
+    k_columns / k_momentum / k_scalars that run beside the prologue exchange (part 1) and their
+    totals, as [(col_p1, col, mom_p1, mom, sca_p1, sca), ...]."""
+    n = nproc_j * nproc_i
+    out = []
+    for r in range(n):
+        cfg = build_config(rc, split, nproc_j, nproc_i, tile_first=r, tile_count=1, comm_rank=r, comm_size=n)
+        v = (ctypes.c_int32 * 6)()
+        if lib().rcmdyn_overlap_shares(ctypes.byref(cfg), v, 1):
+            raise EngineError(lib().rcmdyn_last_error(None).decode())
+        out.append(tuple(v))
+    return out
 
 
 class DynCore:

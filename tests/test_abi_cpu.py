@@ -197,3 +197,22 @@ def test_bench_loads_engine_before_torch():
     assert "import torch" not in src[:src.index("def main():")]
     assert body.index("rt = runtime_info()") < body.index("import torch")
     assert "runtime_per_rank" in body
+
+
+def test_overlap_shares_on_the_scaling_tiles():
+    """rcmdyn_overlap_shares (host-only): on C3's 2/4/8-GPU tiles part 1 of k_momentum and
+    k_scalars (the blocks beside the prologue exchange) is non-empty -- the block columns are
+    shifted so one lies inside R -- and k_columns' part 1 is R itself."""
+    from regcm_amd.config import CONFIGS, set_nproc
+    from regcm_amd import icbc
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    for n, lo in ((2, 0.6), (4, 0.5), (8, 0.4)):
+        cj, ci = set_nproc(n, rc.jx, rc.iy)
+        sh = dycore.overlap_shares(rc, data["split"], cj, ci)
+        assert len(sh) == n
+        tot = [sum(x[q] for x in sh) for q in range(6)]
+        assert tot[0] / tot[1] > 0.9
+        assert tot[2] / tot[3] > lo and tot[4] / tot[5] > lo, (n, tot)
+    one = dycore.overlap_shares(rc, data["split"], 1, 1)
+    assert one[0][0] == 0 and one[0][2] == 0 and one[0][4] == 0

@@ -231,6 +231,25 @@ def test_overlap_parts_bit_identical(monkeypatch, mode):
     assert np.allclose(a[:2], b[:2], rtol=1e-12, atol=0), (a, b)   # the partials in another order
 
 
+@pytest.mark.parametrize("nproc", [(2, 1), (2, 2), (2, 4)], ids=str)
+def test_overlap_shifted_blocks_bit_identical(nproc):
+    """C3 on the tiles of the 2/4/8-GPU runs (96 x 192, 96 x 96, 96 x 48): the block columns of
+    k_momentum / k_scalars in parts 1 and 2 start at the origin that puts one 64-wide column
+    wholly inside the part-1 rectangle (rcmdyn_overlap_shares: 62 / 56 / 44 % of their points
+    beside the exchange, none with the default origin).  Bit-identical to one tile."""
+    from regcm_amd.dycore import DynCore
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    ref = DynCore(rc, data["split"])
+    til = DynCore(rc, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    for e in (ref, til):
+        e.put_state(data["state"])
+        e.bdyval()
+        e.step(5)
+    for name in STATE_FIELDS:
+        assert np.array_equal(ref.get(name), til.get(name)), name
+
+
 def test_c2_ten_steps():
     rc = CONFIGS["C2"]
     data = icbc.generate(rc)

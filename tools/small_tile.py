@@ -1,6 +1,8 @@
 """Per-step device time of the hydrostatic step on a small single-tile domain (the size of one
 rank's tile when the driver's scaling runs split C3 over 2/4/8 GPUs): the kernel-latency floor
-of a rank's step before any exchange.  python tools/small_tile.py"""
+of a rank's step before any exchange; then, per rank count, the share of each update kernel
+that runs beside the prologue exchange (rcmdyn_overlap_shares, host-only: `--shares` prints
+only that and needs no GPU).  python tools/small_tile.py [--shares]"""
 import dataclasses
 import os
 import sys
@@ -10,7 +12,25 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 from regcm_amd import icbc  # noqa: E402
 from regcm_amd.config import CONFIGS  # noqa: E402
-from regcm_amd.dycore import DynCore  # noqa: E402
+from regcm_amd.config import set_nproc  # noqa: E402
+from regcm_amd.dycore import DynCore, overlap_shares  # noqa: E402
+
+
+def shares():
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    print("part 1 (beside the prologue exchange), share of each kernel's points over all ranks:")
+    for n in (2, 4, 8):
+        cj, ci = set_nproc(n, rc.jx, rc.iy)
+        sh = overlap_shares(rc, data["split"], cj, ci)
+        tot = [sum(x[q] for x in sh) for q in range(6)]
+        print(f"  {n} ranks ({cj}x{ci} tiles of {rc.jx // cj}x{rc.iy // ci}): k_columns {tot[0] / tot[1]:.0%}, "
+              f"k_momentum {tot[2] / tot[3]:.0%}, k_scalars {tot[4] / tot[5]:.0%}", flush=True)
+
+
+if "--shares" in sys.argv:
+    shares()
+    sys.exit(0)
 
 for jx, iy in ((192, 192), (96, 192), (96, 96), (96, 48)):
     rc = dataclasses.replace(CONFIGS["C3"], jx=jx, iy=iy)
@@ -36,3 +56,5 @@ e.step(4)
 kt = e.kernel_times(5)
 for name, (n, us) in sorted(kt.items(), key=lambda kv: -kv[1][1] * kv[1][0]):
     print(f"  {name:32s} {n / 5:4.1f}/step {us * 1e3:8.2f} us")
+
+shares()
