@@ -276,6 +276,8 @@ struct rcmdyn_engine {
   double last_ms = 0.0;
   // RCMDYN_NO_GRAPH=1 runs rcmdyn_step eagerly (the path of RCCL-decomposed runs), for timing
   const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
+  // k_momentum and k_scalars as one launch (k_update); RCMDYN_NO_FUSE_UPDATE=1: two launches
+  const bool fuse_update = std::getenv("RCMDYN_NO_FUSE_UPDATE") == nullptr;
   // rcmdyn_step's hydrostatic bdyval runs inside k_split_correct_bdy (RCMDYN_NO_FUSE_BDY: two
   // launches of its own, as after rcmdyn_tend)
   const bool no_fuse_bdy = [] {
@@ -1990,6 +1992,13 @@ struct rcmdyn_engine {
     const int pm = part == 0 ? 0 : (t.nint && t.mom_in ? part : (part == 1 ? -1 : 0));
     const int ps = part == 0 ? 0 : (t.nint && t.sca_in ? part : (part == 1 ? -1 : 0));
     const int mo = pm > 0 ? t.mj0 : g.jdi1, so = ps > 0 ? t.sj0 : g.jcx1();     // block-column origins
+    if (fuse_update && pm >= 0 && ps >= 0) {
+      const int mnx = (mj2 - mo + MBJ) / MBJ, mny = (mi2 - g.idi1 + MBI) / MBI;
+      const int snx = (g.jcx2() - so + SBJ) / SBJ, sny = (g.icx2() - g.icx1() + SBI) / SBI;
+      KLAUNCH(k_update, dim3(std::max(mnx, snx), std::max(mny, sny), 2 * cfg.kz), dim3(SBT), 0, stream, g, dc, ds,
+              fields(t, pm), fields(t, ps), mnx, mny, snx, sny);
+      return;
+    }
     if (pm >= 0)
       KLAUNCH(k_momentum, dim3((mj2 - mo + MBJ) / MBJ, (mi2 - g.idi1 + MBI) / MBI, cfg.kz), dim3(MBT), 0,
               stream, g, dc, ds, fields(t, pm));

@@ -526,22 +526,30 @@ constexpr int TW0 = MBJ + 1, TH0 = MBI + 1;   // halo 1 on the low sides (j-1, i
 #ifndef SC_LB
 #define SC_LB 4
 #endif
-__global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* __restrict__ c,
-                                                     const StepState* __restrict__ s, Fields f) {
-  __shared__ double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
-  __shared__ double sUM[TH2][TW2], sVM[TH2][TW2];
+// LDS of one k_momentum block
+struct MomLDS {
+  double sUMC[TH1][TW1], sVMC[TH1][TW1], sUD[TH1][TW1], sVD[TH1][TW1];
+  double sUM[TH2][TW2], sVM[TH2][TW2];
   // ubd3d/vbd3d (consumed by xkc) share storage with the PGF log terms formed afterwards
-  __shared__ union {
+  union {
     struct { double UB[TH2][TW2], VB[TH2][TW2]; } b;
     struct { double LU[MBI][TW0], LV[TH0][MBJ]; } l;
   } sX;
+  double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
+};
+// one k_momentum block (bx, by, bz) with its LDS (k_momentum, or the momentum blocks of k_update)
+__device__ __forceinline__ void momentum_block(const Geom& g, const Consts* __restrict__ c,
+                                               const StepState* __restrict__ s, const Fields& f, MomLDS& L,
+                                               int bx, int by, int bz) {
+  auto& sUMC = L.sUMC; auto& sVMC = L.sVMC; auto& sUD = L.sUD; auto& sVD = L.sVD;
+  auto& sUM = L.sUM; auto& sVM = L.sVM; auto& sX = L.sX;
+  auto& sTV = L.sTV; auto& sQ0 = L.sQ0; auto& sQ1 = L.sQ1; auto& sPH = L.sPH; auto& sPS = L.sPS; auto& sXK = L.sXK;
 #define sUB sX.b.UB
 #define sVB sX.b.VB
-  __shared__ double sTV[TH0][TW0], sQ0[TH0][TW0], sQ1[TH0][TW0], sPH[TH0][TW0], sPS[TH0][TW0], sXK[TH0][TW0];
   const int tid = threadIdx.x;
   PT_DECL
-  const int J0 = (f.pt.part ? f.pt.mj0 : g.jdi1) + (int)blockIdx.x * MBJ, I0 = g.idi1 + (int)blockIdx.y * MBI;
-  const int k = (int)blockIdx.z + 1;
+  const int J0 = (f.pt.part ? f.pt.mj0 : g.jdi1) + bx * MBJ, I0 = g.idi1 + by * MBI;
+  const int k = bz + 1;
   if (part_skip(f.pt, J0 - 2, J0 + MBJ + 1, I0 - 2, I0 + MBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -832,6 +840,11 @@ __global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* _
   ST(f.b1v, o3, cv);
   PT_PRINT(2);
 }
+__global__ __launch_bounds__(MBT, MO_LB) void k_momentum(Geom g, const Consts* __restrict__ c,
+                                                     const StepState* __restrict__ s, Fields f) {
+  __shared__ MomLDS L;
+  momentum_block(g, c, s, f, L, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
+}
 
 // ---------------------------------------------------------------------------------------
 // K4. Scalars at the cross points jce x ice, one level per block of SBJ x SBI points:
@@ -943,17 +956,24 @@ __device__ __forceinline__ void scalars_qraw(const Consts* __restrict__ c, const
   ST(n ? f.b2qc : f.b2qv, o3, n2);
 }
 
-__global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __restrict__ c,
-                                                    const StepState* __restrict__ s, Fields f) {
-  __shared__ double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
-  __shared__ double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
-  __shared__ double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
+// LDS of one k_scalars block
+struct ScaLDS {
+  double sUMC[SDH][SDW], sVMC[SDH][SDW], sUD[SDH][SDW], sVD[SDH][SDW], sUB[SDH][SDW], sVB[SDH][SDW];
+  double sPS[SH1][SW1], sXT[SH1][SW1], sXQV[SH1][SW1], sXQC[SH1][SW1];
+  double sTB[SH2][SW2], sQVB[SH2][SW2], sQCB[SH2][SW2];
+};
+__device__ __forceinline__ void scalars_block(const Geom& g, const Consts* __restrict__ c,
+                                              const StepState* __restrict__ s, const Fields& f, ScaLDS& L,
+                                              int bx, int by, int bz) {
+  auto& sUMC = L.sUMC; auto& sVMC = L.sVMC; auto& sUD = L.sUD; auto& sVD = L.sVD; auto& sUB = L.sUB;
+  auto& sVB = L.sVB; auto& sPS = L.sPS; auto& sXT = L.sXT; auto& sXQV = L.sXQV; auto& sXQC = L.sXQC;
+  auto& sTB = L.sTB; auto& sQVB = L.sQVB; auto& sQCB = L.sQCB;
   const int tid = threadIdx.x;
   PT_DECL
   // the tile's cross points and its ghost ring (k_qfilter's moisture fix reads the forecasts
   // there); boundary branches test global indices
-  const int J0 = (f.pt.part ? f.pt.sj0 : g.jcx1()) + (int)blockIdx.x * SBJ, I0 = g.icx1() + (int)blockIdx.y * SBI;
-  const int k = (int)blockIdx.z + 1;
+  const int J0 = (f.pt.part ? f.pt.sj0 : g.jcx1()) + bx * SBJ, I0 = g.icx1() + by * SBI;
+  const int k = bz + 1;
   if (part_skip(f.pt, J0 - 2, J0 + SBJ + 1, I0 - 2, I0 + SBI + 1)) return;   // the staged halo-2 tile
   const uint32_t P8 = g.P8, L8 = g.L8;
   const uint32_t kof = (uint32_t)(k - 1) * L8;
@@ -1223,6 +1243,32 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
     if (qown) scalars_qraw(c, f, 1, fcqc, o2, o3, ps, pb);
   }
   PT_PRINT(3);
+}
+__global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __restrict__ c,
+                                                    const StepState* __restrict__ s, Fields f) {
+  __shared__ ScaLDS L;
+  scalars_block(g, c, s, f, L, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
+}
+
+// k_momentum and k_scalars in one launch: blockIdx.z < kz a scalars block of level z + 1, else
+// a momentum block of level z - kz + 1 (x/y: the larger of the two grids; a block past its own
+// grid exits).  Both read only k_columns' outputs and the state and write disjoint buffers, so
+// the two block sets are independent; one launch drains one tail instead of two, and with the
+// longer scalars blocks dispatched first the momentum blocks fill it (C3, alternating on one
+// box: 203.5-212.1 us/step against 211.2-222.9 with the momentum blocks first, 222.3-224.1
+// interleaved by level, 218.8-223.6 as two launches).
+__global__ __launch_bounds__(SBT, SC_LB) void k_update(Geom g, const Consts* __restrict__ c,
+                                                   const StepState* __restrict__ s, Fields fm, Fields fs,
+                                                   int mnx, int mny, int snx, int sny) {
+  __shared__ union { MomLDS m; ScaLDS s; } L;
+  const int kz = c->kz, bz = (int)blockIdx.z, bx = (int)blockIdx.x, by = (int)blockIdx.y;
+  const bool mom = bz >= kz;
+  const int lz = mom ? bz - kz : bz;
+  if (mom) {
+    if (bx < mnx && by < mny) momentum_block(g, c, s, fm, L.m, bx, by, lz);
+  } else if (bx < snx && by < sny) {
+    scalars_block(g, c, s, fs, L.s, bx, by, lz);
+  }
 }
 #undef DIFFU_X
 #undef H2T

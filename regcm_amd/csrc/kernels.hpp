@@ -121,6 +121,8 @@ __global__ void k_sladv(Geom g, const Consts* __restrict__ c, StepState* s, Fiel
 __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f, QxArgs q);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
+__global__ void k_update(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields fm, Fields fs,
+                         int mnx, int mny, int snx, int sny);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
                                 const double* __restrict__ a1v, const double* __restrict__ a2u,

@@ -297,11 +297,12 @@ def test_kernel_times_hook(c1_data):
         b = name.split("<")[0]
         base[b[:-3] if b.endswith("_km") else b] = v
     # rcmdyn_step's step: bdyval's boundary lines run inside k_split_correct_bdy, k_qfilter's
-    # work in k_columns / k_scalars / the extra blocks of k_split_project and k_split_correct
-    for k in ("k_momentum", "k_scalars", "k_columns", "k_split_project",
+    # work in k_columns / k_scalars / the extra blocks of k_split_project and k_split_correct;
+    # k_momentum and k_scalars share one launch (k_update)
+    for k in ("k_update", "k_columns", "k_split_project",
               "k_spstep_fused", "k_split_correct_bdy", "k_bdyval_qc"):
         assert k in base and base[k][0] == 3 and base[k][1] > 0.0, k
-    for k in ("k_bdyval_set", "k_split_correct", "k_qfilter"):
+    for k in ("k_bdyval_set", "k_split_correct", "k_qfilter", "k_momentum", "k_scalars"):
         assert k not in base, sorted(base)
 
 
