@@ -335,13 +335,14 @@ def test_qfilter_fusion_equals_qfilter(c1_data, monkeypatch, variant, nproc):
         e.bdyval()
         e.step(5)
     assert fused.get_time() == sep.get_time()
-    for name in list(STATE_FIELDS) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
+    for name in state_fields(rcv) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
         assert np.array_equal(fused.get(name), sep.get(name)), name
     assert np.array_equal(fused.reductions(), sep.reductions())
 
 
 FUSE_CASES = [({}, (1, 1)), ({}, (2, 2)), ({}, (1, 3)), ({"iboudy": 4}, (1, 1)), ({"iboudy": 4}, (2, 2)),
-              ({"isladvec": 1}, (2, 1)), ({"ibltyp": 2}, (1, 1)), ({"ibltyp": 2}, (2, 2))]
+              ({"isladvec": 1}, (2, 1)), ({"ibltyp": 2}, (1, 1)), ({"ibltyp": 2}, (2, 2)),
+              ({"ipptls": 2}, (1, 1)), ({"ipptls": 2}, (2, 2)), ({"ipptls": 2, "iboudy": 4}, (2, 1))]
 
 
 @pytest.mark.parametrize("variant,nproc", FUSE_CASES, ids=lambda x: str(x))
@@ -357,6 +358,7 @@ def test_fused_bdyval_equals_separate(c1_data, monkeypatch, variant, nproc):
     st = {k: v.copy() for k, v in data["state"].items()}
     if rcv.ibltyp == 2:
         st.update(icbc.tke_state(rcv))
+    st = with_species(rcv, st)     # ipptls = 2: patchy cloud, so the qc inflow/outflow acts
     fused = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
     monkeypatch.setenv("RCMDYN_NO_FUSE_BDY", "1")
     sep = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
@@ -365,7 +367,7 @@ def test_fused_bdyval_equals_separate(c1_data, monkeypatch, variant, nproc):
         e.bdyval()
         e.step(5)
     assert fused.get_time() == sep.get_time()
-    for name in list(STATE_FIELDS) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
+    for name in state_fields(rcv) + (["ATM1_TKE", "ATM2_TKE"] if rcv.ibltyp == 2 else []):
         assert np.array_equal(fused.get(name), sep.get(name)), name
     assert np.array_equal(fused.reductions(), sep.reductions())
 
