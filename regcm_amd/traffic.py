@@ -14,6 +14,10 @@ regcm_amd/csrc/kernels.hip with tendency diagnostics off:
   k_scalars     reads atm1 u,v,t,qv,qc, atm2 u,v (xkc), atm2 t,qv,qc, qdot (11) + t,q b0/bt in
                 band (4 f_b); writes next atm1/atm2 t, cqv, cqc and (qfuse, the RAW filter of
                 the non-negative forecasts) next atm1/atm2 qv, qc (8); 2-D: 12 + psc
+  k_update      k_momentum's and k_scalars' blocks in one launch: the union of their fields
+                (the state both read counted once): reads atm1 u,v,t,qv,qc, atm2 u,v,t,qv,qc,
+                qdot, xkc, phi (13) + u,v,t,q b0/bt in band (8 f_b); writes the 12 of the two;
+                2-D: 14
   k_columns     reads atm1 u,v,t,qv,qc (5); writes qdot, phi (2); 2-D: 12 + (qfuse) the
                 RA-filtered p* into the next buffers (2); the keep copies are O(perimeter)
   k_qfilter     (RCMDYN_NO_QFUSE) reads cqv,cqc, atm1/atm2 qv,qc (6); writes next atm1/atm2
@@ -33,6 +37,7 @@ def band_fraction(jx: int, iy: int, nspgx: int) -> float:
 KERNEL_FIELDS = {
     "k_momentum": (13, 4, 9),
     "k_scalars": (19, 4, 13),
+    "k_update": (25, 8, 14),
     "k_columns": (7, 0, 14),
     "k_qfilter": (10, 0, 5),
     "k_split_project": (6, 0, 20),
