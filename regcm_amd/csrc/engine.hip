@@ -243,6 +243,7 @@ struct rcmdyn_engine {
   const int graph_steps = std::getenv("RCMDYN_GRAPH_STEPS") ? std::max(1, std::min(2, std::atoi(std::getenv("RCMDYN_GRAPH_STEPS")))) : 2;
   hipGraphExec_t gtend[2] = {nullptr, nullptr};   // tend alone (the drop-in rcmdyn_tend)
   hipGraphExec_t gbdy[2] = {nullptr, nullptr};    // bdyval alone (rcmdyn_bdyval)
+  hipGraphExec_t gbdyf[2] = {nullptr, nullptr};   // rcmdyn_bdyval with the deferred corrections
   // step error flags: host-mapped snapshot ring written by the last launch of every tend,
   // one event per slot; the host checks a step's flags once its event completed and keeps
   // at most FLAG_LAG steps unchecked, so no entry point synchronises the stream per step
@@ -285,6 +286,13 @@ struct rcmdyn_engine {
     return v && *v && std::strcmp(v, "0") != 0;
   }();
   bool fuse_bdy = false;      // set by step_once for the tend + bdyval pair it runs
+  // the drop-in pair (rcmdyn_tend, then rcmdyn_bdyval): tend leaves its split corrections
+  // pending and bdyval launches them with its boundary lines (k_split_correct_bdy, the form of
+  // rcmdyn_step); any other call in between launches them alone first (settle).
+  // RCMDYN_NO_DEFER_CORR=1: tend launches them itself.
+  const bool no_defer_corr = std::getenv("RCMDYN_NO_DEFER_CORR") != nullptr;
+  bool defer_corr = false;    // set by tend_call / post_physics around the tend they run
+  bool corr_pending = false;  // the last tend's corrections are not launched yet
   // the hydrostatic step without k_qfilter (its work in k_columns, k_scalars and the extra
   // blocks of k_split_project / k_split_correct); RCMDYN_NO_QFUSE=1 launches k_qfilter
   const bool no_qfuse = [] {
@@ -760,7 +768,7 @@ struct rcmdyn_engine {
   }
 
   void invalidate_graphs() {
-    for (hipGraphExec_t* g : {gexec, gexec2, gtend, gbdy})
+    for (hipGraphExec_t* g : {gexec, gexec2, gtend, gbdy, gbdyf})
       for (int p = 0; p < 2; p++)
         if (g[p]) { (void)hipGraphExecDestroy(g[p]); g[p] = nullptr; }
   }
@@ -998,6 +1006,7 @@ struct rcmdyn_engine {
   }
 
   void put(int f, const double* src, int j1, int j2, int i1, int i2, int k1, int k2) {
+    settle();
     const bool qxf = f >= RCMDYN_ATM1_QI && f <= RCMDYN_QSPHY;
     const bool phyf = (f >= RCMDYN_TPHY && f <= RCMDYN_WPHY) || (f >= RCMDYN_QIPHY && f <= RCMDYN_QSPHY);
     const bool binf = f >= RCMDYN_XUB_B1 && f <= RCMDYN_ATM0_PSDOT;
@@ -1081,6 +1090,7 @@ struct rcmdyn_engine {
 
   // mod_bdycod::bdyin from read_icbc on (bdyin.hip)
   void bdyin() {
+    settle();
     if (tiles.empty() || !tiles[0].bin[0]) throw std::runtime_error("rcmdyn_bdyin: no ICBC record was put (XUB_B1 ..)");
     const int kz = cfg.kz;
     const bool nh = cfg.idynamic == 2;
@@ -1150,6 +1160,7 @@ struct rcmdyn_engine {
   }
 
   void get(int f, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
+    settle();
     if (!diag && (f == RCMDYN_TTEN || f == RCMDYN_UTEN || f == RCMDYN_VTEN || f == RCMDYN_QVTEN ||
                   f == RCMDYN_QCTEN || f == RCMDYN_OMEGA || f == RCMDYN_XKC))
       throw std::runtime_error("rcmdyn_get: tendency diagnostics are off (rcmdyn_set_diagnostics)");
@@ -2102,7 +2113,17 @@ struct rcmdyn_engine {
     }
     // the fused split step also produced ddsum/dhsum on the left/bottom ghost ring
     if (!fused) xch({{FK::DHSUM, ns}}, 1, 1);
-    // corrections + rcmtimer advance (last tile's launch)
+    // corrections + rcmtimer advance (last tile's launch); deferred to bdyval in the drop-in pair
+    if (defer_corr && !fuse_bdy) corr_pending = true;
+    else launch_corrections(fuse_bdy);
+    hs.lcount += 1;
+    if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+
+  // the split corrections + rcmtimer advance (last tile's launch); bdy: with bdyval's boundary
+  // lines (k_split_correct_bdy; k_bdyval_qc then advances the clock)
+  void launch_corrections(bool bdy) {
+    const int kz = cfg.kz, ns = cfg.nsplit;
     for (size_t q = 0; q < tiles.size(); q++) {
       Tile& t = tiles[q];
       const Geom& g = t.g;
@@ -2113,7 +2134,7 @@ struct rcmdyn_engine {
       const QFix qf = qfix(t);
       const int nser = qfuse() ? (int)((2 * kz + gr.x * gr.y - 1) / (gr.x * gr.y)) : 0;
       gr.z += nser;
-      if (fuse_bdy) {
+      if (bdy) {
         // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
         // levels, 4 per block
         const unsigned per = 4 * gr.x * gr.y;
@@ -2131,8 +2152,28 @@ struct rcmdyn_engine {
 #undef RCM_SC
       }
     }
-    hs.lcount += 1;
-    if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
+  }
+  bool can_defer() const { return cfg.idynamic != 2 && !no_fuse_bdy && !no_defer_corr && (ntiles == 1 || split_fused()); }
+  // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
+  void settle() {
+    if (!corr_pending) return;
+    corr_pending = false;
+    launch_corrections(false);
+    note_step(hs.lcount);
+  }
+  // rcmdyn_bdyval after a deferring tend: the corrections with the boundary lines, then the
+  // rest of bdyval as rcmdyn_step runs it
+  void fused_bdyval() {
+    corr_pending = false;
+    fuse_bdy = true;
+    try {
+      launch_corrections(true);
+      bdyval();
+    } catch (...) {
+      fuse_bdy = false;
+      throw;
+    }
+    fuse_bdy = false;
   }
 
   // one spstep substep: gradient of delh(src) -> (uu,vv) -> divergence -> mode update
@@ -2240,6 +2281,7 @@ struct rcmdyn_engine {
 
   void step(int n) {
     prepare();
+    settle();
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
@@ -2280,20 +2322,41 @@ struct rcmdyn_engine {
   // replays its own captured graph and returns without synchronising the stream
   void tend_call() {
     prepare();
+    settle();
     check(FLAG_LAG);
     const int par = tiles[0].cur;
-    if (graph_ok()) {
-      if (!gtend[par]) capture(par, 1);
-      HIPCHK(hipGraphLaunch(gtend[par], stream));
-      replayed_tend();
-    } else {
-      tend();
+    defer_corr = can_defer();
+    try {
+      if (graph_ok()) {
+        if (!gtend[par]) capture(par, 1);
+        HIPCHK(hipGraphLaunch(gtend[par], stream));
+        replayed_tend();
+        corr_pending = defer_corr;
+      } else {
+        tend();
+      }
+    } catch (...) {
+      defer_corr = false;
+      throw;
     }
-    note_step(hs.lcount);
+    defer_corr = false;
+    if (!corr_pending) note_step(hs.lcount);     // else at the corrections' launch
   }
   void bdyval_call() {
     prepare();
     const int par = tiles[0].cur;
+    if (corr_pending) {
+      if (graph_ok() && !ghosts_stale) {
+        if (!gbdyf[par]) capture(par, 4);
+        HIPCHK(hipGraphLaunch(gbdyf[par], stream));
+        corr_pending = false;
+        replayed_bdyval();
+      } else {
+        fused_bdyval();
+      }
+      note_step(hs.lcount);
+      return;
+    }
     // after a put the ghost rings are not step results: bdyval runs eagerly (its slice
     // exchange depends on that, bdyval())
     if (graph_ok() && !ghosts_stale) {
@@ -2309,20 +2372,24 @@ struct rcmdyn_engine {
   // host bookkeeping done in tend()/bdyval() is rolled back, the replay redoes it per launch
   void capture(int par, int what, int nsteps = 1) {
     const StepState save = hs;
+    const bool pend = corr_pending;
     std::vector<int> curs;
     for (auto& t : tiles) curs.push_back(t.cur);
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (int q = 0; q < nsteps; q++) {
       if (what == 3) step_once();
+      else if (what == 4) fused_bdyval();
       else if (what & 1) tend();
       else bdyval();
     }
     HIPCHK(hipStreamEndCapture(stream, &graph));
-    hipGraphExec_t& x = nsteps == 2 ? gexec2[par] : what == 3 ? gexec[par] : what == 1 ? gtend[par] : gbdy[par];
+    hipGraphExec_t& x = nsteps == 2 ? gexec2[par] : what == 3 ? gexec[par] : what == 4 ? gbdyf[par]
+                        : what == 1 ? gtend[par] : gbdy[par];
     HIPCHK(hipGraphInstantiate(&x, graph, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(graph));
     hs = save;
+    corr_pending = pend;
     for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
   }
 
@@ -2341,6 +2408,7 @@ struct rcmdyn_engine {
 
   void kernel_times(int nsteps, int cap, char* names, int32_t* launches, double* avg, int32_t* count) {
     prepare();
+    settle();
     KernelProf kp;
     HIPCHK(hipStreamSynchronize(stream));
     prof = &kp;
@@ -2374,6 +2442,7 @@ struct rcmdyn_engine {
   }
 
   void set_time(long long lcount, double dt, double xbctime) {
+    settle();
     HIPCHK(hipStreamSynchronize(stream));
     pending.clear();
     gpending.clear();
@@ -2385,6 +2454,7 @@ struct rcmdyn_engine {
   }
 
   void reductions(double out[3]) {
+    settle();
     check(0);
     HIPCHK(hipStreamSynchronize(stream));
     StepState st;
@@ -2405,6 +2475,7 @@ struct rcmdyn_engine {
   }
 
   void diagnostics(double out[4]) {
+    settle();
     HIPCHK(hipStreamSynchronize(stream));
     check_now();
     StepState st;
@@ -2590,6 +2661,7 @@ int rcmdyn_tend(rcmdyn_t* h) { return guard(h, [&] { h->tend_call(); }); }
 int rcmdyn_tend_pre_physics(rcmdyn_t* h) {
   return guard(h, [&] {
     h->prepare();
+    h->settle();
     h->check(rcmdyn_engine::FLAG_LAG);
     h->tend(rcmdyn_engine::TEND_PRE, true);
   });
@@ -2598,9 +2670,17 @@ int rcmdyn_tend_pre_physics(rcmdyn_t* h) {
 int rcmdyn_tend_post_physics(rcmdyn_t* h) {
   return guard(h, [&] {
     h->prepare();
+    h->settle();
     h->check(rcmdyn_engine::FLAG_LAG);
-    h->tend(rcmdyn_engine::TEND_POST);
-    h->note_step(h->hs.lcount);
+    h->defer_corr = h->can_defer();       // the corrections go with the next rcmdyn_bdyval
+    try {
+      h->tend(rcmdyn_engine::TEND_POST);
+    } catch (...) {
+      h->defer_corr = false;
+      throw;
+    }
+    h->defer_corr = false;
+    if (!h->corr_pending) h->note_step(h->hs.lcount);
   });
 }
 
@@ -2617,6 +2697,7 @@ int rcmdyn_step(rcmdyn_t* h, int32_t nsteps) { return guard(h, [&] { h->step(nst
 
 int rcmdyn_synchronize(rcmdyn_t* h) {
   return guard(h, [&] {
+    h->settle();                                     // a deferred step's flags are checked here
     if (h->comm) h->note_step(h->hs.lcount, true);   // collective: every rank synchronizes
     HIPCHK(hipStreamSynchronize(h->stream));
     h->check(0);

@@ -372,6 +372,44 @@ def test_fused_bdyval_equals_separate(c1_data, monkeypatch, variant, nproc):
     assert np.array_equal(fused.reductions(), sep.reductions())
 
 
+@pytest.mark.parametrize("nproc", [(1, 1), (2, 2)], ids=str)
+def test_deferred_corrections_any_call_order(c1_data, monkeypatch, nproc):
+    """rcmdyn_tend leaves its split corrections to the next rcmdyn_bdyval (launched with the
+    boundary lines, rcmdyn_step's k_split_correct_bdy); a get, a put or a synchronize in
+    between launches them first.  Every order is bit-identical to rcmdyn_step and to tend
+    launching them itself (RCMDYN_NO_DEFER_CORR)."""
+    from regcm_amd.dycore import DynCore
+    rc, data = c1_data
+    st = with_species(rc, data["state"])
+    mk = lambda: DynCore(rc, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    ref, a, b = mk(), mk(), mk()
+    monkeypatch.setenv("RCMDYN_NO_DEFER_CORR", "1")
+    c = mk()
+    for e in (ref, a, b, c):
+        e.put_state(st)
+        e.bdyval()
+    ref.step(6)
+    for n in range(6):
+        a.tend()
+        a.bdyval()
+        b.tend()
+        if n % 3 == 0:
+            b.get("ATM1_T")            # settles the corrections before bdyval
+        elif n % 3 == 1:
+            b.synchronize()
+        else:
+            b.put("ATM1_QV", b.get("ATM1_QV"))
+        b.bdyval()
+        c.tend()
+        c.bdyval()
+    for name in STATE_FIELDS:
+        r = ref.get(name)
+        for e in (a, b, c):
+            assert np.array_equal(e.get(name), r), name
+    assert a.get_time() == ref.get_time() == b.get_time() == c.get_time()
+    assert np.array_equal(a.reductions(), ref.reductions())
+
+
 def _dependent_negatives(cq, rc):
     """(k, i, j) cross points of the interior where the reference's serial sweep reads an
     already-fixed predecessor (Main/mod_tendency.F90:382-393)."""
