@@ -2153,7 +2153,11 @@ struct rcmdyn_engine {
       }
     }
   }
-  bool can_defer() const { return cfg.idynamic != 2 && !no_fuse_bdy && !no_defer_corr && (ntiles == 1 || split_fused()); }
+  // not with a communicator: a rank-local call (a get) between tend and bdyval would then issue
+  // the step's flag reduction on one rank only
+  bool can_defer() const {
+    return cfg.idynamic != 2 && !comm && !no_fuse_bdy && !no_defer_corr && (ntiles == 1 || split_fused());
+  }
   // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
   void settle() {
     if (!corr_pending) return;
