@@ -377,3 +377,33 @@ def test_nh_species_step_forms(qx_n1, monkeypatch, env):
     for name in NH_ALL:
         same = np.array_equal(ref.get(name), alt.get(name))
         assert same, name
+
+
+@pytest.mark.parametrize("core", ["hydrostatic", "nh"])
+def test_species_smooth_decomposition_bit_identical(c1_data, core):
+    """With smooth hydrometeor layers (no cloud edges, so no negative forecast reaches the fix
+    at a tile edge) a 2 x 2 decomposition with nqx = 5 is bit-identical to one tile, as the
+    reference's decompositions are; with cloud edges the fix itself depends on the tiles
+    (test_species_tiles_match_oracle_tiles)."""
+    from regcm_amd.dycore import DynCore
+    if core == "nh":
+        rc = dataclasses.replace(CONFIGS["N1"], ipptls=2)
+        data = icbc.generate_nh(rc)
+    else:
+        rc = dataclasses.replace(c1_data[0], ipptls=2)
+        data = c1_data[1]
+    st = dict(data["state"])
+    hsig = (rc.sigma[1:] + rc.sigma[:-1]) * 0.5
+    ps = st["PSA"][0]
+    for nm, (peak, s0, w) in {"QC": (2e-4, 0.75, 0.15), "QI": (5e-5, 0.3, 0.1), "QR": (1e-4, 0.92, 0.08),
+                              "QS": (8e-5, 0.55, 0.12)}.items():
+        layer = peak * (0.2 + np.exp(-0.5 * ((hsig - s0) / w) ** 2))    # positive everywhere
+        st[f"ATM1_{nm}"] = layer[:, None, None] * ps[None]
+        st[f"ATM2_{nm}"] = 0.98 * st[f"ATM1_{nm}"]
+    one = start(DynCore, rc, data, st)
+    til = start(DynCore, rc, data, st, (2, 2))
+    one.step(4)
+    til.step(4)
+    names = (NH_ALL if core == "nh" else ALL)
+    for name in names:
+        assert np.array_equal(one.get(name), til.get(name)), name
