@@ -279,6 +279,13 @@ struct rcmdyn_engine {
   const bool no_graph = std::getenv("RCMDYN_NO_GRAPH") != nullptr;
   // k_momentum and k_scalars as one launch (k_update); RCMDYN_NO_FUSE_UPDATE=1: two launches
   const bool fuse_update = std::getenv("RCMDYN_NO_FUSE_UPDATE") == nullptr;
+  // NH: tend's time filters of t, qv, qc in k_nh_tend_c and the negative-moisture fix, into
+  // the other parity (Tile::tq); RCMDYN_NH_NO_TFUSE=1: in place in k_nh_tfilter_a1
+  const bool nh_tfuse = std::getenv("RCMDYN_NH_NO_TFUSE") == nullptr;
+  // parity of t, qv, qc: the step's ping-pong (hydrostatic), Tile::tq (NH)
+  int thp(const Tile& t) const { return cfg.idynamic == 2 ? t.tq : t.cur; }
+  // the parity the step graphs are captured for
+  int gpar() const { return thp(tiles[0]); }
   // rcmdyn_step's hydrostatic bdyval runs inside k_split_correct_bdy (RCMDYN_NO_FUSE_BDY: two
   // launches of its own, as after rcmdyn_tend)
   const bool no_fuse_bdy = [] {
@@ -611,9 +618,12 @@ struct rcmdyn_engine {
 
   NHFields nhfields(Tile& t) {
     NHFields f = nhf[&t - tiles.data()];
-    const int c = t.cur;
-    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[c]; f.a1qv = t.a1qv[c]; f.a1qc = t.a1qc[c];
-    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[c]; f.a2qv = t.a2qv[c]; f.a2qc = t.a2qc[c];
+    const int c = t.cur, q = thp(t), o = 1 - q;
+    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[q]; f.a1qv = t.a1qv[q]; f.a1qc = t.a1qc[q];
+    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[q]; f.a2qv = t.a2qv[q]; f.a2qc = t.a2qc[q];
+    f.b1t = t.a1t[o]; f.b1qv = t.a1qv[o]; f.b1qc = t.a1qc[o];
+    f.b2t = t.a2t[o]; f.b2qv = t.a2qv[o]; f.b2qc = t.a2qc[o];
+    f.tfuse = nh_tfuse ? 1 : 0;
     f.psa = t.psa_[c]; f.psb = t.psb_[c];
     f.msfx = t.msfx; f.msfd = t.msfd; f.coriol = t.coriol; f.ht = t.ht; f.xmsf = t.xmsf; f.dmsf = t.dmsf;
     f.hgfact = t.hgfact; f.rgcr = t.rgcr; f.rgdt = t.rgdt; f.ibcr = t.ibcr; f.ibdt = t.ibdt;
@@ -857,12 +867,12 @@ struct rcmdyn_engine {
 
   // ------------------------------------------------------------------ field access
   double* fptr(Tile& t, FK f) {
-    const int c = t.cur;
+    const int c = t.cur, q = thp(t);
     switch (f) {
-      case FK::A1U: return t.a1u[c]; case FK::A1V: return t.a1v[c]; case FK::A1T: return t.a1t[c];
-      case FK::A1QV: return t.a1qv[c]; case FK::A1QC: return t.a1qc[c];
-      case FK::A2U: return t.a2u[c]; case FK::A2V: return t.a2v[c]; case FK::A2T: return t.a2t[c];
-      case FK::A2QV: return t.a2qv[c]; case FK::A2QC: return t.a2qc[c];
+      case FK::A1U: return t.a1u[c]; case FK::A1V: return t.a1v[c]; case FK::A1T: return t.a1t[q];
+      case FK::A1QV: return t.a1qv[q]; case FK::A1QC: return t.a1qc[q];
+      case FK::A2U: return t.a2u[c]; case FK::A2V: return t.a2v[c]; case FK::A2T: return t.a2t[q];
+      case FK::A2QV: return t.a2qv[q]; case FK::A2QC: return t.a2qc[q];
       case FK::PSA: return t.psa_[c]; case FK::PSB: return t.psb_[c];
       case FK::PSDOTA: return t.psdota; case FK::PSDOTB: return t.psdotb;
       case FK::RPSDA: return t.rpsda; case FK::RPSDB: return t.rpsdb; case FK::QDOT: return t.qdot;
@@ -976,11 +986,11 @@ struct rcmdyn_engine {
     }
     switch (f) {
       case RCMDYN_ATM1_U: return t.a1u[c]; case RCMDYN_ATM1_V: return t.a1v[c];
-      case RCMDYN_ATM1_T: return t.a1t[c]; case RCMDYN_ATM1_QV: return t.a1qv[c];
-      case RCMDYN_ATM1_QC: return t.a1qc[c];
+      case RCMDYN_ATM1_T: return t.a1t[thp(t)]; case RCMDYN_ATM1_QV: return t.a1qv[thp(t)];
+      case RCMDYN_ATM1_QC: return t.a1qc[thp(t)];
       case RCMDYN_ATM2_U: return t.a2u[c]; case RCMDYN_ATM2_V: return t.a2v[c];
-      case RCMDYN_ATM2_T: return t.a2t[c]; case RCMDYN_ATM2_QV: return t.a2qv[c];
-      case RCMDYN_ATM2_QC: return t.a2qc[c];
+      case RCMDYN_ATM2_T: return t.a2t[thp(t)]; case RCMDYN_ATM2_QV: return t.a2qv[thp(t)];
+      case RCMDYN_ATM2_QC: return t.a2qc[thp(t)];
       case RCMDYN_XUB_B0: return t.ub0; case RCMDYN_XUB_BT: return t.ubt;
       case RCMDYN_XVB_B0: return t.vb0; case RCMDYN_XVB_BT: return t.vbt;
       case RCMDYN_XTB_B0: return t.tb0; case RCMDYN_XTB_BT: return t.tbt;
@@ -1140,8 +1150,8 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const int c = t.cur;
       SliceArgs a{};
-      a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[c];
-      a.a2qv = t.a2qv[c]; a.a2qc = t.a2qc[c]; a.psa = t.psa_[c]; a.psb = t.psb_[c];
+      a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[thp(t)];
+      a.a2qv = t.a2qv[thp(t)]; a.a2qc = t.a2qc[thp(t)]; a.psa = t.psa_[c]; a.psb = t.psb_[c];
       a.rpsb = t.rpsb; a.rpsdb = t.rpsdb; a.rpsda = t.rpsda; a.msfx = t.msfx; a.qdot = t.qdot; a.pten = t.pten;
       if (cfg.idynamic == 2) {
         const NHFields& h = nhf[&t - tiles.data()];
@@ -1578,13 +1588,13 @@ struct rcmdyn_engine {
 
   // all buffers of one tile for its current parity (see Fields)
   Fields fields(Tile& t) {
-    const int c = t.cur, n = 1 - c;
+    const int c = t.cur, n = 1 - c, q = thp(t), o = 1 - q;
     Fields f{};
-    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[c]; f.a1qv = t.a1qv[c]; f.a1qc = t.a1qc[c];
-    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[c]; f.a2qv = t.a2qv[c]; f.a2qc = t.a2qc[c];
+    f.a1u = t.a1u[c]; f.a1v = t.a1v[c]; f.a1t = t.a1t[q]; f.a1qv = t.a1qv[q]; f.a1qc = t.a1qc[q];
+    f.a2u = t.a2u[c]; f.a2v = t.a2v[c]; f.a2t = t.a2t[q]; f.a2qv = t.a2qv[q]; f.a2qc = t.a2qc[q];
     f.psa = t.psa_[c]; f.psb = t.psb_[c];
-    f.b1u = t.a1u[n]; f.b1v = t.a1v[n]; f.b1t = t.a1t[n]; f.b1qv = t.a1qv[n]; f.b1qc = t.a1qc[n];
-    f.b2u = t.a2u[n]; f.b2v = t.a2v[n]; f.b2t = t.a2t[n]; f.b2qv = t.a2qv[n]; f.b2qc = t.a2qc[n];
+    f.b1u = t.a1u[n]; f.b1v = t.a1v[n]; f.b1t = t.a1t[o]; f.b1qv = t.a1qv[o]; f.b1qc = t.a1qc[o];
+    f.b2u = t.a2u[n]; f.b2v = t.a2v[n]; f.b2t = t.a2t[o]; f.b2qv = t.a2qv[o]; f.b2qc = t.a2qc[o];
     f.bpsa = t.psa_[n]; f.bpsb = t.psb_[n];
     f.msfx = t.msfx; f.msfd = t.msfd; f.coriol = t.coriol; f.ht = t.ht; f.xmsf = t.xmsf; f.dmsf = t.dmsf;
     f.hgfact = t.hgfact; f.mapf = t.mapf;
@@ -1765,9 +1775,10 @@ struct rcmdyn_engine {
       }
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
-      // tend's time filters with part A of the first acoustic sub-step (sound, :163-718)
+      // tend's time filters (tfuse = 0) with part A of the first acoustic sub-step (sound, :163-718)
       KLAUNCH(k_nh_tfilter_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc, f);
     });
+    if (nh_tfuse) for (auto& t : tiles) t.tq = 1 - t.tq;     // the filtered t, qv, qc
     // sound, Main/mod_sound.F90:163-718
     for (int it = 1; it <= istep; it++) {
       // part A: sub-step 1 in k_nh_tfilter_a1, the later ones in the previous k_nh_sound_cd
@@ -1889,7 +1900,8 @@ struct rcmdyn_engine {
         KLAUNCH(k_bdyval_qx, dim3(kz, hc.nsp), dim3(256), 0, stream, t.g, ds, qx_args(t), -1, (int)!cfg.present_qc,
                 t.psa_[c], slices(t), slen);
       KLAUNCH(k_bdyval_qc, dim3(kz), dim3(256), 0, stream, t.g, (int)!cfg.present_qc, (int)(cfg.iboudy == 3 || cfg.iboudy == 4),
-              t.a1qc[c], t.a1qv[c], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()), dflags);
+              t.a1qc[thp(t)], t.a1qv[thp(t)], t.psa_[c], slices(t), slen, ds, cfg.dtsec, (int)(q + 1 == tiles.size()),
+              dflags);
     }
     tke_bdyval();
     hs.xbctime = hs.xbctime + cfg.dtsec;
@@ -2208,10 +2220,10 @@ struct rcmdyn_engine {
   }
 
   BdyArgs bdy_args(Tile& t, int set_ps) {
-    const int c = t.cur;
+    const int c = t.cur, q = thp(t);
     BdyArgs a{};
-    a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a1t = t.a1t[c]; a.a1qv = t.a1qv[c]; a.a1qc = t.a1qc[c];
-    a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[c]; a.a2qv = t.a2qv[c]; a.a2qc = t.a2qc[c];
+    a.a1u = t.a1u[c]; a.a1v = t.a1v[c]; a.a1t = t.a1t[q]; a.a1qv = t.a1qv[q]; a.a1qc = t.a1qc[q];
+    a.a2u = t.a2u[c]; a.a2v = t.a2v[c]; a.a2t = t.a2t[q]; a.a2qv = t.a2qv[q]; a.a2qc = t.a2qc[q];
     a.psa = t.psa_[c]; a.psb = t.psb_[c];
     a.ub0 = t.ub0; a.ubt = t.ubt; a.vb0 = t.vb0; a.vbt = t.vbt; a.tb0 = t.tb0; a.tbt = t.tbt;
     a.qb0 = t.qb0; a.qbt = t.qbt; a.pb0 = t.pb0; a.pbt = t.pbt;
@@ -2278,6 +2290,7 @@ struct rcmdyn_engine {
   // host bookkeeping of a replayed tend / bdyval (what tend() and bdyval() do on the host)
   void replayed_tend() {
     if (cfg.idynamic != 2) for (auto& t : tiles) t.cur = 1 - t.cur;
+    else if (nh_tfuse) for (auto& t : tiles) t.tq = 1 - t.tq;
     hs.lcount += 1;
     if (hs.lcount == 2) hs.dt = 2.0 * cfg.dtsec;
   }
@@ -2292,7 +2305,7 @@ struct rcmdyn_engine {
     HIPCHK(hipEventRecord(e0, stream));
     for (int s = 0; s < n; s++) {
       check(FLAG_LAG);
-      const int par = tiles[0].cur;
+      const int par = gpar();
       if (graph_steps == 2 && s + 1 < n && graph_ok(2)) {
         if (!gexec2[par]) capture(par, 3, 2);
         HIPCHK(hipGraphLaunch(gexec2[par], stream));
@@ -2328,7 +2341,7 @@ struct rcmdyn_engine {
     prepare();
     settle();
     check(FLAG_LAG);
-    const int par = tiles[0].cur;
+    const int par = gpar();
     defer_corr = can_defer();
     try {
       if (graph_ok()) {
@@ -2348,7 +2361,7 @@ struct rcmdyn_engine {
   }
   void bdyval_call() {
     prepare();
-    const int par = tiles[0].cur;
+    const int par = gpar();
     if (corr_pending) {
       if (graph_ok() && !ghosts_stale) {
         if (!gbdyf[par]) capture(par, 4);
@@ -2377,8 +2390,8 @@ struct rcmdyn_engine {
   void capture(int par, int what, int nsteps = 1) {
     const StepState save = hs;
     const bool pend = corr_pending;
-    std::vector<int> curs;
-    for (auto& t : tiles) curs.push_back(t.cur);
+    std::vector<int> curs, tqs;
+    for (auto& t : tiles) { curs.push_back(t.cur); tqs.push_back(t.tq); }
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
     for (int q = 0; q < nsteps; q++) {
@@ -2394,7 +2407,7 @@ struct rcmdyn_engine {
     HIPCHK(hipGraphDestroy(graph));
     hs = save;
     corr_pending = pend;
-    for (size_t q = 0; q < tiles.size(); q++) tiles[q].cur = curs[q];
+    for (size_t q = 0; q < tiles.size(); q++) { tiles[q].cur = curs[q]; tiles[q].tq = tqs[q]; }
   }
 
   // rcmdyn_exchange_plan: the communication calls of put + bdyval + nsteps x (tend + bdyval),

@@ -139,6 +139,7 @@ struct Tile {
   double *a2u[2], *a2v[2], *a2t[2], *a2qv[2], *a2qc[2];
   double *psa_[2], *psb_[2];
   int cur = 0;
+  int tq = 0;     // NH core: parity of t, qv, qc (the fused time filters ping-pong them)
   double *dstor, *hstor;
   // statics
   double *msfx, *msfd, *coriol, *ht, *xmsf, *dmsf, *hgfact, *mapf;

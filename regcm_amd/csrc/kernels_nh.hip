@@ -299,6 +299,41 @@ __device__ __forceinline__ double diffx_l(const Geom& g, const Consts* c, double
 #undef SA
 }
 
+// time filters of t (RA), qv and qc (RAW), Main/mod_tendency.F90:422-427 (p* is constant):
+// o1, o2: atm1, atm2 before the filter; v: the forecast (for qv, qc fixed where negative);
+// n1, n2: atm1, atm2 after it
+__device__ __forceinline__ void nh_ra_t(const Consts* c, double o1, double o2, double v, double& n1, double& n2) {
+  const double d = c->gnu1 * (v + o2 - d_two * o1);
+  n2 = o1 + d;
+  n1 = v;
+}
+__device__ __forceinline__ void nh_raw_qv(const Consts* c, double o1, double o2, double v, double psa, double psb,
+                                          double& n1, double& n2) {
+  const double beta = 0.53;
+  const double d = c->gnu1 * (v + o2 - d_two * o1);
+  n2 = dmax(o1 + beta * d, MINQQ * psa);
+  n1 = dmax(v + (beta - d_one) * d, MINQQ * psb);
+}
+__device__ __forceinline__ void nh_raw_qc(const Consts* c, double o1, double o2, double v, double& n1, double& n2) {
+  const double beta = 0.53;
+  const double d = c->gnu2 * (v + o2 - d_two * o1);
+  double m = o1 + beta * d, q = v + (beta - d_one) * d;
+  if (m < d_zero) m = d_zero;
+  if (q < d_zero) q = d_zero;
+  n2 = m;
+  n1 = q;
+}
+// tfuse: the RAW filter of qv (n = 0) or qc (n = 1) at one point into the other parity
+__device__ __forceinline__ void nh_filter_q_to(const Geom& g, const Consts* c, const NHFields& f, int n, int j, int i, int k,
+                                               double v) {
+  double n1, n2;
+  if (n == 0)
+    nh_raw_qv(c, F3(f.a1qv, j, i, k), F3(f.a2qv, j, i, k), v, F2(f.psa, j, i), F2(f.psb, j, i), n1, n2);
+  else
+    nh_raw_qc(c, F3(f.a1qc, j, i, k), F3(f.a2qc, j, i, k), v, n1, n2);
+  F3(n ? f.b1qc : f.b1qv, j, i, k) = n1;
+  F3(n ? f.b2qc : f.b2qv, j, i, k) = n2;
+}
 // ---------------------------------------------------------------------------------------
 // The tendency chain of the NH core as two point kernels.  For each variable the reference
 // accumulates pc_dynamic over several loop nests -- advection (hadv/vadv), curvature or the
@@ -370,6 +405,11 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     if (k <= kz && IN_CE(j, i)) {
       F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k);
       F3(f.cqc, j, i, k) = F3(f.a2qc, j, i, k);
+    }
+    if (f.tfuse && k <= kz) {     // no filter here: the other parity keeps the values
+      F3(f.b1t, j, i, k) = F3(f.a1t, j, i, k); F3(f.b2t, j, i, k) = F3(f.a2t, j, i, k);
+      F3(f.b1qv, j, i, k) = F3(f.a1qv, j, i, k); F3(f.b2qv, j, i, k) = F3(f.a2qv, j, i, k);
+      F3(f.b1qc, j, i, k) = F3(f.a1qc, j, i, k); F3(f.b2qc, j, i, k) = F3(f.a2qc, j, i, k);
     }
     return;
   }
@@ -528,7 +568,9 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     tt = tt + 0.0;
     if (ray) tt = tt + tau * ((F3(f.tb0, j, i, k) + xt * F3(f.tbt, j, i, k)) - F3(f.a2t, j, i, k));
     if (wdiag) F3(f.tten, j, i, k) = tt;
-    F3(f.ct, j, i, k) = F3(f.a2t, j, i, k) + dt * tt;
+    const double o2 = F3(f.a2t, j, i, k), ctv = o2 + dt * tt;
+    if (f.tfuse) nh_ra_t(c, F3(f.a1t, j, i, k), o2, ctv, F3(f.b1t, j, i, k), F3(f.b2t, j, i, k));
+    else F3(f.ct, j, i, k) = ctv;
   }
   // ================= qv: hadvqv (or the semi-Lagrangian start), vadvqv, adiabatic, boundary,
   // diffusion, forecast
@@ -559,7 +601,10 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     qv = qv + 0.0;
     if (ray) qv = qv + tau * ((F3(f.qb0, j, i, k) + xt * F3(f.qbt, j, i, k)) - F3(f.a2qv, j, i, k));
     if (wdiag) F3(f.qvten, j, i, k) = qv;
-    F3(f.cqv, j, i, k) = F3(f.a2qv, j, i, k) + dt * qv;
+    const double o2 = F3(f.a2qv, j, i, k), cq = o2 + dt * qv;
+    F3(f.cqv, j, i, k) = cq;
+    if (f.tfuse && !(cq < d_zero))      // a negative forecast: filtered after its fix
+      nh_raw_qv(c, F3(f.a1qv, j, i, k), o2, cq, ps, pbs, F3(f.b1qv, j, i, k), F3(f.b2qv, j, i, k));
   }
   // ================= qc: hadvqx (or the semi-Lagrangian start), vadv4d ind = 1, adiabatic,
   // diffusion, forecast
@@ -583,7 +628,10 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     double qc = d_zero + cd + PHY(qcphy);
     qc = qc + 0.0;
     if (wdiag) F3(f.qcten, j, i, k) = qc;
-    F3(f.cqc, j, i, k) = F3(f.a2qc, j, i, k) + dt * qc;
+    const double o2 = F3(f.a2qc, j, i, k), cq = o2 + dt * qc;
+    F3(f.cqc, j, i, k) = cq;
+    if (f.tfuse && !(cq < d_zero))
+      nh_raw_qc(c, F3(f.a1qc, j, i, k), o2, cq, F3(f.b1qc, j, i, k), F3(f.b2qc, j, i, k));
   }
 }
 
@@ -792,8 +840,13 @@ __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
     const double* sv = n ? f.cqc : f.cqv;
     double* fx = n ? f.fqc : f.fqv;
     if (F3(sv, j, i, k) < d_zero) {
-      if (nh_negfix_dependent(g, sv, j, i, k)) atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
-      else F3(fx, j, i, k) = nh_negfix_sum(g, sv, fx, j, i, k, false);
+      if (nh_negfix_dependent(g, sv, j, i, k)) {
+        atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+      } else {
+        const double v = nh_negfix_sum(g, sv, fx, j, i, k, false);
+        F3(fx, j, i, k) = v;
+        if (f.tfuse) nh_filter_q_to(g, c, f, n, j, i, k, v);
+      }
     }
   }
 }
@@ -815,42 +868,29 @@ __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHField
         while (mask) {
           const int b = __ffsll((long long)mask) - 1;
           mask &= mask - 1;
-          F3(fx, j0 + b, i, k) = nh_negfix_sum(g, sv, fx, j0 + b, i, k, true);
+          const double v = nh_negfix_sum(g, sv, fx, j0 + b, i, k, true);
+          F3(fx, j0 + b, i, k) = v;
+          if (f.tfuse) nh_filter_q_to(g, c, f, n, j0 + b, i, k, v);
         }
       }
     }
   if (lane == 0) f.depplane[plane] = 0;
 }
 
-// time filters of t (RA), qv and qc (RAW), Main/mod_tendency.F90:422-427 (p* is constant),
-// at one interior cross point and level
+// tfuse = 0: the three time filters in place at one interior cross point and level
 __device__ __forceinline__ void nh_tfilter_at(const Geom& g, const Consts* c, const NHFields& f, int j, int i,
                                               int k) {
-  {
-    const double o1 = F3(f.a1t, j, i, k), o2 = F3(f.a2t, j, i, k), nw = F3(f.ct, j, i, k);
-    const double d = c->gnu1 * (nw + o2 - d_two * o1);
-    F3(f.a2t, j, i, k) = o1 + d;
-    F3(f.a1t, j, i, k) = nw;
-  }
-  const double beta = 0.53;
+  nh_ra_t(c, F3(f.a1t, j, i, k), F3(f.a2t, j, i, k), F3(f.ct, j, i, k), F3(f.a1t, j, i, k), F3(f.a2t, j, i, k));
   {
     double v = F3(f.cqv, j, i, k);
     if (v < d_zero) v = F3(f.fqv, j, i, k);
-    const double o1 = F3(f.a1qv, j, i, k), o2 = F3(f.a2qv, j, i, k);
-    const double d = c->gnu1 * (v + o2 - d_two * o1);
-    F3(f.a2qv, j, i, k) = dmax(o1 + beta * d, MINQQ * F2(f.psa, j, i));
-    F3(f.a1qv, j, i, k) = dmax(v + (beta - d_one) * d, MINQQ * F2(f.psb, j, i));
+    nh_raw_qv(c, F3(f.a1qv, j, i, k), F3(f.a2qv, j, i, k), v, F2(f.psa, j, i), F2(f.psb, j, i),
+              F3(f.a1qv, j, i, k), F3(f.a2qv, j, i, k));
   }
   {
     double v = F3(f.cqc, j, i, k);
     if (v < d_zero) v = F3(f.fqc, j, i, k);
-    const double o1 = F3(f.a1qc, j, i, k), o2 = F3(f.a2qc, j, i, k);
-    const double d = c->gnu2 * (v + o2 - d_two * o1);
-    double m = o1 + beta * d, q = v + (beta - d_one) * d;
-    if (m < d_zero) m = d_zero;
-    if (q < d_zero) q = d_zero;
-    F3(f.a2qc, j, i, k) = m;
-    F3(f.a1qc, j, i, k) = q;
+    nh_raw_qc(c, F3(f.a1qc, j, i, k), F3(f.a2qc, j, i, k), v, F3(f.a1qc, j, i, k), F3(f.a2qc, j, i, k));
   }
 }
 
@@ -879,7 +919,7 @@ __device__ __forceinline__ void nh_sound_a1_at(const Geom& g, const Consts* c, c
 __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
-  if (k <= c->kz && IN_CI(j, i)) nh_tfilter_at(g, c, f, j, i, k);
+  if (!f.tfuse && k <= c->kz && IN_CI(j, i)) nh_tfilter_at(g, c, f, j, i, k);
   nh_sound_a1_at(g, c, f, j, i, k);
 }
 

@@ -50,6 +50,12 @@ struct NHFields {
                                  // the reference reports, Main/mod_sound.F90:634-646)
   // nqx = 5: atm1 qi, qr, qs (the water load of the adiabatic w term; null for nqx = 2)
   const double* qxa1[NQXH];
+  // tfuse = 1: the time filters of t, qv, qc (Main/mod_tendency.F90:422-427) write the other
+  // parity b* of those fields (k_nh_tend_c at non-negative forecasts, the negative-moisture fix
+  // at the fixed points; k_nh_tend_c copies the points no filter writes); tfuse = 0: in place
+  // in k_nh_tfilter_a1
+  double *b1t, *b1qv, *b1qc, *b2t, *b2qv, *b2qc;
+  int tfuse;
 };
 constexpr int NH_CFL_SLOTS = 1024;
 // block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,

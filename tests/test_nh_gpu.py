@@ -184,6 +184,37 @@ def test_nh_overlap_modes(nh_data, monkeypatch, mode):
         assert np.array_equal(ref.get(name), til.get(name)), name
 
 
+TFUSE_CASES = [({}, (1, 1)), ({}, (2, 2)), ({"isladvec": 1}, (1, 1)), ({"iboudy": 4}, (2, 1)),
+               ({"ipptls": 2}, (1, 1)), ({"idiffu": 3}, (1, 1))]
+
+
+@pytest.mark.parametrize("variant,nproc", TFUSE_CASES, ids=lambda x: str(x))
+def test_nh_fused_time_filters_bit_identical(nh_data, monkeypatch, variant, nproc):
+    """The time filters of t, qv, qc fused into k_nh_tend_c and the negative-moisture fix
+    (into the other parity, Tile::tq) equal the in-place filter pass (RCMDYN_NH_NO_TFUSE=1)
+    bit for bit: eager and graph-replayed steps, the drop-in pair, an odd step count (the
+    state read from the second parity) and a put between steps."""
+    from regcm_amd.dycore import DynCore
+    rc, data = nh_data
+    rcv = dataclasses.replace(rc, **variant)
+    st = with_species(rcv, data["state"])
+    fused = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    monkeypatch.setenv("RCMDYN_NH_NO_TFUSE", "1")
+    inplace = DynCore(rcv, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
+    fields = NH_FIELDS + (QX_STATE_FIELDS if rcv.nqx > 2 else [])
+    for e in (fused, inplace):
+        e.put_state(st)
+        e.bdyval()
+        e.step(5)
+        for _ in range(2):
+            e.tend()
+            e.bdyval()
+        e.put("ATM1_T", e.get("ATM1_T") * (1.0 + 1e-12))
+        e.step(2)
+    for name in fields:
+        assert np.array_equal(fused.get(name), inplace.get(name)), name
+
+
 @pytest.mark.parametrize("variant", NH_DECOMP_VARIANTS, ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()))
 def test_nh_variant_decomposition(nh_data, variant):
     from regcm_amd.dycore import DynCore
