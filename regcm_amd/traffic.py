@@ -49,14 +49,15 @@ KERNEL_FIELDS = {
     #                  writes se, sf, pi, pp (4)
     #   k_nh_tend_c    reads atm1 u, v, t, qv, qc, pp, w, atm2 t, qv, qc, pp, w, th, qdot, cr,
     #                  rho0, rho1, xpr, xkcr, z0, zf0 (21) + t, qv, pp, w b0/bt in the band
-    #                  (8 f_b); writes wten, ppten, atmc t, qv, qc (5); the decoupled products
+    #                  (8 f_b); writes wten, ppten, atmc qv, qc and the time-filtered atm1/atm2
+    #                  t, qv, qc into the other parity (10; tfilter fused); the decoupled products
     #                  (xw, xpp, xqv, xqc, umc, vmc, the b-level fields, xkc, xkcf) are formed
     #                  from these as they are read
     #   k_nh_tend_d    reads atm1 u, v, w, atm2 u, v, ud, vd, cr, qdot, xkcr, z0 (11) + u, v b0/bt
     #                  in the band (4 f_b); writes uten, vten (2)
     "k_nh_sound_cd": (21, 0, 5),
     "k_nh_sound_bc": (17, 0, 6),
-    "k_nh_tend_c": (26, 8, 9),
+    "k_nh_tend_c": (31, 8, 9),
     "k_nh_tend_d": (13, 4, 10),
 }
 
