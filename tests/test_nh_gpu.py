@@ -209,6 +209,9 @@ def test_nh_fused_time_filters_bit_identical(nh_data, monkeypatch, variant, npro
         for _ in range(2):
             e.tend()
             e.bdyval()
+        e.tend_pre_physics()
+        e.tend_post_physics()
+        e.bdyval()
         e.put("ATM1_T", e.get("ATM1_T") * (1.0 + 1e-12))
         e.step(2)
     for name in fields:
