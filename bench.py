@@ -50,7 +50,8 @@ def pmc_traffic(kernel: str, config: str):
         return None, None
     if d.get("digest") != kernels_digest() or d.get("config") != config:
         return None, None
-    k = d.get("kernels", {}).get(kernel)
+    ks = d.get("kernels", {})
+    k = ks.get(kernel) or ks.get("void " + kernel)     # rocprofv3 names templates "void name<...>"
     if not k:
         return None, None
     return k["hbm_bytes_per_launch"], d.get("source")

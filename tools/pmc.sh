@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${CFG:-C3}
 mkdir -p $OUT
-BENCH="python3 bench.py --config ${CFG:-C3} --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --prof-steps 0"
+BENCH="python3 bench.py --config ${CFG:-C3} --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --prof-steps 0 --settle-ms 0"
 pass() {  # pass <name> <counters...>
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT/$name -o $name --output-format csv -- $BENCH \
