@@ -185,7 +185,7 @@ def main():
                     help="host threads of the CPU baseline (0: every CPU this process is granted)")
     ap.add_argument("--prof-steps", type=int, default=5,
                     help="eager steps timed per kernel with HIP events (dominant-kernel roofline)")
-    ap.add_argument("--settle-ms", type=float, default=300.0,
+    ap.add_argument("--settle-ms", type=float, default=100.0,
                     help="untimed steps run for this long before the warm-up (GPU clock ramp); 0: none")
     args = ap.parse_args()
 
@@ -338,7 +338,7 @@ def main():
                    "note": "untimed steps before the W warm-up steps, until --settle-ms of wall time has "
                            "passed: from an idle GPU the first ~40 ms of steps run at a lower clock "
                            "(C3, one box: 0.218-0.221 ms/step timed over 20 steps after 5 warm-up, "
-                           "0.2025 over 200 or 1000; profiles/r04/c3_settle.log)"},
+                           "0.2025 over 200 or 1000; 100 ms of settle measured as good as 300; profiles/r04/c3_settle.log)"},
     }
     if world > 1:
         line["runtime_per_rank"] = rts
