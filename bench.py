@@ -33,7 +33,7 @@ def kernels_digest() -> str:
     h = hashlib.sha256()
     src = os.path.join(ROOT, "regcm_amd", "csrc")
     for f in sorted(os.listdir(src)):
-        if f.endswith((".hip", ".hpp")):
+        if f.endswith((".hip", ".hpp")) or f == "Makefile":     # sources and their compile flags
             with open(os.path.join(src, f), "rb") as fh:
                 h.update(fh.read())
     return h.hexdigest()[:16]
