@@ -150,11 +150,12 @@ def cpu_baseline(rc, data, budget_s: float = 15.0, threads: int = 0):
     return res
 
 
-def settle(eng, seconds: float, dist):
+def settle(eng, seconds: float, bcast=None):
     """Untimed steps until `seconds` of wall time have passed on rank 0 (chunks doubling up to
-    64 steps; rank 0's decision is broadcast so every rank runs the same steps).  Returns
-    (steps, seconds).  From an idle GPU the first tens of milliseconds of work run below the
-    steady clock, which a timed window of K = 20 C3 steps (4 ms) would otherwise measure."""
+    64 steps; with more than one rank, bcast(int) -> int returns rank 0's decision, so every
+    rank runs the same steps).  Returns (steps, seconds).  From an idle GPU the first tens of
+    milliseconds of work run below the steady clock, which a timed window of K = 20 C3 steps
+    (4 ms) would otherwise measure."""
     if seconds <= 0:
         return 0, 0.0
     n, chunk, t0 = 0, 1, time.perf_counter()
@@ -163,11 +164,8 @@ def settle(eng, seconds: float, dist):
         eng.synchronize()
         n += chunk
         done = time.perf_counter() - t0 >= seconds
-        if dist is not None:
-            import torch
-            flag = torch.tensor([1 if done else 0], dtype=torch.int32)
-            dist.broadcast(flag, src=0)
-            done = bool(flag.item())
+        if bcast is not None:
+            done = bool(bcast(1 if done else 0))
         if done:
             return n, time.perf_counter() - t0
         chunk = min(2 * chunk, 64)
@@ -229,7 +227,13 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    settle_steps, settle_s = settle(eng, args.settle_ms * 1e-3, dist)
+    bcast = None
+    if dist is not None:
+        def bcast(v):
+            t = torch.tensor([v], dtype=torch.int32)
+            dist.broadcast(t, src=0)
+            return int(t.item())
+    settle_steps, settle_s = settle(eng, args.settle_ms * 1e-3, bcast)
     eng.step(args.warmup)
     barrier()
     t0 = time.perf_counter()

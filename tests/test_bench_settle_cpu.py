@@ -41,7 +41,13 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     eng = _CountingEngine(0.002 if rank == 0 else 0.0005)    # rank 1 three times faster
-    n, s = bench.settle(eng, 0.05, dist)
+    import torch
+
+    def bcast(v):
+        t = torch.tensor([v], dtype=torch.int32)
+        dist.broadcast(t, src=0)
+        return int(t.item())
+    n, s = bench.settle(eng, 0.05, bcast)
     q.put((rank, n, eng.steps, s))
     dist.destroy_process_group()
 
