@@ -21,6 +21,15 @@
 
 namespace rcm {
 
+// k_nh_tend_c is compiled in a translation unit of its own (kernels_nh_tc.hip includes this file
+// with RCM_NH_TEND_C_TU defined) so that the Makefile can give it its own device scheduler; the
+// other kernels are compiled here
+#ifdef RCM_NH_TEND_C_TU
+#define NH_OTHER_KERNELS 0
+#else
+#define NH_OTHER_KERNELS 1
+#endif
+
 static constexpr double EGRAV_NH = 9.80665;                 // Share/mod_constants.F90:85
 static constexpr double REARTHRAD = 1.0 / 6.371229e6;       // :282-284
 static constexpr double MATHPI = 3.1415926535897932384626433832795029;
@@ -77,6 +86,7 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 // the points exchange(th,1) fills: th is pointwise in atmx%t and atm1%pr, which are defined
 // there.  The other decoupled fields -- umc, vmc, umd, vmd and atmx w, pp, qv, qc -- are one
 // product (and clip) of a state field each and are formed by their readers.
+#if NH_OTHER_KERNELS
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
@@ -99,9 +109,11 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   if (IN_CI(j, i))
     F3(f.xpr, j, i, k) = (xtv - F3(f.t0, j, i, k) - xpp / (c->cpd * F3(f.rho0, j, i, k))) / xt;
 }
+#endif
 
 // compute_omega NH (:1157-1191), one thread per cross column: qdot from w and the terrain
 // slopes of the reference p*, then the mass divergence with the qdot term
+#if NH_OTHER_KERNELS
 __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
@@ -139,6 +151,7 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
     F3(f.cr, j, i, k) = (a + b) * dummy + (F3(f.qdot, j, i, k + 1) - F3(f.qdot, j, i, k)) * ps / c->dsigma[k];
   }
 }
+#endif
 
 // mkslice NH subset (Main/mod_slice.F90:163-183, 278-281): the b-level decoupled winds, t, q,
 // pp and w (atm2 times 1/psdotb or 1/psb, q clipped at minqq / 0) are formed by their readers
@@ -150,6 +163,7 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
 
 // calc_coeff NH (Main/mod_diffusion.F90:215-250): Smagorinsky coefficient with the
 // vertical-velocity term, unscaled (xkcr) ...
+#if NH_OTHER_KERNELS
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
@@ -164,6 +178,7 @@ __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f)
   const double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
   F3(f.xkcr, j, i, k) = dmin(F2(f.hgfact, j, i) + c->dydc * duv, c->xkhmax);
 }
+#endif
 
 // ... then scaled by rdxsq and p* (b) by their readers: xkc, xkcf (cross interior, full
 // levels: xkcr of level k-1) in k_nh_tend_c, xkd (dot interior, the four-point mean) in
@@ -232,6 +247,7 @@ __device__ __forceinline__ double diffx_at(const Geom& g, const Consts* c, doubl
 // atm2 fields of mkslice (Main/mod_slice.F90:163-183, 215-238).  blockIdx.z: 0 u and v, 1 t,
 // 2 qv, 3 qc, 4 pp, 5 w, 6.. qi, qr, qs (nqx = 5); blockIdx.y = level.  k_nh_tend_c /
 // k_nh_tend_d / k_nh_qx_tend add them in the reference's place of the diffusion term.
+#if NH_OTHER_KERNELS
 __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs qx) {
   const int i = g.ide1 + (int)(blockIdx.x * blockDim.x + threadIdx.x), k = (int)blockIdx.y + 1;
   const int q0 = (int)blockIdx.z, kz = c->kz;
@@ -262,6 +278,7 @@ __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, Qx
   const double xkc = d_one * (c->diff6 * F2(ps, j, i));
   F3(d6, j, i, k) = xkc * diffu6_bracket(j, i, g.gjx - 1, g.giy - 1, fv, lv);
 }
+#endif
 // the column term where k_nh_tend_c / k_nh_tend_d add diffusion
 __device__ __forceinline__ double diff6_add(const Geom& g, double ften, const double* d6, int jc, int j, int i, int k) {
   return j == jc ? ften + F3(d6, j, i, k) : ften;
@@ -358,6 +375,13 @@ constexpr int TC_NF = 5;
 #ifndef TC_W
 #define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
 #endif
+// relaxation and physics-tendency terms of k_nh_tend_c and k_nh_tend_d (#undef after k_nh_tend_d)
+#define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
+#define RELAX5(x, b0, bt, a) \
+  x = nh_relax(x, xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), FG(b0, bt, a, j + 1, i), \
+               FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
+#define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
+#if !NH_OTHER_KERNELS
 template <bool QX>
 __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, NHFields f, int wdiag,
@@ -457,11 +481,6 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     else if (c->iboudy == 1) { xf = c->fcx[ib]; xg = c->gcx[ib]; }
     else { xf = c->hefc[ib][kc]; xg = c->hegc[ib][kc]; }
   }
-#define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
-#define RELAX5(x, b0, bt, a) \
-  x = nh_relax(x, xf, xg, FG(b0, bt, a, j, i), FG(b0, bt, a, j - 1, i), FG(b0, bt, a, j + 1, i), \
-               FG(b0, bt, a, j, i - 1), FG(b0, bt, a, j, i + 1))
-#define PHY(p) (f.p ? F3(f.p, j, i, k) : 0.0)
   // ================= w on full levels k = 1..kz+1
   {
     double wd = d_zero;
@@ -639,6 +658,8 @@ template __global__ void k_nh_tend_c<false>(Geom, const Consts* __restrict__, co
                                              int, int);
 template __global__ void k_nh_tend_c<true>(Geom, const Consts* __restrict__, const StepState* __restrict__, NHFields,
                                             int, int);
+#endif
+#if NH_OTHER_KERNELS
 
 // k_nh_tend_d stages its horizontal stencil operands of one level for a 64 x 4 block plus a
 // 2-point halo in LDS, one load (and for ubd/msfd, vbd/msfd one division) per staged point:
@@ -1430,4 +1451,5 @@ __global__ void k_nh_bdyval_w1(Geom g, NHFields f) {
   }
 }
 
+#endif  // NH_OTHER_KERNELS
 }  // namespace rcm
