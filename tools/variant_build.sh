@@ -11,11 +11,11 @@ rm -rf $W && mkdir -p $W/regcm_amd/csrc $W/include
 cp regcm_amd/csrc/*.hip regcm_amd/csrc/*.hpp regcm_amd/csrc/Makefile $W/regcm_amd/csrc/
 cp include/*.h $W/include/
 mkdir -p varlib
-# SCHED_NH="<flags>" replaces the Makefile's device-scheduler flags of kernels_nh.hip
-if [ -n "${SCHED_NH+x}" ]; then
-  make -s -C $W/regcm_amd/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function $*" SCHED_kernels_nh="$SCHED_NH"
-else
-  make -s -C $W/regcm_amd/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function $*"
-fi
+# SCHED_NH="<flags>" replaces the Makefile's device-scheduler flags of kernels_nh.hip, SCHED_K those
+# of kernels.hip (SCHED_kernels)
+MV=()
+[ -n "${SCHED_NH+x}" ] && MV+=("SCHED_kernels_nh=$SCHED_NH")
+[ -n "${SCHED_K+x}" ] && MV+=("SCHED_kernels=$SCHED_K")
+make -s -C $W/regcm_amd/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function $*" "${MV[@]}"
 cp $W/regcm_amd/librcmdyn.so varlib/var_$name.so
 echo "built varlib/var_$name.so"
