@@ -106,6 +106,21 @@ def test_c2_hundred_steps_rel_l2():
     check_close(e, o, rc, STATE_FIELDS, 1e-9, 1e-7, "C2 100 steps")
 
 
+def test_c3_hundred_steps_rel_l2():
+    """The headline grid over a longer run: C3, 100 steps (4.2 simulated hours, past the
+    leapfrog dt switch and two flag-reduction intervals of the graph replay), rel-L2 <= 1e-9
+    per prognostic field, SURVEY 8(c)'s 100-step bound."""
+    rc = CONFIGS["C3"]
+    data = icbc.generate(rc)
+    o, e = oracle(rc, data), engine(rc, data)
+    for n in range(4):
+        o.step(25)
+        e.step(25)
+        say("C3 step", 25 * (n + 1))
+    assert e.get_time() == o.get_time()
+    check_close(e, o, rc, STATE_FIELDS, 1e-9, 1e-7, "C3 100 steps")
+
+
 def test_c4_two_by_two_tiles():
     """C4 (384x384x23 on 2x2 tiles): the decomposed engine is bit-identical to one tile over
     3 steps, and both match the oracle after 2 steps."""
