@@ -185,3 +185,17 @@ def test_n2_vs_oracle():
     o.step(2)
     e.step(2)
     check_close(e, o, rc, NH_FIELDS, 1e-10, 1e-10, "N2 3 steps")
+
+
+def test_n2_hundred_steps_rel_l2():
+    """The NH core over a longer run: N2, 100 steps (graph-replayed after the first two),
+    rel-L2 <= 1e-9 per prognostic field, SURVEY 8(c)'s 100-step bound."""
+    rc = CONFIGS["N2"]
+    data = icbc.generate_nh(rc)
+    o, e = oracle(rc, data), engine(rc, data)
+    for n in range(4):
+        o.step(25)
+        e.step(25)
+        say("N2 step", 25 * (n + 1))
+    assert e.get_time() == o.get_time()
+    check_close(e, o, rc, NH_FIELDS, 1e-9, 1e-7, "N2 100 steps")
