@@ -29,6 +29,9 @@ constexpr int MBJ = 64, MBI = RCM_MBI, MBT = MBJ * MBI;
 #define RCM_SBI 8
 #endif
 constexpr int SBJ = 64, SBI = RCM_SBI, SBT = SBJ * SBI;
+// other block heights were round-3 experiments; the round-4 build (k_update, the species) is
+// tested with 64 x 8 only, and 64 x 4 fails a parity test there
+static_assert(MBI == 8 && SBI == 8, "RCM_MBI / RCM_SBI other than 8 are not supported");
 struct SegList {
   Seg s[MAXSEG];
   int n;
