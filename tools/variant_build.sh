@@ -12,10 +12,11 @@ cp regcm_amd/csrc/*.hip regcm_amd/csrc/*.hpp regcm_amd/csrc/Makefile $W/regcm_am
 cp include/*.h $W/include/
 mkdir -p varlib
 # SCHED_NH="<flags>" replaces the Makefile's device-scheduler flags of kernels_nh.hip, SCHED_K those
-# of kernels.hip (SCHED_kernels)
+# of kernels.hip (SCHED_kernels), SCHED_TC those of kernels_nh_tc.hip (k_nh_tend_c)
 MV=()
 [ -n "${SCHED_NH+x}" ] && MV+=("SCHED_kernels_nh=$SCHED_NH")
 [ -n "${SCHED_K+x}" ] && MV+=("SCHED_kernels=$SCHED_K")
+[ -n "${SCHED_TC+x}" ] && MV+=("SCHED_kernels_nh_tc=$SCHED_TC")
 make -s -C $W/regcm_amd/csrc -j8 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wno-unused-function $*" "${MV[@]}"
 cp $W/regcm_amd/librcmdyn.so varlib/var_$name.so
 echo "built varlib/var_$name.so"
