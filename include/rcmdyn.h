@@ -243,7 +243,9 @@ int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
  * (-1 for collectives); count = doubles (collectives: elements); signature = hash of the
  * message's box shapes (0 for collectives).  *count = records in the plan (at most cap are
  * written).  Every message A sends B must be the receive B posts from A, in the same order on
- * the same channel, which a multi-rank job needs and tests check. */
+ * the same channel, which a multi-rank job needs and tests check.  The plan models no put
+ * between steps: a KPBL put (ibltyp = 2, iuwvadv = 1, hydrostatic) adds one width-1 exchange
+ * of kpbl before the next tend, on every rank alike. */
 int rcmdyn_exchange_plan(const rcmdyn_config* cfg, int32_t nsteps, int64_t* ops, int64_t cap, int64_t* count);
 /* Halo/compute overlap of the hydrostatic step, host-only (no GPU): for each of the first cap
  * tiles this engine would own, out[6q .. 6q+5] = {k_columns points in the part-1 rectangle R,
@@ -290,7 +292,11 @@ int rcmdyn_step(rcmdyn_t* h, int32_t nsteps);  /* nsteps x (tend + bdyval), grap
 /* Waits for the device and reports a failure of any step issued so far.  In RCCL mode it is
  * COLLECTIVE (it max-reduces the step error flags over the job so that every rank stops at
  * the same call): every rank must call it, as every rank calls rcmdyn_step and
- * rcmdyn_reductions. */
+ * rcmdyn_reductions.  In RCCL mode a step failure (CFL / NaN / departure point) this rank's
+ * own flags hold is sticky at the host read points (get, diagnostics): it is reported there
+ * before the job-wide reduction carries it, and again at every later read, until
+ * rcmdyn_set_time (the host's restart from a SAV state) clears the flags.  The reference's
+ * fatal ends the job there (Main/abort.F90:20-36), as a host should. */
 int rcmdyn_synchronize(rcmdyn_t* h);
 
 /* Diagnostics of the last tend: out[0]=ptntot, out[1]=pt2tot (Bleck noise sums of the

@@ -643,6 +643,26 @@ struct rcmdyn_engine {
     return f;
   }
 
+  // The LDS-tiled kernels stage a tile sized at compile time (their __launch_bounds__ = the
+  // tile's thread count) and index it by threadIdx; their launches take grid and block from the
+  // same kernels.hpp constants.  Check once that the code objects were built for those tiles, so
+  // a block-size mismatch between a kernel and its launch fails here, not as unwritten points.
+  void check_block_sizes() {
+    struct K { const void* f; int threads; const char* name; };
+    const K ks[] = {{(const void*)k_update, SBT, "k_update"},
+                    {(const void*)k_momentum, MBT, "k_momentum"},
+                    {(const void*)k_scalars, SBT, "k_scalars"},
+                    {(const void*)k_qx_tend, QBT, "k_qx_tend"}};
+    for (const K& k : ks) {
+      hipFuncAttributes a{};
+      HIPCHK(hipFuncGetAttributes(&a, k.f));
+      if (a.maxThreadsPerBlock != k.threads)
+        throw std::runtime_error(std::string("rcmdyn: ") + k.name + " was compiled for " +
+                                 std::to_string(a.maxThreadsPerBlock) + " threads per block, launched with " +
+                                 std::to_string(k.threads));
+    }
+  }
+
   void create(const rcmdyn_config* c, std::vector<PlanOp>* plan = nullptr) {
     cfg = *c;
     dry = plan != nullptr;
@@ -707,6 +727,7 @@ struct rcmdyn_engine {
       comm.reset(make_plan_comm(cfg.comm_rank, plan));
       return;
     }
+    check_block_sizes();
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&dc, sizeof(Consts)));
     HIPCHK(hipMemcpy(dc, &hc, sizeof(Consts), hipMemcpyHostToDevice));
@@ -1062,7 +1083,9 @@ struct rcmdyn_engine {
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
     if ((f >= RCMDYN_XUB_B0 && f <= RCMDYN_XPSB_BT) || (f >= RCMDYN_XPPB_B0 && f <= RCMDYN_XWWB_BT)) bdy_dirty = true;
-    if (f == RCMDYN_KPBL) kpbl_dirty = true;
+    // only the hydrostatic vadv4d ind = 3 (k_scalars, k_qx_tend) reads kpbl on the ghost ring;
+    // the NH kernels read it at their own point
+    if (f == RCMDYN_KPBL && hc.iqxvadv == 3 && cfg.idynamic != 2) kpbl_dirty = true;
     ghosts_stale = true;
     if (f >= RCMDYN_ATM0_PS && f <= RCMDYN_CRY) invalidate_graphs();
   }
@@ -2053,7 +2076,7 @@ struct rcmdyn_engine {
       // nqx = 5: the hydrometeors beyond qc, their forecast (and ring), then the fix and filter
       each([&](Tile& t) {
         const Geom& g = t.g;
-        KLAUNCH(k_qx_tend, dim3((g.jcx2() - g.jcx1() + SBJ) / SBJ, (g.icx2() - g.icx1() + SBI) / SBI, kz), dim3(SBT),
+        KLAUNCH(k_qx_tend, dim3((g.jcx2() - g.jcx1() + QBJ) / QBJ, (g.icx2() - g.icx1() + QBI) / QBI, kz), dim3(QBT),
                 0, stream, g, dc, ds, fields(t), qx_args(t));
       });
       if (!fused) {
@@ -2173,17 +2196,17 @@ struct rcmdyn_engine {
   // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
   void settle() {
     if (!corr_pending) return;
+    launch_corrections(false);     // if this throws, the corrections stay pending for the next call
     corr_pending = false;
-    launch_corrections(false);
     note_step(hs.lcount);
   }
   // rcmdyn_bdyval after a deferring tend: the corrections with the boundary lines, then the
   // rest of bdyval as rcmdyn_step runs it
   void fused_bdyval() {
-    corr_pending = false;
     fuse_bdy = true;
     try {
       launch_corrections(true);
+      corr_pending = false;
       bdyval();
     } catch (...) {
       fuse_bdy = false;

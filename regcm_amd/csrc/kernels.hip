@@ -1851,11 +1851,7 @@ __device__ __forceinline__ void split_correct_body(
   const bool di0 = idi && in(jp, g.jdi1, jd2), di1 = idi && in(jp + 1, g.jdi1, jd2);
   // every operand is loaded before the first store (the state buffers are not __restrict__:
   // a store would order the later loads behind it)
-#ifdef SKIP_CORR3D
-  const bool cx = k == 1 && (ci0 || ci1), dx = false;
-#else
   const bool cx = ci0 || ci1, dx = di0 || di1;
-#endif
   double dd[2][NS];
   double2 pa{}, pb{}, t1{}, t2{}, u1{}, v1{}, u2{}, v2{}, pd{}, md{};
   double2 h0[NS], hs[NS];

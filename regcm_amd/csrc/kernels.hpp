@@ -29,9 +29,16 @@ constexpr int MBJ = 64, MBI = RCM_MBI, MBT = MBJ * MBI;
 #define RCM_SBI 8
 #endif
 constexpr int SBJ = 64, SBI = RCM_SBI, SBT = SBJ * SBI;
-// other block heights were round-3 experiments; the round-4 build (k_update, the species) is
-// tested with 64 x 8 only, and 64 x 4 fails a parity test there
-static_assert(MBI == 8 && SBI == 8, "RCM_MBI / RCM_SBI other than 8 are not supported");
+// k_update runs a momentum block or a scalars block in every workgroup of one launch, so the
+// two block kinds must have the same thread count (their heights may differ only with it)
+static_assert(MBT == SBT, "k_update launches momentum and scalars blocks with one block size");
+// LDS-tiled species block of k_qx_tend (cross points j x i at one level).  Independent of the
+// scalars tile: the launch in tend_post uses these constants, and the engine checks at create
+// that the kernel was compiled for QBT threads (check_block_sizes, engine.hip)
+#ifndef RCM_QBI
+#define RCM_QBI 8
+#endif
+constexpr int QBJ = 64, QBI = RCM_QBI, QBT = QBJ * QBI;
 struct SegList {
   Seg s[MAXSEG];
   int n;

@@ -35,7 +35,7 @@
 namespace rcm {
 
 namespace {
-constexpr int QBJ = 64, QBI = 8, QBT = QBJ * QBI;
+// QBJ x QBI (kernels.hpp): the launch's grid and block come from the same constants
 constexpr int QDW = QBJ + 1, QDH = QBI + 1;    // dot points j..j+QBJ, i..i+QBI
 constexpr int QW1 = QBJ + 2, QH1 = QBI + 2;    // halo 1
 constexpr int QW2 = QBJ + 4, QH2 = QBI + 4;    // halo 2

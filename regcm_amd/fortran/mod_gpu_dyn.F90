@@ -162,11 +162,78 @@ module mod_gpu_dyn
       import :: c_int, c_int8_t
       integer(c_int8_t), intent(out) :: out(128)
     end function
+    ! waits for the device and reports any failed step; COLLECTIVE in RCCL mode (every rank
+    ! calls it, as every rank calls rcmdyn_step)
+    integer(c_int) function rcmdyn_synchronize(h) bind(c, name='rcmdyn_synchronize')
+      import :: c_int, c_ptr
+      type(c_ptr), value :: h
+    end function
+    ! set_nproc (Main/mpplib/mod_mppparam.F90:1053-1371), host-only: cpus = (cpus_j, cpus_i)
+    integer(c_int) function rcmdyn_set_nproc(nproc, jx, iy, cpus) bind(c, name='rcmdyn_set_nproc')
+      import :: c_int, c_int32_t
+      integer(c_int32_t), value :: nproc, jx, iy
+      integer(c_int32_t), intent(out) :: cpus(2)
+    end function
+    ! ext = (jde1,jde2,ide1,ide2,jce1,jce2,ice1,ice2), bdy = (left,right,bottom,top), host-only
+    integer(c_int) function rcmdyn_tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy) &
+        bind(c, name='rcmdyn_tile_extent')
+      import :: c_int, c_int32_t
+      integer(c_int32_t), value :: jx, iy, nproc_j, nproc_i, tile
+      integer(c_int32_t), intent(out) :: ext(8), bdy(4)
+    end function
+    ! the communication calls of one rank (7 int64 per record), host-only
+    integer(c_int) function rcmdyn_exchange_plan(cfg, nsteps, ops, cap, count) bind(c, name='rcmdyn_exchange_plan')
+      import :: c_int, c_int32_t, c_int64_t, rcmdyn_config
+      type(rcmdyn_config), intent(in) :: cfg
+      integer(c_int32_t), value :: nsteps
+      integer(c_int64_t), intent(out) :: ops(*)
+      integer(c_int64_t), value :: cap
+      integer(c_int64_t), intent(out) :: count
+    end function
+    ! per tile, the points of the update kernels that run beside the prologue exchange
+    integer(c_int) function rcmdyn_overlap_shares(cfg, out, cap) bind(c, name='rcmdyn_overlap_shares')
+      import :: c_int, c_int32_t, rcmdyn_config
+      type(rcmdyn_config), intent(in) :: cfg
+      integer(c_int32_t), intent(out) :: out(*)
+      integer(c_int32_t), value :: cap
+    end function
+    ! the HIP runtime and librccl the engine is bound to (a NUL-terminated string)
+    integer(c_int) function rcmdyn_runtime_info(buf, len) bind(c, name='rcmdyn_runtime_info')
+      import :: c_int, c_char, c_int32_t
+      character(kind=c_char), intent(out) :: buf(*)
+      integer(c_int32_t), value :: len
+    end function
+    ! average device ms per step of the last rcmdyn_step call
+    integer(c_int) function rcmdyn_last_step_ms(h, ms) bind(c, name='rcmdyn_last_step_ms')
+      import :: c_int, c_ptr, c_double
+      type(c_ptr), value :: h
+      real(c_double), intent(out) :: ms
+    end function
+    ! the per-point tendency diagnostics (f_tten .. f_xkc) on (1) or off (0, the default)
+    integer(c_int) function rcmdyn_set_diagnostics(h, on) bind(c, name='rcmdyn_set_diagnostics')
+      import :: c_int, c_ptr, c_int32_t
+      type(c_ptr), value :: h
+      integer(c_int32_t), value :: on
+    end function
+    ! per-kernel device time over nsteps eager steps (names: 48 characters per kernel)
+    integer(c_int) function rcmdyn_kernel_times(h, nsteps, cap, names, launches, avg_ms, count) &
+        bind(c, name='rcmdyn_kernel_times')
+      import :: c_int, c_ptr, c_int32_t, c_char, c_double
+      type(c_ptr), value :: h
+      integer(c_int32_t), value :: nsteps, cap
+      character(kind=c_char), intent(out) :: names(*)
+      integer(c_int32_t), intent(out) :: launches(*)
+      real(c_double), intent(out) :: avg_ms(*)
+      integer(c_int32_t), intent(out) :: count
+    end function
   end interface
 
   public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
   public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics, rcmdyn_reductions
-  public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics, rcmdyn_bdyin
+  public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics, rcmdyn_bdyin, rcmdyn_last_error
+  public :: rcmdyn_synchronize, rcmdyn_set_nproc, rcmdyn_tile_extent, rcmdyn_exchange_plan
+  public :: rcmdyn_overlap_shares, rcmdyn_runtime_info, rcmdyn_last_step_ms, rcmdyn_set_diagnostics
+  public :: rcmdyn_kernel_times
   public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d
 
   contains
