@@ -65,6 +65,14 @@ static __device__ int rcm_pt_count = 0;
   const int k = (int)blockIdx.z + 1;                              \
   (void)k;
 
+// The frame's rows start on 128-B lines (pitch of 16 doubles), but the index ranges start a
+// few points in (jde1 = j0 + G): a 64-wide wavefront from jde1 touches five lines per field
+// instead of four, and the fifth is fetched again by the neighbouring block (another XCD).
+// ALIGN_J moves a box's first thread column down to the line boundary at or below j1 (those
+// lanes idle: every such kernel rejects j < j1 by its own range test); jalign (engine.hpp) is
+// the host's matching count of extra columns for the grid.
+#define ALIGN_J(j1) ((j1) - jalign(g, j1))
+
 // psc2psd at one dot point, Main/mpplib/mod_mppparam.F90:13811-13862.
 __device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int j, int i, double& v) {
   if (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2)) {

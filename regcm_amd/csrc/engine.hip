@@ -265,6 +265,7 @@ struct rcmdyn_engine {
   int gslot = 0;
   bool statics_dirty = true;
   bool bdy_dirty = true;
+  bool dprd_put = false;      // NH: dprddx / dprddy put since the last check (check_dprd)
   bool kpbl_dirty = false;    // kpbl put since the last tend: its ghost ring is stale
   bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
   bool capturing = false;
@@ -1088,6 +1089,7 @@ struct rcmdyn_engine {
     if (f == RCMDYN_KPBL && hc.iqxvadv == 3 && cfg.idynamic != 2) kpbl_dirty = true;
     ghosts_stale = true;
     if (f >= RCMDYN_ATM0_PS && f <= RCMDYN_CRY) invalidate_graphs();
+    if (f == RCMDYN_DPRDDX || f == RCMDYN_DPRDDY || (dprd_put && f == RCMDYN_ATM0_PR)) dprd_put = true;
   }
 
   // physics coupling seam: the pc_physic buffers exist from the first put of one of them on
@@ -1518,6 +1520,28 @@ struct rcmdyn_engine {
     exchange_generic(fn, on, on);
   }
 
+  // NH_DPRFORM: the acoustic update forms dprddx / dprddy from atm0%pr as the reference
+  // defines them (Main/mod_params.F90:2676-2686); values a host put must be exactly those, or
+  // the engine would silently compute with others
+  void check_dprd() {
+    dprd_put = false;
+    if (!NH_DPRFORM || cfg.idynamic != 2 || dry) return;
+    int* bad = nullptr;
+    HIPCHK(hipMalloc(&bad, sizeof(int)));
+    HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), stream));
+    for (auto& t : tiles) {
+      const Geom& g = t.g;
+      KLAUNCH(k_nh_check_dprd, grid3(g.jdi2 - g.jdi1 + 1, g.idi2 - g.idi1 + 1, cfg.kz), BLK, 0, stream, g,
+              nhf[&t - tiles.data()], bad);
+    }
+    int n = 0;
+    HIPCHK(hipMemcpyAsync(&n, bad, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(hipFree(bad));
+    if (n) throw std::runtime_error("rcmdyn: DPRDDX/DPRDDY differ from atm0%pr's four-point differences at " +
+                                    std::to_string(n) + " points (Main/mod_params.F90:2676-2686)");
+  }
+
   // ------------------------------------------------------------------ the step
   template <class F>
   void each(F fn) { for (auto& t : tiles) fn(t); }
@@ -1540,6 +1564,7 @@ struct rcmdyn_engine {
       statics_dirty = false;
       invalidate_graphs();
     }
+    if (dprd_put) check_dprd();
     if (bdy_dirty) {
       const int kz = cfg.kz;
       // width 2: the ghost-ring kernels relax at ghost points (stencil radius 1)
@@ -1693,14 +1718,16 @@ struct rcmdyn_engine {
     // on the second stream beside k_nh_tend_c (which reads them at its own point only), the
     // cqv/cqc exchange beside k_nh_tend_d (which does not read them)
     const bool ovl = ntiles > 1 && !no_overlap && phase == TEND_ALL && !slice && cfg.isladvec != 1;
-    struct Grids { dim3 fr, ce1, cek, ci1, cik, cik1, di1, dik; };
+    // ci1a: the interior cross columns from the 128-B line at or below jci1 (NH_ALIGN)
+    struct Grids { dim3 fr, ce1, cek, ci1, cik, cik1, di1, dik, ci1a; };
     auto grids = [&](const Geom& g) {
       const int nce_j = g.jce2 - g.jce1 + 1, nce_i = g.ice2 - g.ice1 + 1;
       const int nci_j = g.jci2 - g.jci1 + 1, nci_i = g.ici2 - g.ici1 + 1;
       const int ndi_j = g.jdi2 - g.jdi1 + 1, ndi_i = g.idi2 - g.idi1 + 1;
       return Grids{grid3(g.nj, g.ni, kp), grid3(nce_j, nce_i, 1), grid3(nce_j, nce_i, kz),
                    grid3(nci_j, nci_i, 1), grid3(nci_j, nci_i, kz), grid3(nci_j, nci_i, kz - 1),
-                   grid3(ndi_j, ndi_i, 1), grid3(ndi_j, ndi_i, kz)};
+                   grid3(ndi_j, ndi_i, 1), grid3(ndi_j, ndi_i, kz),
+                   grid3(nci_j + (NH_ALIGN ? jalign(g, g.jci1) : 0), nci_i, 1)};
     };
     if (phase & TEND_PRE) {
     // isladvec = 1: k_sladv forms ud*msfd two points out (the reference exchanges atmx%ud 2
@@ -1817,8 +1844,8 @@ struct rcmdyn_engine {
                     fin, first, 2);
           return;
         }
-        KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1, g.ide2 - g.ide1 + 1, kz), BLK, 0, stream, g, dc, ds,
-                nhfields(t), istep, fin, first, part);
+        KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1 + (NH_ALIGN ? jalign(g, g.jde1) : 0), g.ide2 - g.ide1 + 1, kz),
+                BLK, 0, stream, g, dc, ds, nhfields(t), istep, fin, first, part);
       };
       if (ntiles > 1 && !no_overlap) {
         side_begin();
@@ -1836,7 +1863,7 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
-        KLAUNCH(k_nh_sound_bc, q.ci1, BLK, 0, stream, g, dc, ds, f, istep, it);
+        KLAUNCH(k_nh_sound_bc, q.ci1a, BLK, 0, stream, g, dc, ds, f, istep, it);
       });
       if (cfg.ifupr == 1) {
         if (it == 1 && alarm) {
@@ -1857,10 +1884,10 @@ struct rcmdyn_engine {
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
         if (ntiles > 1)
-          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
+          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD ? q.ci1a : q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
                   (int)(it < istep));
         else
-          KLAUNCH(k_nh_sound_cd, q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep),
+          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD ? q.ci1a : q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep),
                   (int)(it < istep));
       });
     }

@@ -76,6 +76,8 @@ struct Geom {
     return j >= 3 && j <= gjx - 2 && i >= 3 && i <= giy - 2;
   }
 };
+// columns between j1 and the frame's 128-B line boundary at or below it (ALIGN_J, devcommon.hpp)
+__host__ __device__ __forceinline__ int jalign(const Geom& g, int j1) { return (j1 - g.j0) & 15; }
 
 // Run constants (read-only on device, one copy per engine).
 struct Consts {

@@ -23,12 +23,18 @@ constexpr int SPX = SPH + 1;
 #ifndef RCM_MBI
 #define RCM_MBI 8
 #endif
-constexpr int MBJ = 64, MBI = RCM_MBI, MBT = MBJ * MBI;
+#ifndef RCM_MBJ
+#define RCM_MBJ 64
+#endif
+constexpr int MBJ = RCM_MBJ, MBI = RCM_MBI, MBT = MBJ * MBI;
 // LDS-tiled scalar (t, qv, qc) block (cross points j x i at one level)
 #ifndef RCM_SBI
 #define RCM_SBI 8
 #endif
-constexpr int SBJ = 64, SBI = RCM_SBI, SBT = SBJ * SBI;
+#ifndef RCM_SBJ
+#define RCM_SBJ 64
+#endif
+constexpr int SBJ = RCM_SBJ, SBI = RCM_SBI, SBT = SBJ * SBI;
 // k_update runs a momentum block or a scalars block in every workgroup of one launch, so the
 // two block kinds must have the same thread count (their heights may differ only with it)
 static_assert(MBT == SBT, "k_update launches momentum and scalars blocks with one block size");

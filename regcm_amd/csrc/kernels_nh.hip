@@ -944,6 +944,20 @@ __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f
   nh_sound_a1_at(g, c, f, j, i, k);
 }
 
+// NH_DPRFORM: the acoustic u, v update forms dprddx / dprddy from atm0%pr; a host that puts
+// them is checked once, after the put, to hold exactly those sums (Main/mod_params.F90:2676-2686)
+// on the interior dot points the update reads (bad[0]: count of differing values)
+__global__ void k_nh_check_dprd(Geom g, NHFields f, int* bad) {
+  THREAD_POINT(g.jdi1, g.idi1);
+  if (!IN_DI(j, i)) return;
+  const double* pr = f.pr0;
+  const double p00 = F3(pr, j, i, k), pm0 = F3(pr, j - 1, i, k), p0m = F3(pr, j, i - 1, k), pmm = F3(pr, j - 1, i - 1, k);
+  const double dx = p00 - pm0 + p0m - pmm, dy = p00 - p0m + pm0 - pmm;
+  const int n = (int)(__double_as_longlong(dx) != __double_as_longlong(F3(f.dprddx, j, i, k))) +
+                (int)(__double_as_longlong(dy) != __double_as_longlong(F3(f.dprddy, j, i, k)));
+  if (n) atomicAdd(bad, n);
+}
+
 // substep part B (:266-296): pressure-gradient update of u, v plus their tendencies
 __device__ __forceinline__ void nh_sound_uv_at(const Geom& g, const Consts* __restrict__ c,
                                                const StepState* __restrict__ s, const NHFields& f, int istep,
@@ -966,10 +980,19 @@ __device__ __forceinline__ void nh_sound_uv_at(const Geom& g, const Consts* __re
                                    F3(f.cdt, j - 1, i - 1, k));
   const double chh = d_half * dts / (rho * c->dx) / F2(f.msfd, j, i);
   const double* pp = f.cpp;
+#if NH_DPRFORM
+  // atm0%dprddx / dprddy (Main/mod_params.F90:2678-2681), formed from atm0%pr as the reference
+  // forms them once: the same four-point sums in the same order, so the same bits
+  const double* pr = f.pr0;
+  const double p00 = F3(pr, j, i, k), pm0 = F3(pr, j - 1, i, k), p0m = F3(pr, j, i - 1, k), pmm = F3(pr, j - 1, i - 1, k);
+  const double dprx = p00 - pm0 + p0m - pmm, dpry = p00 - p0m + pm0 - pmm;
+#else
+  const double dprx = F3(f.dprddx, j, i, k), dpry = F3(f.dprddy, j, i, k);
+#endif
   double u = (first ? init_u(j, i) : F3(f.cu, j, i, k)) - chh * (F3(pp, j, i, k) - F3(pp, j - 1, i, k) + F3(pp, j, i - 1, k) -
-                                        F3(pp, j - 1, i - 1, k) - F3(f.dprddx, j, i, k) * dppdp0);
+                                        F3(pp, j - 1, i - 1, k) - dprx * dppdp0);
   double v = (first ? init_v(j, i) : F3(f.cv, j, i, k)) - chh * (F3(pp, j, i, k) - F3(pp, j, i - 1, k) + F3(pp, j - 1, i, k) -
-                                        F3(pp, j - 1, i - 1, k) - F3(f.dprddy, j, i, k) * dppdp0);
+                                        F3(pp, j - 1, i - 1, k) - dpry * dppdp0);
   const double cu = u + F3(f.uten, j, i, k), cv = v + F3(f.vten, j, i, k);
   F3(f.cu, j, i, k) = cu;
   F3(f.cv, j, i, k) = cv;
@@ -1004,7 +1027,7 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
     nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
     return;
   }
-  THREAD_POINT(g.jde1, g.ide1);
+  THREAD_POINT(NH_ALIGN ? ALIGN_J(g.jde1) : g.jde1, g.ide1);
   if (part == 1 && nh_uv_strip(g, j, i)) return;
   nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
 }
@@ -1072,7 +1095,7 @@ __device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, c
 __global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c,
                                                              const StepState* __restrict__ s, NHFields f,
                                                              int istep, int it) {
-  THREAD_POINT(g.jci1, g.ici1);
+  THREAD_POINT(NH_ALIGN ? ALIGN_J(g.jci1) : g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double dts = s->dt / (double)istep;
@@ -1239,7 +1262,7 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
   __shared__ double sM[169];
   __shared__ unsigned long long sred[4];
   const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
-  const int J0 = g.jci1 + (int)blockIdx.x * 64, I0 = g.ici1 + (int)blockIdx.y * 4;
+  const int J0 = (NH_ALIGN_CD ? ALIGN_J(g.jci1) : g.jci1) + (int)blockIdx.x * 64, I0 = g.ici1 + (int)blockIdx.y * 4;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   const bool upr = c->ifupr == 1;
   if (upr) {

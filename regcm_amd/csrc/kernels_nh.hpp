@@ -74,6 +74,21 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_ZFIRST
 #define NH_ZFIRST 1
 #endif
+// acoustic kernels: thread columns aligned to the frame's 128-B lines (ALIGN_J, devcommon.hpp).
+// C5, alternating on one box (profiles/r05/c5_nh_align_ab.log): k_nh_sound_bc 762 -> 747 us;
+// k_nh_sound_uv unchanged; k_nh_sound_cd 905-953 -> 981-1019 us (its 13th block column of
+// mostly idle lanes lengthens a latency-bound column walk), so cd keeps the unaligned map
+#ifndef NH_ALIGN
+#define NH_ALIGN 1
+#endif
+#ifndef NH_ALIGN_CD
+#define NH_ALIGN_CD 0
+#endif
+// k_nh_sound_uv forms atm0%dprddx / dprddy from atm0%pr where it reads them
+// (Main/mod_params.F90:2676-2686: four-point sums, no rounding beyond the reference's)
+#ifndef NH_DPRFORM
+#define NH_DPRFORM 1
+#endif
 
 struct QxArgs;
 __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs q);
@@ -86,6 +101,7 @@ __global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepStat
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_check_dprd(Geom g, NHFields f, int* bad);
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int fin, int first, int part);
 __global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
 __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields f, double* gbuf);

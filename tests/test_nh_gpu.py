@@ -119,6 +119,26 @@ def test_nh_rest_state():
         assert np.abs(e.get(n)[:, :-1, :-1] / ps).max() < lim, n
 
 
+def test_nh_dprddx_formed_from_pr(nh_data):
+    """The acoustic u, v update forms atm0%dprddx / dprddy from atm0%pr
+    (Main/mod_params.F90:2676-2686); the host's put of the reference's values passes the
+    engine's check, and a put that is not those four-point sums is refused at the next call
+    instead of being silently replaced."""
+    from regcm_amd.dycore import DynCore, EngineError
+    rc, data = nh_data
+    e = DynCore(rc, data["split"])
+    e.put_state(data["state"])
+    e.bdyval()
+    e.step(1)
+    bad = data["state"]["DPRDDX"].copy()
+    bad[3, 10, 10] += 1e-9
+    e.put("DPRDDX", bad)
+    with pytest.raises(EngineError, match="DPRDDX/DPRDDY differ"):
+        e.step(1)
+    e.put("DPRDDX", data["state"]["DPRDDX"])
+    e.step(1)
+
+
 NH_VARIANTS = [{"iboudy": 4}, {"iboudy": 3}, {"iboudy": 2}, {"idiffu": 2}, {"idiffu": 3}, {"ifupr": 0}, {"ifrayd": 0}, {"isladvec": 1},
                {"upstream_mode": 0}, {"stability_enhance": 0}, {"ipptls": 2}]
 # idiffu = 3 depends on the decomposition as the reference's does (test_nh_idiffu3_tiles), and

@@ -57,4 +57,5 @@ kt = e.kernel_times(5)
 for name, (n, us) in sorted(kt.items(), key=lambda kv: -kv[1][1] * kv[1][0]):
     print(f"  {name:32s} {n / 5:4.1f}/step {us * 1e3:8.2f} us")
 
-shares()
+if "--no-shares" not in sys.argv:
+    shares()
