@@ -19,12 +19,16 @@ constexpr int SPB = 16, SPH = 8;
 constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
-// LDS-tiled momentum block (dot points j x i at one level)
+// LDS-tiled momentum block (dot points j x i at one level).  32 x 8 (256 threads, 39 KB of
+// LDS: four blocks per CU): at C3 k_update 108 -> 97 us and the step 214 -> 200-203 us; on
+// the 96-point rows of the scaling runs' tiles no half-idle second block column, and 96 x 48
+// fits one round of blocks (step 88.6 -> 81.1 us); 64 x 8, 32 x 16 and 64 x 4 measured slower
+// (round 5, alternating on one box: profiles/r05/tile_ab_w32.log)
 #ifndef RCM_MBI
 #define RCM_MBI 8
 #endif
 #ifndef RCM_MBJ
-#define RCM_MBJ 64
+#define RCM_MBJ 32
 #endif
 constexpr int MBJ = RCM_MBJ, MBI = RCM_MBI, MBT = MBJ * MBI;
 // LDS-tiled scalar (t, qv, qc) block (cross points j x i at one level)
@@ -32,7 +36,7 @@ constexpr int MBJ = RCM_MBJ, MBI = RCM_MBI, MBT = MBJ * MBI;
 #define RCM_SBI 8
 #endif
 #ifndef RCM_SBJ
-#define RCM_SBJ 64
+#define RCM_SBJ 32
 #endif
 constexpr int SBJ = RCM_SBJ, SBI = RCM_SBI, SBT = SBJ * SBI;
 // k_update runs a momentum block or a scalars block in every workgroup of one launch, so the

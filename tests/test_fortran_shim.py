@@ -318,6 +318,11 @@ def test_fortran_host_hydrostatic(c1_data):
     _gets(s, rc, STATE_FIELDS)
     s.add(RUNTIME).add(KTIMES, 1).add(DESTROY)
     py, fo = s.run_python(), s.run_fortran()
+    # the runtime paths are each process's own (a Python host that imported torch binds torch's
+    # libamdhip64 / librccl, the Fortran host /opt/rocm's): the same report, not the same text
+    for r in (py[-2], fo[-2]):
+        assert r.startswith("hip=") and "; rccl=" in r, r
+    py[-2] = fo[-2] = None
     assert_same(py, fo)
     assert py[0][0] != 0 and "diagnostics" in py[0][1]
     assert py[1][0] == 7                         # 3 tend + bdyval, then rcmdyn_step(4)
