@@ -496,8 +496,8 @@ struct rcmdyn_engine {
       if (cfg.isladvec == 1) t.slqx[n] = dalloc(t, P3);
       if (cfg.idiffu == 3) t.d6qx[n] = dalloc(t, P * (kz + 1));
     }
-    if (hc.nsp) t.depx = talloc<int>(t, (size_t)hc.nsp * kz);
-    t.depplane = talloc<int>(t, 2 * kz);
+    if (hc.nsp) t.depx = talloc<unsigned>(t, (size_t)hc.nsp * kz * negfix_rowwords(g));
+    t.depplane = talloc<unsigned>(t, 2 * (size_t)kz * negfix_rowwords(g));
     if (cfg.idynamic != 2) {
       t.negcnt = talloc<int>(t, 1);
       t.neglist = talloc<uint32_t>(t, 2 * P3);     // every (point, level, qv|qc) at most once
@@ -528,7 +528,7 @@ struct rcmdyn_engine {
     }
     // column blocks of k_columns (one noise partial each)
     // k_columns blocks: 64 columns x one row, over the tile and its ghost ring
-    t.ncolx = (g.jdx2() - g.jdx1() + 64) / 64;
+    t.ncolx = (g.jdx2() - g.jdx1() + COLW) / COLW;
     t.nred = t.ncolx * (g.idx2() - g.idx1() + 1);
     if (overlap()) setup_overlap(t);
     t.red_off = red_total;
@@ -1595,9 +1595,9 @@ struct rcmdyn_engine {
     if (t.rja > t.rjb || t.ria > t.rib) return;
     const long box = (long)(g.jdx2() - g.jdx1() + 1) * (g.idx2() - g.idx1() + 1);
     const long rin = (long)(t.rjb - t.rja + 1) * (t.rib - t.ria + 1);
-    t.rnxb = (t.rjb - t.rja + 64) / 64;
+    t.rnxb = (t.rjb - t.rja + COLW) / COLW;
     t.nint = t.rnxb * (t.rib - t.ria + 1);
-    t.nring = (int)((box - rin + 63) / 64);
+    t.nring = (int)((box - rin + COLW - 1) / COLW);
     t.nred = t.nint + t.nring;
     auto inner = [&](int J0, int I0, int bj, int bi) {
       return J0 - 2 >= t.rja && J0 + bj + 1 <= t.rjb && I0 - 2 >= t.ria && I0 + bi + 1 <= t.rib;
@@ -1632,7 +1632,7 @@ struct rcmdyn_engine {
   }
 
   // dynamic LDS of the two-phase column kernels: 4 x kz x 64 doubles
-  size_t col_lds() const { return sizeof(double) * 4 * 64 * (size_t)cfg.kz; }
+  size_t col_lds() const { return sizeof(double) * 4 * COLW * (size_t)cfg.kz; }
 
   // all buffers of one tile for its current parity (see Fields)
   Fields fields(Tile& t) {
@@ -1821,10 +1821,11 @@ struct rcmdyn_engine {
         // else of the step; k_nh_tend_c read atm1 for the water load before)
         KLAUNCH(k_qx_fix, grid3(g.jdx2() - g.jdx1() + 1, g.idx2() - g.idx1() + 1, kz), BLK, 0, stream, g, dc,
                 qx_args(t));      // the column box, as the hydrostatic launch: its jci x ici fix
-        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(64), 0, stream, g, dc, qx_args(t));
+        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
+                qx_args(t));
       }
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
-      KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(64), 0, stream, g, dc, f);
+      KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc, f);
       // tend's time filters (tfuse = 0) with part A of the first acoustic sub-step (sound, :163-718)
       KLAUNCH(k_nh_tfilter_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc, f);
     });
@@ -2007,12 +2008,12 @@ struct rcmdyn_engine {
       if (ring) {
         const int W = g.jdx2() - g.jdx1() + 1, H = g.idx2() - g.idx1() + 1;
         const long nkeep = qfuse() ? (long)(4 * W + 4 * std::max(H - 4, 0)) * kz : 0;
-        nsp = (int)((g.nj * (long)g.ni + 511) / 512 + (nkeep + 511) / 512);
+        nsp = (int)((g.nj * (long)g.ni + COLT - 1) / COLT + (nkeep + COLT - 1) / COLT);
       }
       if (hc.nsp)
-        KLAUNCH(k_columns<true>, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
+        KLAUNCH(k_columns<true>, dim3(ncol + nsp), dim3(COLT), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
       else
-        KLAUNCH(k_columns<false>, dim3(ncol + nsp), dim3(512), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
+        KLAUNCH(k_columns<false>, dim3(ncol + nsp), dim3(COLT), col_lds(), stream, g, dc, ds, fields(t, part), t.ncolx, ncol);
     };
     if (overlap()) {
       // the whole exchange on the second stream; meanwhile part 1 of k_columns and, in a whole
@@ -2115,7 +2116,8 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         KLAUNCH(k_qx_fix, grid3(g.jdx2() - g.jdx1() + 1, g.idx2() - g.idx1() + 1, kz), BLK, 0, stream, g, dc,
                 qx_args(t));
-        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(64), 0, stream, g, dc, qx_args(t));
+        KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
+                qx_args(t));
       });
     }
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
@@ -2132,11 +2134,12 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
       const QFix q = qfix(t);
-      const int nxp = (g.jdx2() - g.jde1 + 64) / 64, nproj = nxp * (g.idx2() - g.ide1 + 1);
+      const int nxp = (g.jdx2() - g.jde1 + SPC) / SPC, nproj = nxp * (g.idx2() - g.ide1 + 1);
       // extra blocks: qfuse the parallel fix of the listed negatives (grid-stride), else the
       // serial sweeps of the planes k_qfilter flagged
-      const int nextra = qfuse() ? NEGFIX_BLOCKS : 2 * kz;
-      KLAUNCH(k_split_project, dim3(nproj + nextra), dim3(512), col_lds(), stream, g, dc, t.a1u[c], t.a1v[c],
+      const int nextra = qfuse() ? NEGFIX_BLOCKS * 512 / (SPC * SPG) : 2 * kz;   // 32 768 threads
+      KLAUNCH(k_split_project, dim3(nproj + nextra), dim3(SPC * SPG), sizeof(double) * 4 * SPC * (size_t)kz, stream, g,
+              dc, t.a1u[c], t.a1v[c],
                          t.a2u[c], t.a2v[c], t.a1t[c], t.a2t[c], t.psa_[c], t.psb_[c], t.msfd, t.mapf, t.dstor,
                          t.hstor, t.deld, t.delh, t.psdota, nxp, nproj, q, t.gw, wide ? t.wdeld : nullptr,
                          t.wdelh, t.wpsdota, t.wpsa, t.a2u[o], t.a2v[o]);
@@ -2194,25 +2197,32 @@ struct rcmdyn_engine {
       const int adv = (int)(q + 1 == tiles.size());
       // qfuse: trailing z slices run the serial sweeps of the flagged moisture planes
       const QFix qf = qfix(t);
-      const int nser = qfuse() ? (int)((2 * kz + gr.x * gr.y - 1) / (gr.x * gr.y)) : 0;
+      // (nqx = 5: in a launch of their own after the corrections, k_negfix_serial, whose block per
+      // plane can run the dense wavefront; the patchy hydrometeor fields come with patchy qc)
+      const bool own = hc.nsp > 0;
+      const int nser = qfuse() && !own ? (int)((2 * kz + gr.x * gr.y - 1) / (gr.x * gr.y)) : 0;
       gr.z += nser;
+      const size_t slds = nser ? sizeof(double) * negfix_lds(g) : 0;     // the sweeps' LDS
       if (bdy) {
         // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
         // levels, 4 per block
         const unsigned per = 4 * gr.x * gr.y;
         gr.z += (6 * bdy_chunks(g) * kz + per - 1) / per;
         const BdyArgs ba = bdy_args(t, 1);
-#define RCM_SCB(NS_) KLAUNCH(k_split_correct_bdy<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, \
+#define RCM_SCB(NS_) KLAUNCH(k_split_correct_bdy<NS_>, gr, BLK, slds, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd, \
                              ds, adv, red, red_total, ba, qf, nser)
         switch (ns) { case 1: RCM_SCB(1); break; case 2: RCM_SCB(2); break; case 3: RCM_SCB(3); break; default: RCM_SCB(4); }
 #undef RCM_SCB
       } else {
-#define RCM_SC(NS_) KLAUNCH(k_split_correct<NS_>, gr, BLK, 0, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd,   \
+#define RCM_SC(NS_) KLAUNCH(k_split_correct<NS_>, gr, BLK, slds, stream, g, dc, t.ddsum, t.dhsum, t.psdota, t.msfd,   \
                             t.psa_[c], t.psb_[c], t.a1t[c], t.a2t[c], t.a1u[c], t.a1v[c], t.a2u[c], t.a2v[c], ds, adv, \
                             red, red_total, dflags, qf, nser)
         switch (ns) { case 1: RCM_SC(1); break; case 2: RCM_SC(2); break; case 3: RCM_SC(3); break; default: RCM_SC(4); }
 #undef RCM_SC
       }
+      if (qfuse() && own)
+        KLAUNCH(k_negfix_serial, dim3(2 * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
+                qf);
     }
   }
   // not with a communicator: a rank-local call (a get) between tend and bdyval would then issue

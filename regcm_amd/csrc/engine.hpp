@@ -76,6 +76,18 @@ struct Geom {
     return j >= 3 && j <= gjx - 2 && i >= 3 && i <= giy - 2;
   }
 };
+// the negative-moisture fix's row bitmap: words per (species, level) plane; the LDS (doubles) of
+// its serial part (qxcommon.hpp): the row sweep's two interior rows and 13 per lane, or the
+// wavefront's 4-slot ring per row; the wavefront's block: a thread per interior row
+__host__ __device__ __forceinline__ int negfix_rowwords(const Geom& g) { return (g.ici2 - g.ici1 + 1 + 31) / 32; }
+__host__ __device__ __forceinline__ int negfix_lds(const Geom& g) {
+  const int a = 2 * (g.jci2 - g.jci1 + 1) + 64 * 13, b = 4 * (g.ici2 - g.ici1 + 1);
+  return a > b ? a : b;
+}
+__host__ __device__ __forceinline__ int negfix_threads(const Geom& g) {
+  const int r = (g.ici2 - g.ici1 + 1 + 63) / 64 * 64;
+  return r < 64 ? 64 : (r > 512 ? 512 : r);
+}
 // columns between j1 and the frame's 128-B line boundary at or below it (ALIGN_J, devcommon.hpp)
 __host__ __device__ __forceinline__ int jalign(const Geom& g, int j1) { return (j1 - g.j0) & 15; }
 
@@ -168,8 +180,8 @@ struct Tile {
   // tendency starts (isladvec = 1) and idiffu = 3 column terms
   double *a1qx[NQXH][2] = {}, *a2qx[NQXH][2] = {};
   double *cqx[NQXH] = {}, *fqx[NQXH] = {}, *slqx[NQXH] = {}, *d6qx[NQXH] = {};
-  int* depx = nullptr;
-  int *depplane;                   // per (n,k) plane flag: a serially dependent negative point
+  unsigned* depx = nullptr;          // nqx = 5: the species planes' row bitmaps (as depplane)
+  unsigned *depplane;              // per (n,k) plane: bitmap of the rows with a serially dependent negative point
   int* negcnt = nullptr;           // hydrostatic qfuse: the negative forecasts k_scalars listed
   uint32_t* neglist = nullptr;
   double *deld, *delh, *ddsum, *dhsum, *uu, *vv;

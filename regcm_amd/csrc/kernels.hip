@@ -119,14 +119,14 @@ __device__ __forceinline__ void keep_point(const Geom& g, const Fields& f, int j
 __device__ __forceinline__ bool column_of(const Geom& g, const Part& p, int bb, int tx, int nxb, int& j, int& i) {
   const int J1 = g.jdx1(), J2 = g.jdx2(), I1 = g.idx1(), I2 = g.idx2();
   if (p.part == 1) {
-    j = p.ja + (bb % p.nxb) * 64 + tx;
+    j = p.ja + (bb % p.nxb) * COLW + tx;
     i = p.ia + bb / p.nxb;
     return j <= p.jb;
   }
   if (p.part == 2) {
     const int W = J2 - J1 + 1, wl = p.ja - J1, wm = wl + (J2 - p.jb);
     const int nb = (p.ia - I1) * W, nm = (p.ib - p.ia + 1) * wm, nt = (I2 - p.ib) * W;
-    int q = bb * 64 + tx;
+    int q = bb * COLW + tx;
     j = J1; i = I1;
     if (q < nb) { i = I1 + q / W; j = J1 + q % W; return true; }
     q -= nb;
@@ -140,7 +140,7 @@ __device__ __forceinline__ bool column_of(const Geom& g, const Part& p, int bb, 
     if (q < nt) { i = p.ib + 1 + q / W; j = J1 + q % W; return true; }
     return false;
   }
-  j = J1 + (bb % nxb) * 64 + tx;
+  j = J1 + (bb % nxb) * COLW + tx;
   i = I1 + bb / nxb;
   return j <= J2;
 }
@@ -157,13 +157,13 @@ __device__ __forceinline__ bool part_skip(const Part& p, int j1, int j2, int i1,
 // QX: nqx = 5, tvfac with the total water load (an instance of its own, so the nqx = 2 kernel
 // keeps its code)
 template <bool QX>
-__global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
+__global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* __restrict__ c, StepState* s, Fields f,
                                                  int nxb, int ncol) {
-  extern __shared__ double lds[];                        // 4 x kz x 64
+  extern __shared__ double lds[];                        // 4 x kz x COLW
   PT_DECL
   const uint32_t P8 = g.P8, L8 = g.L8;
   const int bb = blockIdx.x;
-  const int nsp = (g.nj * g.ni + 511) / 512;
+  const int nsp = (g.nj * g.ni + COLT - 1) / COLT;
   if (bb >= ncol + nsp) {
     // qfuse: the copies of keep_point on the two outer rows and columns of the column box (every
     // point that has one), one (point, level) per thread; in blocks of their own so that the 2
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
     const int J1 = g.jdx1(), J2 = g.jdx2(), I1 = g.idx1(), I2 = g.idx2();
     const int W = J2 - J1 + 1, H = I2 - I1 + 1;
     const int nb = 4 * W + 4 * (H > 4 ? H - 4 : 0);
-    const int q = (bb - ncol - nsp) * 512 + (int)threadIdx.x;
+    const int q = (bb - ncol - nsp) * COLT + (int)threadIdx.x;
     const int k = q / nb + 1, p = q % nb;
     if (k > c->kz) return;
     int jj, ii;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   if (bb >= ncol) {
     // surface pressures (and with qfuse the copy of p*) on the frame points outside the column
     // box, all ghost points
-    const int q = (bb - ncol) * 512 + (int)threadIdx.x;
+    const int q = (bb - ncol) * COLT + (int)threadIdx.x;
     const int jj = g.j0 + q % g.nj, ii = g.i0 + q / g.nj;
     if (ii < g.i0 + g.ni && !(in(jj, g.jdx1(), g.jdx2()) && in(ii, g.idx1(), g.idx2()))) {
       surface_pressures_at(g, f, jj, ii);
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   }
   // k_scalars appends after this (part 2 follows part 1 and the k_scalars blocks of part 1)
   if (f.qfuse && bb == 0 && threadIdx.x == 0 && f.pt.part != 2) *f.negcnt = 0;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;     // column, level group (0..7)
+  const int tx = (int)threadIdx.x % COLW, ty = (int)threadIdx.x / COLW;     // column, level group (0..7)
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
   // columns compute exactly what their owners do (qdot, phi, pten and the new p* there replace
@@ -213,9 +213,9 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   const bool ci = ce && g.gci(j, i);
   const int kz = c->kz;
   double* sMD = lds;                                      // mass divergence, [k-1][tx]
-  double* sTD = lds + kz * 64;                            // td
-  double* sTV = lds + 2 * kz * 64;                        // tvfac
-  double* sLG = lds + 3 * kz * 64;                        // log ratio of the layer below level k
+  double* sTD = lds + kz * COLW;                            // td
+  double* sTV = lds + 2 * kz * COLW;                        // tvfac
+  double* sLG = lds + 3 * kz * COLW;                        // log ratio of the layer below level k
   const uint32_t o2 = valid ? g.o2(j, i) : 0u;
   const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
   if (valid && ty == 7) surface_pressures_at(g, f, j, i);
@@ -247,14 +247,14 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
       if (k > kz) break;
       const double a = u11[n] * m11 + u10[n] * m10 - u01[n] * m01 - u00[n] * m00;
       const double bq = v11[n] * m11 + v01[n] * m01 - v10[n] * m10 - v00[n] * m00;
-      sMD[(k - 1) * 64 + tx] = (a + bq) * dummy;
+      sMD[(k - 1) * COLW + tx] = (a + bq) * dummy;
       const double qv = dmax(qq[n] * rp, MINQQ);
       const double qc = dmax(cc[n] * rp, d_zero);
       double tdk = tt[n] * (d_one + ep1 * qv);
       // ipgf = 1: minus the reference-atmosphere temperature (ttld, :1893-1964)
       if (c->ipgf == 1) tdk = tdk - psk * T00PG * rcm_powpos((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
-      sTD[(k - 1) * 64 + tx] = tdk;
-      sTV[(k - 1) * 64 + tx] = d_one / (d_one + qc / (d_one + qv));
+      sTD[(k - 1) * COLW + tx] = tdk;
+      sTV[(k - 1) * COLW + tx] = d_one / (d_one + qc / (d_one + qv));
       }
     }
     if (QX) {
@@ -266,14 +266,14 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
         const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
         double qcd = d_zero + dmax(LD(f.a1qc, o3) * rp, d_zero);
         for (int q = 0; q < NQXH; q++) qcd = qcd + dmax(LD(f.qxa1[q], o3) * rp, d_zero);
-        sTV[(k - 1) * 64 + tx] = d_one / (d_one + qcd / (d_one + qv));
+        sTV[(k - 1) * COLW + tx] = d_one / (d_one + qcd / (d_one + qv));
       }
     }
     PT_MARK();
     // the hypsometric log ratios in a loop of their own (no loads in flight there: the log's
     // polynomial constants stay in registers without spilling)
     for (int k = ty + 1; k <= kz; k += 8)
-      sLG[(k - 1) * 64 + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
+      sLG[(k - 1) * COLW + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
                                         : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
     PT_MARK();
   }
@@ -286,12 +286,12 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
     if (!ce) {
       for (int k = 1; k <= kz + 1; k++) ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, d_zero);
     } else {
-      for (int k = 1; k <= kz; k++) pt = pt - sMD[(k - 1) * 64 + tx] * c->dsigma[k];
+      for (int k = 1; k <= kz; k++) pt = pt - sMD[(k - 1) * COLW + tx] * c->dsigma[k];
       ST(f.pten, o2, pt);
       double q = d_zero;
       ST(f.qdot, o2, d_zero);
       for (int k = 2; k <= kz; k++) {
-        q = q - (pt + sMD[(k - 2) * 64 + tx]) * c->dsigma[k - 1] * rp;
+        q = q - (pt + sMD[(k - 2) * COLW + tx]) * c->dsigma[k - 1] * rp;
         ST(f.qdot, o2 + (uint32_t)(k - 1) * L8, q);
       }
       ST(f.qdot, o2 + (uint32_t)kz * L8, d_zero);
@@ -333,20 +333,22 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
       }
     }
   }
-  if (ce && ty == 1) {
+  // the geopotential column on another wavefront than the pten/qdot scan (COLW = 32: level
+  // groups 2k and 2k+1 share wavefront k)
+  if (ce && ty == (COLW == 32 ? 2 : 1)) {
     // geopotential column, bottom-up
     const double ps = LD(f.psa, o2);
-    double tdk1 = sTD[(kz - 1) * 64 + tx];
-    const double tv = tdk1 * rp * sTV[(kz - 1) * 64 + tx];
+    double tdk1 = sTD[(kz - 1) * COLW + tx];
+    const double tv = tdk1 * rp * sTV[(kz - 1) * COLW + tx];
     double top = LD(f.ht, o2);
     if (c->ipgf == 1) top = top + rgas * T00PG / c->pgfaa1 * rcm_powpos((ps + ptop) / P00PG, c->pgfaa1);  // :2045
-    double ph = top - rgas * tv * sLG[(kz - 1) * 64 + tx];
+    double ph = top - rgas * tv * sLG[(kz - 1) * COLW + tx];
     ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
     for (int lev = kz - 1; lev >= 1; lev--) {
-      const double tdl = sTD[(lev - 1) * 64 + tx];
+      const double tdl = sTD[(lev - 1) * COLW + tx];
       const double tvavg = ((tdl * c->dsigma[lev] + tdk1 * c->dsigma[lev + 1]) /
-                            (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * sTV[(lev - 1) * 64 + tx];
-      ph = ph - rgas * tvavg * sLG[(lev - 1) * 64 + tx];
+                            (ps * (c->dsigma[lev] + c->dsigma[lev + 1]))) * sTV[(lev - 1) * COLW + tx];
+      ph = ph - rgas * tvavg * sLG[(lev - 1) * COLW + tx];
       ST(f.phi, o2 + (uint32_t)(lev - 1) * L8, ph);
       tdk1 = tdl;
     }
@@ -357,12 +359,12 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   // 1) reduces to wavefront 0's halving tree from w = 32 (adding the +0.0 terms of the other
   // wavefronts changes no bit): a shuffle reduction in registers, and no LDS for it (3 blocks
   // per CU fit the column LDS, so one round of blocks covers C3)
-  if (ty == 0) {
+  if (threadIdx.x < 64) {         // wavefront 0 (COLW = 32: level groups 0 and 1, the latter's terms +0.0)
     for (int w = 32; w > 0; w >>= 1) {
       na = na + __shfl_down(na, w);
       nb = nb + __shfl_down(nb, w);
     }
-    if (tx == 0) {
+    if (threadIdx.x == 0) {
       const int slot = f.red_off + (f.pt.part == 2 ? f.pt.rbase : 0) + bb;
       f.red[2 * slot] = na;
       f.red[2 * slot + 1] = nb;
@@ -370,9 +372,9 @@ __global__ __launch_bounds__(512, COL_LB) void k_columns(Geom g, const Consts* _
   }
   PT_PRINT(1);
 }
-template __global__ __launch_bounds__(512, COL_LB) void k_columns<false>(Geom, const Consts* __restrict__, StepState*,
+template __global__ __launch_bounds__(COLT, COL_LB) void k_columns<false>(Geom, const Consts* __restrict__, StepState*,
                                                                         Fields, int, int);
-template __global__ __launch_bounds__(512, COL_LB) void k_columns<true>(Geom, const Consts* __restrict__, StepState*,
+template __global__ __launch_bounds__(COLT, COL_LB) void k_columns<true>(Geom, const Consts* __restrict__, StepState*,
                                                                        Fields, int, int);
 
 // ---------------------------------------------------------------------------------------
@@ -1351,7 +1353,7 @@ __global__ __launch_bounds__(256, QF_LB) void k_qfilter(Geom g, const Consts* __
         bool done = true;
         if (v < d_zero) {
           if (negfix_dependent(g, sv, j, i, k)) {
-            atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+            negfix_mark(g, f.depplane, n * c->kz + (k - 1), i);
             done = false;                       // fixed and filtered by the serial sweep
           } else {
             v = negfix_sum(g, sv, fx, j, i, k, false);
@@ -1369,38 +1371,58 @@ __global__ __launch_bounds__(256, QF_LB) void k_qfilter(Geom g, const Consts* __
 }
 
 // serial sweep of one flagged (n,k) plane by one wavefront (see K6)
-__device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFix q, int plane_id) {
-  if (!q.depplane[plane_id]) return;
+__device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFix q, int plane_id, double* lds) {
   const int kz = c->kz;
   const int n = plane_id / kz, k = plane_id % kz + 1;
-  const double* sv = n ? q.cqc : q.cqv;
-  double* fx = n ? q.fqc : q.fqv;
-  const int lane = threadIdx.x;
-  for (int i = g.ici1; i <= g.ici2; i++) {
-    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
-      const int j = j0 + lane;
-      const bool flagged = (j <= g.jci2) && F3(sv, j, i, k) < d_zero && negfix_dependent(g, sv, j, i, k);
-      unsigned long long mask = __ballot(flagged);
-      if (lane == 0) {
-        while (mask) {
-          const int bidx = __ffsll((long long)mask) - 1;
-          mask &= mask - 1;
-          const int jj = j0 + bidx;
-          const double v = negfix_sum(g, sv, fx, jj, i, k, true);
-          F3(fx, jj, i, k) = v;
-          double n1, n2;
-          // the RA-filtered p* of the step (Main/mod_tendency.F90:420), formed again from psc and
-          // the step's p* (with qfuse k_split_correct corrects psa/psb beside this sweep)
-          const double pc = F2(q.psc, jj, i), po = F2(q.opsa, jj, i);
-          raw_filter(c, n, v, F3(n ? q.o1qc : q.o1qv, jj, i, k), F3(n ? q.o2qc : q.o2qv, jj, i, k), pc,
-                     po + c->gnu1 * (pc + F2(q.opsb, jj, i) - d_two * po), n1, n2);
-          F3(n ? q.n1qc : q.n1qv, jj, i, k) = n1;
-          F3(n ? q.n2qc : q.n2qv, jj, i, k) = n2;
-        }
-      }
-    }
+  const double* o1 = n ? q.o1qc : q.o1qv;
+  const double* o2 = n ? q.o2qc : q.o2qv;
+  double* n1p = n ? q.n1qc : q.n1qv;
+  double* n2p = n ? q.n2qc : q.n2qv;
+  negfix_sweep(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane_id, k, lds, [=](int jj, int i, double v) {
+    // the RA-filtered p* of the step (Main/mod_tendency.F90:420), formed again from psc and the
+    // step's p* (with qfuse k_split_correct corrects psa/psb beside this sweep)
+    double n1, n2;
+    const double pc = F2(q.psc, jj, i), po = F2(q.opsa, jj, i);
+    raw_filter(c, n, v, F3(o1, jj, i, k), F3(o2, jj, i, k), pc, po + c->gnu1 * (pc + F2(q.opsb, jj, i) - d_two * po),
+               n1, n2);
+    F3(n1p, jj, i, k) = n1;
+    F3(n2p, jj, i, k) = n2;
+  });
+}
+
+// qfuse with nqx = 5: the qv / qc planes' serial fix in a launch of its own after the split
+// corrections, a block per plane (negfix_resolve: the dense wavefront or the row sweep); the
+// filter of a fixed point from its atm1, atm2 and the step's p* (x = o1, o2, psc, opsa, opsb)
+struct QvRaw {
+  static constexpr int NI = 5;
+  Geom g;
+  const Consts* c;
+  const double *o1, *o2, *psc, *opsa, *opsb;
+  double *n1p, *n2p;
+  int n, k;
+  __device__ void load(int j, int i, double* x) const {
+    x[0] = F3(o1, j, i, k); x[1] = F3(o2, j, i, k);
+    x[2] = F2(psc, j, i); x[3] = F2(opsa, j, i); x[4] = F2(opsb, j, i);
   }
-  if (lane == 0) q.depplane[plane_id] = 0;
+  __device__ void apply(int j, int i, double v, const double* x) const {
+    double n1, n2;
+    const double pc = x[2], po = x[3];
+    raw_filter(c, n, v, x[0], x[1], pc, po + c->gnu1 * (pc + x[4] - d_two * po), n1, n2);
+    F3(n1p, j, i, k) = n1;
+    F3(n2p, j, i, k) = n2;
+  }
+};
+__global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q) {
+  extern __shared__ double lds[];
+  const int plane = (int)blockIdx.x, kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  const QvRaw acc{g, c, n ? q.o1qc : q.o1qv, n ? q.o2qc : q.o2qv, q.psc, q.opsa, q.opsb,
+                  n ? q.n1qc : q.n1qv, n ? q.n2qc : q.n2qv, n, k};
+  negfix_resolve(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane, k, lds, negfix_lds(g), acc,
+                 [=](int jj, int i, double v) {
+                   double x[5];
+                   acc.load(jj, i, x);
+                   acc.apply(jj, i, v, x);
+                 });
 }
 
 // qfuse: k_qfilter's fix of the negative forecasts k_scalars listed, one entry per thread
@@ -1418,7 +1440,7 @@ __device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int
     const int i = g.i0 + (int)(r / g.pitch), j = g.j0 + (int)(r % g.pitch);
     const double* sv = n ? q.cqc : q.cqv;
     if (negfix_dependent(g, sv, j, i, k)) {
-      atomicOr(&q.depplane[n * c->kz + (k - 1)], 1);
+      negfix_mark(g, q.depplane, n * c->kz + (k - 1), i);
       continue;
     }
     double* fx = n ? q.fqc : q.fqv;
@@ -1444,33 +1466,34 @@ __device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int
 #ifndef SP_LB
 #define SP_LB 5
 #endif
-__global__ __launch_bounds__(512, SP_LB) void k_split_project(
+__global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
     const double* __restrict__ a2t, const double* __restrict__ psa, const double* __restrict__ psb,
     const double* __restrict__ msfd, const double* __restrict__ mapf, double* dstor, double* hstor, double* deld,
     double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw, double* wdeld, double* wdelh,
     double* wpsdota, double* wpsa, const double* __restrict__ o2u, const double* __restrict__ o2v) {
-  extern __shared__ double lds[];                        // 4 x kz x 64
+  extern __shared__ double lds[];                        // 4 x kz x SPC
   const int b = blockIdx.x;
   if (b >= nproj) {
-    if (qf.negcnt) negfix_list(g, c, qf, (b - nproj) * 512 + (int)threadIdx.x, ((int)gridDim.x - nproj) * 512);
-    else if (threadIdx.x < 64) negfix_serial_plane(g, c, qf, b - nproj);
+    if (qf.negcnt) negfix_list(g, c, qf, (b - nproj) * (int)blockDim.x + (int)threadIdx.x, ((int)gridDim.x - nproj) * (int)blockDim.x);
+    else if (threadIdx.x < 64)
+      negfix_serial_plane(g, c, qf, b - nproj, negfix_lds(g) <= 4 * c->kz * SPC ? lds : nullptr);
     return;
   }
   PT_DECL
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tx = (int)threadIdx.x % SPC, ty = (int)threadIdx.x / SPC;
   // owned dot points, plus psdota on the right/top ghost ring (the split corrections of the
   // ghost-ring u, v read it there)
-  const int j = g.jde1 + (b % nxp) * 64 + tx, i = g.ide1 + b / nxp;
+  const int j = g.jde1 + (b % nxp) * SPC + tx, i = g.ide1 + b / nxp;
   const bool valid = j <= g.jde2 && i <= g.ide2;
   const bool vpd = j <= g.jdx2() && i <= g.idx2();
   const bool ce = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const int kz = c->kz;
   double* sD1 = lds;
-  double* sD2 = lds + kz * 64;
-  double* sT1 = lds + 2 * kz * 64;
-  double* sT2 = lds + 3 * kz * 64;
+  double* sD2 = lds + kz * SPC;
+  double* sT1 = lds + 2 * kz * SPC;
+  double* sT2 = lds + 3 * kz * SPC;
   if (ty == 0) {
     double v;
     if (valid) {
@@ -1491,16 +1514,16 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
     const double* U01 = old_at(j, i + 1) ? o2u : a2u; const double* V01 = old_at(j, i + 1) ? o2v : a2v;
     const double* U11 = old_at(j + 1, i + 1) ? o2u : a2u; const double* V11 = old_at(j + 1, i + 1) ? o2v : a2v;
     const double* U10 = old_at(j + 1, i) ? o2u : a2u; const double* V10 = old_at(j + 1, i) ? o2v : a2v;
-    for (int k = ty + 1; k <= kz; k += 8) {
+    for (int k = ty + 1; k <= kz; k += SPG) {
 #define DIV(U, V, U01, U11, U10, V01, V11, V10)                                                            \
   (-(F3(U01, j, i + 1, k) * m01) + (F3(U11, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) +                \
    (F3(U10, j + 1, i, k) * m10) + (F3(V01, j, i + 1, k) * m01) + (F3(V11, j + 1, i + 1, k) * m11) -            \
    (F3(V, j, i, k) * m00) - (F3(V10, j + 1, i, k) * m10))
-      sD1[(k - 1) * 64 + tx] = DIV(a1u, a1v, a1u, a1u, a1u, a1v, a1v, a1v);
-      sD2[(k - 1) * 64 + tx] = DIV(a2u, a2v, U01, U11, U10, V01, V11, V10);
+      sD1[(k - 1) * SPC + tx] = DIV(a1u, a1v, a1u, a1u, a1u, a1v, a1v, a1v);
+      sD2[(k - 1) * SPC + tx] = DIV(a2u, a2v, U01, U11, U10, V01, V11, V10);
 #undef DIV
-      sT1[(k - 1) * 64 + tx] = F3(a1t, j, i, k);
-      sT2[(k - 1) * 64 + tx] = F3(a2t, j, i, k);
+      sT1[(k - 1) * SPC + tx] = F3(a1t, j, i, k);
+      sT2[(k - 1) * SPC + tx] = F3(a2t, j, i, k);
     }
   }
   __syncthreads();
@@ -1516,7 +1539,7 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
     wpsa[qw] = F2(psa, j, i);
     wpsdota[qw] = F2(psdota, j, i);
   }
-  for (int w = ty; w < 2 * ns; w += 8) {
+  for (int w = ty; w < 2 * ns; w += SPG) {
     const int l = w % ns + 1;
     if (w < ns) {
       const double ds = dstor[(long)(l - 1) * g.plane + q];
@@ -1525,8 +1548,8 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
         const double mf = F2(mapf, j, i);
         for (int k = 1; k <= kz; k++) {
           const double zr = c->zmatxr[l - 1][k - 1];
-          d3 = d3 + zr * rdx2 * mf * sD1[(k - 1) * 64 + tx];
-          d2 = d2 + zr * rdx2 * mf * sD2[(k - 1) * 64 + tx];
+          d3 = d3 + zr * rdx2 * mf * sD1[(k - 1) * SPC + tx];
+          d2 = d2 + zr * rdx2 * mf * sD2[(k - 1) * SPC + tx];
         }
       }
       SLOT(deld, l, 1)[q] = ds - d2;
@@ -1543,8 +1566,8 @@ __global__ __launch_bounds__(512, SP_LB) void k_split_project(
         h2 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pbv - c->pd);
         for (int k = 1; k <= kz; k++) {
           const double ta = c->tau[l - 1][k - 1], pdk = c->pdlog[l - 1][k], ek = c->eps1[l - 1][k];
-          h3 = h3 + pdk + ta * sT1[(k - 1) * 64 + tx] / pa + ek * (pa - c->pd);
-          h2 = h2 + pdk + ta * sT2[(k - 1) * 64 + tx] / pbv + ek * (pbv - c->pd);
+          h3 = h3 + pdk + ta * sT1[(k - 1) * SPC + tx] / pa + ek * (pa - c->pd);
+          h2 = h2 + pdk + ta * sT2[(k - 1) * SPC + tx] / pbv + ek * (pbv - c->pd);
         }
       }
       SLOT(delh, l, 1)[q] = hs - h2;
@@ -1658,7 +1681,11 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
   const int jr0 = J1 - SPH, ir0 = I1 - SPH;          // region origin (global)
   const int tx = threadIdx.x, ty = threadIdx.y;        // R x R, one region point each
   const double aam = c->aam[l - 1], dtau = c->dtau[l - 1], hbar = c->hbar[l - 1];
+#ifdef RCM_SP_TIMING_M2      // timing-only builds (wrong results): the sub-step count capped
+  const int m2 = min((int)aam * 2, RCM_SP_TIMING_M2);
+#else
   const int m2 = (int)aam * 2;
+#endif
   const double dtau2 = dtau * d_two, rdx2 = d_one / c->dx2;
 #define WSLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * w.plane)
   const double* D1 = WSLOT(deld, l, 1); const double* D2 = WSLOT(deld, l, 2); const double* D3 = WSLOT(deld, l, 3);
@@ -1704,10 +1731,15 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
   int n0 = 0, n1 = 1;                                   // slot indices (reference slots 1, 2)
   for (int n = 1; n <= m2; n++) {
     const int src = (n == 1) ? n0 : n1;
+    // sub-step n must leave deld/delh valid within rho = m2 - n points of the owned block (the
+    // owned points after the last): its update runs on that band only and its gradient on the
+    // dot points the band reads; the rows outside are whole wavefronts (two region rows each)
+    // that skip the sub-step's work
+    const int rho = m2 - n, lo = SPH - rho, hi = SPH + SPB - 1 + rho;
     // gradient of delh(src) at dot points -> (uu, vv)
     for (int r = 0; r < NR; r++) {
       const int lj = tx, li = ty + SPR * r;
-      if (di[r] && lj >= 1 && li >= 1) {
+      if (di[r] && lj >= 1 && li >= 1 && in(li, lo, hi + 1) && in(lj, lo, hi + 1)) {
         const double a = Hs[src][li][lj], b = Hs[src][li - 1][lj], cc = Hs[src][li][lj - 1], dd = Hs[src][li - 1][lj - 1];
         double w1 = (a + b - cc - dd) / ufac[r];
         double w2 = (a + cc - b - dd) / ufac[r];
@@ -1721,6 +1753,7 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
     const int nn = (n == 1) ? n1 : n0;                  // forward writes n1; leapfrog n2 = n0
     for (int r = 0; r < NR; r++) {
       const int lj = tx, li = ty + SPR * r;
+      if (!(in(li, lo, hi) && in(lj, lo, hi))) continue;
       if (ci[r] && lj + 1 < SPR && li + 1 < SPR) {
         const double w3 = rdx2 * mf[r] *
             (-U[li + 1][lj] + U[li + 1][lj + 1] - U[li][lj] + U[li][lj + 1] +
@@ -1740,7 +1773,7 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
         if (n == 1) Hs[nn][li][lj] = Hs[n0][li][lj] * ((aam - d_one) / aam);
         else Hs[nn][li][lj] = d_two * Hs[n1][li][lj] - Hs[n0][li][lj];
       }
-      if (ce[r]) {
+      if (ce[r] && own[r]) {          // only the owned points' sums are stored
         sd[r] = sd[r] + Ds[nn][li][lj];
         sh[r] = sh[r] + Hs[nn][li][lj];
       }
@@ -1784,7 +1817,8 @@ __device__ __forceinline__ void split_correct_body(
   if (nser && (int)blockIdx.z >= (int)gridDim.z - nser) {
     const int plane = (((int)blockIdx.z - ((int)gridDim.z - nser)) * (int)gridDim.y + (int)blockIdx.y) *
                           (int)gridDim.x + (int)blockIdx.x;
-    if (threadIdx.y == 0 && plane < 2 * c->kz) negfix_serial_plane(g, c, qf, plane);
+    extern __shared__ double nlds[];            // negfix_lds(g) doubles when nser > 0 (the launch)
+    if (threadIdx.y == 0 && plane < 2 * c->kz) negfix_serial_plane(g, c, qf, plane, nlds);
     return;
   }
   // bdyval blocks first: the leading z slices (blockIdx.z < zbdy) are dispatched before any

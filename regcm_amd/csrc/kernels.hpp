@@ -17,6 +17,21 @@ constexpr int NEGFIX_BLOCKS = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
 constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
+// k_columns: COLW columns x 8 level groups per block (COLT threads, 4 x kz x COLW doubles of LDS;
+// 32 measured 1-2 us slower at C3 than 64, profiles/r05/tile_ab_colw.log)
+#ifndef RCM_COLW
+#define RCM_COLW 64
+#endif
+constexpr int COLW = RCM_COLW, COLT = COLW * 8;
+// k_split_project: SPC dot columns x SPG level groups per block (256 threads, 4 x kz x SPC
+// doubles of LDS).  At C3 one row of 64 columns x 8 groups (512 threads) gave 576 blocks, a
+// round and an eighth on 256 CUs at two blocks each; 32 x 8 gives 1 152 blocks of 23 KB, five
+// per CU, one round (the kernel's time did not change: its block life, not the tail, sets it;
+// profiles/r05/tile_ab_colw.log)
+#ifndef RCM_SPC
+#define RCM_SPC 32
+#endif
+constexpr int SPC = RCM_SPC, SPG = 8;
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level).  32 x 8 (256 threads, 39 KB of
@@ -48,7 +63,10 @@ static_assert(MBT == SBT, "k_update launches momentum and scalars blocks with on
 #ifndef RCM_QBI
 #define RCM_QBI 8
 #endif
-constexpr int QBJ = 64, QBI = RCM_QBI, QBT = QBJ * QBI;
+#ifndef RCM_QBJ
+#define RCM_QBJ 64
+#endif
+constexpr int QBJ = RCM_QBJ, QBI = RCM_QBI, QBT = QBJ * QBI;
 struct SegList {
   Seg s[MAXSEG];
   int n;
@@ -86,7 +104,7 @@ struct Fields {
   double *qdot, *phi, *cqv, *cqc, *fqv, *fqc;
   double *slqv, *slqc;         // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv)
   double *d6u, *d6v, *d6t, *d6qv, *d6qc;   // idiffu = 3 column terms (k_diffu6)
-  int* depplane;
+  unsigned* depplane;
   double *tten, *uten, *vten, *qvten, *qcten, *omega, *xkcs;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy;
@@ -112,7 +130,7 @@ struct QxArgs {
   double *cq[NQXH], *fq[NQXH];
   double *sl[NQXH], *d6[NQXH];
   const double* phy[NQXH];
-  int* dep;                    // per (species, level) plane: a serially dependent negative point
+  unsigned* dep;               // per (species, level) plane: row bitmap of the serially dependent negative points
   int nsp;                     // hydrometeors beyond qc (0 for nqx = 2)
 };
 
@@ -127,7 +145,7 @@ struct QFix {
   // the step's p* before its RA filter and psc: the serial sweep (in k_split_correct with
   // qfuse, beside the split corrections of psa/psb) forms the filtered p* from them
   const double *psc, *opsa, *opsb;
-  int* depplane;
+  unsigned* depplane;
   // qfuse: the negative forecasts k_scalars listed (k_split_project fixes the independent ones
   // in parallel; the serial sweeps of the flagged planes run in k_split_correct)
   const int* negcnt;
@@ -144,6 +162,7 @@ __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState*
 __global__ void k_update(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields fm, Fields fs,
                          int mnx, int mny, int snx, int sny);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
+__global__ void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
                                 const double* __restrict__ a1v, const double* __restrict__ a2u,
                                 const double* __restrict__ a2v, const double* __restrict__ a1t,

@@ -18,6 +18,7 @@
 #include "kernels.hpp"
 #include "fastmath.hpp"
 #include "devcommon.hpp"
+#include "qxcommon.hpp"
 
 namespace rcm {
 
@@ -848,12 +849,6 @@ __device__ __forceinline__ double nh_negfix_sum(const Geom& g, const double* sv,
     }
   return 0.01 * sum / 9.0;
 }
-__device__ __forceinline__ bool nh_negfix_dependent(const Geom& g, const double* sv, int j, int i, int k) {
-#define NEG(J, I) (in(J, g.jci1, g.jci2) && in(I, g.ici1, g.ici2) && F3(sv, J, I, k) < d_zero)
-  return NEG(j - 1, i) || NEG(j - 1, i - 1) || NEG(j, i - 1) || NEG(j + 1, i - 1);
-#undef NEG
-}
-
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
@@ -861,8 +856,8 @@ __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
     const double* sv = n ? f.cqc : f.cqv;
     double* fx = n ? f.fqc : f.fqv;
     if (F3(sv, j, i, k) < d_zero) {
-      if (nh_negfix_dependent(g, sv, j, i, k)) {
-        atomicOr(&f.depplane[n * c->kz + (k - 1)], 1);
+      if (negfix_dependent(g, sv, j, i, k)) {
+        negfix_mark(g, f.depplane, n * c->kz + (k - 1), i);
       } else {
         const double v = nh_negfix_sum(g, sv, fx, j, i, k, false);
         F3(fx, j, i, k) = v;
@@ -872,30 +867,40 @@ __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
   }
 }
 
-// one 64-lane block per (n, k) plane; flagged planes swept in the reference order
-__global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f) {
+// one 64-lane block per (n, k) plane: the marked rows swept in the reference order
+// (negfix_sweep, qxcommon.hpp; dynamic LDS negfix_lds(g))
+// the filters of a fixed point (tfuse) from its atm1, atm2 (and p*a, p*b for qv) in x
+struct NhQRaw {
+  static constexpr int NI = 4;
+  Geom g;
+  const Consts* c;
+  const double *a1, *a2, *psa, *psb;
+  double *b1, *b2;
+  int n, k, tfuse;
+  __device__ void load(int j, int i, double* x) const {
+    if (!tfuse) { x[0] = x[1] = x[2] = x[3] = 0.0; return; }
+    x[0] = F3(a1, j, i, k); x[1] = F3(a2, j, i, k);
+    x[2] = n == 0 ? F2(psa, j, i) : 0.0; x[3] = n == 0 ? F2(psb, j, i) : 0.0;
+  }
+  __device__ void apply(int j, int i, double v, const double* x) const {
+    if (!tfuse) return;
+    double n1, n2;
+    if (n == 0) nh_raw_qv(c, x[0], x[1], v, x[2], x[3], n1, n2);
+    else nh_raw_qc(c, x[0], x[1], v, n1, n2);
+    F3(b1, j, i, k) = n1;
+    F3(b2, j, i, k) = n2;
+  }
+};
+__global__ __launch_bounds__(512) void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f) {
+  extern __shared__ double lds[];
   const int plane = blockIdx.x;
-  if (!f.depplane[plane]) return;
   const int kz = c->kz, n = plane / kz, k = plane % kz + 1;
-  const double* sv = n ? f.cqc : f.cqv;
-  double* fx = n ? f.fqc : f.fqv;
-  const int lane = threadIdx.x;
-  for (int i = g.ici1; i <= g.ici2; i++)
-    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
-      const int j = j0 + lane;
-      const bool flagged = (j <= g.jci2) && F3(sv, j, i, k) < d_zero && nh_negfix_dependent(g, sv, j, i, k);
-      unsigned long long mask = __ballot(flagged);
-      if (lane == 0) {
-        while (mask) {
-          const int b = __ffsll((long long)mask) - 1;
-          mask &= mask - 1;
-          const double v = nh_negfix_sum(g, sv, fx, j0 + b, i, k, true);
-          F3(fx, j0 + b, i, k) = v;
-          if (f.tfuse) nh_filter_q_to(g, c, f, n, j0 + b, i, k, v);
-        }
-      }
-    }
-  if (lane == 0) f.depplane[plane] = 0;
+  const NhQRaw acc{g, c, n ? f.a1qc : f.a1qv, n ? f.a2qc : f.a2qv, f.psa, f.psb, n ? f.b1qc : f.b1qv,
+                   n ? f.b2qc : f.b2qv, n, k, f.tfuse};
+  negfix_resolve(g, n ? f.cqc : f.cqv, n ? f.fqc : f.fqv, f.depplane, plane, k, lds, negfix_lds(g), acc,
+                 [&](int jj, int i, double v) {
+                   if (f.tfuse) nh_filter_q_to(g, c, f, n, jj, i, k, v);
+                 });
 }
 
 // tfuse = 0: the three time filters in place at one interior cross point and level

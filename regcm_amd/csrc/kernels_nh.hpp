@@ -40,7 +40,7 @@ struct NHFields {
   const double* kpbl;
   // forecasts (atmc) and fixed moisture
   double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
-  int* depplane;
+  unsigned* depplane;
   // sound work (Main/mod_sound.F90:40-60)
   double *wo, *se, *sf, *saa, *sb, *sc, *rhs, *sca, *sg1, *sg2, *ptend, *pxup, *pyvp, *tk;
   double *scc, *scdd, *scj, *spi, *estore, *astore, *tmask;

@@ -29,6 +29,222 @@ __device__ __forceinline__ bool negfix_dependent(const Geom& g, const double* sv
 #undef NEG
 }
 
+// ---- the serial part of the negative-moisture fix (Main/mod_tendency.F90:382-393)
+// The parallel passes (k_qfilter / k_split_project's list blocks, k_qx_fix, k_nh_negfix) fix
+// every negative point whose four sweep-predecessors are non-negative and mark, per (species,
+// level) plane, the rows that hold a dependent one (a bitmap of negfix_rowwords words per
+// plane).  negfix_sweep then resolves one plane in the reference's order with one wavefront:
+// only the marked rows are visited; per chunk of 64 points every lane stages its point's nine
+// neighbours (and the parallel pass's fixed values of its negative predecessors) in LDS in one
+// round of loads, and lane 0 walks the chunk's dependent points in order on LDS alone, taking a
+// dependent predecessor's value from the fixed values this sweep keeps for the current and
+// the previous row.  Each value is the reference's expression (0.01 * the nine |q| summed in
+// its order / 9), so the result is the sweep's, bit for bit.  The caller passes negfix_lds(g)
+// doubles of LDS (lds), or null: then lane 0 reads every operand from memory.
+__device__ __forceinline__ void negfix_mark(const Geom& g, unsigned* dep, int plane, int i) {
+  const int r = i - g.ici1;
+  atomicOr(&dep[plane * negfix_rowwords(g) + (r >> 5)], 1u << (r & 31));
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// one wavefront (lane = threadIdx.x & 63) resolves plane `plane` (level k of sv / fx); post(j,
+// i, v) writes what follows from a fixed value (the filters), on the lane of point (j, i)
+template <class Post>
+__device__ void negfix_sweep(const Geom& g, const double* sv, double* fx, unsigned* dep, int plane, int k,
+                             double* lds, Post post) {
+  const int lane = (int)threadIdx.x & 63;
+  const int nw = negfix_rowwords(g), W = g.jci2 - g.jci1 + 1;
+  unsigned* words = dep + plane * nw;
+  const bool inlds = lds != nullptr;
+  double(*pre)[13] = (double(*)[13])(lds + 2 * W);
+  int last = -2, cur = 0;
+  for (int w = 0; w < nw; w++) {
+    unsigned bits = words[w];
+    if (!bits) continue;
+    while (bits) {
+      const int r = __ffs((int)bits) - 1;
+      bits &= bits - 1;
+      const int i = g.ici1 + 32 * w + r;
+      const bool pv = last == i - 1;
+      cur ^= 1;
+      // this sweep's fixed values of the current and the previous row (two LDS rows, alternating)
+      double* rowc = lds + (cur ? W : 0);
+      const double* rowp = lds + (cur ? 0 : W);
+      if (inlds)
+        for (int x = lane; x < W; x += 64) rowc[x] = -1.0;
+      wave_lds_sync();
+      for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
+        const int j = j0 + lane;
+        const bool fl = j <= g.jci2 && F3(sv, j, i, k) < d_zero && negfix_dependent(g, sv, j, i, k);
+        const unsigned long long mask = __ballot(fl);
+        if (!mask) continue;
+        if (!inlds) {
+          if (lane == 0) {
+            unsigned long long m = mask;
+            while (m) {
+              const int b = __ffsll((long long)m) - 1;
+              m &= m - 1;
+              const double v = negfix_sum(g, sv, fx, j0 + b, i, k, true);
+              F3(fx, j0 + b, i, k) = v;
+              post(j0 + b, i, v);
+            }
+          }
+          continue;
+        }
+        if (fl) {
+          int s = 0;
+          for (int ii = i - 1; ii <= i + 1; ii++)
+            for (int jj = j - 1; jj <= j + 1; jj++, s++) {
+              const double v = F3(sv, jj, ii, k);
+              pre[lane][s] = v;
+              if (s < 4)
+                pre[lane][9 + s] =
+                    (in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) ? F3(fx, jj, ii, k) : d_zero;
+            }
+        }
+        wave_lds_sync();
+        if (lane == 0) {
+          unsigned long long m = mask;
+          while (m) {
+            const int b = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int jb = j0 + b;
+            double sum = 0.0;
+            int s = 0;
+            for (int ii = i - 1; ii <= i + 1; ii++)
+              for (int jj = jb - 1; jj <= jb + 1; jj++, s++) {
+                double v = pre[b][s];
+                if (s < 4 && in(jj, g.jci1, g.jci2) && in(ii, g.ici1, g.ici2) && v < d_zero) {
+                  // a negative sweep-predecessor: this sweep's fixed value, or the parallel pass's
+                  const double rv = s == 3 ? rowc[jj - g.jci1] : (pv ? rowp[jj - g.jci1] : -1.0);
+                  v = rv >= d_zero ? rv : pre[b][9 + s];
+                }
+                sum = sum + fabs(v);
+              }
+            rowc[jb - g.jci1] = 0.01 * sum / 9.0;
+          }
+        }
+        wave_lds_sync();
+        if (fl) {
+          const double v = rowc[j - g.jci1];
+          F3(fx, j, i, k) = v;
+          post(j, i, v);
+        }
+      }
+      last = i;
+    }
+    if (lane == 0) words[w] = 0;
+  }
+}
+
+// LDS-only block barrier: waits for this wave's LDS operations, not for its global loads in flight
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Dense planes (many marked rows): the sweep as a skewed wavefront.  Point (j, i) depends only
+// on its sweep-predecessors (j-1, i) and (j-1..j+1, i-1), so with one thread per row and row i
+// two steps behind row i-1 (step t = j - jci1 + 2 (i - ici1)) every dependency was resolved one
+// or more steps earlier: W + 2 (R - 1) steps, one LDS barrier each, for the whole plane.  Each
+// thread keeps the fixed value of its own previous point in a register and publishes its
+// fixed values in a 4-slot LDS ring per row (ring: 4 R doubles) for the row below; it streams
+// its 3 x 3 window of the original forecasts and the post inputs A::load of its row through a
+// register queue loaded P steps ahead, so no step waits on memory.  Every negative point of
+// the plane is evaluated (an independent one gives the parallel pass's value again); only the
+// dependent ones are stored and post-processed (A::apply).  Needs R <= the block's threads.
+template <class A>
+__device__ void negfix_dense(const Geom& g, const double* sv, double* fx, int k, double* ring, const A& acc) {
+  constexpr int P = 4, NQ = 3 + A::NI;
+  const int r = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  const int R = g.ici2 - g.ici1 + 1, W = g.jci2 - g.jci1 + 1, S = W + 2 * (R - 1);
+  const bool act = r < R;
+  const int i = g.ici1 + r;
+  auto qload = [&](int jc, double* q) {
+    const bool ok = act && jc >= g.jci1 - 1 && jc <= g.jci2 + 1;
+#pragma unroll
+    for (int d = 0; d < 3; d++) q[d] = ok ? F3(sv, jc, i - 1 + d, k) : 0.0;
+    if (act && in(jc, g.jci1, g.jci2)) acc.load(jc, i, q + 3);
+    else
+#pragma unroll
+      for (int d = 3; d < NQ; d++) q[d] = 0.0;
+  };
+  int j = g.jci1 - 2 * r;                    // this row's column at step 0
+  double w0[NQ], w1[NQ], w2[NQ], qa[P][NQ], qb[P][NQ];
+  qload(j - 1, w0);
+  qload(j, w1);
+  qload(j + 1, w2);
+#pragma unroll
+  for (int u = 0; u < P; u++) qload(j + 2 + u, qa[u]);
+  double prev = 0.0;                         // the fixed value of (j - 1, i)
+  const bool up = r >= 1;                    // row i - 1 is interior
+  for (int t0 = 0; t0 < S; t0 += P) {
+#pragma unroll
+    for (int u = 0; u < P; u++) qload(j + 2 + P + u, qb[u]);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int jj = j + u;
+      if (act && t0 + u < S && in(jj, g.jci1, g.jci2) && w1[1] < d_zero) {
+        const bool p0 = up && jj - 1 >= g.jci1 && w0[0] < d_zero, p1 = up && w1[0] < d_zero;
+        const bool p2 = up && jj + 1 <= g.jci2 && w2[0] < d_zero, p3 = jj - 1 >= g.jci1 && w0[1] < d_zero;
+        const double* rp = ring + 4 * (r - 1);
+        double sum = 0.0;
+        sum = sum + fabs(p0 ? rp[(jj - 1) & 3] : w0[0]);
+        sum = sum + fabs(p1 ? rp[jj & 3] : w1[0]);
+        sum = sum + fabs(p2 ? rp[(jj + 1) & 3] : w2[0]);
+        sum = sum + fabs(p3 ? prev : w0[1]);
+        sum = sum + fabs(w1[1]);
+        sum = sum + fabs(w2[1]);
+        sum = sum + fabs(w0[2]);
+        sum = sum + fabs(w1[2]);
+        sum = sum + fabs(w2[2]);
+        const double v = 0.01 * sum / 9.0;
+        ring[4 * r + (jj & 3)] = v;
+        prev = v;
+        if (p0 || p1 || p2 || p3) {
+          F3(fx, jj, i, k) = v;
+          acc.apply(jj, i, v, w1 + 3);
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int d = 0; d < NQ; d++) { w0[d] = w1[d]; w1[d] = w2[d]; w2[d] = qa[u][d]; }
+    }
+#pragma unroll
+    for (int u = 0; u < P; u++)
+#pragma unroll
+      for (int d = 0; d < NQ; d++) qa[u][d] = qb[u][d];
+    j += P;
+  }
+}
+
+// One (species, level) plane's serial fix by a whole block: nothing when no row is marked, the
+// wavefront when more than NEGFIX_SPARSE rows are and the block has a thread per row (and lds
+// holds the ring), else the row sweep by wavefront 0.  lds: ldsn doubles (see negfix_lds).
+constexpr int NEGFIX_SPARSE = 16;
+template <class A, class Post>
+__device__ void negfix_resolve(const Geom& g, const double* sv, double* fx, unsigned* dep, int plane, int k,
+                               double* lds, int ldsn, const A& acc, Post post) {
+  const int nw = negfix_rowwords(g), R = g.ici2 - g.ici1 + 1;
+  unsigned* words = dep + plane * nw;
+  int nm = 0;
+  for (int w = 0; w < nw; w++) nm += __popc(words[w]);
+  if (nm == 0) return;
+  const int T = (int)(blockDim.x * blockDim.y * blockDim.z);
+  const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  if (nm > NEGFIX_SPARSE && R <= T && 4 * R <= ldsn) {
+    negfix_dense(g, sv, fx, k, lds, acc);
+    __syncthreads();                           // every wave read the bitmap before it is cleared
+    for (int w = tid; w < nw; w += T) words[w] = 0;
+    return;
+  }
+  if (tid < 64) negfix_sweep(g, sv, fx, dep, plane, k, negfix_lds(g) <= ldsn ? lds : nullptr, post);
+}
+
 // RAW filters of one point (filter_raw_qv / filter_raw_4d) with the filtered p*
 __device__ __forceinline__ void raw_filter(const Consts* c, int n, double fq, double o1, double o2v, double pa,
                                            double pb, double& n1, double& n2) {

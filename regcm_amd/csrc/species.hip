@@ -268,7 +268,7 @@ __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q) {
     double v = LD(q.cq[n], o3);
     if (v < d_zero) {
       if (negfix_dependent(g, q.cq[n], j, i, k)) {
-        atomicOr(&q.dep[n * c->kz + (k - 1)], 1);
+        negfix_mark(g, q.dep, n * c->kz + (k - 1), i);
         continue;
       }
       v = negfix_sum(g, q.cq[n], q.fq[n], j, i, k, false);
@@ -283,40 +283,39 @@ __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q) {
   }
 }
 
-// K_QX3.  The serial sweep of one flagged (species, level) plane by one wavefront (see K6 of
-// kernels.hip): flagged points in i-major, j-minor order reading already-fixed predecessors.
-__global__ void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q) {
-  const int plane = (int)blockIdx.x, kz = c->kz;
-  if (plane >= q.nsp * kz || !q.dep[plane]) return;
-  const int n = plane / kz, k = plane % kz + 1;
-  const double* sv = q.cq[n];
-  double* fx = q.fq[n];
-  const int lane = threadIdx.x;
-  const double beta = 0.53;
-  for (int i = g.ici1; i <= g.ici2; i++) {
-    for (int j0 = g.jci1; j0 <= g.jci2; j0 += 64) {
-      const int j = j0 + lane;
-      const bool flagged = (j <= g.jci2) && F3(sv, j, i, k) < d_zero && negfix_dependent(g, sv, j, i, k);
-      unsigned long long mask = __ballot(flagged);
-      if (lane == 0) {
-        while (mask) {
-          const int b = __ffsll((long long)mask) - 1;
-          mask &= mask - 1;
-          const int jj = j0 + b;
-          const double v = negfix_sum(g, sv, fx, jj, i, k, true);
-          F3(fx, jj, i, k) = v;
-          const double a1 = F3(q.a1[n], jj, i, k), a2 = F3(q.a2[n], jj, i, k);
-          const double d = c->gnu2 * (v + a2 - d_two * a1);
-          double m = a1 + beta * d, x = v + (beta - d_one) * d;
-          if (m < d_zero) m = d_zero;
-          if (x < d_zero) x = d_zero;
-          F3(q.b2[n], jj, i, k) = m;
-          F3(q.b1[n], jj, i, k) = x;
-        }
-      }
-    }
+// K_QX3.  The serial sweep of one (species, level) plane by one wavefront (negfix_sweep,
+// qxcommon.hpp): the marked rows' dependent negative points in i-major, j-minor order, each
+// fixed from its already-fixed predecessors, then RAW-filtered; dynamic LDS negfix_lds(g)
+// filter_raw_4d of a fixed point (gnu2, the zero floor) from its atm1, atm2 (x)
+struct QxRaw {
+  static constexpr int NI = 2;
+  Geom g;
+  const double *a1, *a2;
+  double *b1, *b2;
+  double gnu2;
+  int k;
+  __device__ void load(int j, int i, double* x) const { x[0] = F3(a1, j, i, k); x[1] = F3(a2, j, i, k); }
+  __device__ void apply(int j, int i, double v, const double* x) const {
+    const double beta = 0.53;
+    const double d = gnu2 * (v + x[1] - d_two * x[0]);
+    double m = x[0] + beta * d, y = v + (beta - d_one) * d;
+    if (m < d_zero) m = d_zero;
+    if (y < d_zero) y = d_zero;
+    F3(b2, j, i, k) = m;
+    F3(b1, j, i, k) = y;
   }
-  if (lane == 0) q.dep[plane] = 0;
+};
+__global__ __launch_bounds__(512) void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q) {
+  extern __shared__ double lds[];
+  const int plane = (int)blockIdx.x, kz = c->kz;
+  if (plane >= q.nsp * kz) return;
+  const int n = plane / kz, k = plane % kz + 1;
+  const QxRaw acc{g, q.a1[n], q.a2[n], q.b1[n], q.b2[n], c->gnu2, k};
+  negfix_resolve(g, q.cq[n], q.fq[n], q.dep, plane, k, lds, negfix_lds(g), acc, [&](int jj, int i, double v) {
+    double x[2];
+    acc.load(jj, i, x);
+    acc.apply(jj, i, v, x);
+  });
 }
 
 // K_QX4.  bdyval for the hydrometeors beyond qc, one block per (level, species): while

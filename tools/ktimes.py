@@ -4,6 +4,7 @@ steps) plus the graph-replayed ms/step: the quick loop for kernel work.
     python tools/ktimes.py [--config C3] [--steps 50] [--prof-steps 5]
 """
 import argparse
+import dataclasses
 import os
 import sys
 import time
@@ -21,12 +22,16 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--prof-steps", type=int, default=5)
     ap.add_argument("--nproc", default="1x1", help="local tiles jxi (all on this GPU)")
+    ap.add_argument("--ipptls", type=int, default=1, help="2: nqx = 5 (qi, qr, qs with icbc.hydrometeor_state)")
     args = ap.parse_args()
-    rc = CONFIGS[args.config]
+    rc = dataclasses.replace(CONFIGS[args.config], ipptls=args.ipptls)
     data = icbc.generate_nh(rc) if rc.idynamic == 2 else icbc.generate(rc)
+    st = dict(data["state"])
+    if args.ipptls == 2:
+        st.update(icbc.hydrometeor_state(rc, st, nqx=rc.nqx))
     pj, pi = (int(x) for x in args.nproc.split("x"))
     e = DynCore(rc, data["split"], nproc_j=pj, nproc_i=pi)
-    e.put_state(data["state"])
+    e.put_state(st)
     e.bdyval()
     e.step(5)
     e.synchronize()
@@ -40,7 +45,7 @@ def main():
         per = n / args.prof_steps * avg * 1e3
         tot += per
         print(f"{name:28s} launches/step {n / args.prof_steps:6.2f}  avg {avg * 1e3:9.2f} us  per step {per:9.2f} us")
-    print(f"{args.config} tiles {args.nproc}: graph-replayed {ms:.4f} ms/step; eager kernel sum {tot / 1e3:.4f} ms/step")
+    print(f"{args.config} ipptls={args.ipptls} tiles {args.nproc}: graph-replayed {ms:.4f} ms/step; eager kernel sum {tot / 1e3:.4f} ms/step")
 
 
 if __name__ == "__main__":
