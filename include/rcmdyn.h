@@ -133,11 +133,18 @@ typedef struct rcmdyn_config {
    * the NH water loading.  ipptls = 0 (no moisture scheme: the hydrometeor tendencies are never
    * summed, :331) and an nqx that does not match ipptls are refused. */
   int32_t ipptls, nqx;
-  /* Options of the reference that this engine does not compute; a non-zero value is refused
-   * at rcmdyn_create ('not supported'): i_band = 1 (tropical band, periodic in j) and
-   * i_crm = 1 (cloud-resolving, periodic in j and i), set_nproc's periodic decompositions
-   * (Main/mpplib/mod_mppparam.F90:1062-1063, 1131-1132, 1224-1257); ichem = 1 (chemical tracers
-   * advected, diffused and nudged by tend, Main/mod_tendency.F90:164, 198, 275, 548, 873). */
+  /* i_band = 1 (dimparam, hydrostatic core): the tropical band, periodic in j
+   * (Main/mpplib/mod_mppparam.F90:1062, 1112-1114, 1131): no tile has a west or east boundary,
+   * the tiles of the first and last tile column are neighbours (one tile in j is its own west
+   * and east neighbour: its periodic exchange is a copy inside the tile), the cross grid takes
+   * every j (:1351-1354: cross fields are defined on j = 1..jx), and only the south and north
+   * rows relax to the boundary data (Main/mod_atm_interface.F90:435-457).  A put fills a band
+   * tile's frame columns past either end of the period from the wrapped columns.  Refused for
+   * idynamic = 2 and for values other than 0 and 1.
+   * Options of the reference that this engine does not compute; a non-zero value is refused
+   * at rcmdyn_create ('not supported'): i_crm = 1 (cloud-resolving, periodic in j and i,
+   * Main/mpplib/mod_mppparam.F90:1063, 1132, 1224-1257); ichem = 1 (chemical tracers advected,
+   * diffused and nudged by tend, Main/mod_tendency.F90:164, 198, 275, 548, 873). */
   int32_t i_band, i_crm, ichem;
 } rcmdyn_config;
 

@@ -173,9 +173,9 @@ class OracleParallel:
     the reference's MPI decomposition on host cores, bit-identical to one tile.  Same host
     API as OracleCore for put/get/bdyval/step/set_time/get_time."""
 
-    def __init__(self, rc, split, nthreads=1):
+    def __init__(self, rc, split, nthreads=1, dims=None):
         from regcm_amd.config import set_nproc
-        cj, ci = set_nproc(int(nthreads), rc.jx, rc.iy)
+        cj, ci = dims if dims is not None else set_nproc(int(nthreads), rc.jx, rc.iy)
         self.rc = rc
         self.nthreads = cj * ci
         self.cfg = build_config(rc, split, cj, ci, tile_first=0, tile_count=1)

@@ -28,7 +28,7 @@
 #define MAXT 256
 
 struct orc_par {
-  int ntiles, cj, ci, kz, jx, iy;
+  int ntiles, cj, ci, kz, jx, iy, band;
   double* glob[3];                   /* whole-domain gathers of the NH radiative condition */
   orc_t* t[MAXT];
   int info[MAXT][16];
@@ -48,9 +48,20 @@ static int recv_dir(int sides, int d) {
   return d == 1 || d == 3 || d == 7;                     /* exchange_rt: from R, T, TR */
 }
 
+/* a band (i_band = 1) is periodic in j (Main/mpplib/mod_mppparam.F90:1131 dim_period(1)) */
 static int peer_of(const orc_par_t* p, int tile, int d) {
   int lj = tile / p->ci + DJ[d], li = tile % p->ci + DI[d];
+  if (p->band) lj = (lj + p->cj) % p->cj;
   return (lj >= 0 && lj < p->cj && li >= 0 && li < p->ci) ? lj * p->ci + li : -1;
+}
+/* offset from a ghost column's j to the same column in the frame of the tile across the
+ * period (0 unless the message from direction d wraps around a band) */
+static int jwrap(const orc_par_t* p, int tile, int d) {
+  if (!p->band) return 0;
+  const int lj = tile / p->ci;
+  if (DJ[d] < 0 && lj == 0) return p->jx;
+  if (DJ[d] > 0 && lj == p->cj - 1) return -p->jx;
+  return 0;
 }
 
 static const int OPP[8] = {1, 0, 3, 2, 7, 6, 5, 4};
@@ -96,6 +107,7 @@ static void xfn(void* ctx, double* a, int nk, int nex, int sides) {
     const double* src = arrived(p, me, d, &q);
     const int* g = p->info[q];
     const size_t pq = (size_t)g[2] * g[3];
+    const int sj = jwrap(p, me, d);
     int j1 = f[4], j2 = f[5], i1 = f[6], i2 = f[7];      /* ghost box received from d */
     if (DJ[d] < 0) { j1 = f[4] - nex; j2 = f[4] - 1; }
     if (DJ[d] > 0) { j1 = f[5] + 1; j2 = f[5] + nex; }
@@ -105,7 +117,7 @@ static void xfn(void* ctx, double* a, int nk, int nex, int sides) {
       for (int i = i1; i <= i2; i++)
         for (int j = j1; j <= j2; j++)
           a[k * pl + (size_t)(i - f[1]) * f[2] + (j - f[0])] =
-              src[k * pq + (size_t)(i - g[1]) * g[2] + (j - g[0])];
+              src[k * pq + (size_t)(i - g[1]) * g[2] + (j + sj - g[0])];
     ack(p, me, q, d);
   }
   drain(p, me, out);
@@ -132,7 +144,8 @@ static void bfn(void* ctx, double* s, int nk, int along) {
     const int* g = p->info[q];
     const int nq = along == 0 ? g[2] : g[3], oq = along == 0 ? g[0] : g[1];
     const int x = side == 0 ? lo - 1 : hi + 1;         /* owned by the peer */
-    for (int k = 0; k < nk; k++) s[(size_t)k * n + (x - o0)] = src[(size_t)k * nq + (x - oq)];
+    const int sx = along == 0 ? jwrap(p, me, d) : 0;
+    for (int k = 0; k < nk; k++) s[(size_t)k * n + (x - o0)] = src[(size_t)k * nq + (x + sx - oq)];
     ack(p, me, q, d);
   }
   drain(p, me, out);
@@ -159,7 +172,7 @@ orc_par_t* orc_par_create(const rcmdyn_config* cfg) {
   if (nt < 1 || nt > MAXT || (cfg->idynamic != 1 && cfg->idynamic != 2)) return NULL;
   orc_par_t* p = (orc_par_t*)calloc(1, sizeof(orc_par_t));
   p->ntiles = nt; p->cj = cfg->nproc_j; p->ci = cfg->nproc_i; p->kz = cfg->kz;
-  p->jx = cfg->jx; p->iy = cfg->iy;
+  p->jx = cfg->jx; p->iy = cfg->iy; p->band = cfg->i_band == 1;
   if (cfg->idynamic == 2 && nt > 1)
     for (int q = 0; q < 3; q++) p->glob[q] = (double*)calloc((size_t)cfg->jx * cfg->iy, sizeof(double));
   for (int t = 0; t < nt; t++) {

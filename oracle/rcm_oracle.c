@@ -163,15 +163,39 @@ static double* alloc3(orc_t* o, int nk) {
 static double dmax(double a, double b) { return (a > b) ? a : (b > a ? b : a); }
 static double dmin(double a, double b) { return (a < b) ? a : (b < a ? b : a); }
 
+/* A band (i_band = 1) on one tile in j is its own west and east neighbour
+ * (Main/mpplib/mod_mppparam.F90:1112-1114: ma%left = ma%right = myid): the exchange's band
+ * branch (:6092-6140) copies the nex columns on each side around the period, rows ide1..ide2
+ * (the box every exchange here moves); exchange_lb fills the left ghost columns only, _rt the
+ * right ones. */
+static void band_self_xch(orc_t* o, double* a, int nk, int nex, int sides) {
+  const int jx = o->jx;
+  for (int k = 1; k <= nk; k++)
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int w = 1; w <= nex; w++) {
+        if (sides != 2) A3(a, o->jde1 - w, i, k) = A3(a, o->jde1 - w + jx, i, k);
+        if (sides != 1) A3(a, o->jde2 + w, i, k) = A3(a, o->jde2 + w - jx, i, k);
+      }
+}
 static void xch(orc_t* o, double* a, int nk, int nex, int sides) {
   if (o->xfn) o->xfn(o->xctx, a, nk, nex, sides);
+  else if (o->cfg.i_band && o->cfg.nproc_j == 1) band_self_xch(o, a, nk, nex, sides);
 }
+/* the boundary slices along j (south / north) exchange their entries one past the tile with
+ * the left / right tiles (exchange_bdy_lr, Main/mod_bdycod.F90:1063-1089): around the period
+ * on a band's single tile */
 static void xchb(orc_t* o, double* s, int along) {
   if (o->bfn) o->bfn(o->xctx, s, o->kz, along);
+  else if (o->cfg.i_band && o->cfg.nproc_j == 1 && along == 0)
+    for (int k = 0; k < o->kz; k++) {
+      double* r = s + (size_t)k * o->nj - o->j0;          /* r[j]: entry of column j */
+      r[o->jde1 - 1] = r[o->jde2];
+      r[o->jde2 + 1] = r[o->jde1];
+    }
 }
 
 /* ---- set_nproc tile extents, Main/mpplib/mod_mppparam.F90:1295-1360 ---- */
-static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4]) {
+static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band) {
   int lj = tile / ci, li = tile % ci;
   int jxp = jx / cj, iyp = iy / ci;
   int js = lj * jxp + 1, is = li * iyp + 1;
@@ -185,12 +209,14 @@ static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], in
   }
   int je = js + jxp - 1, ie = is + iyp - 1;
   ext[0] = js; ext[1] = je; ext[2] = is; ext[3] = ie;
-  ext[4] = js; ext[5] = (je == jx) ? je - 1 : je;
+  /* a band (i_band = 1) is periodic in j: no west/east boundary, and the cross grid takes every
+   * j (global_cross_jend = global_dot_jend, Main/mpplib/mod_mppparam.F90:1351-1354) */
+  ext[4] = js; ext[5] = (je == jx && !band) ? je - 1 : je;
   ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
-  bdy[0] = (lj == 0); bdy[1] = (lj == cj - 1); bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band; bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
 }
 
-/* ---- setup_boundaries, Main/mod_atm_interface.F90:383-542 (non-band, non-CRM) ---- */
+/* ---- setup_boundaries, Main/mod_atm_interface.F90:383-542 (non-CRM) ---- */
 static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
   int jx = o->jx, iy = o->iy;
   int icx = ldot ? 0 : 1, icy = ldot ? 0 : 1;
@@ -200,6 +226,16 @@ static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
   int jgbr1 = jx - icx - nsp + 2, jgbr2 = jx - icx - 1;
   for (int i = o->i0; i < o->i0 + o->ni; i++)
     for (int j = o->j0; j < o->j0 + o->nj; j++) { A2(rg, j, i) = 0; A2(ib, j, i) = -1; }
+  if (o->cfg.i_band) {
+    /* a band (:435-455): the south and north rows only, every j ("j < jgbl1 .and. j > jgbr2"
+     * skips none) */
+    for (int i = o->ide1; i <= o->ide2; i++)
+      for (int j = o->jde1; j <= o->jde2; j++) {
+        if (i >= igbb1 && i <= igbb2) { A2(ib, j, i) = i - igbb1 + 2; A2(rg, j, i) = 1; }
+        if (i >= igbt1 && i <= igbt2) { A2(ib, j, i) = igbt2 - i + 2; A2(rg, j, i) = 2; }
+      }
+    return;
+  }
   for (int i = o->ide1; i <= o->ide2; i++) {   /* South */
     if (i >= igbb1 && i <= igbb2)
       for (int j = o->jde1; j <= o->jde2; j++)
@@ -252,16 +288,17 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   /* a non-hydrostatic tile of a decomposition needs the whole-domain gather of sound's upper
    * radiative condition (Main/mod_sound.F90:496-497): orc_set_gather, before the first step */
   if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
-  /* nqx from ipptls >= 1 (Main/mod_params.F90:1358-1366); band, CRM, chemistry not restated */
-  if (cfg->ipptls < 1 || cfg->nqx != (cfg->ipptls > 1 ? 5 : 2) || cfg->i_band || cfg->i_crm || cfg->ichem)
-    return NULL;
+  /* nqx from ipptls >= 1 (Main/mod_params.F90:1358-1366); a band (i_band = 1) for the
+   * hydrostatic core; CRM and chemistry not restated */
+  if (cfg->ipptls < 1 || cfg->nqx != (cfg->ipptls > 1 ? 5 : 2) || cfg->i_crm || cfg->ichem) return NULL;
+  if (cfg->i_band && (cfg->i_band != 1 || cfg->idynamic != 1)) return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
   o->sound_probe = -1;
   o->cfg = *cfg;
   o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
   o->nsplit = cfg->nsplit; o->nqx = cfg->nqx;
   int ext[8], bdy[4];
-  tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy);
+  tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy, cfg->i_band);
   o->bl = bdy[0]; o->br = bdy[1]; o->bb = bdy[2]; o->bt = bdy[3];
   /* Main/mod_atm_interface.F90:231-302 */
   o->jde1 = o->jdi1 = o->jdii1 = ext[0]; o->jde2 = o->jdi2 = o->jdii2 = ext[1];
@@ -602,6 +639,14 @@ int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int 
         if (j < o->j0 || j >= o->j0 + o->nj) continue;
         A3(a, j, i, k) = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)];
       }
+      /* a band's frame columns past either end of the period take the wrapped column, as its
+       * periodic exchange would give them */
+      if (o->cfg.i_band)
+        for (int j = o->j0; j < o->j0 + o->nj; j++) {
+          const int jw = j < 1 ? j + o->jx : (j > o->jx ? j - o->jx : j);
+          if (jw == j || jw < j1 || jw > j2) continue;
+          A3(a, j, i, k) = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (jw - j1)];
+        }
     }
   }
   if (field == RCMDYN_MSFX || field == RCMDYN_MSFD || field == RCMDYN_HT) prepare_static(o);

@@ -192,7 +192,8 @@ class RunConfig:
     nuk: float = 5.0                 # uwparam, Main/mod_params.F90:480
     iuwvadv: int = 0                 # uwparam; 1 with ibltyp = 2: PBL-aware qc vertical flux (vadv4d ind = 3)
     ipptls: int = 1                  # physicsparam; > 1 (WSM5 / NT): nqx = 5, Main/mod_params.F90:1358-1366
-    i_band: int = 0                  # dimparam / physicsparam options the engine refuses
+    i_band: int = 0                  # 1: tropical band, periodic in j (hydrostatic core only)
+    # i_crm, ichem: physicsparam options the engine refuses
     i_crm: int = 0
     ichem: int = 0
     tkemin: float = 1.0e-3           # uwtkemin, Main/pbllib/mod_pbl_uwtcm.F90:86

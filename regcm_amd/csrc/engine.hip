@@ -54,7 +54,9 @@ struct HipError : std::runtime_error {
 constexpr double EGRAV = 9.80665, BOLTZK = 1.3806504e-23, NAVGDR = 6.02214129e23;
 constexpr double AMD = 28.96454, AMW = 18.01528, VONKAR = 0.4;
 
-void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4]) {
+// band (i_band = 1): periodic in j, so no tile has a west/east boundary and the cross grid
+// takes every j (global_cross_jend = global_dot_jend, Main/mpplib/mod_mppparam.F90:1351-1354)
+void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band = 0) {
   int lj = tile / ci, li = tile % ci;
   int jxp = jx / cj, iyp = iy / ci;
   int js = lj * jxp + 1, is = li * iyp + 1;
@@ -68,16 +70,17 @@ void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4
   }
   int je = js + jxp - 1, ie = is + iyp - 1;
   ext[0] = js; ext[1] = je; ext[2] = is; ext[3] = ie;
-  ext[4] = js; ext[5] = (je == jx) ? je - 1 : je;
+  ext[4] = js; ext[5] = (je == jx && !band) ? je - 1 : je;
   ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
-  bdy[0] = (lj == 0); bdy[1] = (lj == cj - 1); bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band; bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
 }
 
-Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G) {
+Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G, int band = 0) {
   int ext[8], bdy[4];
-  tile_extent(jx, iy, cj, ci, tile, ext, bdy);
+  tile_extent(jx, iy, cj, ci, tile, ext, bdy, band);
   Geom g{};
   g.bl = bdy[0]; g.br = bdy[1]; g.bb = bdy[2]; g.bt = bdy[3];
+  g.band = band;
   g.gjx = jx; g.giy = iy;
   g.jde1 = g.jdi1 = g.jdii1 = ext[0]; g.jde2 = g.jdi2 = g.jdii2 = ext[1];
   g.ide1 = g.idi1 = g.idii1 = ext[2]; g.ide2 = g.idi2 = g.idii2 = ext[3];
@@ -107,7 +110,8 @@ Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G) {
   return g;
 }
 
-// setup_boundaries, Main/mod_atm_interface.F90:383-542 (global indices, non-band)
+// setup_boundaries, Main/mod_atm_interface.F90:383-542 (global indices).  A band (i_band = 1,
+// :435-455) has the south and north bands only, over every j.
 void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::vector<int8_t>& rg,
                       std::vector<int16_t>& ib) {
   int icx = ldot ? 0 : 1, icy = ldot ? 0 : 1;
@@ -121,6 +125,15 @@ void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::ve
   // global index, so ghost points carry their owners' values
   const int fi1 = std::max(1, g.i0), fi2 = std::min(iy, g.i0 + g.ni - 1);
   const int fj1 = std::max(1, g.j0), fj2 = std::min(jx, g.j0 + g.nj - 1);
+  if (g.band) {
+    // periodic ghosts carry the band rows too
+    for (int i = fi1; i <= fi2; i++)
+      for (int j = g.j0; j < g.j0 + g.nj; j++) {
+        if (i >= igbb1 && i <= igbb2) set(j, i, 1, i - igbb1 + 2);
+        if (i >= igbt1 && i <= igbt2) set(j, i, 2, igbt2 - i + 2);
+      }
+    return;
+  }
   for (int i = fi1; i <= fi2; i++)
     if (i >= igbb1 && i <= igbb2)
       for (int j = fj1; j <= fj2; j++)
@@ -273,6 +286,7 @@ struct rcmdyn_engine {
   long staging_cap = 0;
   double* red = nullptr;     // noise-sum partials of every tile (k_columns)
   int red_total = 0;
+  bool halo = false;          // ghost rings come from exchanges: a decomposition, or a band (periodic in j)
   bool diag = false;         // write the per-tend diagnostic fields
   KernelProf* prof = nullptr;  // set while rcmdyn_kernel_times runs
   double last_ms = 0.0;
@@ -316,7 +330,7 @@ struct rcmdyn_engine {
     return v && *v && std::strcmp(v, "0") != 0;
   }();
   // (idiffu = 3: the column terms are formed after the whole exchange, so no overlap)
-  bool overlap() const { return ntiles > 1 && cfg.idynamic != 2 && cfg.idiffu != 3 && !no_overlap; }
+  bool overlap() const { return halo && cfg.idynamic != 2 && cfg.idiffu != 3 && !no_overlap; }
   bool post_inner = false;    // tend_pre ran part 1 of k_momentum / k_scalars
   std::string err;
   std::unique_ptr<Comm> comm;
@@ -458,6 +472,7 @@ struct rcmdyn_engine {
     const int dj[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, di[8] = {0, 0, -1, 1, -1, -1, 1, 1};
     for (int d = 0; d < 8; d++) {
       int lj = t.lj + dj[d], li = t.li + di[d];
+      if (cfg.i_band) lj = (lj + cfg.nproc_j) % cfg.nproc_j;      // periodic in j (a tile may be its own)
       t.nbr[d] = (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
     }
     for (int b = 0; b < 2; b++) {
@@ -507,8 +522,8 @@ struct rcmdyn_engine {
     t.uu = dalloc(t, P); t.vv = dalloc(t, P);
     t.tten = dalloc(t, P3); t.uten = dalloc(t, P3); t.vten = dalloc(t, P3);
     t.qvten = dalloc(t, P3); t.qcten = dalloc(t, P3); t.omega = dalloc(t, P3); t.xkcs = dalloc(t, P3);
-    if (ntiles > 1) {                       // wide frame of the fused split step
-      t.gw = make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, index, SPH + G);
+    if (halo) {                       // wide frame of the fused split step
+      t.gw = make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, index, SPH + G, cfg.i_band);
       const size_t PW = t.gw.plane;
       t.wdeld = dalloc(t, PW * 3 * ns); t.wdelh = dalloc(t, PW * 3 * ns);
       t.wpsa = dalloc(t, PW); t.wpsdota = dalloc(t, PW);
@@ -522,7 +537,7 @@ struct rcmdyn_engine {
     staging_cap = std::max<long>(staging_cap, 8L * (std::max(g.nj, g.ni) + 2 * G) * (32 + 16 * (hc.nsp > 0)) * (kz + 1));
     t.sbuf = dalloc(t, staging_cap);
     t.rbuf = dalloc(t, staging_cap);
-    if (cfg.nproc_j * cfg.nproc_i > 1) {
+    if (halo) {
       t.sbuf2 = dalloc(t, staging_cap);
       t.rbuf2 = dalloc(t, staging_cap);
     }
@@ -582,7 +597,7 @@ struct rcmdyn_engine {
       f.cfl = nhf[0].cfl;
       f.cfll = nhf[0].cfll;
     }
-    if (ntiles > 1) t.westore = dalloc(t, t.gw.plane);
+    if (halo) t.westore = dalloc(t, t.gw.plane);
     nhf.push_back(f);
   }
 
@@ -687,7 +702,9 @@ struct rcmdyn_engine {
     if (cfg.nqx != (cfg.ipptls > 1 ? 5 : 2))
       throw std::runtime_error("rcmdyn: nqx must be 2 for ipptls = 1 and 5 for ipptls = 2 (Main/mod_params.F90:1358-1366)");
     // periodic decompositions and chemical tracers are not built: refused, not ignored
-    if (cfg.i_band != 0) throw std::runtime_error("rcmdyn: i_band = 1 (periodic tropical band) is not supported");
+    if (cfg.i_band != 0 && cfg.i_band != 1) throw std::runtime_error("rcmdyn: i_band must be 0 or 1");
+    if (cfg.i_band != 0 && cfg.idynamic == 2)
+      throw std::runtime_error("rcmdyn: i_band = 1 (periodic tropical band) is built for the hydrostatic core only");
     if (cfg.i_crm != 0) throw std::runtime_error("rcmdyn: i_crm = 1 (periodic CRM domain) is not supported");
     if (cfg.ichem != 0) throw std::runtime_error("rcmdyn: ichem = 1 (chemical tracers) is not supported");
     if (const char* m = std::getenv("RCMDYN_RCCL_CHAN2"))   // the removed second-communicator modes
@@ -702,6 +719,7 @@ struct rcmdyn_engine {
     if (cfg.nsplit < 1 || cfg.nsplit > MAXSPLIT) throw std::runtime_error("rcmdyn: nsplit out of range");
     if (cfg.nspgx >= MAXNSP || cfg.nspgd != cfg.nspgx) throw std::runtime_error("rcmdyn: nspgx/nspgd unsupported");
     ntiles = cfg.nproc_j * cfg.nproc_i;
+    halo = ntiles > 1 || cfg.i_band != 0;
     if (ntiles < 1 || cfg.tile_first < 0 || cfg.tile_count < 1 || cfg.tile_first + cfg.tile_count > ntiles)
       throw std::runtime_error("rcmdyn: bad tile range");
     if (!dry) {
@@ -709,7 +727,7 @@ struct rcmdyn_engine {
       HIPCHK(hipGetDevice(&device));
     }
     for (int t = 0; t < ntiles; t++) {
-      all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t));
+      all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t, G, cfg.i_band));
       const Geom& g = all.back();
       if (g.jde2 - g.jde1 + 1 < 3 || g.ide2 - g.ide1 + 1 < 3)
         throw std::runtime_error("rcmdyn: Too much processors (tile < 3x3), mod_mppparam.F90:1365");
@@ -759,7 +777,7 @@ struct rcmdyn_engine {
         comm.reset(make_rccl_comm(cfg));
       }
     }
-    else if (force_rccl && ntiles > 1) comm.reset(make_rccl_self_comm());
+    else if (force_rccl && halo) comm.reset(make_rccl_self_comm());
     if (comm) {
       HIPCHK(hipMalloc(&derr, sizeof(int32_t)));
       HIPCHK(hipHostMalloc((void**)&hgerr, sizeof(int32_t) * NFLAGSLOT, hipHostMallocMapped | hipHostMallocCoherent));
@@ -767,7 +785,7 @@ struct rcmdyn_engine {
       HIPCHK(hipHostGetDevicePointer((void**)&dgerr, hgerr, 0));
       for (auto& e : gev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
-    if (ntiles > 1) {
+    if (halo) {
       HIPCHK(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIPCHK(hipEventCreateWithFlags(&evfork, hipEventDisableTiming));
       for (hipEvent_t& e : evjoin) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1078,8 +1096,12 @@ struct rcmdyn_engine {
       HIPCHK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
       for (int k = std::max(k1, 1); k <= std::min(k2, nk); k++)
         for (int i = std::max(i1, g.i0); i <= std::min(i2, g.i0 + g.ni - 1); i++)
-          for (int j = std::max(j1, g.j0); j <= std::min(j2, g.j0 + g.nj - 1); j++)
-            h[(size_t)(k - 1) * g.plane + g.ix(j, i)] = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (j - j1)];
+          for (int j = g.j0; j <= g.j0 + g.nj - 1; j++) {
+            // a band's frame columns past either end of the period take the wrapped column
+            const int jw = !cfg.i_band ? j : (j < 1 ? j + cfg.jx : (j > cfg.jx ? j - cfg.jx : j));
+            if (jw < j1 || jw > j2) continue;
+            h[(size_t)(k - 1) * g.plane + g.ix(j, i)] = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (jw - j1)];
+          }
       HIPCHK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
@@ -1247,7 +1269,9 @@ struct rcmdyn_engine {
     return d == 1 || d == 3 || d == 7;
   }
   int peer_of(const Tile& t, int d) const {
-    const int lj = t.lj + DJ[d], li = t.li + DI[d];
+    int lj = t.lj + DJ[d];
+    const int li = t.li + DI[d];
+    if (cfg.i_band) lj = (lj + cfg.nproc_j) % cfg.nproc_j;       // periodic in j (may be t itself)
     return (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
   }
   Tile* local_tile(int idx) {
@@ -1309,7 +1333,7 @@ struct rcmdyn_engine {
   }
   void exchange_generic(const SegFn& fn, const std::function<bool(int)>& send_on,
                         const std::function<bool(int)>& recv_on) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     // staging of the stream this exchange is issued on (the two streams' exchanges overlap)
     auto SB = [&](Tile& x) { return on2 ? x.sbuf2 : x.sbuf; };
     auto RB = [&](Tile& x) { return on2 ? x.rbuf2 : x.rbuf; };
@@ -1334,17 +1358,21 @@ struct rcmdyn_engine {
           recvs.push_back({comm->rank(), RB(*pt) + R[pq].start[OPP[d]], (size_t)S[q].count[d], R[pq].sig[OPP[d]]});
           continue;
         }
-        if (S[q].count[d]) {
-          if (pt) {
-            const size_t pq = pt - tiles.data();
-            if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
-            DHIPCHK(hipMemcpyAsync(RB(*pt) + R[pq].start[OPP[d]], SB(t) + S[q].start[d],
-                                   S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
-          } else {
-            sends.push_back({p, SB(t) + S[q].start[d], (size_t)S[q].count[d], S[q].sig[d]});
-          }
+        if (S[q].count[d] && pt) {
+          const size_t pq = pt - tiles.data();
+          if (R[pq].count[OPP[d]] != S[q].count[d]) throw std::runtime_error("rcmdyn: halo size mismatch");
+          DHIPCHK(hipMemcpyAsync(RB(*pt) + R[pq].start[OPP[d]], SB(t) + S[q].start[d],
+                                 S[q].count[d] * sizeof(double), hipMemcpyDeviceToDevice, stream));
         }
         if (R[q].count[d] && !pt) recvs.push_back({p, RB(t) + R[q].start[d], (size_t)R[q].count[d], R[q].sig[d]});
+      }
+      // remote sends in the order of the receiver's directions: the n-th message between two
+      // ranks matches the n-th receive, and in a band of two tiles in j one peer is both the
+      // left and the right neighbour
+      for (int e = 0; e < 8; e++) {
+        const int d = OPP[e], p = peer_of(t, d);
+        if (p < 0 || !S[q].count[d] || local_tile(p)) continue;
+        sends.push_back({p, SB(t) + S[q].start[d], (size_t)S[q].count[d], S[q].sig[d]});
       }
     }
     if (!sends.empty() || !recvs.empty()) {
@@ -1370,7 +1398,7 @@ struct rcmdyn_engine {
     xchv(std::vector<XField>(fields), width, sides);
   }
   void xchv(std::vector<XField> fs, int width = 1, int sides = 0) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     for (XField& x : fs) {
       if (x.width == 0) x.width = width;
       if (x.sides < 0) x.sides = sides;
@@ -1389,7 +1417,7 @@ struct rcmdyn_engine {
   // streams' RCCL calls go to one communicator in the same order on every rank; captured
   // into the step graph as a fork/join.
   void fork_point() {
-    if (ntiles == 1) return;
+    if (!halo) return;
     DHIPCHK(hipEventRecord(evfork, stream));
   }
   // one communicator for both streams (RCMDYN_RCCL_CHAN2=one): the second stream's exchange
@@ -1399,7 +1427,7 @@ struct rcmdyn_engine {
     if (comm && comm->shared_channels()) fork_point();
   }
   void xch_begin(std::vector<XField> fs, int slot = 0) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
     std::swap(stream, stream2);
     on2 = true;
@@ -1427,13 +1455,13 @@ struct rcmdyn_engine {
   // at this point and sends the following launches there, side_end records their completion
   // (slot) and sends launches back, side_join makes the engine's stream wait for them.
   void side_begin() {
-    if (ntiles == 1) return;
+    if (!halo) return;
     DHIPCHK(hipEventRecord(evfork, stream));
     DHIPCHK(hipStreamWaitEvent(stream2, evfork, 0));
     std::swap(stream, stream2);
   }
   void side_end(int slot) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     DHIPCHK(hipEventRecord(evjoin[slot], stream));
     std::swap(stream, stream2);
     join_pending[slot] = true;
@@ -1442,7 +1470,7 @@ struct rcmdyn_engine {
 
   // exchange_lb of xdelh = delh(:,:,l,src) (Main/mod_split.F90:498-499)
   void xch_delh_slot(int l, int src) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     const long off = ((long)(src - 1) * cfg.nsplit + (l - 1));
     auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
       v.push_back(field_seg(t, t.delh + off * t.g.plane, 1, d, 1, send));
@@ -1452,7 +1480,7 @@ struct rcmdyn_engine {
 
   // width-w exchange of 2-D planes held in the tiles' wide frames (fused split step)
   void xch_wide(std::initializer_list<std::pair<double* Tile::*, int>> fields, int w) {
-    if (ntiles == 1) return;
+    if (!halo) return;
     std::vector<std::pair<double* Tile::*, int>> fs(fields);
     auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
       int b[4];
@@ -1470,7 +1498,7 @@ struct rcmdyn_engine {
   // the fused split step is exact on a decomposition when every tile is at least SPX wide
   // (its depth-SPX halo then comes from the direct neighbours only)
   bool wide_ok() const {
-    if (ntiles == 1) return true;
+    if (!halo) return true;
     for (const Geom& g : all)
       if (g.jde2 - g.jde1 + 1 < SPX || g.ide2 - g.ide1 + 1 < SPX) return false;
     return true;
@@ -1492,7 +1520,7 @@ struct rcmdyn_engine {
   // south/north slices (by j) with the left/right tiles, west/east slices (by i) with the
   // bottom/top tiles; width 1, every level.
   void xch_slices() {
-    if (ntiles == 1) return;
+    if (!halo) return;
     const int kz = cfg.kz;
     auto fn = [&](Tile& t, int d, bool send, std::vector<Seg>& v) {
       const Geom& g = t.g;
@@ -1553,7 +1581,7 @@ struct rcmdyn_engine {
         KLAUNCH(k_prepare_static, grid3(t.g.nj, t.g.ni, 1), BLK, 0, stream, t.g, dc, cfg.diffu_hgtf,
                 t.msfx, t.msfd, t.ht, t.xmsf, t.dmsf, t.hgfact, t.mapf);
       });
-      if (ntiles > 1) {
+      if (halo) {
         each([&](Tile& t) {
           copy_wide(t, t.msfx, t.wmsfx, 1);
           copy_wide(t, t.msfd, t.wmsfd, 1);
@@ -1717,7 +1745,7 @@ struct rcmdyn_engine {
     // halo/compute overlap of a whole tend on a decomposed domain: the cr/qdot/xkcr exchange
     // on the second stream beside k_nh_tend_c (which reads them at its own point only), the
     // cqv/cqc exchange beside k_nh_tend_d (which does not read them)
-    const bool ovl = ntiles > 1 && !no_overlap && phase == TEND_ALL && !slice && cfg.isladvec != 1;
+    const bool ovl = halo && !no_overlap && phase == TEND_ALL && !slice && cfg.isladvec != 1;
     // ci1a: the interior cross columns from the 128-B line at or below jci1 (NH_ALIGN)
     struct Grids { dim3 fr, ce1, cek, ci1, cik, cik1, di1, dik, ci1a; };
     auto grids = [&](const Geom& g) {
@@ -1848,7 +1876,7 @@ struct rcmdyn_engine {
         KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1 + (NH_ALIGN ? jalign(g, g.jde1) : 0), g.ide2 - g.ide1 + 1, kz),
                 BLK, 0, stream, g, dc, ds, nhfields(t), istep, fin, first, part);
       };
-      if (ntiles > 1 && !no_overlap) {
+      if (halo && !no_overlap) {
         side_begin();
         each([&](Tile& t) { sound_uv(t, 1); });
         side_end(0);
@@ -1875,7 +1903,7 @@ struct rcmdyn_engine {
           KLAUNCH(k_nh_tmask, dim3(1), dim3(256), 0, stream, tiles[0].g, dc, nh_gbuf, nhf[0].tmask);
           nh_tmask_valid = true;
         }
-        if (ntiles > 1) {
+        if (halo) {
           each([&](Tile& t) { copy_wide(t, nhf[&t - tiles.data()].estore, t.westore, 1); });
           xch_wide({{&Tile::westore, 1}}, 6);
         }
@@ -1884,7 +1912,7 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
-        if (ntiles > 1)
+        if (halo)
           KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD ? q.ci1a : q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
                   (int)(it < istep));
         else
@@ -2051,7 +2079,7 @@ struct rcmdyn_engine {
       KLAUNCH(k_diffu6, dim3((g.ide2 - g.ide1 + 64) / 64, kz, 4 + hc.nsp), dim3(64), 0, stream, g, dc, fields(t),
               qx_args(t));
     });
-    if (ntiles > 1) {
+    if (halo) {
       std::vector<XField> d6{{FK::D6U, kz}, {FK::D6V, kz}, {FK::D6T, kz}, {FK::D6QV, kz}, {FK::D6QC, kz}};
       add_qx(d6, FK::D6QX0, kz, 0);
       xchv(d6);
@@ -2129,7 +2157,7 @@ struct rcmdyn_engine {
     });
     // splitf, Main/mod_split.F90:243-461
     if (!fused) xch({{FK::PSA, 1}, {FK::A1U, kz, 1, 2}, {FK::A1V, kz, 1, 2}, {FK::A2U, kz, 1, 2}, {FK::A2V, kz, 1, 2}});
-    const bool wide = fused && ntiles > 1;     // k_split_project also fills the wide frames
+    const bool wide = fused && halo;     // k_split_project also fills the wide frames
     each([&](Tile& t) {
       const Geom& g = t.g;
       const int c = t.cur, o = 1 - c;
@@ -2153,7 +2181,7 @@ struct rcmdyn_engine {
       each([&](Tile& t) {
         const Geom& g = t.g;
         dim3 gr((g.jcx2() - g.jcx1() + SPB) / SPB, (g.icx2() - g.icx1() + SPB) / SPB, ns);
-        if (ntiles > 1)
+        if (halo)
           KLAUNCH(k_spstep_fused, gr, dim3(SPR, SPR), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
                   t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
         else
@@ -2228,7 +2256,7 @@ struct rcmdyn_engine {
   // not with a communicator: a rank-local call (a get) between tend and bdyval would then issue
   // the step's flag reduction on one rank only
   bool can_defer() const {
-    return cfg.idynamic != 2 && !comm && !no_fuse_bdy && !no_defer_corr && (ntiles == 1 || split_fused());
+    return cfg.idynamic != 2 && !comm && !no_fuse_bdy && !no_defer_corr && (!halo || split_fused());
   }
   // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
   void settle() {
@@ -2325,7 +2353,7 @@ struct rcmdyn_engine {
   // inflow/outflow pass in a launch of its own.  A decomposed domain needs no slice exchange
   // then (split_fused: every tile computes its ghost ring).
   void step_once() {
-    fuse_bdy = cfg.idynamic != 2 && !no_fuse_bdy && (ntiles == 1 || split_fused());
+    fuse_bdy = cfg.idynamic != 2 && !no_fuse_bdy && (!halo || split_fused());
     try {
       tend();
       bdyval();

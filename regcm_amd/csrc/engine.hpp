@@ -31,6 +31,7 @@ struct Geom {
   int jci1ga, jci2ga, ici1ga, ici2ga;
   int jde1gb, jde2gb, ide1gb, ide2gb, jce1gb, jce2gb, ice1gb, ice2gb;
   int bl, br, bb, bt;              // has_bdyleft/right/bottom/top
+  int band;                        // i_band = 1: periodic in j, no west/east boundary (bl = br = 0)
   int gjx, giy;                    // global dot-grid extents
   int j0, i0;                      // global index of frame origin
   int nj, ni;                      // frame size (nj <= pitch)
@@ -59,22 +60,26 @@ struct Geom {
   __host__ __device__ __forceinline__ int icx1() const { return ice1 - (bb ? 0 : 1); }
   __host__ __device__ __forceinline__ int icx2() const { return ice2 + (bt ? 0 : 1); }
   // Global index classes (Main/mod_atm_interface.F90:231-302 on one tile): equal to the tile
-  // ranges jce/jci/jcii/jdi/jdii on owned points, and defined on ghost points.
+  // ranges jce/jci/jcii/jdi/jdii on owned points, and defined on ghost points.  In a band
+  // (i_band = 1) every j is interior: the grid is periodic in j and both grids take all jx
+  // points (Main/mpplib/mod_mppparam.F90:1131, 1351-1354).
   __host__ __device__ __forceinline__ bool gce(int j, int i) const {
-    return j >= 1 && j <= gjx - 1 && i >= 1 && i <= giy - 1;
+    return (band || (j >= 1 && j <= gjx - 1)) && i >= 1 && i <= giy - 1;
   }
   __host__ __device__ __forceinline__ bool gci(int j, int i) const {
-    return j >= 2 && j <= gjx - 2 && i >= 2 && i <= giy - 2;
+    return (band || (j >= 2 && j <= gjx - 2)) && i >= 2 && i <= giy - 2;
   }
   __host__ __device__ __forceinline__ bool gcii(int j, int i) const {
-    return j >= 3 && j <= gjx - 3 && i >= 3 && i <= giy - 3;
+    return (band || (j >= 3 && j <= gjx - 3)) && i >= 3 && i <= giy - 3;
   }
   __host__ __device__ __forceinline__ bool gdi(int j, int i) const {
-    return j >= 2 && j <= gjx - 1 && i >= 2 && i <= giy - 1;
+    return (band || (j >= 2 && j <= gjx - 1)) && i >= 2 && i <= giy - 1;
   }
   __host__ __device__ __forceinline__ bool gdii(int j, int i) const {
-    return j >= 3 && j <= gjx - 2 && i >= 3 && i <= giy - 2;
+    return (band || (j >= 3 && j <= gjx - 2)) && i >= 3 && i <= giy - 2;
   }
+  // global west / east boundary column tests (never in a band)
+  __host__ __device__ __forceinline__ bool gjeq(int j, int v) const { return !band && j == v; }
 };
 // the negative-moisture fix's row bitmap: words per (species, level) plane; the LDS (doubles) of
 // its serial part (qxcommon.hpp): the row sweep's two interior rows and 13 per lane, or the

@@ -37,7 +37,8 @@ namespace rcm {
 // the atm2-derived ones (the stencils of the ghost-ring kernels), inside the global domain.
 __device__ __forceinline__ void surface_pressures_at(const Geom& g, const Fields& f, int j, int i) {
   auto ring = [&](int d, int jhi, int ihi) {
-    return in(j, max(1, g.jde1 - d), min(jhi, g.jde2 + d)) && in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
+    const bool jok = g.band ? in(j, g.jde1 - d, g.jde2 + d) : in(j, max(1, g.jde1 - d), min(jhi, g.jde2 + d));
+    return jok && in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
   };
   if (ring(2, g.gjx - 1, g.giy - 1)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
   if (ring(3, g.gjx - 1, g.giy - 1)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
@@ -403,12 +404,12 @@ __device__ double2 udvd_bdy(const Geom& g, const Fields& f, int j, int i, uint32
   // the reference exchanges)
   auto we = [&](int jj, int ii) {
     if (in(ii, 2, g.giy - 1)) {
-      if (jj == 1 && LD(f.a1u, g.o2(jj, ii) + kof) <= d_zero) return base(2, ii);
-      if (jj == g.gjx && LD(f.a1u, g.o2(jj, ii) + kof) >= d_zero) return base(g.gjx - 1, ii);
+      if (g.gjeq(jj, 1) && LD(f.a1u, g.o2(jj, ii) + kof) <= d_zero) return base(2, ii);
+      if (g.gjeq(jj, g.gjx) && LD(f.a1u, g.o2(jj, ii) + kof) >= d_zero) return base(g.gjx - 1, ii);
     }
     return base(jj, ii);
   };
-  if (in(j, 1, g.gjx)) {
+  if (g.band || in(j, 1, g.gjx)) {
     if (i == 1 && LD(f.a1v, g.o2(j, i) + kof) >= d_zero) return we(j, 2);
     if (i == g.giy && LD(f.a1v, g.o2(j, i) + kof) <= d_zero) return we(j, g.giy - 1);
   }
@@ -433,14 +434,14 @@ __global__ __launch_bounds__(256) void k_sladv(Geom g, const Consts* __restrict_
   auto ua = [&](int jj, int ii) {
     const uint32_t q2 = g.o2(jj, ii);
     double ud;
-    if (ib4 && (jj == 1 || jj == g.gjx || ii == 1 || ii == g.giy)) ud = udvd_bdy(g, f, jj, ii, kof).x;
+    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || ii == 1 || ii == g.giy)) ud = udvd_bdy(g, f, jj, ii, kof).x;
     else ud = LD(f.a1u, q2 + kof) * LD(f.rpsda, q2);
     return ud * LD(f.msfd, q2);
   };
   auto va = [&](int jj, int ii) {
     const uint32_t q2 = g.o2(jj, ii);
     double vd;
-    if (ib4 && (jj == 1 || jj == g.gjx || ii == 1 || ii == g.giy)) vd = udvd_bdy(g, f, jj, ii, kof).y;
+    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || ii == 1 || ii == g.giy)) vd = udvd_bdy(g, f, jj, ii, kof).y;
     else vd = LD(f.a1v, q2 + kof) * LD(f.rpsda, q2);
     return vd * LD(f.msfd, q2);
   };
@@ -624,7 +625,7 @@ __device__ __forceinline__ void momentum_block(const Geom& g, const Consts* __re
       double ud = ok ? au[n] * ar[n] : 0.0, vd = ok ? av[n] * ar[n] : 0.0;
       if ((c->iboudy == 3 || c->iboudy == 4) && ok) {
         const int jg = J0 - 1 + jj, ig = I0 - 1 + ii;
-        if (jg == 1 || jg == g.gjx || ig == 1 || ig == g.giy) {
+        if (g.gjeq(jg, 1) || g.gjeq(jg, g.gjx) || ig == 1 || ig == g.giy) {
           const double2 bb = udvd_bdy(g, f, jg, ig, kof);
           ud = bb.x; vd = bb.y;
         }
@@ -803,8 +804,8 @@ __device__ __forceinline__ void momentum_block(const Geom& g, const Consts* __re
   vt = vt + xkd * (z4_c1 * (UM(sVM, 1, 0) + UM(sVM, -1, 0) + UM(sVM, 0, 1) + UM(sVM, 0, -1)) +        \
                    z4_c2 * (UM(sVM, 0, 0)));
     if (c->idiffu == 1) {
-      if (j == 2) { LAPD(); }
-      if (j == g.gjx - 1) { LAPD(); }
+      if (g.gjeq(j, 2)) { LAPD(); }
+      if (g.gjeq(j, g.gjx - 1)) { LAPD(); }
       if (i == 2) { LAPD(); }
       if (i == g.giy - 1) { LAPD(); }
     }
@@ -927,9 +928,9 @@ __global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f, QxArgs 
           (z4_c1 * (H2T(S, 2, 0) + H2T(S, -2, 0) + H2T(S, 0, 2) + H2T(S, 0, -2)) +                \
            z4_c2 * (H2T(S, 1, 0) + H2T(S, -1, 0) + H2T(S, 0, 1) + H2T(S, 0, -1)) +                \
            z4_c3 * H2T(S, 0, 0));                                                                 \
-    if (j == 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (g.gjeq(j, 2)) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
-    if (j == g.gjx - 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
+    if (g.gjeq(j, g.gjx - 2)) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
     if (i == 2) ften = ften + d_one * xkcs * (z4_c1 * (H2T(S, 1, 0) + H2T(S, -1, 0) + \
         H2T(S, 0, 1) + H2T(S, 0, -1)) + z4_c2 * H2T(S, 0, 0));                                   \
@@ -1703,11 +1704,11 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
     // region points outside frame w (a partial last block) lie in the contaminated rim: they
     // are read as zero and never reach an output point
     const bool inw = in(j, w.j0, w.j0 + w.nj - 1) && in(i, w.i0, w.i0 + w.ni - 1);
-    ce[r] = inw && in(j, 1, gjx - 1) && in(i, 1, giy - 1);
-    ci[r] = inw && in(j, 2, gjx - 2) && in(i, 2, giy - 2);
-    di[r] = inw && in(j, 2, gjx - 1) && in(i, 2, giy - 1);
+    ce[r] = inw && g.gce(j, i);
+    ci[r] = inw && g.gci(j, i);
+    di[r] = inw && g.gdi(j, i);
     bnd[r] = ce[r] && !ci[r] &&
-             (((j == 1 || j == gjx - 1) && in(i, 2, giy - 2)) || i == 1 || i == giy - 1);
+             (((g.gjeq(j, 1) || g.gjeq(j, gjx - 1)) && in(i, 2, giy - 2)) || i == 1 || i == giy - 1);
     own[r] = in(j, J1, J1 + SPB - 1) && in(i, I1, I1 + SPB - 1);
     const long q = ce[r] ? w.ix(j, i) : 0;
     Ds[0][li][lj] = ce[r] ? D1[q] : 0.0; Ds[1][li][lj] = ce[r] ? D2[q] : 0.0;

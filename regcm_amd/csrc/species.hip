@@ -61,8 +61,8 @@ __device__ __forceinline__ double qx_diffu(const Geom& g, const Consts* __restri
   auto lap = [&](double x) {
     return x + d_one * xkcs * (z4_c1 * (f(1, 0) + f(-1, 0) + f(0, 1) + f(0, -1)) + z4_c2 * f(0, 0));
   };
-  if (j == 2) ften = lap(ften);
-  if (j == g.gjx - 2) ften = lap(ften);
+  if (g.gjeq(j, 2)) ften = lap(ften);
+  if (g.gjeq(j, g.gjx - 2)) ften = lap(ften);
   if (i == 2) ften = lap(ften);
   if (i == g.giy - 2) ften = lap(ften);
   return ften;

@@ -79,7 +79,7 @@ module mod_gpu_dyn
     integer(c_int32_t) :: ibltyp, iuwvadv
     real(c_double) :: nuk, tkemin
     ! ABI 6: physicsparam ipptls and the nqx param sets from it (2, or 5 for ipptls >= 2);
-    ! i_band, i_crm, ichem (refused if set)
+    ! i_band (1: tropical band, hydrostatic core), i_crm, ichem (refused if set)
     integer(c_int32_t) :: ipptls, nqx
     integer(c_int32_t) :: i_band, i_crm, ichem
   end type rcmdyn_config

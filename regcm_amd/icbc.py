@@ -44,6 +44,19 @@ def psc2psd_global(pc: np.ndarray) -> np.ndarray:
     return pd
 
 
+def psc2psd_band(pc: np.ndarray) -> np.ndarray:
+    """psc2psd of a band (i_band = 1): periodic in j, so every column takes the interior form and
+    the bottom/top rows the two-point means; no west/east lines or corners
+    (Main/mpplib/mod_mppparam.F90:13811-13862 with has_bdyleft = has_bdyright = .false.)."""
+    iy, jx = pc.shape
+    pm = np.roll(pc, 1, axis=1)                          # pc(j-1), periodic
+    pd = np.zeros_like(pc)
+    pd[1:iy - 1] = (pc[1:iy - 1] + pc[0:iy - 2] + pm[1:iy - 1] + pm[0:iy - 2]) * 0.25
+    pd[iy - 1] = (pc[iy - 2] + pm[iy - 2]) * 0.5
+    pd[0] = (pc[0] + pm[0]) * 0.5
+    return pd
+
+
 def _qsat(t: np.ndarray, p_pa: np.ndarray) -> np.ndarray:
     es = 611.2 * np.exp(17.67 * (t - 273.15) / (t - 29.65))
     es = np.minimum(es, 0.5 * p_pa)
@@ -73,7 +86,9 @@ def generate(rc: RunConfig, seed: int = SEED, hmax: float = None) -> dict:
     expo = C.egrav / (C.rgas * 0.0065)
     ps = C.stdpcb * (1.0 - 0.0065 * ht / 288.15) ** expo
     pstar = ps - ptop
-    pdot = psc2psd_global(pstar)
+    band = getattr(rc, "i_band", 0) == 1
+    p2d = psc2psd_band if band else psc2psd_global
+    pdot = p2d(pstar)
 
     p_pa = (hsig[:, None, None] * pstar[None] + ptop) * 1000.0            # (kz, iy, jx)
     t = np.maximum(288.15 * (p_pa / 101325.0) ** (C.rgas * 0.0065 / C.egrav), 216.65)
@@ -85,14 +100,15 @@ def generate(rc: RunConfig, seed: int = SEED, hmax: float = None) -> dict:
 
     # time-level 1 of the boundary data
     pstar1 = pstar + 0.1
-    pdot1 = psc2psd_global(pstar1)
+    pdot1 = p2d(pstar1)
     t1, u1, v1, qv1 = t + 1.0, u + 1.0, v + 1.0, qv * 1.02
     rdtbdy = 1.0 / rc.dtbdys
 
     def cross(a):
         out = a.copy()
         out[..., iy - 1, :] = 0.0
-        out[..., :, jx - 1] = 0.0
+        if not band:                     # a band's cross grid takes every j
+            out[..., :, jx - 1] = 0.0
         return out
 
     ub0, vb0 = u * pdot[None], v * pdot[None]
@@ -147,7 +163,8 @@ def hydrometeor_state(rc: RunConfig, st: dict, seed: int = SEED + 5, nqx: int = 
         mask = (rng.uniform(size=(kz, iy, jx)) < 0.6).astype(np.float64)
         q = layer[:, None, None] * mask * rng.uniform(0.5, 1.5, size=(kz, iy, jx))
         q[:, iy - 1, :] = 0.0
-        q[:, :, jx - 1] = 0.0
+        if getattr(rc, "i_band", 0) != 1:       # a band's cross grid takes every j
+            q[:, :, jx - 1] = 0.0
         out[f"ATM1_{nm}"] = q * ps[None]
         out[f"ATM2_{nm}"] = q * ps[None] * rng.uniform(0.95, 1.0, size=(kz, iy, jx))
     return out
@@ -163,6 +180,10 @@ def spinit_storage(rc: RunConfig, split: dict, st: dict):
     mapf = 1.0 / (msfx * msfx)
     uuu = st["ATM2_U"] * msfd[None]
     vvv = st["ATM2_V"] * msfd[None]
+    band = getattr(rc, "i_band", 0) == 1
+    if band:
+        # periodic in j: the cross grid takes every j, and u, v at j+1 of the last column wrap
+        return _spinit_storage_band(rc, split, st, uuu, vvv, mapf, rdx2)
     ce = (slice(0, iy - 1), slice(0, jx - 1))
     dstor = np.zeros((ns, iy, jx))
     hstor = np.zeros((ns, iy, jx))
@@ -174,6 +195,36 @@ def spinit_storage(rc: RunConfig, split: dict, st: dict):
             expr = (((((((-u[1:iy, 0:jx - 1] + u[1:iy, 1:jx]) - u[0:iy - 1, 0:jx - 1]) +
                         u[0:iy - 1, 1:jx]) + v[1:iy, 0:jx - 1]) + v[1:iy, 1:jx]) -
                      v[0:iy - 1, 0:jx - 1]) - v[0:iy - 1, 1:jx])
+            d = d + ((zmatxr[l, k] * mapf[ce]) * rdx2) * expr
+        dstor[l][ce] = d
+    psb = st["PSB"][0][ce]
+    sigmah, varpa1, tau, pd, ptop = split["sigmah"], split["varpa1"], split["tau"], split["pd"], rc.ptop
+    for l in range(ns):
+        pdlog = varpa1[l, kz] * math.log(sigmah[kz] * pd + ptop)
+        eps1 = varpa1[l, kz] * sigmah[kz] / (sigmah[kz] * pd + ptop)
+        h = pdlog + eps1 * (psb - pd)
+        for k in range(kz):
+            pdlog = varpa1[l, k] * math.log(sigmah[k] * pd + ptop)
+            eps1 = varpa1[l, k] * sigmah[k] / (sigmah[k] * pd + ptop)
+            eps = eps1 * (psb - pd)
+            h = ((h + pdlog) + (tau[l, k] * st["ATM2_T"][k][ce]) / psb) + eps
+        hstor[l][ce] = h
+    return dstor, hstor
+
+
+def _spinit_storage_band(rc, split, st, uuu, vvv, mapf, rdx2):
+    jx, iy, kz, ns = rc.jx, rc.iy, rc.kz, rc.nsplit
+    ce = (slice(0, iy - 1), slice(0, jx))
+    dstor = np.zeros((ns, iy, jx))
+    hstor = np.zeros((ns, iy, jx))
+    zmatxr = split["zmatxr"]
+    for l in range(ns):
+        d = np.zeros((iy - 1, jx))
+        for k in range(kz):
+            u, v = uuu[k], vvv[k]
+            up, vp = np.roll(u, -1, axis=1), np.roll(v, -1, axis=1)     # (j+1), periodic
+            expr = (((((((-u[1:iy] + up[1:iy]) - u[0:iy - 1]) + up[0:iy - 1]) + v[1:iy]) + vp[1:iy]) -
+                     v[0:iy - 1]) - vp[0:iy - 1])
             d = d + ((zmatxr[l, k] * mapf[ce]) * rdx2) * expr
         dstor[l][ce] = d
     psb = st["PSB"][0][ce]
@@ -335,6 +386,7 @@ def tke_state(rc: RunConfig, seed: int = SEED) -> dict:
         t = prof * (1.0 + 0.3 * rng.standard_normal((kz + 1, iy, jx))) + 0.02 * n
         t = np.maximum(t, rc.tkemin)
         t[:, iy - 1, :] = 0.0
-        t[:, :, jx - 1] = 0.0
+        if getattr(rc, "i_band", 0) != 1:
+            t[:, :, jx - 1] = 0.0
         out[name] = t
     return out

@@ -90,6 +90,16 @@ def test_tile_extents_partition_domain():
     assert widths == [33, 32, 32]
 
 
+def test_band_refused_for_nonhydrostatic():
+    import dataclasses
+    from regcm_amd.config import CONFIGS
+    from regcm_amd import icbc
+    rc = dataclasses.replace(CONFIGS["N1"], i_band=1)
+    data = icbc.generate_nh(CONFIGS["N1"])
+    with pytest.raises(dycore.EngineError, match="i_band"):
+        dycore.DynCore(rc, data["split"])
+
+
 def test_create_without_gpu_fails_loudly():
     """On a host without a GPU the engine refuses to start (no silent CPU fallback)."""
     try:
@@ -111,7 +121,7 @@ def test_create_without_gpu_fails_loudly():
                                      ({"iboudy": 0}, "iboudy"),
                                      ({"ibltyp": 2, "iuwvadv": 2}, "iuwvadv"),
                                      ({"ipptls": 0}, "ipptls"), ({"ipptls": 3}, "ipptls"),
-                                     ({"i_band": 1}, "i_band"), ({"i_crm": 1}, "i_crm"),
+                                     ({"i_band": 2}, "i_band"), ({"i_crm": 1}, "i_crm"),
                                      ({"ichem": 1}, "ichem")])
 def test_create_refuses_unbuilt_options(opt, msg):
     """A drop-in refuses what it does not compute: option values whose reference branches are

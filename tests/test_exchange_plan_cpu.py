@@ -22,7 +22,7 @@ def plans(rc, split, cj, ci, nsteps):
     return [dycore.exchange_plan(rc, split, cj, ci, r, nsteps) for r in range(cj * ci)]
 
 
-def check_plans(pl, cj, ci):
+def check_plans(pl, cj, ci, band=False):
     n = cj * ci
     sends, recvs = defaultdict(list), defaultdict(list)
     colls = []
@@ -45,8 +45,8 @@ def check_plans(pl, cj, ci):
         lj, li = divmod(r, ci)
         for dj in (-1, 0, 1):
             for di in (-1, 0, 1):
-                q = (lj + dj, li + di)
-                if (dj or di) and 0 <= q[0] < cj and 0 <= q[1] < ci:
+                q = ((lj + dj) % cj if band else lj + dj, li + di)
+                if (dj or di) and 0 <= q[0] < cj and 0 <= q[1] < ci and q != (lj, li):
                     assert sends.get((r, q[0] * ci + q[1], 0)), (r, q)
     return sum(len(v) for v in sends.values()), len(colls[0])
 
@@ -84,6 +84,23 @@ def test_hydrostatic_variant_plans_match(variant):
     rc = dataclasses.replace(CONFIGS["C1"], **variant)
     data = icbc.generate(CONFIGS["C1"])
     check_plans(plans(rc, data["split"], 2, 2, 3), 2, 2)
+
+
+@pytest.mark.parametrize("name,cj,ci", [("C1", 2, 2), ("C1", 3, 1), ("C1", 1, 3), ("C3", 2, 4), ("C3", 4, 2)], ids=str)
+@pytest.mark.parametrize("variant", [{}, {"isladvec": 1, "ibltyp": 2}, {"idiffu": 3}],
+                         ids=lambda v: ",".join(f"{k}={x}" for k, x in v.items()) or "default")
+def test_band_plans_match(name, cj, ci, variant):
+    """A band (i_band = 1) is periodic in j: the tiles of the first and the last tile column
+    are neighbours, and with two tiles in j one rank is both the west and the east neighbour,
+    so its messages to that rank must be issued in the order the receiver posts them; with one
+    tile in j the periodic exchange is the rank's own copy (no message)."""
+    rc = dataclasses.replace(CONFIGS[name], i_band=1, **variant)
+    data = icbc.generate(rc)
+    pl = plans(rc, data["split"], cj, ci, 3)
+    msgs, _ = check_plans(pl, cj, ci, band=True)
+    assert msgs > 0
+    if cj > 1:                       # the wrap-around pair exchanges
+        assert any(((p[:, 1] == 1) & (p[:, 4] == (cj - 1) * ci)).any() for p in pl[:ci])
 
 
 def test_narrow_tiles_per_substep_exchange_plans_match():

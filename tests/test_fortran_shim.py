@@ -274,7 +274,7 @@ def test_fortran_host_only_entry_points(c1_data):
     assert_same(py, fo)
     assert py[3] == (2, 4) and py[-2].shape[0] > 0
     bad = build_config(rc, data["split"])
-    bad.i_band = 1
+    bad.i_band = 2
     s = Script(bad).soft().add(CREATE)
     py, fo = s.run_python(), s.run_fortran()
     assert py == fo and py[0][0] != 0 and "i_band" in py[0][1], py
