@@ -30,6 +30,8 @@ __device__ __forceinline__ double dmin(double a, double b) { return (a < b) ? a 
 
 __device__ __forceinline__ bool in(int v, int lo, int hi) { return v >= lo && v <= hi; }
 
+
+
 // Block phase timing (build with -DRCM_PHASE_TIMING): thread 0 of every block records
 // wall-clock marks (100 MHz) into a device buffer that rcm_phase_dump() (kernels.hip) writes
 // to a file; the measurement behind the kernel structure notes in DESIGN.md.
@@ -57,6 +59,31 @@ static __device__ int rcm_pt_count = 0;
 #define PT_MARK() do { } while (0)
 #define PT_PRINT(KID_) do { } while (0)
 #endif
+
+// XCD-aware block placement.  The workgroups of a launch go round-robin over the 8 XCDs, each
+// with its own L2: in blockIdx order the four neighbours of a tile run on other XCDs, so every
+// stencil halo is fetched again from beyond L2.  xcd_block() renumbers the blocks: launch-order
+// block b takes tile start(b % 8) + b / 8 of the row-major tile order (x fastest, z slowest), so
+// each XCD walks one contiguous band of tile rows and the rows above and below a tile are (but
+// at the band edges) its own XCD's.
+struct Blk3 {
+  int x, y, z;
+};
+__device__ __forceinline__ Blk3 xcd_block() {
+  const int nx = (int)gridDim.x, ny = (int)gridDim.y;
+  const int n = nx * ny * (int)gridDim.z;
+  const int b = ((int)blockIdx.z * ny + (int)blockIdx.y) * nx + (int)blockIdx.x;
+  const int per = n >> 3, rem = n & 7, x = b & 7;
+  const int t = x * per + (x < rem ? x : rem) + (b >> 3);
+  return {t % nx, (t / nx) % ny, t / (nx * ny)};
+}
+// THREAD_POINT over xcd_block()'s tile
+#define THREAD_POINT_XCD(j1, i1)                                        \
+  const Blk3 xb_ = xcd_block();                                         \
+  const int j = (j1) + xb_.x * (int)blockDim.x + (int)threadIdx.x;      \
+  const int i = (i1) + xb_.y * (int)blockDim.y + (int)threadIdx.y;      \
+  const int k = xb_.z + 1;                                              \
+  (void)k;
 
 // thread -> (j, i, k) over a box starting at (j1, i1); k = blockIdx.z + 1
 #define THREAD_POINT(j1, i1)                                   \

@@ -2180,13 +2180,22 @@ struct rcmdyn_engine {
     if (fused) {
       each([&](Tile& t) {
         const Geom& g = t.g;
-        dim3 gr((g.jcx2() - g.jcx1() + SPB) / SPB, (g.icx2() - g.icx1() + SPB) / SPB, ns);
-        if (halo)
-          KLAUNCH(k_spstep_fused, gr, dim3(SPR, SPR), 0, stream, g, t.gw, dc, t.wdeld, t.wdelh, t.wmsfx, t.wmsfd,
-                  t.wpsdota, t.wmapf, t.wpsa, t.ddsum, t.dhsum);
+        // 16 x 16 owned points per block, or 8 x 8 when that leaves most CUs idle (a rank tile
+        // of a multi-GPU run): the sub-step chain is the block's latency, and 8 x 8 blocks cut
+        // it per block (576 region points instead of 1024) at the price of more halo points
+        const int W = g.jcx2() - g.jcx1() + 1, H = g.icx2() - g.icx1() + 1;
+        const bool small = (long)((W + 15) / 16) * ((H + 15) / 16) * ns < SP8_BELOW;
+        const Geom& w = halo ? t.gw : g;
+        const double *dd = halo ? t.wdeld : t.deld, *dh = halo ? t.wdelh : t.delh;
+        const double *mx = halo ? t.wmsfx : t.msfx, *md = halo ? t.wmsfd : t.msfd;
+        const double *pd = halo ? t.wpsdota : t.psdota, *mp = halo ? t.wmapf : t.mapf;
+        const double* pa = halo ? t.wpsa : t.psa_[t.cur];
+        if (small)
+          KLAUNCH(k_spstep_fused<8>, dim3((W + 7) / 8, (H + 7) / 8, ns), dim3(8 + 2 * SPH, 8 + 2 * SPH), 0, stream, g, w,
+                  dc, dd, dh, mx, md, pd, mp, pa, t.ddsum, t.dhsum);
         else
-          KLAUNCH(k_spstep_fused, gr, dim3(SPR, SPR), 0, stream, g, g, dc, t.deld, t.delh, t.msfx, t.msfd,
-                  t.psdota, t.mapf, t.psa_[t.cur], t.ddsum, t.dhsum);
+          KLAUNCH(k_spstep_fused<16>, dim3((W + 15) / 16, (H + 15) / 16, ns), dim3(16 + 2 * SPH, 16 + 2 * SPH), 0,
+                  stream, g, w, dc, dd, dh, mx, md, pd, mp, pa, t.ddsum, t.dhsum);
       });
     } else {
       each([&](Tile& t) {

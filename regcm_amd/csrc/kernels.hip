@@ -1107,12 +1107,18 @@ __device__ __forceinline__ void scalars_block(const Geom& g, const Consts* __res
   const double xkcs = xkc * c->rdxsq * pb;
   if (f.xkcs) ST(f.xkcs, o3, xkcs);
   // ================= temperature
+#if RCM_SC_TIMING_PART == 2
+  if (0)
+#endif
   {
     double td = d_zero + hadv_flux(c, xm, ps, uavg1, uavg2, vavg1, vavg2, H1T(sXT, 0, 0), H1T(sXT, -1, 0),
                                    H1T(sXT, 1, 0), H1T(sXT, 0, -1), H1T(sXT, 0, 1), 1);
     // vadv3d ind = 1 (Main/mod_advection.F90:771-783): pf/pb from psb (mkslice :263-271)
     {
       const double ptop = c->ptop, c287 = c->c287;
+#if RCM_SC_TIMING_PART >= 3
+#define powpos(x, y) ((x) + 0.0 * (y))
+#endif
 #define PF(K) ((c->sigma[K] * pb + ptop) * d_1000)
 #define PB(K) ((c->hsigma[K] * pb + ptop) * d_1000)
       if (k >= 2)
@@ -1123,6 +1129,9 @@ __device__ __forceinline__ void scalars_block(const Geom& g, const Consts* __res
                          c->twt2[k + 1] * t1 * powpos(PF(k + 1) / PB(k), c287))) * c->xds[k];
 #undef PB
 #undef PF
+#if RCM_SC_TIMING_PART >= 3
+#undef powpos
+#endif
     }
     // omega, Main/mod_tendency.F90:1200-1214
     double om;
@@ -1164,6 +1173,9 @@ __device__ __forceinline__ void scalars_block(const Geom& g, const Consts* __res
     ST(f.b2t, o3, t1 + d);
     ST(f.b1t, o3, ct);
   }
+#if RCM_SC_TIMING_PART == 1 || RCM_SC_TIMING_PART == 3
+  return;
+#endif
   // ================= qv
   // hadvqv, or the semi-Lagrangian start of qxdyn from k_sladv (isladvec = 1, :1361-1363)
   double tq = c->isladvec ? LD(f.slqv, o3)
@@ -1467,6 +1479,9 @@ __device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int
 #ifndef SP_LB
 #define SP_LB 5
 #endif
+#ifndef SP_KU
+#define SP_KU 1
+#endif
 __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
@@ -1515,16 +1530,34 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
     const double* U01 = old_at(j, i + 1) ? o2u : a2u; const double* V01 = old_at(j, i + 1) ? o2v : a2v;
     const double* U11 = old_at(j + 1, i + 1) ? o2u : a2u; const double* V11 = old_at(j + 1, i + 1) ? o2v : a2v;
     const double* U10 = old_at(j + 1, i) ? o2u : a2u; const double* V10 = old_at(j + 1, i) ? o2v : a2v;
-    for (int k = ty + 1; k <= kz; k += SPG) {
-#define DIV(U, V, U01, U11, U10, V01, V11, V10)                                                            \
-  (-(F3(U01, j, i + 1, k) * m01) + (F3(U11, j + 1, i + 1, k) * m11) - (F3(U, j, i, k) * m00) +                \
-   (F3(U10, j + 1, i, k) * m10) + (F3(V01, j, i + 1, k) * m01) + (F3(V11, j + 1, i + 1, k) * m11) -            \
-   (F3(V, j, i, k) * m00) - (F3(V10, j + 1, i, k) * m10))
-      sD1[(k - 1) * SPC + tx] = DIV(a1u, a1v, a1u, a1u, a1u, a1v, a1v, a1v);
-      sD2[(k - 1) * SPC + tx] = DIV(a2u, a2v, U01, U11, U10, V01, V11, V10);
+    // SP_KU levels per pass: every load of the pass is issued before any use
+    for (int k0 = ty + 1; k0 <= kz; k0 += SPG * SP_KU) {
+      double x[SP_KU][18];
+#pragma unroll
+      for (int n = 0; n < SP_KU; n++) {
+        const int k = min(k0 + SPG * n, kz);
+        x[n][0] = F3(a1u, j, i + 1, k); x[n][1] = F3(a1u, j + 1, i + 1, k);
+        x[n][2] = F3(a1u, j, i, k); x[n][3] = F3(a1u, j + 1, i, k);
+        x[n][4] = F3(a1v, j, i + 1, k); x[n][5] = F3(a1v, j + 1, i + 1, k);
+        x[n][6] = F3(a1v, j, i, k); x[n][7] = F3(a1v, j + 1, i, k);
+        x[n][8] = F3(U01, j, i + 1, k); x[n][9] = F3(U11, j + 1, i + 1, k);
+        x[n][10] = F3(a2u, j, i, k); x[n][11] = F3(U10, j + 1, i, k);
+        x[n][12] = F3(V01, j, i + 1, k); x[n][13] = F3(V11, j + 1, i + 1, k);
+        x[n][14] = F3(a2v, j, i, k); x[n][15] = F3(V10, j + 1, i, k);
+        x[n][16] = F3(a1t, j, i, k); x[n][17] = F3(a2t, j, i, k);
+      }
+#pragma unroll
+      for (int n = 0; n < SP_KU; n++) {
+        const int k = k0 + SPG * n;
+        if (k > kz) break;
+#define DIV(o) (-(x[n][o] * m01) + (x[n][o + 1] * m11) - (x[n][o + 2] * m00) + (x[n][o + 3] * m10) + \
+                (x[n][o + 4] * m01) + (x[n][o + 5] * m11) - (x[n][o + 6] * m00) - (x[n][o + 7] * m10))
+        sD1[(k - 1) * SPC + tx] = DIV(0);
+        sD2[(k - 1) * SPC + tx] = DIV(8);
 #undef DIV
-      sT1[(k - 1) * SPC + tx] = F3(a1t, j, i, k);
-      sT2[(k - 1) * SPC + tx] = F3(a2t, j, i, k);
+        sT1[(k - 1) * SPC + tx] = x[n][16];
+        sT2[(k - 1) * SPC + tx] = x[n][17];
+      }
     }
   }
   __syncthreads();
@@ -1563,12 +1596,13 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
       double h3 = d_zero, h2 = d_zero;
       if (ce) {
         const double pa = F2(psa, j, i), pbv = F2(psb, j, i);
+        const double rpa = d_one / pa, rpbv = d_one / pbv;
         h3 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pa - c->pd);
         h2 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pbv - c->pd);
         for (int k = 1; k <= kz; k++) {
           const double ta = c->tau[l - 1][k - 1], pdk = c->pdlog[l - 1][k], ek = c->eps1[l - 1][k];
-          h3 = h3 + pdk + ta * sT1[(k - 1) * SPC + tx] / pa + ek * (pa - c->pd);
-          h2 = h2 + pdk + ta * sT2[(k - 1) * SPC + tx] / pbv + ek * (pbv - c->pd);
+          h3 = h3 + pdk + div_by(ta * sT1[(k - 1) * SPC + tx], pa, rpa) + ek * (pa - c->pd);
+          h2 = h2 + pdk + div_by(ta * sT2[(k - 1) * SPC + tx], pbv, rpbv) + ek * (pbv - c->pd);
         }
       }
       SLOT(delh, l, 1)[q] = hs - h2;
@@ -1669,10 +1703,12 @@ __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int
 // for a tile of a decomposition is a wide frame whose ghost ring holds its neighbours' values
 // to depth SPH (one width-SPH exchange per step instead of three per sub-step); the masks use
 // global indices so ghost points evolve exactly as on their owning tile.  Outputs use frame g.
-__global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
+template <int SB>
+__global__ __launch_bounds__((SB + 2 * SPH) * (SB + 2 * SPH)) void k_spstep_fused(
     Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh,
     const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota,
     const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum) {
+  constexpr int SPB = SB, SPR = SB + 2 * SPH, SPP = SPR + 1;   // owned side, region side, LDS pitch
   __shared__ double Ds[2][SPR][SPP], Hs[2][SPR][SPP], U[SPR][SPP], V[SPR][SPP];
   const int l = blockIdx.z + 1;
   // owned blocks tile the tile's cross points plus its ghost ring (k_split_correct reads
@@ -1697,6 +1733,7 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
   // (leapfrog) are loop-invariant and formed once
   constexpr int NR = 1;
   double d3f[NR], h3f[NR], d3l[NR], h3l[NR], ps[NR], mf[NR], ufac[NR], msd[NR], sd[NR], sh[NR];
+  double rps[NR], rufac[NR];                            // 1/ps, 1/ufac for div_by
   bool ce[NR], ci[NR], bnd[NR], di[NR], own[NR];
   const double m2d = (double)m2;
   for (int r = 0; r < NR; r++) {
@@ -1719,6 +1756,8 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
     ps[r] = ci[r] ? psa[w.ix(j, i)] : 1.0;
     mf[r] = ci[r] ? mapf[w.ix(j, i)] : 0.0;
     ufac[r] = di[r] ? c->dx2 * msfx[w.ix(j, i)] : 1.0;
+    rufac[r] = d_one / ufac[r];
+    rps[r] = d_one / ps[r];
     msd[r] = di[r] ? msfd[w.ix(j, i)] : 0.0;
     sd[r] = ce[r] ? Ds[0][li][lj] : 0.0;     // ddsum(ce) = deld(n0)
     sh[r] = ce[r] ? Hs[0][li][lj] : 0.0;
@@ -1742,8 +1781,8 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
       const int lj = tx, li = ty + SPR * r;
       if (di[r] && lj >= 1 && li >= 1 && in(li, lo, hi + 1) && in(lj, lo, hi + 1)) {
         const double a = Hs[src][li][lj], b = Hs[src][li - 1][lj], cc = Hs[src][li][lj - 1], dd = Hs[src][li - 1][lj - 1];
-        double w1 = (a + b - cc - dd) / ufac[r];
-        double w2 = (a + cc - b - dd) / ufac[r];
+        double w1 = div_by(a + b - cc - dd, ufac[r], rufac[r]);
+        double w2 = div_by(a + cc - b - dd, ufac[r], rufac[r]);
         w1 = w1 * pda[r];
         w2 = w2 * pda[r];
         U[li][lj] = w1 * msd[r];
@@ -1761,12 +1800,12 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
              V[li + 1][lj] + V[li + 1][lj + 1] - V[li][lj] - V[li][lj + 1]);
         if (n == 1) {
           const double dn = Ds[n0][li][lj] - dtau * w3 + d3f[r];
-          const double hn = Hs[n0][li][lj] - dtau * hbar * Ds[n0][li][lj] / ps[r] + h3f[r];
+          const double hn = Hs[n0][li][lj] - div_by(dtau * hbar * Ds[n0][li][lj], ps[r], rps[r]) + h3f[r];
           Ds[nn][li][lj] = dn;
           Hs[nn][li][lj] = hn;
         } else {
           const double dn = Ds[n0][li][lj] - dtau2 * w3 + d3l[r];
-          const double hn = Hs[n0][li][lj] - dtau2 * hbar * Ds[n1][li][lj] / ps[r] + h3l[r];
+          const double hn = Hs[n0][li][lj] - div_by(dtau2 * hbar * Ds[n1][li][lj], ps[r], rps[r]) + h3l[r];
           Ds[nn][li][lj] = dn;
           Hs[nn][li][lj] = hn;
         }
@@ -1792,6 +1831,12 @@ __global__ __launch_bounds__(SPR * SPR) void k_spstep_fused(
     }
   }
 }
+template __global__ __launch_bounds__(32 * 32) void k_spstep_fused<16>(Geom, Geom, const Consts* __restrict__,
+    const double* __restrict__, const double* __restrict__, const double* __restrict__, const double* __restrict__,
+    const double* __restrict__, const double* __restrict__, const double* __restrict__, double*, double*);
+template __global__ __launch_bounds__(24 * 24) void k_spstep_fused<8>(Geom, Geom, const Consts* __restrict__,
+    const double* __restrict__, const double* __restrict__, const double* __restrict__, const double* __restrict__,
+    const double* __restrict__, const double* __restrict__, const double* __restrict__, double*, double*);
 
 __device__ __forceinline__ void bdyval_point(const Geom& g, double xt, bool integ, const BdyArgs& a, int line, int x,
                                              int k, bool interior);

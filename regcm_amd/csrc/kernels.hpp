@@ -16,6 +16,16 @@ constexpr int MAXSEG = 64;
 constexpr int NEGFIX_BLOCKS = 64;
 // fused spstep tiling: SPB x SPB owned cross points + SPH halo (>= sub-steps per mode)
 constexpr int SPB = 16, SPH = 8;
+// the 8 x 8 form (k_spstep_fused<8>) below this many 16 x 16 blocks (engine.hip)
+// timing-only builds (wrong results): the scalars blocks run 1 = the t chain only, 2 = the
+// moisture chains only, 3 = the t chain only without the x**y of vadv3d, 4 = every chain
+// without the x**y of vadv3d
+#ifndef RCM_SC_TIMING_PART
+#define RCM_SC_TIMING_PART 0
+#endif
+#ifndef SP8_BELOW
+#define SP8_BELOW 128
+#endif
 constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
 // k_columns: COLW columns x 8 level groups per block (COLT threads, 4 x kz x COLW doubles of LDS;
 // 32 measured 1-2 us slower at C3 than 64, profiles/r05/tile_ab_colw.log)
@@ -175,6 +185,7 @@ __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const doub
 __global__ void k_spstep_init(Geom g, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, double* ddsum, double* dhsum);
 __global__ void k_spstep_grad(Geom g, const Consts* __restrict__ c, int l, int src, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, double* uu, double* vv);
 __global__ void k_spstep_update(Geom g, const Consts* __restrict__ c, int l, int n0, int n1, int nn, int leap, const double* __restrict__ uu, const double* __restrict__ vv, const double* __restrict__ mapf, const double* __restrict__ psa, double* deld, double* delh, double* ddsum, double* dhsum);
+template <int SB>
 __global__ void k_spstep_fused(Geom g, Geom w, const Consts* __restrict__ c, const double* __restrict__ deld, const double* __restrict__ delh, const double* __restrict__ msfx, const double* __restrict__ msfd, const double* __restrict__ psdota, const double* __restrict__ mapf, const double* __restrict__ psa, double* ddsum, double* dhsum);
 template <int NS>
 __global__ __launch_bounds__(256) void k_split_correct(Geom g, const Consts* __restrict__ c, const double* __restrict__ ddsum, const double* __restrict__ dhsum, const double* __restrict__ psdota, const double* __restrict__ msfd, double* psa, double* psb, double* a1t, double* a2t, double* a1u, double* a1v, double* a2u, double* a2v, StepState* s, int advance, const double* __restrict__ red, int red_total, FlagSnap* ring, QFix qf, int nser);

@@ -1032,7 +1032,7 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
     nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
     return;
   }
-  THREAD_POINT(NH_ALIGN ? ALIGN_J(g.jde1) : g.jde1, g.ide1);
+  NH_SOUND_POINT(NH_ALIGN ? ALIGN_J(g.jde1) : g.jde1, g.ide1);
   if (part == 1 && nh_uv_strip(g, j, i)) return;
   nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
 }
@@ -1100,7 +1100,7 @@ __device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, c
 __global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c,
                                                              const StepState* __restrict__ s, NHFields f,
                                                              int istep, int it) {
-  THREAD_POINT(NH_ALIGN ? ALIGN_J(g.jci1) : g.jci1, g.ici1);
+  NH_SOUND_POINT(NH_ALIGN ? ALIGN_J(g.jci1) : g.jci1, g.ici1);
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double dts = s->dt / (double)istep;
@@ -1267,7 +1267,12 @@ __global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const doub
   __shared__ double sM[169];
   __shared__ unsigned long long sred[4];
   const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
-  const int J0 = (NH_ALIGN_CD ? ALIGN_J(g.jci1) : g.jci1) + (int)blockIdx.x * 64, I0 = g.ici1 + (int)blockIdx.y * 4;
+#if NH_XCD
+  const Blk3 xb = xcd_block();
+#else
+  const Blk3 xb = {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+#endif
+  const int J0 = (NH_ALIGN_CD ? ALIGN_J(g.jci1) : g.jci1) + xb.x * 64, I0 = g.ici1 + xb.y * 4;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   const bool upr = c->ifupr == 1;
   if (upr) {

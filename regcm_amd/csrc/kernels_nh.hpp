@@ -84,6 +84,17 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_ALIGN_CD
 #define NH_ALIGN_CD 0
 #endif
+// acoustic kernels: XCD-aware block placement (xcd_block, devcommon.hpp).  C5, alternating on
+// one box (profiles/r05/rejected/c5_xcd_ab.log): k_nh_sound_bc unchanged, k_nh_sound_cd
+// 884-894 -> 852-882 us, k_nh_sound_uv 519-521 -> 532-542 us, the step unchanged: off
+#ifndef NH_XCD
+#define NH_XCD 0
+#endif
+#if NH_XCD
+#define NH_SOUND_POINT(j1, i1) THREAD_POINT_XCD(j1, i1)
+#else
+#define NH_SOUND_POINT(j1, i1) THREAD_POINT(j1, i1)
+#endif
 // k_nh_sound_uv forms atm0%dprddx / dprddy from atm0%pr where it reads them
 // (Main/mod_params.F90:2676-2686: four-point sums, no rounding beyond the reference's)
 #ifndef NH_DPRFORM

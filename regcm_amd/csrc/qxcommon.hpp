@@ -336,53 +336,35 @@ __device__ void bdyval_qc_level(const Geom& g, int do_qc, int do_qv, double* a1q
   if (!do_qc) return;
   // The west/east pass reads the interior columns jci1/jci2 on rows ice1..ice2 before the
   // south/north pass rewrites rows ice1/ice2 on jci1..jci2: the two passes share exactly the
-  // four points (jci1|jci2, ice1|ice2), which are read here before any write.  Otherwise the
-  // passes are independent (west/east writes columns jce1/jce2, which south/north never reads;
-  // south/north reads rows ici1/ici2, which nothing writes), so every chunk of the loop below
-  // may write as soon as it has read, whatever the tile's extent.
-  const double c11 = F3(a1qc, g.jci1, g.ice1, k), c12 = F3(a1qc, g.jci1, g.ice2, k);
-  const double c21 = F3(a1qc, g.jci2, g.ice1, k), c22 = F3(a1qc, g.jci2, g.ice2, k);
-  __syncthreads();
-  auto qcw = [&](int jc, int i) {
-    if (i == g.ice1) return jc == g.jci1 ? c11 : c21;
-    if (i == g.ice2) return jc == g.jci1 ? c12 : c22;
-    return F3(a1qc, jc, i, k);
-  };
+  // four points (jci1|jci2, ice1|ice2).  Otherwise the passes are independent (west/east writes
+  // columns jce1/jce2, which south/north never reads; south/north reads rows ici1/ici2, which
+  // nothing writes).  So the first chunk issues every load (its operands and the four shared
+  // points) before one barrier and its stores: one memory round trip.  A later chunk (a tile
+  // wider or taller than the block) reads the shared points of row ice2 from those first loads.
   const int ni = g.ice2 - g.ice1 + 1, nj = g.jci2 - g.jci1 + 1, nx = max(ni, nj);
+  double c12 = 0.0, c22 = 0.0;
   for (int base = 0; base < nx; base += (int)blockDim.x) {
     const int x = base + (int)threadIdx.x;
     const int i = g.ice1 + x, j = g.jci1 + x;
     const bool wi = x < ni, sj = x < nj;
-    double vw = 0.0, ve = 0.0, vs = 0.0, vn = 0.0;
-    bool ow = false, oe = false, os = false, on = false;
-    if (wi && g.bl) {
-      const double qxint = qcw(g.jci1, i) / ps(g.jci1, i);
-      const double w = SLI(sl.s[0], i, k) + SLI(sl.s[0], i + 1, k) + SLI(sl.s[1], i, k) + SLI(sl.s[1], i + 1, k);
-      vw = (w > d_zero) ? d_zero : qxint * ps(g.jce1, i);
-      ow = true;
-    }
-    if (wi && g.br) {
-      const double qxint = qcw(g.jci2, i) / ps(g.jci2, i);
-      const double w = SLI(sl.s[2], i, k) + SLI(sl.s[2], i + 1, k) + SLI(sl.s[3], i, k) + SLI(sl.s[3], i + 1, k);
-      ve = (w < d_zero) ? d_zero : qxint * ps(g.jce2, i);
-      oe = true;
-    }
-    if (sj && g.bb) {
-      const double qxint = F3(a1qc, j, g.ici1, k) / ps(j, g.ici1);
-      const double w = SLJ(sl.s[12], j, k) + SLJ(sl.s[12], j + 1, k) + SLJ(sl.s[13], j, k) + SLJ(sl.s[13], j + 1, k);
-      vs = (w > d_zero) ? d_zero : qxint * ps(j, g.ice1);
-      os = true;
-    }
-    if (sj && g.bt) {
-      const double qxint = F3(a1qc, j, g.ici2, k) / ps(j, g.ici2);
-      const double w = SLJ(sl.s[14], j, k) + SLJ(sl.s[14], j + 1, k) + SLJ(sl.s[15], j, k) + SLJ(sl.s[15], j + 1, k);
-      vn = (w < d_zero) ? d_zero : qxint * ps(j, g.ice2);
-      on = true;
-    }
-    if (ow) F3(a1qc, g.jce1, i, k) = vw;
-    if (oe) F3(a1qc, g.jce2, i, k) = ve;
-    if (os) F3(a1qc, j, g.ice1, k) = vs;
-    if (on) F3(a1qc, j, g.ice2, k) = vn;
+    const bool ow = wi && g.bl, oe = wi && g.br, os = sj && g.bb, on = sj && g.bt;
+    if (base == 0) { c12 = F3(a1qc, g.jci1, g.ice2, k); c22 = F3(a1qc, g.jci2, g.ice2, k); }
+    const bool late = base > 0 && i == g.ice2;       // (jci1|jci2, ice2) after the first chunk
+    // operands (lanes without a line read their own row's valid address and discard it)
+    const int ia = wi ? i : g.ice1, ja = sj ? j : g.jci1;
+    const double qwi = late ? c12 : F3(a1qc, g.jci1, ia, k), pwi = ps(g.jci1, ia), pwe = ps(g.jce1, ia);
+    const double qei = late ? c22 : F3(a1qc, g.jci2, ia, k), pei = ps(g.jci2, ia), pee = ps(g.jce2, ia);
+    const double ww = SLI(sl.s[0], ia, k) + SLI(sl.s[0], ia + 1, k) + SLI(sl.s[1], ia, k) + SLI(sl.s[1], ia + 1, k);
+    const double we = SLI(sl.s[2], ia, k) + SLI(sl.s[2], ia + 1, k) + SLI(sl.s[3], ia, k) + SLI(sl.s[3], ia + 1, k);
+    const double qsi = F3(a1qc, ja, g.ici1, k), psi = ps(ja, g.ici1), pse = ps(ja, g.ice1);
+    const double qni = F3(a1qc, ja, g.ici2, k), pni = ps(ja, g.ici2), pne = ps(ja, g.ice2);
+    const double ws = SLJ(sl.s[12], ja, k) + SLJ(sl.s[12], ja + 1, k) + SLJ(sl.s[13], ja, k) + SLJ(sl.s[13], ja + 1, k);
+    const double wn = SLJ(sl.s[14], ja, k) + SLJ(sl.s[14], ja + 1, k) + SLJ(sl.s[15], ja, k) + SLJ(sl.s[15], ja + 1, k);
+    if (base == 0) __syncthreads();                  // every read of the shared points is done
+    if (ow) F3(a1qc, g.jce1, i, k) = (ww > d_zero) ? d_zero : (qwi / pwi) * pwe;
+    if (oe) F3(a1qc, g.jce2, i, k) = (we < d_zero) ? d_zero : (qei / pei) * pee;
+    if (os) F3(a1qc, j, g.ice1, k) = (ws > d_zero) ? d_zero : (qsi / psi) * pse;
+    if (on) F3(a1qc, j, g.ice2, k) = (wn < d_zero) ? d_zero : (qni / pni) * pne;
   }
 }
 

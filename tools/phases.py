@@ -31,8 +31,13 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--nproc", default="1x1")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--shape", default="", help="JXxIY: the config on a domain of that size (rank-tile studies)")
     args = ap.parse_args()
     rc = CONFIGS[args.config]
+    if args.shape:
+        import dataclasses
+        jx, iy = (int(x) for x in args.shape.split("x"))
+        rc = dataclasses.replace(rc, jx=jx, iy=iy)
     data = icbc.generate(rc)
     pj, pi = (int(x) for x in args.nproc.split("x"))
     e = DynCore(rc, data["split"], nproc_j=pj, nproc_i=pi)
