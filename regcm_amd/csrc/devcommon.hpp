@@ -77,6 +77,16 @@ __device__ __forceinline__ Blk3 xcd_block() {
   const int t = x * per + (x < rem ? x : rem) + (b >> 3);
   return {t % nx, (t / nx) % ny, t / (nx * ny)};
 }
+// the same within one z slice: (x, y) renumbered so each XCD walks one contiguous band of the
+// slice's rows; z (a level, say) keeps its launch order
+__device__ __forceinline__ void xcd_tile2d(int& bx, int& by) {
+  const int nx = (int)gridDim.x, n = nx * (int)gridDim.y;
+  const int b = (int)blockIdx.y * nx + (int)blockIdx.x;
+  const int per = n >> 3, rem = n & 7, x = b & 7;
+  const int t = x * per + (x < rem ? x : rem) + (b >> 3);
+  bx = t % nx;
+  by = t / nx;
+}
 // THREAD_POINT over xcd_block()'s tile
 #define THREAD_POINT_XCD(j1, i1)                                        \
   const Blk3 xb_ = xcd_block();                                         \

@@ -2098,7 +2098,8 @@ struct rcmdyn_engine {
       const int mnx = (mj2 - mo + MBJ) / MBJ, mny = (mi2 - g.idi1 + MBI) / MBI;
       const int snx = (g.jcx2() - so + SBJ) / SBJ, sny = (g.icx2() - g.icx1() + SBI) / SBI;
       KLAUNCH(k_update, dim3(std::max(mnx, snx), std::max(mny, sny), 2 * cfg.kz), dim3(SBT), 0, stream, g, dc, ds,
-              fields(t, pm), fields(t, ps), mnx, mny, snx, sny);
+              fields(t, pm), fields(t, ps), mnx, mny, snx, sny,
+              (int)((long)(g.jde2 - g.jde1 + 1) * (g.ide2 - g.ide1 + 1) < UPD_XCD_BELOW));
       return;
     }
     if (pm >= 0)
@@ -2230,7 +2231,9 @@ struct rcmdyn_engine {
       Tile& t = tiles[q];
       const Geom& g = t.g;
       const int c = t.cur;
-      dim3 gr = grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
+      const long npts = (long)((g.jdx2() - g.jde1 + 2) / 2) * (g.idx2() - g.ide1 + 1);   // point pairs per level
+      dim3 gr = SCOR_FLAT ? dim3((unsigned)((npts + 255) / 256), 1, kz)
+                          : grid3((g.jdx2() - g.jde1 + 2) / 2, g.idx2() - g.ide1 + 1, kz);
       const int adv = (int)(q + 1 == tiles.size());
       // qfuse: trailing z slices run the serial sweeps of the flagged moisture planes
       const QFix qf = qfix(t);

@@ -1274,9 +1274,11 @@ __global__ __launch_bounds__(SBT, SC_LB) void k_scalars(Geom g, const Consts* __
 // interleaved by level, 218.8-223.6 as two launches).
 __global__ __launch_bounds__(SBT, SC_LB) void k_update(Geom g, const Consts* __restrict__ c,
                                                    const StepState* __restrict__ s, Fields fm, Fields fs,
-                                                   int mnx, int mny, int snx, int sny) {
+                                                   int mnx, int mny, int snx, int sny, int xcd) {
   __shared__ union { MomLDS m; ScaLDS s; } L;
-  const int kz = c->kz, bz = (int)blockIdx.z, bx = (int)blockIdx.x, by = (int)blockIdx.y;
+  const int kz = c->kz, bz = (int)blockIdx.z;
+  int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+  if (xcd) xcd_tile2d(bx, by);
   const bool mom = bz >= kz;
   const int lz = mom ? bz - kz : bz;
   if (mom) {
@@ -1884,8 +1886,17 @@ __device__ __forceinline__ void split_correct_body(
     PT_PRINT(6);
     return;
   }
+#if SCOR_FLAT
+  // the (pair, row) points of a level flattened: every lane of a block has a point (no idle
+  // second block column on a 192-wide tile), rows follow one another in the lanes
+  const int npr = (g.jdx2() - g.jde1 + 2) / 2;
+  const int q = (int)blockIdx.x * 256 + (int)threadIdx.y * 64 + (int)threadIdx.x;
+  const int j = g.jde1 + q % npr;
+  const int i = g.ide1 + q / npr;
+#else
   const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int i = g.ide1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+#endif
   const int k = (int)blockIdx.z - zbdy + 1;
   // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
   // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch

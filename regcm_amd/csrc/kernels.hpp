@@ -23,6 +23,18 @@ constexpr int SPB = 16, SPH = 8;
 #ifndef RCM_SC_TIMING_PART
 #define RCM_SC_TIMING_PART 0
 #endif
+// k_update: XCD-aware tile placement within each level (xcd_tile2d, devcommon.hpp) on tiles of
+// fewer points than this (rank tiles).  Alternating on one box (profiles/r05/tile_ab_uxcd.log,
+// c3_uxcd_ab.log): 96x48 0.0792 -> 0.0773-0.0783 ms, 96x96 0.0962 -> 0.0936, 96x192 0.1325 ->
+// 0.1310 ms; the 192x192 tile 2-5 us slower in k_update (99-101 -> 102-104 us), so off there
+#ifndef UPD_XCD_BELOW
+#define UPD_XCD_BELOW (192 * 192 / 2 + 1)
+#endif
+// k_split_correct(_bdy): the level's point pairs flattened over the blocks (1) or 64 x 4 pair
+// tiles (0)
+#ifndef SCOR_FLAT
+#define SCOR_FLAT 1
+#endif
 #ifndef SP8_BELOW
 #define SP8_BELOW 128
 #endif
@@ -170,7 +182,7 @@ __global__ void k_momentum(Geom g, const Consts* __restrict__ c, const StepState
 __global__ void k_diffu6(Geom g, const Consts* __restrict__ c, Fields f, QxArgs q);
 __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f);
 __global__ void k_update(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields fm, Fields fs,
-                         int mnx, int mny, int snx, int sny);
+                         int mnx, int mny, int snx, int sny, int xcd);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
 __global__ void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
