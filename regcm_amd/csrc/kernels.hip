@@ -202,7 +202,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
   }
   // k_scalars appends after this (part 2 follows part 1 and the k_scalars blocks of part 1)
   if (f.qfuse && bb == 0 && threadIdx.x == 0 && f.pt.part != 2) *f.negcnt = 0;
-  const int tx = (int)threadIdx.x % COLW, ty = (int)threadIdx.x / COLW;     // column, level group (0..7)
+  const int tx = (int)threadIdx.x % COLW, ty = (int)threadIdx.x / COLW;     // column, level group
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
   // columns compute exactly what their owners do (qdot, phi, pten and the new p* there replace
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
   double* sLG = lds + 3 * kz * COLW;                        // log ratio of the layer below level k
   const uint32_t o2 = valid ? g.o2(j, i) : 0u;
   const double ptop = c->ptop, rgas = c->rgas, ep1 = c->ep1;
-  if (valid && ty == 7) surface_pressures_at(g, f, j, i);
+  if (valid && ty == COLG - 1) surface_pressures_at(g, f, j, i);
   PT_MARK();
   double rp = 0.0;
   if (ce) {
@@ -232,11 +232,11 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
     rp = d_one / psk;                                    // rpsa (K1), the same division
     // two levels per thread and pass: every load of the pass is issued before any use
     constexpr int KU = COL_KU;
-    for (int k0 = ty + 1; k0 <= kz; k0 += 8 * KU) {
+    for (int k0 = ty + 1; k0 <= kz; k0 += COLG * KU) {
       double u00[KU], u10[KU], u01[KU], u11[KU], v00[KU], v10[KU], v01[KU], v11[KU], tt[KU], qq[KU], cc[KU];
 #pragma unroll
       for (int n = 0; n < KU; n++) {
-        const int kk = k0 + 8 * n;
+        const int kk = k0 + COLG * n;
         const uint32_t o3 = o2 + (uint32_t)((kk <= kz ? kk : kz) - 1) * L8;
         u00[n] = LD(f.a1u, o3); u10[n] = LD(f.a1u, O3(1, 0)); u01[n] = LD(f.a1u, O3(0, 1)); u11[n] = LD(f.a1u, O3(1, 1));
         v00[n] = LD(f.a1v, o3); v10[n] = LD(f.a1v, O3(1, 0)); v01[n] = LD(f.a1v, O3(0, 1)); v11[n] = LD(f.a1v, O3(1, 1));
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
       }
 #pragma unroll
       for (int n = 0; n < KU; n++) {
-      const int k = k0 + 8 * n;
+      const int k = k0 + COLG * n;
       if (k > kz) break;
       const double a = u11[n] * m11 + u10[n] * m10 - u01[n] * m01 - u00[n] * m00;
       const double bq = v11[n] * m11 + v01[n] * m01 - v10[n] * m10 - v00[n] * m00;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
       // nqx = 5: tvfac with the total water load qcd = ((0 + qc) + qi) + qr + qs (decouple
       // :1107-1115, each atmx%qx = max(atm1 * rpsa, 0); pressure_gradient_force :2037), over the
       // levels this thread formed above
-      for (int k = ty + 1; k <= kz; k += 8) {
+      for (int k = ty + 1; k <= kz; k += COLG) {
         const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
         const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
         double qcd = d_zero + dmax(LD(f.a1qc, o3) * rp, d_zero);
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
     PT_MARK();
     // the hypsometric log ratios in a loop of their own (no loads in flight there: the log's
     // polynomial constants stay in registers without spilling)
-    for (int k = ty + 1; k <= kz; k += 8)
+    for (int k = ty + 1; k <= kz; k += COLG)
       sLG[(k - 1) * COLW + tx] = (k < kz) ? rcm_log((c->hsigma[k] + ptop * rp) / (c->hsigma[k + 1] + ptop * rp))
                                         : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
     PT_MARK();

@@ -44,7 +44,10 @@ constexpr int SPR = SPB + 2 * SPH, SPP = SPR + 1;  // region side, LDS row pitch
 #ifndef RCM_COLW
 #define RCM_COLW 64
 #endif
-constexpr int COLW = RCM_COLW, COLT = COLW * 8;
+#ifndef RCM_COLG
+#define RCM_COLG 8
+#endif
+constexpr int COLW = RCM_COLW, COLG = RCM_COLG, COLT = COLW * COLG;   // COLG level groups
 // k_split_project: SPC dot columns x SPG level groups per block (256 threads, 4 x kz x SPC
 // doubles of LDS).  At C3 one row of 64 columns x 8 groups (512 threads) gave 576 blocks, a
 // round and an eighth on 256 CUs at two blocks each; 32 x 8 gives 1 152 blocks of 23 KB, five

@@ -79,6 +79,22 @@ def test_hydrostatic_ranks_bit_identical(name, cj, ci):
     assert all(e.get_time() == ref.get_time() for e in engs)
 
 
+@pytest.mark.parametrize("cj,ci", [(2, 1), (2, 2), (1, 2), (3, 1)], ids=str)
+def test_band_ranks_bit_identical(cj, ci):
+    """The tropical band (i_band = 1) on ranks: the first and last tile columns are remote
+    neighbours across the period, with two tiles in j one rank is both the west and the east
+    peer (its messages in the receiver's direction order), and with one tile in j a rank's
+    periodic exchange stays inside it.  Bit-identical to one tile."""
+    import dataclasses
+    rc = dataclasses.replace(CONFIGS["C1"], i_band=1)
+    data = icbc.generate(rc)
+    nsteps = 10
+    engs = run_ranks(rc, data, cj, ci, nsteps, f"band{cj}{ci}")
+    ref = single(rc, data, nsteps)
+    for f in STATE_FIELDS:
+        assert np.array_equal(gather(engs, f), ref.get(f)), f
+
+
 def test_hydrostatic_ranks_variant_sladv_tke():
     """isladvec = 1 (the widest prologue halos) with UW TKE (its exchange on both channels)."""
     import dataclasses
