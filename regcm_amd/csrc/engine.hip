@@ -683,6 +683,11 @@ struct rcmdyn_engine {
     cfg = *c;
     dry = plan != nullptr;
     if (cfg.abi_version != RCMDYN_ABI_VERSION) throw std::runtime_error("rcmdyn: ABI version mismatch");
+#if RCM_SC_TIMING_PART || defined(RCM_SP_TIMING_M2)
+    // a timing-only build computes wrong results on purpose: never by accident
+    if (!std::getenv("RCMDYN_TIMING_BUILD"))
+      throw std::runtime_error("rcmdyn: this library is a timing-only build (set RCMDYN_TIMING_BUILD=1 to run it)");
+#endif
     if (cfg.idynamic != 1 && cfg.idynamic != 2) throw std::runtime_error("rcmdyn: idynamic must be 1 or 2");
     if (cfg.idynamic == 2) {
       if (!(cfg.nh_dtsmax > 0.0) || !(cfg.nh_xmsf > 0.0))

@@ -15,8 +15,8 @@ fi
 n=0
 for v in ${VARS:-head}; do
   n=$((n+1))
-  timeout -k 10 200 env RCMDYN_LIB=varlib/var_$v.so python tools/small_tile.py --no-shares > gpurun_out/t_${n}_$v.log 2>&1 || { echo "small_tile $v failed"; tail -3 gpurun_out/t_${n}_$v.log; exit 3; }
-  timeout -k 10 200 env RCMDYN_LIB=varlib/var_$v.so python bench.py --steps 200 --warmup 20 --no-cpu-baseline --prof-steps 5 > gpurun_out/t_${n}_$v.json 2> gpurun_out/t_${n}_$v.err || { echo "bench $v failed"; tail -3 gpurun_out/t_${n}_$v.err; exit 3; }
+  timeout -k 10 200 env RCMDYN_TIMING_BUILD=1 RCMDYN_LIB=varlib/var_$v.so python tools/small_tile.py --no-shares > gpurun_out/t_${n}_$v.log 2>&1 || { echo "small_tile $v failed"; tail -3 gpurun_out/t_${n}_$v.log; exit 3; }
+  timeout -k 10 200 env RCMDYN_TIMING_BUILD=1 RCMDYN_LIB=varlib/var_$v.so python bench.py --steps 200 --warmup 20 --no-cpu-baseline --prof-steps 5 > gpurun_out/t_${n}_$v.json 2> gpurun_out/t_${n}_$v.err || { echo "bench $v failed"; tail -3 gpurun_out/t_${n}_$v.err; exit 3; }
   echo "== $n $v"; cat gpurun_out/t_${n}_$v.log
   python3 -c "import json; d=json.loads(open('gpurun_out/t_${n}_$v.json').read().strip().splitlines()[-1]); k=d.get('kernel_us',{}); print('C3', round(d['ms_per_step']*1e3,1), 'us/step', k)"
 done
