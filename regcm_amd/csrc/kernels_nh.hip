@@ -80,6 +80,15 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
   return we(j, i);
 }
 
+// ud, vd of one dot point from its atm1 u, v (au, av) and 1/p*dot (r), already loaded by the
+// caller: udvd_nh's values (the inflow/outflow rule only on the global boundary lines)
+__device__ __forceinline__ double2 udvd_nh_ld(const Geom& g, int iboudy, const NHFields& f, double au, double av,
+                                              double r, int j, int i, int k) {
+  if ((iboudy == 3 || iboudy == 4) && (j == 1 || j == g.gjx || i == 1 || i == g.giy))
+    return udvd_nh(g, iboudy, f.a1u, f.a1v, f.rpsda, j, i, k);
+  return make_double2(au * r, av * r);
+}
+
 // ---------------------------------------------------------------------------------------
 // decouple NH (Main/mod_tendency.F90:852-1066): the decoupled winds ud, vd (with the iboudy
 // inflow/outflow rule) on the dot frame; atm1 pr/rho, the buoyancy helper atmx%pr and the
@@ -91,11 +100,13 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) {
   FRAME_POINT();
   const int kz = c->kz;
+#if !NH_UDFORM
   if (k <= kz && in(j, g.jde1ga, g.jde2ga) && in(i, g.ide1ga, g.ide2ga)) {
     const double2 d = udvd_nh(g, c->iboudy, f.a1u, f.a1v, f.rpsda, j, i, k);
     F3(f.ud, j, i, k) = d.x;                           // umd = ud*msfd: formed by omega, tend_d
     F3(f.vd, j, i, k) = d.y;
   }
+#endif
   if (!(in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga))) return;
   const double rp = F2(f.rpsa, j, i);
   if (k > kz) return;
@@ -134,6 +145,54 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   const double ps0 = F2(f.ps0, j, i), dx = F2(f.dpsdxm, j, i), dy = F2(f.dpsdym, j, i);
   F3(f.qdot, j, i, 1) = d_zero;
   F3(f.qdot, j, i, kz + 1) = d_zero;
+#if NH_UDFORM
+  // ud, vd formed here from atm1 u, v at the column's four dot points (decouple no longer
+  // stores them), one pass over the levels: the level's winds give qdot(k) and, with
+  // qdot(k-1), the mass divergence cr(k-1) (the same expressions as the two loops below)
+  (void)ucc; (void)vcc;
+  const double r00 = F2(f.rpsda, j, i), r01 = F2(f.rpsda, j, i + 1), r10 = F2(f.rpsda, j + 1, i),
+               r11 = F2(f.rpsda, j + 1, i + 1);
+  const int ib = c->iboudy;
+  const double ps = F2(f.psa, j, i), rpa = F2(f.rpsa, j, i);
+  struct W4 { double u00, u01, u10, u11, v00, v01, v10, v11; };
+  auto ld = [&](int kk) {
+    W4 a;
+    a.u00 = F3(f.a1u, j, i, kk); a.u01 = F3(f.a1u, j, i + 1, kk); a.u10 = F3(f.a1u, j + 1, i, kk);
+    a.u11 = F3(f.a1u, j + 1, i + 1, kk);
+    a.v00 = F3(f.a1v, j, i, kk); a.v01 = F3(f.a1v, j, i + 1, kk); a.v10 = F3(f.a1v, j + 1, i, kk);
+    a.v11 = F3(f.a1v, j + 1, i + 1, kk);
+    return a;
+  };
+  auto dsum = [&](const W4& a, int kk, double& uk, double& vk) {     // ucc, vcc
+    const double2 d00 = udvd_nh_ld(g, ib, f, a.u00, a.v00, r00, j, i, kk);
+    const double2 d01 = udvd_nh_ld(g, ib, f, a.u01, a.v01, r01, j, i + 1, kk);
+    const double2 d10 = udvd_nh_ld(g, ib, f, a.u10, a.v10, r10, j + 1, i, kk);
+    const double2 d11 = udvd_nh_ld(g, ib, f, a.u11, a.v11, r11, j + 1, i + 1, kk);
+    uk = d00.x * m00 + d01.x * m01 + d10.x * m10 + d11.x * m11;
+    vk = d00.y * m00 + d01.y * m01 + d10.y * m10 + d11.y * m11;
+  };
+  auto crab = [&](const W4& a) {       // umc, vmc = atm1 u, v * msfd (decouple)
+    const double x = a.u11 * m11 + a.u10 * m10 - a.u01 * m01 - a.u00 * m00;
+    const double y = a.v11 * m11 + a.v01 * m01 - a.v10 * m10 - a.v00 * m00;
+    return x + y;
+  };
+  W4 wa = ld(1);
+  double um, vm;
+  dsum(wa, 1, um, vm);
+  double abm = crab(wa), qm = d_zero;
+  for (int k = 2; k <= kz; k++) {
+    const W4 wb = ld(k);
+    double uk, vk;
+    dsum(wb, k, uk, vk);
+    const double qk = -F3(f.rhof0, j, i, k) * EGRAV_NH * (F3(f.a1w, j, i, k) * rpa) / ps0 -
+                      c->sigma[k] * (dx * (c->twt1[k] * uk + c->twt2[k] * um) +
+                                     dy * (c->twt1[k] * vk + c->twt2[k] * vm));
+    F3(f.qdot, j, i, k) = qk;
+    F3(f.cr, j, i, k - 1) = abm * dummy + (qk - qm) * ps / c->dsigma[k - 1];
+    abm = crab(wb); qm = qk; um = uk; vm = vk;
+  }
+  F3(f.cr, j, i, kz) = abm * dummy + (d_zero - qm) * ps / c->dsigma[kz];
+#else
   double um = ucc(1), vm = vcc(1);
   for (int k = 2; k <= kz; k++) {
     const double uk = ucc(k), vk = vcc(k);
@@ -151,6 +210,7 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
                      F3(f.a1v, j + 1, i, k) * m10 - F3(f.a1v, j, i, k) * m00;
     F3(f.cr, j, i, k) = (a + b) * dummy + (F3(f.qdot, j, i, k + 1) - F3(f.qdot, j, i, k)) * ps / c->dsigma[k];
   }
+#endif
 }
 #endif
 
@@ -683,8 +743,16 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
       ok[n] = q < TDW * TDH && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
       const int jr = ok[n] ? jg : j0c(g), ir = ok[n] ? ig : i0c(g);
       const double m = F2(f.msfd, jr, ir);
+#if NH_UDFORM
+      // ud, vd formed from the atm1 winds loaded for umc, vmc (decouple no longer stores them)
+      const double au = F3(f.a1u, jr, ir, k), av = F3(f.a1v, jr, ir, k);
+      va[n][0] = au * m; va[n][1] = av * m;                                     // umc, vmc
+      const double2 d = udvd_nh_ld(g, c->iboudy, f, au, av, F2(f.rpsda, jr, ir), jr, ir, k);
+      va[n][2] = d.x; va[n][3] = d.y; va[n][4] = F3(f.cr, jr, ir, k);
+#else
       va[n][0] = F3(f.a1u, jr, ir, k) * m; va[n][1] = F3(f.a1v, jr, ir, k) * m;   // umc, vmc
       va[n][2] = F3(f.ud, jr, ir, k); va[n][3] = F3(f.vd, jr, ir, k); va[n][4] = F3(f.cr, jr, ir, k);
+#endif
       va[n][5] = UBD(jr, ir, k); va[n][6] = VBD(jr, ir, k);
       va[n][5] = va[n][5] / m; va[n][6] = va[n][6] / m;     // UM of diffu_d, Main/mod_diffusion.F90:281-411
     }

@@ -100,6 +100,11 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_DPRFORM
 #define NH_DPRFORM 1
 #endif
+// decouple's ud, vd (atm1 u, v * 1/p*dot with the iboudy = 3/4 inflow/outflow rule) formed by
+// their readers, k_nh_omega and k_nh_tend_d's staging, from the atm1 winds they load anyway
+#ifndef NH_UDFORM
+#define NH_UDFORM 1
+#endif
 
 struct QxArgs;
 __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs q);
