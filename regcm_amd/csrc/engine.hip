@@ -1799,7 +1799,7 @@ struct rcmdyn_engine {
       const Geom& g = t.g;
       const NHFields f = nhfields(t);
       const Grids q = grids(g);
-      KLAUNCH(k_nh_coeff_raw, q.cek, BLK, 0, stream, g, dc, f);
+      KLAUNCH(k_nh_coeff_raw, NH_XKCOL ? q.ce1 : q.cek, BLK, 0, stream, g, dc, f);
     });
     // ovl: the exchange is issued in TEND_POST, after k_nh_tend_c went to the second stream
     if (!ovl) xch({{FK::NCR, kz}, {FK::QDOT, kp}, {FK::NXKCR, kz}});
@@ -1860,7 +1860,10 @@ struct rcmdyn_engine {
       KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc, f);
       // tend's time filters (tfuse = 0) with part A of the first acoustic sub-step (sound, :163-718)
-      KLAUNCH(k_nh_tfilter_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc, f);
+      if (NH_A1COL && nh_tfuse)     // part A alone: one column walk per cross column
+        KLAUNCH(k_nh_a1_col, q.ce1, BLK, 0, stream, g, dc, f);
+      else
+        KLAUNCH(k_nh_tfilter_a1, grid3(g.jce2 - g.jce1 + 1, g.ice2 - g.ice1 + 1, kp), BLK, 0, stream, g, dc, f);
     });
     if (nh_tfuse) for (auto& t : tiles) t.tq = 1 - t.tq;     // the filtered t, qv, qc
     // sound, Main/mod_sound.F90:163-718

@@ -225,6 +225,35 @@ __global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
 // calc_coeff NH (Main/mod_diffusion.F90:215-250): Smagorinsky coefficient with the
 // vertical-velocity term, unscaled (xkcr) ...
 #if NH_OTHER_KERNELS
+#if NH_XKCOL
+// one thread per cross frame column walking k = 1..kz: a2w * (1/p*b) of level k+1 is carried to
+// the next level (the point form reads it again from the k+1 plane); the same values
+__global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  const double rpb = F2(f.rpsb, j, i), hg = F2(f.hgfact, j, i);
+  const double r00 = F2(f.rpsdb, j, i), r10 = F2(f.rpsdb, j + 1, i), r01 = F2(f.rpsdb, j, i + 1),
+               r11 = F2(f.rpsdb, j + 1, i + 1);
+  const int kz = c->kz;
+  double wk = F3(f.a2w, j, i, 1) * rpb;
+#pragma unroll 2
+  for (int kk = 1; kk <= kz; kk++) {
+    const double u00 = F3(f.a2u, j, i, kk) * r00, u10 = F3(f.a2u, j + 1, i, kk) * r10,
+                 u01 = F3(f.a2u, j, i + 1, kk) * r01, u11 = F3(f.a2u, j + 1, i + 1, kk) * r11;
+    const double v00 = F3(f.a2v, j, i, kk) * r00, v10 = F3(f.a2v, j + 1, i, kk) * r10,
+                 v01 = F3(f.a2v, j, i + 1, kk) * r01, v11 = F3(f.a2v, j + 1, i + 1, kk) * r11;
+    const double wk1 = F3(f.a2w, j, i, kk + 1) * rpb;
+    const double dudx = u10 + u11 - u00 - u01;
+    const double dvdx = v10 + v11 - v00 - v01;
+    const double dudy = u01 + u11 - u00 - u10;
+    const double dvdy = v01 + v11 - v00 - v10;
+    const double dwdz = wk - wk1;
+    const double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
+    F3(f.xkcr, j, i, kk) = dmin(hg + c->dydc * duv, c->xkhmax);
+    wk = wk1;
+  }
+}
+#else
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
@@ -239,6 +268,7 @@ __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f)
   const double duv = sqrt(dmax((dudx - dvdy) * (dudx - dvdy) + (dvdx + dudy) * (dvdx + dudy) - dwdz * dwdz, d_zero));
   F3(f.xkcr, j, i, k) = dmin(F2(f.hgfact, j, i) + c->dydc * duv, c->xkhmax);
 }
+#endif
 #endif
 
 // ... then scaled by rdxsq and p* (b) by their readers: xkc, xkcf (cross interior, full
@@ -1015,6 +1045,29 @@ __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f
   if (!IN_CE(j, i)) return;
   if (!f.tfuse && k <= c->kz && IN_CI(j, i)) nh_tfilter_at(g, c, f, j, i, k);
   nh_sound_a1_at(g, c, f, j, i, k);
+}
+
+// tfuse: the same part A as one column walk per cross frame column (k_nh_tfilter_a1 with tfuse
+// does nothing else): each level's atm2 pp * (1/p*b) and atm0%pr are loaded once and carried to
+// the levels above and below, where the point form reads them again from the k+-1 planes
+// (the same products and differences, so the same bits)
+__global__ void k_nh_a1_col(Geom g, const Consts* __restrict__ c, NHFields f) {
+  THREAD_POINT(g.jce1, g.ice1);
+  if (!IN_CE(j, i)) return;
+  const int kz = c->kz;
+  const double rpb = F2(f.rpsb, j, i);
+  double pm = F3(f.a2pp, j, i, 1) * rpb, p0 = pm;          // pp at km1 = max(k-1, 1) and k
+  double rm = F3(f.pr0, j, i, 1), r0 = rm;
+#pragma unroll 4
+  for (int kk = 1; kk <= kz; kk++) {
+    const int kp1 = (kz < kk + 1) ? kz : kk + 1;
+    const double pp = F3(f.a2pp, j, i, kp1) * rpb, rp = F3(f.pr0, j, i, kp1);
+    F3(f.cw, j, i, kk) = F3(f.a2w, j, i, kk) * rpb;
+    F3(f.cpp, j, i, kk) = p0;
+    F3(f.cdt, j, i, kk) = (pm - pp) / (rm - rp);
+    pm = p0; p0 = pp; rm = r0; r0 = rp;
+  }
+  F3(f.cw, j, i, kz + 1) = F3(f.a2w, j, i, kz + 1) * rpb;
 }
 
 // NH_DPRFORM: the acoustic u, v update forms dprddx / dprddy from atm0%pr; a host that puts

@@ -105,6 +105,14 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_UDFORM
 #define NH_UDFORM 1
 #endif
+// part A of acoustic sub-step 1 (tfuse) and calc_coeff's xkcr as column walks (one thread per
+// column, k carried in registers) instead of one thread per point and level
+#ifndef NH_A1COL
+#define NH_A1COL 1
+#endif
+#ifndef NH_XKCOL
+#define NH_XKCOL 1
+#endif
 
 struct QxArgs;
 __global__ void k_nh_diffu6(Geom g, const Consts* __restrict__ c, NHFields f, QxArgs q);
@@ -117,6 +125,7 @@ __global__ void k_nh_tend_d(Geom g, const Consts* __restrict__ c, const StepStat
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_negfix_serial(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f);
+__global__ void k_nh_a1_col(Geom g, const Consts* __restrict__ c, NHFields f);
 __global__ void k_nh_check_dprd(Geom g, NHFields f, int* bad);
 __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int fin, int first, int part);
 __global__ void k_nh_sound_bc(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int it);
