@@ -126,7 +126,12 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
 // compute_omega NH (:1157-1191), one thread per cross column: qdot from w and the terrain
 // slopes of the reference p*, then the mass divergence with the qdot term
 #if NH_OTHER_KERNELS
-__global__ void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
+// 256-thread blocks at 3 waves/SIMD: the one-pass form needs 138 VGPRs (under the default
+// 1 024-thread bound it spilled 44 B at 128); C5 321 -> 279 us (profiles/r05/c5_cd_omega_ab.log)
+#ifndef NHOM_W
+#define NHOM_W 3
+#endif
+__global__ __launch_bounds__(256, NHOM_W) void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
   THREAD_POINT(g.jce1, g.ice1);
   if (!IN_CE(j, i)) return;
   const int kz = c->kz;
@@ -1381,7 +1386,12 @@ __global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restri
 // sorts above every finite value, raising the stop).
 // estore is read from the frame ge (the tile frame, or on a decomposed domain the wide frame
 // filled by a 6-deep exchange: the convolution reaches 6 points, clamped to the interior).
-__global__ __launch_bounds__(256) void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est,
+#ifdef NHCD_W
+#define NHCD_LB __launch_bounds__(256, NHCD_W)
+#else
+#define NHCD_LB __launch_bounds__(256)
+#endif
+__global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est,
                                                      const Consts* __restrict__ c, const StepState* __restrict__ s,
                                                      NHFields f, int istep, int last, int nexta) {
   __shared__ double sE[4 + 12][64 + 12];
