@@ -1900,7 +1900,7 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
-        KLAUNCH(k_nh_sound_bc, q.ci1a, BLK, 0, stream, g, dc, ds, f, istep, it);
+        KLAUNCH(k_nh_sound_bc, NH_WRAP ? q.ci1 : q.ci1a, BLK, 0, stream, g, dc, ds, f, istep, it);
       });
       if (cfg.ifupr == 1) {
         if (it == 1 && alarm) {
@@ -1921,10 +1921,10 @@ struct rcmdyn_engine {
         const NHFields f = nhfields(t);
         const Grids q = grids(g);
         if (halo)
-          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD ? q.ci1a : q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
+          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD && !NH_WRAP ? q.ci1a : q.ci1, BLK, 0, stream, g, t.gw, t.westore, dc, ds, f, istep, (int)(it == istep),
                   (int)(it < istep));
         else
-          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD ? q.ci1a : q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep),
+          KLAUNCH(k_nh_sound_cd, NH_ALIGN_CD && !NH_WRAP ? q.ci1a : q.ci1, BLK, 0, stream, g, g, f.estore, dc, ds, f, istep, (int)(it == istep),
                   (int)(it < istep));
       });
     }

@@ -40,6 +40,15 @@ static constexpr double P00 = 1.000000e5;                  // Share/mod_constant
 #define IN_CI(j, i) (in(j, g.jci1, g.jci2) && in(i, g.ici1, g.ici2))
 #define IN_DI(j, i) (in(j, g.jdi1, g.jdi2) && in(i, g.idi1, g.idi2))
 #define IN_DE(j, i) (in(j, g.jde1, g.jde2) && in(i, g.ide1, g.ide2))
+// wrap_j (NH_WRAP): column of lane tx in block column bx over the n columns from j1, the block
+// columns starting on the 128-B line at or below j1; lanes below j1 (block column 0 only) take
+// the columns past the last of the ceil(n/64) block columns
+__device__ __forceinline__ int wrap_j(const Geom& g, int j1, int n, int bx, int tx) {
+  const int ja = j1 - jalign(g, j1);
+  int j = ja + bx * 64 + tx;
+  if (j < j1) j += ((n + 63) / 64) * 64;
+  return j;
+}
 #if NH_ZFIRST
 #define TBX ((int)blockIdx.y)
 #define TBY ((int)blockIdx.z)
@@ -1226,7 +1235,12 @@ __device__ __forceinline__ NhB1 nh_sound_b1_at(const Geom& g, const Consts* c, c
 __global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Consts* __restrict__ c,
                                                              const StepState* __restrict__ s, NHFields f,
                                                              int istep, int it) {
+#if NH_WRAP
+  const int j = wrap_j(g, g.jci1, g.jci2 - g.jci1 + 1, (int)blockIdx.x, (int)threadIdx.x);
+  const int i = g.ici1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+#else
   NH_SOUND_POINT(NH_ALIGN ? ALIGN_J(g.jci1) : g.jci1, g.ici1);
+#endif
   if (!IN_CI(j, i)) return;
   const int kz = c->kz;
   const double dts = s->dt / (double)istep;
@@ -1403,7 +1417,16 @@ __global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict_
 #else
   const Blk3 xb = {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
 #endif
-  const int J0 = (NH_ALIGN_CD ? ALIGN_J(g.jci1) : g.jci1) + xb.x * 64, I0 = g.ici1 + xb.y * 4;
+#if NH_WRAP
+  // block column 0's lanes below jci1 take the row's tail columns (wrap_j): their 13 x 13
+  // neighbourhoods come from a second staged tile, sT2, at the tail
+  const int nci = g.jci2 - g.jci1 + 1, ja = g.jci1 - jalign(g, g.jci1);
+  const int J0 = ja + xb.x * 64, JT = ja + ((nci + 63) / 64) * 64;
+  __shared__ double sT2[4 + 12][16 + 12];
+#else
+  const int J0 = (NH_ALIGN_CD ? ALIGN_J(g.jci1) : g.jci1) + xb.x * 64;
+#endif
+  const int I0 = g.ici1 + xb.y * 4;
   const int tid = threadIdx.y * 64 + threadIdx.x;
   const bool upr = c->ifupr == 1;
   if (upr) {
@@ -1414,10 +1437,30 @@ __global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict_
       in_ = (in_ < ilo) ? ilo : (in_ > ihi ? ihi : in_);
       sE[ii][jj] = est[ge.ix(jn, in_)];
     }
+#if NH_WRAP
+    if (xb.x == 0 && J0 < g.jci1)
+      for (int q = tid; q < 16 * 28; q += 256) {
+        const int jj = q % 28, ii = q / 28;
+        int jn = JT - 6 + jj, in_ = I0 - 6 + ii;
+        jn = (jn < jlo) ? jlo : (jn > jhi ? jhi : jn);
+        jn = (jn < ge.j0 + ge.nj) ? jn : ge.j0 + ge.nj - 1;     // an empty tail: stay in the frame
+        in_ = (in_ < ilo) ? ilo : (in_ > ihi ? ihi : in_);
+        sT2[ii][jj] = est[ge.ix(jn, in_)];
+      }
+#endif
     if (tid < 169) sM[tid] = f.tmask[tid];
     __syncthreads();
   }
+#if NH_WRAP
+  const bool tail = J0 + (int)threadIdx.x < g.jci1;
+  const int j = tail ? JT + (J0 + (int)threadIdx.x - ja) : J0 + (int)threadIdx.x, i = I0 + (int)threadIdx.y;
+  const double* tE = tail ? &sT2[0][0] : &sE[0][0];
+  const int tW = tail ? 28 : 76, tJ = tail ? JT : J0;
+#else
   const int j = J0 + (int)threadIdx.x, i = I0 + (int)threadIdx.y;
+  const double* tE = &sE[0][0];
+  const int tW = 76, tJ = J0;
+#endif
   const bool active = IN_CI(j, i);
   unsigned long long cfl = 0ull;                       // bits of the column's CFL maximum
   if (active) {
@@ -1430,7 +1473,7 @@ __global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict_
         int inn = i + nsi; inn = (inn < ilo) ? ilo : (inn > ihi ? ihi : inn);
         for (int nsj = -6; nsj <= 6; nsj++) {
           int jnn = j + nsj; jnn = (jnn < jlo) ? jlo : (jnn > jhi ? jhi : jnn);
-          wpval = wpval + sE[inn - I0 + 6][jnn - J0 + 6] * sM[(nsj + 6) * 13 + (nsi + 6)];
+          wpval = wpval + tE[(inn - I0 + 6) * tW + (jnn - tJ + 6)] * sM[(nsj + 6) * 13 + (nsi + 6)];
         }
       }
     }

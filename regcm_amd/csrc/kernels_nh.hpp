@@ -84,6 +84,13 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_ALIGN_CD
 #define NH_ALIGN_CD 0
 #endif
+// NH_WRAP: the column kernels k_nh_sound_bc / k_nh_sound_cd on line-aligned block columns
+// without the extra column of waves ALIGN_J adds (wrap_j): the lanes of block column 0 that
+// fall below jci1 take the row's last columns instead, so a row of 768 columns is 12 waves,
+// 11 of them on whole 128-B lines (was 12 misaligned, or 13 aligned)
+#ifndef NH_WRAP
+#define NH_WRAP 1
+#endif
 // acoustic kernels: XCD-aware block placement (xcd_block, devcommon.hpp).  C5, alternating on
 // one box (profiles/r05/rejected/c5_xcd_ab.log): k_nh_sound_bc unchanged, k_nh_sound_cd
 // 884-894 -> 852-882 us, k_nh_sound_uv 519-521 -> 532-542 us, the step unchanged: off
