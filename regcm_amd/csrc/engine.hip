@@ -1881,7 +1881,7 @@ struct rcmdyn_engine {
                     fin, first, 2);
           return;
         }
-        KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1 + (NH_ALIGN ? jalign(g, g.jde1) : 0), g.ide2 - g.ide1 + 1, kz),
+        KLAUNCH(k_nh_sound_uv, grid3(g.jde2 - g.jde1 + 1 + (NH_ALIGN && !NH_WRAP_PT ? jalign(g, g.jde1) : 0), g.ide2 - g.ide1 + 1, kz),
                 BLK, 0, stream, g, dc, ds, nhfields(t), istep, fin, first, part);
       };
       if (halo && !no_overlap) {

@@ -49,6 +49,17 @@ __device__ __forceinline__ int wrap_j(const Geom& g, int j1, int n, int bx, int 
   if (j < j1) j += ((n + 63) / 64) * 64;
   return j;
 }
+// thread -> (j, i, k) over the columns j1..j2 on wrap_j's block columns (64 x 4 blocks, grid3's
+// count of block columns); NH_WRAP_PT = 0: THREAD_POINT from j1
+#if NH_WRAP_PT
+#define WRAP_POINT(j1, j2, i1)                                                        \
+  const int j = wrap_j(g, j1, (j2) - (j1) + 1, (int)blockIdx.x, (int)threadIdx.x);   \
+  const int i = (i1) + (int)(blockIdx.y * blockDim.y + threadIdx.y);                 \
+  const int k = (int)blockIdx.z + 1;                                                  \
+  (void)k;
+#else
+#define WRAP_POINT(j1, j2, i1) THREAD_POINT(j1, i1)
+#endif
 #if NH_ZFIRST
 #define TBX ((int)blockIdx.y)
 #define TBY ((int)blockIdx.z)
@@ -141,7 +152,7 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
 #define NHOM_W 3
 #endif
 __global__ __launch_bounds__(256, NHOM_W) void k_nh_omega(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jce1, g.ice1);
+  WRAP_POINT(g.jce1, g.jce2, g.ice1);
   if (!IN_CE(j, i)) return;
   const int kz = c->kz;
   const double dummy = d_one / (c->dx2 * F2(f.msfx, j, i) * F2(f.msfx, j, i));
@@ -243,7 +254,7 @@ __global__ __launch_bounds__(256, NHOM_W) void k_nh_omega(Geom g, const Consts* 
 // one thread per cross frame column walking k = 1..kz: a2w * (1/p*b) of level k+1 is carried to
 // the next level (the point form reads it again from the k+1 plane); the same values
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jce1, g.ice1);
+  WRAP_POINT(g.jce1, g.jce2, g.ice1);
   if (!IN_CE(j, i)) return;
   const double rpb = F2(f.rpsb, j, i), hg = F2(f.hgfact, j, i);
   const double r00 = F2(f.rpsdb, j, i), r10 = F2(f.rpsdb, j + 1, i), r01 = F2(f.rpsdb, j, i + 1),
@@ -269,7 +280,7 @@ __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f)
 }
 #else
 __global__ void k_nh_coeff_raw(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jce1, g.ice1);
+  WRAP_POINT(g.jce1, g.jce2, g.ice1);
   if (!IN_CE(j, i)) return;
   const double u00 = UBD(j, i, k), u10 = UBD(j + 1, i, k), u01 = UBD(j, i + 1, k), u11 = UBD(j + 1, i + 1, k);
   const double v00 = VBD(j, i, k), v10 = VBD(j + 1, i, k), v01 = VBD(j, i + 1, k), v11 = VBD(j + 1, i + 1, k);
@@ -962,7 +973,7 @@ __device__ __forceinline__ double nh_negfix_sum(const Geom& g, const double* sv,
   return 0.01 * sum / 9.0;
 }
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jci1, g.ici1);
+  WRAP_POINT(g.jci1, g.jci2, g.ici1);
   if (!IN_CI(j, i)) return;
   for (int n = 0; n < 2; n++) {
     const double* sv = n ? f.cqc : f.cqv;
@@ -1066,7 +1077,7 @@ __global__ void k_nh_tfilter_a1(Geom g, const Consts* __restrict__ c, NHFields f
 // the levels above and below, where the point form reads them again from the k+-1 planes
 // (the same products and differences, so the same bits)
 __global__ void k_nh_a1_col(Geom g, const Consts* __restrict__ c, NHFields f) {
-  THREAD_POINT(g.jce1, g.ice1);
+  WRAP_POINT(g.jce1, g.jce2, g.ice1);
   if (!IN_CE(j, i)) return;
   const int kz = c->kz;
   const double rpb = F2(f.rpsb, j, i);
@@ -1167,7 +1178,11 @@ __global__ void k_nh_sound_uv(Geom g, const Consts* __restrict__ c, const StepSt
     nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
     return;
   }
+#if NH_WRAP_PT
+  WRAP_POINT(g.jde1, g.jde2, g.ide1);
+#else
   NH_SOUND_POINT(NH_ALIGN ? ALIGN_J(g.jde1) : g.jde1, g.ide1);
+#endif
   if (part == 1 && nh_uv_strip(g, j, i)) return;
   nh_sound_uv_at(g, c, s, f, istep, fin, first, j, i, k);
 }

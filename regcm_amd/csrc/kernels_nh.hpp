@@ -91,6 +91,11 @@ constexpr int NH_CFL_SLOTS = 1024;
 #ifndef NH_WRAP
 #define NH_WRAP 1
 #endif
+// the same line-aligned columns for the NH point and column kernels that start at jce1, jci1 or
+// jde1 (k_nh_sound_uv, k_nh_omega, k_nh_coeff_raw, k_nh_a1_col, k_nh_negfix)
+#ifndef NH_WRAP_PT
+#define NH_WRAP_PT 1
+#endif
 // acoustic kernels: XCD-aware block placement (xcd_block, devcommon.hpp).  C5, alternating on
 // one box (profiles/r05/rejected/c5_xcd_ab.log): k_nh_sound_bc unchanged, k_nh_sound_cd
 // 884-894 -> 852-882 us, k_nh_sound_uv 519-521 -> 532-542 us, the step unchanged: off
