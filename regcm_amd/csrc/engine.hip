@@ -571,13 +571,11 @@ struct rcmdyn_engine {
   void setup_nh(Tile& t) {
     const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
     NHFields f{};
-    for (double** p : {&f.a1pp, &f.a2pp, &f.ud, &f.vd,
-                       &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.tdyn, &f.qvdyn, &f.qcdyn, &f.udyn, &f.vdyn,
-                       &f.ppten, &f.ppdyn, &f.ct, &f.cu, &f.cv, &f.cpp, &f.cdt, &f.se, &f.sf, &f.saa, &f.sb,
-                       &f.sc, &f.rhs, &f.sca, &f.sg1, &f.sg2, &f.ptend, &f.pxup, &f.pyvp, &f.tk, &f.scc, &f.scdd,
-                       &f.scj, &f.spi, &f.th})
+    for (double** p : {&f.a1pp, &f.a2pp, &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.ppten, &f.ct, &f.cu, &f.cv,
+                       &f.cpp, &f.cdt, &f.se, &f.sf, &f.spi, &f.th})
       *p = dalloc(t, P3);
-    for (double** p : {&f.a1w, &f.a2w, &f.wten, &f.wdyn, &f.cw, &f.wo})
+    if (!NH_UDFORM) { f.ud = dalloc(t, P3); f.vd = dalloc(t, P3); }
+    for (double** p : {&f.a1w, &f.a2w, &f.wten, &f.cw})
       *p = dalloc(t, P4);
     f.ppb0 = dalloc(t, P3); f.ppbt = dalloc(t, P3); f.wwb0 = dalloc(t, P4); f.wwbt = dalloc(t, P4);
     f.pr0 = dalloc(t, P3); f.t0 = dalloc(t, P3); f.rho0 = dalloc(t, P3); f.z0 = dalloc(t, P3);

@@ -26,10 +26,10 @@ struct NHFields {
   double *ud, *vd, *pr1, *rho1, *xpr;
   double *th;                    // potential temperature atmx%t*(p00/atm1%pr)**rovcp (ithadv = 1)
   double *cr, *qdot;
-  double *xkcr, *uavg1, *uavg2, *vavg1, *vavg2;
-  // tendencies: total (pc_total) and dynamic (pc_dynamic)
-  double *tten, *tdyn, *qvten, *qvdyn, *qcten, *qcdyn, *uten, *udyn, *vten, *vdyn;
-  double *ppten, *ppdyn, *wten, *wdyn;
+  double *xkcr;
+  // total tendencies (pc_total; pc_dynamic stays in the tendency kernels' registers)
+  double *tten, *qvten, *qcten, *uten, *vten;
+  double *ppten, *wten;
   // physics tendencies of the coupling seam (null: physics stubbed, the terms are 0)
   const double *tphy, *qvphy, *qcphy, *uphy, *vphy, *ppphy, *wphy;
   // semi-Lagrangian qv/qc tendency starts (isladvec = 1, k_sladv; null otherwise)
@@ -41,9 +41,9 @@ struct NHFields {
   // forecasts (atmc) and fixed moisture
   double *ct, *cqv, *cqc, *fqv, *fqc, *cu, *cv, *cpp, *cw, *cdt;
   unsigned* depplane;
-  // sound work (Main/mod_sound.F90:40-60)
-  double *wo, *se, *sf, *saa, *sb, *sc, *rhs, *sca, *sg1, *sg2, *ptend, *pxup, *pyvp, *tk;
-  double *scc, *scdd, *scj, *spi, *estore, *astore, *tmask;
+  // sound work (Main/mod_sound.F90:40-60) that crosses a kernel boundary: the sweep's e, f
+  // (k_nh_sound_bc -> k_nh_sound_cd), pi, the radiative condition's inputs and mask
+  double *se, *sf, *spi, *estore, *astore, *tmask;
   unsigned long long* cfl;       // NH_CFL_SLOTS partial maxima of the step's CFL (non-negative
                                  // doubles as ordered bits), reduced by k_nh_advance
   unsigned long long* cfll;      // the same for the last acoustic sub-step alone (the value
