@@ -1261,7 +1261,6 @@ __global__ __launch_bounds__(256, NHBC_W) void k_nh_sound_bc(Geom g, const Const
   const double dts = s->dt / (double)istep;
   const double msfx = F2(f.msfx, j, i), ps0 = F2(f.ps0, j, i), rpb = F2(f.rpsb, j, i);
   const double m[4] = {F2(f.msfd, j, i), F2(f.msfd, j + 1, i), F2(f.msfd, j, i + 1), F2(f.msfd, j + 1, i + 1)};
-
   const double bet = c->nhbet, bp = (d_one + bet) * d_half, bm = (d_one - bet) * d_half;
   const double bpxbp = bp * bp, bpxbm = bp * bm;
   const double* w = f.cw;                       // still the old w (wo) on levels 1..kz+1
