@@ -1927,7 +1927,8 @@ struct rcmdyn_engine {
       });
     }
     each([&](Tile& t) {
-      KLAUNCH(k_nh_sound_final, grids(t.g).fr, BLK, 0, stream, t.g, dc, nhfields(t));
+      KLAUNCH(k_nh_sound_final, dim3((nh_frame_ring(t.g) + 255) / 256, kz + 1), dim3(256), 0, stream, t.g, dc,
+              nhfields(t));
     });
     KLAUNCH(k_nh_advance, dim3(1), dim3(256), 0, stream, dc, ds, nhf[0]);
     hs.lcount += 1;

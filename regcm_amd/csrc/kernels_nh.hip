@@ -1592,10 +1592,28 @@ __global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict_
 // sub-step's k_nh_sound_uv filters u, v and its k_nh_sound_cd pp and w on the interior; what
 // remains is the small-value clamp of w (the acoustic w, atm1/atm2 w) on the other frame
 // points.  k = 1..kz+1.
+// The frame points outside the interior as a list (nh_frame_ring: the rows below and above the
+// interior over the frame's width, then the columns left and right of it), blockIdx.y = k - 1:
+// a whole-frame grid spent 39 us at C5 on threads that return at once.
+int nh_frame_ring(const Geom& g) {
+  return (g.ici1 - g.i0 + g.i0 + g.ni - 1 - g.ici2) * g.nj + (g.ici2 - g.ici1 + 1) * (g.jci1 - g.j0 + g.j0 + g.nj - 1 - g.jci2);
+}
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f) {
-  FRAME_POINT();
   (void)c;
-  if (IN_CI(j, i)) return;
+  const int W = g.nj, wl = g.jci1 - g.j0, wr = g.j0 + g.nj - 1 - g.jci2;
+  const int hb = g.ici1 - g.i0, ht = g.i0 + g.ni - 1 - g.ici2, hm = g.ici2 - g.ici1 + 1;
+  int q = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int k = (int)blockIdx.y + 1;
+  int j, i;
+  if (q < hb * W) { i = g.i0 + q / W; j = g.j0 + q % W; }
+  else if ((q -= hb * W) < ht * W) { i = g.ici2 + 1 + q / W; j = g.j0 + q % W; }
+  else if ((q -= ht * W) < hm * (wl + wr)) {
+    const int m = q % (wl + wr);
+    i = g.ici1 + q / (wl + wr);
+    j = m < wl ? g.j0 + m : g.jci2 + 1 + (m - wl);
+  } else {
+    return;
+  }
   double w = F3(f.cw, j, i, k);
   if (fabs(w) < DLOWVAL) w = d_zero;
   F3(f.cw, j, i, k) = w;

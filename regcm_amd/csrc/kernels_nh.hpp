@@ -145,6 +145,7 @@ __global__ void k_nh_tmask_gather(Geom g, const Consts* __restrict__ c, NHFields
 __global__ void k_nh_tmask(Geom g, const Consts* __restrict__ c, const double* __restrict__ gbuf, double* tmask);
 __global__ void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict__ est, const Consts* __restrict__ c, const StepState* __restrict__ s, NHFields f, int istep, int last, int nexta);
 __global__ void k_nh_sound_final(Geom g, const Consts* __restrict__ c, NHFields f);
+int nh_frame_ring(const Geom& g);     // k_nh_sound_final's points per level
 __global__ void k_nh_advance(const Consts* __restrict__ c, StepState* s, NHFields f);
 __global__ void k_nh_bdyval(Geom g, int kz, const StepState* __restrict__ s, NHFields f);
 __global__ void k_nh_bdyval_w1(Geom g, NHFields f);
