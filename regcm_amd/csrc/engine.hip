@@ -571,10 +571,15 @@ struct rcmdyn_engine {
   void setup_nh(Tile& t) {
     const size_t P = t.g.plane, P3 = P * cfg.kz, P4 = P * (cfg.kz + 1);
     NHFields f{};
-    for (double** p : {&f.a1pp, &f.a2pp, &f.pr1, &f.rho1, &f.xpr, &f.cr, &f.xkcr, &f.ppten, &f.ct, &f.cu, &f.cv,
+    for (double** p : {&f.a1pp, &f.a2pp, &f.pr1, &f.rho1, &f.cr, &f.xkcr, &f.ppten, &f.ct, &f.cu, &f.cv,
                        &f.cpp, &f.cdt, &f.se, &f.sf, &f.spi, &f.th})
       *p = dalloc(t, P3);
+    if (!NH_XPRFORM) f.xpr = dalloc(t, P3);
     if (!NH_UDFORM) { f.ud = dalloc(t, P3); f.vd = dalloc(t, P3); }
+    if (NH_NEGLIST) {             // every interior point of both species at most once
+      f.neglist = talloc<unsigned>(t, 2 * P3);
+      f.negcnt = talloc<int>(t, 1);
+    }
     for (double** p : {&f.a1w, &f.a2w, &f.wten, &f.cw})
       *p = dalloc(t, P4);
     f.ppb0 = dalloc(t, P3); f.ppbt = dalloc(t, P3); f.wwb0 = dalloc(t, P4); f.wwbt = dalloc(t, P4);
@@ -1855,7 +1860,10 @@ struct rcmdyn_engine {
         KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
                 qx_args(t));
       }
-      KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
+      if (NH_NEGLIST)
+        KLAUNCH(k_nh_negfix, dim3(1024), dim3(256), 0, stream, g, dc, f);
+      else
+        KLAUNCH(k_nh_negfix, q.cik, BLK, 0, stream, g, dc, f);
       KLAUNCH(k_nh_negfix_serial, dim3(2 * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc, f);
       // tend's time filters (tfuse = 0) with part A of the first acoustic sub-step (sound, :163-718)
       if (NH_A1COL && nh_tfuse)     // part A alone: one column walk per cross column

@@ -130,6 +130,9 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   if (!(in(j, g.jce1ga, g.jce2ga) && in(i, g.ice1ga, g.ice2ga))) return;
   const double rp = F2(f.rpsa, j, i);
   if (k > kz) return;
+#if NH_NEGLIST
+  if (j == g.jce1 && i == g.ice1 && k == 1) *f.negcnt = 0;      // k_nh_tend_c lists after this
+#endif
   const double xt = F3(f.a1t, j, i, k) * rp;
   const double xqv = dmax(F3(f.a1qv, j, i, k) * rp, MINQQ);
   const double xtv = xt * (d_one + c->ep1 * xqv);
@@ -138,8 +141,10 @@ __global__ void k_nh_decouple(Geom g, const Consts* __restrict__ c, NHFields f) 
   F3(f.pr1, j, i, k) = pr1;      // atmx t, tv, qv, qc, pp, w: formed by their readers
   F3(f.rho1, j, i, k) = pr1 / (c->rgas * xtv);
   F3(f.th, j, i, k) = xt * rcm_powpos(P00 / pr1, c->rovcp);
+#if !NH_XPRFORM
   if (IN_CI(j, i))
     F3(f.xpr, j, i, k) = (xtv - F3(f.t0, j, i, k) - xpp / (c->cpd * F3(f.rho0, j, i, k))) / xt;
+#endif
 }
 #endif
 
@@ -638,8 +643,21 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
                            (c->dsigma[k - 1] * F3(f.rho1, j, i, k) + c->dsigma[k] * F3(f.rho1, j, i, k - 1));
       const double uaq = d_rfour * (c->twt1[k] * uk + c->twt2[k] * um);
       const double vaq = d_rfour * (c->twt1[k] * vk + c->twt2[k] * vm);
+#if NH_XPRFORM
+      // decouple's atmx%pr (:1040-1048) at k and k-1, formed here as decouple formed it
+      auto xprat = [&](int kk) {
+        const double xt = F3(f.a1t, j, i, kk) * r0;
+        const double xqv = dmax(F3(f.a1qv, j, i, kk) * r0, MINQQ);
+        const double xtv = xt * (d_one + c->ep1 * xqv);
+        const double xpp = F3(f.a1pp, j, i, kk) * r0;
+        return (xtv - F3(f.t0, j, i, kk) - xpp / (c->cpd * F3(f.rho0, j, i, kk))) / xt;
+      };
+      const double xprm = xprat(k - 1), xprk = xprat(k);
+#else
+      const double xprm = F3(f.xpr, j, i, k - 1), xprk = F3(f.xpr, j, i, k);
+#endif
       wd = wd +
-          (c->twt2[k] * F3(f.xpr, j, i, k - 1) + c->twt1[k] * F3(f.xpr, j, i, k)) * rofac * EGRAV_NH * ps +
+          (c->twt2[k] * xprm + c->twt1[k] * xprk) * rofac * EGRAV_NH * ps +
           ex * (uaq * crx - vaq * cry) + (uaq * uaq + vaq * vaq) * REARTHRAD * rps +
           (F3(f.a1w, j, i, k) * r0) * (c->twt1[k] * F3(f.cr, j, i, k) + c->twt2[k] * F3(f.cr, j, i, k - 1));
       wd = wd - EGRAV_NH * ps * (c->twt2[k] * xqload(k - 1) + c->twt1[k] * xqload(k));
@@ -740,6 +758,9 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     F3(f.cqv, j, i, k) = cq;
     if (f.tfuse && !(cq < d_zero))      // a negative forecast: filtered after its fix
       nh_raw_qv(c, F3(f.a1qv, j, i, k), o2, cq, ps, pbs, F3(f.b1qv, j, i, k), F3(f.b2qv, j, i, k));
+#if NH_NEGLIST
+    if (cq < d_zero) f.neglist[atomicAdd(f.negcnt, 1)] = (unsigned)(((long)(k - 1) * g.plane + g.ix(j, i)) * 2);
+#endif
   }
   // ================= qc: hadvqx (or the semi-Lagrangian start), vadv4d ind = 1, adiabatic,
   // diffusion, forecast
@@ -767,6 +788,9 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     F3(f.cqc, j, i, k) = cq;
     if (f.tfuse && !(cq < d_zero))
       nh_raw_qc(c, F3(f.a1qc, j, i, k), o2, cq, F3(f.b1qc, j, i, k), F3(f.b2qc, j, i, k));
+#if NH_NEGLIST
+    if (cq < d_zero) f.neglist[atomicAdd(f.negcnt, 1)] = (unsigned)(((long)(k - 1) * g.plane + g.ix(j, i)) * 2 + 1);
+#endif
   }
 }
 
@@ -972,23 +996,43 @@ __device__ __forceinline__ double nh_negfix_sum(const Geom& g, const double* sv,
     }
   return 0.01 * sum / 9.0;
 }
+// one negative forecast (species n) at an interior point: fixed in parallel when no sweep
+// predecessor is negative, else its plane's row is marked for the serial sweep
+__device__ __forceinline__ void nh_negfix_at(const Geom& g, const Consts* c, const NHFields& f, int n, int j, int i,
+                                             int k) {
+  const double* sv = n ? f.cqc : f.cqv;
+  double* fx = n ? f.fqc : f.fqv;
+  if (negfix_dependent(g, sv, j, i, k)) {
+    negfix_mark(g, f.depplane, n * c->kz + (k - 1), i);
+  } else {
+    const double v = nh_negfix_sum(g, sv, fx, j, i, k, false);
+    F3(fx, j, i, k) = v;
+    if (f.tfuse) nh_filter_q_to(g, c, f, n, j, i, k, v);
+  }
+}
+#if NH_NEGLIST
+// NH_NEGLIST: the entries k_nh_tend_c listed, grid-stride (the list is unordered; every entry is
+// an independent point, as in the point form below)
+__global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
+  const int cnt = *f.negcnt;
+  for (int e = (int)(blockIdx.x * blockDim.x + threadIdx.x); e < cnt; e += (int)(gridDim.x * blockDim.x)) {
+    const unsigned w = f.neglist[e];
+    const int n = (int)(w & 1u);
+    const long el = (long)(w >> 1);
+    const int k = (int)(el / g.plane) + 1;
+    const long r = el % g.plane;
+    const int i = g.i0 + (int)(r / g.pitch), j = g.j0 + (int)(r % g.pitch);
+    nh_negfix_at(g, c, f, n, j, i, k);
+  }
+}
+#else
 __global__ void k_nh_negfix(Geom g, const Consts* __restrict__ c, NHFields f) {
   WRAP_POINT(g.jci1, g.jci2, g.ici1);
   if (!IN_CI(j, i)) return;
-  for (int n = 0; n < 2; n++) {
-    const double* sv = n ? f.cqc : f.cqv;
-    double* fx = n ? f.fqc : f.fqv;
-    if (F3(sv, j, i, k) < d_zero) {
-      if (negfix_dependent(g, sv, j, i, k)) {
-        negfix_mark(g, f.depplane, n * c->kz + (k - 1), i);
-      } else {
-        const double v = nh_negfix_sum(g, sv, fx, j, i, k, false);
-        F3(fx, j, i, k) = v;
-        if (f.tfuse) nh_filter_q_to(g, c, f, n, j, i, k, v);
-      }
-    }
-  }
+  for (int n = 0; n < 2; n++)
+    if (F3(n ? f.cqc : f.cqv, j, i, k) < d_zero) nh_negfix_at(g, c, f, n, j, i, k);
 }
+#endif
 
 // one 64-lane block per (n, k) plane: the marked rows swept in the reference order
 // (negfix_sweep, qxcommon.hpp; dynamic LDS negfix_lds(g))

@@ -56,6 +56,10 @@ struct NHFields {
   // in k_nh_tfilter_a1
   double *b1t, *b1qv, *b1qc, *b2t, *b2qv, *b2qc;
   int tfuse;
+  // NH_NEGLIST: k_nh_tend_c lists its negative qv/qc forecasts (entry (k-1)*plane + ix, times 2,
+  // plus the species bit) for k_nh_negfix, which visits the list instead of every point
+  unsigned* neglist;
+  int* negcnt;
 };
 constexpr int NH_CFL_SLOTS = 1024;
 // block order of the NH tendency kernels: NH_ZFIRST = 1 launches them as (levels, tiles_j,
@@ -95,6 +99,14 @@ constexpr int NH_CFL_SLOTS = 1024;
 // jde1 (k_nh_sound_uv, k_nh_omega, k_nh_coeff_raw, k_nh_a1_col, k_nh_negfix)
 #ifndef NH_WRAP_PT
 #define NH_WRAP_PT 1
+#endif
+#ifndef NH_NEGLIST
+#define NH_NEGLIST 1
+#endif
+// k_nh_tend_c forms decouple's buoyancy helper atmx%pr (xpr) at k and k-1 from the operands it
+// loads (decouple stops storing it, and reading t0, rho0 for it)
+#ifndef NH_XPRFORM
+#define NH_XPRFORM 1
 #endif
 // acoustic kernels: XCD-aware block placement (xcd_block, devcommon.hpp).  C5, alternating on
 // one box (profiles/r05/rejected/c5_xcd_ab.log): k_nh_sound_bc unchanged, k_nh_sound_cd
