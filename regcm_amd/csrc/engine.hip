@@ -315,6 +315,12 @@ struct rcmdyn_engine {
   const bool no_defer_corr = std::getenv("RCMDYN_NO_DEFER_CORR") != nullptr;
   bool defer_corr = false;    // set by tend_call / post_physics around the tend they run
   bool corr_pending = false;  // the last tend's corrections are not launched yet
+  // lazy tend (drop-in pair): rcmdyn_tend does the host bookkeeping and leaves the launch to
+  // the next call: rcmdyn_bdyval replays the one-step graph of tend + bdyval (rcmdyn_step's),
+  // any other call (settle) replays tend's own graph first.  RCMDYN_NO_LAZY_TEND=1: off
+  const bool lazy_tend = std::getenv("RCMDYN_NO_LAZY_TEND") == nullptr;
+  bool tend_pending = false;
+  int lazy_par = 0;
   // the hydrostatic step without k_qfilter (its work in k_columns, k_scalars and the extra
   // blocks of k_split_project / k_split_correct); RCMDYN_NO_QFUSE=1 launches k_qfilter
   const bool no_qfuse = [] {
@@ -2287,6 +2293,11 @@ struct rcmdyn_engine {
   }
   // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
   void settle() {
+    if (tend_pending) {              // the lazy tend's own graph (captured with deferred corrections)
+      tend_pending = false;
+      HIPCHK(hipGraphLaunch(gtend[lazy_par], stream));
+      corr_pending = true;
+    }
     if (!corr_pending) return;
     launch_corrections(false);     // if this throws, the corrections stay pending for the next call
     corr_pending = false;
@@ -2461,6 +2472,17 @@ struct rcmdyn_engine {
     try {
       if (graph_ok()) {
         if (!gtend[par]) capture(par, 1);
+        if (lazy_tend && defer_corr && !ghosts_stale) {
+          if (!gexec[par]) {
+            defer_corr = false;          // the step graph runs tend with its corrections
+            capture(par, 3);
+          }
+          defer_corr = false;
+          tend_pending = true;
+          lazy_par = par;
+          replayed_tend();               // the clock and parities as after the launch
+          return;                        // note_step: at the launch
+        }
         HIPCHK(hipGraphLaunch(gtend[par], stream));
         replayed_tend();
         corr_pending = defer_corr;
@@ -2476,6 +2498,13 @@ struct rcmdyn_engine {
   }
   void bdyval_call() {
     prepare();
+    if (tend_pending) {              // the lazy tend and this bdyval: one step graph
+      tend_pending = false;
+      HIPCHK(hipGraphLaunch(gexec[lazy_par], stream));
+      replayed_bdyval();
+      note_step(hs.lcount);
+      return;
+    }
     const int par = gpar();
     if (corr_pending) {
       if (graph_ok() && !ghosts_stale) {
@@ -2870,6 +2899,7 @@ int rcmdyn_last_step_ms(rcmdyn_t* h, double* ms) { return guard(h, [&] { *ms = h
 
 int rcmdyn_set_diagnostics(rcmdyn_t* h, int32_t on) {
   return guard(h, [&] {
+    h->settle();                                     // a lazy tend replays its graph first
     HIPCHK(hipStreamSynchronize(h->stream));
     if (h->diag != (on != 0)) {
       h->diag = (on != 0);

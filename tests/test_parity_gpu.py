@@ -374,40 +374,51 @@ def test_fused_bdyval_equals_separate(c1_data, monkeypatch, variant, nproc):
 
 @pytest.mark.parametrize("nproc", [(1, 1), (2, 2)], ids=str)
 def test_deferred_corrections_any_call_order(c1_data, monkeypatch, nproc):
-    """rcmdyn_tend leaves its split corrections to the next rcmdyn_bdyval (launched with the
-    boundary lines, rcmdyn_step's k_split_correct_bdy); a get, a put or a synchronize in
-    between launches them first.  Every order is bit-identical to rcmdyn_step and to tend
-    launching them itself (RCMDYN_NO_DEFER_CORR)."""
+    """rcmdyn_tend leaves its launch to the next call (lazy tend: rcmdyn_bdyval replays
+    rcmdyn_step's one-step graph) and, when launched alone, its split corrections to the next
+    rcmdyn_bdyval (launched with the boundary lines, rcmdyn_step's k_split_correct_bdy); a get,
+    a put, a synchronize or a reductions call in between launches them first.  Every order is
+    bit-identical to rcmdyn_step, to tend launching its own graph at once
+    (RCMDYN_NO_LAZY_TEND) and to tend launching its corrections itself
+    (RCMDYN_NO_DEFER_CORR), and the clock a host reads after tend is the same either way."""
     from regcm_amd.dycore import DynCore
     rc, data = c1_data
     st = with_species(rc, data["state"])
     mk = lambda: DynCore(rc, data["split"], nproc_j=nproc[0], nproc_i=nproc[1])
     ref, a, b = mk(), mk(), mk()
+    monkeypatch.setenv("RCMDYN_NO_LAZY_TEND", "1")
+    d = mk()                           # tend launches its own graph at once
     monkeypatch.setenv("RCMDYN_NO_DEFER_CORR", "1")
     c = mk()
-    for e in (ref, a, b, c):
+    for e in (ref, a, b, c, d):
         e.put_state(st)
         e.bdyval()
-    ref.step(6)
-    for n in range(6):
+    ref.step(8)
+    for n in range(8):
         a.tend()
         a.bdyval()
         b.tend()
-        if n % 3 == 0:
-            b.get("ATM1_T")            # settles the corrections before bdyval
-        elif n % 3 == 1:
+        t_mid = b.get_time()           # the clock after tend, before any launch
+        if n % 4 == 0:
+            b.get("ATM1_T")            # settles the lazy tend and its corrections before bdyval
+        elif n % 4 == 1:
             b.synchronize()
-        else:
+        elif n % 4 == 2:
             b.put("ATM1_QV", b.get("ATM1_QV"))
+        else:
+            b.reductions()
+        assert b.get_time() == t_mid
         b.bdyval()
-        c.tend()
-        c.bdyval()
+        for e in (c, d):
+            e.tend()
+            e.bdyval()
     for name in STATE_FIELDS:
         r = ref.get(name)
-        for e in (a, b, c):
+        for e in (a, b, c, d):
             assert np.array_equal(e.get(name), r), name
-    assert a.get_time() == ref.get_time() == b.get_time() == c.get_time()
+    assert a.get_time() == ref.get_time() == b.get_time() == c.get_time() == d.get_time()
     assert np.array_equal(a.reductions(), ref.reductions())
+    assert np.array_equal(d.reductions(), ref.reductions())
 
 
 def _dependent_negatives(cq, rc):
