@@ -274,3 +274,32 @@ def test_nh_idiffu3_tiles(nh_data, nthreads):
         for name in NH_FIELDS:
             err = relerr(e.get(name), o.get(name), rcv, name)
             assert err < tol, (name, err, nsteps)
+
+
+def test_nh_negative_moisture_list(nh_data):
+    """Clusters of negative NH qc forecasts: k_nh_tend_c lists them, k_nh_negfix fixes the
+    independent ones from the list and the serial sweep the dependent ones, reproducing the
+    reference's order-dependent fix (Main/mod_tendency.F90:382-393) bit for bit."""
+    from oracle.oracle import OracleCore
+    from regcm_amd.dycore import DynCore
+    from tests.test_parity_gpu import _dependent_negatives
+    rc, data = nh_data
+    st = {k: v.copy() for k, v in data["state"].items()}
+    rng = np.random.default_rng(11)
+    ps = st["PSA"][0]
+    pat = rng.uniform(0.0, 2.0e-5, size=st["ATM1_QC"].shape) * (rng.uniform(size=st["ATM1_QC"].shape) < 0.5)
+    st["ATM1_QC"] = pat * ps[None]
+    st["ATM2_QC"] = np.zeros_like(pat)
+    o = OracleCore(rc, data["split"])
+    e = DynCore(rc, data["split"])
+    e.set_diagnostics(True)
+    for c in (o, e):
+        c.put_state(st)
+        c.bdyval()
+        c.tend()
+    dt = o.get_time()[1]
+    assert _dependent_negatives(dt * o.get("QCTEN"), rc) > 0
+    assert int((dt * o.get("QCTEN")[:, 1:rc.iy - 2, 1:rc.jx - 2] < 0).sum()) > 1000
+    for name in ("ATM1_QC", "ATM2_QC", "QCTEN"):
+        a, b = e.get(name), o.get(name)
+        assert np.array_equal(a[:, 1:rc.iy - 2, 1:rc.jx - 2], b[:, 1:rc.iy - 2, 1:rc.jx - 2]), name
