@@ -328,6 +328,9 @@ struct rcmdyn_engine {
     return v && *v && std::strcmp(v, "0") != 0;
   }();
   bool qfuse() const { return cfg.idynamic != 2 && !no_qfuse; }
+  // nqx = 5, hydrostatic qfuse: the species' serial fix joins the qv / qc one after the split
+  // corrections (k_negfix_serial_qx)
+  bool serial_with_corr() const { return NEGFIX_POST && qfuse() && hc.nsp > 0; }
   // halo/compute overlap of the hydrostatic prologue exchange (Part, kernels.hpp) on a
   // decomposed domain; RCMDYN_NO_OVERLAP=1: the atm1/p* part first, then the atm2 part beside
   // k_columns only
@@ -517,7 +520,10 @@ struct rcmdyn_engine {
       if (cfg.isladvec == 1) t.slqx[n] = dalloc(t, P3);
       if (cfg.idiffu == 3) t.d6qx[n] = dalloc(t, P * (kz + 1));
     }
-    if (hc.nsp) t.depx = talloc<unsigned>(t, (size_t)hc.nsp * kz * negfix_rowwords(g));
+    if (hc.nsp) {
+      t.depx = talloc<unsigned>(t, (size_t)hc.nsp * kz * negfix_rowwords(g));
+      t.depxf = talloc<unsigned>(t, (size_t)hc.nsp * kz * (g.ici2 - g.ici1 + 1));
+    }
     t.depplane = talloc<unsigned>(t, 2 * (size_t)kz * negfix_rowwords(g));
     if (cfg.idynamic != 2) {
       t.negcnt = talloc<int>(t, 1);
@@ -1712,8 +1718,8 @@ struct rcmdyn_engine {
 
   // the hydrometeors beyond qc (nqx = 5) for the current parity: a* current, b* next (the
   // hydrostatic ping-pong; the NH core updates a* in place)
-  QxArgs qx_args(Tile& t) {
-    const int c = t.cur, n1 = 1 - c;
+  QxArgs qx_args(Tile& t, int par = -1) {
+    const int c = par < 0 ? t.cur : par, n1 = 1 - c;
     QxArgs q{};
     q.nsp = hc.nsp;
     for (int n = 0; n < hc.nsp; n++) {
@@ -1723,6 +1729,7 @@ struct rcmdyn_engine {
       q.cq[n] = t.cqx[n]; q.fq[n] = t.fqx[n]; q.sl[n] = t.slqx[n]; q.d6[n] = t.d6qx[n]; q.phy[n] = t.phyx[n];
     }
     q.dep = t.depx;
+    q.depf = t.depxf;
     return q;
   }
   // the XField entries of the hydrometeors beyond qc for one kind (A1QX0 ..), width w
@@ -1865,6 +1872,9 @@ struct rcmdyn_engine {
                 qx_args(t));      // the column box, as the hydrostatic launch: its jci x ici fix
         KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
                 qx_args(t));
+        if (NEGFIX_POST)
+          KLAUNCH(k_qx_post, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, hc.nsp * kz), BLK, 0, stream, g, dc,
+                  qx_args(t));
       }
       if (NH_NEGLIST)
         KLAUNCH(k_nh_negfix, dim3(1024), dim3(256), 0, stream, g, dc, f);
@@ -2166,8 +2176,12 @@ struct rcmdyn_engine {
         const Geom& g = t.g;
         KLAUNCH(k_qx_fix, grid3(g.jdx2() - g.jdx1() + 1, g.idx2() - g.idx1() + 1, kz), BLK, 0, stream, g, dc,
                 qx_args(t));
+        if (serial_with_corr()) return;          // the serial chains then run in launch_corrections
         KLAUNCH(k_qx_serial, dim3(hc.nsp * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
                 qx_args(t));
+        if (NEGFIX_POST)
+          KLAUNCH(k_qx_post, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, hc.nsp * kz), BLK, 0, stream, g, dc,
+                  qx_args(t));
       });
     }
     if (!fused) xch({{FK::CQV, kz}, {FK::CQC, kz}});     // else k_scalars computed the ring
@@ -2281,9 +2295,18 @@ struct rcmdyn_engine {
         switch (ns) { case 1: RCM_SC(1); break; case 2: RCM_SC(2); break; case 3: RCM_SC(3); break; default: RCM_SC(4); }
 #undef RCM_SC
       }
-      if (qfuse() && own)
+      if (serial_with_corr()) {
+        // the qv / qc and the species planes' serial chains in one launch (the species' operands
+        // of the step before tend_post's flip), then their filters
+        const QxArgs qx = qx_args(t, 1 - t.cur);
+        KLAUNCH(k_negfix_serial_qx, dim3((2 + hc.nsp) * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g),
+                stream, g, dc, qf, qx);
+        KLAUNCH(k_negfix_post, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, 2 * kz), BLK, 0, stream, g, dc, qf);
+        KLAUNCH(k_qx_post, grid3(g.jci2 - g.jci1 + 1, g.ici2 - g.ici1 + 1, hc.nsp * kz), BLK, 0, stream, g, dc, qx);
+      } else if (qfuse() && own) {
         KLAUNCH(k_negfix_serial, dim3(2 * kz), dim3(negfix_threads(g)), sizeof(double) * negfix_lds(g), stream, g, dc,
                 qf);
+      }
     }
   }
   // not with a communicator: a rank-local call (a get) between tend and bdyval would then issue

@@ -186,6 +186,7 @@ struct Tile {
   double *a1qx[NQXH][2] = {}, *a2qx[NQXH][2] = {};
   double *cqx[NQXH] = {}, *fqx[NQXH] = {}, *slqx[NQXH] = {}, *d6qx[NQXH] = {};
   unsigned* depx = nullptr;          // nqx = 5: the species planes' row bitmaps (as depplane)
+  unsigned* depxf = nullptr;         // nqx = 5: the species planes' row flags (k_qx_fix -> k_qx_serial)
   unsigned *depplane;              // per (n,k) plane: bitmap of the rows with a serially dependent negative point
   int* negcnt = nullptr;           // hydrostatic qfuse: the negative forecasts k_scalars listed
   uint32_t* neglist = nullptr;

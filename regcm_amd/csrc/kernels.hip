@@ -1430,6 +1430,11 @@ struct QvRaw {
 __global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q) {
   extern __shared__ double lds[];
   const int plane = (int)blockIdx.x, kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  if (NEGFIX_POST) {
+    negfix_resolve(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane, k, lds, negfix_lds(g), NoPost{},
+                   [](int, int, double) {});
+    return;
+  }
   const QvRaw acc{g, c, n ? q.o1qc : q.o1qv, n ? q.o2qc : q.o2qv, q.psc, q.opsa, q.opsb,
                   n ? q.n1qc : q.n1qv, n ? q.n2qc : q.n2qv, n, k};
   negfix_resolve(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane, k, lds, negfix_lds(g), acc,
@@ -1438,6 +1443,22 @@ __global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __r
                    acc.load(jj, i, x);
                    acc.apply(jj, i, v, x);
                  });
+}
+
+// NEGFIX_POST: the filters of the points k_negfix_serial fixed, a thread per interior point of
+// a (qv | qc, level) plane (z = plane)
+__global__ void k_negfix_post(Geom g, const Consts* __restrict__ c, QFix q) {
+  const int j = g.jci1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int i = g.ici1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int plane = (int)blockIdx.z, kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  if (j > g.jci2 || i > g.ici2) return;
+  const double* sv = n ? q.cqc : q.cqv;
+  if (!negfix_is_dependent(g, sv, j, i, k)) return;
+  const QvRaw acc{g, c, n ? q.o1qc : q.o1qv, n ? q.o2qc : q.o2qv, q.psc, q.opsa, q.opsb,
+                  n ? q.n1qc : q.n1qv, n ? q.n2qc : q.n2qv, n, k};
+  double x[5];
+  acc.load(j, i, x);
+  acc.apply(j, i, F3(n ? q.fqc : q.fqv, j, i, k), x);
 }
 
 // qfuse: k_qfilter's fix of the negative forecasts k_scalars listed, one entry per thread

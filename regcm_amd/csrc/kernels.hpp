@@ -156,6 +156,8 @@ struct QxArgs {
   double *sl[NQXH], *d6[NQXH];
   const double* phy[NQXH];
   unsigned* dep;               // per (species, level) plane: row bitmap of the serially dependent negative points
+  unsigned* depf;              // per (species, level) plane and row: k_qx_fix's flag of such a point (k_qx_serial
+                               // turns the flags into the bitmap)
   int nsp;                     // hydrometeors beyond qc (0 for nqx = 2)
 };
 
@@ -187,7 +189,13 @@ __global__ void k_scalars(Geom g, const Consts* __restrict__ c, const StepState*
 __global__ void k_update(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields fm, Fields fs,
                          int mnx, int mny, int snx, int sny, int xcd);
 __global__ void k_qfilter(Geom g, const Consts* __restrict__ c, Fields f);
+// NEGFIX_POST (qxcommon.hpp): the serial fix passes resolve the chain, k_negfix_post / k_qx_post
+// apply the filters of the points they fixed
+#ifndef NEGFIX_POST
+#define NEGFIX_POST 1
+#endif
 __global__ void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q);
+__global__ void k_negfix_post(Geom g, const Consts* __restrict__ c, QFix q);
 __global__ void k_split_project(Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u,
                                 const double* __restrict__ a1v, const double* __restrict__ a2u,
                                 const double* __restrict__ a2v, const double* __restrict__ a1t,
@@ -229,6 +237,8 @@ __global__ void k_copy_frame(Geom g, Geom w, int nplanes, const double* __restri
 __global__ void k_qx_tend(Geom g, const Consts* __restrict__ c, const StepState* __restrict__ s, Fields f, QxArgs q);
 __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q);
 __global__ void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q);
+__global__ void k_qx_post(Geom g, const Consts* __restrict__ c, QxArgs q);
+__global__ void k_negfix_serial_qx(Geom g, const Consts* __restrict__ c, QFix qf, QxArgs q);
 struct NHFields;
 // the non-hydrostatic chains of the same hydrometeors (in place; k_qx_fix / k_qx_serial then
 // run with b* = a*)

@@ -222,6 +222,21 @@ __device__ void negfix_dense(const Geom& g, const double* sv, double* fx, int k,
   }
 }
 
+// NEGFIX_POST (kernels.hpp): the serial pass resolves the chain only (the fixed values into fx)
+// and a parallel launch afterwards (k_negfix_post, k_qx_post) applies the filters of the
+// dependent points, so the wavefront's steps carry the forecasts alone: every load of the
+// row-per-lane wavefront touches 64 lines, and the filters' inputs were 5 (qv/qc) or 2 (species)
+// more such loads per step (C3, nqx = 5: k_negfix_serial 365 -> 175 us, k_qx_serial 295 -> 220)
+struct NoPost {
+  static constexpr int NI = 0;
+  __device__ void load(int, int, double*) const {}
+  __device__ void apply(int, int, double, const double*) const {}
+};
+// a dependent negative point of the plane (the serial pass fixed it): the post launches' test
+__device__ __forceinline__ bool negfix_is_dependent(const Geom& g, const double* sv, int j, int i, int k) {
+  return F3(sv, j, i, k) < d_zero && negfix_dependent(g, sv, j, i, k);
+}
+
 // One (species, level) plane's serial fix by a whole block: nothing when no row is marked, the
 // wavefront when more than NEGFIX_SPARSE rows are and the block has a thread per row (and lds
 // holds the ring), else the row sweep by wavefront 0.  lds: ldsn doubles (see negfix_lds).

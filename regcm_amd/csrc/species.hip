@@ -266,11 +266,17 @@ __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q) {
       continue;
     }
     double v = LD(q.cq[n], o3);
+    // a wavefront is one row of one level (blockDim.x = 64): the first of its dependent points
+    // flags the row with a plain store (every writer stores the same 1; device-scope atomics on
+    // the few bitmap words serialised at the memory side: 190 of this kernel's 215 us at C3)
+    const bool dp = v < d_zero && negfix_dependent(g, q.cq[n], j, i, k);
+    const unsigned long long dm = __ballot(dp);
+    if (dp) {
+      if ((int)(threadIdx.x & 63) == __ffsll((long long)dm) - 1)
+        q.depf[(n * c->kz + (k - 1)) * (g.ici2 - g.ici1 + 1) + (i - g.ici1)] = 1u;
+      continue;
+    }
     if (v < d_zero) {
-      if (negfix_dependent(g, q.cq[n], j, i, k)) {
-        negfix_mark(g, q.dep, n * c->kz + (k - 1), i);
-        continue;
-      }
       v = negfix_sum(g, q.cq[n], q.fq[n], j, i, k, false);
       ST(q.fq[n], o3, v);
     }
@@ -305,17 +311,71 @@ struct QxRaw {
     F3(b1, j, i, k) = y;
   }
 };
-__global__ __launch_bounds__(512) void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q) {
-  extern __shared__ double lds[];
-  const int plane = (int)blockIdx.x, kz = c->kz;
+// one (species, level) plane of k_qx_serial (lds: negfix_lds(g) doubles)
+__device__ __forceinline__ void qx_serial_plane(const Geom& g, const Consts* __restrict__ c, const QxArgs& q,
+                                                int plane, double* lds) {
+  const int kz = c->kz;
   if (plane >= q.nsp * kz) return;
   const int n = plane / kz, k = plane % kz + 1;
+  {
+    // k_qx_fix's row flags into this plane's bitmap words (negfix_resolve reads those), flags
+    // cleared for the next step
+    const int R = g.ici2 - g.ici1 + 1, T = (int)(blockDim.x * blockDim.y * blockDim.z);
+    const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+    unsigned* fl = q.depf + plane * R;
+    unsigned* words = q.dep + plane * negfix_rowwords(g);
+    for (int b = 0; b < R; b += T) {
+      const int r = b + tid;
+      const bool f = r < R && fl[r] != 0u;
+      if (f) fl[r] = 0u;
+      const unsigned long long m = __ballot(f);
+      if (r < R && (r & 31) == 0) words[r >> 5] = (unsigned)(m >> (r & 32));
+    }
+    __syncthreads();
+  }
+  if (NEGFIX_POST) {
+    negfix_resolve(g, q.cq[n], q.fq[n], q.dep, plane, k, lds, negfix_lds(g), NoPost{}, [](int, int, double) {});
+    return;
+  }
   const QxRaw acc{g, q.a1[n], q.a2[n], q.b1[n], q.b2[n], c->gnu2, k};
   negfix_resolve(g, q.cq[n], q.fq[n], q.dep, plane, k, lds, negfix_lds(g), acc, [&](int jj, int i, double v) {
     double x[2];
     acc.load(jj, i, x);
     acc.apply(jj, i, v, x);
   });
+}
+__global__ __launch_bounds__(512) void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q) {
+  extern __shared__ double lds[];
+  qx_serial_plane(g, c, q, (int)blockIdx.x, lds);
+}
+// NEGFIX_POST, hydrostatic qfuse: the serial chains of the qv / qc planes (blocks [0, 2 kz), as
+// k_negfix_serial) and of the species planes (k_qx_serial) in one launch after the split
+// corrections: the two sets of planes are independent, so the launch takes the longer chain's
+// time instead of the sum (k_qx_fix's flags wait for it; nothing of the split reads the species)
+__global__ __launch_bounds__(512) void k_negfix_serial_qx(Geom g, const Consts* __restrict__ c, QFix qf, QxArgs q) {
+  extern __shared__ double lds[];
+  const int b = (int)blockIdx.x, kz = c->kz;
+  if (b >= 2 * kz) {
+    qx_serial_plane(g, c, q, b - 2 * kz, lds);
+    return;
+  }
+  const int n = b / kz, k = b % kz + 1;
+  negfix_resolve(g, n ? qf.cqc : qf.cqv, n ? qf.fqc : qf.fqv, qf.depplane, b, k, lds, negfix_lds(g), NoPost{},
+                 [](int, int, double) {});
+}
+
+// NEGFIX_POST: filter_raw_4d of the points k_qx_serial fixed, a thread per interior point of a
+// (species, level) plane (z = plane)
+__global__ void k_qx_post(Geom g, const Consts* __restrict__ c, QxArgs q) {
+  const int j = g.jci1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int i = g.ici1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
+  const int plane = (int)blockIdx.z, kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  if (j > g.jci2 || i > g.ici2 || n >= q.nsp) return;
+  if (!negfix_is_dependent(g, q.cq[n], j, i, k)) return;
+  const QxRaw acc{g, q.a1[n], q.a2[n], q.b1[n], q.b2[n], c->gnu2, k};
+  double x[2];
+  acc.load(j, i, x);
+  acc.apply(j, i, F3(q.fq[n], j, i, k), x);
 }
 
 // K_QX4.  bdyval for the hydrometeors beyond qc, one block per (level, species): while
