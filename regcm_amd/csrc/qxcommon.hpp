@@ -4,6 +4,7 @@
 #pragma once
 #include "kernels.hpp"
 #include "devcommon.hpp"
+#include "fastmath.hpp"
 
 namespace rcm {
 
@@ -202,7 +203,10 @@ __device__ void negfix_dense(const Geom& g, const double* sv, double* fx, int k,
         sum = sum + fabs(w0[2]);
         sum = sum + fabs(w1[2]);
         sum = sum + fabs(w2[2]);
-        const double v = 0.01 * sum / 9.0;
+        // / 9 as div_by (fastmath.hpp: the division's bits from the rounded reciprocal in three
+        // dependent operations; the step's critical path runs through it), for normal operands
+        const double xs = 0.01 * sum;
+        const double v = xs >= 0x1p-960 ? div_by(xs, 9.0, 1.0 / 9.0) : xs / 9.0;
         ring[4 * r + (jj & 3)] = v;
         prev = v;
         if (p0 || p1 || p2 || p3) {
