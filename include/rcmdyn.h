@@ -236,6 +236,12 @@ int rcmdyn_set_nproc(int32_t nproc, int32_t jx, int32_t iy, int32_t cpus[2]);
  * bdy[4] = {has_bdyleft, has_bdyright, has_bdybottom, has_bdytop}.  Host-only. */
 int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
                        int32_t tile, int32_t ext[8], int32_t bdy[4]);
+/* The same for the grid and decomposition of cfg (jx, iy, nproc_j, nproc_i), with the periodic
+ * directions of i_band (j) and i_crm (i): a periodic direction has no boundary side and its
+ * cross range takes every point (Main/mpplib/mod_mppparam.F90:1131-1132, 1340-1360), as the
+ * engine's own tiles do.  rcmdyn_tile_extent is this call with i_band = i_crm = 0; a band or
+ * CRM host picks its points with this one.  Host-only. */
+int rcmdyn_tile_extent_cfg(const rcmdyn_config* cfg, int32_t tile, int32_t ext[8], int32_t bdy[4]);
 
 /* Communication plan of one rank, host-only (no GPU, no communicator): the halo messages and
  * collectives that rank cfg->comm_rank (one tile per rank: tile_first = comm_rank, tile_count

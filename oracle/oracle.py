@@ -45,6 +45,7 @@ def lib():
         L.orc_put.argtypes = [P, i, dp, i, i, i, i, i, i]
         L.orc_get.argtypes = [P, i, dp, i, i, i, i, i, i]
         L.orc_set_sound_probe.argtypes = [P, i]
+        L.orc_set_tend_probe.argtypes = [P, i]
         L.orc_get_work.restype = i
         L.orc_get_work.argtypes = [P, ctypes.c_char_p, dp, ctypes.c_size_t]
         L.orc_set_time.argtypes = [P, ctypes.c_longlong, ctypes.c_double, ctypes.c_double]
@@ -125,6 +126,9 @@ class OracleCore:
 
     def set_sound_probe(self, nsub):
         lib().orc_set_sound_probe(self.h, nsub)
+
+    def set_tend_probe(self, stage):
+        lib().orc_set_tend_probe(self.h, stage)
 
     def get_work(self, name):
         """An internal work array (orc_get_work) on the global (iy, jx) grid of a one-tile

@@ -135,6 +135,7 @@ struct orc {
   double *a1tke, *a2tke, *ctke, *tkedyn, *tkeps, *tkephy;
   double* kpbl;      /* ibltyp = 2: the UW scheme's PBL-top level (put; iuwvadv = 1 reads it) */
   int sound_probe;   /* test hook (orc_set_sound_probe): sound returns after this many sub-steps */
+  int tend_probe;    /* test hook (orc_set_tend_probe): the hydrostatic tend returns at this stage */
   /* bdyin: raw record (u, v, t, qv, ps, pp, w), coupled b1 (same order), NH atm0%psdot */
   double *bin[7], *bb1[7], *psdot0;
   double rhmin, rhmax;
@@ -672,6 +673,7 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
   else if (o->nh && !strcmp(name, "pi")) a = o->s_pi;
   else if (o->nh && !strcmp(name, "pr1")) a = o->pr1;
   else if (o->nh && !strcmp(name, "rho1")) a = o->rho1;
+  else if (!strcmp(name, "ct")) a = o->ct;
   else if (!strcmp(name, "cqv")) a = o->cq[0];
   else if (!strcmp(name, "cqc")) a = o->cq[1];
   else if (o->nqx > 2 && !strcmp(name, "cqi")) a = o->cq[2];
@@ -687,6 +689,7 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
 }
 
 void orc_set_sound_probe(orc_t* o, int nsub) { o->sound_probe = nsub; }
+void orc_set_tend_probe(orc_t* o, int stage) { o->tend_probe = stage; }
 
 int orc_get(orc_t* o, int field, double* dst, int j1, int j2, int i1, int i2, int k1, int k2) {
   int nk; double* a = field_ptr(o, field, &nk);
@@ -3170,6 +3173,9 @@ int orc_tend(orc_t* o) {
         A3(o->uten, j, i, k) = A3(o->uten, j, i, k) + A3(o->udyn, j, i, k) + A3(o->phy[3], j, i, k);
         A3(o->vten, j, i, k) = A3(o->vten, j, i, k) + A3(o->vdyn, j, i, k) + A3(o->phy[4], j, i, k);
       }
+  /* test hook: every tendency summed, the t / qx forecasts (and their negative fix) in ct / cq,
+   * atm1 / atm2 and p* not yet filtered */
+  if (o->tend_probe == 1) return 0;
   /* time filters, :419-427, Main/mod_timefilter.F90 */
   double g1 = o->cfg.gnu1, beta = 0.53;
   for (int i = o->ici1; i <= o->ici2; i++)                          /* filter_ra_2d */
@@ -3209,6 +3215,8 @@ int orc_tend(orc_t* o) {
         A3(o->a2v, j, i, k) = A3(o->a1v, j, i, k) + d;
         A3(o->a1v, j, i, k) = A3(o->cv, j, i, k);
       }
+  /* test hook: the state splitf starts from (every time filter applied) */
+  if (o->tend_probe == 2) return 0;
   splitf(o);
   /* rcmtimer%advance and dt switch, :608-616 */
   o->lcount += 1;

@@ -60,6 +60,11 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap);
 /* test hook: the NH sound returns after nsub sub-steps (0: right after its set-up), before
  * the time filters, so a test can check one sub-step; -1 (default) runs sound whole */
 void orc_set_sound_probe(orc_t* o, int nsub);
+/* test hook: the hydrostatic tend returns early (without advancing the clock): 1 = after every
+ * tendency is summed and the t / qx forecasts and their negative fix are formed (work arrays
+ * "ct", "cqv", "cqc"), before any time filter; 2 = after the time filters, at the entry of
+ * splitf; 0 (default) runs tend whole */
+void orc_set_tend_probe(orc_t* o, int stage);
 void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
 void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);
 int orc_tend(orc_t* o);     /* returns 1 on CFL violation (NaN ptntot) */

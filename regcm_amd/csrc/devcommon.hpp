@@ -87,6 +87,20 @@ __device__ __forceinline__ void xcd_tile2d(int& bx, int& by) {
   bx = t % nx;
   by = t / nx;
 }
+// the same over a range of the launch: the blocks B in [base, base + n) of the launch's linear
+// (dispatch) order, renumbered 0..n-1 so that each XCD (B mod 8) takes one contiguous run; a
+// kernel whose consecutive work items share operands (the levels of one column block, the rows
+// of one column stripe) then finds them in its own XCD's L2
+__device__ __forceinline__ int xcd_range(int B, int base, int n) {
+  const int x = B & 7, b0 = base & 7;
+  int t = 0;
+  for (int y = 0; y < x; y++) {
+    const int f = base + ((y - b0 + 8) & 7);        // first block of the range on XCD y
+    t += f < base + n ? (base + n - 1 - f) / 8 + 1 : 0;
+  }
+  const int fx = base + ((x - b0 + 8) & 7);
+  return t + (B - fx) / 8;
+}
 // THREAD_POINT over xcd_block()'s tile
 #define THREAD_POINT_XCD(j1, i1)                                        \
   const Blk3 xb_ = xcd_block();                                         \

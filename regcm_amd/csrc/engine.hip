@@ -55,8 +55,9 @@ constexpr double EGRAV = 9.80665, BOLTZK = 1.3806504e-23, NAVGDR = 6.02214129e23
 constexpr double AMD = 28.96454, AMW = 18.01528, VONKAR = 0.4;
 
 // band (i_band = 1): periodic in j, so no tile has a west/east boundary and the cross grid
-// takes every j (global_cross_jend = global_dot_jend, Main/mpplib/mod_mppparam.F90:1351-1354)
-void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band = 0) {
+// takes every j (global_cross_jend = global_dot_jend, Main/mpplib/mod_mppparam.F90:1351-1354);
+// crm (i_crm = 1): the same in i (dim_period(2), :1132, 1340-1342)
+void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band = 0, int crm = 0) {
   int lj = tile / ci, li = tile % ci;
   int jxp = jx / cj, iyp = iy / ci;
   int js = lj * jxp + 1, is = li * iyp + 1;
@@ -71,8 +72,9 @@ void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4
   int je = js + jxp - 1, ie = is + iyp - 1;
   ext[0] = js; ext[1] = je; ext[2] = is; ext[3] = ie;
   ext[4] = js; ext[5] = (je == jx && !band) ? je - 1 : je;
-  ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
-  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band; bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+  ext[6] = is; ext[7] = (ie == iy && !crm) ? ie - 1 : ie;
+  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band;
+  bdy[2] = (li == 0) && !crm; bdy[3] = (li == ci - 1) && !crm;
 }
 
 Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G, int band = 0) {
@@ -278,7 +280,8 @@ struct rcmdyn_engine {
   int gslot = 0;
   bool statics_dirty = true;
   bool bdy_dirty = true;
-  bool dprd_put = false;      // NH: dprddx / dprddy put since the last check (check_dprd)
+  bool dprd_put = false;      // NH: a dprddx / dprddy check is pending (check_dprd); sticky until it passes
+  bool dprd_any = false;      // NH: dprddx / dprddy were put (a later atm0%pr put re-arms the check)
   bool kpbl_dirty = false;    // kpbl put since the last tend: its ghost ring is stale
   bool ghosts_stale = true;   // state put since the last tend: ghost rings are not step results
   bool capturing = false;
@@ -320,6 +323,12 @@ struct rcmdyn_engine {
   // any other call (settle) replays tend's own graph first.  RCMDYN_NO_LAZY_TEND=1: off
   const bool lazy_tend = std::getenv("RCMDYN_NO_LAZY_TEND") == nullptr;
   bool tend_pending = false;
+  // fault injection for the tests (RCMDYN_INJECT_LAUNCH_FAILURE=n at create): the n-th launch of
+  // a lazy tend's graph fails before it is issued, as a failed hipGraphLaunch would
+  int inject_fail = 0;
+  void inject_launch_failure() {
+    if (inject_fail > 0 && --inject_fail == 0) throw std::runtime_error("rcmdyn: injected launch failure");
+  }
   int lazy_par = 0;
   // the hydrostatic step without k_qfilter (its work in k_columns, k_scalars and the extra
   // blocks of k_split_project / k_split_correct); RCMDYN_NO_QFUSE=1 launches k_qfilter
@@ -694,6 +703,22 @@ struct rcmdyn_engine {
     }
   }
 
+  // The dynamic LDS the launches request grows with the tile: the serial moisture fix's
+  // (negfix_lds / negfix_sweep_lds, a row of the plane) and k_split_project's (4 x kz x SPC).
+  // Check the owned tiles' requests against the device's limit at create, so a tile too large
+  // for them is refused here rather than failing a launch inside a step.
+  void check_lds() {
+    int maxs = 0;
+    HIPCHK(hipDeviceGetAttribute(&maxs, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+    for (int t = 0; t < cfg.tile_count; t++) {
+      const Geom& g = all[cfg.tile_first + t];
+      const size_t need = sizeof(double) * (size_t)std::max(negfix_lds(g), 4 * cfg.kz * SPC);
+      if (need > (size_t)maxs)
+        throw std::runtime_error("rcmdyn: tile " + std::to_string(cfg.tile_first + t) + " needs " + std::to_string(need) +
+                                 " bytes of LDS per block, the device allows " + std::to_string(maxs));
+    }
+  }
+
   void create(const rcmdyn_config* c, std::vector<PlanOp>* plan = nullptr) {
     cfg = *c;
     dry = plan != nullptr;
@@ -767,6 +792,8 @@ struct rcmdyn_engine {
       return;
     }
     check_block_sizes();
+    check_lds();
+    if (const char* e = std::getenv("RCMDYN_INJECT_LAUNCH_FAILURE")) inject_fail = std::atoi(e);
     HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc(&dc, sizeof(Consts)));
     HIPCHK(hipMemcpy(dc, &hc, sizeof(Consts), hipMemcpyHostToDevice));
@@ -1131,7 +1158,8 @@ struct rcmdyn_engine {
     if (f == RCMDYN_KPBL && hc.iqxvadv == 3 && cfg.idynamic != 2) kpbl_dirty = true;
     ghosts_stale = true;
     if (f >= RCMDYN_ATM0_PS && f <= RCMDYN_CRY) invalidate_graphs();
-    if (f == RCMDYN_DPRDDX || f == RCMDYN_DPRDDY || (dprd_put && f == RCMDYN_ATM0_PR)) dprd_put = true;
+    if (f == RCMDYN_DPRDDX || f == RCMDYN_DPRDDY) dprd_any = true;
+    if (f == RCMDYN_DPRDDX || f == RCMDYN_DPRDDY || (dprd_any && f == RCMDYN_ATM0_PR)) dprd_put = true;
   }
 
   // physics coupling seam: the pc_physic buffers exist from the first put of one of them on
@@ -1572,8 +1600,7 @@ struct rcmdyn_engine {
   // defines them (Main/mod_params.F90:2676-2686); values a host put must be exactly those, or
   // the engine would silently compute with others
   void check_dprd() {
-    dprd_put = false;
-    if (!NH_DPRFORM || cfg.idynamic != 2 || dry) return;
+    if (!NH_DPRFORM || cfg.idynamic != 2 || dry) { dprd_put = false; return; }
     int* bad = nullptr;
     HIPCHK(hipMalloc(&bad, sizeof(int)));
     HIPCHK(hipMemsetAsync(bad, 0, sizeof(int), stream));
@@ -1586,8 +1613,10 @@ struct rcmdyn_engine {
     HIPCHK(hipMemcpyAsync(&n, bad, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
     HIPCHK(hipFree(bad));
+    // a mismatch stays pending: every later call fails the same way until a put corrects it
     if (n) throw std::runtime_error("rcmdyn: DPRDDX/DPRDDY differ from atm0%pr's four-point differences at " +
                                     std::to_string(n) + " points (Main/mod_params.F90:2676-2686)");
+    dprd_put = false;
   }
 
   // ------------------------------------------------------------------ the step
@@ -2277,7 +2306,7 @@ struct rcmdyn_engine {
       const bool own = hc.nsp > 0;
       const int nser = qfuse() && !own ? (int)((2 * kz + gr.x * gr.y - 1) / (gr.x * gr.y)) : 0;
       gr.z += nser;
-      const size_t slds = nser ? sizeof(double) * negfix_lds(g) : 0;     // the sweeps' LDS
+      const size_t slds = nser ? sizeof(double) * negfix_sweep_lds(g) : 0;     // the sweeps' LDS (row sweeps only)
       if (bdy) {
         // the bdyval blocks: leading z slices of 6 lines x bdy_chunks 64-point chunks x kz
         // levels, 4 per block
@@ -2317,8 +2346,9 @@ struct rcmdyn_engine {
   // a call other than rcmdyn_bdyval after a tend that deferred its corrections: launch them
   void settle() {
     if (tend_pending) {              // the lazy tend's own graph (captured with deferred corrections)
-      tend_pending = false;
+      inject_launch_failure();
       HIPCHK(hipGraphLaunch(gtend[lazy_par], stream));
+      tend_pending = false;          // only once launched: a failed launch leaves the tend pending
       corr_pending = true;
     }
     if (!corr_pending) return;
@@ -2522,8 +2552,9 @@ struct rcmdyn_engine {
   void bdyval_call() {
     prepare();
     if (tend_pending) {              // the lazy tend and this bdyval: one step graph
-      tend_pending = false;
+      inject_launch_failure();
       HIPCHK(hipGraphLaunch(gexec[lazy_par], stream));
+      tend_pending = false;          // only once launched: a failure keeps the step pending
       replayed_bdyval();
       note_step(hs.lcount);
       return;
@@ -2787,9 +2818,14 @@ int rcmdyn_overlap_shares(const rcmdyn_config* cfg, int32_t* out, int32_t cap) {
 
 int rcmdyn_destroy(rcmdyn_t* h) {
   if (!h) return 0;
-  int rc = guard(h, [&] { h->destroy(); });
+  // a lazy tend (or deferred corrections) still pending is launched first, so the host's last
+  // tend is not dropped without a word: its failure is this call's return code
+  const int rc0 = guard(h, [&] { h->settle(); });
+  const std::string err0 = h->err;
+  const int rc = guard(h, [&] { h->destroy(); });
+  if (rc0 || rc) g_last_error = rc0 ? err0 : h->err;      // h is gone: rcmdyn_last_error(NULL)
   delete h;
-  return rc;
+  return rc0 ? rc0 : rc;
 }
 
 const char* rcmdyn_last_error(rcmdyn_t* h) { return h ? h->err.c_str() : g_last_error.c_str(); }
@@ -2817,6 +2853,14 @@ int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
                        int32_t bdy[4]) {
   if (tile < 0 || tile >= nproc_j * nproc_i) return 1;
   tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy);
+  return 0;
+}
+
+int rcmdyn_tile_extent_cfg(const rcmdyn_config* cfg, int32_t tile, int32_t ext[8], int32_t bdy[4]) {
+  if (!cfg || !ext || !bdy) return 1;
+  if (tile < 0 || cfg->nproc_j < 1 || cfg->nproc_i < 1 || tile >= cfg->nproc_j * cfg->nproc_i) return 1;
+  if ((cfg->i_band != 0 && cfg->i_band != 1) || (cfg->i_crm != 0 && cfg->i_crm != 1)) return 1;
+  tile_extent(cfg->jx, cfg->iy, cfg->nproc_j, cfg->nproc_i, tile, ext, bdy, cfg->i_band, cfg->i_crm);
   return 0;
 }
 

@@ -85,13 +85,18 @@ struct Geom {
 // its serial part (qxcommon.hpp): the row sweep's two interior rows and 13 per lane, or the
 // wavefront's 4-slot ring per row; the wavefront's block: a thread per interior row
 __host__ __device__ __forceinline__ int negfix_rowwords(const Geom& g) { return (g.ici2 - g.ici1 + 1 + 31) / 32; }
-__host__ __device__ __forceinline__ int negfix_lds(const Geom& g) {
-  const int a = 2 * (g.jci2 - g.jci1 + 1) + 64 * 13, b = 4 * (g.ici2 - g.ici1 + 1);
-  return a > b ? a : b;
-}
 __host__ __device__ __forceinline__ int negfix_threads(const Geom& g) {
   const int r = (g.ici2 - g.ici1 + 1 + 63) / 64 * 64;
   return r < 64 ? 64 : (r > 512 ? 512 : r);
+}
+// the row sweep's LDS (one wavefront: two rows + 13 per lane)
+__host__ __device__ __forceinline__ int negfix_sweep_lds(const Geom& g) { return 2 * (g.jci2 - g.jci1 + 1) + 64 * 13; }
+// the LDS of a launch whose block per plane can run either path: the wavefront's 4-slot ring per
+// row is added only when a negfix_threads block holds a thread per row (a tall tile
+// then requests the sweep's LDS and keeps it, instead of failing the launch)
+__host__ __device__ __forceinline__ int negfix_lds(const Geom& g) {
+  const int a = negfix_sweep_lds(g), R = g.ici2 - g.ici1 + 1, b = R <= negfix_threads(g) ? 4 * R : 0;
+  return a > b ? a : b;
 }
 // columns between j1 and the frame's 128-B line boundary at or below it (ALIGN_J, devcommon.hpp)
 __host__ __device__ __forceinline__ int jalign(const Geom& g, int j1) { return (j1 - g.j0) & 15; }

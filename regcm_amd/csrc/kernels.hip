@@ -1513,13 +1513,16 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
     double* delh, double* psdota, int nxp, int nproj, QFix qf, Geom gw, double* wdeld, double* wdelh,
     double* wpsdota, double* wpsa, const double* __restrict__ o2u, const double* __restrict__ o2v) {
   extern __shared__ double lds[];                        // 4 x kz x SPC
-  const int b = blockIdx.x;
-  if (b >= nproj) {
+  if ((int)blockIdx.x >= nproj) {
+    const int b = blockIdx.x;
     if (qf.negcnt) negfix_list(g, c, qf, (b - nproj) * (int)blockDim.x + (int)threadIdx.x, ((int)gridDim.x - nproj) * (int)blockDim.x);
     else if (threadIdx.x < 64)
-      negfix_serial_plane(g, c, qf, b - nproj, negfix_lds(g) <= 4 * c->kz * SPC ? lds : nullptr);
+      negfix_serial_plane(g, c, qf, b - nproj, negfix_sweep_lds(g) <= 4 * c->kz * SPC ? lds : nullptr);
     return;
   }
+  // SP_XCD: each XCD takes a contiguous run of column rows, so the i + 1 row of the u, v
+  // divergence, which the next row's block loads as its own, is a hit in the same L2
+  const int b = SP_XCD ? xcd_range((int)blockIdx.x, 0, nproj) : (int)blockIdx.x;
   PT_DECL
   const int tx = (int)threadIdx.x % SPC, ty = (int)threadIdx.x / SPC;
   // owned dot points, plus psdota on the right/top ghost ring (the split corrections of the
@@ -1886,7 +1889,7 @@ __device__ __forceinline__ void split_correct_body(
   if (nser && (int)blockIdx.z >= (int)gridDim.z - nser) {
     const int plane = (((int)blockIdx.z - ((int)gridDim.z - nser)) * (int)gridDim.y + (int)blockIdx.y) *
                           (int)gridDim.x + (int)blockIdx.x;
-    extern __shared__ double nlds[];            // negfix_lds(g) doubles when nser > 0 (the launch)
+    extern __shared__ double nlds[];            // negfix_sweep_lds(g) doubles when nser > 0 (the launch)
     if (threadIdx.y == 0 && plane < 2 * c->kz) negfix_serial_plane(g, c, qf, plane, nlds);
     return;
   }
@@ -1911,19 +1914,31 @@ __device__ __forceinline__ void split_correct_body(
   // the (pair, row) points of a level flattened: every lane of a block has a point (no idle
   // second block column on a 192-wide tile), rows follow one another in the lanes
   const int npr = (g.jdx2() - g.jde1 + 2) / 2;
-  const int q = (int)blockIdx.x * 256 + (int)threadIdx.y * 64 + (int)threadIdx.x;
+#if SCOR_XCD
+  // the kz levels of one pair block run consecutively on one XCD: the 2-D sums, psdota and
+  // msfd each level reads are fetched into that XCD's L2 once
+  const int tq = xcd_range(((int)blockIdx.z * (int)gridDim.y + (int)blockIdx.y) * (int)gridDim.x + (int)blockIdx.x,
+                           zbdy * (int)gridDim.x, kz * (int)gridDim.x);
+  const int bxq = tq / kz, k = tq % kz + 1;
+  const bool first = tq == 0;
+#else
+  const int bxq = (int)blockIdx.x, k = (int)blockIdx.z - zbdy + 1;
+  const bool first = blockIdx.x == 0 && (int)blockIdx.z == zbdy;
+#endif
+  const int q = bxq * 256 + (int)threadIdx.y * 64 + (int)threadIdx.x;
   const int j = g.jde1 + q % npr;
   const int i = g.ide1 + q / npr;
 #else
   const int j = g.jde1 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
   const int i = g.ide1 + (int)(blockIdx.y * blockDim.y + threadIdx.y);
-#endif
   const int k = (int)blockIdx.z - zbdy + 1;
+  const bool first = blockIdx.x == 0 && blockIdx.y == 0 && (int)blockIdx.z == zbdy;
+#endif
   // last tile's launch, block 0: the Bleck noise sums of every tile (fixed-order tree over the
   // k_columns partials, Main/mod_tendency.F90:1449-1459), then rcmtimer%advance + dt switch
   // (:608-616); nothing else here reads the clock.  The same lane then copies the step's error
   // flags into the host-mapped ring (k_flag_snapshot's work; this is the step's last flag writer)
-  if (advance && blockIdx.x == 0 && blockIdx.y == 0 && (int)blockIdx.z == zbdy) {
+  if (advance && first) {
     __shared__ double sa[256], sb[256];
     const int t = threadIdx.y * blockDim.x + threadIdx.x;
     double a = 0.0, b = 0.0;

@@ -57,6 +57,15 @@ constexpr int COLW = RCM_COLW, COLG = RCM_COLG, COLT = COLW * COLG;   // COLG le
 #define RCM_SPC 32
 #endif
 constexpr int SPC = RCM_SPC, SPG = 8;
+// k_split_project / k_split_correct(_bdy): XCD-contiguous block placement (xcd_range,
+// devcommon.hpp): the rows a projection block shares with the next row's block, and the 2-D
+// split sums every level of a correction block column reads, stay in one L2
+#ifndef SP_XCD
+#define SP_XCD 0
+#endif
+#ifndef SCOR_XCD
+#define SCOR_XCD 0
+#endif
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level).  32 x 8 (256 threads, 39 KB of

@@ -40,8 +40,8 @@ __device__ __forceinline__ bool negfix_dependent(const Geom& g, const double* sv
 // round of loads, and lane 0 walks the chunk's dependent points in order on LDS alone, taking a
 // dependent predecessor's value from the fixed values this sweep keeps for the current and
 // the previous row.  Each value is the reference's expression (0.01 * the nine |q| summed in
-// its order / 9), so the result is the sweep's, bit for bit.  The caller passes negfix_lds(g)
-// doubles of LDS (lds), or null: then lane 0 reads every operand from memory.
+// its order / 9), so the result is the sweep's, bit for bit.  The caller passes
+// negfix_sweep_lds(g) doubles of LDS (lds), or null: then lane 0 reads every operand from memory.
 __device__ __forceinline__ void negfix_mark(const Geom& g, unsigned* dep, int plane, int i) {
   const int r = i - g.ici1;
   atomicOr(&dep[plane * negfix_rowwords(g) + (r >> 5)], 1u << (r & 31));
@@ -261,7 +261,7 @@ __device__ void negfix_resolve(const Geom& g, const double* sv, double* fx, unsi
     for (int w = tid; w < nw; w += T) words[w] = 0;
     return;
   }
-  if (tid < 64) negfix_sweep(g, sv, fx, dep, plane, k, negfix_lds(g) <= ldsn ? lds : nullptr, post);
+  if (tid < 64) negfix_sweep(g, sv, fx, dep, plane, k, negfix_sweep_lds(g) <= ldsn ? lds : nullptr, post);
 }
 
 // RAW filters of one point (filter_raw_qv / filter_raw_4d) with the filtered p*

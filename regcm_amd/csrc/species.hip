@@ -266,14 +266,13 @@ __global__ void k_qx_fix(Geom g, const Consts* __restrict__ c, QxArgs q) {
       continue;
     }
     double v = LD(q.cq[n], o3);
-    // a wavefront is one row of one level (blockDim.x = 64): the first of its dependent points
-    // flags the row with a plain store (every writer stores the same 1; device-scope atomics on
-    // the few bitmap words serialised at the memory side: 190 of this kernel's 215 us at C3)
+    // a dependent point flags its row with a plain store (every writer stores the same 1, so
+    // it holds for any block shape; the lanes of one row store one address, a single
+    // transaction; device-scope atomics on the few bitmap words serialised at the memory side:
+    // 190 of this kernel's 215 us at C3)
     const bool dp = v < d_zero && negfix_dependent(g, q.cq[n], j, i, k);
-    const unsigned long long dm = __ballot(dp);
     if (dp) {
-      if ((int)(threadIdx.x & 63) == __ffsll((long long)dm) - 1)
-        q.depf[(n * c->kz + (k - 1)) * (g.ici2 - g.ici1 + 1) + (i - g.ici1)] = 1u;
+      q.depf[(n * c->kz + (k - 1)) * (g.ici2 - g.ici1 + 1) + (i - g.ici1)] = 1u;
       continue;
     }
     if (v < d_zero) {

@@ -26,7 +26,7 @@ _lib = None
 
 EXPORTED = [
     "rcmdyn_create", "rcmdyn_destroy", "rcmdyn_last_error", "rcmdyn_set_nproc",
-    "rcmdyn_tile_extent", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
+    "rcmdyn_tile_extent", "rcmdyn_tile_extent_cfg", "rcmdyn_put", "rcmdyn_get", "rcmdyn_set_time", "rcmdyn_get_time",
     "rcmdyn_tend", "rcmdyn_bdyval", "rcmdyn_step", "rcmdyn_synchronize", "rcmdyn_diagnostics",
     "rcmdyn_comm_unique_id", "rcmdyn_last_step_ms", "rcmdyn_set_diagnostics", "rcmdyn_kernel_times",
     "rcmdyn_tend_pre_physics", "rcmdyn_tend_post_physics", "rcmdyn_bdyin", "rcmdyn_reductions", "rcmdyn_runtime_info",
@@ -55,6 +55,7 @@ def lib():
     L.rcmdyn_last_error.restype = ctypes.c_char_p
     L.rcmdyn_set_nproc.argtypes = [i32, i32, i32, ctypes.POINTER(i32)]
     L.rcmdyn_tile_extent.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
+    L.rcmdyn_tile_extent_cfg.argtypes = [ctypes.POINTER(RcmdynConfig), i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]
     L.rcmdyn_put.argtypes = [P, i32, dp, i32, i32, i32, i32, i32, i32]
     L.rcmdyn_get.argtypes = [P, i32, dp, i32, i32, i32, i32, i32, i32]
     L.rcmdyn_set_time.argtypes = [P, ctypes.c_int64, ctypes.c_double, ctypes.c_double]
@@ -87,10 +88,19 @@ def set_nproc(nproc: int, jx: int, iy: int):
     return int(cp[0]), int(cp[1])
 
 
-def tile_extent(jx: int, iy: int, nproc_j: int, nproc_i: int, tile: int):
+def tile_extent(jx: int, iy: int, nproc_j: int, nproc_i: int, tile: int, i_band: int = 0, i_crm: int = 0):
+    """Index ranges of one tile, ([jde1, jde2, ide1, ide2, jce1, jce2, ice1, ice2],
+    [left, right, bottom, top]).  With i_band / i_crm the j / i direction is periodic
+    (rcmdyn_tile_extent_cfg): no boundary side there, and the cross range takes every point."""
     ext = (ctypes.c_int32 * 8)()
     bdy = (ctypes.c_int32 * 4)()
-    if lib().rcmdyn_tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy):
+    if i_band or i_crm:
+        cfg = RcmdynConfig()
+        cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i = jx, iy, nproc_j, nproc_i
+        cfg.i_band, cfg.i_crm = i_band, i_crm
+        if lib().rcmdyn_tile_extent_cfg(ctypes.byref(cfg), tile, ext, bdy):
+            raise EngineError("rcmdyn_tile_extent_cfg failed")
+    elif lib().rcmdyn_tile_extent(jx, iy, nproc_j, nproc_i, tile, ext, bdy):
         raise EngineError("rcmdyn_tile_extent failed")
     return list(ext), list(bdy)
 
@@ -161,9 +171,12 @@ class DynCore:
             raise EngineError(lib().rcmdyn_last_error(self.h).decode())
 
     def close(self):
+        """rcmdyn_destroy: a lazy tend still pending is launched first; its failure raises."""
         if self.h:
-            lib().rcmdyn_destroy(self.h)
+            rc = lib().rcmdyn_destroy(self.h)
             self.h = ctypes.c_void_p()
+            if rc:
+                raise EngineError(lib().rcmdyn_last_error(None).decode())
 
     def __del__(self):
         try:

@@ -181,6 +181,14 @@ module mod_gpu_dyn
       integer(c_int32_t), value :: jx, iy, nproc_j, nproc_i, tile
       integer(c_int32_t), intent(out) :: ext(8), bdy(4)
     end function
+    ! the same for cfg's grid and decomposition with its periodic directions (i_band: j,
+    ! i_crm: i), as the engine's tiles are cut; host-only
+    integer(c_int) function rcmdyn_tile_extent_cfg(cfg, tile, ext, bdy) bind(c, name='rcmdyn_tile_extent_cfg')
+      import :: c_int, c_int32_t, rcmdyn_config
+      type(rcmdyn_config), intent(in) :: cfg
+      integer(c_int32_t), value :: tile
+      integer(c_int32_t), intent(out) :: ext(8), bdy(4)
+    end function
     ! the communication calls of one rank (7 int64 per record), host-only
     integer(c_int) function rcmdyn_exchange_plan(cfg, nsteps, ops, cap, count) bind(c, name='rcmdyn_exchange_plan')
       import :: c_int, c_int32_t, c_int64_t, rcmdyn_config
@@ -231,7 +239,7 @@ module mod_gpu_dyn
   public :: rcmdyn_create, rcmdyn_destroy, rcmdyn_put, rcmdyn_get, rcmdyn_set_time
   public :: rcmdyn_get_time, rcmdyn_tend, rcmdyn_bdyval, rcmdyn_step, rcmdyn_diagnostics, rcmdyn_reductions
   public :: rcmdyn_tend_pre_physics, rcmdyn_tend_post_physics, rcmdyn_bdyin, rcmdyn_last_error
-  public :: rcmdyn_synchronize, rcmdyn_set_nproc, rcmdyn_tile_extent, rcmdyn_exchange_plan
+  public :: rcmdyn_synchronize, rcmdyn_set_nproc, rcmdyn_tile_extent, rcmdyn_tile_extent_cfg, rcmdyn_exchange_plan
   public :: rcmdyn_overlap_shares, rcmdyn_runtime_info, rcmdyn_last_step_ms, rcmdyn_set_diagnostics
   public :: rcmdyn_kernel_times
   public :: rcmdyn_comm_unique_id, gpu_dyn_check, gpu_put3d, gpu_get3d, gpu_put2d, gpu_get2d

@@ -150,6 +150,11 @@ program test_shim
       read(10) j1, i1, n, m, k1
       ierr = rcmdyn_tile_extent(j1, i1, n, m, k1, ext, bdy)
       if ( ierr == 0 ) write(11) ext, bdy
+    case ( 25 )
+      ! the extents of tile n of cfg's decomposition, with its periodic directions
+      read(10) n
+      ierr = rcmdyn_tile_extent_cfg(cfg, n, ext, bdy)
+      if ( ierr == 0 ) write(11) ext, bdy
     case ( 21 )
       ! the plan of rank cfg%comm_rank: size it, then fetch it
       read(10) n

@@ -90,6 +90,29 @@ def test_tile_extents_partition_domain():
     assert widths == [33, 32, 32]
 
 
+@pytest.mark.parametrize("band,crm", [(1, 0), (0, 1), (1, 1)])
+def test_tile_extents_periodic(band, crm):
+    """rcmdyn_tile_extent_cfg: a periodic direction (i_band: j, i_crm: i) has no boundary side
+    on any tile and its cross range takes every point (mod_mppparam.F90:1131-1132, 1340-1360);
+    the tiles still cover the dot grid exactly once, and the other direction is unchanged."""
+    jx, iy = 97, 50
+    cj, ci = 3, 2
+    cover = [[0] * (jx + 1) for _ in range(iy + 1)]
+    for t in range(cj * ci):
+        ext, bdy = dycore.tile_extent(jx, iy, cj, ci, t, i_band=band, i_crm=crm)
+        plain, pbdy = dycore.tile_extent(jx, iy, cj, ci, t)
+        jde1, jde2, ide1, ide2, jce1, jce2, ice1, ice2 = ext
+        assert ext[:4] == plain[:4]
+        for i in range(ide1, ide2 + 1):
+            for j in range(jde1, jde2 + 1):
+                cover[i][j] += 1
+        assert jce2 == (jde2 if band else plain[5])
+        assert ice2 == (ide2 if crm else plain[7])
+        assert bdy[:2] == ([0, 0] if band else pbdy[:2])
+        assert bdy[2:] == ([0, 0] if crm else pbdy[2:])
+    assert all(cover[i][j] == 1 for i in range(1, iy + 1) for j in range(1, jx + 1))
+
+
 def test_band_refused_for_nonhydrostatic():
     import dataclasses
     from regcm_amd.config import CONFIGS

@@ -34,7 +34,7 @@ EXE = os.path.join(FDIR, "test_shim")
 # op codes of test_shim.F90
 END, CREATE, DESTROY, PUT, GET, TEND, BDYVAL, STEP, PRE, POST, BDYIN, SYNC = range(12)
 SET_TIME, GET_TIME, SET_DIAG, REDUCTIONS, DIAGNOSTICS, LAST_MS, RUNTIME = range(12, 19)
-SET_NPROC, TILE_EXTENT, PLAN, SHARES, KTIMES, SOFT = range(19, 25)
+SET_NPROC, TILE_EXTENT, PLAN, SHARES, KTIMES, SOFT, TILE_EXTENT_CFG = range(19, 26)
 
 
 def _build():
@@ -126,6 +126,10 @@ class Script:
             elif code == TILE_EXTENT:
                 ext, bdy = (ctypes.c_int32 * 8)(), (ctypes.c_int32 * 4)()
                 rc = L.rcmdyn_tile_extent(*a, ext, bdy)
+                res = [tuple(ext) + tuple(bdy)]
+            elif code == TILE_EXTENT_CFG:
+                ext, bdy = (ctypes.c_int32 * 8)(), (ctypes.c_int32 * 4)()
+                rc = L.rcmdyn_tile_extent_cfg(ctypes.byref(self.cfg), a[0], ext, bdy)
                 res = [tuple(ext) + tuple(bdy)]
             elif code == PLAN:
                 n = ctypes.c_int64()
@@ -224,7 +228,7 @@ class Script:
                 out.append(bytes(arr(1024, np.uint8)).split(b"\0", 1)[0].decode())
             elif code == SET_NPROC:
                 out.append(take("<2i"))
-            elif code == TILE_EXTENT:
+            elif code in (TILE_EXTENT, TILE_EXTENT_CFG):
                 out.append(take("<12i"))
             elif code == PLAN:
                 n, = take("<q")
@@ -273,6 +277,14 @@ def test_fortran_host_only_entry_points(c1_data):
     py, fo = s.run_python(), s.run_fortran()
     assert_same(py, fo)
     assert py[3] == (2, 4) and py[-2].shape[0] > 0
+    # the band-aware extents (i_band = 1: no west/east side, the cross range ends at jx)
+    band = build_config(dataclasses.replace(c3, i_band=1), split3, 2, 4, tile_first=0, tile_count=8)
+    s = Script(band)
+    for t in range(8):
+        s.add(TILE_EXTENT_CFG, t)
+    py, fo = s.run_python(), s.run_fortran()
+    assert_same(py, fo)
+    assert py[7][5] == c3.jx and py[7][8:10] == (0, 0), py[7]
     bad = build_config(rc, data["split"])
     bad.i_band = 2
     s = Script(bad).soft().add(CREATE)

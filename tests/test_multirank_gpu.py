@@ -139,15 +139,19 @@ def test_job_reductions_over_ranks():
         assert abs(o[0] - ref[0]) <= 1e-12 * abs(ref[0]) and abs(o[1] - ref[1]) <= 1e-12 * abs(ref[1])
 
 
-def test_uw_kpbl_put_on_own_points():
+@pytest.mark.parametrize("band", [0, 1], ids=["lam", "band"])
+def test_uw_kpbl_put_on_own_points(band):
     """iuwvadv = 1 with each rank putting kpbl on its own cross points only (as the physics
     computes it): vadv4d ind = 3 of the fused step reads kpbl on the ghost ring
     k_scalars computes in place of the cqv/cqc exchange, so the engine exchanges a put kpbl once
-    before the next tend.  Bit-identical to the single tile with the global put."""
+    before the next tend.  Bit-identical to the single tile with the global put.  The band's
+    ranks take their points from the band-aware extents (rcmdyn_tile_extent_cfg): the last tile
+    column's cross range then ends at jx, not jx - 1."""
     import dataclasses
     from regcm_amd.dycore import tile_extent
-    rc = dataclasses.replace(CONFIGS["C1"], ibltyp=2, iuwvadv=1)
-    base = icbc.generate(CONFIGS["C1"])
+    rc0 = dataclasses.replace(CONFIGS["C1"], i_band=band)
+    rc = dataclasses.replace(rc0, ibltyp=2, iuwvadv=1)
+    base = icbc.generate(rc0)
     st = dict(base["state"], **icbc.tke_state(rc))
     st.update(icbc.hydrometeor_state(rc, st, nqx=2))
     rng = np.random.default_rng(5)
@@ -155,8 +159,9 @@ def test_uw_kpbl_put_on_own_points():
     cj, ci = 2, 2
 
     def own_kpbl(e, r):
-        ext, _ = tile_extent(rc.jx, rc.iy, cj, ci, r)
+        ext, _ = tile_extent(rc.jx, rc.iy, cj, ci, r, i_band=band)
         j1, j2, i1, i2 = ext[4], ext[5], ext[6], ext[7]
+        assert not band or r // ci < cj - 1 or j2 == rc.jx
         e.put("KPBL", kpbl[:, i1 - 1:i2, j1 - 1:j2], j1=j1, i1=i1)
 
     data = {"split": base["split"], "state": st}
