@@ -674,6 +674,8 @@ int orc_get_work(orc_t* o, const char* name, double* dst, size_t cap) {
   else if (o->nh && !strcmp(name, "pr1")) a = o->pr1;
   else if (o->nh && !strcmp(name, "rho1")) a = o->rho1;
   else if (!strcmp(name, "ct")) a = o->ct;
+  else if (!strcmp(name, "qdynv")) a = o->qdyn[0];
+  else if (!strcmp(name, "qdync")) a = o->qdyn[1];
   else if (!strcmp(name, "cqv")) a = o->cq[0];
   else if (!strcmp(name, "cqc")) a = o->cq[1];
   else if (o->nqx > 2 && !strcmp(name, "cqi")) a = o->cq[2];
@@ -1567,6 +1569,7 @@ static int advection(orc_t* o) {
     /* slhadv_x / hdvg_x of qv and the hydrometeors (:1361-1363, 1378-1380); the reference runs
      * the qv pass, then vadv of qv, then the qx pass: the passes touch disjoint qxdyn planes */
     bad = sl_advection(o);
+    if (o->tend_probe == 3) return bad;     /* test hook: qxdyn holds the semi-Lagrangian terms only */
     vadvqv(o);
   } else {
     hadv_scalar(o, o->xq[0], o->qdyn[0], 2); /* hadvqv */
@@ -2361,6 +2364,7 @@ static int nh_advection(orc_t* o) {
   nh_theta_advection(o);                      /* ithadv = 1, :1347-1356 */
   if (o->cfg.isladvec == 1) {                 /* :1361-1363, 1378-1380, as in advection() */
     bad = sl_advection(o);
+    if (o->tend_probe == 3) return bad;     /* test hook: qxdyn holds the semi-Lagrangian terms only */
     vadvqv(o);
   } else {
     hadv_scalar(o, o->xq[0], o->qdyn[0], 2);
@@ -3138,6 +3142,7 @@ int orc_tend(orc_t* o) {
   memset(o->vten, 0, n3 * 8); memset(o->vdyn, 0, n3 * 8);
   for (int n = 0; n < o->nqx; n++) { memset(o->qten[n], 0, n3 * 8); memset(o->qdyn[n], 0, n3 * 8); }
   int slbad = advection(o);
+  if (o->tend_probe == 3 && o->cfg.isladvec == 1) return 0;
   if (o->cfg.ibltyp == 2) tke_tend(o);
   curvature(o);
   adiabatic(o);

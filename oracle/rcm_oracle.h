@@ -63,7 +63,8 @@ void orc_set_sound_probe(orc_t* o, int nsub);
 /* test hook: the hydrostatic tend returns early (without advancing the clock): 1 = after every
  * tendency is summed and the t / qx forecasts and their negative fix are formed (work arrays
  * "ct", "cqv", "cqc"), before any time filter; 2 = after the time filters, at the entry of
- * splitf; 0 (default) runs tend whole */
+ * splitf; 3 (isladvec = 1) = right after the semi-Lagrangian pass, whose terms are then all the
+ * qv / qc dynamic tendencies hold (work arrays "qdynv", "qdync"); 0 (default) runs tend whole */
 void orc_set_tend_probe(orc_t* o, int stage);
 void orc_set_time(orc_t* o, long long lcount, double dt, double xbctime);
 void orc_get_time(const orc_t* o, long long* lcount, double* dt, double* xbctime);

@@ -1319,20 +1319,26 @@ def test_nh_oracle_threads_match_single_tile(nthreads, variant):
         assert np.array_equal(par.get(name), ref.get(name)), name
 
 
-def test_nh_sound_substep_matches_numpy_restatement():
+@pytest.mark.parametrize("ifupr", [0, 1])
+def test_nh_sound_substep_matches_numpy_restatement(ifupr):
     """One acoustic sub-step of sound (Main/mod_sound.F90:249-682, the first sub-step of the
-    first step, upper radiative condition off: ifupr = 0) against an independent NumPy
-    restatement, from the state sound starts with (the oracle stopped right after sound's
-    set-up, orc_set_sound_probe(0)) to the state after the sub-step (probe 1): dp'/dp0, the
-    pressure-gradient update of u and v (:266-296), the lower boundary w and the lid, the
-    coefficients cc, cdd, cj, ca, g1, g2 and the Ikawa tridiagonal (a, b, c, rhs; :322-457),
-    the pp predictor (:459-468), the upward elimination and the downward w sweep
-    (:470-479, 566-573), the zero-gradient w on the boundary ring (:577-607), the new pp, pi
-    and the dp'/dt temperature correction of atm1 and atm2 t (:661-680)."""
+    first step) against an independent NumPy restatement, from the state sound starts with (the
+    oracle stopped right after sound's set-up, orc_set_sound_probe(0)) to the state after the
+    sub-step (probe 1): dp'/dp0, the pressure-gradient update of u and v (:266-296), the lower
+    boundary w, the coefficients cc, cdd, cj, ca, g1, g2 and the Ikawa tridiagonal (a, b, c,
+    rhs; :322-457), the pp predictor (:459-468), the upward elimination and the downward w
+    sweep (:470-479, 566-573), the zero-gradient w on the boundary ring (:577-607), the new pp,
+    pi and the dp'/dt temperature correction of atm1 and atm2 t (:661-680).  The lid: w = 0
+    (ifupr = 0), or the upper radiative condition (ifupr = 1, :486-562): estore and astore
+    from the elimination's top coefficients, the day-alarm means abar and rhon over the
+    interior (rnpts of init_sound, :120), the 13 x 13 tmask from the fi, fj, fk, fl weights
+    (:126-141, 523-543) and its convolution of estore with the indices clamped to the interior
+    (:551-561).  The transcendental terms (the tmask's sin / cos) make it <= 1e-11 relative."""
     import dataclasses
+    import math
     from oracle.oracle import OracleCore
     from regcm_amd import constants as C
-    rc = dataclasses.replace(CONFIGS["N1"], ifupr=0)
+    rc = dataclasses.replace(CONFIGS["N1"], ifupr=ifupr)
     data = icbc.generate_nh(rc)
     runs = []
     for probe in (0, 1):
@@ -1401,6 +1407,7 @@ def test_nh_sound_substep_matches_numpy_restatement():
     ppnew = pp.copy()
     pinew = np.zeros_like(pp)
     a1t, a2tn = a["ATM1_T"].copy(), a["ATM2_T"].copy()
+    cols = {}
     for i in range(2, iy - 1):
         for j in range(2, jx - 1):
             wo = [None] + [W(k, i, j) for k in range(1, kp + 1)]
@@ -1466,7 +1473,50 @@ def test_nh_sound_substep_matches_numpy_restatement():
                 den = aa[k] * e[k] + bb[k]
                 e[k - 1] = -cq[k] / den
                 f[k - 1] = (rhs[k] - f[k] * aa[k]) / den
-            wk[1] = 0.0
+            cols[(j, i)] = (wo, e, f, cj, cdd, wk, pold, pc)
+    wpval = {c: 0.0 for c in cols}
+    if ifupr:
+        # :486-493: estore, astore at every interior column (pc[1]: the predicted pp at k = 1)
+        est, ast = {}, {}
+        for (j, i), (wo, e, f, cj, cdd, wk, pold, pc) in cols.items():
+            den = (cdd[1] + cj[1]) * bp
+            est[(j, i)] = pc[1] + f[1] * den
+            ast[(j, i)] = den * e[1] + (cj[1] - cdd[1]) * bp
+        # :506-543, the day alarm on the first step: the means and the mask
+        atot = rhontot = 0.0
+        for i in range(2, iy - 1):
+            for j in range(2, jx - 1):
+                atot = atot + ast[(j, i)]
+                ensq = egrav * egrav / cpd / (a2t[0][i - 1][j - 1] * rpsb[i - 1, j - 1])
+                rhontot = rhontot + rho1[0][i - 1][j - 1] * math.sqrt(ensq)
+        rnpts = 1.0 / float(((iy - 1) - 2) * ((jx - 1) - 2))
+        abar, rhon = atot * rnpts, rhontot * rnpts
+        dxmsfb = 2.0 / (dx * dx) / data["split"]["nh_xmsf"]
+        fk = [1.0] + [2.0] * 5 + [1.0]
+        fw = {n: (0.5 if abs(n) == 6 else 1.0) for n in range(-6, 7)}
+        tmask = {(jj, ii): 0.0 for ii in range(-6, 7) for jj in range(-6, 7)}
+        for kk in range(7):
+            for ll in range(7):
+                xkeff = dxmsfb * math.sin(math.pi * kk / 12.0) * math.cos(math.pi * ll / 12.0)
+                xleff = dxmsfb * math.sin(math.pi * ll / 12.0) * math.cos(math.pi * kk / 12.0)
+                xkleff = math.sqrt(xkeff * xkeff + xleff * xleff)
+                for ii in range(-6, 7):
+                    for jj in range(-6, 7):
+                        tmask[(jj, ii)] = tmask[(jj, ii)] + (fw[ii] * fw[jj] * fk[kk] * fk[ll]) / 144.0 * \
+                            math.cos(2.0 * math.pi * kk * ii / 12.0) * math.cos(2.0 * math.pi * ll * jj / 12.0) * \
+                            xkleff / (rhon - abar * xkleff)
+        # :551-561: the convolution, indices clamped to icross1+1 .. icross2-1
+        for (j, i) in cols:
+            acc = 0.0
+            for ii in range(-6, 7):
+                inn = min(max(2, i + ii), (iy - 1) - 1)
+                for jj in range(-6, 7):
+                    jnn = min(max(2, j + jj), (jx - 1) - 1)
+                    acc = acc + est[(jnn, inn)] * tmask[(jj, ii)]
+            wpval[(j, i)] = acc
+        assert max(abs(x) for x in wpval.values()) > 1e-6      # the lid moves
+    for (j, i), (wo, e, f, cj, cdd, wk, pold, pc) in cols.items():
+            wk[1] = wpval[(j, i)]
             for k in range(1, kz + 1):
                 wk[k + 1] = e[k] * wk[k] + f[k]
             for k in range(1, kp + 1):

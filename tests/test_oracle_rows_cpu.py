@@ -595,3 +595,130 @@ def test_bdyval_matches_numpy_restatement(variant):
     if rc.iboudy in (3, 4):
         plain = _bdyval_np(g, dataclasses.replace(rc, iboudy=5), s, b, lc, dt, xbc)
         assert not np.array_equal(want["ATM1_QV"], plain["ATM1_QV"])
+
+
+# ------------------------------------------------------------------- semi-Lagrangian pass
+
+def _sladvection_np(g, rc, u1, v1, psa, msfx, msfd, a2q, a1q, dt):
+    """One semi-Lagrangian pass of the moisture species (isladvec = 1,
+    Main/mod_tendency.F90:1361-1363, 1378-1380): ua = atmx%umd = (atm1%u/psdota)*msfd
+    (decouple :889, :999-1000; psdota = psc2psd of the step's p*), adv_velocity (.false.)
+    (Main/mod_sladvection.F90:91-114, vadym1 reads va(j+1,i) twice as written), trajcalc_x
+    (:134-222: the departure point to third order in dt, dtsq/dtcb of Main/mod_tendency.F90:
+    614-615, the fatal check, the indices clamped to the boundary lines), slhadv_x4d (:425-470:
+    bilinear outer rows, cubic inner rows, the cubic in y, the quasi-monotone clamp when
+    iqmsl = 1, the dlowval test) and hdvg_x4d (:621-657).  Returns {species: tendency}."""
+    psdota = _psc2psd_np(g, psa)
+    rps = np.zeros_like(psdota)
+    Jd, Id = g.box(g.jde1, g.jde2, g.ide1, g.ide2)
+    g.put(rps, Jd, Id, 1.0 / g.at(psdota, Jd, Id))
+    ua, va = u1 * rps * msfd, v1 * rps * msfd
+    dx = rc.ds * 1000.0
+    ddx = ddy = dx
+    dtsq, dtcb = dt * dt, dt * dt * dt
+    out = {n: np.zeros_like(q) for n, q in a2q.items()}
+
+    def U(k, j, i):
+        return ua[k, i - 1, g.wrap(np.array(j)) - 1]
+
+    def Va(k, j, i):
+        return va[k, i - 1, g.wrap(np.array(j)) - 1]
+
+    def mx(j, i):
+        return msfx[i - 1, g.wrap(np.array(j)) - 1]
+
+    def md(j, i):
+        return msfd[i - 1, g.wrap(np.array(j)) - 1]
+
+    for k in range(rc.kz):
+        for i in range(g.ici1, g.ici2 + 1):
+            for j in range(g.jci1, g.jci2 + 1):
+                uadvx = 0.25 * (U(k, j, i) + U(k, j, i + 1) + U(k, j + 1, i + 1) + U(k, j + 1, i)) / mx(j, i)
+                uadxp1 = 0.25 * (U(k, j + 1, i) + U(k, j + 1, i + 1) + U(k, j + 2, i + 1) + U(k, j + 2, i)) / mx(j + 1, i)
+                uadxm1 = 0.25 * (U(k, j, i) + U(k, j, i + 1) + U(k, j - 1, i + 1) + U(k, j - 1, i)) / mx(j - 1, i)
+                vadvy = 0.25 * (Va(k, j, i) + Va(k, j, i + 1) + Va(k, j + 1, i + 1) + Va(k, j + 1, i)) / mx(j, i)
+                vadyp1 = 0.25 * (Va(k, j, i + 1) + Va(k, j + 1, i + 1) + Va(k, j + 1, i + 2) + Va(k, j, i + 2)) / mx(j, i + 1)
+                vadym1 = 0.25 * (Va(k, j, i) + Va(k, j, i - 1) + Va(k, j + 1, i) + Va(k, j + 1, i)) / mx(j, i - 1)
+                ux = 0.5 * (uadxp1 - uadxm1) / ddx
+                uxx = (uadxp1 - 2.0 * uadvx + uadxm1) / (ddx * ddx)
+                xdis = -uadvx * dt + 0.5 * (dtsq * uadvx * ux) - (dtcb * uadvx) * (ux * ux + uadvx * uxx) / 6.0
+                xn = xdis / ddx
+                xnp = int(xn)
+                assert abs(xnp) <= 1                              # else fatal('SLADVECTION')
+                alfax = abs((xnp * ddx - xdis) / ddx)
+                xsn = int(math.copysign(1.0, xn))
+                xnd = j + xnp
+                xm1 = xnd + xsn
+                xm2 = xm1 + xsn
+                xp1 = xnd - xsn
+                if g.bl:
+                    xnd, xm1, xm2, xp1 = (max(x, g.jce1) for x in (xnd, xm1, xm2, xp1))
+                if g.br:
+                    xnd, xm1, xm2, xp1 = (min(x, g.jce2) for x in (xnd, xm1, xm2, xp1))
+                vy = 0.5 * (vadyp1 - vadym1) / ddy
+                vyy = (vadyp1 - 2.0 * vadvy + vadym1) / (ddy * ddy)
+                ydis = -vadvy * dt + 0.5 * (dtsq * vadvy * vy) - (dtcb * vadvy) * (vy * vy + vadvy * vyy) / 6.0
+                yn = ydis / ddy
+                ynp = int(yn)
+                assert abs(ynp) <= 1
+                betay = abs((ynp * ddy - ydis) / ddy)
+                ysn = int(math.copysign(1.0, yn))
+                ynd = i + ynp
+                ym1 = ynd + ysn
+                ym2 = ym1 + ysn
+                yp1 = ynd - ysn
+                ynd, ym1, ym2, yp1 = (min(max(y, g.ice1), g.ice2) for y in (ynd, ym1, ym2, yp1))
+                alfm2 = -(alfax * (1.0 - alfax * alfax)) / 6.0
+                alfm1 = (alfax * (1.0 + alfax) * (2.0 - alfax)) / 2.0
+                alf0 = ((1.0 - alfax * alfax) * (2.0 - alfax)) / 2.0
+                alfp1 = -(alfax * (1.0 - alfax) * (2.0 - alfax)) / 6.0
+                betm2 = -(betay * (1.0 - betay * betay)) / 6.0
+                betm1 = (betay * (1.0 + betay) * (2.0 - betay)) / 2.0
+                bet0 = ((1.0 - betay * betay) * (2.0 - betay)) / 2.0
+                betp1 = -(betay * (1.0 - betay) * (2.0 - betay)) / 6.0
+                ucapf = (U(k, j + 1, i + 1) * md(j + 1, i + 1) + U(k, j + 1, i) * md(j + 1, i)) * 0.5
+                ucapi = (U(k, j, i + 1) * md(j, i + 1) + U(k, j, i) * md(j, i)) * 0.5
+                vcapf = (Va(k, j + 1, i + 1) * md(j + 1, i + 1) + Va(k, j, i + 1) * md(j, i + 1)) * 0.5
+                vcapi = (Va(k, j + 1, i) * md(j + 1, i) + Va(k, j, i) * md(j, i)) * 0.5
+                hdvg = ((ucapf - ucapi) / dx + (vcapf - vcapi) / dx) / (mx(j, i) * mx(j, i))
+                for n, q in a2q.items():
+                    def Q(jj, ii):
+                        return q[k, ii - 1, g.wrap(np.array(jj)) - 1]
+                    bl1 = alfax * Q(xm1, yp1) + (1.0 - alfax) * Q(xnd, yp1)
+                    bl2 = alfax * Q(xm1, ym2) + (1.0 - alfax) * Q(xnd, ym2)
+                    cb1 = alfm2 * Q(xm2, ynd) + alfm1 * Q(xm1, ynd) + alf0 * Q(xnd, ynd) + alfp1 * Q(xp1, ynd)
+                    cb2 = alfm2 * Q(xm2, ym1) + alfm1 * Q(xm1, ym1) + alf0 * Q(xnd, ym1) + alfp1 * Q(xp1, ym1)
+                    tbadp = betm2 * bl2 + betm1 * cb2 + bet0 * cb1 + betp1 * bl1
+                    tsla = tbadp
+                    if rc.iqmsl == 1:
+                        four = (Q(xnd, ynd), Q(xnd, ym1), Q(xm1, ynd), Q(xm1, ym1))
+                        tbmax, tbmin = max(four), min(four)
+                        tsla = tbmax if tbadp > tbmax else (tbmin if tbadp < tbmin else tbadp)
+                    ften = 0.0
+                    if abs(tsla - Q(j, i)) > 1.0e-20:                # dlowval, Share/mod_constants.F90:68
+                        ften = ften + (tsla - Q(j, i)) / dt
+                    a1 = a1q[n][k, i - 1, j - 1]
+                    tatot = a1 * hdvg if a1 > np.finfo(np.float64).eps else 0.0
+                    out[n][k, i - 1, j - 1] = ften - tatot
+    return out
+
+
+@pytest.mark.parametrize("variant", [{}, {"iqmsl": 0}, {"band": True}], ids=["qmsl", "plain", "band"])
+def test_semi_lagrangian_pass_matches_numpy_restatement(variant):
+    """The qv / qc semi-Lagrangian terms of one tend (the oracle stopped right after the pass,
+    probe 3) equal the NumPy trajcalc_x + slhadv_x4d + hdvg_x4d bit for bit."""
+    variant = dict(variant)
+    band = variant.pop("band", False)
+    rc, data, st = _case(band=band, isladvec=1, **variant)
+    o = _oracle(rc, data, st, probe=3)
+    g = Grid(rc)
+    s = {n: o.get(n) for n in ("ATM1_U", "ATM1_V", "PSA", "MSFX", "MSFD", "ATM1_QV", "ATM1_QC", "ATM2_QV", "ATM2_QC")}
+    _, dt, _ = o.get_time()
+    o.tend()
+    want = _sladvection_np(g, rc, s["ATM1_U"], s["ATM1_V"], s["PSA"][0], s["MSFX"][0], s["MSFD"][0],
+                           {"v": s["ATM2_QV"], "c": s["ATM2_QC"]}, {"v": s["ATM1_QV"], "c": s["ATM1_QC"]}, dt)
+    J, I = g.box(g.jci1, g.jci2, g.ici1, g.ici2)
+    for n in ("v", "c"):
+        got = o.get_work("qdyn" + n)
+        assert np.array_equal(g.at(got, J, I), g.at(want[n], J, I)), n
+        assert np.abs(g.at(want[n], J, I)).max() > 0.0

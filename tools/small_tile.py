@@ -32,6 +32,27 @@ if "--shares" in sys.argv:
     shares()
     sys.exit(0)
 
+if "--nh" in sys.argv:
+    # the non-hydrostatic C5 domain (768x768x41, 3 km) on the 8-GPU tiling (2x4): each rank's
+    # 384x192x41 tile as one single-tile run, its step without any exchange (the floor the
+    # 8-GPU C5 run sees per rank), then its per-kernel times
+    rc = dataclasses.replace(CONFIGS["C5"], jx=384, iy=192)
+    data = icbc.generate_nh(rc)
+    e = DynCore(rc, data["split"])
+    e.put_state(data["state"])
+    e.bdyval()
+    e.step(6)
+    e.synchronize()
+    t0 = time.perf_counter()
+    e.step(40)
+    e.synchronize()
+    dt = (time.perf_counter() - t0) / 40
+    print(f"C5 physics on 384x192x{rc.kz} (the 8-GPU rank tile): {dt * 1e3:.3f} ms/step", flush=True)
+    kt = e.kernel_times(3)
+    for name, (n, us) in sorted(kt.items(), key=lambda kv: -kv[1][1] * kv[1][0]):
+        print(f"  {name:32s} {n / 3:4.1f}/step {us * 1e3:9.2f} us")
+    sys.exit(0)
+
 for jx, iy in ((192, 192), (96, 192), (96, 96), (96, 48)):
     rc = dataclasses.replace(CONFIGS["C3"], jx=jx, iy=iy)
     data = icbc.generate(rc)
