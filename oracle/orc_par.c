@@ -28,7 +28,7 @@
 #define MAXT 256
 
 struct orc_par {
-  int ntiles, cj, ci, kz, jx, iy, band;
+  int ntiles, cj, ci, kz, jx, iy, band, crm;
   double* glob[3];                   /* whole-domain gathers of the NH radiative condition */
   orc_t* t[MAXT];
   int info[MAXT][16];
@@ -48,10 +48,12 @@ static int recv_dir(int sides, int d) {
   return d == 1 || d == 3 || d == 7;                     /* exchange_rt: from R, T, TR */
 }
 
-/* a band (i_band = 1) is periodic in j (Main/mpplib/mod_mppparam.F90:1131 dim_period(1)) */
+/* a band (i_band = 1) is periodic in j (Main/mpplib/mod_mppparam.F90:1131 dim_period(1)),
+ * CRM (i_crm = 1) in i as well (:1132 dim_period(2)) */
 static int peer_of(const orc_par_t* p, int tile, int d) {
   int lj = tile / p->ci + DJ[d], li = tile % p->ci + DI[d];
   if (p->band) lj = (lj + p->cj) % p->cj;
+  if (p->crm) li = (li + p->ci) % p->ci;
   return (lj >= 0 && lj < p->cj && li >= 0 && li < p->ci) ? lj * p->ci + li : -1;
 }
 /* offset from a ghost column's j to the same column in the frame of the tile across the
@@ -61,6 +63,15 @@ static int jwrap(const orc_par_t* p, int tile, int d) {
   const int lj = tile / p->ci;
   if (DJ[d] < 0 && lj == 0) return p->jx;
   if (DJ[d] > 0 && lj == p->cj - 1) return -p->jx;
+  return 0;
+}
+
+/* the same for a ghost row across the CRM period in i */
+static int iwrap(const orc_par_t* p, int tile, int d) {
+  if (!p->crm) return 0;
+  const int li = tile % p->ci;
+  if (DI[d] < 0 && li == 0) return p->iy;
+  if (DI[d] > 0 && li == p->ci - 1) return -p->iy;
   return 0;
 }
 
@@ -107,7 +118,7 @@ static void xfn(void* ctx, double* a, int nk, int nex, int sides) {
     const double* src = arrived(p, me, d, &q);
     const int* g = p->info[q];
     const size_t pq = (size_t)g[2] * g[3];
-    const int sj = jwrap(p, me, d);
+    const int sj = jwrap(p, me, d), si = iwrap(p, me, d);
     int j1 = f[4], j2 = f[5], i1 = f[6], i2 = f[7];      /* ghost box received from d */
     if (DJ[d] < 0) { j1 = f[4] - nex; j2 = f[4] - 1; }
     if (DJ[d] > 0) { j1 = f[5] + 1; j2 = f[5] + nex; }
@@ -117,7 +128,7 @@ static void xfn(void* ctx, double* a, int nk, int nex, int sides) {
       for (int i = i1; i <= i2; i++)
         for (int j = j1; j <= j2; j++)
           a[k * pl + (size_t)(i - f[1]) * f[2] + (j - f[0])] =
-              src[k * pq + (size_t)(i - g[1]) * g[2] + (j + sj - g[0])];
+              src[k * pq + (size_t)(i + si - g[1]) * g[2] + (j + sj - g[0])];
     ack(p, me, q, d);
   }
   drain(p, me, out);
@@ -144,7 +155,7 @@ static void bfn(void* ctx, double* s, int nk, int along) {
     const int* g = p->info[q];
     const int nq = along == 0 ? g[2] : g[3], oq = along == 0 ? g[0] : g[1];
     const int x = side == 0 ? lo - 1 : hi + 1;         /* owned by the peer */
-    const int sx = along == 0 ? jwrap(p, me, d) : 0;
+    const int sx = along == 0 ? jwrap(p, me, d) : iwrap(p, me, d);
     for (int k = 0; k < nk; k++) s[(size_t)k * n + (x - o0)] = src[(size_t)k * nq + (x + sx - oq)];
     ack(p, me, q, d);
   }
@@ -172,7 +183,7 @@ orc_par_t* orc_par_create(const rcmdyn_config* cfg) {
   if (nt < 1 || nt > MAXT || (cfg->idynamic != 1 && cfg->idynamic != 2)) return NULL;
   orc_par_t* p = (orc_par_t*)calloc(1, sizeof(orc_par_t));
   p->ntiles = nt; p->cj = cfg->nproc_j; p->ci = cfg->nproc_i; p->kz = cfg->kz;
-  p->jx = cfg->jx; p->iy = cfg->iy; p->band = cfg->i_band == 1;
+  p->jx = cfg->jx; p->iy = cfg->iy; p->band = cfg->i_band == 1; p->crm = cfg->i_crm == 1;
   if (cfg->idynamic == 2 && nt > 1)
     for (int q = 0; q < 3; q++) p->glob[q] = (double*)calloc((size_t)cfg->jx * cfg->iy, sizeof(double));
   for (int t = 0; t < nt; t++) {

@@ -178,9 +178,23 @@ static void band_self_xch(orc_t* o, double* a, int nk, int nex, int sides) {
         if (sides != 1) A3(a, o->jde2 + w, i, k) = A3(a, o->jde2 + w - jx, i, k);
       }
 }
+/* CRM (i_crm = 1, with the band) on one tile in i is its own south and north neighbour
+ * (Main/mpplib/mod_mppparam.F90:1104-1108, 1132): the rows past either end of the period,
+ * every column of the frame the j pass filled (so the corners wrap in both directions) */
+static void crm_self_xch(orc_t* o, double* a, int nk, int nex, int sides) {
+  const int iy = o->iy;
+  const int j1 = o->cfg.nproc_j == 1 ? o->jde1 - nex : o->jde1, j2 = o->cfg.nproc_j == 1 ? o->jde2 + nex : o->jde2;
+  for (int k = 1; k <= nk; k++)
+    for (int w = 1; w <= nex; w++)
+      for (int j = j1; j <= j2; j++) {
+        if (sides != 2) A3(a, j, o->ide1 - w, k) = A3(a, j, o->ide1 - w + iy, k);
+        if (sides != 1) A3(a, j, o->ide2 + w, k) = A3(a, j, o->ide2 + w - iy, k);
+      }
+}
 static void xch(orc_t* o, double* a, int nk, int nex, int sides) {
-  if (o->xfn) o->xfn(o->xctx, a, nk, nex, sides);
-  else if (o->cfg.i_band && o->cfg.nproc_j == 1) band_self_xch(o, a, nk, nex, sides);
+  if (o->xfn) { o->xfn(o->xctx, a, nk, nex, sides); return; }
+  if (o->cfg.i_band && o->cfg.nproc_j == 1) band_self_xch(o, a, nk, nex, sides);
+  if (o->cfg.i_crm && o->cfg.nproc_i == 1) crm_self_xch(o, a, nk, nex, sides);
 }
 /* the boundary slices along j (south / north) exchange their entries one past the tile with
  * the left / right tiles (exchange_bdy_lr, Main/mod_bdycod.F90:1063-1089): around the period
@@ -196,7 +210,7 @@ static void xchb(orc_t* o, double* s, int along) {
 }
 
 /* ---- set_nproc tile extents, Main/mpplib/mod_mppparam.F90:1295-1360 ---- */
-static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band) {
+static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4], int band, int crm) {
   int lj = tile / ci, li = tile % ci;
   int jxp = jx / cj, iyp = iy / ci;
   int js = lj * jxp + 1, is = li * iyp + 1;
@@ -213,11 +227,13 @@ static void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], in
   /* a band (i_band = 1) is periodic in j: no west/east boundary, and the cross grid takes every
    * j (global_cross_jend = global_dot_jend, Main/mpplib/mod_mppparam.F90:1351-1354) */
   ext[4] = js; ext[5] = (je == jx && !band) ? je - 1 : je;
-  ext[6] = is; ext[7] = (ie == iy) ? ie - 1 : ie;
-  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band; bdy[2] = (li == 0); bdy[3] = (li == ci - 1);
+  /* CRM (i_crm = 1): the same in i (dim_period(2), global_cross_iend = global_dot_iend, :1340-1342) */
+  ext[6] = is; ext[7] = (ie == iy && !crm) ? ie - 1 : ie;
+  bdy[0] = (lj == 0) && !band; bdy[1] = (lj == cj - 1) && !band;
+  bdy[2] = (li == 0) && !crm; bdy[3] = (li == ci - 1) && !crm;
 }
 
-/* ---- setup_boundaries, Main/mod_atm_interface.F90:383-542 (non-CRM) ---- */
+/* ---- setup_boundaries, Main/mod_atm_interface.F90:383-542 ---- */
 static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
   int jx = o->jx, iy = o->iy;
   int icx = ldot ? 0 : 1, icy = ldot ? 0 : 1;
@@ -227,6 +243,7 @@ static void setup_boundaries(orc_t* o, int ldot, signed char* rg, int* ib) {
   int jgbr1 = jx - icx - nsp + 2, jgbr2 = jx - icx - 1;
   for (int i = o->i0; i < o->i0 + o->ni; i++)
     for (int j = o->j0; j < o->j0 + o->nj; j++) { A2(rg, j, i) = 0; A2(ib, j, i) = -1; }
+  if (o->cfg.i_crm) return;      /* CRM: no relaxation band at all (:434, "if (.not. ma%crmflag)") */
   if (o->cfg.i_band) {
     /* a band (:435-455): the south and north rows only, every j ("j < jgbl1 .and. j > jgbr2"
      * skips none) */
@@ -289,17 +306,22 @@ orc_t* orc_create(const rcmdyn_config* cfg) {
   /* a non-hydrostatic tile of a decomposition needs the whole-domain gather of sound's upper
    * radiative condition (Main/mod_sound.F90:496-497): orc_set_gather, before the first step */
   if (cfg->idynamic != 1 && cfg->idynamic != 2) return NULL;
-  /* nqx from ipptls >= 1 (Main/mod_params.F90:1358-1366); a band (i_band = 1) for the
-   * hydrostatic core; CRM and chemistry not restated */
-  if (cfg->ipptls < 1 || cfg->nqx != (cfg->ipptls > 1 ? 5 : 2) || cfg->i_crm || cfg->ichem) return NULL;
-  if (cfg->i_band && (cfg->i_band != 1 || cfg->idynamic != 1)) return NULL;
+  /* nqx from ipptls >= 1 (Main/mod_params.F90:1358-1366); a band (i_band = 1) for both cores;
+   * CRM (i_crm = 1: periodic in i too, PreProc/CRM/crm_test.in) for the non-hydrostatic core
+   * over the band, with iboudy = 0 (fixed lateral values: no boundary line exists) or any
+   * other iboudy (none relaxes anything); chemistry not restated.  iboudy = 0 without CRM (the
+   * b0-only branches of bdyval) is not restated either. */
+  if (cfg->ipptls < 1 || cfg->nqx != (cfg->ipptls > 1 ? 5 : 2) || cfg->ichem) return NULL;
+  if (cfg->i_band != 0 && cfg->i_band != 1) return NULL;
+  if (cfg->i_crm && (cfg->i_crm != 1 || !cfg->i_band || cfg->idynamic != 2)) return NULL;
+  if (cfg->iboudy == 0 && !cfg->i_crm) return NULL;
   orc_t* o = (orc_t*)calloc(1, sizeof(orc_t));
   o->sound_probe = -1;
   o->cfg = *cfg;
   o->jx = cfg->jx; o->iy = cfg->iy; o->kz = cfg->kz; o->kzp1 = cfg->kz + 1;
   o->nsplit = cfg->nsplit; o->nqx = cfg->nqx;
   int ext[8], bdy[4];
-  tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy, cfg->i_band);
+  tile_extent(o->jx, o->iy, cfg->nproc_j, cfg->nproc_i, cfg->tile_first, ext, bdy, cfg->i_band, cfg->i_crm);
   o->bl = bdy[0]; o->br = bdy[1]; o->bb = bdy[2]; o->bt = bdy[3];
   /* Main/mod_atm_interface.F90:231-302 */
   o->jde1 = o->jdi1 = o->jdii1 = ext[0]; o->jde2 = o->jdi2 = o->jdii2 = ext[1];
@@ -649,6 +671,17 @@ int orc_put(orc_t* o, int field, const double* src, int j1, int j2, int i1, int 
           A3(a, j, i, k) = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (jw - j1)];
         }
     }
+    /* CRM: the frame rows past either end of the period take the wrapped row (and column) */
+    if (o->cfg.i_crm)
+      for (int i = o->i0; i < o->i0 + o->ni; i++) {
+        const int iw = i < 1 ? i + o->iy : (i > o->iy ? i - o->iy : i);
+        if (iw == i || iw < i1 || iw > i2) continue;
+        for (int j = o->j0; j < o->j0 + o->nj; j++) {
+          const int jw = !o->cfg.i_band ? j : (j < 1 ? j + o->jx : (j > o->jx ? j - o->jx : j));
+          if (jw < j1 || jw > j2) continue;
+          A3(a, j, i, k) = src[((size_t)(k - k1) * ni + (iw - i1)) * nj + (jw - j1)];
+        }
+      }
   }
   if (field == RCMDYN_MSFX || field == RCMDYN_MSFD || field == RCMDYN_HT) prepare_static(o);
   return 0;
@@ -2501,6 +2534,15 @@ static void nh_diffu_xk(orc_t* o, double* ften, const double* f, const double* x
 #undef LAP2
 }
 
+/* the global cross grid (Main/mpplib/mod_mppparam.F90:1486-1516): njcross / nicross points, and
+ * its interior jci / ici range (every point in a periodic direction) */
+static int njcross(const orc_t* o) { return o->cfg.i_band ? o->jx : o->jx - 1; }
+static int nicross(const orc_t* o) { return o->cfg.i_crm ? o->iy : o->iy - 1; }
+static int gcj1(const orc_t* o) { return o->cfg.i_band ? 1 : 2; }
+static int gcj2(const orc_t* o) { return o->cfg.i_band ? o->jx : o->jx - 2; }
+static int gci1(const orc_t* o) { return o->cfg.i_crm ? 1 : 2; }
+static int gci2(const orc_t* o) { return o->cfg.i_crm ? o->iy : o->iy - 2; }
+
 /* tau, Main/mod_bdycod.F90:5115-5123 */
 static double nh_tau(orc_t* o, double z, double zmax) {
   double rayhd = o->cfg.rayhd;
@@ -2535,7 +2577,8 @@ static void nh_raydamp_uv(orc_t* o) {
     for (int k = 1; k <= kmax; k++)
       for (int i = o->idi1; i <= o->idi2; i++)
         for (int j = o->jdi1; j <= o->jdi2; j++) {
-          double bval = A3(b0, j, i, k) + xt * A3(bt, j, i, k);
+          /* CRM: toward 0 (raydampuv_c with sval = d_zero, Main/mod_tendency.F90:467-469) */
+          double bval = o->cfg.i_crm ? d_zero : A3(b0, j, i, k) + xt * A3(bt, j, i, k);
           double zz = d_rfour * (A3(z, j, i, k) + A3(z, j - 1, i, k) + A3(z, j, i - 1, k) + A3(z, j - 1, i - 1, k));
           double zm = d_rfour * (A3(z, j, i, 1) + A3(z, j - 1, i, 1) + A3(z, j, i - 1, 1) + A3(z, j - 1, i - 1, 1));
           A3(ten, j, i, k) = A3(ten, j, i, k) + nh_tau(o, zz, zm) * (bval - A3(var, j, i, k));
@@ -2562,8 +2605,8 @@ static void nh_tmask(orc_t* o, const double* rpsb) {
       }
     const double* ga = o->gfn(o->xctx, o->astore, 1);
     const double* gr = o->gfn(o->xctx, o->s_tr, 2);
-    for (int i = 2; i <= o->iy - 2; i++)
-      for (int j = 2; j <= o->jx - 2; j++) {
+    for (int i = gci1(o); i <= gci2(o); i++)
+      for (int j = gcj1(o); j <= gcj2(o); j++) {
         atot = atot + ga[(size_t)(i - 1) * o->jx + (j - 1)];
         rhontot = rhontot + gr[(size_t)(i - 1) * o->jx + (j - 1)];
       }
@@ -2575,7 +2618,9 @@ static void nh_tmask(orc_t* o, const double* rpsb) {
         rhontot = rhontot + A3(o->rho1, j, i, 1) * sqrt(ensq);
       }
   }
-  double rnpts = d_one / (double)((o->iy - 3) * (o->jx - 3));
+  /* rnpts = 1/((nicross-2)*(njcross-2)), init_sound :120 (nicross = iy in CRM, njcross = jx in
+   * a band: the count then differs from the points summed, as in the reference) */
+  double rnpts = d_one / (double)((nicross(o) - 2) * (njcross(o) - 2));
   double abar = atot * rnpts, rhon = rhontot * rnpts;
   double dxmsfb = d_two / o->dxsq / o->cfg.nh_xmsf;
   memset(o->tmask, 0, sizeof(o->tmask));
@@ -2805,7 +2850,7 @@ static int nh_sound(orc_t* o) {
           A2(o->astore, j, i) = denom * A3(e, j, i, 1) + (A3(cj, j, i, 1) - A3(cdd, j, i, 1)) * bp;
         }
       if (day_alarm && it == 1) nh_tmask(o, rpsb);
-      int ilo = 2, ihi = o->iy - 2, jlo = 2, jhi = o->jx - 2;  /* icross1+1 .. icross2-1 */
+      int ilo = 2, ihi = nicross(o) - 1, jlo = 2, jhi = njcross(o) - 1;  /* icross1+1 .. icross2-1 */
       /* decomposed: the whole-domain estore (Main/mod_sound.F90:496-497) */
       const double* ge = o->gfn ? o->gfn(o->xctx, o->estore, 0) : NULL;
       for (int i = o->ici1; i <= o->ici2; i++)
@@ -3064,7 +3109,7 @@ static int nh_tend(orc_t* o) {
         A3(o->qten[0], j, i, k) = A3(o->qten[0], j, i, k) + 0.0;
         A3(o->qten[1], j, i, k) = A3(o->qten[1], j, i, k) + 0.0;
       }
-  if (o->cfg.ifrayd == 1) {                   /* :356-364 */
+  if (o->cfg.ifrayd == 1 && !o->cfg.i_crm) {  /* :356-364 (not in CRM mode) */
     nh_raydamp_x(o, o->z0, o->a2t, o->tten, o->tb0, o->tbt, kz);
     nh_raydamp_x(o, o->z0, o->a2q[0], o->qten[0], o->qb0, o->qbt, kz);
   }
@@ -3100,7 +3145,9 @@ static int nh_tend(orc_t* o) {
   /* Rayleigh damping of u, v, pp, w and decoupling of the tendencies (:466-499) */
   if (o->cfg.ifrayd == 1) {
     nh_raydamp_uv(o);
-    nh_raydamp_x(o, o->z0, o->a2pp, o->ppten, o->ppb0, o->ppbt, kz);
+    /* CRM: pp toward 0 (raydamp3f, :468-470), else toward its boundary values (raydamp3) */
+    if (o->cfg.i_crm) nh_raydamp_x(o, o->z0, o->a2pp, o->ppten, NULL, NULL, kz);
+    else nh_raydamp_x(o, o->z0, o->a2pp, o->ppten, o->ppb0, o->ppbt, kz);
     nh_raydamp_x(o, o->zf0, o->a2w, o->wten, NULL, NULL, kp);
   }
   for (int k = 1; k <= kz; k++)

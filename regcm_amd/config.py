@@ -244,6 +244,11 @@ CONFIGS = {
     "N1": RunConfig(jx=40, iy=36, kz=18, ds=3.0, dt=9.0, idynamic=2, name="N1 40x36x18 NH 3km"),
     "N2": RunConfig(jx=96, iy=96, kz=41, ds=3.0, dt=9.0, idynamic=2, name="N2 96x96x41 NH 3km"),
     "C5": RunConfig(jx=768, iy=768, kz=41, ds=3.0, dt=9.0, idynamic=2, name="C5 768x768x41 NH 3km"),
+    # the reference's own non-hydrostatic namelist, PreProc/CRM/crm_test.in: 64x64x23 at 3 km,
+    # dt 5 s, ptop 5 cb, i_band = 1 and i_crm = 1 (periodic in j and i, :16-17), iboudy = 0,
+    # ibltyp = 2 (:81-82), idynamic = 2 (:123); every other option at its default
+    "CRM": RunConfig(jx=64, iy=64, kz=23, ds=3.0, dt=5.0, idynamic=2, i_band=1, i_crm=1, iboudy=0, ibltyp=2,
+                     name="CRM 64x64x23 NH 3km crm_test.in"),
 }
 
 

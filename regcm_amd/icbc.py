@@ -372,6 +372,77 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
     return dict(state=st, split=split)
 
 
+def generate_crm(rc: RunConfig, seed: int = SEED) -> dict:
+    """Synthetic doubly periodic state of a cloud-resolving run (i_crm = 1 over a band,
+    PreProc/CRM/crm_test.in: TOGA-COARE at clat = 0, NORMER projection, ocean).
+
+    Every field is defined on the whole periodic grid: with i_band and i_crm the cross grid
+    takes every j and every i (Main/mpplib/mod_mppparam.F90:1340-1360), so no row or column is
+    left unset.  Flat terrain and unit map factors make the reference state and the statics
+    horizontally uniform (nhbase, Share/mod_nhinterp.F90:74-106, on the whole grid; dpsdxm,
+    dpsdym, dprddx, dprddy = 0; f = 0 and the full-Coriolis terms of latitude 0); the
+    temperature carries crm_test.in's 0.1 % perturbation (lperturb_t, perturb_frac_t) on a
+    standard-atmosphere profile, qv 70 % of saturation, periodic winds u = 5 + 3 sin(2 pi i/iy),
+    v = 2 sin(2 pi j/jx) m/s with noise, pp in hydrostatic balance (nhpp), small noise in w and
+    a boundary-layer TKE (ibltyp = 2).  The boundary data equal the initial state (the CRM's
+    Rayleigh damping relaxes u, v, pp, w toward 0 and damps no t or qv: nothing reads them).
+    init_sound's scalars follow Main/mod_sound.F90:120, 143-153 with nicross = iy, njcross = jx."""
+    from . import nhbase
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    jx, iy, kz = rc.jx, rc.iy, rc.kz
+    sigma = np.asarray(rc.sigma)
+    hsig = (sigma[1:] + sigma[:-1]) * 0.5
+    ptop = rc.ptop
+    dx = rc.ds * 1000.0
+    jj, ii = np.meshgrid(np.arange(1, jx + 1, dtype=np.float64), np.arange(1, iy + 1, dtype=np.float64))
+    ter = np.zeros((iy, jx))
+    args = (ptop, rc.base_state_pressure, rc.logp_lrate, rc.base_state_ts0)
+    ps0, pr0, t0, rho0, z0 = nhbase.nhbase(ter, hsig, *args)
+    _, pf0, _, rhof0, zf0 = nhbase.nhbase(ter, sigma, *args)
+    st = {"ATM0_PS": ps0[None].copy(), "ATM0_PR": pr0, "ATM0_T": t0, "ATM0_RHO": rho0, "ATM0_Z": z0,
+          "ATM0_PF": pf0, "ATM0_RHOF": rhof0, "ATM0_ZF": zf0}
+    zero2 = np.zeros((1, iy, jx))
+    for n in ("DPSDXM", "DPSDYM", "DMDX", "DMDY", "DDY", "CRY", "CORIOL", "HT"):
+        st[n] = zero2.copy()
+    st["DPRDDX"], st["DPRDDY"] = np.zeros((kz, iy, jx)), np.zeros((kz, iy, jx))
+    st["EF"], st["EX"] = np.full((1, iy, jx), nhbase.EOMEG2), np.full((1, iy, jx), nhbase.EOMEG2)
+    st["DDX"], st["CRX"] = np.ones((1, iy, jx)), np.ones((1, iy, jx))
+    st["MSFX"], st["MSFD"] = np.ones((1, iy, jx)), np.ones((1, iy, jx))
+    pstar = ps0 * 1.0e-3                                     # Main/mod_init.F90:146
+    t = np.maximum(288.15 * (pr0 / 101325.0) ** (C.rgas * 0.0065 / C.egrav), 216.65)
+    t = t * (1.0 + 0.001 * rng.uniform(-1.0, 1.0, t.shape))
+    qv = 0.7 * _qsat(t, pr0)
+    pp = nhpp(sigma, t, t * (1.0 + C.ep1 * qv), pr0, t0, pstar, ps0, ptop)
+    u = (5.0 + 3.0 * np.sin(2.0 * math.pi * ii / iy))[None] + rng.normal(0.0, 0.3, (kz, iy, jx))
+    v = (2.0 * np.sin(2.0 * math.pi * jj / jx))[None] + rng.normal(0.0, 0.3, (kz, iy, jx))
+    w = np.zeros((kz + 1, iy, jx))
+    w[1:kz] = rng.normal(0.0, 0.02, (kz - 1, iy, jx))
+    ps3 = pstar[None]
+    st["PSA"], st["PSB"] = ps3.copy(), ps3.copy()
+    for lvl in ("ATM1", "ATM2"):
+        st[f"{lvl}_U"], st[f"{lvl}_V"] = u * ps3, v * ps3           # psdot = p* (uniform)
+        st[f"{lvl}_T"], st[f"{lvl}_QV"] = t * ps3, qv * ps3
+        st[f"{lvl}_QC"] = np.zeros((kz, iy, jx))
+        st[f"{lvl}_PP"] = pp * ps3
+        st[f"{lvl}_W"] = w * ps3
+    sig = sigma[:, None, None]
+    prof = 1.5 * np.exp(-(1.0 - sig) / 0.08)
+    for n, name in enumerate(("ATM1_TKE", "ATM2_TKE")):
+        st[name] = np.maximum(prof * (1.0 + 0.3 * rng.standard_normal((kz + 1, iy, jx))) + 0.02 * n, rc.tkemin)
+    for b, a in (("XUB", "ATM1_U"), ("XVB", "ATM1_V"), ("XTB", "ATM1_T"), ("XQB", "ATM1_QV"),
+                 ("XPPB", "ATM1_PP"), ("XWWB", "ATM1_W")):
+        st[f"{b}_B0"], st[f"{b}_BT"] = st[a].copy(), np.zeros_like(st[a])
+    st["XPSB_B0"], st["XPSB_BT"] = ps3.copy(), np.zeros((1, iy, jx))
+    split = spinit_constants(rc.sigma, ptop, kz, rc.dt, rc.nsplit)
+    rnpts = 1.0 / float((iy - 2) * (jx - 2))                 # (nicross-2)*(njcross-2), :120
+    split["nh_xmsf"] = float(np.sum(st["MSFX"][0])) * rnpts
+    cs = math.sqrt(nhbase.XGAMMA * C.rgas * float(np.max(t0)))
+    split["nh_dtsmax"] = dx / cs / (1.0 + rc.nhxkd)
+    st["DSTOR"] = np.zeros((rc.nsplit, iy, jx))
+    st["HSTOR"] = np.zeros((rc.nsplit, iy, jx))
+    return dict(state=st, split=split)
+
+
 def tke_state(rc: RunConfig, seed: int = SEED) -> dict:
     """Synthetic UW-PBL turbulent kinetic energy (ibltyp = 2): atm1/atm2 tke on the kz+1 full
     sigma levels (decoupled, m2/s2), a boundary-layer profile of up to ~1.5 m2/s2 decaying

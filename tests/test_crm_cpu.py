@@ -1,0 +1,98 @@
+"""The cloud-resolving configuration of the reference's only non-hydrostatic namelist
+(PreProc/CRM/crm_test.in: i_band = 1, i_crm = 1, iboudy = 0, ibltyp = 2, idynamic = 2,
+64 x 64 x 23 at 3 km, dt 5 s) on the oracle restatement (CPU).
+
+With i_crm over a band the grid is periodic in j and i (Main/mpplib/mod_mppparam.F90:1104-1108,
+1131-1132): no tile has a boundary side, the cross grid takes every point (:1340-1360), the
+relaxation band is empty (Main/mod_atm_interface.F90:434), the Rayleigh damping relaxes u, v, pp
+toward 0 and leaves t, qv alone (Main/mod_tendency.F90:356-363, 466-475), bdyval has no line
+to set (its iboudy = 0 branches act on boundary lines only), and sound has no zero-gradient
+ring while its radiative condition keeps the reference's interior clamp (Main/mod_sound.F90:
+551-561) and its init_sound count rnpts = 1/((nicross-2)(njcross-2)) (:120).  The
+decomposition follows the reference's multi-rank path, whose periodic neighbours include the
+corners; its one-rank path (nproc = 1, :1082-1128) ends the cross grid at jx-1, iy-1 and leaves
+the corner neighbours null, so a one-rank reference run and a decomposed one disagree there.
+
+Checks: 20 steps stay finite and active; a resting atmosphere stays at rest; without the
+radiative condition (whose clamp is not translation invariant) a rotation of the state in j and
+i commutes with the step bit for bit; tiles over OpenMP threads (orc_par.c, periodic peers in
+both directions, the day-alarm sums in one-tile order) equal one tile bit for bit.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from regcm_amd import icbc
+from regcm_amd.config import CONFIGS
+
+FIELDS = ["ATM1_U", "ATM1_V", "ATM1_T", "ATM1_QV", "ATM1_QC", "ATM2_U", "ATM2_V", "ATM2_T", "ATM2_QV",
+          "ATM2_QC", "ATM1_PP", "ATM2_PP", "ATM1_W", "ATM2_W", "ATM1_TKE", "ATM2_TKE"]
+
+
+def _crm(**kw):
+    rc = dataclasses.replace(CONFIGS["CRM"], **kw)
+    return rc, icbc.generate_crm(rc)
+
+
+def _run(rc, data, st, nsteps, dims=None):
+    from oracle.oracle import OracleCore, OracleParallel
+    o = OracleParallel(rc, data["split"], dims=dims) if dims else OracleCore(rc, data["split"])
+    o.put_state(st)
+    o.bdyval()
+    o.step(nsteps)
+    return o
+
+
+def test_crm_oracle_runs_stably():
+    rc, data = _crm()
+    o = _run(rc, data, data["state"], 20)
+    ps = data["state"]["PSA"][0, 0, 0]
+    w = o.get("ATM1_W") / ps
+    assert np.isfinite(w).all() and 1e-3 < np.abs(w).max() < 5.0
+    for f in FIELDS:
+        assert np.isfinite(o.get(f)).all(), f
+    assert not np.array_equal(o.get("ATM1_T"), data["state"]["ATM1_T"])
+    assert o.get_time()[0] == 20
+
+
+def test_crm_rest_state_stays_at_rest():
+    """t = t0, qv = qc = 0, u = v = w = pp = 0 over flat terrain stays at rest within the
+    reference state's own hydrostatic offset (the NH rest test's bound, |u|, |w| < 1e-4 m/s)."""
+    rc, data = _crm()
+    st = dict(data["state"])
+    ps3 = st["PSA"]
+    for lvl in ("ATM1", "ATM2"):
+        st[f"{lvl}_T"] = st["ATM0_T"] * ps3
+        for f in ("U", "V", "PP", "QV", "QC"):
+            st[f"{lvl}_{f}"] = np.zeros_like(st[f"{lvl}_T"])
+        st[f"{lvl}_W"] = np.zeros_like(st[f"{lvl}_W"])
+    o = _run(rc, data, st, 10)
+    ps = st["PSA"][0, 0, 0]
+    for f in ("ATM1_U", "ATM1_V", "ATM1_W"):
+        assert np.abs(o.get(f)).max() / ps < 1e-4, f
+    for f in ("ATM1_U", "ATM1_W", "ATM1_PP", "ATM1_T"):    # and stays horizontally uniform
+        a = o.get(f)
+        assert np.array_equal(a, np.broadcast_to(a[:, :1, :1], a.shape)), f
+
+
+def test_crm_rotation_commutes_with_step():
+    """Without the radiative condition the doubly periodic step is translation invariant."""
+    rc, data = _crm(ifupr=0)
+    m, n = 13, 7
+    rot = {k: np.roll(v, (n, m), axis=(-2, -1)) if v.ndim == 3 and v.shape[-2:] == (rc.iy, rc.jx) else v
+           for k, v in data["state"].items()}
+    a = _run(rc, data, data["state"], 5)
+    b = _run(rc, data, rot, 5)
+    for f in FIELDS:
+        assert np.array_equal(np.roll(a.get(f), (n, m), axis=(-2, -1)), b.get(f)), f
+
+
+@pytest.mark.parametrize("dims", [(2, 1), (1, 2), (2, 2), (1, 1)], ids=str)
+def test_crm_oracle_tiles_match_one_tile(dims):
+    rc, data = _crm()
+    one = _run(rc, data, data["state"], 6)
+    til = _run(rc, data, data["state"], 6, dims=dims)
+    for f in FIELDS:
+        assert np.array_equal(one.get(f), til.get(f)), f
+    assert one.get_time() == til.get_time()
