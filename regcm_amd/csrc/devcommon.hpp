@@ -147,7 +147,7 @@ __device__ __forceinline__ bool psc2psd_at(const Geom& g, const double* pc, int 
 // edges, corner copies.  Equal to psc2psd_at on every owned point.
 __device__ __forceinline__ double psc2psd_global(const Geom& g, const double* pc, int j, int i) {
   const int jx = g.gjx, iy = g.giy;
-  const bool jin = g.band || (j >= 2 && j <= jx - 1), iin = i >= 2 && i <= iy - 1;   // a band: every j
+  const bool jin = g.band || (j >= 2 && j <= jx - 1), iin = g.crm || (i >= 2 && i <= iy - 1);   // a band: every j, CRM: every i
   if (jin && iin) return (F2(pc, j, i) + F2(pc, j, i - 1) + F2(pc, j - 1, i) + F2(pc, j - 1, i - 1)) * d_rfour;
   if (jin && i == iy) return (F2(pc, j, iy - 1) + F2(pc, j - 1, iy - 1)) * d_half;
   if (jin && i == 1) return (F2(pc, j, 1) + F2(pc, j - 1, 1)) * d_half;

@@ -77,12 +77,13 @@ void tile_extent(int jx, int iy, int cj, int ci, int tile, int ext[8], int bdy[4
   bdy[2] = (li == 0) && !crm; bdy[3] = (li == ci - 1) && !crm;
 }
 
-Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G, int band = 0) {
+Geom make_geom(int jx, int iy, int cj, int ci, int tile, int gh = G, int band = 0, int crm = 0) {
   int ext[8], bdy[4];
-  tile_extent(jx, iy, cj, ci, tile, ext, bdy, band);
+  tile_extent(jx, iy, cj, ci, tile, ext, bdy, band, crm);
   Geom g{};
   g.bl = bdy[0]; g.br = bdy[1]; g.bb = bdy[2]; g.bt = bdy[3];
   g.band = band;
+  g.crm = crm;
   g.gjx = jx; g.giy = iy;
   g.jde1 = g.jdi1 = g.jdii1 = ext[0]; g.jde2 = g.jdi2 = g.jdii2 = ext[1];
   g.ide1 = g.idi1 = g.idii1 = ext[2]; g.ide2 = g.idi2 = g.idii2 = ext[3];
@@ -127,6 +128,7 @@ void setup_boundaries(const Geom& g, int jx, int iy, int nsp, bool ldot, std::ve
   // global index, so ghost points carry their owners' values
   const int fi1 = std::max(1, g.i0), fi2 = std::min(iy, g.i0 + g.ni - 1);
   const int fj1 = std::max(1, g.j0), fj2 = std::min(jx, g.j0 + g.nj - 1);
+  if (g.crm) return;            // CRM: no relaxation band at all (:434, "if (.not. ma%crmflag)")
   if (g.band) {
     // periodic ghosts carry the band rows too
     for (int i = fi1; i <= fi2; i++)
@@ -449,7 +451,7 @@ struct rcmdyn_engine {
     if (cfg.idynamic == 2) {
       c.xkhz = cfg.ckh * c.dx;
       c.xkhmax = 2.0 * c.xkhmax;
-      c.ifupr = cfg.ifupr; c.ifrayd = cfg.ifrayd; c.rayndamp = cfg.rayndamp;
+      c.ifupr = cfg.ifupr; c.ifrayd = cfg.ifrayd; c.rayndamp = cfg.rayndamp; c.crm = cfg.i_crm;
       c.rayalpha0 = cfg.rayalpha0; c.rayhd = cfg.rayhd; c.nhbet = cfg.nhbet; c.nhxkd = cfg.nhxkd;
       c.nh_dtsmax = cfg.nh_dtsmax; c.nh_xmsf = cfg.nh_xmsf;
       c.xgamma = 1.0 / (1.0 - c.rgas * (1.0 / c.cpd));           // Main/mod_sound.F90:77
@@ -491,6 +493,7 @@ struct rcmdyn_engine {
     for (int d = 0; d < 8; d++) {
       int lj = t.lj + dj[d], li = t.li + di[d];
       if (cfg.i_band) lj = (lj + cfg.nproc_j) % cfg.nproc_j;      // periodic in j (a tile may be its own)
+      if (cfg.i_crm) li = (li + cfg.nproc_i) % cfg.nproc_i;       // CRM: periodic in i too
       t.nbr[d] = (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
     }
     for (int b = 0; b < 2; b++) {
@@ -544,7 +547,7 @@ struct rcmdyn_engine {
     t.tten = dalloc(t, P3); t.uten = dalloc(t, P3); t.vten = dalloc(t, P3);
     t.qvten = dalloc(t, P3); t.qcten = dalloc(t, P3); t.omega = dalloc(t, P3); t.xkcs = dalloc(t, P3);
     if (halo) {                       // wide frame of the fused split step
-      t.gw = make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, index, SPH + G, cfg.i_band);
+      t.gw = make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, index, SPH + G, cfg.i_band, cfg.i_crm);
       const size_t PW = t.gw.plane;
       t.wdeld = dalloc(t, PW * 3 * ns); t.wdelh = dalloc(t, PW * 3 * ns);
       t.wpsa = dalloc(t, PW); t.wpsdota = dalloc(t, PW);
@@ -739,7 +742,12 @@ struct rcmdyn_engine {
     if (cfg.ibltyp == 2 && !(cfg.tkemin >= 0.0))
       throw std::runtime_error("rcmdyn: ibltyp=2 needs tkemin (uwtkemin) >= 0");
     if (cfg.iuwvadv != 0 && cfg.iuwvadv != 1) throw std::runtime_error("rcmdyn: iuwvadv must be 0 or 1");
-    if (cfg.iboudy < 1 || cfg.iboudy > 5) throw std::runtime_error("rcmdyn: iboudy must be 1 to 5");
+    if (cfg.iboudy < 0 || cfg.iboudy > 5) throw std::runtime_error("rcmdyn: iboudy must be 0 to 5");
+    // iboudy = 0 (fixed lateral values): the b0-only branches of bdyval (Main/mod_bdycod.F90:944,
+    // 1317, 1535) act on the boundary lines only, so with CRM, which has none, it is the empty
+    // boundary of crm_test.in; on a limited area those branches are not built
+    if (cfg.iboudy == 0 && cfg.i_crm != 1)
+      throw std::runtime_error("rcmdyn: iboudy = 0 (fixed lateral values) is built for i_crm = 1 only");
     // physicsparam ipptls and the nqx param derives from it (Main/mod_params.F90:1358-1366)
     if (cfg.ipptls < 1 || cfg.ipptls > 2)
       throw std::runtime_error("rcmdyn: ipptls must be 1 or 2 (ipptls = 0 leaves the hydrometeor tendencies unsummed, "
@@ -748,9 +756,14 @@ struct rcmdyn_engine {
       throw std::runtime_error("rcmdyn: nqx must be 2 for ipptls = 1 and 5 for ipptls = 2 (Main/mod_params.F90:1358-1366)");
     // periodic decompositions and chemical tracers are not built: refused, not ignored
     if (cfg.i_band != 0 && cfg.i_band != 1) throw std::runtime_error("rcmdyn: i_band must be 0 or 1");
-    if (cfg.i_band != 0 && cfg.idynamic == 2)
-      throw std::runtime_error("rcmdyn: i_band = 1 (periodic tropical band) is built for the hydrostatic core only");
-    if (cfg.i_crm != 0) throw std::runtime_error("rcmdyn: i_crm = 1 (periodic CRM domain) is not supported");
+    // CRM (i_crm = 1, PreProc/CRM/crm_test.in): periodic in j and i, for the non-hydrostatic
+    // core over the band; CRM without the band decomposes differently on one rank and on
+    // several in the reference (Main/mpplib/mod_mppparam.F90:1104-1108 against 1132)
+    if (cfg.i_crm != 0 && cfg.i_crm != 1) throw std::runtime_error("rcmdyn: i_crm must be 0 or 1");
+    if (cfg.i_crm == 1 && (cfg.i_band != 1 || cfg.idynamic != 2))
+      throw std::runtime_error("rcmdyn: i_crm = 1 is built for the non-hydrostatic core over the band (i_band = 1)");
+    if (cfg.i_band != 0 && cfg.idynamic == 2 && cfg.idiffu == 3)
+      throw std::runtime_error("rcmdyn: idiffu = 3 on the non-hydrostatic band / CRM is not supported");
     if (cfg.ichem != 0) throw std::runtime_error("rcmdyn: ichem = 1 (chemical tracers) is not supported");
     if (const char* m = std::getenv("RCMDYN_RCCL_CHAN2"))   // the removed second-communicator modes
       if (std::string(m) != "one") throw std::runtime_error("rcmdyn: RCMDYN_RCCL_CHAN2 must be one (or unset)");
@@ -772,7 +785,7 @@ struct rcmdyn_engine {
       HIPCHK(hipGetDevice(&device));
     }
     for (int t = 0; t < ntiles; t++) {
-      all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t, G, cfg.i_band));
+      all.push_back(make_geom(cfg.jx, cfg.iy, cfg.nproc_j, cfg.nproc_i, t, G, cfg.i_band, cfg.i_crm));
       const Geom& g = all.back();
       if (g.jde2 - g.jde1 + 1 < 3 || g.ide2 - g.ide1 + 1 < 3)
         throw std::runtime_error("rcmdyn: Too much processors (tile < 3x3), mod_mppparam.F90:1365");
@@ -1142,13 +1155,17 @@ struct rcmdyn_engine {
       std::vector<double> h((size_t)nk * g.plane);
       HIPCHK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
       for (int k = std::max(k1, 1); k <= std::min(k2, nk); k++)
-        for (int i = std::max(i1, g.i0); i <= std::min(i2, g.i0 + g.ni - 1); i++)
+        for (int i = g.i0; i <= g.i0 + g.ni - 1; i++) {
+          // CRM: the frame rows past either end of the period take the wrapped row
+          const int iw = !cfg.i_crm ? i : (i < 1 ? i + cfg.iy : (i > cfg.iy ? i - cfg.iy : i));
+          if (iw < i1 || iw > i2) continue;
           for (int j = g.j0; j <= g.j0 + g.nj - 1; j++) {
             // a band's frame columns past either end of the period take the wrapped column
             const int jw = !cfg.i_band ? j : (j < 1 ? j + cfg.jx : (j > cfg.jx ? j - cfg.jx : j));
             if (jw < j1 || jw > j2) continue;
-            h[(size_t)(k - 1) * g.plane + g.ix(j, i)] = src[((size_t)(k - k1) * ni + (i - i1)) * nj + (jw - j1)];
+            h[(size_t)(k - 1) * g.plane + g.ix(j, i)] = src[((size_t)(k - k1) * ni + (iw - i1)) * nj + (jw - j1)];
           }
+        }
       HIPCHK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
     }
     if (f >= RCMDYN_MSFX && f <= RCMDYN_HT) statics_dirty = true;
@@ -1318,8 +1335,9 @@ struct rcmdyn_engine {
   }
   int peer_of(const Tile& t, int d) const {
     int lj = t.lj + DJ[d];
-    const int li = t.li + DI[d];
+    int li = t.li + DI[d];
     if (cfg.i_band) lj = (lj + cfg.nproc_j) % cfg.nproc_j;       // periodic in j (may be t itself)
+    if (cfg.i_crm) li = (li + cfg.nproc_i) % cfg.nproc_i;        // CRM: periodic in i too
     return (lj >= 0 && lj < cfg.nproc_j && li >= 0 && li < cfg.nproc_i) ? lj * cfg.nproc_i + li : -1;
   }
   Tile* local_tile(int idx) {

@@ -32,6 +32,7 @@ struct Geom {
   int jde1gb, jde2gb, ide1gb, ide2gb, jce1gb, jce2gb, ice1gb, ice2gb;
   int bl, br, bb, bt;              // has_bdyleft/right/bottom/top
   int band;                        // i_band = 1: periodic in j, no west/east boundary (bl = br = 0)
+  int crm;                         // i_crm = 1 (with the band): periodic in i too (bb = bt = 0)
   int gjx, giy;                    // global dot-grid extents
   int j0, i0;                      // global index of frame origin
   int nj, ni;                      // frame size (nj <= pitch)
@@ -62,24 +63,35 @@ struct Geom {
   // Global index classes (Main/mod_atm_interface.F90:231-302 on one tile): equal to the tile
   // ranges jce/jci/jcii/jdi/jdii on owned points, and defined on ghost points.  In a band
   // (i_band = 1) every j is interior: the grid is periodic in j and both grids take all jx
-  // points (Main/mpplib/mod_mppparam.F90:1131, 1351-1354).
+  // points (Main/mpplib/mod_mppparam.F90:1131, 1351-1354); with CRM (i_crm = 1) every i too
+  // (:1132, 1340-1342).
   __host__ __device__ __forceinline__ bool gce(int j, int i) const {
-    return (band || (j >= 1 && j <= gjx - 1)) && i >= 1 && i <= giy - 1;
+    return (band || (j >= 1 && j <= gjx - 1)) && (crm || (i >= 1 && i <= giy - 1));
   }
   __host__ __device__ __forceinline__ bool gci(int j, int i) const {
-    return (band || (j >= 2 && j <= gjx - 2)) && i >= 2 && i <= giy - 2;
+    return (band || (j >= 2 && j <= gjx - 2)) && (crm || (i >= 2 && i <= giy - 2));
   }
   __host__ __device__ __forceinline__ bool gcii(int j, int i) const {
-    return (band || (j >= 3 && j <= gjx - 3)) && i >= 3 && i <= giy - 3;
+    return (band || (j >= 3 && j <= gjx - 3)) && (crm || (i >= 3 && i <= giy - 3));
   }
   __host__ __device__ __forceinline__ bool gdi(int j, int i) const {
-    return (band || (j >= 2 && j <= gjx - 1)) && i >= 2 && i <= giy - 1;
+    return (band || (j >= 2 && j <= gjx - 1)) && (crm || (i >= 2 && i <= giy - 1));
   }
   __host__ __device__ __forceinline__ bool gdii(int j, int i) const {
-    return (band || (j >= 3 && j <= gjx - 2)) && i >= 3 && i <= giy - 2;
+    return (band || (j >= 3 && j <= gjx - 2)) && (crm || (i >= 3 && i <= giy - 2));
   }
-  // global west / east boundary column tests (never in a band)
+  // global west / east boundary column tests (never in a band) and south / north row tests
+  // (never with CRM)
   __host__ __device__ __forceinline__ bool gjeq(int j, int v) const { return !band && j == v; }
+  __host__ __device__ __forceinline__ bool gieq(int i, int v) const { return !crm && i == v; }
+  // the global cross grid (Main/mpplib/mod_mppparam.F90:1486-1516): njcross / nicross points,
+  // and its interior range jci / ici over the whole domain (every point in a periodic direction)
+  __host__ __device__ __forceinline__ int njcross() const { return band ? gjx : gjx - 1; }
+  __host__ __device__ __forceinline__ int nicross() const { return crm ? giy : giy - 1; }
+  __host__ __device__ __forceinline__ int gcj1() const { return band ? 1 : 2; }
+  __host__ __device__ __forceinline__ int gcj2() const { return band ? gjx : gjx - 2; }
+  __host__ __device__ __forceinline__ int gci1() const { return crm ? 1 : 2; }
+  __host__ __device__ __forceinline__ int gci2() const { return crm ? giy : giy - 2; }
 };
 // the negative-moisture fix's row bitmap: words per (species, level) plane; the LDS (doubles) of
 // its serial part (qxcommon.hpp): the row sweep's two interior rows and 13 per lane, or the
@@ -125,6 +137,7 @@ struct Consts {
   double pdlog[MAXSPLIT][MAXKZ + 2], eps1[MAXSPLIT][MAXKZ + 2], pd;
   // non-hydrostatic core (idynamic = 2): nonhydroparam and init_sound scalars
   int idynamic, ifupr, ifrayd, rayndamp;
+  int crm;                     // i_crm = 1: the Rayleigh damping of u, v, pp toward 0, none of t, qv
   double rayalpha0, rayhd, nhbet, nhxkd, nh_dtsmax, nh_xmsf, xgamma, dds[MAXKZ + 2];
   // moisture species (physicsparam ipptls, Main/mod_params.F90:1358-1366): nqx = 2 (qv, qc)
   // or 5 (qv, qc, qi, qr, qs); nsp = nqx - 2 hydrometeors beyond qc

@@ -38,7 +38,8 @@ namespace rcm {
 __device__ __forceinline__ void surface_pressures_at(const Geom& g, const Fields& f, int j, int i) {
   auto ring = [&](int d, int jhi, int ihi) {
     const bool jok = g.band ? in(j, g.jde1 - d, g.jde2 + d) : in(j, max(1, g.jde1 - d), min(jhi, g.jde2 + d));
-    return jok && in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
+    const bool iok = g.crm ? in(i, g.ide1 - d, g.ide2 + d) : in(i, max(1, g.ide1 - d), min(ihi, g.ide2 + d));
+    return jok && iok;
   };
   if (ring(2, g.gjx - 1, g.giy - 1)) F2(f.rpsa, j, i) = d_one / F2(f.psa, j, i);
   if (ring(3, g.gjx - 1, g.giy - 1)) F2(f.rpsb, j, i) = d_one / F2(f.psb, j, i);
@@ -434,14 +435,14 @@ __global__ __launch_bounds__(256) void k_sladv(Geom g, const Consts* __restrict_
   auto ua = [&](int jj, int ii) {
     const uint32_t q2 = g.o2(jj, ii);
     double ud;
-    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || ii == 1 || ii == g.giy)) ud = udvd_bdy(g, f, jj, ii, kof).x;
+    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || g.gieq(ii, 1) || g.gieq(ii, g.giy))) ud = udvd_bdy(g, f, jj, ii, kof).x;
     else ud = LD(f.a1u, q2 + kof) * LD(f.rpsda, q2);
     return ud * LD(f.msfd, q2);
   };
   auto va = [&](int jj, int ii) {
     const uint32_t q2 = g.o2(jj, ii);
     double vd;
-    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || ii == 1 || ii == g.giy)) vd = udvd_bdy(g, f, jj, ii, kof).y;
+    if (ib4 && (g.gjeq(jj, 1) || g.gjeq(jj, g.gjx) || g.gieq(ii, 1) || g.gieq(ii, g.giy))) vd = udvd_bdy(g, f, jj, ii, kof).y;
     else vd = LD(f.a1v, q2 + kof) * LD(f.rpsda, q2);
     return vd * LD(f.msfd, q2);
   };

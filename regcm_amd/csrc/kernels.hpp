@@ -59,12 +59,16 @@ constexpr int COLW = RCM_COLW, COLG = RCM_COLG, COLT = COLW * COLG;   // COLG le
 constexpr int SPC = RCM_SPC, SPG = 8;
 // k_split_project / k_split_correct(_bdy): XCD-contiguous block placement (xcd_range,
 // devcommon.hpp): the rows a projection block shares with the next row's block, and the 2-D
-// split sums every level of a correction block column reads, stay in one L2
+// split sums every level of a correction block column reads, stay in one L2.  Round 6,
+// alternating on one box (profiles/r06/tile_ab_split_xcd.log): k_split_project 24.4 -> 18.1-19.5
+// us at C3, the C3 step 193.9-199.8 -> 186.0-189.9 us; the correction placement is neutral at
+// C3 and takes the 96x48 rank tile's correction kernel 12.9 -> 10.9 us (step 0.0783-0.0788 ->
+// 0.0771-0.0772 ms with both)
 #ifndef SP_XCD
-#define SP_XCD 0
+#define SP_XCD 1
 #endif
 #ifndef SCOR_XCD
-#define SCOR_XCD 0
+#define SCOR_XCD 1
 #endif
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;

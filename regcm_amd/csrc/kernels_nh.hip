@@ -88,14 +88,14 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
   // the reference exchanges)
   auto we = [&](int jj, int ii) {
     if (in(ii, 2, g.giy - 1)) {
-      if (jj == 1 && F3(a1u, jj, ii, k) <= d_zero) return base(2, ii);
-      if (jj == g.gjx && F3(a1u, jj, ii, k) >= d_zero) return base(g.gjx - 1, ii);
+      if (g.gjeq(jj, 1) && F3(a1u, jj, ii, k) <= d_zero) return base(2, ii);
+      if (g.gjeq(jj, g.gjx) && F3(a1u, jj, ii, k) >= d_zero) return base(g.gjx - 1, ii);
     }
     return base(jj, ii);
   };
-  if (in(j, 1, g.gjx)) {
-    if (i == 1 && F3(a1v, j, i, k) >= d_zero) return we(j, 2);
-    if (i == g.giy && F3(a1v, j, i, k) <= d_zero) return we(j, g.giy - 1);
+  if (g.band || in(j, 1, g.gjx)) {
+    if (g.gieq(i, 1) && F3(a1v, j, i, k) >= d_zero) return we(j, 2);
+    if (g.gieq(i, g.giy) && F3(a1v, j, i, k) <= d_zero) return we(j, g.giy - 1);
   }
   return we(j, i);
 }
@@ -104,7 +104,7 @@ __device__ double2 udvd_nh(const Geom& g, int iboudy, const double* a1u, const d
 // caller: udvd_nh's values (the inflow/outflow rule only on the global boundary lines)
 __device__ __forceinline__ double2 udvd_nh_ld(const Geom& g, int iboudy, const NHFields& f, double au, double av,
                                               double r, int j, int i, int k) {
-  if ((iboudy == 3 || iboudy == 4) && (j == 1 || j == g.gjx || i == 1 || i == g.giy))
+  if ((iboudy == 3 || iboudy == 4) && (g.gjeq(j, 1) || g.gjeq(j, g.gjx) || g.gieq(i, 1) || g.gieq(i, g.giy)))
     return udvd_nh(g, iboudy, f.a1u, f.a1v, f.rpsda, j, i, k);
   return make_double2(au * r, av * r);
 }
@@ -692,12 +692,12 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     if (nudge) RELAX5(pd, f.ppb0, f.ppbt, f.a2pp);
     pd = c->idiffu == 3 ? diff6_add(g, pd, f.d6pp, g.jci2, j, i, k) : diffx_l(g, c, pd, sT[3], xkc, j, i, ti, tj);
     double pt = pt0 + pd + PHY(ppphy);
-    if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3, decoupling, acoustic-step scaling
-      pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *
-                    ((F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k)) - F3(f.a2pp, j, i, k));
+    if (c->ifrayd == 1 && k <= c->rayndamp)       // raydamp3 (CRM: raydamp3f toward 0, :468-470),
+      pt = pt + nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) *  // decoupling, acoustic-step scaling
+                    ((c->crm ? d_zero : F3(f.ppb0, j, i, k) + xt * F3(f.ppbt, j, i, k)) - F3(f.a2pp, j, i, k));
     F3(f.ppten, j, i, k) = (pt * F2(f.rpsa, j, i)) * dts;
   }
-  const bool ray = c->ifrayd == 1 && k <= c->rayndamp;
+  const bool ray = c->ifrayd == 1 && k <= c->rayndamp && !c->crm;   // no t/qv damping in CRM mode (:359)
   const double tau = ray ? nh_tau(c, F3(f.z0, j, i, k), F3(f.z0, j, i, 1)) : d_zero;
   // ================= t, ithadv = 1 (:1347-1356, 1594-1600): thten = hadvt of th, then vadv3d
   // ind = 0 (nk = kz) of tha = th*p*, plus th*cr; tdyn = atm1%t*thten/tha
@@ -969,8 +969,9 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
     const double zz = d_rfour * (F3(z, j, i, k) + F3(z, j - 1, i, k) + F3(z, j, i - 1, k) + F3(z, j - 1, i - 1, k));
     const double zm = d_rfour * (F3(z, j, i, 1) + F3(z, j - 1, i, 1) + F3(z, j, i - 1, 1) + F3(z, j - 1, i - 1, 1));
     const double tau = nh_tau(c, zz, zm);
-    ut = ut + tau * ((F3(f.ub0, j, i, k) + xt * F3(f.ubt, j, i, k)) - F3(f.a2u, j, i, k));
-    vt = vt + tau * ((F3(f.vb0, j, i, k) + xt * F3(f.vbt, j, i, k)) - F3(f.a2v, j, i, k));
+    // CRM: toward 0 (raydampuv_c with sval = d_zero, Main/mod_tendency.F90:467-469)
+    ut = ut + tau * ((c->crm ? d_zero : F3(f.ub0, j, i, k) + xt * F3(f.ubt, j, i, k)) - F3(f.a2u, j, i, k));
+    vt = vt + tau * ((c->crm ? d_zero : F3(f.vb0, j, i, k) + xt * F3(f.vbt, j, i, k)) - F3(f.a2v, j, i, k));
   }
   const double dts = s->dt / (double)istep;
   F3(f.uten, j, i, k) = (ut * F2(f.rpsda, j, i)) * dts;
@@ -1402,14 +1403,16 @@ __global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restri
   __shared__ double sh[2];
   __shared__ double sA[TMC], sR[TMC];
   const long n = (long)g.gjx * g.giy;
-  const int nj = g.gjx - 3, ni = g.giy - 3;       // j = 2..gjx-2, i = 2..giy-2
+  // the global interior cross points (j = 2..jx-2, i = 2..iy-2; every point of a periodic
+  // direction: a band's j, CRM's i)
+  const int j1 = g.gcj1(), i1 = g.gci1(), nj = g.gcj2() - j1 + 1, ni = g.gci2() - i1 + 1;
   const long total = (long)nj * ni;
   double atot = d_zero, rhontot = d_zero;
   for (long base = 0; base < total; base += TMC) {
     const int cnt = (int)((total - base) < TMC ? (total - base) : TMC);
     for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
       const long p = base + t;                    // i-major, j-minor: the reference's loop order
-      const int i = 2 + (int)(p / nj), j = 2 + (int)(p % nj);
+      const int i = i1 + (int)(p / nj), j = j1 + (int)(p % nj);
       const long q = (long)(i - 1) * g.gjx + (j - 1);
       sA[t] = gbuf[q];
       sR[t] = gbuf[n + q];
@@ -1420,7 +1423,9 @@ __global__ __launch_bounds__(256) void k_nh_tmask(Geom g, const Consts* __restri
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double rnpts = d_one / (double)((g.giy - 3) * (g.gjx - 3));
+    // init_sound's count, Main/mod_sound.F90:120: 1/((nicross-2)*(njcross-2)) (with CRM it
+    // differs from the number of points summed, as in the reference)
+    const double rnpts = d_one / (double)((g.nicross() - 2) * (g.njcross() - 2));
     sh[0] = atot * rnpts;
     sh[1] = rhontot * rnpts;
   }
@@ -1470,7 +1475,7 @@ __global__ NHCD_LB void k_nh_sound_cd(Geom g, Geom ge, const double* __restrict_
   __shared__ double sE[4 + 12][64 + 12];
   __shared__ double sM[169];
   __shared__ unsigned long long sred[4];
-  const int ilo = 2, ihi = g.giy - 2, jlo = 2, jhi = g.gjx - 2;   // icross1+1 .. icross2-1
+  const int ilo = 2, ihi = g.nicross() - 1, jlo = 2, jhi = g.njcross() - 1;   // icross1+1 .. icross2-1
 #if NH_XCD
   const Blk3 xb = xcd_block();
 #else

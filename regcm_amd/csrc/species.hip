@@ -63,8 +63,8 @@ __device__ __forceinline__ double qx_diffu(const Geom& g, const Consts* __restri
   };
   if (g.gjeq(j, 2)) ften = lap(ften);
   if (g.gjeq(j, g.gjx - 2)) ften = lap(ften);
-  if (i == 2) ften = lap(ften);
-  if (i == g.giy - 2) ften = lap(ften);
+  if (g.gieq(i, 2)) ften = lap(ften);
+  if (g.gieq(i, g.giy - 2)) ften = lap(ften);
   return ften;
 }
 

@@ -74,8 +74,8 @@ __global__ void k_tke_tend(Geom g, const Consts* __restrict__ c, const StepState
       const double lap2 = z4_c1 * (X(1, 0) + X(-1, 0) + X(0, 1) + X(0, -1)) + z4_c2 * X(0, 0);
       if (g.gjeq(j, 2)) ften = ften + fac * xk * lap2;
       if (g.gjeq(j, g.gjx - 2)) ften = ften + fac * xk * lap2;
-      if (i == 2) ften = ften + fac * xk * lap2;
-      if (i == g.giy - 2) ften = ften + fac * xk * lap2;
+      if (g.gieq(i, 2)) ften = ften + fac * xk * lap2;
+      if (g.gieq(i, g.giy - 2)) ften = ften + fac * xk * lap2;
     }
 #undef X
   }

@@ -374,7 +374,9 @@ def generate_nh(rc: RunConfig, seed: int = SEED, hmax: float = None, w_noise: fl
 
 def generate_crm(rc: RunConfig, seed: int = SEED) -> dict:
     """Synthetic doubly periodic state of a cloud-resolving run (i_crm = 1 over a band,
-    PreProc/CRM/crm_test.in: TOGA-COARE at clat = 0, NORMER projection, ocean).
+    PreProc/CRM/crm_test.in: TOGA-COARE at clat = 0, NORMER projection, ocean).  With
+    i_crm = 0 the same fields serve a non-hydrostatic band (periodic in j, relaxing to the
+    initial state at its south and north rows).
 
     Every field is defined on the whole periodic grid: with i_band and i_crm the cross grid
     takes every j and every i (Main/mpplib/mod_mppparam.F90:1340-1360), so no row or column is
@@ -434,8 +436,13 @@ def generate_crm(rc: RunConfig, seed: int = SEED) -> dict:
         st[f"{b}_B0"], st[f"{b}_BT"] = st[a].copy(), np.zeros_like(st[a])
     st["XPSB_B0"], st["XPSB_BT"] = ps3.copy(), np.zeros((1, iy, jx))
     split = spinit_constants(rc.sigma, ptop, kz, rc.dt, rc.nsplit)
-    rnpts = 1.0 / float((iy - 2) * (jx - 2))                 # (nicross-2)*(njcross-2), :120
-    split["nh_xmsf"] = float(np.sum(st["MSFX"][0])) * rnpts
+    # init_sound: xmsf = sum(msfx(jci1:jci2,ici1:ici2)) * rnpts, rnpts = 1/((nicross-2)*(njcross-2))
+    # (:120, 143-145); the global jci / ici take every point of a periodic direction
+    njc, nic = (jx if rc.i_band else jx - 1), (iy if rc.i_crm else iy - 1)
+    j1, j2 = (1, jx) if rc.i_band else (2, jx - 2)
+    i1, i2 = (1, iy) if rc.i_crm else (2, iy - 2)
+    rnpts = 1.0 / float((nic - 2) * (njc - 2))
+    split["nh_xmsf"] = float(np.sum(st["MSFX"][0][i1 - 1:i2, j1 - 1:j2])) * rnpts
     cs = math.sqrt(nhbase.XGAMMA * C.rgas * float(np.max(t0)))
     split["nh_dtsmax"] = dx / cs / (1.0 + rc.nhxkd)
     st["DSTOR"] = np.zeros((rc.nsplit, iy, jx))

@@ -113,13 +113,19 @@ def test_tile_extents_periodic(band, crm):
     assert all(cover[i][j] == 1 for i in range(1, iy + 1) for j in range(1, jx + 1))
 
 
-def test_band_refused_for_nonhydrostatic():
+@pytest.mark.parametrize("bad,msg", [(dict(i_band=0), "i_crm"), (dict(idynamic=1), "i_crm"),
+                                     (dict(i_crm=0), "iboudy = 0"), (dict(idiffu=3), "idiffu = 3")],
+                         ids=["crm-without-band", "crm-hydrostatic", "iboudy0-lam", "nh-band-idiffu3"])
+def test_periodic_refusals(bad, msg):
+    """CRM is built for the non-hydrostatic core over the band (PreProc/CRM/crm_test.in);
+    iboudy = 0 only where no boundary line exists (CRM); the sixth-order diffusion not on the
+    NH band.  Refused at create, before any device is touched."""
     import dataclasses
     from regcm_amd.config import CONFIGS
     from regcm_amd import icbc
-    rc = dataclasses.replace(CONFIGS["N1"], i_band=1)
-    data = icbc.generate_nh(CONFIGS["N1"])
-    with pytest.raises(dycore.EngineError, match="i_band"):
+    rc = dataclasses.replace(CONFIGS["CRM"], **bad)
+    data = icbc.generate_crm(CONFIGS["CRM"])
+    with pytest.raises(dycore.EngineError, match=msg):
         dycore.DynCore(rc, data["split"])
 
 

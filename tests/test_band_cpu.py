@@ -103,14 +103,16 @@ def test_band_stays_bounded():
     assert t.min() > 150.0 and t.max() < 340.0
 
 
-def test_band_refused_for_nonhydrostatic_and_bad_values():
-    """i_band = 1 is built for the hydrostatic core; other values are refused (oracle and
-    engine alike: the engine's refusal is checked in test_abi_cpu)."""
+def test_band_bad_values_refused():
+    """i_band is 0 or 1 (both cores since round 6); CRM needs the band and the NH core, and
+    iboudy = 0 needs CRM (oracle and engine alike: the engine's refusals are checked in
+    test_abi_cpu)."""
     from oracle.oracle import OracleCore
-    rc = dataclasses.replace(CONFIGS["N1"], i_band=1)
     data = icbc.generate_nh(CONFIGS["N1"])
-    with pytest.raises(RuntimeError):
-        OracleCore(rc, data["split"])
+    for bad in (dict(i_crm=1), dict(i_crm=1, i_band=1, idynamic=1), dict(iboudy=0)):
+        with pytest.raises(RuntimeError):
+            OracleCore(dataclasses.replace(CONFIGS["N1"], **bad), data["split"])
+    OracleCore(dataclasses.replace(CONFIGS["N1"], i_band=1), data["split"]).close()
     rc = dataclasses.replace(CONFIGS["C1"], i_band=2)
     with pytest.raises(RuntimeError):
         OracleCore(rc, icbc.generate(CONFIGS["C1"])["split"])

@@ -96,3 +96,16 @@ def test_crm_oracle_tiles_match_one_tile(dims):
     for f in FIELDS:
         assert np.array_equal(one.get(f), til.get(f)), f
     assert one.get_time() == til.get_time()
+
+
+@pytest.mark.parametrize("variant", [{}, {"iboudy": 4}, {"ibltyp": 2}], ids=str)
+def test_nh_band_oracle_tiles_match_one_tile(variant):
+    """The non-hydrostatic band without CRM (periodic in j, relaxed south and north rows) on
+    2 x 2 threaded tiles equals one tile bit for bit."""
+    rc, data = _crm(i_crm=0, iboudy=5, ibltyp=1)
+    rc = dataclasses.replace(rc, **variant)
+    st = {k: v for k, v in data["state"].items() if "TKE" not in k or rc.ibltyp == 2}
+    one = _run(rc, data, st, 6)
+    til = _run(rc, data, st, 6, dims=(2, 2))
+    for f in FIELDS[:14]:
+        assert np.array_equal(one.get(f), til.get(f)), f
