@@ -201,15 +201,19 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
     }
     return;
   }
+  // COL_XCD: the column blocks of one tile in XCD-contiguous runs of rows, so a block's i + 1
+  // row (the dot points of its divergence) is the next row's block's own and a hit in the same
+  // L2; the noise partial keeps the block's logical slot, so the sums are unchanged
+  const int cb = (COL_XCD && f.pt.part == 0) ? xcd_range(bb, 0, ncol) : bb;
   // k_scalars appends after this (part 2 follows part 1 and the k_scalars blocks of part 1)
-  if (f.qfuse && bb == 0 && threadIdx.x == 0 && f.pt.part != 2) *f.negcnt = 0;
+  if (f.qfuse && cb == 0 && threadIdx.x == 0 && f.pt.part != 2) *f.negcnt = 0;
   const int tx = (int)threadIdx.x % COLW, ty = (int)threadIdx.x / COLW;     // column, level group
 
   // Blocks cover the columns of the tile plus its ghost ring toward neighbours: the ghost
   // columns compute exactly what their owners do (qdot, phi, pten and the new p* there replace
   // the reference's exchanges of them).
   int j, i;
-  const bool valid = column_of(g, f.pt, bb, tx, nxb, j, i);
+  const bool valid = column_of(g, f.pt, cb, tx, nxb, j, i);
   const bool own = valid && in(j, g.jce1, g.jce2) && in(i, g.ice1, g.ice2);
   const bool ce = valid && in(j, g.jcx1(), g.jcx2()) && in(i, g.icx1(), g.icx2());
   const bool ci = ce && g.gci(j, i);
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
       nb = nb + __shfl_down(nb, w);
     }
     if (threadIdx.x == 0) {
-      const int slot = f.red_off + (f.pt.part == 2 ? f.pt.rbase : 0) + bb;
+      const int slot = f.red_off + (f.pt.part == 2 ? f.pt.rbase : 0) + cb;
       f.red[2 * slot] = na;
       f.red[2 * slot + 1] = nb;
     }

@@ -70,6 +70,10 @@ constexpr int SPC = RCM_SPC, SPG = 8;
 #ifndef SCOR_XCD
 #define SCOR_XCD 1
 #endif
+// k_columns: the same for its column blocks of a whole tile (part 0)
+#ifndef COL_XCD
+#define COL_XCD 0
+#endif
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;
 // LDS-tiled momentum block (dot points j x i at one level).  32 x 8 (256 threads, 39 KB of

@@ -168,3 +168,30 @@ def test_band_c3_tiles_bit_identical():
     til.step(4)
     for name in fields(rc):
         assert np.array_equal(one.get(name), til.get(name)), name
+
+
+def test_band_reference_grid_test_009():
+    """The reference's own band run, Testing/test_009.in: 720 x 210 x 18 at ds = 55.5994675 km,
+    dt = 150 s, i_band = 1, iboudy = 5 (:3-5, 16; a wide, non-square grid) against the oracle
+    after 1, 3 and 10 steps, and its 8-GPU tiling (2 x 4) bit-identical to one tile."""
+    from oracle.oracle import OracleCore
+    rc = dataclasses.replace(CONFIGS["C1"], jx=720, iy=210, kz=18, ds=55.5994675, dt=150.0, i_band=1,
+                             name="test_009 band 720x210x18")
+    data = icbc.generate(rc)
+    st = dict(data["state"])
+    o = OracleCore(rc, data["split"])
+    o.put_state(st)
+    o.bdyval()
+    e = engine(rc, data, st)
+    til = engine(rc, data, st, 2, 4)
+    for name in fields(rc):
+        assert relerr(e.get(name), o.get(name), rc, name) == 0.0, name
+    for nsteps, tol in ((1, 1e-12), (2, 1e-11), (7, 1e-9)):
+        o.step(nsteps)
+        e.step(nsteps)
+        til.step(nsteps)
+        for name in fields(rc):
+            err = relerr(e.get(name), o.get(name), rc, name)
+            assert err < tol, (name, err, nsteps)
+            assert np.array_equal(e.get(name), til.get(name)), name
+    assert e.get_time() == o.get_time() == til.get_time()
