@@ -446,6 +446,8 @@ struct rcmdyn_engine {
       }
     }
     c.pd = cfg.pd;
+    // RCMDYN_NEGFIX_MODE=1 (tests): the row sweep for every marked plane, dense ones included
+    c.negfix_mode = std::getenv("RCMDYN_NEGFIX_MODE") ? std::atoi(std::getenv("RCMDYN_NEGFIX_MODE")) : 0;
     // non-hydrostatic core: diffusion constants (Main/mod_diffusion.F90:108-113), sound
     c.idynamic = cfg.idynamic;
     if (cfg.idynamic == 2) {

@@ -138,6 +138,7 @@ struct Consts {
   // non-hydrostatic core (idynamic = 2): nonhydroparam and init_sound scalars
   int idynamic, ifupr, ifrayd, rayndamp;
   int crm;                     // i_crm = 1: the Rayleigh damping of u, v, pp toward 0, none of t, qv
+  int negfix_mode;             // serial fix of a dense plane: 0 the wavefront, 1 the row sweep (tests)
   double rayalpha0, rayhd, nhbet, nhxkd, nh_dtsmax, nh_xmsf, xgamma, dds[MAXKZ + 2];
   // moisture species (physicsparam ipptls, Main/mod_params.F90:1358-1366): nqx = 2 (qv, qc)
   // or 5 (qv, qc, qi, qr, qs); nsp = nqx - 2 hydrometeors beyond qc

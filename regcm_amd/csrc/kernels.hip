@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __r
   const int plane = (int)blockIdx.x, kz = c->kz, n = plane / kz, k = plane % kz + 1;
   if (NEGFIX_POST) {
     negfix_resolve(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane, k, lds, negfix_lds(g), NoPost{},
-                   [](int, int, double) {});
+                   [](int, int, double) {}, c->negfix_mode);
     return;
   }
   const QvRaw acc{g, c, n ? q.o1qc : q.o1qv, n ? q.o2qc : q.o2qv, q.psc, q.opsa, q.opsb,
@@ -1447,7 +1447,7 @@ __global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __r
                    double x[5];
                    acc.load(jj, i, x);
                    acc.apply(jj, i, v, x);
-                 });
+                 }, c->negfix_mode);
 }
 
 // NEGFIX_POST: the filters of the points k_negfix_serial fixed, a thread per interior point of

@@ -70,9 +70,12 @@ constexpr int SPC = RCM_SPC, SPG = 8;
 #ifndef SCOR_XCD
 #define SCOR_XCD 1
 #endif
-// k_columns: the same for its column blocks of a whole tile (part 0)
+// k_columns: the same for its column blocks of a whole tile (part 0): the next row's column block,
+// whose loads overlap this one's (atm1 at i + 1, p* at i +- 1), on the same XCD.  C3 k_columns
+// 26.4-28.2 -> 24.3-25.6 us, the step 184.8 -> 183.7 us (3 alternations on one box), neutral on
+// the 96 x 48 rank tile (profiles/r06/tile_ab_colx_spbdy.log)
 #ifndef COL_XCD
-#define COL_XCD 0
+#define COL_XCD 1
 #endif
 // depth of the wide exchange: SPH plus the ghost ring the fused split step also produces
 constexpr int SPX = SPH + 1;

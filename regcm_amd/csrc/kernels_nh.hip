@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(512) void k_nh_negfix_serial(Geom g, const Consts* 
   negfix_resolve(g, n ? f.cqc : f.cqv, n ? f.fqc : f.fqv, f.depplane, plane, k, lds, negfix_lds(g), acc,
                  [&](int jj, int i, double v) {
                    if (f.tfuse) nh_filter_q_to(g, c, f, n, jj, i, k, v);
-                 });
+                 }, c->negfix_mode);
 }
 
 // tfuse = 0: the three time filters in place at one interior cross point and level

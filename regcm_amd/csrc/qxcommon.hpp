@@ -243,11 +243,12 @@ __device__ __forceinline__ bool negfix_is_dependent(const Geom& g, const double*
 
 // One (species, level) plane's serial fix by a whole block: nothing when no row is marked, the
 // wavefront when more than NEGFIX_SPARSE rows are and the block has a thread per row (and lds
-// holds the ring), else the row sweep by wavefront 0.  lds: ldsn doubles (see negfix_lds).
+// holds the ring), else the row sweep by wavefront 0.  lds: ldsn doubles (see negfix_lds);
+// mode (Consts::negfix_mode, tests): 1 runs the row sweep on every marked plane.
 constexpr int NEGFIX_SPARSE = 16;
 template <class A, class Post>
 __device__ void negfix_resolve(const Geom& g, const double* sv, double* fx, unsigned* dep, int plane, int k,
-                               double* lds, int ldsn, const A& acc, Post post) {
+                               double* lds, int ldsn, const A& acc, Post post, int mode = 0) {
   const int nw = negfix_rowwords(g), R = g.ici2 - g.ici1 + 1;
   unsigned* words = dep + plane * nw;
   int nm = 0;
@@ -255,7 +256,7 @@ __device__ void negfix_resolve(const Geom& g, const double* sv, double* fx, unsi
   if (nm == 0) return;
   const int T = (int)(blockDim.x * blockDim.y * blockDim.z);
   const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
-  if (nm > NEGFIX_SPARSE && R <= T && 4 * R <= ldsn) {
+  if (mode == 0 && nm > NEGFIX_SPARSE && R <= T && 4 * R <= ldsn) {
     negfix_dense(g, sv, fx, k, lds, acc);
     __syncthreads();                           // every wave read the bitmap before it is cleared
     for (int w = tid; w < nw; w += T) words[w] = 0;

@@ -333,7 +333,7 @@ __device__ __forceinline__ void qx_serial_plane(const Geom& g, const Consts* __r
     __syncthreads();
   }
   if (NEGFIX_POST) {
-    negfix_resolve(g, q.cq[n], q.fq[n], q.dep, plane, k, lds, negfix_lds(g), NoPost{}, [](int, int, double) {});
+    negfix_resolve(g, q.cq[n], q.fq[n], q.dep, plane, k, lds, negfix_lds(g), NoPost{}, [](int, int, double) {}, c->negfix_mode);
     return;
   }
   const QxRaw acc{g, q.a1[n], q.a2[n], q.b1[n], q.b2[n], c->gnu2, k};
@@ -341,7 +341,7 @@ __device__ __forceinline__ void qx_serial_plane(const Geom& g, const Consts* __r
     double x[2];
     acc.load(jj, i, x);
     acc.apply(jj, i, v, x);
-  });
+  }, c->negfix_mode);
 }
 __global__ __launch_bounds__(512) void k_qx_serial(Geom g, const Consts* __restrict__ c, QxArgs q) {
   extern __shared__ double lds[];
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(512) void k_negfix_serial_qx(Geom g, const Consts* 
   }
   const int n = b / kz, k = b % kz + 1;
   negfix_resolve(g, n ? qf.cqc : qf.cqv, n ? qf.fqc : qf.fqv, qf.depplane, b, k, lds, negfix_lds(g), NoPost{},
-                 [](int, int, double) {});
+                 [](int, int, double) {}, c->negfix_mode);
 }
 
 // NEGFIX_POST: filter_raw_4d of the points k_qx_serial fixed, a thread per interior point of a

@@ -147,7 +147,7 @@ NHB_FIELDS = FIELDS[:16]
 def nh_band_case(variant=None):
     """The CRM case's fields as a band (i_crm = 0): periodic in j, the south and north rows
     relax to the boundary data (the initial state) with iboudy = 5 by default."""
-    rc = dataclasses.replace(CONFIGS["CRM"], i_crm=0, iboudy=5, ibltyp=1, **(variant or {}))
+    rc = dataclasses.replace(CONFIGS["CRM"], **{"i_crm": 0, "iboudy": 5, "ibltyp": 1, **(variant or {})})
     data = icbc.generate_crm(rc)
     st = {k: v for k, v in data["state"].items() if "TKE" not in k or rc.ibltyp == 2}
     return rc, data, st

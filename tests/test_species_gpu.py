@@ -218,6 +218,26 @@ def test_species_step_forms(qx_c1, monkeypatch, env):
         assert same, name
 
 
+@pytest.mark.parametrize("name", ["C1", "C3"])
+def test_negfix_wavefront_equals_row_sweep(name, monkeypatch):
+    """The serial fix of a dense plane two ways (qxcommon.hpp): the skewed wavefront (default)
+    and the row sweep in the reference's order (RCMDYN_NEGFIX_MODE=1) give the same state bit for
+    bit, on the patchy hydrometeor fields whose qi / qr / qs and qc planes hold chains of
+    dependent negatives (at C3, the grid of tools/species_bench.py, hundreds of links deep)."""
+    from regcm_amd.dycore import DynCore
+    rc = dataclasses.replace(CONFIGS[name], ipptls=2)
+    data = icbc.generate(CONFIGS[name])
+    st = species_state(rc, data)
+    runs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RCMDYN_NEGFIX_MODE", mode)
+        e = start(DynCore, rc, data, st)
+        e.step(4)
+        runs.append(e)
+    for name_ in ALL:
+        assert np.array_equal(runs[0].get(name_), runs[1].get(name_)), name_
+
+
 def test_species_physics_seam(qx_c1):
     """qxphy of qi, qr, qs enter the sums as the reference adds them (:332-335), against the
     oracle; pre + post physics is the whole tend."""
