@@ -118,6 +118,22 @@ def test_nonhydrostatic_ranks_bit_identical():
         assert np.array_equal(gather(engs, f), ref.get(f)), f
 
 
+@pytest.mark.parametrize("cj,ci", [(2, 2), (1, 2), (2, 1)], ids=str)
+def test_crm_ranks_bit_identical(cj, ci):
+    """PreProc/CRM/crm_test.in's configuration (i_crm = 1: NH, periodic in j and i, UW TKE) on
+    ranks: every tile's four sides are remote peers across one of the two periods (with two
+    tiles in a direction one rank is both neighbours there, with one tile the periodic exchange
+    stays inside the rank), the corner peers wrap in both directions, and the day-alarm sums of
+    the radiative condition are all-reduced.  Bit-identical to one tile."""
+    from regcm_amd.config import CONFIGS as C
+    rc = C["CRM"]
+    data = icbc.generate_crm(rc)
+    engs = run_ranks(rc, data, cj, ci, 4, f"crm{cj}{ci}")
+    ref = single(rc, data, 4)
+    for f in STATE_FIELDS[:12] + NH_STATE_FIELDS + ["ATM1_TKE", "ATM2_TKE"]:
+        assert np.array_equal(gather(engs, f), ref.get(f)), f
+
+
 def test_job_reductions_over_ranks():
     """rcmdyn_reductions is collective: every rank gets the job-wide ptntot/pt2tot (sums of the
     tiles' partials) equal to the single tile's within the reordering of one sum."""
