@@ -240,7 +240,8 @@ int rcmdyn_tile_extent(int32_t jx, int32_t iy, int32_t nproc_j, int32_t nproc_i,
  * directions of i_band (j) and i_crm (i): a periodic direction has no boundary side and its
  * cross range takes every point (Main/mpplib/mod_mppparam.F90:1131-1132, 1340-1360), as the
  * engine's own tiles do.  rcmdyn_tile_extent is this call with i_band = i_crm = 0; a band or
- * CRM host picks its points with this one.  Host-only. */
+ * CRM host picks its points with this one.  Returns non-zero for a tile or flag out of range,
+ * and for i_crm = 1 without i_band = 1 (rcmdyn_create refuses that configuration).  Host-only. */
 int rcmdyn_tile_extent_cfg(const rcmdyn_config* cfg, int32_t tile, int32_t ext[8], int32_t bdy[4]);
 
 /* Communication plan of one rank, host-only (no GPU, no communicator): the halo messages and

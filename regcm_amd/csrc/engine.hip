@@ -2880,6 +2880,7 @@ int rcmdyn_tile_extent_cfg(const rcmdyn_config* cfg, int32_t tile, int32_t ext[8
   if (!cfg || !ext || !bdy) return 1;
   if (tile < 0 || cfg->nproc_j < 1 || cfg->nproc_i < 1 || tile >= cfg->nproc_j * cfg->nproc_i) return 1;
   if ((cfg->i_band != 0 && cfg->i_band != 1) || (cfg->i_crm != 0 && cfg->i_crm != 1)) return 1;
+  if (cfg->i_crm && !cfg->i_band) return 1;              // CRM is built over the band only (create refuses it)
   tile_extent(cfg->jx, cfg->iy, cfg->nproc_j, cfg->nproc_i, tile, ext, bdy, cfg->i_band, cfg->i_crm);
   return 0;
 }

@@ -90,13 +90,16 @@ def test_tile_extents_partition_domain():
     assert widths == [33, 32, 32]
 
 
-@pytest.mark.parametrize("band,crm", [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("band,crm", [(1, 0), (1, 1)])
 def test_tile_extents_periodic(band, crm):
     """rcmdyn_tile_extent_cfg: a periodic direction (i_band: j, i_crm: i) has no boundary side
     on any tile and its cross range takes every point (mod_mppparam.F90:1131-1132, 1340-1360);
-    the tiles still cover the dot grid exactly once, and the other direction is unchanged."""
+    the tiles still cover the dot grid exactly once, and the other direction is unchanged.  CRM
+    without the band is refused, as rcmdyn_create refuses it."""
     jx, iy = 97, 50
     cj, ci = 3, 2
+    with pytest.raises(dycore.EngineError):
+        dycore.tile_extent(jx, iy, cj, ci, 0, i_band=0, i_crm=1)
     cover = [[0] * (jx + 1) for _ in range(iy + 1)]
     for t in range(cj * ci):
         ext, bdy = dycore.tile_extent(jx, iy, cj, ci, t, i_band=band, i_crm=crm)
