@@ -539,6 +539,7 @@ struct rcmdyn_engine {
       t.depxf = talloc<unsigned>(t, (size_t)hc.nsp * kz * (g.ici2 - g.ici1 + 1));
     }
     t.depplane = talloc<unsigned>(t, 2 * (size_t)kz * negfix_rowwords(g));
+    t.depqf = talloc<unsigned>(t, 2 * (size_t)kz * (g.ici2 - g.ici1 + 1));
     if (cfg.idynamic != 2) {
       t.negcnt = talloc<int>(t, 1);
       t.neglist = talloc<uint32_t>(t, 2 * P3);     // every (point, level, qv|qc) at most once
@@ -2413,8 +2414,8 @@ struct rcmdyn_engine {
     const int c = t.cur, o = 1 - c;
     QFix q{t.cqv, t.cqc, t.fqv, t.fqc, t.a1qv[o], t.a1qc[o], t.a2qv[o], t.a2qc[o],
            t.a1qv[c], t.a1qc[c], t.a2qv[c], t.a2qc[c], t.psa_[c], t.psb_[c], t.psc, t.psa_[o], t.psb_[o],
-           t.depplane, nullptr, nullptr};
-    if (qfuse()) { q.negcnt = t.negcnt; q.neglist = t.neglist; }
+           t.depplane, nullptr, nullptr, nullptr};
+    if (qfuse()) { q.negcnt = t.negcnt; q.neglist = t.neglist; q.depf = t.depqf; }
     return q;
   }
 

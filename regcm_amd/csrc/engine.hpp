@@ -206,6 +206,7 @@ struct Tile {
   double *cqx[NQXH] = {}, *fqx[NQXH] = {}, *slqx[NQXH] = {}, *d6qx[NQXH] = {};
   unsigned* depx = nullptr;          // nqx = 5: the species planes' row bitmaps (as depplane)
   unsigned* depxf = nullptr;         // nqx = 5: the species planes' row flags (k_qx_fix -> k_qx_serial)
+  unsigned* depqf = nullptr;         // qfuse: the qv / qc planes' row flags (negfix_list -> the serial passes)
   unsigned *depplane;              // per (n,k) plane: bitmap of the rows with a serially dependent negative point
   int* negcnt = nullptr;           // hydrostatic qfuse: the negative forecasts k_scalars listed
   uint32_t* neglist = nullptr;

@@ -239,6 +239,7 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
     constexpr int KU = COL_KU;
     for (int k0 = ty + 1; k0 <= kz; k0 += COLG * KU) {
       double u00[KU], u10[KU], u01[KU], u11[KU], v00[KU], v10[KU], v01[KU], v11[KU], tt[KU], qq[KU], cc[KU];
+      double xq[KU][QX ? NQXH : 1];
 #pragma unroll
       for (int n = 0; n < KU; n++) {
         const int kk = k0 + COLG * n;
@@ -246,6 +247,10 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
         u00[n] = LD(f.a1u, o3); u10[n] = LD(f.a1u, O3(1, 0)); u01[n] = LD(f.a1u, O3(0, 1)); u11[n] = LD(f.a1u, O3(1, 1));
         v00[n] = LD(f.a1v, o3); v10[n] = LD(f.a1v, O3(1, 0)); v01[n] = LD(f.a1v, O3(0, 1)); v11[n] = LD(f.a1v, O3(1, 1));
         tt[n] = LD(f.a1t, o3); qq[n] = LD(f.a1qv, o3); cc[n] = LD(f.a1qc, o3);
+        // nqx = 5: the species of the total water load, in the same round of loads
+        if (QX)
+#pragma unroll
+          for (int q = 0; q < NQXH; q++) xq[n][q] = LD(f.qxa1[q], o3);
       }
 #pragma unroll
       for (int n = 0; n < KU; n++) {
@@ -260,19 +265,16 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
       // ipgf = 1: minus the reference-atmosphere temperature (ttld, :1893-1964)
       if (c->ipgf == 1) tdk = tdk - psk * T00PG * rcm_powpos((c->hsigma[k] * psk + ptop) / P00PG, c->pgfaa1);
       sTD[(k - 1) * COLW + tx] = tdk;
-      sTV[(k - 1) * COLW + tx] = d_one / (d_one + qc / (d_one + qv));
-      }
-    }
-    if (QX) {
-      // nqx = 5: tvfac with the total water load qcd = ((0 + qc) + qi) + qr + qs (decouple
-      // :1107-1115, each atmx%qx = max(atm1 * rpsa, 0); pressure_gradient_force :2037), over the
-      // levels this thread formed above
-      for (int k = ty + 1; k <= kz; k += COLG) {
-        const uint32_t o3 = o2 + (uint32_t)(k - 1) * L8;
-        const double qv = dmax(LD(f.a1qv, o3) * rp, MINQQ);
-        double qcd = d_zero + dmax(LD(f.a1qc, o3) * rp, d_zero);
-        for (int q = 0; q < NQXH; q++) qcd = qcd + dmax(LD(f.qxa1[q], o3) * rp, d_zero);
+      if (QX) {
+        // nqx = 5: tvfac with the total water load qcd = ((0 + qc) + qi) + qr + qs (decouple
+        // :1107-1115, each atmx%qx = max(atm1 * rpsa, 0); pressure_gradient_force :2037)
+        double qcd = d_zero + qc;
+#pragma unroll
+        for (int q = 0; q < NQXH; q++) qcd = qcd + dmax(xq[n][q] * rp, d_zero);
         sTV[(k - 1) * COLW + tx] = d_one / (d_one + qcd / (d_one + qv));
+      } else {
+        sTV[(k - 1) * COLW + tx] = d_one / (d_one + qc / (d_one + qv));
+      }
       }
     }
     PT_MARK();
@@ -1394,6 +1396,10 @@ __global__ __launch_bounds__(256, QF_LB) void k_qfilter(Geom g, const Consts* __
 __device__ __forceinline__ void negfix_serial_plane(Geom g, const Consts* c, QFix q, int plane_id, double* lds) {
   const int kz = c->kz;
   const int n = plane_id / kz, k = plane_id % kz + 1;
+  if (q.depf) {                        // the list pass's row flags (one wavefront calls this)
+    negfix_collect(g, q.depf, q.depplane, plane_id, (int)threadIdx.x & 63, 64);
+    wave_lds_sync();
+  }
   const double* o1 = n ? q.o1qc : q.o1qv;
   const double* o2 = n ? q.o2qc : q.o2qv;
   double* n1p = n ? q.n1qc : q.n1qv;
@@ -1435,6 +1441,10 @@ struct QvRaw {
 __global__ __launch_bounds__(512) void k_negfix_serial(Geom g, const Consts* __restrict__ c, QFix q) {
   extern __shared__ double lds[];
   const int plane = (int)blockIdx.x, kz = c->kz, n = plane / kz, k = plane % kz + 1;
+  if (q.depf) {
+    negfix_collect(g, q.depf, q.depplane, plane, (int)threadIdx.x, (int)blockDim.x);
+    __syncthreads();
+  }
   if (NEGFIX_POST) {
     negfix_resolve(g, n ? q.cqc : q.cqv, n ? q.fqc : q.fqv, q.depplane, plane, k, lds, negfix_lds(g), NoPost{},
                    [](int, int, double) {}, c->negfix_mode);
@@ -1481,7 +1491,8 @@ __device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int
     const int i = g.i0 + (int)(r / g.pitch), j = g.j0 + (int)(r % g.pitch);
     const double* sv = n ? q.cqc : q.cqv;
     if (negfix_dependent(g, sv, j, i, k)) {
-      negfix_mark(g, q.depplane, n * c->kz + (k - 1), i);
+      if (q.depf) q.depf[(n * c->kz + (k - 1)) * (g.ici2 - g.ici1 + 1) + (i - g.ici1)] = 1u;
+      else negfix_mark(g, q.depplane, n * c->kz + (k - 1), i);
       continue;
     }
     double* fx = n ? q.fqc : q.fqv;

@@ -197,6 +197,10 @@ struct QFix {
   // in parallel; the serial sweeps of the flagged planes run in k_split_correct)
   const int* negcnt;
   const uint32_t* neglist;
+  // qfuse: per (qv | qc, level) plane and row, the list pass's flag of a dependent point (a plain
+  // store: atomics on the few bitmap words of a plane serialise at the memory side); the serial
+  // passes OR the flags into depplane first (negfix_collect, qxcommon.hpp)
+  unsigned* depf;
 };
 
 __global__ void k_surface_pressures(Geom g, Fields f);

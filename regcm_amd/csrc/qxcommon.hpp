@@ -46,6 +46,23 @@ __device__ __forceinline__ void negfix_mark(const Geom& g, unsigned* dep, int pl
   const int r = i - g.ici1;
   atomicOr(&dep[plane * negfix_rowwords(g) + (r >> 5)], 1u << (r & 31));
 }
+// The row flags a parallel pass stored for plane `plane` (depf: R flags per plane, a plain
+// store per dependent point) ORed into its bitmap words, the flags cleared for the next step:
+// the tid-th of nt threads (nt a multiple of 64, whole wavefronts: a row chunk per wavefront
+// and ballot); the caller synchronises before the words are read.
+__device__ __forceinline__ void negfix_collect(const Geom& g, unsigned* depf, unsigned* dep, int plane, int tid, int nt) {
+  const int R = g.ici2 - g.ici1 + 1;
+  unsigned* fl = depf + plane * R;
+  unsigned* words = dep + plane * negfix_rowwords(g);
+  for (int b = 0; b < R; b += nt) {
+    const int r = b + tid;
+    const bool f = r < R && fl[r] != 0u;
+    if (f) fl[r] = 0u;
+    const unsigned long long m = __ballot(f);
+    const unsigned w = (unsigned)(m >> (r & 32));
+    if (r < R && (r & 31) == 0 && w) words[r >> 5] |= w;
+  }
+}
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

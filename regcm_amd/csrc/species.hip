@@ -359,6 +359,10 @@ __global__ __launch_bounds__(512) void k_negfix_serial_qx(Geom g, const Consts* 
     return;
   }
   const int n = b / kz, k = b % kz + 1;
+  if (qf.depf) {
+    negfix_collect(g, qf.depf, qf.depplane, b, (int)threadIdx.x, (int)blockDim.x);
+    __syncthreads();
+  }
   negfix_resolve(g, n ? qf.cqc : qf.cqv, n ? qf.fqc : qf.fqv, qf.depplane, b, k, lds, negfix_lds(g), NoPost{},
                  [](int, int, double) {}, c->negfix_mode);
 }
