@@ -156,6 +156,9 @@ __device__ __forceinline__ bool part_skip(const Part& p, int j1, int j2, int i1,
 #ifndef COL_KU
 #define COL_KU 1
 #endif
+#ifndef COL_PF
+#define COL_PF 1
+#endif
 // QX: nqx = 5, tvfac with the total water load (an instance of its own, so the nqx = 2 kernel
 // keeps its code)
 template <bool QX>
@@ -285,6 +288,36 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
                                         : rcm_log((c->hsigma[kz] + ptop * rp) / (d_one + ptop * rp));
     PT_MARK();
   }
+  // the operands of new_pressure (scan wavefront) and of the geopotential column are loaded
+  // before the barrier, so their latency overlaps the wait for the other level groups instead
+  // of following the pten / qdot scan (COL_PF = 0: loaded where they are used)
+  const int gwave = COLW == 32 ? 2 : 1;
+#if COL_PF
+  double psbv = 0.0, pav = 0.0, pbt0 = 0.0, dtv = 0.0, xbt = 0.0, fg1[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  int rgc = 0, ibc = 0;
+  if (ce && ty == 0) {
+    psbv = LD(f.psb, o2);
+    pav = LD(f.psa, o2);
+    rgc = f.rgcr[o2 >> 3];
+    ibc = f.ibcr[o2 >> 3];
+    dtv = s->dt;
+    xbt = s->xbctime;
+    if (ci) {
+      pbt0 = LD(f.pbt, o2);
+      const int dj[5] = {0, -1, 1, 0, 0}, di[5] = {0, 0, 0, -1, 1};
+#pragma unroll
+      for (int n = 0; n < 5; n++) {
+        const uint32_t q = O2(dj[n], di[n]);
+        fg1[n] = (LD(f.pb0, q) + (xbt + dtv) * LD(f.pbt, q)) - LD(f.psb, q);
+      }
+    }
+  }
+  double gps = 0.0, ght = 0.0;
+  if (ce && ty == gwave) {
+    gps = LD(f.psa, o2);
+    ght = LD(f.ht, o2);
+  }
+#endif
   __syncthreads();
   PT_MARK();
   double na = 0.0, nb = 0.0;
@@ -306,6 +339,17 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
     }
     if (ce) {
       // new_pressure
+#if COL_PF
+      const double dt = dtv;
+      if (ci && rgc > 0 && c->iboudy == 4) {
+        // sponge2d, Main/mod_bdycod.F90:3065-3122
+        pt = c->wgtx[ibc] * pt + (d_one - c->wgtx[ibc]) * pbt0;
+      } else if (ci && rgc > 0) {
+        double xf, xg;
+        nudge_coef(c, ibc, kz, xf, xg);
+        pt = relax(pt, xf, xg, fg1[0], fg1[1], fg1[2], fg1[3], fg1[4]);
+      }
+#else
       const double dt = s->dt;
       const double psbv = LD(f.psb, o2);
       if (ci && f.rgcr[o2 >> 3] > 0 && c->iboudy == 4) {
@@ -320,12 +364,17 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
         pt = relax(pt, xf, xg, FG1(0, 0), FG1(-1, 0), FG1(1, 0), FG1(0, -1), FG1(0, 1));
 #undef FG1
       }
+#endif
       ST(f.ptenn, o2, pt);
       const double pc = psbv + pt * dt;
       ST(f.psc, o2, pc);
       if (f.qfuse) {
         // the RA filter of p* (Main/mod_tendency.F90:420, filter_ra_2d) into the next buffers
+#if COL_PF
+        const double pa = pav;
+#else
         const double pa = LD(f.psa, o2);
+#endif
         if (ci) {
           const double d = c->gnu1 * (pc + psbv - d_two * pa);
           ST(f.bpsb, o2, pa + d);
@@ -337,18 +386,27 @@ __global__ __launch_bounds__(COLT, COL_LB) void k_columns(Geom g, const Consts* 
       }
       if (s->lcount > 0 && ci && own) {
         na = fabs(pt);
+#if COL_PF
+        nb = fabs((pc + psbv - d_two * pav) / (dt * dt * d_rfour));
+#else
         nb = fabs((pc + psbv - d_two * LD(f.psa, o2)) / (dt * dt * d_rfour));
+#endif
       }
     }
   }
   // the geopotential column on another wavefront than the pten/qdot scan (COLW = 32: level
   // groups 2k and 2k+1 share wavefront k)
-  if (ce && ty == (COLW == 32 ? 2 : 1)) {
+  if (ce && ty == gwave) {
     // geopotential column, bottom-up
+#if COL_PF
+    const double ps = gps;
+    double top = ght;
+#else
     const double ps = LD(f.psa, o2);
+    double top = LD(f.ht, o2);
+#endif
     double tdk1 = sTD[(kz - 1) * COLW + tx];
     const double tv = tdk1 * rp * sTV[(kz - 1) * COLW + tx];
-    double top = LD(f.ht, o2);
     if (c->ipgf == 1) top = top + rgas * T00PG / c->pgfaa1 * rcm_powpos((ps + ptop) / P00PG, c->pgfaa1);  // :2045
     double ph = top - rgas * tv * sLG[(kz - 1) * COLW + tx];
     ST(f.phi, o2 + (uint32_t)(kz - 1) * L8, ph);
@@ -1521,6 +1579,9 @@ __device__ __forceinline__ void negfix_list(Geom g, const Consts* c, QFix q, int
 #ifndef SP_KU
 #define SP_KU 1
 #endif
+#ifndef SP_PF
+#define SP_PF 1
+#endif
 __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
     Geom g, const Consts* __restrict__ c, const double* __restrict__ a1u, const double* __restrict__ a1v,
     const double* __restrict__ a2u, const double* __restrict__ a2v, const double* __restrict__ a1t,
@@ -1602,12 +1663,27 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
       }
     }
   }
+  // the 2-D operands of this thread's first (mode, sum) item are loaded before the barrier, so
+  // their latency overlaps the wait instead of following it (SP_PF = 0: loaded where used)
+  const int ns = c->nsplit;
+  const long q = valid ? g.ix(j, i) : 0;
+#if SP_PF
+  double pf_st = 0.0, pf_a = 0.0, pf_b = 0.0;
+  if (valid && ty < 2 * ns) {
+    const int l = ty % ns + 1;
+    if (ty < ns) {
+      pf_st = dstor[(long)(l - 1) * g.plane + q];
+      if (ce) pf_a = F2(mapf, j, i);
+    } else {
+      pf_st = hstor[(long)(l - 1) * g.plane + q];
+      if (ce) { pf_a = F2(psa, j, i); pf_b = F2(psb, j, i); }
+    }
+  }
+#endif
   __syncthreads();
   PT_MARK();
   if (!valid) return;
-  const long q = g.ix(j, i);
   const double rdx2 = d_one / c->dx2;
-  const int ns = c->nsplit;
   // decomposed domain: the split step's inputs also go to the wide frame its exchange fills
   const long qw = wdeld ? gw.ix(j, i) : 0;
 #define WSLOT(a, l, s) ((a) + ((long)((s) - 1) * c->nsplit + ((l) - 1)) * gw.plane)
@@ -1617,11 +1693,12 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
   }
   for (int w = ty; w < 2 * ns; w += SPG) {
     const int l = w % ns + 1;
+    const bool pf = SP_PF && w == ty;
     if (w < ns) {
-      const double ds = dstor[(long)(l - 1) * g.plane + q];
+      const double ds = pf ? pf_st : dstor[(long)(l - 1) * g.plane + q];
       double d3 = d_zero, d2 = d_zero;
       if (ce) {
-        const double mf = F2(mapf, j, i);
+        const double mf = pf ? pf_a : F2(mapf, j, i);
         for (int k = 1; k <= kz; k++) {
           const double zr = c->zmatxr[l - 1][k - 1];
           d3 = d3 + zr * rdx2 * mf * sD1[(k - 1) * SPC + tx];
@@ -1634,10 +1711,10 @@ __global__ __launch_bounds__(SPC * SPG, SP_LB) void k_split_project(
       if (wdeld) { WSLOT(wdeld, l, 1)[qw] = ds - d2; WSLOT(wdeld, l, 2)[qw] = d2; WSLOT(wdeld, l, 3)[qw] = d3 - ds; }
       dstor[(long)(l - 1) * g.plane + q] = d2;
     } else {
-      const double hs = hstor[(long)(l - 1) * g.plane + q];
+      const double hs = pf ? pf_st : hstor[(long)(l - 1) * g.plane + q];
       double h3 = d_zero, h2 = d_zero;
       if (ce) {
-        const double pa = F2(psa, j, i), pbv = F2(psb, j, i);
+        const double pa = pf ? pf_a : F2(psa, j, i), pbv = pf ? pf_b : F2(psb, j, i);
         const double rpa = d_one / pa, rpbv = d_one / pbv;
         h3 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pa - c->pd);
         h2 = c->pdlog[l - 1][kz + 1] + c->eps1[l - 1][kz + 1] * (pbv - c->pd);
