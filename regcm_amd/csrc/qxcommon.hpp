@@ -243,6 +243,101 @@ __device__ void negfix_dense(const Geom& g, const double* sv, double* fx, int k,
   }
 }
 
+// The same wavefront with the row-to-row hand-over in registers (NEGFIX_DPP): lane l of a
+// wavefront holds row r = 64 w + l, and the value row r - 1 fixed in the previous step moves to
+// lane l with one cross-lane shift (DPP wave_shr:1, or __shfl_up with NEGFIX_DPP = 2) instead of
+// an LDS ring behind a block barrier every step.  Each lane keeps the three values of the row
+// above that its window reads (columns jj - 1, jj, jj + 1) in registers.  Lane 0 of wavefront w > 0
+// takes row 64 w - 1's values from an LDS ring written by lane 63 of wavefront w - 1, which runs
+// SK steps ahead (wavefront w's rows start SK steps later than the two-per-row skew gives), so one
+// block barrier every SK steps makes those writes visible: W + 2 (R - 1) + SK (nw - 1) steps.
+// Every value is the same expression on the same operands as negfix_dense's, bit for bit.
+#ifndef NEGFIX_DPP
+#define NEGFIX_DPP 1
+#endif
+__device__ __forceinline__ double lane_shr1(double x) {      // lane l gets lane l - 1's x
+#if NEGFIX_DPP == 2
+  return __shfl_up(x, 1, 64);
+#else
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);   // wave_shr:1
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+#endif
+}
+template <class A>
+__device__ void negfix_dense_dpp(const Geom& g, const double* sv, double* fx, int k, double* ring, const A& acc) {
+  constexpr int P = 4, NQ = 3 + A::NI, SK = 8;
+  const int r = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
+  const int lane = r & 63, wv = r >> 6;
+  const int R = g.ici2 - g.ici1 + 1, W = g.jci2 - g.jci1 + 1, nwv = (R + 63) >> 6;
+  const int S = W + 2 * (R - 1) + SK * (nwv - 1);
+  const bool act = r < R;
+  const int i = g.ici1 + r;
+  auto qload = [&](int jc, double* q) {
+    const bool ok = act && jc >= g.jci1 - 1 && jc <= g.jci2 + 1;
+#pragma unroll
+    for (int d = 0; d < 3; d++) q[d] = ok ? F3(sv, jc, i - 1 + d, k) : 0.0;
+    if (act && in(jc, g.jci1, g.jci2)) acc.load(jc, i, q + 3);
+    else
+#pragma unroll
+      for (int d = 3; d < NQ; d++) q[d] = 0.0;
+  };
+  int j = g.jci1 - 2 * r - SK * wv;          // this row's column at step 0
+  double w0[NQ], w1[NQ], w2[NQ], qa[P][NQ], qb[P][NQ];
+  qload(j - 1, w0);
+  qload(j, w1);
+  qload(j + 1, w2);
+#pragma unroll
+  for (int u = 0; u < P; u++) qload(j + 2 + u, qa[u]);
+  double prev = 0.0;                         // the fixed value of (j - 1, i)
+  double pub = 0.0;                          // this lane's value of the last step (for row i + 1)
+  double cm1 = 0.0, c0 = 0.0, cp1 = 0.0;     // row i - 1's values at columns jj - 1, jj, jj + 1
+  const bool up = r >= 1;                    // row i - 1 is interior
+  const bool from_ring = lane == 0 && wv > 0, to_ring = lane == 63 && wv < nwv - 1;
+  for (int t0 = 0; t0 < S; t0 += P) {
+#pragma unroll
+    for (int u = 0; u < P; u++) qload(j + 2 + P + u, qb[u]);
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int t = t0 + u, jj = j + u;
+      if ((t & (SK - 1)) == 0) lds_barrier();  // lane 63's ring writes of SK or more steps ago
+      double recv = lane_shr1(pub);
+      if (from_ring) recv = ring[(wv - 1) * 64 + ((jj + 1) & 63)];
+      cm1 = c0; c0 = cp1; cp1 = recv;
+      if (act && t < S && in(jj, g.jci1, g.jci2) && w1[1] < d_zero) {
+        const bool p0 = up && jj - 1 >= g.jci1 && w0[0] < d_zero, p1 = up && w1[0] < d_zero;
+        const bool p2 = up && jj + 1 <= g.jci2 && w2[0] < d_zero, p3 = jj - 1 >= g.jci1 && w0[1] < d_zero;
+        double sum = 0.0;
+        sum = sum + fabs(p0 ? cm1 : w0[0]);
+        sum = sum + fabs(p1 ? c0 : w1[0]);
+        sum = sum + fabs(p2 ? cp1 : w2[0]);
+        sum = sum + fabs(p3 ? prev : w0[1]);
+        sum = sum + fabs(w1[1]);
+        sum = sum + fabs(w2[1]);
+        sum = sum + fabs(w0[2]);
+        sum = sum + fabs(w1[2]);
+        sum = sum + fabs(w2[2]);
+        const double xs = 0.01 * sum;
+        const double v = xs >= 0x1p-960 ? div_by(xs, 9.0, 1.0 / 9.0) : xs / 9.0;
+        pub = v;
+        prev = v;
+        if (p0 || p1 || p2 || p3) {
+          F3(fx, jj, i, k) = v;
+          acc.apply(jj, i, v, w1 + 3);
+        }
+      }
+      if (to_ring) ring[wv * 64 + (jj & 63)] = pub;
+#pragma unroll
+      for (int d = 0; d < NQ; d++) { w0[d] = w1[d]; w1[d] = w2[d]; w2[d] = qa[u][d]; }
+    }
+#pragma unroll
+    for (int u = 0; u < P; u++)
+#pragma unroll
+      for (int d = 0; d < NQ; d++) qa[u][d] = qb[u][d];
+    j += P;
+  }
+}
+
 // NEGFIX_POST (kernels.hpp): the serial pass resolves the chain only (the fixed values into fx)
 // and a parallel launch afterwards (k_negfix_post, k_qx_post) applies the filters of the
 // dependent points, so the wavefront's steps carry the forecasts alone: every load of the
@@ -274,7 +369,8 @@ __device__ void negfix_resolve(const Geom& g, const double* sv, double* fx, unsi
   const int T = (int)(blockDim.x * blockDim.y * blockDim.z);
   const int tid = (int)(threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z));
   if (mode == 0 && nm > NEGFIX_SPARSE && R <= T && 4 * R <= ldsn) {
-    negfix_dense(g, sv, fx, k, lds, acc);
+    if (NEGFIX_DPP) negfix_dense_dpp(g, sv, fx, k, lds, acc);
+    else negfix_dense(g, sv, fx, k, lds, acc);
     __syncthreads();                           // every wave read the bitmap before it is cleared
     for (int w = tid; w < nw; w += T) words[w] = 0;
     return;
