@@ -496,6 +496,9 @@ constexpr int TC_NF = 5;
 #ifndef TC_W
 #define TC_W 1      // 6 or 8 waves/SIMD measured slower (4.73, 5.35 ms against 3.82)
 #endif
+#ifndef TC_UV
+#define TC_UV 1
+#endif
 // relaxation and physics-tendency terms of k_nh_tend_c and k_nh_tend_d (#undef after k_nh_tend_d)
 #define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
 #define RELAX5(x, b0, bt, a) \
@@ -516,6 +519,41 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   const int kz = c->kz;
   const double xt = s->xbctime + s->dt;
   const bool inframe = j < g.j0 + g.nj && i < g.i0 + g.ni;
+#if TC_UV
+  // TC_UV: atm1 u, v of levels k and k - 1 at the block's (32 + 1) x (8 + 1) dot points, staged
+  // too: the four-point wind averages of start_advect and the adiabatic term read them at every
+  // cross point of the block (the same values, so the same bits)
+  __shared__ double sU[2][TCI + 1][TCJ + 1], sV[2][TCI + 1][TCJ + 1];
+  {
+    const int J0 = g.j0 + TBX * TCJ, I0 = g.i0 + TBY * TCI;
+    const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+    constexpr int ND = (TCJ + 1) * (TCI + 1), NSU = (ND + TCT - 1) / TCT;
+    double vu[NSU][4];
+#pragma unroll
+    for (int n = 0; n < NSU; n++) {
+      const int q = tid + n * TCT, jg = J0 + q % (TCJ + 1), ig = I0 + q / (TCJ + 1);
+      const bool okq = q < ND && jg < g.j0 + g.nj && ig < g.i0 + g.ni;
+      const int jr = okq ? jg : g.j0, ir = okq ? ig : g.i0;
+      vu[n][0] = (okq && k <= kz) ? F3(f.a1u, jr, ir, k) : 0.0;
+      vu[n][1] = (okq && k <= kz) ? F3(f.a1v, jr, ir, k) : 0.0;
+      vu[n][2] = (okq && k >= 2 && k - 1 <= kz) ? F3(f.a1u, jr, ir, k - 1) : 0.0;
+      vu[n][3] = (okq && k >= 2 && k - 1 <= kz) ? F3(f.a1v, jr, ir, k - 1) : 0.0;
+    }
+#pragma unroll
+    for (int n = 0; n < NSU; n++) {
+      const int q = tid + n * TCT, jj = q % (TCJ + 1), ii = q / (TCJ + 1);
+      if (q < ND) {
+        sU[0][ii][jj] = vu[n][0]; sV[0][ii][jj] = vu[n][1];
+        sU[1][ii][jj] = vu[n][2]; sV[1][ii][jj] = vu[n][3];
+      }
+    }
+  }
+#define A1U(dj, di, kk) sU[(kk) == k ? 0 : 1][(int)threadIdx.y + (di)][(int)threadIdx.x + (dj)]
+#define A1V(dj, di, kk) sV[(kk) == k ? 0 : 1][(int)threadIdx.y + (di)][(int)threadIdx.x + (dj)]
+#else
+#define A1U(dj, di, kk) F3(f.a1u, j + (dj), i + (di), kk)
+#define A1V(dj, di, kk) F3(f.a1v, j + (dj), i + (di), kk)
+#endif
   {
     const int J0 = g.j0 + TBX * TCJ - 2, I0 = g.i0 + TBY * TCI - 2;
     const int tid = threadIdx.y * blockDim.x + threadIdx.x;
@@ -584,10 +622,10 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     }
   };
   auto avg = [&](int kk, double& u1, double& u2, double& v1, double& v2) {   // start_advect :114-119
-    u1 = F3(f.a1u, j, i + 1, kk) * m01 + F3(f.a1u, j, i, kk) * m00;          // umc = atm1 u * msfd
-    u2 = F3(f.a1u, j + 1, i + 1, kk) * m11 + F3(f.a1u, j + 1, i, kk) * m10;
-    v1 = F3(f.a1v, j + 1, i, kk) * m10 + F3(f.a1v, j, i, kk) * m00;
-    v2 = F3(f.a1v, j + 1, i + 1, kk) * m11 + F3(f.a1v, j, i + 1, kk) * m01;
+    u1 = A1U(0, 1, kk) * m01 + A1U(0, 0, kk) * m00;                         // umc = atm1 u * msfd
+    u2 = A1U(1, 1, kk) * m11 + A1U(1, 0, kk) * m10;
+    v1 = A1V(1, 0, kk) * m10 + A1V(0, 0, kk) * m00;
+    v2 = A1V(1, 1, kk) * m11 + A1V(0, 1, kk) * m01;
   };
   // boundary relaxation (:1462-1501, Main/mod_bdycod.F90): nudging coefficients of the band
   const bool band = f.rgcr[g.ix(j, i)] > 0;
@@ -630,12 +668,8 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
     if (k >= 2) wd = wd + wflux(k - 1) * c->dds[k];
     if (k <= kz) wd = wd - wflux(k) * c->dds[k];
     if (k >= 2 && k <= kz) {                       // adiabatic NH, Main/mod_tendency.F90:1601-1671
-      auto ucc = [&](int kk) {
-        return F3(f.a1u, j, i, kk) + F3(f.a1u, j, i + 1, kk) + F3(f.a1u, j + 1, i, kk) + F3(f.a1u, j + 1, i + 1, kk);
-      };
-      auto vcc = [&](int kk) {
-        return F3(f.a1v, j, i, kk) + F3(f.a1v, j, i + 1, kk) + F3(f.a1v, j + 1, i, kk) + F3(f.a1v, j + 1, i + 1, kk);
-      };
+      auto ucc = [&](int kk) { return A1U(0, 0, kk) + A1U(0, 1, kk) + A1U(1, 0, kk) + A1U(1, 1, kk); };
+      auto vcc = [&](int kk) { return A1V(0, 0, kk) + A1V(0, 1, kk) + A1V(1, 0, kk) + A1V(1, 1, kk); };
       const double uk = ucc(k), vk = vcc(k), um = ucc(k - 1), vm = vcc(k - 1);
       const double rps = r0;
       const double ex = F2(f.ex, j, i), crx = F2(f.crx, j, i), cry = F2(f.cry, j, i);
@@ -794,6 +828,8 @@ __global__ __launch_bounds__(TCT, TC_W) void k_nh_tend_c(Geom g, const Consts* _
   }
 }
 
+#undef A1U
+#undef A1V
 template __global__ void k_nh_tend_c<false>(Geom, const Consts* __restrict__, const StepState* __restrict__, NHFields,
                                              int, int);
 template __global__ void k_nh_tend_c<true>(Geom, const Consts* __restrict__, const StepState* __restrict__, NHFields,
