@@ -499,6 +499,9 @@ constexpr int TC_NF = 5;
 #ifndef TC_UV
 #define TC_UV 1
 #endif
+#ifndef TD_X
+#define TD_X 1
+#endif
 // relaxation and physics-tendency terms of k_nh_tend_c and k_nh_tend_d (#undef after k_nh_tend_d)
 #define FG(b0, bt, a, J, I) ((F3(b0, J, I, k) + xt * F3(bt, J, I, k)) - F3(a, J, I, k))
 #define RELAX5(x, b0, bt, a) \
@@ -846,6 +849,44 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
   __shared__ double sUA[TDH][TDW], sVA[TDH][TDW], sU[TDH][TDW], sV[TDH][TDW], sCR[TDH][TDW];
   __shared__ double sBU[TDH][TDW], sBV[TDH][TDW];
   const int j = g.jdi1 + TBX * 64 + (int)threadIdx.x, i = g.idi1 + TBY * TD_I + (int)threadIdx.y, k = TBZ + 1;
+#if TD_X
+  // TD_X: the cross fields a dot point averages over its four cross points -- qdot at k and
+  // k + 1 (vadvuv), atm1 w at k and k + 1 (the curvature terms) and xkcr at k (calc_coeff's xkd)
+  // -- at the block's 65 x (TD_I + 1) cross points (j - 1 .. j + 63, i - 1 .. i + TD_I - 1)
+  __shared__ double sQD[2][TD_I + 1][65], sWD[2][TD_I + 1][65], sXK[TD_I + 1][65];
+  {
+    const int J0 = g.jdi1 + TBX * 64 - 1, I0 = g.idi1 + TBY * TD_I - 1;
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    constexpr int NC = 65 * (TD_I + 1), NSC = (NC + TDT - 1) / TDT;
+    double vc[NSC][5];
+#pragma unroll
+    for (int n = 0; n < NSC; n++) {
+      const int q = tid + n * TDT, jg = J0 + q % 65, ig = I0 + q / 65;
+      const bool okq = q < NC && jg >= g.j0 && jg < g.j0 + g.nj && ig >= g.i0 && ig < g.i0 + g.ni;
+      const int jr = okq ? jg : j0c(g), ir = okq ? ig : i0c(g);
+      vc[n][0] = okq ? F3(f.qdot, jr, ir, k) : 0.0;
+      vc[n][1] = okq ? F3(f.qdot, jr, ir, k + 1) : 0.0;
+      vc[n][2] = okq ? F3(f.a1w, jr, ir, k) : 0.0;
+      vc[n][3] = okq ? F3(f.a1w, jr, ir, k + 1) : 0.0;
+      vc[n][4] = okq ? F3(f.xkcr, jr, ir, k) : 0.0;
+    }
+#pragma unroll
+    for (int n = 0; n < NSC; n++) {
+      const int q = tid + n * TDT, jj = q % 65, ii = q / 65;
+      if (q < NC) {
+        sQD[0][ii][jj] = vc[n][0]; sQD[1][ii][jj] = vc[n][1];
+        sWD[0][ii][jj] = vc[n][2]; sWD[1][ii][jj] = vc[n][3]; sXK[ii][jj] = vc[n][4];
+      }
+    }
+  }
+#define QDC(dj, di, kk) sQD[(kk) == k ? 0 : 1][(int)threadIdx.y + 1 + (di)][(int)threadIdx.x + 1 + (dj)]
+#define WDC(dj, di, kk) sWD[(kk) == k ? 0 : 1][(int)threadIdx.y + 1 + (di)][(int)threadIdx.x + 1 + (dj)]
+#define XKC(dj, di) sXK[(int)threadIdx.y + 1 + (di)][(int)threadIdx.x + 1 + (dj)]
+#else
+#define QDC(dj, di, kk) F3(f.qdot, j + (dj), i + (di), kk)
+#define WDC(dj, di, kk) F3(f.a1w, j + (dj), i + (di), kk)
+#define XKC(dj, di) F3(f.xkcr, j + (dj), i + (di), k)
+#endif
   {
     const int J0 = g.jdi1 + TBX * 64 - 2, I0 = g.idi1 + TBY * TD_I - 2;
     const int tid = threadIdx.y * 64 + threadIdx.x;
@@ -916,8 +957,7 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
   // (subtracted), in the reference's loop order
   {
     auto flux = [&](int kk, double& uu, double& vv) {
-      const double qq = d_rfour * (F3(f.qdot, j, i, kk) + F3(f.qdot, j, i - 1, kk) + F3(f.qdot, j - 1, i, kk) +
-                                   F3(f.qdot, j - 1, i - 1, kk));
+      const double qq = d_rfour * (QDC(0, 0, kk) + QDC(0, -1, kk) + QDC(-1, 0, kk) + QDC(-1, -1, kk));
       uu = qq * (c->twt1[kk] * F3(f.a1u, j, i, kk) + c->twt2[kk] * F3(f.a1u, j, i, kk - 1));
       vv = qq * (c->twt1[kk] * F3(f.a1v, j, i, kk) + c->twt2[kk] * F3(f.a1v, j, i, kk - 1));
     };
@@ -935,10 +975,8 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
   }
   // curvature NH (:1839-1879): horizontal and vertical Coriolis, horizontal and vertical curvature
   {
-    const double* w = f.a1w;
-    const double wadot = 0.125 * (F3(w, j - 1, i - 1, k) + F3(w, j - 1, i, k) + F3(w, j, i - 1, k) + F3(w, j, i, k));
-    const double wadotp1 = 0.125 * (F3(w, j - 1, i - 1, k + 1) + F3(w, j - 1, i, k + 1) + F3(w, j, i - 1, k + 1) +
-                                    F3(w, j, i, k + 1));
+    const double wadot = 0.125 * (WDC(-1, -1, k) + WDC(-1, 0, k) + WDC(0, -1, k) + WDC(0, 0, k));
+    const double wadotp1 = 0.125 * (WDC(-1, -1, k + 1) + WDC(-1, 0, k + 1) + WDC(0, -1, k + 1) + WDC(0, 0, k + 1));
     const double wabar = wadot + wadotp1;
     const double amfac = wabar * F2(f.rpsda, j, i) * REARTHRAD;
     const double uc = F3(f.a1u, j, i, k), vc = F3(f.a1v, j, i, k);
@@ -968,8 +1006,8 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
   // diffu_d, Main/mod_diffusion.F90:281-411 (UM = ubd/msfd, vbd/msfd staged)
   {
 #define UM(S, J, I) L2(S, (J) - j, (I) - i)
-    const double xkd = d_rfour * (F3(f.xkcr, j, i, k) + F3(f.xkcr, j - 1, i - 1, k) + F3(f.xkcr, j - 1, i, k) +
-                                  F3(f.xkcr, j, i - 1, k)) * c->rdxsq * F2(f.psdotb, j, i);   // calc_coeff
+    const double xkd = d_rfour * (XKC(0, 0) + XKC(-1, -1) + XKC(-1, 0) + XKC(0, -1)) * c->rdxsq *
+                       F2(f.psdotb, j, i);   // calc_coeff
 #pragma unroll
     for (int pass = 0; pass < 2; pass++) {
       double (*b)[TDW] = pass ? sBV : sBU;
@@ -1013,6 +1051,9 @@ __global__ __launch_bounds__(TDT) void k_nh_tend_d(Geom g, const Consts* __restr
   F3(f.uten, j, i, k) = (ut * F2(f.rpsda, j, i)) * dts;
   F3(f.vten, j, i, k) = (vt * F2(f.rpsda, j, i)) * dts;
 }
+#undef QDC
+#undef WDC
+#undef XKC
 #undef PHY
 #undef RELAX5
 #undef FG
